@@ -1,0 +1,160 @@
+"""ctypes binding of the C-ABI in ``include/d3rlpy_amd.h``.
+
+The library is loaded AFTER ``torch`` so that it binds to the HIP runtime
+instance torch already loaded (both carry the soname ``libamdhip64.so.7``);
+streams and device pointers handed over from torch are then valid here.
+
+There is no fallback: if the library is missing or a call fails, a
+``RuntimeError`` is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must be loaded first: shares its HIP runtime)
+
+_LIB_PATH = Path(__file__).resolve().parent / "libd3rlpy_amd.so"
+
+c_f32p = C.POINTER(C.c_float)
+c_i64p = C.POINTER(C.c_int64)
+c_u32p = C.POINTER(C.c_uint32)
+c_u8p = C.POINTER(C.c_uint8)
+c_i32p = C.POINTER(C.c_int32)
+vp = C.c_void_p
+
+
+class GemmDesc(C.Structure):
+    _fields_ = [
+        ("A", vp), ("B", vp), ("C", vp), ("bias", vp), ("mask", vp),
+        ("M", C.c_int64), ("N", C.c_int64), ("K", C.c_int64), ("batch", C.c_int64),
+        ("sAb", C.c_int64), ("sAm", C.c_int64), ("sAk", C.c_int64),
+        ("sBb", C.c_int64), ("sBk", C.c_int64), ("sBn", C.c_int64),
+        ("sCb", C.c_int64), ("sCm", C.c_int64), ("sCn", C.c_int64),
+        ("sbias_b", C.c_int64),
+        ("sMb", C.c_int64), ("sMm", C.c_int64), ("sMn", C.c_int64),
+        ("splits", C.c_int64), ("sCs", C.c_int64),
+        ("alpha", C.c_float), ("relu", C.c_int32), ("accumulate", C.c_int32),
+    ]
+
+
+class AdamSegment(C.Structure):
+    _fields_ = [
+        ("param", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("grad", vp),
+        ("numel", C.c_int64), ("n_partials", C.c_int64), ("partial_stride", C.c_int64),
+        ("grad_out", vp),
+    ]
+
+
+class CqlSampleDesc(C.Structure):
+    _fields_ = [
+        ("head", vp), ("obs", vp), ("next_obs", vp), ("act", vp),
+        ("eps_temp", vp), ("eps_pi", vp), ("u_rand", vp), ("eps_actor", vp),
+        ("x_q", vp), ("x_targ", vp), ("x_actor", vp),
+        ("logp_temp", vp), ("logp_is", vp), ("actor_u", vp), ("actor_logp", vp),
+        ("B", C.c_int32), ("D", C.c_int32), ("A", C.c_int32), ("N", C.c_int32),
+        ("min_logstd", C.c_float), ("max_logstd", C.c_float),
+    ]
+
+
+class CqlLossDesc(C.Structure):
+    _fields_ = [
+        ("q", vp), ("q_targ", vp), ("logp_temp", vp), ("logp_is", vp),
+        ("rew", vp), ("term", vp), ("n_steps", vp),
+        ("log_temp", vp), ("temp_m", vp), ("temp_v", vp), ("temp_step", vp),
+        ("log_alpha", vp), ("alpha_m", vp), ("alpha_v", vp), ("alpha_step", vp),
+        ("dq", vp), ("metrics", vp), ("scalars", vp),
+        ("B", C.c_int32), ("A", C.c_int32), ("N", C.c_int32), ("C", C.c_int32),
+        ("R", C.c_int64),
+        ("gamma", C.c_float), ("temp_lr", C.c_double), ("alpha_lr", C.c_double),
+        ("beta1", C.c_double), ("beta2", C.c_double), ("adam_eps", C.c_double),
+        ("alpha_threshold", C.c_float), ("conservative_weight", C.c_float),
+        ("update_temp", C.c_int32), ("update_alpha", C.c_int32), ("update_critic", C.c_int32),
+    ]
+
+
+class SacActorHeadDesc(C.Structure):
+    _fields_ = [
+        ("head", vp), ("eps", vp), ("u", vp), ("logp", vp),
+        ("dq_da", vp), ("ld_da", C.c_int64), ("da_off", C.c_int64), ("sda_c", C.c_int64),
+        ("q", vp), ("sqc", C.c_int64), ("scalars", vp),
+        ("dhead", vp), ("metrics", vp),
+        ("B", C.c_int32), ("A", C.c_int32), ("C", C.c_int32),
+        ("min_logstd", C.c_float), ("max_logstd", C.c_float),
+    ]
+
+
+class GatherDesc(C.Structure):
+    _fields_ = [
+        ("obs", vp), ("frames", vp), ("act", vp), ("act_i", vp), ("rew", vp),
+        ("t_row", vp), ("t_ep_start", vp), ("t_ep_last", vp), ("t_terminal", vp),
+        ("n_trans", C.c_int64),
+        ("D", C.c_int32), ("A", C.c_int32), ("frame_bytes", C.c_int32),
+        ("n_frames", C.c_int32), ("n_steps", C.c_int32),
+        ("gamma", C.c_float),
+        ("idx", vp), ("idx_out", vp), ("seed", C.c_uint64), ("ctr", vp), ("ticket", vp),
+        ("B", C.c_int32),
+        ("o_obs", vp), ("o_frames", vp), ("o_act", vp), ("o_act_i", vp),
+        ("o_rew", vp), ("o_next_obs", vp), ("o_next_frames", vp),
+        ("o_term", vp), ("o_n_steps", vp),
+    ]
+
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "d3a_abi_version": (C.c_int, []),
+    "d3a_last_error": (C.c_char_p, []),
+    "d3a_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "d3a_gemm_f32": (C.c_int, [C.POINTER(GemmDesc), vp]),
+    "d3a_rowdot_f32": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
+                                 C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
+    "d3a_colreduce_f32": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64,
+                                    C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
+    "d3a_outer_mask_f32": (C.c_int, [vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
+                                     C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
+    "d3a_adam_f32": (C.c_int, [vp, C.c_int32, C.c_int64, vp, vp, C.c_double, C.c_double,
+                               C.c_double, C.c_double, vp]),
+    "d3a_soft_update_f32": (C.c_int, [vp, vp, C.c_int64, C.c_double, vp]),
+    "d3a_metrics_push": (C.c_int, [vp, C.c_int32, vp, C.c_int64, vp, vp]),
+    "d3a_philox_fill": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_float, C.c_float, C.c_uint64,
+                                  vp, vp, vp]),
+    "d3a_cql_sample": (C.c_int, [C.POINTER(CqlSampleDesc), vp]),
+    "d3a_cql_loss": (C.c_int, [C.POINTER(CqlLossDesc), vp]),
+    "d3a_sac_actor_dq": (C.c_int, [vp, C.c_int64, C.c_int32, C.c_int32, vp, C.c_int64, vp]),
+    "d3a_sac_actor_head": (C.c_int, [C.POINTER(SacActorHeadDesc), vp]),
+    "d3a_gather_batch": (C.c_int, [C.POINTER(GatherDesc), vp]),
+}
+
+EXPORTED = tuple(_SIGNATURES)
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load (once) and return the native library; raise if it is missing."""
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            raise RuntimeError(
+                f"d3rlpy_amd native library not built: {_LIB_PATH} is missing "
+                "(run `python -m d3rlpy_amd._build`). There is no CPU fallback."
+            )
+        mode = getattr(os, "RTLD_GLOBAL", 0) | getattr(os, "RTLD_NOW", 0)
+        L = C.CDLL(str(_LIB_PATH), mode=mode)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().d3a_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def library_path() -> Path:
+    return _LIB_PATH

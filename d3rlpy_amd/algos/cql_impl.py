@@ -1,0 +1,470 @@
+"""CQLImpl on HIP kernels — drop-in for d3rlpy/algos/torch/cql_impl.py:21-243.
+
+Same constructor arguments, same ``update_temp / update_alpha /
+update_critic / update_actor / update_critic_target / update_actor_target``
+methods and return types; plus ``update_step`` which runs the whole
+``CQL._update`` schedule (algos/cql.py:234-258) as one device-side pipeline
+(and, after the first call, as one HIP-graph replay).
+
+Pipeline of one update_step (all on the current stream, no host sync):
+  1  policy trunk+head on [obs; next_obs]  (2B rows; the policy is unchanged
+     until update_actor, so this one evaluation serves update_temp,
+     update_alpha, the critic's conservative term and target, and the actor)
+  2  d3a_cql_sample: every action sample, log-prob and Q-input row
+  3  critic ensemble forward over 6NB+B rows (alpha set | critic set | data)
+     and the target ensemble over B rows
+  4  d3a_cql_loss: temperature Adam, alpha Adam, TD target, dL/dQ per row
+  5  critic backward over the 3NB+B critic rows, Adam (critic)
+  6  critic forward at (s, tanh u) with the new critic, dQ/da, policy-head
+     gradient, policy backward, Adam (actor)
+  7  soft update of both targets (one launch over the flat buffer)
+
+Row layout of the Q-input matrix x_q ([6NB+B][D+A], shared by the C critics):
+  set s in {0: update_alpha, 1: update_critic}, rows s*3NB + blk*NB + b*N + n
+    blk 0: (obs_b, tanh(mu(obs_b) + eps*std))      _compute_policy_is_values(obs_t, obs_t)
+    blk 1: (obs_b, tanh(mu(next_b) + eps*std))     _compute_policy_is_values(obs_tp1, obs_t)
+    blk 2: (obs_b, U(-1, 1))                       _compute_random_is_values(obs_t)
+  rows 6NB + b: (obs_b, act_b)                     data values / TD error
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+from torch import nn
+
+from .. import _native as NAT
+from .. import mlp, ops
+from ..nets import AdamGroup, EnsembleMLP, GradSpace, ParamStore
+from .impl_base import DeviceBatch, ImplBase, as_device_batch
+
+METRIC_NAMES = ("temp_loss", "temp", "alpha_loss", "alpha", "critic_loss", "actor_loss",
+                "td_loss", "conservative_loss")
+
+
+class CQLImpl(ImplBase):
+    def __init__(
+        self,
+        observation_shape: Sequence[int],
+        action_size: int,
+        actor_learning_rate: float,
+        critic_learning_rate: float,
+        temp_learning_rate: float,
+        alpha_learning_rate: float,
+        actor_optim_factory,
+        critic_optim_factory,
+        temp_optim_factory,
+        alpha_optim_factory,
+        actor_encoder_factory,
+        critic_encoder_factory,
+        q_func_factory,
+        gamma: float,
+        tau: float,
+        n_critics: int,
+        initial_temperature: float,
+        initial_alpha: float,
+        alpha_threshold: float,
+        conservative_weight: float,
+        n_action_samples: int,
+        soft_q_backup: bool,
+        use_gpu,
+        scaler,
+        action_scaler,
+        reward_scaler,
+    ):
+        super().__init__(observation_shape, action_size, scaler, action_scaler, reward_scaler,
+                         use_gpu)
+        if soft_q_backup:
+            raise NotImplementedError("soft_q_backup=True is not supported by the HIP CQLImpl")
+        if q_func_factory.get_type() != "mean":
+            raise NotImplementedError("CQL on HIP supports the 'mean' Q function")
+        if len(observation_shape) != 1:
+            raise NotImplementedError("CQL on HIP supports vector observations")
+        if scaler is not None or action_scaler is not None or reward_scaler is not None:
+            raise NotImplementedError("scalers are not supported by the HIP CQLImpl yet")
+        self._actor_learning_rate = actor_learning_rate
+        self._critic_learning_rate = critic_learning_rate
+        self._temp_learning_rate = temp_learning_rate
+        self._alpha_learning_rate = alpha_learning_rate
+        self._actor_optim_factory = actor_optim_factory
+        self._critic_optim_factory = critic_optim_factory
+        self._temp_optim_factory = temp_optim_factory
+        self._alpha_optim_factory = alpha_optim_factory
+        self._actor_encoder_factory = actor_encoder_factory
+        self._critic_encoder_factory = critic_encoder_factory
+        self._q_func_factory = q_func_factory
+        self._gamma = gamma
+        self._tau = tau
+        self._n_critics = n_critics
+        self._initial_temperature = initial_temperature
+        self._initial_alpha = initial_alpha
+        self._alpha_threshold = alpha_threshold
+        self._conservative_weight = conservative_weight
+        self._n_action_samples = n_action_samples
+        self._soft_q_backup = soft_q_backup
+        self._min_logstd, self._max_logstd = -20.0, 2.0
+        self._built = False
+        self._ws: Dict[int, "_Workspace"] = {}
+
+    # ------------------------------------------------------------------ build
+    def build(self) -> None:
+        dev = self.torch_device
+        D, A, C = self._observation_shape[0], self._action_size, self._n_critics
+        hq = list(self._critic_encoder_factory.hidden_units)
+        hp = list(self._actor_encoder_factory.hidden_units)
+        store = ParamStore()
+        # critic first, then policy: mirrors DDPGBaseImpl.build order (ddpg_impl.py:95-111)
+        self.critic = EnsembleMLP(store, "q", C, [D + A] + hq + [1])
+        self.policy = EnsembleMLP(store, "pi", 1, [D] + hp + [2 * A])
+        store.allocate(dev)
+        self.store = store
+        self._init_like_reference()
+        self.targ = store.like()
+        self.targ.data.copy_(store.data)
+        # scalar parameters: log_temp, log_alpha (create_parameter((1,1), log(v)))
+        self.log_temp = torch.full((1,), math.log(self._initial_temperature), device=dev)
+        self.log_alpha = torch.full((1,), math.log(self._initial_alpha), device=dev)
+        self.temp_m = torch.zeros(1, device=dev)
+        self.temp_v = torch.zeros(1, device=dev)
+        self.temp_step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.alpha_m = torch.zeros(1, device=dev)
+        self.alpha_v = torch.zeros(1, device=dev)
+        self.alpha_step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._built = True
+
+    def _init_like_reference(self) -> None:
+        """nn.Linear default init in the reference construction order."""
+        D, A, C = self._observation_shape[0], self._action_size, self._n_critics
+        hq = list(self._critic_encoder_factory.hidden_units)
+        hp = list(self._actor_encoder_factory.hidden_units)
+        with torch.random.fork_rng(devices=[]):
+            for c in range(C):
+                sizes = [D + A] + hq
+                for l in range(len(hq)):
+                    self.critic.load_linear(l, c, nn.Linear(sizes[l], sizes[l + 1]))
+                self.critic.load_linear(len(hq), c, nn.Linear(hq[-1], 1))
+            sizes = [D] + hp
+            for l in range(len(hp)):
+                self.policy.load_linear(l, 0, nn.Linear(sizes[l], sizes[l + 1]))
+            mu, ls = nn.Linear(hp[-1], A), nn.Linear(hp[-1], A)
+            Wh, bh = self.policy.export_linear(len(hp), 0)
+            with torch.no_grad():
+                Wh[:A].copy_(mu.weight)
+                Wh[A:].copy_(ls.weight)
+                bh[:A].copy_(mu.bias)
+                bh[A:].copy_(ls.bias)
+
+    # ------------------------------------------------------------- workspace
+    def _workspace(self, B: int) -> "_Workspace":
+        ws = self._ws.get(B)
+        if ws is None:
+            ws = _Workspace(self, B)
+            self._ws[B] = ws
+        return ws
+
+    # --------------------------------------------------------------- updates
+    def update_step(self, batch, noise: Optional[Dict[str, torch.Tensor]] = None,
+                    sync: bool = True, use_graph: bool = True):
+        """Whole CQL._update: temp, alpha, critic, actor, both target updates."""
+        flags = (self._temp_learning_rate > 0, self._alpha_learning_rate > 0, True, True, True)
+        return self._run(batch, flags, noise, sync, use_graph)
+
+    def update_temp(self, batch) -> Tuple[np.ndarray, np.ndarray]:
+        m = self._run(batch, (True, False, False, False, False), None, True, False)
+        return np.float32(m["temp_loss"]), np.float32(m["temp"])
+
+    def update_alpha(self, batch) -> Tuple[np.ndarray, np.ndarray]:
+        m = self._run(batch, (False, True, False, False, False), None, True, False)
+        return np.float32(m["alpha_loss"]), np.float32(m["alpha"])
+
+    def update_critic(self, batch) -> np.ndarray:
+        m = self._run(batch, (False, False, True, False, False), None, True, False)
+        return np.float32(m["critic_loss"])
+
+    def update_actor(self, batch) -> np.ndarray:
+        m = self._run(batch, (False, False, False, True, False), None, True, False)
+        return np.float32(m["actor_loss"])
+
+    def update_critic_target(self) -> None:
+        s, e = self.store.span(self.critic.names())
+        ops.soft_update(self.targ.data[s:e], self.store.data[s:e], self._tau)
+
+    def update_actor_target(self) -> None:
+        s, e = self.store.span(self.policy.names())
+        ops.soft_update(self.targ.data[s:e], self.store.data[s:e], self._tau)
+
+    def _run(self, batch, flags, noise, sync, use_graph):
+        db = as_device_batch(batch, self.torch_device)
+        ws = self._workspace(db.batch_size)
+        ws.stage(db, noise)
+        ws.execute(flags, use_graph=use_graph and noise is None)
+        if not sync:
+            return ws.metrics
+        vals = ws.metrics.cpu().numpy()
+        return {k: float(v) for k, v in zip(METRIC_NAMES, vals)}
+
+    # ------------------------------------------------------------- inference
+    def _policy_head(self, x: torch.Tensor) -> torch.Tensor:
+        B = x.shape[0]
+        acts = mlp.Acts.alloc(self.policy, B, self.torch_device)
+        x = x.contiguous().float()
+        mlp.forward(self.policy, self.store, x.data_ptr(), True, x.shape[1], acts)
+        return acts.out[0]
+
+    def _predict_best_action(self, x: torch.Tensor) -> torch.Tensor:
+        A = self._action_size
+        return torch.tanh(self._policy_head(x)[:, :A])
+
+    def _sample_action(self, x: torch.Tensor) -> torch.Tensor:
+        A = self._action_size
+        h = self._policy_head(x)
+        std = h[:, A:].clamp(self._min_logstd, self._max_logstd).exp()
+        return torch.tanh(h[:, :A] + torch.randn_like(std) * std)
+
+    def _predict_value(self, x: torch.Tensor, action: torch.Tensor) -> torch.Tensor:
+        xa = torch.cat([x.float(), action.float()], dim=1).contiguous()
+        acts = mlp.Acts.alloc(self.critic, xa.shape[0], self.torch_device)
+        mlp.forward(self.critic, self.store, xa.data_ptr(), True, xa.shape[1], acts)
+        return acts.out  # [C][B]
+
+    # ------------------------------------------------------------ inspection
+    def critic_grad(self, name: str) -> torch.Tensor:
+        return self._last_ws().critic_opt.grad(name)
+
+    def policy_grad(self, name: str) -> torch.Tensor:
+        return self._last_ws().actor_opt.grad(name)
+
+    def _last_ws(self) -> "_Workspace":
+        return next(iter(self._ws.values()))
+
+
+class _Workspace:
+    """Every device buffer of one update at batch size B (graph-capture safe)."""
+
+    def __init__(self, impl: CQLImpl, B: int):
+        dev = impl.torch_device
+        self.impl = impl
+        D, A, C, N = impl._observation_shape[0], impl._action_size, impl._n_critics, \
+            impl._n_action_samples
+        self.B, self.D, self.A, self.C, self.N = B, D, A, C, N
+        NB = N * B
+        self.NB = NB
+        self.R = 6 * NB + B
+        DA = D + A
+        z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        # staged batch: obs2 = [obs; next_obs]
+        self.obs2 = z(2 * B, D)
+        self.act = z(B, A)
+        self.rew = z(B)
+        self.term = z(B)
+        self.nsteps = z(B)
+        # noise: [eps_temp | eps_pi (2 sets x 2 x N x B x A) | eps_actor | u_rand (2 x NB x A)]
+        self.n_normal = (B + 4 * NB + B) * A
+        self.n_uniform = 2 * NB * A
+        self.noise = z(self.n_normal + self.n_uniform)
+        o = 0
+        self.eps_temp = self.noise[o:o + B * A]; o += B * A
+        self.eps_pi = self.noise[o:o + 4 * NB * A]; o += 4 * NB * A
+        self.eps_actor = self.noise[o:o + B * A]; o += B * A
+        self.u_rand = self.noise[o:o + 2 * NB * A]
+        self.rng_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.rng_ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.seed = int(torch.randint(0, 2**62, (1,)).item())
+        # policy forward on 2B rows
+        self.pacts = mlp.Acts.alloc(impl.policy, 2 * B, dev)
+        # sample outputs
+        self.x_q = z(self.R, DA)
+        self.x_targ = z(B, DA)
+        self.x_actor = z(B, DA)
+        self.logp_temp = z(B)
+        self.logp_is = z(4 * NB)
+        self.actor_u = z(B, A)
+        self.actor_logp = z(B)
+        # critic / target / actor-critic activations
+        self.qacts = mlp.Acts.alloc(impl.critic, self.R, dev)
+        self.tacts = mlp.Acts.alloc(impl.critic, B, dev)
+        self.aacts = mlp.Acts.alloc(impl.critic, B, dev)
+        self.dq = z(C, self.R)
+        self.adq = z(C, B)
+        self.adx = z(C, B, DA)
+        self.dhead = z(B, 2 * A)
+        self.metrics = z(len(METRIC_NAMES))
+        self.scalars = z(4)
+        # backward spaces + optimisers
+        self.Rc = 3 * NB + B
+        self.cgrads = GradSpace(dev)
+        self.cbwd = mlp.BackwardSpace(impl.critic, self.Rc, self.cgrads, dev)
+        self.abwd = mlp.BackwardSpace(impl.critic, B, None, dev)
+        self.pgrads = GradSpace(dev)
+        self.pbwd = mlp.BackwardSpace(impl.policy, B, self.pgrads, dev)
+        f = impl._critic_optim_factory
+        self.critic_opt = AdamGroup(impl.store, impl.critic.names(), self.cgrads,
+                                    impl._critic_learning_rate, f.betas, f.eps)
+        f = impl._actor_optim_factory
+        self.actor_opt = AdamGroup(impl.store, impl.policy.names(), self.pgrads,
+                                   impl._actor_learning_rate, f.betas, f.eps)
+        # share optimiser state across workspaces of other batch sizes
+        prev = [w for w in impl._ws.values()]
+        if prev:
+            raise NotImplementedError("one batch size per CQLImpl is supported")
+        self._graphs: Dict[Tuple, torch.cuda.CUDAGraph] = {}
+        self._ran_eager = set()
+        self._build_descs()
+
+    def _build_descs(self):
+        impl = self.impl
+        s = NAT.CqlSampleDesc()
+        s.head = self.pacts.out.data_ptr()
+        s.obs = self.obs2.data_ptr()
+        s.next_obs = self.obs2.data_ptr() + 4 * self.B * self.D
+        s.act = self.act.data_ptr()
+        s.eps_temp = self.eps_temp.data_ptr()
+        s.eps_pi = self.eps_pi.data_ptr()
+        s.u_rand = self.u_rand.data_ptr()
+        s.eps_actor = self.eps_actor.data_ptr()
+        s.x_q, s.x_targ, s.x_actor = (self.x_q.data_ptr(), self.x_targ.data_ptr(),
+                                      self.x_actor.data_ptr())
+        s.logp_temp, s.logp_is = self.logp_temp.data_ptr(), self.logp_is.data_ptr()
+        s.actor_u, s.actor_logp = self.actor_u.data_ptr(), self.actor_logp.data_ptr()
+        s.B, s.D, s.A, s.N = self.B, self.D, self.A, self.N
+        s.min_logstd, s.max_logstd = impl._min_logstd, impl._max_logstd
+        self.sample_desc = s
+
+        l = NAT.CqlLossDesc()
+        l.q, l.q_targ = self.qacts.out.data_ptr(), self.tacts.out.data_ptr()
+        l.logp_temp, l.logp_is = self.logp_temp.data_ptr(), self.logp_is.data_ptr()
+        l.rew, l.term, l.n_steps = self.rew.data_ptr(), self.term.data_ptr(), self.nsteps.data_ptr()
+        l.log_temp, l.temp_m, l.temp_v, l.temp_step = (impl.log_temp.data_ptr(),
+                                                       impl.temp_m.data_ptr(),
+                                                       impl.temp_v.data_ptr(),
+                                                       impl.temp_step.data_ptr())
+        l.log_alpha, l.alpha_m, l.alpha_v, l.alpha_step = (impl.log_alpha.data_ptr(),
+                                                           impl.alpha_m.data_ptr(),
+                                                           impl.alpha_v.data_ptr(),
+                                                           impl.alpha_step.data_ptr())
+        l.dq, l.metrics, l.scalars = (self.dq.data_ptr(), self.metrics.data_ptr(),
+                                      self.scalars.data_ptr())
+        l.B, l.A, l.N, l.C, l.R = self.B, self.A, self.N, self.C, self.R
+        l.gamma = impl._gamma
+        tf, af = impl._temp_optim_factory, impl._alpha_optim_factory
+        l.temp_lr, l.alpha_lr = impl._temp_learning_rate, impl._alpha_learning_rate
+        # both scalar optimisers are AdamFactory instances with the same defaults
+        assert tuple(tf.betas) == tuple(af.betas) and tf.eps == af.eps
+        l.beta1, l.beta2, l.adam_eps = tf.betas[0], tf.betas[1], tf.eps
+        l.alpha_threshold = impl._alpha_threshold
+        l.conservative_weight = impl._conservative_weight
+        self.loss_desc = l
+
+        h = NAT.SacActorHeadDesc()
+        h.head = self.pacts.out.data_ptr()
+        h.eps = self.eps_actor.data_ptr()
+        h.u = self.actor_u.data_ptr()
+        h.logp = self.actor_logp.data_ptr()
+        h.dq_da = self.adx.data_ptr()
+        h.ld_da, h.da_off, h.sda_c = self.D + self.A, self.D, self.B * (self.D + self.A)
+        h.q, h.sqc = self.aacts.out.data_ptr(), self.B
+        h.scalars = self.scalars.data_ptr()
+        h.dhead, h.metrics = self.dhead.data_ptr(), self.metrics.data_ptr()
+        h.B, h.A, h.C = self.B, self.A, self.C
+        h.min_logstd, h.max_logstd = impl._min_logstd, impl._max_logstd
+        self.head_desc = h
+
+    # ---------------------------------------------------------------- inputs
+    def stage(self, db: DeviceBatch, noise: Optional[Dict[str, torch.Tensor]]) -> None:
+        B, D = self.B, self.D
+        if db.obs.data_ptr() != self.obs2.data_ptr():
+            self.obs2[:B].copy_(db.obs.view(B, D), non_blocking=True)
+            self.obs2[B:].copy_(db.next_obs.view(B, D), non_blocking=True)
+            self.act.copy_(db.act.view(B, self.A), non_blocking=True)
+            self.rew.copy_(db.rew.view(B), non_blocking=True)
+            self.term.copy_(db.term.view(B), non_blocking=True)
+            self.nsteps.copy_(db.n_steps.view(B), non_blocking=True)
+        self._external_noise = noise is not None
+        if noise is not None:
+            self.set_noise(noise)
+
+    def set_noise(self, nz: Dict[str, torch.Tensor]) -> None:
+        """Inject the reference-shaped draws of oracle.cql.CQLNoise (parity mode)."""
+        B, A, N, NB = self.B, self.A, self.N, self.NB
+        dev = self.noise.device
+        g = lambda k: torch.as_tensor(nz[k], dtype=torch.float32).to(dev).contiguous()  # noqa
+        self.eps_temp.copy_(g("eps_temp").view(-1))
+        ep = self.eps_pi.view(2, 2, N, B, A)
+        ep[0, 0].copy_(g("alpha_pi_t").view(N, B, A))
+        ep[0, 1].copy_(g("alpha_pi_tp1").view(N, B, A))
+        ep[1, 0].copy_(g("critic_pi_t").view(N, B, A))
+        ep[1, 1].copy_(g("critic_pi_tp1").view(N, B, A))
+        ur = self.u_rand.view(2, NB, A)
+        ur[0].copy_(g("alpha_rand").view(NB, A))
+        ur[1].copy_(g("critic_rand").view(NB, A))
+        self.eps_actor.copy_(g("eps_actor").view(-1))
+
+    # ------------------------------------------------------------- pipeline
+    def execute(self, flags, use_graph: bool) -> None:
+        key = tuple(bool(f) for f in flags) + (self._external_noise,)
+        if not use_graph:
+            self._enqueue(*flags)
+            return
+        g = self._graphs.get(key)
+        if g is None:
+            if key not in self._ran_eager:
+                # first call: run eagerly (loads code objects, real update)
+                self._ran_eager.add(key)
+                self._enqueue(*flags)
+                return
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g):
+                self._enqueue(*flags)
+            self._graphs[key] = g
+        g.replay()
+
+    def _enqueue(self, temp: bool, alpha: bool, critic: bool, actor: bool, targets: bool) -> None:
+        impl = self.impl
+        B, D, A, C, N, NB, R = self.B, self.D, self.A, self.C, self.N, self.NB, self.R
+        DA = D + A
+        if not self._external_noise:
+            ops.philox_fill(self.noise, self.n_normal, self.n_uniform, -1.0, 1.0, self.seed,
+                            self.rng_ctr, self.rng_ticket)
+        if temp or alpha or critic or actor:
+            # 1. policy on [obs; next_obs]
+            mlp.forward(impl.policy, impl.store, self.obs2.data_ptr(), True, D, self.pacts)
+            # 2. samples and Q inputs
+            ops.call_desc("d3a_cql_sample", self.sample_desc)
+        if alpha or critic:
+            # 3. critic forward (alpha set only when update_alpha runs)
+            r0 = 0 if alpha else 3 * NB
+            mlp.forward(impl.critic, impl.store, self.x_q.data_ptr(), True, DA, self.qacts, r0, R)
+        if critic:
+            mlp.forward(impl.critic, impl.targ, self.x_targ.data_ptr(), True, DA, self.tacts)
+        if temp or alpha or critic:
+            l = self.loss_desc
+            l.update_temp, l.update_alpha, l.update_critic = int(temp), int(alpha), int(critic)
+            ops.call_desc("d3a_cql_loss", l)
+        if critic:
+            # 5. critic backward on rows [3NB, R) and Adam
+            r0 = 3 * NB
+            mlp.backward(self.cbwd, impl.store, self.x_q.data_ptr(), True, DA, self.qacts,
+                         self.dq.data_ptr() + 4 * r0, 1, R, r0, self.Rc)
+            self.critic_opt.launch()
+        if actor:
+            if not (temp or alpha or critic):
+                # scalars[0] = exp(log_temp) is produced by the loss kernel
+                l = self.loss_desc
+                l.update_temp, l.update_alpha, l.update_critic = 0, 0, 0
+                ops.call_desc("d3a_cql_loss", l)
+            # 6. actor: Q(s, tanh u) with the updated critic, dQ/da, policy backward
+            mlp.forward(impl.critic, impl.store, self.x_actor.data_ptr(), True, DA, self.aacts)
+            NAT.check(NAT.lib().d3a_sac_actor_dq(self.aacts.out.data_ptr(), B, C, B,
+                                                 self.adq.data_ptr(), B, ops._stream()),
+                      "d3a_sac_actor_dq")
+            mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA, self.aacts,
+                         self.adq.data_ptr(), 1, B, 0, B, weight_grads=False, dx=self.adx)
+            ops.call_desc("d3a_sac_actor_head", self.head_desc)
+            mlp.backward(self.pbwd, impl.store, self.obs2.data_ptr(), True, D, self.pacts,
+                         self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B)
+            self.actor_opt.launch()
+        if targets:
+            ops.soft_update(impl.targ.data, impl.store.data, impl._tau)

@@ -1,0 +1,103 @@
+// Shared helpers for the d3rlpy_amd HIP library (gfx950 / CDNA4 only).
+//
+// Every entry point in include/d3rlpy_amd.h returns an int status: 0 on
+// success, a negative code otherwise; d3a_last_error() returns the message.
+// Kernels are enqueued on the caller's stream and never synchronise, so every
+// entry point is legal inside hipStreamBeginCapture / torch.cuda.graph.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+namespace d3a {
+
+constexpr int kWave = 64;  // CDNA wavefront width
+
+void set_error(const char* fmt, ...);
+
+#define D3A_CHECK_ARG(cond, ...)                 \
+  do {                                           \
+    if (!(cond)) {                               \
+      ::d3a::set_error(__VA_ARGS__);             \
+      return -1;                                 \
+    }                                            \
+  } while (0)
+
+#define D3A_LAUNCH_CHECK(name)                                              \
+  do {                                                                      \
+    hipError_t _e = hipGetLastError();                                      \
+    if (_e != hipSuccess) {                                                 \
+      ::d3a::set_error("%s: launch failed: %s", name, hipGetErrorString(_e)); \
+      return -2;                                                            \
+    }                                                                       \
+  } while (0)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Block-wide sum for blockDim.x a multiple of 64 (<= 1024).  `scratch` must
+// hold blockDim.x / 64 floats.  Result is broadcast to every thread.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; ++i) s += scratch[i];  // fixed order: deterministic
+  return s;
+}
+
+// torch.nn.functional.softplus(x, beta=1, threshold=20)
+__device__ __forceinline__ float softplus_t(float x) {
+  return x > 20.f ? x : log1pf(expf(x));
+}
+
+__device__ __forceinline__ float sigmoidf_t(float x) { return 1.f / (1.f + expf(-x)); }
+
+// Philox-4x32-10 counter-based generator: (key, counter) -> 4 uint32.
+struct Philox {
+  __device__ static inline void round(uint32_t c[4], const uint32_t k[2]) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    uint64_t p0 = (uint64_t)M0 * c[0];
+    uint64_t p1 = (uint64_t)M1 * c[2];
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c[0] = hi1 ^ c[1] ^ k[0];
+    c[1] = lo1;
+    c[2] = hi0 ^ c[3] ^ k[1];
+    c[3] = lo0;
+  }
+  __device__ static inline void gen(uint64_t seed, uint64_t ctr_hi, uint64_t ctr_lo,
+                                    uint32_t out[4]) {
+    uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t c[4] = {(uint32_t)ctr_lo, (uint32_t)(ctr_lo >> 32), (uint32_t)ctr_hi,
+                     (uint32_t)(ctr_hi >> 32)};
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      round(c, k);
+      k[0] += 0x9E3779B9u;
+      k[1] += 0xBB67AE85u;
+    }
+    out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = c[3];
+  }
+};
+
+// uint32 -> uniform float in (0, 1]
+__device__ __forceinline__ float u01(uint32_t x) {
+  return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+}  // namespace d3a

@@ -1,0 +1,335 @@
+// Fused CQL / SAC stages of one conservative Q-learning update.
+//
+// Reference: d3rlpy/algos/torch/cql_impl.py (CQLImpl), sac_impl.py
+// (SACImpl.update_temp / compute_actor_loss), models/torch/policies.py
+// (SquashedNormalPolicy), models/torch/distributions.py
+// (SquashedGaussianDistribution._log_prob_from_raw_y).
+//
+// The GEMM-heavy parts (policy and critic MLPs) run on gemm.hip; these
+// kernels do the per-row sampling / log-prob / logsumexp / loss / gradient
+// seeding work in between, so that the update never leaves the device and
+// needs no host synchronisation.
+#include "common.hpp"
+#include "../../include/d3rlpy_amd.h"
+
+namespace d3a {
+namespace {
+
+constexpr float kLn2 = 0.69314718055994530942f;
+// math.log(math.sqrt(2 * math.pi)) as the fp32 scalar torch uses
+constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
+
+// SquashedGaussianDistribution sample + log-prob for one row:
+//   std = exp(clamp(ls, lo, hi)); u = mu + eps * std; a = tanh(u)
+//   logp = sum_j [Normal(mu, std).log_prob(u) - 2 (log 2 - u - softplus(-2u))]
+__device__ __forceinline__ float squashed_sample(const float* mu, const float* ls, const float* eps,
+                                                 int A, float lo, float hi, float* act,
+                                                 float* u_out) {
+  float logp = 0.f;
+  for (int j = 0; j < A; ++j) {
+    const float l = fminf(fmaxf(ls[j], lo), hi);
+    const float sd = expf(l);
+    const float u = mu[j] + eps[j] * sd;
+    const float d = u - mu[j];
+    const float var = sd * sd;
+    const float lp = -(d * d) / (2.f * var) - logf(sd) - kLogSqrt2Pi;
+    const float jac = 2.f * (kLn2 - u - softplus_t(-2.f * u));
+    logp += lp - jac;
+    if (act) act[j] = tanhf(u);
+    if (u_out) u_out[j] = u;
+  }
+  return logp;
+}
+
+__global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) {
+  const int64_t B = d.B, N = d.N, A = d.A, D = d.D;
+  const int64_t NB = N * B;
+  const int64_t DA = D + A;
+  const int64_t R = 6 * NB + B;           // x_q rows
+  const int64_t total = R + 3 * B;         // + temp, target, actor rows
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t H = 2 * A;                 // head row width
+  float act[16];
+
+  if (i < 6 * NB) {
+    const int64_t s = i / (3 * NB);        // 0 = alpha set, 1 = critic set
+    const int64_t w = i % (3 * NB);
+    const int64_t blk = w / NB;            // 0 pi(.|s_t), 1 pi(.|s_t+1), 2 uniform
+    const int64_t r = w % NB;              // = b * N + n
+    const int64_t b = r / N, n = r % N;
+    float* x = d.x_q + i * DA;
+    const float* o = d.obs + b * D;
+    for (int64_t j = 0; j < D; ++j) x[j] = o[j];
+    if (blk < 2) {
+      // policy rows: head row b (obs) or B + b (next_obs); noise [s][blk][n][b]
+      const float* hrow = d.head + (blk * B + b) * H;
+      const float* e = d.eps_pi + (((s * 2 + blk) * N + n) * B + b) * A;
+      const float lp = squashed_sample(hrow, hrow + A, e, (int)A, d.min_logstd, d.max_logstd,
+                                       act, nullptr);
+      d.logp_is[(s * 2 + blk) * NB + r] = lp;
+      for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
+    } else {
+      const float* u = d.u_rand + (s * NB + r) * A;
+      for (int64_t j = 0; j < A; ++j) x[D + j] = u[j];
+    }
+  } else if (i < R) {
+    // data rows (obs_t, a_t)
+    const int64_t b = i - 6 * NB;
+    float* x = d.x_q + i * DA;
+    for (int64_t j = 0; j < D; ++j) x[j] = d.obs[b * D + j];
+    for (int64_t j = 0; j < A; ++j) x[D + j] = d.act[b * A + j];
+  } else if (i < R + B) {
+    // update_temp sample: log-prob only
+    const int64_t b = i - R;
+    const float* hrow = d.head + b * H;
+    d.logp_temp[b] = squashed_sample(hrow, hrow + A, d.eps_temp + b * A, (int)A, d.min_logstd,
+                                     d.max_logstd, nullptr, nullptr);
+  } else if (i < R + 2 * B) {
+    // deterministic target action tanh(mu(s_t+1)) (NormalPolicy.best_action)
+    const int64_t b = i - R - B;
+    const float* hrow = d.head + (B + b) * H;
+    float* x = d.x_targ + b * DA;
+    for (int64_t j = 0; j < D; ++j) x[j] = d.next_obs[b * D + j];
+    for (int64_t j = 0; j < A; ++j) x[D + j] = tanhf(hrow[j]);
+  } else {
+    // actor sample (rsample, with gradient later)
+    const int64_t b = i - R - 2 * B;
+    const float* hrow = d.head + b * H;
+    float* x = d.x_actor + b * DA;
+    for (int64_t j = 0; j < D; ++j) x[j] = d.obs[b * D + j];
+    d.actor_logp[b] = squashed_sample(hrow, hrow + A, d.eps_actor + b * A, (int)A, d.min_logstd,
+                                      d.max_logstd, act, d.actor_u + b * A);
+    for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
+  }
+}
+
+// Adam on a single scalar parameter (torch single-tensor path); returns new p.
+__device__ float adam_scalar(float* p, float* m, float* v, int64_t* step, float g, double lr,
+                             double b1, double b2, double eps) {
+  const int64_t t = *step + 1;
+  float mm = fmaf((float)(1.0 - b1), __fsub_rn(g, *m), *m);
+  float vv = __fmul_rn(*v, (float)b2);
+  vv = __fadd_rn(vv, __fmul_rn(__fmul_rn((float)(1.0 - b2), g), g));
+  const double bc1 = 1.0 - pow(b1, (double)t);
+  const double bc2 = 1.0 - pow(b2, (double)t);
+  const float step_size = (float)(lr / bc1);
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vv), (float)sqrt(bc2)), (float)eps);
+  const float pn = __fadd_rn(*p, __fmul_rn(-step_size, __fdiv_rn(mm, denom)));
+  *m = mm; *v = vv; *p = pn; *step = t;
+  return pn;
+}
+
+// logsumexp over the 3N importance-sampled values of (c, b) in set s.
+__device__ __forceinline__ float is_value(const d3a_cql_loss_desc& d, int64_t c, int64_t s,
+                                          int64_t b, int64_t j, float rand_logp) {
+  const int64_t N = d.N, NB = (int64_t)d.N * d.B;
+  const int64_t blk = j / N, n = j % N;
+  const int64_t r = b * N + n;
+  const float qv = d.q[c * d.R + s * 3 * NB + blk * NB + r];
+  if (blk < 2) return qv - d.logp_is[(s * 2 + blk) * NB + r];
+  return qv - rand_logp;
+}
+
+__device__ float lse_row(const d3a_cql_loss_desc& d, int64_t c, int64_t s, int64_t b,
+                         float rand_logp) {
+  const int64_t M = 3 * (int64_t)d.N;
+  float mx = -INFINITY;
+  for (int64_t j = 0; j < M; ++j) mx = fmaxf(mx, is_value(d, c, s, b, j, rand_logp));
+  if (isinf(mx)) mx = 0.f;  // torch.logsumexp: |max| == inf -> use 0 as the shift
+  float se = 0.f;
+  for (int64_t j = 0; j < M; ++j) se += expf(is_value(d, c, s, b, j, rand_logp) - mx);
+  return logf(se) + mx;
+}
+
+__global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
+  __shared__ float scratch[16];
+  __shared__ float sh[4];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int64_t B = d.B, C = d.C, N = d.N, NB = N * B;
+  // random_log_probs = math.log(0.5 ** action_size) (cql_impl.py:191)
+  const float rand_logp = (float)log(pow(0.5, (double)d.A));
+
+  // ---- update_temp (sac_impl.py:123-146) ----
+  if (d.update_temp) {
+    float s = 0.f;
+    for (int64_t b = tid; b < B; b += nt) s += d.logp_temp[b] - (float)d.A;
+    const float tsum = block_sum(s, scratch);
+    if (tid == 0) {
+      const float e = expf(*d.log_temp);
+      // loss = -(exp(log_temp) * targ_temp).mean()
+      const float loss = -(e * tsum) / (float)B;
+      const float g = (-1.f / (float)B) * tsum * e;
+      const float ln = adam_scalar(d.log_temp, d.temp_m, d.temp_v, d.temp_step, g, d.temp_lr,
+                                   d.beta1, d.beta2, d.adam_eps);
+      d.metrics[0] = loss;
+      d.metrics[1] = expf(ln);
+    }
+  }
+  __syncthreads();
+
+  // ---- update_alpha (cql_impl.py:119-141) on sample set 0 ----
+  if (d.update_alpha) {
+    float sl = 0.f, sd = 0.f;
+    for (int64_t p = tid; p < C * B; p += nt) {
+      const int64_t c = p / B, b = p % B;
+      sl += lse_row(d, c, 0, b, rand_logp);
+      sd += d.q[c * d.R + 6 * NB + b];
+    }
+    const float lsum = block_sum(sl, scratch);
+    const float dsum = block_sum(sd, scratch);
+    if (tid == 0) {
+      const float loss = lsum / (float)(C * B) - dsum / (float)(C * B);
+      const float scaled = d.conservative_weight * loss;
+      const float e = expf(*d.log_alpha);
+      const float ca = fminf(fmaxf(e, 0.f), 1e6f);
+      const float cons = ca * (scaled - d.alpha_threshold);
+      const bool pass = (e >= 0.f) && (e <= 1e6f);
+      const float g = pass ? -(scaled - d.alpha_threshold) * e : 0.f;
+      const float ln = adam_scalar(d.log_alpha, d.alpha_m, d.alpha_v, d.alpha_step, g,
+                                   d.alpha_lr, d.beta1, d.beta2, d.adam_eps);
+      d.metrics[2] = -cons;
+      d.metrics[3] = expf(ln);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    sh[0] = fminf(fmaxf(expf(*d.log_alpha), 0.f), 1e6f);
+    d.scalars[0] = expf(*d.log_temp);
+    d.scalars[1] = sh[0];
+  }
+  __syncthreads();
+  const float ca = sh[0];
+
+  if (!d.update_critic) return;
+  // ---- update_critic loss and dL/dQ (ddpg_impl.py:138-165, cql_impl.py:110-117) ----
+  const float gcons = ca * d.conservative_weight / (float)(C * B);
+  float s_td = 0.f, s_l = 0.f, s_d = 0.f;
+  for (int64_t p = tid; p < C * B; p += nt) {
+    const int64_t c = p / B, b = p % B;
+    // deterministic target: min over target critics
+    float tq = d.q_targ[b];
+    for (int64_t k = 1; k < C; ++k) tq = fminf(tq, d.q_targ[k * B + b]);
+    const float gam = powf(d.gamma, d.n_steps[b]);
+    const float y = d.rew[b] + gam * tq * (1.f - d.term[b]);
+    const float qd = d.q[c * d.R + 6 * NB + b];
+    const float diff = qd - y;
+    s_td += diff * diff;
+    s_d += qd;
+    const float l = lse_row(d, c, 1, b, rand_logp);
+    s_l += l;
+    // softmax weights of the critic-set IS values
+    const int64_t M = 3 * N;
+    for (int64_t j = 0; j < M; ++j) {
+      const int64_t blk = j / N, n = j % N;
+      const float v = is_value(d, c, 1, b, j, rand_logp);
+      d.dq[c * d.R + 3 * NB + blk * NB + b * N + n] = gcons * expf(v - l);
+    }
+    d.dq[c * d.R + 6 * NB + b] = 2.f * diff / (float)B - gcons;
+  }
+  // alpha-set rows carry no critic gradient
+  for (int64_t p = tid; p < C * 3 * NB; p += nt) {
+    const int64_t c = p / (3 * NB), r = p % (3 * NB);
+    d.dq[c * d.R + r] = 0.f;
+  }
+  const float td = block_sum(s_td, scratch) / (float)B;
+  const float lsum = block_sum(s_l, scratch);
+  const float dsum = block_sum(s_d, scratch);
+  if (tid == 0) {
+    const float loss = lsum / (float)(C * B) - dsum / (float)(C * B);
+    const float cons = ca * (d.conservative_weight * loss - d.alpha_threshold);
+    d.metrics[4] = td + cons;
+    d.metrics[6] = td;
+    d.metrics[7] = cons;
+  }
+}
+
+__global__ __launch_bounds__(256) void sac_actor_dq_kernel(const float* q, int64_t sqc, int C,
+                                                           int B, float* dq, int64_t sdq) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  int arg = 0;
+  float mn = q[b];
+  for (int c = 1; c < C; ++c) {
+    const float v = q[c * sqc + b];
+    if (v < mn) { mn = v; arg = c; }
+  }
+  for (int c = 0; c < C; ++c) dq[c * sdq + b] = (c == arg) ? -1.f / (float)B : 0.f;
+}
+
+__global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_desc d) {
+  __shared__ float scratch[4];
+  const int tid = threadIdx.x;
+  const int A = d.A, B = d.B, C = d.C;
+  const float et = d.scalars[0];
+  const float dlogp = et / (float)B;
+  float lsum = 0.f;
+  for (int b = tid; b < B; b += blockDim.x) {
+    const float* hrow = d.head + (int64_t)b * 2 * A;
+    float qmin = d.q[b];
+    for (int c = 1; c < C; ++c) qmin = fminf(qmin, d.q[c * d.sqc + b]);
+    lsum += et * d.logp[b] - qmin;
+    for (int j = 0; j < A; ++j) {
+      float da = 0.f;
+      for (int c = 0; c < C; ++c) da += d.dq_da[c * d.sda_c + (int64_t)b * d.ld_da + d.da_off + j];
+      const float mu = hrow[j], lsr = hrow[A + j];
+      const float l = fminf(fmaxf(lsr, d.min_logstd), d.max_logstd);
+      const float sd = expf(l);
+      const float u = d.u[b * A + j];
+      const float e = d.eps[b * A + j];
+      const float th = tanhf(u);
+      const float dm = u - mu;
+      const float var = sd * sd;
+      // d logp / d u (direct): -(u-mu)/var + 2 - 4 sigmoid(-2u)
+      const float dlp_du = -dm / var + 2.f - 4.f * sigmoidf_t(-2.f * u);
+      const float du = da * (1.f - th * th) + dlogp * dlp_du;
+      const float dmu = du + dlogp * (dm / var);
+      const float dsd = du * e + dlogp * ((dm * dm) / (var * sd) - 1.f / sd);
+      const bool pass = (lsr >= d.min_logstd) && (lsr <= d.max_logstd);
+      d.dhead[(int64_t)b * 2 * A + j] = dmu;
+      d.dhead[(int64_t)b * 2 * A + A + j] = pass ? dsd * sd : 0.f;
+    }
+  }
+  const float tot = block_sum(lsum, scratch);
+  if (tid == 0) d.metrics[5] = tot / (float)B;
+}
+
+}  // namespace
+}  // namespace d3a
+
+using namespace d3a;
+
+extern "C" int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream) {
+  D3A_CHECK_ARG(d, "d3a_cql_sample: null desc");
+  D3A_CHECK_ARG(d->A >= 1 && d->A <= 16, "d3a_cql_sample: action size must be in [1,16]");
+  D3A_CHECK_ARG(d->B >= 1 && d->N >= 1 && d->D >= 1, "d3a_cql_sample: bad sizes");
+  const int64_t total = 6LL * d->N * d->B + 4LL * d->B;
+  hipLaunchKernelGGL(cql_sample_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, *d);
+  D3A_LAUNCH_CHECK("d3a_cql_sample");
+  return 0;
+}
+
+extern "C" int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream) {
+  D3A_CHECK_ARG(d, "d3a_cql_loss: null desc");
+  D3A_CHECK_ARG(d->R == 6LL * d->N * d->B + d->B, "d3a_cql_loss: R must be 6NB+B");
+  hipLaunchKernelGGL(cql_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, *d);
+  D3A_LAUNCH_CHECK("d3a_cql_loss");
+  return 0;
+}
+
+extern "C" int d3a_sac_actor_dq(const float* q, int64_t sqc, int32_t C, int32_t B, float* dq,
+                                int64_t sdq, void* stream) {
+  D3A_CHECK_ARG(q && dq && C >= 1 && B >= 1, "d3a_sac_actor_dq: bad args");
+  hipLaunchKernelGGL(sac_actor_dq_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, q, sqc, C, B, dq, sdq);
+  D3A_LAUNCH_CHECK("d3a_sac_actor_dq");
+  return 0;
+}
+
+extern "C" int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream) {
+  D3A_CHECK_ARG(d && d->B >= 1 && d->A >= 1 && d->C >= 1, "d3a_sac_actor_head: bad args");
+  hipLaunchKernelGGL(sac_actor_head_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *d);
+  D3A_LAUNCH_CHECK("d3a_sac_actor_head");
+  return 0;
+}

@@ -1,0 +1,304 @@
+// Bandwidth-bound helpers: 1-output heads, column reductions (bias / head
+// weight gradients), relu-masked outer products, Adam, soft target update and
+// the Philox noise generator.  All loads are coalesced along the contiguous
+// (feature) dimension; reductions are in a fixed order (deterministic).
+#include <cstdarg>
+#include "common.hpp"
+#include "../../include/d3rlpy_amd.h"
+
+namespace d3a {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+namespace {
+
+// ---- rowdot: one wave per row, 4 floats per lane per step -------------------
+__global__ __launch_bounds__(256) void rowdot_kernel(const float* X, int64_t sXb, int64_t sXr,
+                                                     const float* w, int64_t swb,
+                                                     const float* bias, int64_t sbb, float* out,
+                                                     int64_t sOb, int64_t rows, int64_t n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t b = blockIdx.y;
+  if (r >= rows) return;
+  const float* x = X + b * sXb + r * sXr;
+  const float* wb = w + b * swb;
+  float acc = 0.f;
+  const bool vec = ((n & 3) == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(wb) & 15) == 0);
+  if (vec) {
+    for (int64_t j = (int64_t)lane * 4; j < n; j += 256) {
+      const float4 a = *reinterpret_cast<const float4*>(x + j);
+      const float4 c = *reinterpret_cast<const float4*>(wb + j);
+      acc += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
+    }
+  } else {
+    for (int64_t j = lane; j < n; j += 64) acc += x[j] * wb[j];
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) out[b * sOb + r] = acc + (bias ? bias[b * sbb] : 0.f);
+}
+
+// ---- colreduce: thread per column, rows split across blockIdx.y ------------
+__global__ __launch_bounds__(256) void colreduce_kernel(const float* X, int64_t sXb, int64_t sXr,
+                                                        const float* w, int64_t swb, float* out,
+                                                        int64_t sOb, int64_t sOs, int64_t rows,
+                                                        int64_t n, int64_t splits) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t s = blockIdx.y, b = blockIdx.z;
+  if (j >= n) return;
+  const int64_t chunk = (rows + splits - 1) / splits;
+  const int64_t r0 = s * chunk;
+  const int64_t r1 = (r0 + chunk < rows) ? r0 + chunk : rows;
+  const float* x = X + b * sXb + j;
+  const float* wb = w ? w + b * swb : nullptr;
+  // fp64 accumulation: bias / head gradients sum thousands of mixed-sign rows
+  double acc = 0.0;
+  if (wb) {
+    for (int64_t r = r0; r < r1; ++r) acc += (double)(wb[r] * x[r * sXr]);
+  } else {
+    for (int64_t r = r0; r < r1; ++r) acc += (double)x[r * sXr];
+  }
+  out[b * sOb + s * sOs + j] = (float)acc;
+}
+
+// ---- outer_mask: out[r][j] = g[r] * w[j] * (h[r][j] > 0) ------------------
+__global__ __launch_bounds__(256) void outer_mask_kernel(const float* g, int64_t sgb,
+                                                         const float* w, int64_t swb,
+                                                         const float* h, int64_t shb, float* out,
+                                                         int64_t sob, int64_t rows, int64_t n) {
+  const int64_t b = blockIdx.y;
+  const int64_t total = rows * n;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= total) return;
+  const float* hb = h + b * shb;
+  float* ob = out + b * sob;
+  const float* wb = w + b * swb;
+  const float* gb = g + b * sgb;
+  if ((n & 3) == 0) {
+    const int64_t r = i / n, j = i % n;
+    const float4 hv = *reinterpret_cast<const float4*>(hb + i);
+    const float4 wv = *reinterpret_cast<const float4*>(wb + j);
+    const float gv = gb[r];
+    float4 o;
+    o.x = hv.x > 0.f ? gv * wv.x : 0.f;
+    o.y = hv.y > 0.f ? gv * wv.y : 0.f;
+    o.z = hv.z > 0.f ? gv * wv.z : 0.f;
+    o.w = hv.w > 0.f ? gv * wv.w : 0.f;
+    *reinterpret_cast<float4*>(ob + i) = o;
+  } else {
+    for (int q = 0; q < 4 && i + q < total; ++q) {
+      const int64_t e = i + q, r = e / n, j = e % n;
+      ob[e] = hb[e] > 0.f ? gb[r] * wb[j] : 0.f;
+    }
+  }
+}
+
+// ---- Adam (torch.optim.adam._single_tensor_adam, weight_decay = 0) ---------
+__global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs, int64_t* step,
+                                                   unsigned int* ticket, double lr, double beta1,
+                                                   double beta2, double eps) {
+  const d3a_adam_segment sg = segs[blockIdx.y];
+  const int64_t t = *step + 1;  // read by every block before the last one commits
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < sg.numel) {
+    double gd = 0.0;  // split-K partials summed in a fixed order, in fp64
+    for (int64_t q = 0; q < sg.n_partials; ++q) gd += (double)sg.grad[q * sg.partial_stride + i];
+    const float g = (float)gd;
+    if (sg.grad_out) sg.grad_out[i] = g;
+    // exp_avg.lerp_(grad, 1 - beta1): weight < 0.5 -> self + w * (end - self)
+    // (ATen's vectorised CPU lerp: fmadd(weight, end - self, self))
+    const float w = (float)(1.0 - beta1);
+    float m = sg.exp_avg[i];
+    m = fmaf(w, __fsub_rn(g, m), m);
+    // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
+    float v = __fmul_rn(sg.exp_avg_sq[i], (float)beta2);
+    const float omb2 = (float)(1.0 - beta2);
+    v = __fadd_rn(v, __fmul_rn(__fmul_rn(omb2, g), g));
+    const double bc1 = 1.0 - pow(beta1, (double)t);
+    const double bc2 = 1.0 - pow(beta2, (double)t);
+    const float step_size = (float)(lr / bc1);
+    const float bc2_sqrt = (float)sqrt(bc2);
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), (float)eps);
+    const float pnew = __fadd_rn(sg.param[i], __fmul_rn(-step_size, __fdiv_rn(m, denom)));
+    sg.exp_avg[i] = m;
+    sg.exp_avg_sq[i] = v;
+    sg.param[i] = pnew;
+  }
+  // the last block to finish commits the step counter
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned nblocks = gridDim.x * gridDim.y;
+    const unsigned prev = atomicAdd(ticket, 1u);
+    if (prev == nblocks - 1) {
+      *step = t;
+      *ticket = 0u;
+    }
+  }
+}
+
+// ---- soft update: fl(fl(p_t * (1 - tau)) + fl(tau * p)) -------------------
+__global__ __launch_bounds__(256) void soft_update_kernel(float* targ, const float* src,
+                                                          int64_t n, float omt, float tau) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) targ[i] = __fadd_rn(__fmul_rn(targ[i], omt), __fmul_rn(tau, src[i]));
+}
+
+// ---- Philox noise ----------------------------------------------------------
+__global__ __launch_bounds__(256) void philox_kernel(float* out, int64_t n_normal,
+                                                     int64_t n_uniform, float lo, float hi,
+                                                     uint64_t seed, int64_t* ctr,
+                                                     unsigned int* ticket) {
+  const int64_t step = *ctr;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one Philox call -> 4 outputs
+  const int64_t total = n_normal + n_uniform;
+  const int64_t e0 = g * 4;
+  if (e0 < total) {
+    uint32_t r[4];
+    Philox::gen(seed, (uint64_t)step, (uint64_t)g, r);
+    float v[4];
+    // Box-Muller pairs
+    {
+      const float u1 = u01(r[0]), u2 = u01(r[1]);
+      const float rad = sqrtf(-2.f * logf(u1));
+      v[0] = rad * cosf(6.283185307179586f * u2);
+      v[1] = rad * sinf(6.283185307179586f * u2);
+      const float u3 = u01(r[2]), u4 = u01(r[3]);
+      const float rad2 = sqrtf(-2.f * logf(u3));
+      v[2] = rad2 * cosf(6.283185307179586f * u4);
+      v[3] = rad2 * sinf(6.283185307179586f * u4);
+    }
+    for (int q = 0; q < 4; ++q) {
+      const int64_t e = e0 + q;
+      if (e < n_normal) out[e] = v[q];
+      else if (e < total) out[e] = lo + (hi - lo) * (u01(r[q]) - 0x1p-24f);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = atomicAdd(ticket, 1u);
+    if (prev == gridDim.x - 1) {
+      *ctr = step + 1;
+      *ticket = 0u;
+    }
+  }
+}
+
+__global__ void metrics_push_kernel(const float* m, int n, float* ring, int64_t cap,
+                                    int64_t* ctr) {
+  const int64_t slot = *ctr % cap;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) ring[slot * n + i] = m[i];
+  __syncthreads();
+  if (threadIdx.x == 0) *ctr = *ctr + 1;
+}
+
+}  // namespace
+}  // namespace d3a
+
+using namespace d3a;
+
+extern "C" int d3a_metrics_push(const float* metrics, int32_t n, float* ring, int64_t cap,
+                                int64_t* ctr, void* stream) {
+  D3A_CHECK_ARG(metrics && ring && ctr && n > 0 && cap > 0, "d3a_metrics_push: bad args");
+  hipLaunchKernelGGL(metrics_push_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, metrics, n,
+                     ring, cap, ctr);
+  D3A_LAUNCH_CHECK("d3a_metrics_push");
+  return 0;
+}
+
+extern "C" int d3a_abi_version(void) { return 1; }
+
+extern "C" const char* d3a_last_error(void) { return d3a::g_err; }
+
+extern "C" int d3a_device_count(int* count) {
+  D3A_CHECK_ARG(count != nullptr, "d3a_device_count: null");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  (void)hipGetLastError();
+  return 0;
+}
+
+extern "C" int d3a_rowdot_f32(const float* X, int64_t sXb, int64_t sXr, const float* w,
+                              int64_t swb, const float* bias, int64_t sbb, float* out,
+                              int64_t sOb, int64_t batch, int64_t rows, int64_t n,
+                              void* stream) {
+  D3A_CHECK_ARG(X && w && out, "d3a_rowdot_f32: null pointer");
+  if (batch <= 0 || rows <= 0) return 0;
+  dim3 grid((unsigned)((rows + 3) / 4), (unsigned)batch);
+  hipLaunchKernelGGL(rowdot_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, sXb, sXr, w, swb,
+                     bias, sbb, out, sOb, rows, n);
+  D3A_LAUNCH_CHECK("d3a_rowdot_f32");
+  return 0;
+}
+
+extern "C" int d3a_colreduce_f32(const float* X, int64_t sXb, int64_t sXr, const float* w,
+                                 int64_t swb, float* out, int64_t sOb, int64_t sOs,
+                                 int64_t batch, int64_t rows, int64_t n, int64_t splits,
+                                 void* stream) {
+  D3A_CHECK_ARG(X && out, "d3a_colreduce_f32: null pointer");
+  D3A_CHECK_ARG(splits >= 1, "d3a_colreduce_f32: splits >= 1");
+  if (batch <= 0 || n <= 0) return 0;
+  dim3 grid((unsigned)((n + 255) / 256), (unsigned)splits, (unsigned)batch);
+  hipLaunchKernelGGL(colreduce_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, sXb, sXr, w,
+                     swb, out, sOb, sOs, rows, n, splits);
+  D3A_LAUNCH_CHECK("d3a_colreduce_f32");
+  return 0;
+}
+
+extern "C" int d3a_outer_mask_f32(const float* g, int64_t sgb, const float* w, int64_t swb,
+                                  const float* h, int64_t shb, float* out, int64_t sob,
+                                  int64_t batch, int64_t rows, int64_t n, void* stream) {
+  D3A_CHECK_ARG(g && w && h && out, "d3a_outer_mask_f32: null pointer");
+  if (batch <= 0 || rows <= 0 || n <= 0) return 0;
+  const int64_t total4 = (rows * n + 3) / 4;
+  dim3 grid((unsigned)((total4 + 255) / 256), (unsigned)batch);
+  hipLaunchKernelGGL(outer_mask_kernel, grid, dim3(256), 0, (hipStream_t)stream, g, sgb, w, swb,
+                     h, shb, out, sob, rows, n);
+  D3A_LAUNCH_CHECK("d3a_outer_mask_f32");
+  return 0;
+}
+
+extern "C" int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg, int64_t max_numel,
+                            int64_t* step, unsigned int* ticket, double lr, double beta1,
+                            double beta2, double eps, void* stream) {
+  D3A_CHECK_ARG(segs && step && ticket, "d3a_adam_f32: null pointer");
+  D3A_CHECK_ARG(n_seg > 0 && n_seg < 65536, "d3a_adam_f32: bad segment count");
+  D3A_CHECK_ARG(max_numel > 0, "d3a_adam_f32: bad max_numel");
+  dim3 grid((unsigned)((max_numel + 255) / 256), (unsigned)n_seg);
+  hipLaunchKernelGGL(adam_kernel, grid, dim3(256), 0, (hipStream_t)stream, segs, step, ticket,
+                     lr, beta1, beta2, eps);
+  D3A_LAUNCH_CHECK("d3a_adam_f32");
+  return 0;
+}
+
+extern "C" int d3a_soft_update_f32(float* targ, const float* src, int64_t n, double tau,
+                                   void* stream) {
+  D3A_CHECK_ARG(targ && src, "d3a_soft_update_f32: null pointer");
+  if (n <= 0) return 0;
+  const float omt = (float)(1.0 - tau);
+  hipLaunchKernelGGL(soft_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, targ, src, n, omt, (float)tau);
+  D3A_LAUNCH_CHECK("d3a_soft_update_f32");
+  return 0;
+}
+
+extern "C" int d3a_philox_fill(float* out, int64_t n_normal, int64_t n_uniform, float lo,
+                               float hi, uint64_t seed, int64_t* ctr, unsigned int* ticket,
+                               void* stream) {
+  D3A_CHECK_ARG(out && ctr && ticket, "d3a_philox_fill: null pointer");
+  const int64_t total = n_normal + n_uniform;
+  if (total <= 0) return 0;
+  const int64_t groups = (total + 3) / 4;
+  hipLaunchKernelGGL(philox_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, out, n_normal, n_uniform, lo, hi, seed, ctr, ticket);
+  D3A_LAUNCH_CHECK("d3a_philox_fill");
+  return 0;
+}

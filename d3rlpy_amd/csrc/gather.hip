@@ -1,0 +1,158 @@
+// Minibatch gather from a device-resident MDP dataset.
+//
+// Reference: TransitionMiniBatch.__cinit__ / _assign_to_batch /
+// _assign_observation / _stack_frames (d3rlpy/dataset.pyx:1053-1342) and the
+// index stream of RandomIterator._next (d3rlpy/iterators/random_iterator.py:38-41).
+//
+// Dataset layout in HBM (structure of arrays, built once by
+// d3rlpy_amd/dataset.py DeviceDataset):
+//   obs[n_rows][D] f32  or  frames[n_rows][frame_bytes] u8   (one row per step)
+//   act[n_rows][A] f32  or  act_i[n_rows] i32, rew[n_rows] f32
+//   per transition i: t_row (its step row), t_ep_start (first row of its
+//   episode), t_ep_last (last transition index of its episode),
+//   t_terminal (1 iff its next observation is the all-zero dummy).
+// Transitions of one episode have consecutive indices, so next_transition is
+// i + 1 unless i == t_ep_last[i].
+//
+// One workgroup per batch row: lane 0 walks the n-step chain (at most
+// n_steps dependent loads), then the whole workgroup copies observation /
+// frame bytes with 16-byte accesses.
+#include "common.hpp"
+#include "../../include/d3rlpy_amd.h"
+
+namespace d3a {
+namespace {
+
+struct RowMeta {
+  int64_t t;          // transition index
+  int64_t row;        // its step row
+  int64_t ep_start;
+  int64_t next_row;   // row of next observation (t+n), or -1 for zeros
+  int64_t next_t;     // transition index at t+n-1
+};
+
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int64_t n,
+                                           int tid, int nt) {
+  // 16-byte path when both ends are aligned
+  if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
+    const int64_t n16 = n >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (int64_t k = tid; k < n16; k += nt) d4[k] = s4[k];
+    for (int64_t k = (n16 << 4) + tid; k < n; k += nt) dst[k] = src[k];
+  } else {
+    for (int64_t k = tid; k < n; k += nt) dst[k] = src[k];
+  }
+}
+
+__device__ __forceinline__ void zero_bytes(uint8_t* dst, int64_t n, int tid, int nt) {
+  for (int64_t k = tid; k < n; k += nt) dst[k] = 0;
+}
+
+__global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
+  __shared__ RowMeta meta;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int64_t b = blockIdx.x;
+
+  if (tid == 0) {
+    int64_t t;
+    if (d.idx) {
+      t = d.idx[b];
+    } else {
+      uint32_t r[4];
+      Philox::gen(d.seed, (uint64_t)(*d.ctr), (uint64_t)b, r);
+      const uint64_t x = ((uint64_t)r[0] << 32) | r[1];
+      t = (int64_t)(x % (uint64_t)d.n_trans);
+      d.idx_out[b] = t;
+    }
+    // n-step return (dataset.pyx:1323-1330)
+    float ret = 0.f;
+    int64_t nt_i = t;
+    int k = 0;
+    for (k = 0; k < d.n_steps; ++k) {
+      ret += d.rew[d.t_row[nt_i]] * powf(d.gamma, (float)k);
+      if (nt_i == d.t_ep_last[nt_i] || k == d.n_steps - 1) break;
+      nt_i += 1;
+    }
+    d.o_rew[b] = ret;
+    const bool term = d.t_terminal[nt_i] != 0;
+    d.o_term[b] = term ? 1.f : 0.f;
+    d.o_n_steps[b] = (float)(k + 1);
+    meta.t = t;
+    meta.row = d.t_row[t];
+    meta.ep_start = d.t_ep_start[t];
+    meta.next_t = nt_i;
+    meta.next_row = term ? -1 : d.t_row[nt_i] + 1;
+    // actions
+    if (d.act_i) d.o_act_i[b] = d.act_i[meta.row];
+  }
+  __syncthreads();
+  const int64_t row = meta.row, nrow = meta.next_row, ep0 = meta.ep_start;
+
+  if (d.act) {
+    for (int j = tid; j < d.A; j += nt) d.o_act[b * d.A + j] = d.act[row * d.A + j];
+  }
+  if (d.obs) {
+    const int D = d.D;
+    for (int j = tid; j < D; j += nt) {
+      d.o_obs[b * D + j] = d.obs[row * D + j];
+      d.o_next_obs[b * D + j] = nrow >= 0 ? d.obs[nrow * D + j] : 0.f;
+    }
+  } else {
+    // image observations with frame stacking (dataset.pyx:1053-1096)
+    const int64_t fb = d.frame_bytes, nf = d.n_frames;
+    uint8_t* o = d.o_frames + b * nf * fb;
+    uint8_t* on = d.o_next_frames + b * nf * fb;
+    for (int64_t q = 0; q < nf; ++q) {
+      // slot nf-1-q holds the frame q steps back, clamped at the episode start
+      const int64_t r = (row - q > ep0) ? row - q : ep0;
+      copy_bytes(o + (nf - 1 - q) * fb, d.frames + r * fb, fb, tid, nt);
+      if (nrow < 0) {
+        zero_bytes(on + (nf - 1 - q) * fb, fb, tid, nt);
+      } else {
+        const int64_t rn = (nrow - q > ep0) ? nrow - q : ep0;
+        copy_bytes(on + (nf - 1 - q) * fb, d.frames + rn * fb, fb, tid, nt);
+      }
+    }
+  }
+
+  // advance the sampler counter once every block has drawn its index
+  if (!d.idx) {
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned prev = atomicAdd(d.ticket, 1u);
+      if (prev == gridDim.x - 1) {
+        *d.ctr = *d.ctr + 1;
+        *d.ticket = 0u;
+      }
+    }
+  }
+}
+
+}  // namespace
+}  // namespace d3a
+
+using namespace d3a;
+
+extern "C" int d3a_gather_batch(const d3a_gather_desc* d, void* stream) {
+  D3A_CHECK_ARG(d, "d3a_gather_batch: null desc");
+  D3A_CHECK_ARG(d->B >= 1, "d3a_gather_batch: batch size must be >= 1");
+  D3A_CHECK_ARG(d->n_trans >= 1, "d3a_gather_batch: empty dataset");
+  D3A_CHECK_ARG(d->rew && d->t_row && d->t_ep_start && d->t_ep_last && d->t_terminal,
+                "d3a_gather_batch: missing transition table");
+  D3A_CHECK_ARG((d->obs != nullptr) != (d->frames != nullptr),
+                "d3a_gather_batch: exactly one of obs / frames");
+  D3A_CHECK_ARG((d->act != nullptr) != (d->act_i != nullptr),
+                "d3a_gather_batch: exactly one of act / act_i");
+  D3A_CHECK_ARG(d->n_steps >= 1 && d->n_frames >= 1, "d3a_gather_batch: n_steps, n_frames >= 1");
+  D3A_CHECK_ARG(d->idx || (d->idx_out && d->ctr && d->ticket),
+                "d3a_gather_batch: indices must be given or drawn (idx_out, ctr, ticket)");
+  D3A_CHECK_ARG(d->obs ? (d->o_obs && d->o_next_obs) : (d->o_frames && d->o_next_frames),
+                "d3a_gather_batch: missing observation outputs");
+  D3A_CHECK_ARG(d->o_rew && d->o_term && d->o_n_steps && (d->act ? d->o_act != nullptr
+                                                                 : d->o_act_i != nullptr),
+                "d3a_gather_batch: missing outputs");
+  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)d->B), dim3(256), 0, (hipStream_t)stream, *d);
+  D3A_LAUNCH_CHECK("d3a_gather_batch");
+  return 0;
+}

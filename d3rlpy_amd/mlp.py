@@ -1,0 +1,174 @@
+"""Forward / backward schedules of a ReLU MLP ensemble on the HIP kernels.
+
+The reference evaluates each critic of an ensemble sequentially through
+autograd (ensemble_q_function.py:95-105, 167-170); here the C members of an
+ensemble are one batched launch per layer, and backward is written out by
+hand (no autograd):
+
+  forward   h_l = relu(h_{l-1} W_l^T + b_l)  (last layer linear, or a row-dot
+            when it has a single output)
+  backward  head:  dW = dy^T h, db = sum dy, dz = dy W * [h > 0]
+            trunk: dW_l = dz_l^T h_{l-1}, db_l = sum dz_l,
+                   dz_{l-1} = dz_l W_l * [h_{l-1} > 0]
+            input: dx = dz_0 W_0 (only when requested)
+
+Weight gradients are written as split-K partial sums (summed in a fixed
+order inside the Adam kernel), so every reduction is deterministic.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+
+from . import ops
+from .nets import EnsembleMLP, GradSpace, ParamStore
+
+
+def n_splits(rows: int, min_rows: int = 256, max_splits: int = 32) -> int:
+    return max(1, min(max_splits, rows // min_rows))
+
+
+@dataclass
+class Acts:
+    """Activation buffers of one forward pass: h[l] is [C][R][H_l] (trunk)."""
+
+    h: List[torch.Tensor]
+    out: torch.Tensor  # [C][R] (single output) or [C][R][out]
+    R: int
+
+    @staticmethod
+    def alloc(net: EnsembleMLP, R: int, device) -> "Acts":
+        hs = [torch.zeros(net.C, R, net.sizes[l + 1], device=device)
+              for l in range(net.n_layers - 1)]
+        out_dim = net.sizes[-1]
+        out = torch.zeros((net.C, R) if out_dim == 1 else (net.C, R, out_dim), device=device)
+        return Acts(hs, out, R)
+
+
+def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: int, acts: Acts,
+            r0: int = 0, r1: Optional[int] = None, sxb: Optional[int] = None) -> None:
+    """Forward rows [r0, r1) of x (row stride ldx) through the ensemble."""
+    R = acts.R
+    r1 = R if r1 is None else r1
+    n = r1 - r0
+    if n <= 0:
+        return
+    C = net.C
+    sizes = net.sizes
+    L = net.n_layers
+    inp, ld_in = x + 4 * r0 * ldx, ldx
+    sxb_ = (0 if x_shared else R * ldx) if sxb is None else sxb
+    for l in range(L - 1):
+        h = acts.h[l]
+        H = sizes[l + 1]
+        ops.linear_fwd(inp, False, ld_in, net.W(l, store), net.b(l, store), h.data_ptr() + 4 * r0 * H,
+                       C, n, sizes[l], H, relu=True, ldy=H, sxb=sxb_ if l == 0 else R * ld_in,
+                       syb=R * H)
+        inp, ld_in = h.data_ptr() + 4 * r0 * H, H
+    out_dim = sizes[-1]
+    Hl = sizes[-2]
+    if out_dim == 1:
+        ops.rowdot(inp, R * Hl if L > 1 else sxb_, ld_in, net.W(L - 1, store), Hl,
+                   net.b(L - 1, store), 1, acts.out.data_ptr() + 4 * r0, R, C, n, Hl)
+    else:
+        ops.linear_fwd(inp, False, ld_in, net.W(L - 1, store), net.b(L - 1, store),
+                       acts.out.data_ptr() + 4 * r0 * out_dim, C, n, Hl, out_dim, relu=False,
+                       ldy=out_dim, sxb=R * Hl if L > 1 else sxb_, syb=R * out_dim)
+
+
+class BackwardSpace:
+    """dz ping-pong buffers + weight-gradient partial workspaces for one net."""
+
+    def __init__(self, net: EnsembleMLP, rows: int, grads: Optional[GradSpace], device,
+                 splits: Optional[int] = None):
+        self.net = net
+        self.rows = rows
+        hidden = net.sizes[1:-1]
+        if len(set(hidden)) > 1:
+            raise NotImplementedError("hidden layers of unequal width are not supported")
+        Hmax = hidden[0] if hidden else 1
+        self.dz = [torch.zeros(net.C, rows, Hmax, device=device) for _ in range(2)]
+        self.splits = n_splits(rows) if splits is None else splits
+        self.grads = grads
+        if grads is not None:
+            for l in range(net.n_layers):
+                o, i = net.sizes[l + 1], net.sizes[l]
+                grads.add(net.wname(l), (net.C, o, i), self.splits)
+                grads.add(net.bname(l), (net.C, o), self.splits)
+
+
+def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: int,
+             acts: Acts, dout: int, ld_dout: int, sdout_b: int, r0: int, n: int,
+             weight_grads: bool = True, dx: Optional[torch.Tensor] = None,
+             sxb: Optional[int] = None) -> None:
+    """Backward of rows [r0, r0+n) given dL/d(output) (``dout`` points at row r0).
+
+    dout layout: [C] x rows, member stride sdout_b, row stride ld_dout (1 for a
+    single-output head).  ``dx`` (if given) receives dL/dx as [C][n][in].
+    """
+    net = bs.net
+    C, L, sizes, R = net.C, net.n_layers, net.sizes, acts.R
+    S = bs.splits
+    assert n <= bs.rows
+    sxb_ = (0 if x_shared else R * ldx) if sxb is None else sxb
+    gs = bs.grads
+
+    def h_ptr(l):  # input activation of layer l at row r0
+        if l == 0:
+            return x + 4 * r0 * ldx, ldx, sxb_
+        H = sizes[l]
+        return acts.h[l - 1].data_ptr() + 4 * r0 * H, H, R * H
+
+    # ---- head layer L-1
+    hin, ld_h, sh = h_ptr(L - 1)
+    Hin = sizes[L - 1]
+    out_dim = sizes[L]
+    cur = bs.dz[0]
+    if weight_grads:
+        gW, gb = gs.get(net.wname(L - 1)), gs.get(net.bname(L - 1))
+        if out_dim == 1:
+            ops.colreduce(hin, sh, ld_h, dout, sdout_b, gW.data_ptr(), Hin, C * Hin, C, n, Hin, S)
+            ops.colreduce(dout, sdout_b, 1, None, 0, gb.data_ptr(), 1, C, C, n, 1, S)
+        else:
+            ops.linear_bwd_w(dout, ld_dout, sdout_b, hin, ld_h, sh, gW.data_ptr(), C, n, Hin,
+                             out_dim, S)
+            ops.colreduce(dout, sdout_b, ld_dout, None, 0, gb.data_ptr(), out_dim, C * out_dim, C,
+                          n, out_dim, S)
+    if L == 1:
+        if dx is not None:
+            ops.linear_bwd_x(dout, ld_dout, sdout_b, net.W(0, store), dx.data_ptr(), sizes[0],
+                             n * sizes[0], C, n, sizes[0], out_dim)
+        return
+    ld_cur = bs.dz[0].shape[2]
+    scur = bs.rows * ld_cur
+    if out_dim == 1:
+        # h is contiguous [rows][H] per member (ld_h == Hin == ld_cur)
+        assert ld_h == Hin == ld_cur
+        ops.outer_mask(dout, sdout_b, net.W(L - 1, store), Hin, hin, sh, cur.data_ptr(), scur, C, n,
+                       Hin)
+    else:
+        ops.linear_bwd_x(dout, ld_dout, sdout_b, net.W(L - 1, store), cur.data_ptr(), ld_cur, scur, C,
+                         n, Hin, out_dim, mask=hin, ldm=ld_h, smb=sh)
+    # ---- trunk layers L-2 .. 0
+    for l in range(L - 2, -1, -1):
+        Hout = sizes[l + 1]
+        Hin = sizes[l]
+        hin, ld_h, sh = h_ptr(l)
+        dz = cur
+        if weight_grads:
+            gW, gb = gs.get(net.wname(l)), gs.get(net.bname(l))
+            ops.linear_bwd_w(dz.data_ptr(), ld_cur, scur, hin, ld_h, sh, gW.data_ptr(), C, n, Hin,
+                             Hout, S)
+            ops.colreduce(dz.data_ptr(), scur, ld_cur, None, 0, gb.data_ptr(), Hout, C * Hout, C, n,
+                          Hout, S)
+        if l > 0:
+            nxt = bs.dz[1] if cur is bs.dz[0] else bs.dz[0]
+            ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(l, store), nxt.data_ptr(), ld_cur,
+                             scur, C, n, Hin, Hout, mask=hin, ldm=ld_h, smb=sh)
+            cur = nxt
+        elif dx is not None:
+            ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(0, store), dx.data_ptr(), Hin,
+                             n * Hin, C, n, Hin, Hout)
+

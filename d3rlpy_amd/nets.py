@@ -1,0 +1,197 @@
+"""Flat, HBM-resident parameter storage for the MLP ensembles of the update.
+
+Layout (per network, one flat fp32 buffer shared by every network of an
+Impl so that a single launch can soft-update all targets):
+
+    for each layer l of an ensemble of C members:
+        W_l  [C][out_l][in_l]   (nn.Linear weight layout, member-major)
+        b_l  [C][out_l]
+
+Segments start at 64-element (256 B) aligned offsets so that every row base
+used by the kernels is 16-byte aligned.  ``nn.Parameter`` views of member c
+(``W_l[c]``) are contiguous, so reference-shaped modules can alias the
+buffer for checkpoints (``state_dict`` layout of d3rlpy/torch_utility.py:97-117).
+
+Initialisation replays the reference construction order with torch's CPU
+generator (nn.Linear defaults), so ``torch.manual_seed(s)`` gives the same
+initial weights as the reference built under the same seed.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import OrderedDict
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+from torch import nn
+
+from . import _native as N
+
+_ALIGN = 64
+
+
+def _align(n: int) -> int:
+    return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+class ParamStore:
+    """Named tensors packed in one flat fp32 buffer."""
+
+    def __init__(self) -> None:
+        self.specs: "OrderedDict[str, Tuple[Tuple[int, ...], int]]" = OrderedDict()
+        self.size = 0
+        self.data: Optional[torch.Tensor] = None
+
+    def add(self, name: str, shape: Sequence[int]) -> int:
+        assert self.data is None, "store already allocated"
+        assert name not in self.specs, name
+        off = self.size
+        n = 1
+        for s in shape:
+            n *= int(s)
+        self.specs[name] = (tuple(int(s) for s in shape), off)
+        self.size = off + _align(n)
+        return off
+
+    def allocate(self, device: torch.device) -> "ParamStore":
+        self.data = torch.zeros(max(self.size, 1), dtype=torch.float32, device=device)
+        return self
+
+    def like(self) -> "ParamStore":
+        """A new store with the identical layout (zero-filled)."""
+        o = ParamStore()
+        o.specs = OrderedDict(self.specs)
+        o.size = self.size
+        assert self.data is not None
+        o.data = torch.zeros_like(self.data)
+        return o
+
+    def offset(self, name: str) -> int:
+        return self.specs[name][1]
+
+    def numel(self, name: str) -> int:
+        n = 1
+        for s in self.specs[name][0]:
+            n *= s
+        return n
+
+    def view(self, name: str) -> torch.Tensor:
+        shape, off = self.specs[name]
+        assert self.data is not None
+        return self.data[off:off + self.numel(name)].view(shape)
+
+    def ptr(self, name: str) -> int:
+        assert self.data is not None
+        return self.data.data_ptr() + 4 * self.offset(name)
+
+    def span(self, names: Sequence[str]) -> Tuple[int, int]:
+        """[start, end) element range covering the given segments."""
+        offs = [self.offset(n) for n in names]
+        ends = [self.offset(n) + self.numel(n) for n in names]
+        return min(offs), max(ends)
+
+
+class EnsembleMLP:
+    """Registers an ensemble of C MLPs ``sizes[0] -> ... -> sizes[-1]`` in a store."""
+
+    def __init__(self, store: ParamStore, prefix: str, n_members: int, sizes: Sequence[int]):
+        self.store = store
+        self.prefix = prefix
+        self.C = n_members
+        self.sizes = list(sizes)
+        self.n_layers = len(sizes) - 1
+        for l in range(self.n_layers):
+            store.add(self.wname(l), (n_members, sizes[l + 1], sizes[l]))
+            store.add(self.bname(l), (n_members, sizes[l + 1]))
+
+    def wname(self, l: int) -> str:
+        return f"{self.prefix}.W{l}"
+
+    def bname(self, l: int) -> str:
+        return f"{self.prefix}.b{l}"
+
+    def names(self) -> List[str]:
+        out = []
+        for l in range(self.n_layers):
+            out += [self.wname(l), self.bname(l)]
+        return out
+
+    def W(self, l: int, store: Optional[ParamStore] = None) -> int:
+        return (store or self.store).ptr(self.wname(l))
+
+    def b(self, l: int, store: Optional[ParamStore] = None) -> int:
+        return (store or self.store).ptr(self.bname(l))
+
+    def load_linear(self, l: int, member: int, lin: nn.Linear, store: Optional[ParamStore] = None):
+        s = store or self.store
+        with torch.no_grad():
+            s.view(self.wname(l))[member].copy_(lin.weight.detach())
+            s.view(self.bname(l))[member].copy_(lin.bias.detach())
+
+    def export_linear(self, l: int, member: int, store: Optional[ParamStore] = None):
+        s = store or self.store
+        return s.view(self.wname(l))[member], s.view(self.bname(l))[member]
+
+
+class GradSpace:
+    """Split-K partial-gradient workspaces, one per parameter segment."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.parts: Dict[str, Tuple[torch.Tensor, int]] = {}
+
+    def add(self, name: str, shape: Sequence[int], n_partials: int) -> torch.Tensor:
+        t = torch.zeros((n_partials,) + tuple(shape), dtype=torch.float32, device=self.device)
+        self.parts[name] = (t, n_partials)
+        return t
+
+    def get(self, name: str) -> torch.Tensor:
+        return self.parts[name][0]
+
+
+class AdamGroup:
+    """A torch.optim.Adam equivalent over a set of segments of a ParamStore.
+
+    Exposes the reduced gradient of the last step per segment (``grad(name)``)
+    for parity tests, and the torch-format state (exp_avg / exp_avg_sq / step).
+    """
+
+    def __init__(self, store: ParamStore, names: Sequence[str], grads: GradSpace, lr: float,
+                 betas=(0.9, 0.999), eps: float = 1e-8, keep_grads: bool = True):
+        assert store.data is not None
+        self.store = store
+        self.names = list(names)
+        self.lr, self.beta1, self.beta2, self.eps = float(lr), float(betas[0]), float(betas[1]), float(eps)
+        dev = store.data.device
+        self.exp_avg = store.like()
+        self.exp_avg_sq = store.like()
+        self.step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.grad_store = store.like() if keep_grads else None
+        segs = (N.AdamSegment * len(self.names))()
+        self.max_numel = 1
+        for i, n in enumerate(self.names):
+            gt, parts = grads.parts[n]
+            numel = store.numel(n)
+            assert gt.numel() == parts * numel, (n, gt.shape, numel)
+            segs[i].param = store.ptr(n)
+            segs[i].exp_avg = self.exp_avg.ptr(n)
+            segs[i].exp_avg_sq = self.exp_avg_sq.ptr(n)
+            segs[i].grad = gt.data_ptr()
+            segs[i].numel = numel
+            segs[i].n_partials = parts
+            segs[i].partial_stride = numel
+            segs[i].grad_out = self.grad_store.ptr(n) if self.grad_store is not None else None
+            self.max_numel = max(self.max_numel, numel)
+        raw = bytes(segs)
+        self.seg_table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+        self._segs = segs
+
+    def launch(self) -> None:
+        from . import ops
+        ops.adam(self.seg_table, len(self.names), self.max_numel, self.step, self.ticket,
+                 self.lr, self.beta1, self.beta2, self.eps)
+
+    def grad(self, name: str) -> torch.Tensor:
+        assert self.grad_store is not None
+        return self.grad_store.view(name)

@@ -1,0 +1,128 @@
+"""Thin Python wrappers around the C-ABI: torch tensors -> raw pointers.
+
+Every wrapper enqueues on torch's *current* HIP stream and never
+synchronises, so a sequence of calls can be captured into a HIP graph with
+``torch.cuda.graph``.  Tensors must be fp32 (or the stated dtype), on the GPU
+and contiguous where a row-major layout is implied.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import torch
+
+from . import _native as N
+
+_F32 = 4
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t: Optional[torch.Tensor], offset: int = 0) -> Optional[int]:
+    """Device address of ``t`` plus ``offset`` elements (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr() + offset * t.element_size()
+
+
+def _need_gpu(*ts: Optional[torch.Tensor]) -> None:
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("d3rlpy_amd ops require device tensors (no CPU fallback)")
+
+
+def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
+         sA: Sequence[int], sB: Sequence[int], sC: Sequence[int],
+         bias: Optional[int] = None, sbias: int = 0,
+         mask: Optional[int] = None, sM: Sequence[int] = (0, 0, 0),
+         relu: bool = False, accumulate: bool = False, splits: int = 1, sCs: int = 0,
+         alpha: float = 1.0) -> None:
+    """C_b,s(m,n) = epi(alpha * sum_k A_b(m,k) B_b(k,n)); strides (batch, row, col)."""
+    d = N.GemmDesc()
+    d.A, d.B, d.C, d.bias, d.mask = A, B, Cp, bias, mask
+    d.M, d.N, d.K, d.batch = M, Nn, K, batch
+    d.sAb, d.sAm, d.sAk = sA
+    d.sBb, d.sBk, d.sBn = sB
+    d.sCb, d.sCm, d.sCn = sC
+    d.sbias_b = sbias
+    d.sMb, d.sMm, d.sMn = sM
+    d.splits, d.sCs = splits, sCs
+    d.alpha, d.relu, d.accumulate = alpha, int(relu), int(accumulate)
+    N.check(N.lib().d3a_gemm_f32(C.byref(d), _stream()), "d3a_gemm_f32")
+
+
+def rowdot(X: int, sXb: int, sXr: int, w: int, swb: int, bias: Optional[int], sbb: int,
+           out: int, sOb: int, batch: int, rows: int, n: int) -> None:
+    N.check(N.lib().d3a_rowdot_f32(X, sXb, sXr, w, swb, bias, sbb, out, sOb, batch, rows, n,
+                                   _stream()), "d3a_rowdot_f32")
+
+
+def colreduce(X: int, sXb: int, sXr: int, w: Optional[int], swb: int, out: int, sOb: int,
+              sOs: int, batch: int, rows: int, n: int, splits: int) -> None:
+    N.check(N.lib().d3a_colreduce_f32(X, sXb, sXr, w, swb, out, sOb, sOs, batch, rows, n,
+                                      splits, _stream()), "d3a_colreduce_f32")
+
+
+def outer_mask(g: int, sgb: int, w: int, swb: int, h: int, shb: int, out: int, sob: int,
+               batch: int, rows: int, n: int) -> None:
+    N.check(N.lib().d3a_outer_mask_f32(g, sgb, w, swb, h, shb, out, sob, batch, rows, n,
+                                       _stream()), "d3a_outer_mask_f32")
+
+
+def adam(segs: torch.Tensor, n_seg: int, max_numel: int, step: torch.Tensor,
+         ticket: torch.Tensor, lr: float, beta1: float, beta2: float, eps: float) -> None:
+    N.check(N.lib().d3a_adam_f32(ptr(segs), n_seg, max_numel, ptr(step), ptr(ticket), lr, beta1,
+                                 beta2, eps, _stream()), "d3a_adam_f32")
+
+
+def soft_update(targ: torch.Tensor, src: torch.Tensor, tau: float) -> None:
+    _need_gpu(targ, src)
+    assert targ.numel() == src.numel() and targ.dtype == src.dtype == torch.float32
+    N.check(N.lib().d3a_soft_update_f32(ptr(targ), ptr(src), targ.numel(), float(tau),
+                                        _stream()), "d3a_soft_update_f32")
+
+
+def philox_fill(out: torch.Tensor, n_normal: int, n_uniform: int, lo: float, hi: float,
+                seed: int, ctr: torch.Tensor, ticket: torch.Tensor) -> None:
+    _need_gpu(out, ctr, ticket)
+    assert out.numel() >= n_normal + n_uniform
+    N.check(N.lib().d3a_philox_fill(ptr(out), n_normal, n_uniform, lo, hi,
+                                    C.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), ptr(ctr), ptr(ticket),
+                                    _stream()), "d3a_philox_fill")
+
+
+def call_desc(fn_name: str, desc: C.Structure) -> None:
+    fn = getattr(N.lib(), fn_name)
+    N.check(fn(C.byref(desc), _stream()), fn_name)
+
+
+# ---------------------------------------------------------------------------
+# nn.Linear helpers over an ensemble of C members stored [C][out][in]
+# ---------------------------------------------------------------------------
+def linear_fwd(x: int, x_shared: bool, ldx: int, W: int, b: int, y: int, C_: int, R: int,
+               n_in: int, n_out: int, relu: bool, ldy: Optional[int] = None,
+               sxb: Optional[int] = None, syb: Optional[int] = None) -> None:
+    """y[c] = act(x[c] @ W[c]^T + b[c]); x rows have stride ldx; y is [C][R][n_out]."""
+    ldy = n_out if ldy is None else ldy
+    sxb = (0 if x_shared else R * ldx) if sxb is None else sxb
+    syb = R * ldy if syb is None else syb
+    gemm(x, W, y, R, n_out, n_in, batch=C_, sA=(sxb, ldx, 1), sB=(n_out * n_in, 1, n_in),
+         sC=(syb, ldy, 1), bias=b, sbias=n_out, relu=relu)
+
+
+def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: int, C_: int,
+                 R: int, n_in: int, n_out: int, mask: Optional[int] = None,
+                 ldm: int = 0, smb: int = 0) -> None:
+    """dx[c] = (dy[c] @ W[c]) * [mask[c] > 0]."""
+    gemm(dy, W, dx, R, n_in, n_out, batch=C_, sA=(sdyb, ldy, 1), sB=(n_out * n_in, n_in, 1),
+         sC=(sdxb, ldx, 1), mask=mask, sM=(smb, ldm, 1))
+
+
+def linear_bwd_w(dy: int, ldy: int, sdyb: int, x: int, ldx: int, sxb: int, dW: int, C_: int,
+                 R: int, n_in: int, n_out: int, splits: int) -> None:
+    """dW[s][c] = sum_{r in split s} dy[c][r]^T x[c][r]  -> partials [splits][C][out][in]."""
+    gemm(dy, x, dW, n_out, n_in, R, batch=C_, sA=(sdyb, 1, ldy), sB=(sxb, ldx, 1),
+         sC=(n_out * n_in, n_in, 1), splits=splits, sCs=C_ * n_out * n_in)

@@ -1,0 +1,263 @@
+/*
+ * d3rlpy_amd — C-ABI of the MI355X (gfx950) offline-RL update engine.
+ *
+ * Boundary: this library replaces the *arithmetic* that the reference d3rlpy
+ * v1.1.0 performs through eager PyTorch inside the Impl update methods and the
+ * Cython minibatch gather.  The Python host layer (d3rlpy_amd/) keeps the
+ * reference's Algo/Impl plugin surface (fit / update / predict,
+ * update_critic / update_actor / update_temp / update_alpha ...) and calls
+ * these entry points through ctypes with raw device pointers.
+ *
+ * Conventions
+ *   - every pointer is a device pointer unless stated otherwise;
+ *   - `stream` is a hipStream_t passed as void* (torch's current stream);
+ *   - nothing here allocates, frees or synchronises: every entry point only
+ *     enqueues kernels, so all of them are legal inside stream capture;
+ *   - return value 0 = enqueued, < 0 = argument or launch error; the message
+ *     is available from d3a_last_error() (thread-local).
+ *   - all math is fp32 (the reference's dtype); strides are in elements.
+ *
+ * The reference interface each entry point replaces is cited per function
+ * (paths relative to the reference repository root).
+ */
+#ifndef D3RLPY_AMD_H_
+#define D3RLPY_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- library ------------------------------------------------------------ */
+int d3a_abi_version(void);
+const char* d3a_last_error(void);
+/* number of visible HIP devices (0 when none). */
+int d3a_device_count(int* count);
+
+/* ---- dense layers (replaces nn.Linear forward/backward as used by
+ *      d3rlpy/models/torch/encoders.py:265-275 _fc_encode, the heads in
+ *      policies.py:57,170-176, q_functions/mean_q_function.py:255-256, and the
+ *      autograd backward of those layers) ---------------------------------- */
+
+/* Batched strided fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32):
+ *   for b < batch, s < splits:
+ *     P = alpha * sum_{k in split s} A_b(m,k) * B_b(k,n)
+ *     v = P (+ bias_b[n]) ; relu ; (* [mask_b(m,n) > 0])
+ *     C_b,s(m,n) = v   (or += v when accumulate)
+ *   A_b(m,k) = A[b*sAb + m*sAm + k*sAk], B_b(k,n) = B[b*sBb + k*sBk + n*sBn],
+ *   C_b,s(m,n) = C[b*sCb + s*sCs + m*sCm + n*sCn].
+ * A forward nn.Linear is (A = x [rows,in], B = W^T i.e. sBk=1,sBn=in),
+ * dX = dY W is (A = dY, B = W), dW = dY^T X is (A = dY^T, B = X). */
+typedef struct d3a_gemm_desc {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias;  /* may be NULL */
+  const float* mask;  /* may be NULL */
+  int64_t M, N, K, batch;
+  int64_t sAb, sAm, sAk;
+  int64_t sBb, sBk, sBn;
+  int64_t sCb, sCm, sCn;
+  int64_t sbias_b;
+  int64_t sMb, sMm, sMn;
+  int64_t splits, sCs;
+  float alpha;
+  int32_t relu;
+  int32_t accumulate;
+} d3a_gemm_desc;
+int d3a_gemm_f32(const d3a_gemm_desc* desc, void* stream);
+
+/* out[b*sOb + r] = sum_j X[b*sXb + r*sXr + j] * w[b*swb + j] + bias[b*sbb]
+ * (the 256->1 head of ContinuousMeanQFunction, mean_q_function.py:255-256) */
+int d3a_rowdot_f32(const float* X, int64_t sXb, int64_t sXr, const float* w,
+                   int64_t swb, const float* bias, int64_t sbb, float* out,
+                   int64_t sOb, int64_t batch, int64_t rows, int64_t n,
+                   void* stream);
+
+/* out[b*sOb + s*sOs + j] = sum_{r in split s} (w ? w[b*swb + r] : 1) *
+ *                          X[b*sXb + r*sXr + j]
+ * (bias gradients and the weight gradient of a 1-output head) */
+int d3a_colreduce_f32(const float* X, int64_t sXb, int64_t sXr,
+                      const float* w, int64_t swb, float* out, int64_t sOb,
+                      int64_t sOs, int64_t batch, int64_t rows, int64_t n,
+                      int64_t splits, void* stream);
+
+/* out[b][r][j] = g[b*sgb + r] * w[b*swb + j] * (h[b][r][j] > 0)
+ * (backward of relu(h) -> 1-output head; h, out row-major [rows][n]) */
+int d3a_outer_mask_f32(const float* g, int64_t sgb, const float* w,
+                       int64_t swb, const float* h, int64_t shb, float* out,
+                       int64_t sob, int64_t batch, int64_t rows, int64_t n,
+                       void* stream);
+
+/* ---- optimiser and target networks ------------------------------------- */
+
+/* One parameter tensor inside a flat buffer, with its gradient given as
+ * `n_partials` partial sums laid out `partial_stride` apart (summed in order
+ * 0..n_partials-1 before the update; n_partials=1 for a plain gradient).   */
+typedef struct d3a_adam_segment {
+  float* param;
+  float* exp_avg;
+  float* exp_avg_sq;
+  const float* grad;
+  int64_t numel;
+  int64_t n_partials;
+  int64_t partial_stride;
+  float* grad_out; /* optional: reduced gradient is stored here (may be NULL) */
+} d3a_adam_segment;
+
+/* torch.optim.Adam single-tensor step (torch/optim/adam.py, weight_decay=0,
+ * amsgrad=False) as created by AdamFactory (d3rlpy/models/optimizers.py:106-138):
+ *   m = lerp(m, g, 1-b1); v = v*b2 + (1-b2)*g*g; t = *step + 1
+ *   p += -(lr/(1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+ * `segs` is a DEVICE array of n_seg segments; *step (device int64) is
+ * incremented once per call after every block has read it. */
+int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg,
+                 int64_t max_numel, int64_t* step, unsigned int* ticket,
+                 double lr, double beta1, double beta2, double eps,
+                 void* stream);
+
+/* soft_sync (d3rlpy/torch_utility.py:27-33): targ = targ*(1-tau) + tau*src,
+ * three separately rounded fp32 ops (mul_, tau*p, add_), bit-exact. */
+int d3a_soft_update_f32(float* targ, const float* src, int64_t n, double tau,
+                        void* stream);
+
+/* Append metrics[0:n] to ring[(*ctr % cap)][0:n] and increment *ctr
+ * (per-step loss history kept on device; read back once per epoch instead of
+ * one device->host sync per update, cf. d3rlpy/base.py:645-657). */
+int d3a_metrics_push(const float* metrics, int32_t n, float* ring, int64_t cap,
+                     int64_t* ctr, void* stream);
+
+/* ---- random numbers ----------------------------------------------------- */
+
+/* Philox4x32-10: out[0:n_normal] ~ N(0,1) (Box-Muller), then
+ * out[n_normal:n_normal+n_uniform] ~ U(lo, hi).  The device counter *ctr is
+ * read by every block and incremented once per call, so a captured graph
+ * draws fresh numbers on every replay (replaces torch.randn / rsample /
+ * uniform_ in policies.py:202-216, cql_impl.py:186, td3_impl.py:67). */
+int d3a_philox_fill(float* out, int64_t n_normal, int64_t n_uniform, float lo,
+                    float hi, uint64_t seed, int64_t* ctr,
+                    unsigned int* ticket, void* stream);
+
+/* ---- CQL / SAC fused stages (d3rlpy/algos/torch/cql_impl.py,
+ *      sac_impl.py) ------------------------------------------------------- */
+
+/* Sampling stage of one CQL update.  Inputs: policy head outputs for the
+ * stacked batch [obs; next_obs] (`head`, [2B][2A] = mu | raw logstd), the
+ * observations, and the step's noise.  Produces every Q-function input row
+ * and every log-probability of the step; see d3rlpy_amd/algos/cql.py for the
+ * row layout.  Mirrors SquashedNormalPolicy.sample_with_log_prob /
+ * sample_n_with_log_prob (policies.py:160-216, distributions.py:112-135). */
+typedef struct d3a_cql_sample_desc {
+  const float* head;      /* [2B][2A] */
+  const float* obs;       /* [B][D]   */
+  const float* next_obs;  /* [B][D]   */
+  const float* act;       /* [B][A]   */
+  const float* eps_temp;  /* [B][A]            update_temp sample        */
+  const float* eps_pi;    /* [2 sets][2][N][B][A] conservative samples   */
+  const float* u_rand;    /* [2 sets][B*N][A]  uniform(-1,1) actions     */
+  const float* eps_actor; /* [B][A]            update_actor sample       */
+  float* x_q;             /* [2 sets * 3*N*B + B][D+A] Q inputs           */
+  float* x_targ;          /* [B][D+A] target-Q inputs (next_obs, tanh mu') */
+  float* x_actor;         /* [B][D+A] actor Q inputs                      */
+  float* logp_temp;       /* [B]                                         */
+  float* logp_is;         /* [2 sets][2][B*N] log-probs of the IS samples */
+  float* actor_u;         /* [B][A]  pre-tanh actor sample                */
+  float* actor_logp;      /* [B]                                         */
+  int32_t B, D, A, N;
+  float min_logstd, max_logstd;
+} d3a_cql_sample_desc;
+int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream);
+
+/* Loss stage of one CQL update, one workgroup: update_temp
+ * (sac_impl.py:123-146) incl. its Adam step on log_temp, update_alpha
+ * (cql_impl.py:119-141) incl. its Adam step on log_alpha, the TD target
+ * (cql_impl.py:232-243, mean_q_function.py:268-270) and dL/dQ of every
+ * critic row of update_critic (cql_impl.py:110-117,196-223). */
+typedef struct d3a_cql_loss_desc {
+  const float* q;          /* [C][R] Q of every x_q row                    */
+  const float* q_targ;     /* [C][B] target Q at (next_obs, tanh mu')      */
+  const float* logp_temp;  /* [B]                                         */
+  const float* logp_is;    /* [2][2][B*N]                                 */
+  const float* rew;        /* [B] */
+  const float* term;       /* [B] */
+  const float* n_steps;    /* [B] */
+  float* log_temp;         /* [1] parameter, updated in place              */
+  float* temp_m; float* temp_v; int64_t* temp_step;
+  float* log_alpha;        /* [1] parameter, updated in place              */
+  float* alpha_m; float* alpha_v; int64_t* alpha_step;
+  float* dq;               /* [C][R] dL_critic/dQ (alpha rows set to 0)    */
+  float* metrics;          /* [8]: temp_loss temp alpha_loss alpha critic_loss
+                              td_loss conservative_loss (reserved)          */
+  float* scalars;          /* [4]: exp(log_temp_new) exp(log_alpha_new) .. */
+  int32_t B, A, N, C;
+  int64_t R;               /* rows per critic in q / dq                    */
+  float gamma;
+  double temp_lr, alpha_lr, beta1, beta2, adam_eps;
+  float alpha_threshold, conservative_weight;
+  int32_t update_temp, update_alpha, update_critic;
+} d3a_cql_loss_desc;
+int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream);
+
+/* Actor stage helpers (SACImpl.compute_actor_loss, sac_impl.py:114-121):
+ * from the critics' Q at (s, tanh u) and the policy head, the per-row
+ * gradient seed for the critics (dq = -1/B on the argmin critic) ...        */
+int d3a_sac_actor_dq(const float* q, int64_t sqc, int32_t C, int32_t B,
+                     float* dq, int64_t sdq, void* stream);
+/* ... and, given dQ/da summed over critics, the policy-head gradient
+ * [B][2A] (dmu | dlogstd_raw) of mean(exp(log_temp)*logp - min_c Q).   */
+typedef struct d3a_sac_actor_head_desc {
+  const float* head;      /* [>=B][2A] policy head rows for obs           */
+  const float* eps;       /* [B][A] */
+  const float* u;         /* [B][A] pre-tanh sample                       */
+  const float* logp;      /* [B] */
+  const float* dq_da;     /* [C][B][ld_da] dQ_c/d(input); action columns at
+                             offset da_off                                */
+  int64_t ld_da, da_off, sda_c;
+  const float* q;         /* [C] x [B], stride sqc */
+  int64_t sqc;
+  const float* scalars;   /* scalars[0] = exp(log_temp) (after update_temp) */
+  float* dhead;           /* [B][2A] */
+  float* metrics;         /* metrics[5] = actor_loss                       */
+  int32_t B, A, C;
+  float min_logstd, max_logstd;
+} d3a_sac_actor_head_desc;
+int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream);
+
+/* ---- device-resident dataset gather (replaces TransitionMiniBatch /
+ *      _assign_to_batch, d3rlpy/dataset.pyx:1139-1342, and the index draw of
+ *      RandomIterator._next, d3rlpy/iterators/random_iterator.py:38-41) ---- */
+typedef struct d3a_gather_desc {
+  /* dataset (device resident, structure of arrays over all stored steps) */
+  const float* obs;          /* [n_rows][D] float observations (or NULL)   */
+  const uint8_t* frames;     /* [n_rows][frame_bytes] image observations   */
+  const float* act;          /* [n_rows][A] continuous actions (or NULL)   */
+  const int32_t* act_i;      /* [n_rows] discrete actions (or NULL)        */
+  const float* rew;          /* [n_rows] */
+  const int64_t* t_row;      /* [n_trans] row of transition i              */
+  const int64_t* t_ep_start; /* [n_trans] first row of its episode         */
+  const int64_t* t_ep_last;  /* [n_trans] last transition index of episode */
+  const uint8_t* t_terminal; /* [n_trans] 1 iff next obs is the zero dummy */
+  int64_t n_trans;
+  int32_t D, A, frame_bytes, n_frames, n_steps;
+  float gamma;
+  /* indices: either given (idx != NULL) or drawn on device (idx_out) */
+  const int64_t* idx;
+  int64_t* idx_out;
+  uint64_t seed;
+  int64_t* ctr;
+  unsigned int* ticket;
+  /* batch outputs */
+  int32_t B;
+  float* o_obs; uint8_t* o_frames;
+  float* o_act; int32_t* o_act_i;
+  float* o_rew; float* o_next_obs; uint8_t* o_next_frames;
+  float* o_term; float* o_n_steps;
+} d3a_gather_desc;
+int d3a_gather_batch(const d3a_gather_desc* d, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* D3RLPY_AMD_H_ */

@@ -1,0 +1,165 @@
+"""Kernel-level parity of the HIP library against plain PyTorch fp32 (GPU only).
+
+Each test calls the C-ABI through d3rlpy_amd.ops on device tensors and
+compares with the same op in torch (computed in fp64 where the tolerance is
+about accumulation order).  Tolerances are stated per test.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from d3rlpy_amd import _native
+    _native.lib()
+    return torch.device("cuda:0")
+
+
+def _rel_err(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).abs().max() / max(1e-30, float(b.abs().max())))
+
+
+@pytest.mark.parametrize("M,N,K,C,relu", [(64, 64, 16, 1, False), (200, 256, 14, 2, True),
+                                          (7936, 256, 256, 2, True), (37, 6, 256, 1, False),
+                                          (1, 1, 1, 1, False), (130, 70, 33, 3, True)])
+def test_linear_forward(dev, M, N, K, C, relu):
+    from d3rlpy_amd import ops
+    g = torch.Generator().manual_seed(M * 7 + N)
+    x = torch.randn(M, K, generator=g).to(dev)
+    W = torch.randn(C, N, K, generator=g).to(dev)
+    b = torch.randn(C, N, generator=g).to(dev)
+    y = torch.full((C, M, N), float("nan"), device=dev)
+    ops.linear_fwd(x.data_ptr(), True, K, W.data_ptr(), b.data_ptr(), y.data_ptr(), C, M, K, N,
+                   relu)
+    torch.cuda.synchronize()
+    ref = torch.einsum("mk,cnk->cmn", x.double(), W.double()) + b.double()[:, None, :]
+    if relu:
+        ref = ref.clamp_min(0)
+    # exact-f32 MFMA chain: error <= K * 2^-24 * sum|a*b| ~ 1e-6 relative at K=256
+    assert _rel_err(y, ref) < 2e-6
+
+
+@pytest.mark.parametrize("R,Nin,Nout,C,splits", [(7936, 256, 256, 2, 31), (256, 14, 256, 2, 1),
+                                                 (100, 3, 7, 1, 3), (513, 256, 6, 1, 2)])
+def test_linear_backward(dev, R, Nin, Nout, C, splits):
+    from d3rlpy_amd import ops
+    g = torch.Generator().manual_seed(R + Nin)
+    x = torch.randn(C, R, Nin, generator=g).to(dev)
+    dy = torch.randn(C, R, Nout, generator=g).to(dev)
+    W = torch.randn(C, Nout, Nin, generator=g).to(dev)
+    h = torch.randn(C, R, Nin, generator=g).to(dev).clamp_min(0)
+    dW = torch.zeros(splits, C, Nout, Nin, device=dev)
+    ops.linear_bwd_w(dy.data_ptr(), Nout, R * Nout, x.data_ptr(), Nin, R * Nin, dW.data_ptr(), C,
+                     R, Nin, Nout, splits)
+    dx = torch.zeros(C, R, Nin, device=dev)
+    ops.linear_bwd_x(dy.data_ptr(), Nout, R * Nout, W.data_ptr(), dx.data_ptr(), Nin, R * Nin, C,
+                     R, Nin, Nout, mask=h.data_ptr(), ldm=Nin, smb=R * Nin)
+    torch.cuda.synchronize()
+    ref_dW = torch.einsum("crn,cri->cni", dy.double(), x.double())
+    ref_dx = torch.einsum("crn,cni->cri", dy.double(), W.double()) * (h.double() > 0)
+    assert _rel_err(dW.sum(0), ref_dW) < 5e-6
+    assert _rel_err(dx, ref_dx) < 5e-6
+
+
+def test_rowdot_colreduce_outer(dev):
+    from d3rlpy_amd import ops
+    g = torch.Generator().manual_seed(3)
+    C, R, H = 2, 1000, 256
+    X = torch.randn(C, R, H, generator=g).to(dev)
+    w = torch.randn(C, H, generator=g).to(dev)
+    bias = torch.randn(C, 1, generator=g).to(dev)
+    out = torch.zeros(C, R, device=dev)
+    ops.rowdot(X.data_ptr(), R * H, H, w.data_ptr(), H, bias.data_ptr(), 1, out.data_ptr(), R, C,
+               R, H)
+    gq = torch.randn(C, R, generator=g).to(dev)
+    S = 4
+    cr = torch.zeros(S, C, H, device=dev)
+    ops.colreduce(X.data_ptr(), R * H, H, gq.data_ptr(), R, cr.data_ptr(), H, C * H, C, R, H, S)
+    om = torch.zeros(C, R, H, device=dev)
+    ops.outer_mask(gq.data_ptr(), R, w.data_ptr(), H, X.data_ptr(), R * H, om.data_ptr(), R * H,
+                   C, R, H)
+    torch.cuda.synchronize()
+    ref = torch.einsum("crh,ch->cr", X.double(), w.double()) + bias.double()
+    assert _rel_err(out, ref) < 2e-6
+    ref_cr = torch.einsum("cr,crh->ch", gq.double(), X.double())
+    assert _rel_err(cr.sum(0), ref_cr) < 2e-6
+    ref_om = gq.double()[:, :, None] * w.double()[:, None, :] * (X.double() > 0)
+    assert torch.equal(om.cpu(), ref_om.float().cpu())
+
+
+def test_soft_update_bit_exact(dev):
+    """soft_sync (torch_utility.py:27-33): three separately rounded fp32 ops."""
+    from d3rlpy_amd import ops
+    g = torch.Generator().manual_seed(4)
+    src = torch.randn(100003, generator=g)
+    targ = torch.randn(100003, generator=g)
+    tau = 0.005
+    ref = targ.clone()
+    ref.mul_(1 - tau)
+    ref.add_(tau * src)
+    t = targ.to(dev)
+    ops.soft_update(t, src.to(dev), tau)
+    assert torch.equal(t.cpu(), ref)
+
+
+def test_adam_matches_torch(dev):
+    """torch.optim.Adam single-tensor step (the oracle's CPU Adam), 3 steps."""
+    from d3rlpy_amd.nets import AdamGroup, GradSpace, ParamStore
+    store = ParamStore()
+    store.add("w", (300, 7))
+    store.add("b", (5,))
+    store.allocate(dev)
+    g = torch.Generator().manual_seed(5)
+    w0 = torch.randn(300, 7, generator=g)
+    b0 = torch.randn(5, generator=g)
+    store.view("w").copy_(w0)
+    store.view("b").copy_(b0)
+    gs = GradSpace(dev)
+    gw = gs.add("w", (300, 7), 3)
+    gb = gs.add("b", (5,), 1)
+    opt = AdamGroup(store, ["w", "b"], gs, lr=3e-4)
+    pw = torch.nn.Parameter(w0.clone())
+    pb = torch.nn.Parameter(b0.clone())
+    topt = torch.optim.Adam([pw, pb], lr=3e-4)
+    for it in range(3):
+        parts = torch.randn(3, 300, 7, generator=g) * 10 ** (-it)
+        gbv = torch.randn(5, generator=g)
+        gw.copy_(parts)
+        gb.copy_(gbv.view(1, 5))
+        opt.launch()
+        pw.grad = parts[0] + parts[1] + parts[2]
+        pb.grad = gbv.clone()
+        topt.step()
+    torch.cuda.synchronize()
+    assert int(opt.step.item()) == 3
+    # identical formula; only the partial-sum order / lerp fma differ (<= few ulp)
+    torch.testing.assert_close(store.view("w").cpu(), pw.detach(), rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(store.view("b").cpu(), pb.detach(), rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(opt.exp_avg_sq.view("w").cpu(), topt.state[pw]["exp_avg_sq"],
+                               rtol=1e-6, atol=1e-12)
+
+
+def test_philox_statistics(dev):
+    from d3rlpy_amd import ops
+    out = torch.zeros(1 << 20, device=dev)
+    ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    tk = torch.zeros(1, dtype=torch.int32, device=dev)
+    nn_ = 1 << 19
+    ops.philox_fill(out, nn_, nn_, -1.0, 1.0, 1234, ctr, tk)
+    first = out.clone()
+    ops.philox_fill(out, nn_, nn_, -1.0, 1.0, 1234, ctr, tk)
+    torch.cuda.synchronize()
+    assert int(ctr.item()) == 2 and int(tk.item()) == 0
+    n = first[:nn_].double()
+    u = first[nn_:].double()
+    assert abs(float(n.mean())) < 0.01 and abs(float(n.std()) - 1) < 0.01
+    assert float(u.min()) >= -1.0 and float(u.max()) < 1.0 and abs(float(u.mean())) < 0.01
+    assert not torch.equal(first, out)  # the counter advanced -> fresh draws
