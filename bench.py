@@ -1,0 +1,232 @@
+#!/usr/bin/env python
+"""Gradient-steps/sec of the CQL update on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): CQL on synthetic
+hopper-medium-v0 shapes — obs 11, act 3, batch 256, n_critics 2,
+n_action_samples 10, hidden [256, 256], reference defaults
+(algos/cql.py:139-161) — over a 1M-transition synthetic D4RL-shaped dataset
+resident in HBM (RandomState(0); 1000-step episodes, terminal on the last
+step).  A "step" = one minibatch gather (device RandomIterator) + one full
+CQL._update (temp, alpha, critic, actor, both target updates) — the inner
+loop of fit() with per-step losses kept on device.
+
+Multi-GPU: K2 does not shard: ``--gpus N`` runs N independent
+learners (one per GPU, distinct seeds, "replicas") launched by
+torch.distributed.run; value = steps completed by all ranks / max-over-ranks
+wall time (weak scaling).
+
+Prints ONE JSON line (rank 0) with roofline (dominant kernel: the critic
+hidden-layer forward GEMM, fp32 MFMA) and cpu_baseline (the oracle's
+op-for-op CPU restatement of the same update, timed on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def _dist_setup():
+    import torch
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    return ws, rank, local
+
+
+def _barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def _max_over_ranks(x: float, ws: int) -> float:
+    if ws == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def build_workload(rank: int, n_transitions: int):
+    from d3rlpy_amd.algos.cql import CQL
+    from d3rlpy_amd.dataset import DeviceDataset
+    from d3rlpy_amd.datasets import get_synthetic_d4rl
+    from d3rlpy_amd.iterators import RandomIterator
+    ds = get_synthetic_d4rl("hopper-medium-v0", n=n_transitions, seed=0)
+    import torch
+    torch.manual_seed(rank)
+    algo = CQL(batch_size=256, n_critics=2, n_action_samples=10)
+    algo.build_with_dataset(ds)
+    ddata = DeviceDataset(ds)
+    it = RandomIterator(ddata, n_steps_per_epoch=1 << 40, batch_size=256,
+                        out=algo.impl.staging_batch(256), seed=1000 + rank)
+    return algo, it
+
+
+def gpu_steps(algo, it, n):
+    for _ in range(n):
+        batch = next(it)
+        algo._update_async(batch)
+
+
+def measure_kernel(ws_obj, reps: int = 50):
+    """Average duration of the dominant kernel via HIP events on its stream."""
+    import torch
+    launch, flops, desc = ws_obj.dominant_kernel()
+    for _ in range(3):
+        launch()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        launch()
+    e1.record(s)
+    torch.cuda.synchronize()
+    avg_s = e0.elapsed_time(e1) / 1e3 / reps
+    return avg_s, flops, desc
+
+
+def cpu_baseline(seconds: float, threads: int):
+    """The oracle CQL update (torch CPU, op for op) + the reference's host
+    sampler restated (per-sample np.random.randint + TransitionMiniBatch gather)."""
+    import torch
+    from oracle.cql import Batch, CQLNoise, CQLOracle
+    from oracle.gather import gather, random_indices, synthetic_dataset, to_episodes, to_transitions
+    torch.set_num_threads(threads)
+    n = 100_000
+    obs, act, rew, term = synthetic_dataset(n, 11, 3, episode_len=1000, seed=0)
+    trans = []
+    for o, a, r, t in to_episodes(obs, act, rew, term):
+        trans += to_transitions(o, a, r, t)
+    orc = CQLOracle(11, 3, n_critics=2, n_action_samples=10, seed=0)
+    gen = torch.Generator().manual_seed(0)
+    np.random.seed(0)
+
+    def step():
+        idx = random_indices(len(trans), 256)
+        b = gather([trans[i] for i in idx])
+        batch = Batch.from_numpy(b["observations"], b["actions"], b["rewards"],
+                                 b["next_observations"], b["terminals"], b["n_steps"])
+        orc.update(batch, CQLNoise.draw(gen, 256, 3, 10))
+
+    for _ in range(2):
+        step()
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        step()
+        k += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return k / el, k, el
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--transitions", type=int, default=1_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(os.path.dirname(
+        os.path.abspath(__file__)), "profiles", "r01_pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    ws, rank, local = _dist_setup()
+    algo, it = build_workload(rank, args.transitions)
+
+    gpu_steps(algo, it, args.warmup)
+    torch.cuda.synchronize()
+    _barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gpu_steps(algo, it, args.steps)
+    torch.cuda.synchronize()
+    _barrier(ws)
+    t1 = time.perf_counter()
+    elapsed = _max_over_ranks(t1 - t0, ws)
+    # sanity: the losses are finite
+    names, vals = algo.impl.read_metrics_ring(None)
+    finite = bool(np.isfinite(vals).all())
+
+    wsp = algo.impl._last_ws()
+    kern_s, kflops, kdesc = measure_kernel(wsp)
+    if rank != 0:
+        if ws > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+
+    peak_tflops = 157.3  # MI355X FP32 MFMA dense peak (MI355X_MICROARCH.md)
+    achieved = kflops / kern_s / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    cpu = None
+    if not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        sps, k, el = cpu_baseline(args.cpu_seconds, threads)
+        cpu = {"value": round(sps, 3), "unit": "gradient-steps/s", "cores": threads,
+               "kind": "port",
+               "sample": f"oracle CQL update (torch CPU, op-for-op restatement of "
+                         f"cql_impl.py/sac_impl.py/ddpg_impl.py) + reference host sampler "
+                         f"restated (np.random.randint per sample + TransitionMiniBatch "
+                         f"gather) on a 100k-transition synthetic dataset; {k} steps in "
+                         f"{el:.1f}s, {threads} threads"}
+    value = ws * args.steps / elapsed
+    out = {
+        "metric": "gradient-steps/sec (CQL, batch=256, obs=11 act=3) at 1/2/4/8 GPU",
+        "value": round(value, 2),
+        "unit": "gradient-steps/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (D4RL hopper-medium-v0 shapes, 1M transitions, HBM-resident)",
+        "config": {"workload": "CQL K2 (configs[1]): obs 11, act 3, batch 256, n_critics 2, "
+                               "n_action_samples 10, hidden [256,256], reference defaults",
+                   "global_batch": 256 * ws, "parallelism": f"replicas x{ws}",
+                   "losses_finite": finite},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak_tflops,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak_tflops, 4),
+                     "traffic": traffic, "kernel": kdesc,
+                     "avg_launch_us": round(kern_s * 1e6, 3)},
+        "cpu_baseline": cpu,
+    }
+    if cpu is not None:
+        out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+    print(json.dumps(out))
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -64,7 +64,7 @@ class CqlLossDesc(C.Structure):
         ("rew", vp), ("term", vp), ("n_steps", vp),
         ("log_temp", vp), ("temp_m", vp), ("temp_v", vp), ("temp_step", vp),
         ("log_alpha", vp), ("alpha_m", vp), ("alpha_v", vp), ("alpha_step", vp),
-        ("dq", vp), ("metrics", vp), ("scalars", vp),
+        ("dq", vp), ("lse", vp), ("metrics", vp), ("scalars", vp),
         ("B", C.c_int32), ("A", C.c_int32), ("N", C.c_int32), ("C", C.c_int32),
         ("R", C.c_int64),
         ("gamma", C.c_float), ("temp_lr", C.c_double), ("alpha_lr", C.c_double),

@@ -37,7 +37,8 @@ from torch import nn
 
 from .. import _native as NAT
 from .. import mlp, ops
-from ..nets import AdamGroup, EnsembleMLP, GradSpace, ParamStore
+from .. import checkpoint as ckpt
+from ..nets import AdamGroup, EnsembleMLP, GradSpace, OptimState, ParamStore
 from .impl_base import DeviceBatch, ImplBase, as_device_batch
 
 METRIC_NAMES = ("temp_loss", "temp", "alpha_loss", "alpha", "critic_loss", "actor_loss",
@@ -132,7 +133,80 @@ class CQLImpl(ImplBase):
         self.alpha_m = torch.zeros(1, device=dev)
         self.alpha_v = torch.zeros(1, device=dev)
         self.alpha_step = torch.zeros(1, dtype=torch.int64, device=dev)
+        f = self._critic_optim_factory
+        self.critic_state = OptimState(store, self.critic.names(), self._critic_learning_rate,
+                                       f.betas, f.eps)
+        f = self._actor_optim_factory
+        self.actor_state = OptimState(store, self.policy.names(), self._actor_learning_rate,
+                                      f.betas, f.eps)
         self._built = True
+
+    # ---------------------------------------------------------- checkpoints
+    def _critic_refs(self):
+        """EnsembleContinuousQFunction.parameters() order and state-dict keys."""
+        refs, L = [], self.critic.n_layers
+        for c in range(self._n_critics):
+            for l in range(L - 1):
+                refs.append((f"_q_funcs.{c}._encoder._fcs.{l}.weight", self.critic.wname(l), c, None))
+                refs.append((f"_q_funcs.{c}._encoder._fcs.{l}.bias", self.critic.bname(l), c, None))
+            refs.append((f"_q_funcs.{c}._fc.weight", self.critic.wname(L - 1), c, None))
+            refs.append((f"_q_funcs.{c}._fc.bias", self.critic.bname(L - 1), c, None))
+        return refs
+
+    def _policy_refs(self):
+        """SquashedNormalPolicy.parameters() order: encoder fcs, _mu, _logstd."""
+        refs, L, A = [], self.policy.n_layers, self._action_size
+        for l in range(L - 1):
+            refs.append((f"_encoder._fcs.{l}.weight", self.policy.wname(l), 0, None))
+            refs.append((f"_encoder._fcs.{l}.bias", self.policy.bname(l), 0, None))
+        mu, ls = slice(0, A), slice(A, 2 * A)
+        refs += [("_mu.weight", self.policy.wname(L - 1), 0, mu),
+                 ("_mu.bias", self.policy.bname(L - 1), 0, mu),
+                 ("_logstd.weight", self.policy.wname(L - 1), 0, ls),
+                 ("_logstd.bias", self.policy.bname(L - 1), 0, ls)]
+        return refs
+
+    def get_state_dict(self) -> Dict[str, dict]:
+        """torch_utility.get_state_dict layout of the reference CQLImpl."""
+        torch.cuda.synchronize()
+        cr, pr = self._critic_refs(), self._policy_refs()
+        tf, af = self._temp_optim_factory, self._alpha_optim_factory
+        return {
+            "_q_func": ckpt.module_state(self.store, cr),
+            "_targ_q_func": ckpt.module_state(self.targ, cr),
+            "_policy": ckpt.module_state(self.store, pr),
+            "_targ_policy": ckpt.module_state(self.targ, pr),
+            "_log_temp": {"_parameter": self.log_temp.detach().view(1, 1).cpu().clone()},
+            "_log_alpha": {"_parameter": self.log_alpha.detach().view(1, 1).cpu().clone()},
+            "_critic_optim": ckpt.adam_state(self.critic_state, cr),
+            "_actor_optim": ckpt.adam_state(self.actor_state, pr),
+            "_temp_optim": ckpt.scalar_adam_state(self.temp_m, self.temp_v, self.temp_step,
+                                                  self._temp_learning_rate, tf.betas, tf.eps),
+            "_alpha_optim": ckpt.scalar_adam_state(self.alpha_m, self.alpha_v, self.alpha_step,
+                                                   self._alpha_learning_rate, af.betas, af.eps),
+        }
+
+    def set_state_dict(self, sd: Dict[str, dict]) -> None:
+        cr, pr = self._critic_refs(), self._policy_refs()
+        ckpt.load_module_state(self.store, cr, sd["_q_func"])
+        ckpt.load_module_state(self.targ, cr, sd["_targ_q_func"])
+        ckpt.load_module_state(self.store, pr, sd["_policy"])
+        ckpt.load_module_state(self.targ, pr, sd["_targ_policy"])
+        with torch.no_grad():
+            self.log_temp.copy_(torch.as_tensor(sd["_log_temp"]["_parameter"]).view(-1))
+            self.log_alpha.copy_(torch.as_tensor(sd["_log_alpha"]["_parameter"]).view(-1))
+        ckpt.load_adam_state(self.critic_state, cr, sd["_critic_optim"])
+        ckpt.load_adam_state(self.actor_state, pr, sd["_actor_optim"])
+        ckpt.load_scalar_adam_state(self.temp_m, self.temp_v, self.temp_step, sd["_temp_optim"])
+        ckpt.load_scalar_adam_state(self.alpha_m, self.alpha_v, self.alpha_step,
+                                    sd["_alpha_optim"])
+        torch.cuda.synchronize()
+
+    def save_model(self, fname: str) -> None:
+        torch.save(self.get_state_dict(), fname)
+
+    def load_model(self, fname: str) -> None:
+        self.set_state_dict(torch.load(fname, map_location="cpu", weights_only=True))
 
     def _init_like_reference(self) -> None:
         """nn.Linear default init in the reference construction order."""
@@ -201,9 +275,41 @@ class CQLImpl(ImplBase):
         ws.stage(db, noise)
         ws.execute(flags, use_graph=use_graph and noise is None)
         if not sync:
-            return ws.metrics
+            return None
         vals = ws.metrics.cpu().numpy()
         return {k: float(v) for k, v in zip(METRIC_NAMES, vals)}
+
+    # ------------------------------------------------- device-side batches
+    def staging_batch(self, batch_size: int) -> DeviceBatch:
+        """DeviceBatch whose tensors ARE this Impl's input buffers: a gather
+        into it feeds update_step with zero copies."""
+        ws = self._workspace(batch_size)
+        B = batch_size
+        return DeviceBatch(ws.obs2[:B], ws.act, ws.rew, ws.obs2[B:], ws.term, ws.nsteps)
+
+    def active_metric_names(self):
+        names = []
+        if self._temp_learning_rate > 0:
+            names += ["temp_loss", "temp"]
+        if self._alpha_learning_rate > 0:
+            names += ["alpha_loss", "alpha"]
+        return names + ["critic_loss", "actor_loss"]
+
+    def metrics_ring(self, n_steps: int):
+        for ws in self._ws.values():
+            ws.ring_ctr.zero_()
+        return n_steps
+
+    def read_metrics_ring(self, handle):
+        names = self.active_metric_names()
+        if not self._ws:
+            return names, np.zeros((0, len(names)), dtype=np.float32)
+        ws = self._last_ws()
+        cnt = int(ws.ring_ctr.item())
+        k = min(cnt, ws.ring.shape[0])
+        vals = ws.ring[:k].cpu().numpy()
+        cols = [METRIC_NAMES.index(n) for n in names]
+        return names, vals[:, cols]
 
     # ------------------------------------------------------------- inference
     def _policy_head(self, x: torch.Tensor) -> torch.Tensor:
@@ -287,11 +393,15 @@ class _Workspace:
         self.tacts = mlp.Acts.alloc(impl.critic, B, dev)
         self.aacts = mlp.Acts.alloc(impl.critic, B, dev)
         self.dq = z(C, self.R)
+        self.lse = z(2, C, B)
         self.adq = z(C, B)
         self.adx = z(C, B, DA)
         self.dhead = z(B, 2 * A)
         self.metrics = z(len(METRIC_NAMES))
         self.scalars = z(4)
+        # per-step metric history (read back once per epoch by the fitter)
+        self.ring = z(1 << 16, len(METRIC_NAMES))
+        self.ring_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         # backward spaces + optimisers
         self.Rc = 3 * NB + B
         self.cgrads = GradSpace(dev)
@@ -299,12 +409,8 @@ class _Workspace:
         self.abwd = mlp.BackwardSpace(impl.critic, B, None, dev)
         self.pgrads = GradSpace(dev)
         self.pbwd = mlp.BackwardSpace(impl.policy, B, self.pgrads, dev)
-        f = impl._critic_optim_factory
-        self.critic_opt = AdamGroup(impl.store, impl.critic.names(), self.cgrads,
-                                    impl._critic_learning_rate, f.betas, f.eps)
-        f = impl._actor_optim_factory
-        self.actor_opt = AdamGroup(impl.store, impl.policy.names(), self.pgrads,
-                                   impl._actor_learning_rate, f.betas, f.eps)
+        self.critic_opt = AdamGroup(impl.critic_state, self.cgrads)
+        self.actor_opt = AdamGroup(impl.actor_state, self.pgrads)
         # share optimiser state across workspaces of other batch sizes
         prev = [w for w in impl._ws.values()]
         if prev:
@@ -346,6 +452,7 @@ class _Workspace:
                                                            impl.alpha_step.data_ptr())
         l.dq, l.metrics, l.scalars = (self.dq.data_ptr(), self.metrics.data_ptr(),
                                       self.scalars.data_ptr())
+        l.lse = self.lse.data_ptr()
         l.B, l.A, l.N, l.C, l.R = self.B, self.A, self.N, self.C, self.R
         l.gamma = impl._gamma
         tf, af = impl._temp_optim_factory, impl._alpha_optim_factory
@@ -400,6 +507,24 @@ class _Workspace:
         ur[0].copy_(g("alpha_rand").view(NB, A))
         ur[1].copy_(g("critic_rand").view(NB, A))
         self.eps_actor.copy_(g("eps_actor").view(-1))
+
+    # ------------------------------------------------------------ roofline
+    def dominant_kernel(self):
+        """(launch_fn, flops_per_launch, description) of the critic hidden-layer
+        forward GEMM over all Q rows of the step (the MFMA-bound hot kernel):
+        C x R x H x H MACs, R = 6NB+B (update_alpha on) rows."""
+        impl = self.impl
+        net, st = impl.critic, impl.store
+        H = net.sizes[2]
+        Hin = net.sizes[1]
+        R, C = self.R, self.C
+        h0, h1 = self.qacts.h[0], self.qacts.h[1]
+
+        def launch():
+            ops.linear_fwd(h0.data_ptr(), False, Hin, net.W(1, st), net.b(1, st), h1.data_ptr(),
+                           C, R, Hin, H, relu=True, ldy=H, sxb=R * Hin, syb=R * H)
+        flops = 2 * C * R * Hin * H
+        return launch, flops, f"gemm_f32 critic layer-2 fwd: C={C} x [{R}x{Hin}]@[{Hin}x{H}]"
 
     # ------------------------------------------------------------- pipeline
     def execute(self, flags, use_graph: bool) -> None:
@@ -468,3 +593,7 @@ class _Workspace:
             self.actor_opt.launch()
         if targets:
             ops.soft_update(impl.targ.data, impl.store.data, impl._tau)
+        NAT.check(NAT.lib().d3a_metrics_push(self.metrics.data_ptr(), len(METRIC_NAMES),
+                                             self.ring.data_ptr(), self.ring.shape[0],
+                                             self.ring_ctr.data_ptr(), ops._stream()),
+                  "d3a_metrics_push")

@@ -205,6 +205,14 @@ class LearnableBase:
             at = self.get_action_type()
             if at != ActionSpace.BOTH:
                 assert (at == ActionSpace.DISCRETE) == discrete, "action space mismatch"
+        if self._scaler is not None and isinstance(dataset, MDPDataset):
+            self._scaler.fit_dataset(dataset)
+        if self._impl is None:
+            obs_shape = self._process_observation_shape(ddata.observation_shape)
+            self.create_impl(obs_shape, ddata.action_size)
+        # the iterator gathers straight into the Impl's input buffers (no copies)
+        out = self._impl.staging_batch(self._batch_size) \
+            if hasattr(self._impl, "staging_batch") else None
         iterator: TransitionIterator
         if n_epochs is None and n_steps is not None:
             assert n_steps >= n_steps_per_epoch
@@ -212,12 +220,13 @@ class LearnableBase:
             iterator = RandomIterator(ddata, n_steps_per_epoch, batch_size=self._batch_size,
                                       n_steps=self._n_steps, gamma=self._gamma,
                                       n_frames=self._n_frames, real_ratio=self._real_ratio,
-                                      generated_maxlen=self._generated_maxlen)
+                                      generated_maxlen=self._generated_maxlen, out=out)
         elif n_epochs is not None and n_steps is None:
             iterator = RoundIterator(ddata, batch_size=self._batch_size, n_steps=self._n_steps,
                                      gamma=self._gamma, n_frames=self._n_frames,
                                      real_ratio=self._real_ratio,
-                                     generated_maxlen=self._generated_maxlen, shuffle=shuffle)
+                                     generated_maxlen=self._generated_maxlen, shuffle=shuffle,
+                                     out=out)
         else:
             raise ValueError("Either of n_epochs or n_steps must be given.")
 
@@ -225,11 +234,6 @@ class LearnableBase:
         logger = OfflineLogger(name, save_metrics=save_metrics, root_dir=logdir,
                                verbose=verbose, with_timestamp=with_timestamp)
         self._active_logger = logger
-        if self._scaler is not None and isinstance(dataset, MDPDataset):
-            self._scaler.fit_dataset(dataset)
-        if self._impl is None:
-            obs_shape = self._process_observation_shape(ddata.observation_shape)
-            self.create_impl(obs_shape, ddata.action_size)
         if save_metrics:
             self.save_params(logger.logdir)
         self._eval_results = defaultdict(list)

@@ -131,24 +131,43 @@ __device__ __forceinline__ float is_value(const d3a_cql_loss_desc& d, int64_t c,
   return qv - rand_logp;
 }
 
-__device__ float lse_row(const d3a_cql_loss_desc& d, int64_t c, int64_t s, int64_t b,
-                         float rand_logp) {
-  const int64_t M = 3 * (int64_t)d.N;
+// Stage A (many waves): one wave per (sample set s, critic c, batch row b):
+// lse[s][c][b] = logsumexp_j v_j over the 3N IS values (torch.logsumexp:
+// amax shift, |max| == inf -> 0), and for the critic set the softmax
+// weights exp(v_j - lse) into dq (scaled by the alpha-dependent factor in
+// stage B).
+__global__ __launch_bounds__(256) void cql_lse_kernel(d3a_cql_loss_desc d) {
+  const int lane = threadIdx.x & 63;
+  const int64_t B = d.B, C = d.C, N = d.N, NB = N * B, M = 3 * N;
+  const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= 2 * C * B) return;
+  const int64_t s = p / (C * B), c = (p / B) % C, b = p % B;
+  if ((s == 0 && !d.update_alpha) || (s == 1 && !d.update_critic)) return;
+  const float rand_logp = (float)log(pow(0.5, (double)d.A));
   float mx = -INFINITY;
-  for (int64_t j = 0; j < M; ++j) mx = fmaxf(mx, is_value(d, c, s, b, j, rand_logp));
-  if (isinf(mx)) mx = 0.f;  // torch.logsumexp: |max| == inf -> use 0 as the shift
+  for (int64_t j = lane; j < M; j += 64) mx = fmaxf(mx, is_value(d, c, s, b, j, rand_logp));
+  mx = wave_max(mx);
+  if (isinf(mx)) mx = 0.f;
   float se = 0.f;
-  for (int64_t j = 0; j < M; ++j) se += expf(is_value(d, c, s, b, j, rand_logp) - mx);
-  return logf(se) + mx;
+  for (int64_t j = lane; j < M; j += 64) se += expf(is_value(d, c, s, b, j, rand_logp) - mx);
+  se = wave_sum(se);
+  const float l = logf(se) + mx;
+  if (lane == 0) d.lse[(s * C + c) * B + b] = l;
+  if (s == 1) {
+    for (int64_t j = lane; j < M; j += 64) {
+      const int64_t blk = j / N, n = j % N;
+      d.dq[c * d.R + 3 * NB + blk * NB + b * N + n] = expf(is_value(d, c, 1, b, j, rand_logp) - l);
+    }
+  }
 }
 
+// Stage B (one workgroup): temperature and alpha Adam steps, TD loss, and
+// final dL/dQ (scales stage A's softmax weights by the new clipped alpha).
 __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   __shared__ float scratch[16];
   __shared__ float sh[4];
   const int tid = threadIdx.x, nt = blockDim.x;
   const int64_t B = d.B, C = d.C, N = d.N, NB = N * B;
-  // random_log_probs = math.log(0.5 ** action_size) (cql_impl.py:191)
-  const float rand_logp = (float)log(pow(0.5, (double)d.A));
 
   // ---- update_temp (sac_impl.py:123-146) ----
   if (d.update_temp) {
@@ -173,7 +192,7 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
     float sl = 0.f, sd = 0.f;
     for (int64_t p = tid; p < C * B; p += nt) {
       const int64_t c = p / B, b = p % B;
-      sl += lse_row(d, c, 0, b, rand_logp);
+      sl += d.lse[c * B + b];
       sd += d.q[c * d.R + 6 * NB + b];
     }
     const float lsum = block_sum(sl, scratch);
@@ -216,21 +235,14 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
     const float diff = qd - y;
     s_td += diff * diff;
     s_d += qd;
-    const float l = lse_row(d, c, 1, b, rand_logp);
-    s_l += l;
-    // softmax weights of the critic-set IS values
-    const int64_t M = 3 * N;
-    for (int64_t j = 0; j < M; ++j) {
-      const int64_t blk = j / N, n = j % N;
-      const float v = is_value(d, c, 1, b, j, rand_logp);
-      d.dq[c * d.R + 3 * NB + blk * NB + b * N + n] = gcons * expf(v - l);
-    }
+    s_l += d.lse[(C + c) * B + b];
     d.dq[c * d.R + 6 * NB + b] = 2.f * diff / (float)B - gcons;
   }
-  // alpha-set rows carry no critic gradient
-  for (int64_t p = tid; p < C * 3 * NB; p += nt) {
-    const int64_t c = p / (3 * NB), r = p % (3 * NB);
-    d.dq[c * d.R + r] = 0.f;
+  // critic-set IS rows: softmax weight * gcons; alpha-set rows: no critic gradient
+  for (int64_t p = tid; p < C * 6 * NB; p += nt) {
+    const int64_t c = p / (6 * NB), r = p % (6 * NB);
+    float* q = d.dq + c * d.R + r;
+    *q = (r < 3 * NB) ? 0.f : gcons * (*q);
   }
   const float td = block_sum(s_td, scratch) / (float)B;
   const float lsum = block_sum(s_l, scratch);
@@ -313,6 +325,12 @@ extern "C" int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream) {
 extern "C" int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream) {
   D3A_CHECK_ARG(d, "d3a_cql_loss: null desc");
   D3A_CHECK_ARG(d->R == 6LL * d->N * d->B + d->B, "d3a_cql_loss: R must be 6NB+B");
+  D3A_CHECK_ARG(d->lse != nullptr, "d3a_cql_loss: lse workspace required");
+  if (d->update_alpha || d->update_critic) {
+    const int64_t waves = 2LL * d->C * d->B;
+    hipLaunchKernelGGL(cql_lse_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, *d);
+  }
   hipLaunchKernelGGL(cql_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, *d);
   D3A_LAUNCH_CHECK("d3a_cql_loss");
   return 0;

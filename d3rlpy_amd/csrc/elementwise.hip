@@ -46,27 +46,40 @@ __global__ __launch_bounds__(256) void rowdot_kernel(const float* X, int64_t sXb
   if (lane == 0) out[b * sOb + r] = acc + (bias ? bias[b * sbb] : 0.f);
 }
 
-// ---- colreduce: thread per column, rows split across blockIdx.y ------------
+// ---- colreduce: column tile of TW columns x RL row lanes per 256-thread block
+// thread t: column (t % TW), row lane (t / TW) walks rows r0+rl, r0+rl+RL, ...;
+// the RL partial sums are combined through LDS in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void colreduce_kernel(const float* X, int64_t sXb, int64_t sXr,
                                                         const float* w, int64_t swb, float* out,
                                                         int64_t sOb, int64_t sOs, int64_t rows,
-                                                        int64_t n, int64_t splits) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                                        int64_t n, int64_t splits, int TW) {
+  __shared__ double part[256];
+  const int t = threadIdx.x;
+  const int RL = 256 / TW;
+  const int cl = t % TW, rl = t / TW;
+  const int64_t j = (int64_t)blockIdx.x * TW + cl;
   const int64_t s = blockIdx.y, b = blockIdx.z;
-  if (j >= n) return;
   const int64_t chunk = (rows + splits - 1) / splits;
   const int64_t r0 = s * chunk;
   const int64_t r1 = (r0 + chunk < rows) ? r0 + chunk : rows;
-  const float* x = X + b * sXb + j;
-  const float* wb = w ? w + b * swb : nullptr;
   // fp64 accumulation: bias / head gradients sum thousands of mixed-sign rows
   double acc = 0.0;
-  if (wb) {
-    for (int64_t r = r0; r < r1; ++r) acc += (double)(wb[r] * x[r * sXr]);
-  } else {
-    for (int64_t r = r0; r < r1; ++r) acc += (double)x[r * sXr];
+  if (j < n) {
+    const float* x = X + b * sXb + j;
+    const float* wb = w ? w + b * swb : nullptr;
+    if (wb) {
+      for (int64_t r = r0 + rl; r < r1; r += RL) acc += (double)(wb[r] * x[r * sXr]);
+    } else {
+      for (int64_t r = r0 + rl; r < r1; r += RL) acc += (double)x[r * sXr];
+    }
   }
-  out[b * sOb + s * sOs + j] = (float)acc;
+  part[t] = acc;
+  __syncthreads();
+  if (rl == 0 && j < n) {
+    double tot = 0.0;
+    for (int q = 0; q < RL; ++q) tot += part[q * TW + cl];
+    out[b * sOb + s * sOs + j] = (float)tot;
+  }
 }
 
 // ---- outer_mask: out[r][j] = g[r] * w[j] * (h[r][j] > 0) ------------------
@@ -105,9 +118,18 @@ __global__ __launch_bounds__(256) void outer_mask_kernel(const float* g, int64_t
 __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs, int64_t* step,
                                                    unsigned int* ticket, double lr, double beta1,
                                                    double beta2, double eps) {
+  __shared__ float s_step_size, s_bc2_sqrt;
   const d3a_adam_segment sg = segs[blockIdx.y];
   const int64_t t = *step + 1;  // read by every block before the last one commits
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (threadIdx.x == 0) {
+    // bias corrections in fp64 exactly as torch computes them in Python floats
+    const double bc1 = 1.0 - pow(beta1, (double)t);
+    const double bc2 = 1.0 - pow(beta2, (double)t);
+    s_step_size = (float)(lr / bc1);
+    s_bc2_sqrt = (float)sqrt(bc2);
+  }
+  __syncthreads();
   if (i < sg.numel) {
     double gd = 0.0;  // split-K partials summed in a fixed order, in fp64
     for (int64_t q = 0; q < sg.n_partials; ++q) gd += (double)sg.grad[q * sg.partial_stride + i];
@@ -122,10 +144,8 @@ __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
     float v = __fmul_rn(sg.exp_avg_sq[i], (float)beta2);
     const float omb2 = (float)(1.0 - beta2);
     v = __fadd_rn(v, __fmul_rn(__fmul_rn(omb2, g), g));
-    const double bc1 = 1.0 - pow(beta1, (double)t);
-    const double bc2 = 1.0 - pow(beta2, (double)t);
-    const float step_size = (float)(lr / bc1);
-    const float bc2_sqrt = (float)sqrt(bc2);
+    const float step_size = s_step_size;
+    const float bc2_sqrt = s_bc2_sqrt;
     const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), (float)eps);
     const float pnew = __fadd_rn(sg.param[i], __fmul_rn(-step_size, __fdiv_rn(m, denom)));
     sg.exp_avg[i] = m;
@@ -246,9 +266,11 @@ extern "C" int d3a_colreduce_f32(const float* X, int64_t sXb, int64_t sXr, const
   D3A_CHECK_ARG(X && out, "d3a_colreduce_f32: null pointer");
   D3A_CHECK_ARG(splits >= 1, "d3a_colreduce_f32: splits >= 1");
   if (batch <= 0 || n <= 0) return 0;
-  dim3 grid((unsigned)((n + 255) / 256), (unsigned)splits, (unsigned)batch);
+  int TW = 1;
+  while (TW < n && TW < 64) TW <<= 1;  // columns per block (power of two <= 64)
+  dim3 grid((unsigned)((n + TW - 1) / TW), (unsigned)splits, (unsigned)batch);
   hipLaunchKernelGGL(colreduce_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, sXb, sXr, w,
-                     swb, out, sOb, sOs, rows, n, splits);
+                     swb, out, sOb, sOs, rows, n, splits, TW);
   D3A_LAUNCH_CHECK("d3a_colreduce_f32");
   return 0;
 }

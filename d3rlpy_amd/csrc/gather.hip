@@ -70,7 +70,11 @@ __global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
     int64_t nt_i = t;
     int k = 0;
     for (k = 0; k < d.n_steps; ++k) {
-      ret += d.rew[d.t_row[nt_i]] * powf(d.gamma, (float)k);
+      // n_step_return += reward * gamma ** i   (dataset.pyx:1325); gamma**i is
+      // evaluated as the fp32 rounding of the fp64 power, then one fp32
+      // multiply and one fp32 add (no contraction), matching oracle/gather.py
+      const float gp = (float)pow((double)d.gamma, (double)k);
+      ret = __fadd_rn(ret, __fmul_rn(d.rew[d.t_row[nt_i]], gp));
       if (nt_i == d.t_ep_last[nt_i] || k == d.n_steps - 1) break;
       nt_i += 1;
     }

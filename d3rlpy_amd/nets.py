@@ -149,24 +149,42 @@ class GradSpace:
         return self.parts[name][0]
 
 
-class AdamGroup:
-    """A torch.optim.Adam equivalent over a set of segments of a ParamStore.
+class OptimState:
+    """torch.optim.Adam state of a set of segments: exp_avg / exp_avg_sq in
+    store-shaped buffers plus the (device) step count of the optimiser."""
 
-    Exposes the reduced gradient of the last step per segment (``grad(name)``)
-    for parity tests, and the torch-format state (exp_avg / exp_avg_sq / step).
-    """
-
-    def __init__(self, store: ParamStore, names: Sequence[str], grads: GradSpace, lr: float,
-                 betas=(0.9, 0.999), eps: float = 1e-8, keep_grads: bool = True):
+    def __init__(self, store: ParamStore, names: Sequence[str], lr: float,
+                 betas=(0.9, 0.999), eps: float = 1e-8):
         assert store.data is not None
         self.store = store
         self.names = list(names)
-        self.lr, self.beta1, self.beta2, self.eps = float(lr), float(betas[0]), float(betas[1]), float(eps)
+        self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
         dev = store.data.device
         self.exp_avg = store.like()
         self.exp_avg_sq = store.like()
         self.step = torch.zeros(1, dtype=torch.int64, device=dev)
         self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+
+
+class AdamGroup:
+    """A torch.optim.Adam equivalent over a set of segments of a ParamStore.
+
+    Exposes the reduced gradient of the last step per segment (``grad(name)``)
+    for parity tests; the optimiser state lives in an ``OptimState``.
+    """
+
+    def __init__(self, state: OptimState, grads: GradSpace, keep_grads: bool = True):
+        store = state.store
+        self.state = state
+        self.store = store
+        self.names = list(state.names)
+        self.lr, self.eps = state.lr, state.eps
+        self.beta1, self.beta2 = state.betas
+        dev = store.data.device
+        self.exp_avg = state.exp_avg
+        self.exp_avg_sq = state.exp_avg_sq
+        self.step = state.step
+        self.ticket = state.ticket
         self.grad_store = store.like() if keep_grads else None
         segs = (N.AdamSegment * len(self.names))()
         self.max_numel = 1

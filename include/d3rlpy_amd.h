@@ -169,7 +169,8 @@ typedef struct d3a_cql_sample_desc {
 } d3a_cql_sample_desc;
 int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream);
 
-/* Loss stage of one CQL update, one workgroup: update_temp
+/* Loss stage of one CQL update (two launches: a wave-per-row logsumexp
+ * kernel, then one workgroup for the scalars): update_temp
  * (sac_impl.py:123-146) incl. its Adam step on log_temp, update_alpha
  * (cql_impl.py:119-141) incl. its Adam step on log_alpha, the TD target
  * (cql_impl.py:232-243, mean_q_function.py:268-270) and dL/dQ of every
@@ -187,6 +188,7 @@ typedef struct d3a_cql_loss_desc {
   float* log_alpha;        /* [1] parameter, updated in place              */
   float* alpha_m; float* alpha_v; int64_t* alpha_step;
   float* dq;               /* [C][R] dL_critic/dQ (alpha rows set to 0)    */
+  float* lse;              /* [2][C][B] workspace: logsumexp per set       */
   float* metrics;          /* [8]: temp_loss temp alpha_loss alpha critic_loss
                               td_loss conservative_loss (reserved)          */
   float* scalars;          /* [4]: exp(log_temp_new) exp(log_alpha_new) .. */

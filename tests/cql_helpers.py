@@ -108,3 +108,13 @@ def max_rel(a, b):
     a = torch.as_tensor(a).double().cpu()
     b = torch.as_tensor(b).double().cpu()
     return float((a - b).abs().max()) / max(1e-30, float(b.abs().max()))
+
+
+ORACLE_STATE_KEYS = ("_q_func", "_targ_q_func", "_policy", "_targ_policy", "_log_temp",
+                     "_log_alpha", "_critic_optim", "_actor_optim", "_temp_optim",
+                     "_alpha_optim")
+
+
+def oracle_state(orc):
+    """torch_utility.get_state_dict(impl) of the oracle (reference attribute names)."""
+    return {k: getattr(orc, k).state_dict() for k in ORACLE_STATE_KEYS}

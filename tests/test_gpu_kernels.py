@@ -125,7 +125,8 @@ def test_adam_matches_torch(dev):
     gs = GradSpace(dev)
     gw = gs.add("w", (300, 7), 3)
     gb = gs.add("b", (5,), 1)
-    opt = AdamGroup(store, ["w", "b"], gs, lr=3e-4)
+    from d3rlpy_amd.nets import OptimState
+    opt = AdamGroup(OptimState(store, ["w", "b"], lr=3e-4), gs)
     pw = torch.nn.Parameter(w0.clone())
     pb = torch.nn.Parameter(b0.clone())
     topt = torch.optim.Adam([pw, pb], lr=3e-4)
@@ -135,7 +136,8 @@ def test_adam_matches_torch(dev):
         gw.copy_(parts)
         gb.copy_(gbv.view(1, 5))
         opt.launch()
-        pw.grad = parts[0] + parts[1] + parts[2]
+        # the kernel sums split-K partials in fp64 (then rounds once)
+        pw.grad = parts.double().sum(0).float()
         pb.grad = gbv.clone()
         topt.step()
     torch.cuda.synchronize()
