@@ -27,7 +27,7 @@ vp = C.c_void_p
 
 class GemmDesc(C.Structure):
     _fields_ = [
-        ("A", vp), ("B", vp), ("C", vp), ("bias", vp), ("mask", vp),
+        ("A", vp), ("B", vp), ("C", vp), ("bias", vp), ("mask", vp), ("rowsum", vp),
         ("M", C.c_int64), ("N", C.c_int64), ("K", C.c_int64), ("batch", C.c_int64),
         ("sAb", C.c_int64), ("sAm", C.c_int64), ("sAk", C.c_int64),
         ("sBb", C.c_int64), ("sBk", C.c_int64), ("sBn", C.c_int64),
@@ -35,7 +35,25 @@ class GemmDesc(C.Structure):
         ("sbias_b", C.c_int64),
         ("sMb", C.c_int64), ("sMm", C.c_int64), ("sMn", C.c_int64),
         ("splits", C.c_int64), ("sCs", C.c_int64),
+        ("sRb", C.c_int64), ("sRs", C.c_int64),
         ("alpha", C.c_float), ("relu", C.c_int32), ("accumulate", C.c_int32),
+        ("variant", C.c_int32),
+    ]
+
+
+class Head1BwdDesc(C.Structure):
+    _fields_ = [
+        ("g", vp), ("sgb", C.c_int64),
+        ("q_min", vp), ("sqb", C.c_int64),
+        ("scale", C.c_float),
+        ("g_out", vp),
+        ("h", vp), ("shb", C.c_int64), ("ldh", C.c_int64),
+        ("w", vp), ("swb", C.c_int64),
+        ("dz", vp), ("sdzb", C.c_int64), ("lddz", C.c_int64),
+        ("dW", vp), ("sWs", C.c_int64),
+        ("db", vp), ("sbs", C.c_int64),
+        ("rows", C.c_int64), ("n", C.c_int64), ("splits", C.c_int64),
+        ("C", C.c_int32),
     ]
 
 
@@ -113,12 +131,14 @@ _SIGNATURES = {
                                     C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
     "d3a_outer_mask_f32": (C.c_int, [vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
                                      C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
-    "d3a_adam_f32": (C.c_int, [vp, C.c_int32, C.c_int64, vp, vp, C.c_double, C.c_double,
+    "d3a_adam_f32": (C.c_int, [vp, C.c_int32, C.c_int64, vp, C.c_double, C.c_double,
                                C.c_double, C.c_double, vp]),
     "d3a_soft_update_f32": (C.c_int, [vp, vp, C.c_int64, C.c_double, vp]),
-    "d3a_metrics_push": (C.c_int, [vp, C.c_int32, vp, C.c_int64, vp, vp]),
+    "d3a_step_end": (C.c_int, [vp, C.c_int32, vp, C.c_int64, vp, vp, C.c_uint32, vp, vp,
+                               C.c_int64, C.c_double, vp]),
     "d3a_philox_fill": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_float, C.c_float, C.c_uint64,
                                   vp, vp, vp]),
+    "d3a_head1_bwd": (C.c_int, [C.POINTER(Head1BwdDesc), vp]),
     "d3a_cql_sample": (C.c_int, [C.POINTER(CqlSampleDesc), vp]),
     "d3a_cql_loss": (C.c_int, [C.POINTER(CqlLossDesc), vp]),
     "d3a_sac_actor_dq": (C.c_int, [vp, C.c_int64, C.c_int32, C.c_int32, vp, C.c_int64, vp]),

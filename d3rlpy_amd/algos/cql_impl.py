@@ -133,12 +133,14 @@ class CQLImpl(ImplBase):
         self.alpha_m = torch.zeros(1, device=dev)
         self.alpha_v = torch.zeros(1, device=dev)
         self.alpha_step = torch.zeros(1, dtype=torch.int64, device=dev)
+        # optimiser step counts: [0] critic, [1] actor (committed by d3a_step_end)
+        self.counters = torch.zeros(8, dtype=torch.int64, device=dev)
         f = self._critic_optim_factory
         self.critic_state = OptimState(store, self.critic.names(), self._critic_learning_rate,
-                                       f.betas, f.eps)
+                                       f.betas, f.eps, step=self.counters[0:1])
         f = self._actor_optim_factory
         self.actor_state = OptimState(store, self.policy.names(), self._actor_learning_rate,
-                                      f.betas, f.eps)
+                                      f.betas, f.eps, step=self.counters[1:2])
         self._built = True
 
     # ---------------------------------------------------------- checkpoints
@@ -582,18 +584,16 @@ class _Workspace:
                 ops.call_desc("d3a_cql_loss", l)
             # 6. actor: Q(s, tanh u) with the updated critic, dQ/da, policy backward
             mlp.forward(impl.critic, impl.store, self.x_actor.data_ptr(), True, DA, self.aacts)
-            NAT.check(NAT.lib().d3a_sac_actor_dq(self.aacts.out.data_ptr(), B, C, B,
-                                                 self.adq.data_ptr(), B, ops._stream()),
-                      "d3a_sac_actor_dq")
+            # dL/dq = -1/B on the argmin critic (backward of min over the ensemble)
             mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA, self.aacts,
-                         self.adq.data_ptr(), 1, B, 0, B, weight_grads=False, dx=self.adx)
+                         self.adq.data_ptr(), 1, B, 0, B, weight_grads=False, dx=self.adx,
+                         q_min=self.aacts.out.data_ptr(), sq_b=B, q_scale=-1.0 / B,
+                         g_out=self.adq.data_ptr())
             ops.call_desc("d3a_sac_actor_head", self.head_desc)
             mlp.backward(self.pbwd, impl.store, self.obs2.data_ptr(), True, D, self.pacts,
                          self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B)
             self.actor_opt.launch()
-        if targets:
-            ops.soft_update(impl.targ.data, impl.store.data, impl._tau)
-        NAT.check(NAT.lib().d3a_metrics_push(self.metrics.data_ptr(), len(METRIC_NAMES),
-                                             self.ring.data_ptr(), self.ring.shape[0],
-                                             self.ring_ctr.data_ptr(), ops._stream()),
-                  "d3a_metrics_push")
+        # 7. soft update of both targets + metric ring + optimiser step counters
+        ops.step_end(impl.counters, (1 if critic else 0) | (2 if actor else 0), self.metrics,
+                     self.ring, self.ring_ctr, impl.targ.data if targets else None,
+                     impl.store.data if targets else None, impl._tau)

@@ -115,8 +115,8 @@ __global__ __launch_bounds__(256) void outer_mask_kernel(const float* g, int64_t
 }
 
 // ---- Adam (torch.optim.adam._single_tensor_adam, weight_decay = 0) ---------
-__global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs, int64_t* step,
-                                                   unsigned int* ticket, double lr, double beta1,
+__global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
+                                                   const int64_t* step, double lr, double beta1,
                                                    double beta2, double eps) {
   __shared__ float s_step_size, s_bc2_sqrt;
   const d3a_adam_segment sg = segs[blockIdx.y];
@@ -152,16 +152,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
     sg.exp_avg_sq[i] = v;
     sg.param[i] = pnew;
   }
-  // the last block to finish commits the step counter
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned nblocks = gridDim.x * gridDim.y;
-    const unsigned prev = atomicAdd(ticket, 1u);
-    if (prev == nblocks - 1) {
-      *step = t;
-      *ticket = 0u;
-    }
-  }
+  // the step counter is committed by d3a_step_end after the update
 }
 
 // ---- soft update: fl(fl(p_t * (1 - tau)) + fl(tau * p)) -------------------
@@ -211,12 +202,27 @@ __global__ __launch_bounds__(256) void philox_kernel(float* out, int64_t n_norma
   }
 }
 
-__global__ void metrics_push_kernel(const float* m, int n, float* ring, int64_t cap,
-                                    int64_t* ctr) {
-  const int64_t slot = *ctr % cap;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) ring[slot * n + i] = m[i];
+// End of an update: soft target update over the whole flat parameter buffer
+// (fl(fl(p_t*(1-tau)) + fl(tau*p)), torch_utility.py:27-33) + metric ring push
+// + optimiser step counters, in one launch.
+__global__ __launch_bounds__(256) void step_end_kernel(const float* m, int n, float* ring,
+                                                       int64_t cap, int64_t* ctr,
+                                                       int64_t* counters, unsigned inc_mask,
+                                                       float* targ, const float* src, int64_t ns,
+                                                       float omt, float tau) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (targ && i < ns) targ[i] = __fadd_rn(__fmul_rn(targ[i], omt), __fmul_rn(tau, src[i]));
+  if (blockIdx.x != 0) return;
+  if (ring) {
+    const int64_t slot = *ctr % cap;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) ring[slot * n + k] = m[k];
+  }
   __syncthreads();
-  if (threadIdx.x == 0) *ctr = *ctr + 1;
+  if (threadIdx.x == 0) {
+    if (ring) *ctr = *ctr + 1;
+    for (int k = 0; k < 32; ++k)
+      if (inc_mask & (1u << k)) counters[k] += 1;
+  }
 }
 
 }  // namespace
@@ -224,12 +230,18 @@ __global__ void metrics_push_kernel(const float* m, int n, float* ring, int64_t 
 
 using namespace d3a;
 
-extern "C" int d3a_metrics_push(const float* metrics, int32_t n, float* ring, int64_t cap,
-                                int64_t* ctr, void* stream) {
-  D3A_CHECK_ARG(metrics && ring && ctr && n > 0 && cap > 0, "d3a_metrics_push: bad args");
-  hipLaunchKernelGGL(metrics_push_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, metrics, n,
-                     ring, cap, ctr);
-  D3A_LAUNCH_CHECK("d3a_metrics_push");
+extern "C" int d3a_step_end(const float* metrics, int32_t n, float* ring, int64_t cap,
+                            int64_t* ring_ctr, int64_t* counters, uint32_t inc_mask, float* targ,
+                            const float* src, int64_t n_soft, double tau, void* stream) {
+  D3A_CHECK_ARG(!ring || (metrics && ring_ctr && n > 0 && cap > 0), "d3a_step_end: bad ring");
+  D3A_CHECK_ARG(!inc_mask || counters, "d3a_step_end: counters required");
+  D3A_CHECK_ARG(!targ || (src && n_soft >= 0), "d3a_step_end: bad soft-update operands");
+  const int64_t ns = targ ? n_soft : 0;
+  const unsigned blocks = (unsigned)(ns > 0 ? (ns + 255) / 256 : 1);
+  hipLaunchKernelGGL(step_end_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, metrics,
+                     n, ring, cap, ring_ctr, counters, inc_mask, targ, src, ns,
+                     (float)(1.0 - tau), (float)tau);
+  D3A_LAUNCH_CHECK("d3a_step_end");
   return 0;
 }
 
@@ -289,14 +301,14 @@ extern "C" int d3a_outer_mask_f32(const float* g, int64_t sgb, const float* w, i
 }
 
 extern "C" int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg, int64_t max_numel,
-                            int64_t* step, unsigned int* ticket, double lr, double beta1,
-                            double beta2, double eps, void* stream) {
-  D3A_CHECK_ARG(segs && step && ticket, "d3a_adam_f32: null pointer");
+                            const int64_t* step, double lr, double beta1, double beta2,
+                            double eps, void* stream) {
+  D3A_CHECK_ARG(segs && step, "d3a_adam_f32: null pointer");
   D3A_CHECK_ARG(n_seg > 0 && n_seg < 65536, "d3a_adam_f32: bad segment count");
   D3A_CHECK_ARG(max_numel > 0, "d3a_adam_f32: bad max_numel");
   dim3 grid((unsigned)((max_numel + 255) / 256), (unsigned)n_seg);
-  hipLaunchKernelGGL(adam_kernel, grid, dim3(256), 0, (hipStream_t)stream, segs, step, ticket,
-                     lr, beta1, beta2, eps);
+  hipLaunchKernelGGL(adam_kernel, grid, dim3(256), 0, (hipStream_t)stream, segs, step, lr, beta1,
+                     beta2, eps);
   D3A_LAUNCH_CHECK("d3a_adam_f32");
   return 0;
 }

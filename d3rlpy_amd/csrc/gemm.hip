@@ -2,27 +2,25 @@
 //
 // Replaces the nn.Linear forward / backward GEMMs of the reference's MLP
 // trunks and heads (d3rlpy/models/torch/encoders.py:265-275,
-// policies.py:57-59,170-176, q_functions/mean_q_function.py:255-256).
+// policies.py:57-59,170-176, q_functions/mean_q_function.py:255-256) and
+// the bias gradients of those layers (fused row sums of the dY^T operand).
 //
-// Tile: 64x64 output per 256-thread workgroup, 4 waves in a 2x2 grid, each
-// wave one 32x32 accumulator of v_mfma_f32_32x32x2_f32 (issue interval ==
-// dependent latency == 64 cycles, so one accumulation chain runs at full
-// rate).  K is staged through LDS in 16-deep tiles, k-major ([k][m] and
-// [k][n]) so that the MFMA operand reads are 32 consecutive floats per half
-// wave (conflict-free ds_read_b32).  The global->LDS loader picks, per
-// operand, the coalesced direction (the unit-stride dimension) and issues
-// 16-byte loads when aligned.  The next K tile is prefetched into registers
-// while the current one is multiplied.  Result numerics: each output is an
-// fp32 fmaf chain over k (exact-f32 MFMA), no reduced precision.
+// Tiling: a workgroup of WAVES_M x WAVES_N waves computes a BM x BN tile,
+// each wave WM_T x WN_T accumulators of v_mfma_f32_32x32x2_f32 (issue
+// interval == dependent latency == 64 cycles, so each accumulation chain runs
+// at full rate).  K is staged through double-buffered LDS tiles BK deep,
+// k-major ([k][m], [k][n]) so that MFMA operand reads are 32 consecutive
+// floats per half wave (conflict-free ds_read_b32).  The global->LDS loader
+// reads along the operand's unit-stride dimension with 16-byte loads when
+// aligned; the next K tile is loaded into registers while the current one is
+// multiplied, one barrier per K tile.  Numerics: every output is an exact
+// fp32 fmaf chain over k (f32-input MFMA), no reduced precision.
+#include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
 
 namespace d3a {
 namespace {
-
-constexpr int BM = 64, BN = 64, BK = 16;
-constexpr int LDA = BM + 4, LDB = BN + 4;  // +4 floats: spread the transposing writes
-constexpr int kThreads = 256;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -31,17 +29,16 @@ enum { MODE_GENERIC = 0, MODE_KCONTIG = 1, MODE_XCONTIG = 2 };
 
 struct Params {
   const float* A; const float* B; float* C;
-  const float* bias; const float* mask;
+  const float* bias; const float* mask; float* rowsum;
   int64_t M, N, K, batch;
   int64_t sAb, sAm, sAk, sBb, sBk, sBn, sCb, sCm, sCn, sbias_b, sMb, sMm, sMn;
-  int64_t splits, sCs, kchunk;
+  int64_t splits, sCs, kchunk, sRb, sRs;
   float alpha;
   int relu, accumulate;
 };
 
-// Load a 4-vector of a tile. `x` is the non-k coordinate (m for A, n for B),
-// `k` the reduction coordinate.  MODE_KCONTIG: the 4 elements are k..k+3 at x;
-// MODE_XCONTIG: x..x+3 at k.  Out-of-range elements are zero.
+// Load a 4-vector of a tile at non-k coordinate x and reduction coordinate k.
+// KCONTIG: elements k..k+3 at x; otherwise x..x+3 at k.  Out of range -> 0.
 template <int MODE>
 __device__ __forceinline__ float4 load4(const float* base, int64_t sx, int64_t sk, int64_t x,
                                         int64_t k, int64_t X, int64_t kend) {
@@ -57,7 +54,7 @@ __device__ __forceinline__ float4 load4(const float* base, int64_t sx, int64_t s
       if (k + 2 < kend) r.z = p[2];
       if (k + 3 < kend) r.w = p[3];
     }
-  } else {  // XCONTIG or GENERIC (4 along x)
+  } else {
     if (k >= kend) return r;
     const float* p = base + k * sk + x * sx;
     if (MODE == MODE_XCONTIG && x + 3 < X && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
@@ -72,15 +69,15 @@ __device__ __forceinline__ float4 load4(const float* base, int64_t sx, int64_t s
   return r;
 }
 
-// Thread -> (x, k) coordinate of the 4-vector it loads inside a 64x16 tile.
-template <int MODE>
-__device__ __forceinline__ void tile_coord(int t, int& xl, int& kl) {
-  if (MODE == MODE_KCONTIG) { xl = t >> 2; kl = (t & 3) * 4; }
-  else { kl = t >> 4; xl = (t & 15) * 4; }
+// vector v of a (X extent) x (BK) tile -> (x, k) coordinates
+template <int MODE, int XT, int BK>
+__device__ __forceinline__ void vcoord(int v, int& xl, int& kl) {
+  if (MODE == MODE_KCONTIG) { xl = v / (BK / 4); kl = (v % (BK / 4)) * 4; }
+  else { kl = v / (XT / 4); xl = (v % (XT / 4)) * 4; }
 }
 
 template <int MODE, int LD>
-__device__ __forceinline__ void store_tile(float* lds, int xl, int kl, float4 v) {
+__device__ __forceinline__ void store4(float* lds, int xl, int kl, float4 v) {
   if (MODE == MODE_KCONTIG) {
     lds[(kl + 0) * LD + xl] = v.x;
     lds[(kl + 1) * LD + xl] = v.y;
@@ -91,10 +88,15 @@ __device__ __forceinline__ void store_tile(float* lds, int xl, int kl, float4 v)
   }
 }
 
-template <int AMODE, int BMODE>
-__global__ __launch_bounds__(kThreads) void gemm_f32_kernel(Params p) {
-  __shared__ __attribute__((aligned(16))) float As[BK * LDA];
-  __shared__ __attribute__((aligned(16))) float Bs[BK * LDB];
+template <int AMODE, int BMODE, int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32_kernel(Params p) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int BM = 32 * WM_T * WAVES_M, BN = 32 * WN_T * WAVES_N;
+  constexpr int LDA = BM + 4, LDB = BN + 4;
+  constexpr int AV = BM * BK / 4 / NT, BV = BN * BK / 4 / NT;  // float4 per thread
+  static_assert(AV >= 1 && BV >= 1, "tile too small for the thread count");
+  __shared__ __attribute__((aligned(16))) float As[2][BK * LDA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB];
 
   const int t = threadIdx.x;
   const int lane = t & 63, wid = t >> 6;
@@ -104,71 +106,158 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(Params p) {
   const int64_t b = bz / p.splits, s = bz % p.splits;
   const int64_t kbeg = s * p.kchunk;
   const int64_t kend = (kbeg + p.kchunk < p.K) ? kbeg + p.kchunk : p.K;
-
   const float* Ab = p.A + b * p.sAb;
   const float* Bb = p.B + b * p.sBb;
 
-  // per-thread tile coordinates
-  int axl, akl, bxl, bkl;
-  tile_coord<AMODE>(t, axl, akl);
-  tile_coord<BMODE>(t, bxl, bkl);
-  // for A: x = m, stride along x = sAm, along k = sAk
-  // for B: x = n, stride along x = sBn, along k = sBk
-  const int64_t a_sx = p.sAm, a_sk = p.sAk, b_sx = p.sBn, b_sk = p.sBk;
-
-  f32x16 acc;
+  int axl[AV], akl[AV], bxl[BV], bkl[BV];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int i = 0; i < AV; ++i) vcoord<AMODE, BM, BK>(t + i * NT, axl[i], akl[i]);
+#pragma unroll
+  for (int i = 0; i < BV; ++i) vcoord<BMODE, BN, BK>(t + i * NT, bxl[i], bkl[i]);
 
-  const int wm = (wid >> 1) * 32, wn = (wid & 1) * 32;
+  f32x16 acc[WM_T][WN_T];
+#pragma unroll
+  for (int i = 0; i < WM_T; ++i)
+#pragma unroll
+    for (int j = 0; j < WN_T; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int wm = (wid / WAVES_N) * (32 * WM_T), wn = (wid % WAVES_N) * (32 * WN_T);
   const int li = lane & 31, lk = lane >> 5;
+  const bool do_rowsum = p.rowsum != nullptr && blockIdx.x == 0;
+  double rs = 0.0;
 
-  float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
+  float4 ra[AV], rb[BV];
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < AV; ++i)
+      ra[i] = load4<AMODE>(Ab, p.sAm, p.sAk, m0 + axl[i], k0 + akl[i], p.M, kend);
+#pragma unroll
+    for (int i = 0; i < BV; ++i)
+      rb[i] = load4<BMODE>(Bb, p.sBn, p.sBk, n0 + bxl[i], k0 + bkl[i], p.N, kend);
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) store4<AMODE, LDA>(As[buf], axl[i], akl[i], ra[i]);
+#pragma unroll
+    for (int i = 0; i < BV; ++i) store4<BMODE, LDB>(Bs[buf], bxl[i], bkl[i], rb[i]);
+  };
+
+  int cur = 0;
   if (kbeg < kend) {
-    ra = load4<AMODE>(Ab, a_sx, a_sk, m0 + axl, kbeg + akl, p.M, kend);
-    rb = load4<BMODE>(Bb, b_sx, b_sk, n0 + bxl, kbeg + bkl, p.N, kend);
+    gload(kbeg);
+    lstore(0);
   }
+  __syncthreads();
   for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
-    store_tile<AMODE, LDA>(As, axl, akl, ra);
-    store_tile<BMODE, LDB>(Bs, bxl, bkl, rb);
-    __syncthreads();
-    if (k0 + BK < kend) {
-      ra = load4<AMODE>(Ab, a_sx, a_sk, m0 + axl, k0 + BK + akl, p.M, kend);
-      rb = load4<BMODE>(Bb, b_sx, b_sk, n0 + bxl, k0 + BK + bkl, p.N, kend);
-    }
+    const bool more = k0 + BK < kend;
+    if (more) gload(k0 + BK);
+    const float* Ac = As[cur];
+    const float* Bc = Bs[cur];
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
-      const float av = As[(kk + lk) * LDA + wm + li];
-      const float bv = Bs[(kk + lk) * LDB + wn + li];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+      float av[WM_T], bv[WN_T];
+#pragma unroll
+      for (int i = 0; i < WM_T; ++i) av[i] = Ac[(kk + lk) * LDA + wm + 32 * i + li];
+#pragma unroll
+      for (int j = 0; j < WN_T; ++j) bv[j] = Bc[(kk + lk) * LDB + wn + 32 * j + li];
+#pragma unroll
+      for (int i = 0; i < WM_T; ++i)
+#pragma unroll
+        for (int j = 0; j < WN_T; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
+    if (do_rowsum && t < BM) {
+#pragma unroll
+      for (int kk = 0; kk < BK; ++kk) rs += (double)Ac[kk * LDA + t];
+    }
+    if (more) lstore(cur ^ 1);
     __syncthreads();
+    cur ^= 1;
   }
+
+  if (do_rowsum && t < BM && m0 + t < p.M)
+    p.rowsum[b * p.sRb + s * p.sRs + m0 + t] = (float)rs;
 
   // epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
   float* Cb = p.C + b * p.sCb + s * p.sCs;
   const float* biasb = p.bias ? p.bias + b * p.sbias_b : nullptr;
   const float* maskb = p.mask ? p.mask + b * p.sMb : nullptr;
-  const int64_t n = n0 + wn + li;
-  if (n >= p.N) return;
-  const float bn = biasb ? biasb[n] : 0.f;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * lk;
-    if (m < p.M) {
-      float v = acc[r] * p.alpha;
-      if (biasb) v += bn;
-      if (p.relu) v = fmaxf(v, 0.f);
-      if (maskb && !(maskb[m * p.sMm + n * p.sMn] > 0.f)) v = 0.f;
-      float* dst = Cb + m * p.sCm + n * p.sCn;
-      if (p.accumulate) *dst += v; else *dst = v;
+  for (int j = 0; j < WN_T; ++j) {
+    const int64_t n = n0 + wn + 32 * j + li;
+    if (n >= p.N) continue;
+    const float bn = biasb ? biasb[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < WM_T; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (m < p.M) {
+          float v = acc[i][j][r] * p.alpha;
+          if (biasb) v += bn;
+          if (p.relu) v = fmaxf(v, 0.f);
+          if (maskb && !(maskb[m * p.sMm + n * p.sMn] > 0.f)) v = 0.f;
+          float* dst = Cb + m * p.sCm + n * p.sCn;
+          if (p.accumulate) *dst += v; else *dst = v;
+        }
+      }
     }
   }
 }
 
+struct Variant {
+  int wm_t, wn_t, waves_m, waves_n, bk;
+};
+// index = d3a_gemm_desc.variant
+constexpr Variant kVariants[] = {
+    {1, 1, 2, 2, 16},  // 0: 64x64   BK16
+    {2, 2, 2, 2, 16},  // 1: 128x128 BK16
+    {2, 1, 2, 2, 16},  // 2: 128x64  BK16
+    {1, 1, 2, 2, 32},  // 3: 64x64   BK32
+    {2, 2, 2, 2, 32},  // 4: 128x128 BK32
+    {1, 2, 2, 2, 16},  // 5: 64x128  BK16
+};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+template <int AM, int BMd, int V>
+void launch_v(const Params& p, hipStream_t st) {
+  constexpr Variant v = kVariants[V];
+  constexpr int BM = 32 * v.wm_t * v.waves_m, BN = 32 * v.wn_t * v.waves_n;
+  dim3 grid((unsigned)((p.N + BN - 1) / BN), (unsigned)((p.M + BM - 1) / BM),
+            (unsigned)(p.batch * p.splits));
+  hipLaunchKernelGGL((gemm_f32_kernel<AM, BMd, v.wm_t, v.wn_t, v.waves_m, v.waves_n, v.bk>), grid,
+                     dim3(64 * v.waves_m * v.waves_n), 0, st, p);
+}
+
 template <int AM, int BMd>
-void launch(const Params& p, dim3 grid, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_f32_kernel<AM, BMd>), grid, dim3(kThreads), 0, st, p);
+void launch_modes(const Params& p, int variant, hipStream_t st) {
+  switch (variant) {
+    case 1: launch_v<AM, BMd, 1>(p, st); break;
+    case 2: launch_v<AM, BMd, 2>(p, st); break;
+    case 3: launch_v<AM, BMd, 3>(p, st); break;
+    case 4: launch_v<AM, BMd, 4>(p, st); break;
+    case 5: launch_v<AM, BMd, 5>(p, st); break;
+    default: launch_v<AM, BMd, 0>(p, st); break;
+  }
+}
+
+// Tile choice: the largest tile that still gives >= ~2 workgroups per CU.
+int choose_variant(const Params& p) {
+  const int64_t big = ((p.M + 127) / 128) * ((p.N + 127) / 128) * p.batch * p.splits;
+  if (p.N >= 128 && p.M >= 128 && big >= 384) return 1;
+  const int64_t mid = ((p.M + 127) / 128) * ((p.N + 63) / 64) * p.batch * p.splits;
+  if (p.M >= 128 && mid >= 384) return 2;
+  return 0;
+}
+
+int env_variant() {
+  static int v = [] {
+    const char* e = getenv("D3A_GEMM_VARIANT");
+    return e ? atoi(e) : -1;
+  }();
+  return v;
 }
 
 }  // namespace
@@ -181,43 +270,50 @@ extern "C" int d3a_gemm_f32(const d3a_gemm_desc* d, void* stream) {
   D3A_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0 && d->batch >= 0,
                 "d3a_gemm_f32: negative size");
   D3A_CHECK_ARG(d->splits >= 1, "d3a_gemm_f32: splits must be >= 1");
+  D3A_CHECK_ARG(d->variant >= -1 && d->variant < kNumVariants, "d3a_gemm_f32: bad variant");
   if (d->M == 0 || d->N == 0 || d->batch == 0) return 0;
   Params p;
   p.A = d->A; p.B = d->B; p.C = d->C; p.bias = d->bias; p.mask = d->mask;
+  p.rowsum = d->rowsum;
   p.M = d->M; p.N = d->N; p.K = d->K; p.batch = d->batch;
   p.sAb = d->sAb; p.sAm = d->sAm; p.sAk = d->sAk;
   p.sBb = d->sBb; p.sBk = d->sBk; p.sBn = d->sBn;
   p.sCb = d->sCb; p.sCm = d->sCm; p.sCn = d->sCn;
   p.sbias_b = d->sbias_b; p.sMb = d->sMb; p.sMm = d->sMm; p.sMn = d->sMn;
-  p.splits = d->splits; p.sCs = d->sCs;
-  // split K in BK multiples
-  int64_t kc = (d->K + d->splits - 1) / d->splits;
-  kc = ((kc + BK - 1) / BK) * BK;
-  p.kchunk = kc > 0 ? kc : BK;
+  p.splits = d->splits; p.sCs = d->sCs; p.sRb = d->sRb; p.sRs = d->sRs;
   p.alpha = d->alpha; p.relu = d->relu; p.accumulate = d->accumulate;
+  int variant = d->variant >= 0 ? d->variant : env_variant();
+  if (variant < 0) variant = choose_variant(p);
+  const int bk = kVariants[variant].bk;
+  // split K in BK multiples (every split starts on a K-tile boundary)
+  int64_t kc = (d->K + d->splits - 1) / d->splits;
+  kc = ((kc + bk - 1) / bk) * bk;
+  p.kchunk = kc > 0 ? kc : bk;
   D3A_CHECK_ARG(d->batch * d->splits < 65536, "d3a_gemm_f32: batch*splits too large");
-  D3A_CHECK_ARG((d->M + BM - 1) / BM < 65536, "d3a_gemm_f32: M too large");
+  D3A_CHECK_ARG((d->M + 31) / 32 < 65536, "d3a_gemm_f32: M too large");
 
   const int am = (d->sAk == 1) ? MODE_KCONTIG : (d->sAm == 1 ? MODE_XCONTIG : MODE_GENERIC);
   const int bm = (d->sBk == 1) ? MODE_KCONTIG : (d->sBn == 1 ? MODE_XCONTIG : MODE_GENERIC);
-  dim3 grid((unsigned)((d->N + BN - 1) / BN), (unsigned)((d->M + BM - 1) / BM),
-            (unsigned)(d->batch * d->splits));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  // GENERIC uses the XCONTIG thread mapping with strided scalar loads
-  const int a = am == MODE_KCONTIG ? 1 : 2, b = bm == MODE_KCONTIG ? 1 : 2;
   if (am == MODE_GENERIC || bm == MODE_GENERIC) {
-    if (am == MODE_GENERIC && bm == MODE_GENERIC) launch<MODE_GENERIC, MODE_GENERIC>(p, grid, st);
+    // strided fallback: smallest tile, scalar loads
+    if (am == MODE_GENERIC && bm == MODE_GENERIC) launch_v<MODE_GENERIC, MODE_GENERIC, 0>(p, st);
     else if (am == MODE_GENERIC) {
-      if (b == 1) launch<MODE_GENERIC, MODE_KCONTIG>(p, grid, st);
-      else launch<MODE_GENERIC, MODE_XCONTIG>(p, grid, st);
+      if (bm == MODE_KCONTIG) launch_v<MODE_GENERIC, MODE_KCONTIG, 0>(p, st);
+      else launch_v<MODE_GENERIC, MODE_XCONTIG, 0>(p, st);
     } else {
-      if (a == 1) launch<MODE_KCONTIG, MODE_GENERIC>(p, grid, st);
-      else launch<MODE_XCONTIG, MODE_GENERIC>(p, grid, st);
+      if (am == MODE_KCONTIG) launch_v<MODE_KCONTIG, MODE_GENERIC, 0>(p, st);
+      else launch_v<MODE_XCONTIG, MODE_GENERIC, 0>(p, st);
     }
-  } else if (a == 1 && b == 1) launch<MODE_KCONTIG, MODE_KCONTIG>(p, grid, st);
-  else if (a == 1 && b == 2) launch<MODE_KCONTIG, MODE_XCONTIG>(p, grid, st);
-  else if (a == 2 && b == 1) launch<MODE_XCONTIG, MODE_KCONTIG>(p, grid, st);
-  else launch<MODE_XCONTIG, MODE_XCONTIG>(p, grid, st);
+  } else if (am == MODE_KCONTIG && bm == MODE_KCONTIG) {
+    launch_modes<MODE_KCONTIG, MODE_KCONTIG>(p, variant, st);
+  } else if (am == MODE_KCONTIG) {
+    launch_modes<MODE_KCONTIG, MODE_XCONTIG>(p, variant, st);
+  } else if (bm == MODE_KCONTIG) {
+    launch_modes<MODE_XCONTIG, MODE_KCONTIG>(p, variant, st);
+  } else {
+    launch_modes<MODE_XCONTIG, MODE_XCONTIG>(p, variant, st);
+  }
   D3A_LAUNCH_CHECK("d3a_gemm_f32");
   return 0;
 }

@@ -1,0 +1,91 @@
+// Backward of the single-output Q head q = relu(h) . w + b, fused.
+//
+// Reference: ContinuousMeanQFunction._fc (q_functions/mean_q_function.py:255-256)
+// and its autograd backward.  For every row r of an ensemble member c:
+//   dz[c][r][j] = g[c][r] * w[c][j] * [h[c][r][j] > 0]        (dL/d pre-relu)
+//   dW[s][c][j] = sum_{r in split s} g[c][r] * h[c][r][j]      (head weight grad)
+//   db[s][c]    = sum_{r in split s} g[c][r]                   (head bias grad)
+// In "argmin" mode the row gradient is not read but derived from the
+// ensemble's Q values: g[c][r] = scale if c is the first argmin over members
+// of q[.][r], else 0 — the backward of ``min`` over critics in
+// SACImpl.compute_actor_loss (sac_impl.py:114-121; torch's min routes the
+// gradient to one index).
+//
+// One launch replaces the column reductions and the masked outer product of
+// the head backward; h is read once.  Grid: (column tiles of 64, row splits,
+// members); 4 waves stride the split's rows, lanes cover columns (coalesced).
+#include "common.hpp"
+#include "../../include/d3rlpy_amd.h"
+
+namespace d3a {
+namespace {
+
+__global__ __launch_bounds__(256) void head1_bwd_kernel(d3a_head1_bwd_desc d) {
+  __shared__ double sw[4][64];
+  __shared__ double sb[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t j = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t s = blockIdx.y, c = blockIdx.z;
+  const int64_t chunk = (d.rows + d.splits - 1) / d.splits;
+  const int64_t r0 = s * chunk;
+  const int64_t r1 = (r0 + chunk < d.rows) ? r0 + chunk : d.rows;
+  const bool colok = j < d.n;
+  const float wj = colok ? d.w[c * d.swb + j] : 0.f;
+  const float* h = d.h + c * d.shb;
+  float* dz = d.dz + c * d.sdzb;
+  double accw = 0.0, accb = 0.0;
+  for (int64_t r = r0 + w; r < r1; r += 4) {
+    float g;
+    if (d.q_min) {
+      // first argmin over members of q[.][r]
+      int arg = 0;
+      float mn = d.q_min[r];
+      for (int k = 1; k < d.C; ++k) {
+        const float v = d.q_min[k * d.sqb + r];
+        if (v < mn) { mn = v; arg = k; }
+      }
+      g = (arg == c) ? d.scale : 0.f;
+      if (d.g_out && lane == 0 && blockIdx.x == 0) d.g_out[c * d.sgb + r] = g;
+    } else {
+      g = d.g[c * d.sgb + r];
+    }
+    if (colok) {
+      const float hv = h[r * d.ldh + j];
+      dz[r * d.lddz + j] = hv > 0.f ? g * wj : 0.f;
+      accw += (double)(g * hv);
+    }
+    accb += (double)g;
+  }
+  if (d.dW) {
+    sw[w][lane] = accw;
+    if (lane == 0) sb[w] = accb;
+    __syncthreads();
+    if (w == 0) {
+      if (colok) {
+        const double t = sw[0][lane] + sw[1][lane] + sw[2][lane] + sw[3][lane];
+        d.dW[s * d.sWs + c * d.n + j] = (float)t;
+      }
+      if (lane == 0 && blockIdx.x == 0 && d.db)
+        d.db[s * d.sbs + c] = (float)(sb[0] + sb[1] + sb[2] + sb[3]);
+    }
+  }
+}
+
+}  // namespace
+}  // namespace d3a
+
+using namespace d3a;
+
+extern "C" int d3a_head1_bwd(const d3a_head1_bwd_desc* d, void* stream) {
+  D3A_CHECK_ARG(d && d->h && d->w && d->dz, "d3a_head1_bwd: null operand");
+  D3A_CHECK_ARG((d->g != nullptr) != (d->q_min != nullptr),
+                "d3a_head1_bwd: exactly one of g / q_min");
+  D3A_CHECK_ARG(d->C >= 1 && d->rows >= 0 && d->n >= 1 && d->splits >= 1,
+                "d3a_head1_bwd: bad sizes");
+  D3A_CHECK_ARG(!d->dW || d->db, "d3a_head1_bwd: dW requires db");
+  if (d->rows == 0) return 0;
+  dim3 grid((unsigned)((d->n + 63) / 64), (unsigned)d->splits, (unsigned)d->C);
+  hipLaunchKernelGGL(head1_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, *d);
+  D3A_LAUNCH_CHECK("d3a_head1_bwd");
+  return 0;
+}

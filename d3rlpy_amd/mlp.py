@@ -22,6 +22,7 @@ from typing import List, Optional
 
 import torch
 
+from . import _native as N
 from . import ops
 from .nets import EnsembleMLP, GradSpace, ParamStore
 
@@ -102,11 +103,14 @@ class BackwardSpace:
 def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: int,
              acts: Acts, dout: int, ld_dout: int, sdout_b: int, r0: int, n: int,
              weight_grads: bool = True, dx: Optional[torch.Tensor] = None,
-             sxb: Optional[int] = None) -> None:
+             sxb: Optional[int] = None, q_min: Optional[int] = None, sq_b: int = 0,
+             q_scale: float = 0.0, g_out: Optional[int] = None) -> None:
     """Backward of rows [r0, r0+n) given dL/d(output) (``dout`` points at row r0).
 
     dout layout: [C] x rows, member stride sdout_b, row stride ld_dout (1 for a
     single-output head).  ``dx`` (if given) receives dL/dx as [C][n][in].
+    With ``q_min`` (single-output heads only) the row gradient is ``q_scale`` on
+    the argmin member of q_min[.][r] (backward of a min over the ensemble).
     """
     net = bs.net
     C, L, sizes, R = net.C, net.n_layers, net.sizes, acts.R
@@ -126,17 +130,11 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
     Hin = sizes[L - 1]
     out_dim = sizes[L]
     cur = bs.dz[0]
-    if weight_grads:
-        gW, gb = gs.get(net.wname(L - 1)), gs.get(net.bname(L - 1))
-        if out_dim == 1:
-            ops.colreduce(hin, sh, ld_h, dout, sdout_b, gW.data_ptr(), Hin, C * Hin, C, n, Hin, S)
-            ops.colreduce(dout, sdout_b, 1, None, 0, gb.data_ptr(), 1, C, C, n, 1, S)
-        else:
-            ops.linear_bwd_w(dout, ld_dout, sdout_b, hin, ld_h, sh, gW.data_ptr(), C, n, Hin,
-                             out_dim, S)
-            ops.colreduce(dout, sdout_b, ld_dout, None, 0, gb.data_ptr(), out_dim, C * out_dim, C,
-                          n, out_dim, S)
     if L == 1:
+        if weight_grads:
+            gW, gb = gs.get(net.wname(0)), gs.get(net.bname(0))
+            ops.linear_bwd_w(dout, ld_dout, sdout_b, hin, ld_h, sh, gW.data_ptr(), C, n, Hin,
+                             out_dim, S, db=gb.data_ptr())
         if dx is not None:
             ops.linear_bwd_x(dout, ld_dout, sdout_b, net.W(0, store), dx.data_ptr(), sizes[0],
                              n * sizes[0], C, n, sizes[0], out_dim)
@@ -144,11 +142,28 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
     ld_cur = bs.dz[0].shape[2]
     scur = bs.rows * ld_cur
     if out_dim == 1:
-        # h is contiguous [rows][H] per member (ld_h == Hin == ld_cur)
-        assert ld_h == Hin == ld_cur
-        ops.outer_mask(dout, sdout_b, net.W(L - 1, store), Hin, hin, sh, cur.data_ptr(), scur, C, n,
-                       Hin)
+        # fused: masked input gradient + head weight/bias gradients, h read once
+        d = N.Head1BwdDesc()
+        if q_min is not None:
+            d.q_min, d.sqb, d.scale = q_min, sq_b, q_scale
+            d.g_out, d.sgb = g_out, sdout_b
+        else:
+            d.g, d.sgb = dout, sdout_b
+        d.h, d.shb, d.ldh = hin, sh, ld_h
+        d.w, d.swb = net.W(L - 1, store), Hin
+        d.dz, d.sdzb, d.lddz = cur.data_ptr(), scur, ld_cur
+        if weight_grads:
+            gW, gb = gs.get(net.wname(L - 1)), gs.get(net.bname(L - 1))
+            d.dW, d.sWs = gW.data_ptr(), C * Hin
+            d.db, d.sbs = gb.data_ptr(), C
+        d.rows, d.n, d.splits, d.C = n, Hin, S if weight_grads else 1, C
+        ops.call_desc("d3a_head1_bwd", d)
     else:
+        assert q_min is None
+        if weight_grads:
+            gW, gb = gs.get(net.wname(L - 1)), gs.get(net.bname(L - 1))
+            ops.linear_bwd_w(dout, ld_dout, sdout_b, hin, ld_h, sh, gW.data_ptr(), C, n, Hin,
+                             out_dim, S, db=gb.data_ptr())
         ops.linear_bwd_x(dout, ld_dout, sdout_b, net.W(L - 1, store), cur.data_ptr(), ld_cur, scur, C,
                          n, Hin, out_dim, mask=hin, ldm=ld_h, smb=sh)
     # ---- trunk layers L-2 .. 0
@@ -160,9 +175,7 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         if weight_grads:
             gW, gb = gs.get(net.wname(l)), gs.get(net.bname(l))
             ops.linear_bwd_w(dz.data_ptr(), ld_cur, scur, hin, ld_h, sh, gW.data_ptr(), C, n, Hin,
-                             Hout, S)
-            ops.colreduce(dz.data_ptr(), scur, ld_cur, None, 0, gb.data_ptr(), Hout, C * Hout, C, n,
-                          Hout, S)
+                             Hout, S, db=gb.data_ptr())
         if l > 0:
             nxt = bs.dz[1] if cur is bs.dz[0] else bs.dz[0]
             ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(l, store), nxt.data_ptr(), ld_cur,

@@ -154,7 +154,7 @@ class OptimState:
     store-shaped buffers plus the (device) step count of the optimiser."""
 
     def __init__(self, store: ParamStore, names: Sequence[str], lr: float,
-                 betas=(0.9, 0.999), eps: float = 1e-8):
+                 betas=(0.9, 0.999), eps: float = 1e-8, step: Optional[torch.Tensor] = None):
         assert store.data is not None
         self.store = store
         self.names = list(names)
@@ -162,8 +162,9 @@ class OptimState:
         dev = store.data.device
         self.exp_avg = store.like()
         self.exp_avg_sq = store.like()
-        self.step = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        # completed steps (device int64, committed by d3a_step_end); may be a
+        # view into an Impl-wide counter array
+        self.step = torch.zeros(1, dtype=torch.int64, device=dev) if step is None else step
 
 
 class AdamGroup:
@@ -184,7 +185,6 @@ class AdamGroup:
         self.exp_avg = state.exp_avg
         self.exp_avg_sq = state.exp_avg_sq
         self.step = state.step
-        self.ticket = state.ticket
         self.grad_store = store.like() if keep_grads else None
         segs = (N.AdamSegment * len(self.names))()
         self.max_numel = 1
@@ -207,7 +207,7 @@ class AdamGroup:
 
     def launch(self) -> None:
         from . import ops
-        ops.adam(self.seg_table, len(self.names), self.max_numel, self.step, self.ticket,
+        ops.adam(self.seg_table, len(self.names), self.max_numel, self.step,
                  self.lr, self.beta1, self.beta2, self.eps)
 
     def grad(self, name: str) -> torch.Tensor:

@@ -39,10 +39,14 @@ def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
          bias: Optional[int] = None, sbias: int = 0,
          mask: Optional[int] = None, sM: Sequence[int] = (0, 0, 0),
          relu: bool = False, accumulate: bool = False, splits: int = 1, sCs: int = 0,
-         alpha: float = 1.0) -> None:
+         alpha: float = 1.0, rowsum: Optional[int] = None, sR: Sequence[int] = (0, 0),
+         variant: int = -1) -> None:
     """C_b,s(m,n) = epi(alpha * sum_k A_b(m,k) B_b(k,n)); strides (batch, row, col)."""
     d = N.GemmDesc()
     d.A, d.B, d.C, d.bias, d.mask = A, B, Cp, bias, mask
+    d.rowsum = rowsum
+    d.sRb, d.sRs = sR
+    d.variant = variant
     d.M, d.N, d.K, d.batch = M, Nn, K, batch
     d.sAb, d.sAm, d.sAk = sA
     d.sBb, d.sBk, d.sBn = sB
@@ -72,10 +76,25 @@ def outer_mask(g: int, sgb: int, w: int, swb: int, h: int, shb: int, out: int, s
                                        _stream()), "d3a_outer_mask_f32")
 
 
-def adam(segs: torch.Tensor, n_seg: int, max_numel: int, step: torch.Tensor,
-         ticket: torch.Tensor, lr: float, beta1: float, beta2: float, eps: float) -> None:
-    N.check(N.lib().d3a_adam_f32(ptr(segs), n_seg, max_numel, ptr(step), ptr(ticket), lr, beta1,
-                                 beta2, eps, _stream()), "d3a_adam_f32")
+def adam(segs: torch.Tensor, n_seg: int, max_numel: int, step: torch.Tensor, lr: float,
+         beta1: float, beta2: float, eps: float) -> None:
+    N.check(N.lib().d3a_adam_f32(ptr(segs), n_seg, max_numel, ptr(step), lr, beta1, beta2, eps,
+                                 _stream()), "d3a_adam_f32")
+
+
+def step_end(counters: Optional[torch.Tensor], inc_mask: int, metrics: Optional[torch.Tensor] = None,
+             ring: Optional[torch.Tensor] = None, ring_ctr: Optional[torch.Tensor] = None,
+             targ: Optional[torch.Tensor] = None, src: Optional[torch.Tensor] = None,
+             tau: float = 0.0) -> None:
+    """Soft target update (optional) + metric ring push + step counters, one launch."""
+    n = metrics.numel() if metrics is not None else 0
+    cap = ring.shape[0] if ring is not None else 0
+    ns = targ.numel() if targ is not None else 0
+    if targ is not None:
+        assert src is not None and src.numel() == ns
+    N.check(N.lib().d3a_step_end(ptr(metrics), n, ptr(ring), cap, ptr(ring_ctr), ptr(counters),
+                                 inc_mask, ptr(targ), ptr(src), ns, float(tau), _stream()),
+            "d3a_step_end")
 
 
 def soft_update(targ: torch.Tensor, src: torch.Tensor, tau: float) -> None:
@@ -122,7 +141,10 @@ def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: 
 
 
 def linear_bwd_w(dy: int, ldy: int, sdyb: int, x: int, ldx: int, sxb: int, dW: int, C_: int,
-                 R: int, n_in: int, n_out: int, splits: int) -> None:
-    """dW[s][c] = sum_{r in split s} dy[c][r]^T x[c][r]  -> partials [splits][C][out][in]."""
+                 R: int, n_in: int, n_out: int, splits: int, db: Optional[int] = None,
+                 variant: int = -1) -> None:
+    """dW[s][c] = sum_{r in split s} dy[c][r]^T x[c][r]  -> partials [splits][C][out][in];
+    if ``db`` is given, also the bias-gradient partials db[s][c][out] = sum_r dy[c][r]."""
     gemm(dy, x, dW, n_out, n_in, R, batch=C_, sA=(sdyb, 1, ldy), sB=(sxb, ldx, 1),
-         sC=(n_out * n_in, n_in, 1), splits=splits, sCs=C_ * n_out * n_in)
+         sC=(n_out * n_in, n_in, 1), splits=splits, sCs=C_ * n_out * n_in,
+         rowsum=db, sR=(n_out, C_ * n_out), variant=variant)

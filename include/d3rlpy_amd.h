@@ -55,6 +55,8 @@ typedef struct d3a_gemm_desc {
   float* C;
   const float* bias;  /* may be NULL */
   const float* mask;  /* may be NULL */
+  float* rowsum;      /* may be NULL: rowsum[b*sRb + s*sRs + m] = sum_{k in s} A_b(m,k)
+                         (the bias gradient when A = dY^T), fp64-accumulated */
   int64_t M, N, K, batch;
   int64_t sAb, sAm, sAk;
   int64_t sBb, sBk, sBn;
@@ -62,9 +64,11 @@ typedef struct d3a_gemm_desc {
   int64_t sbias_b;
   int64_t sMb, sMm, sMn;
   int64_t splits, sCs;
+  int64_t sRb, sRs;
   float alpha;
   int32_t relu;
   int32_t accumulate;
+  int32_t variant;    /* tile configuration, -1 = automatic */
 } d3a_gemm_desc;
 int d3a_gemm_f32(const d3a_gemm_desc* desc, void* stream);
 
@@ -90,6 +94,29 @@ int d3a_outer_mask_f32(const float* g, int64_t sgb, const float* w,
                        int64_t sob, int64_t batch, int64_t rows, int64_t n,
                        void* stream);
 
+/* Fused backward of the 1-output Q head q = relu(h).w + b
+ * (ContinuousMeanQFunction._fc, mean_q_function.py:255-256), per member c:
+ *   dz[c][r][j] = g[c][r] * w[c][j] * [h[c][r][j] > 0]
+ *   dW[s][c][j] = sum_{r in split s} g[c][r] h[c][r][j],  db[s][c] = sum g
+ * With q_min != NULL the row gradient is `scale` on the first argmin member of
+ * q_min[.][r] and 0 elsewhere (backward of min over critics in
+ * SACImpl.compute_actor_loss, sac_impl.py:114-121), optionally stored to g_out.
+ * dW/db may be NULL (input gradient only). */
+typedef struct d3a_head1_bwd_desc {
+  const float* g;      int64_t sgb;            /* [C] x rows (or NULL)      */
+  const float* q_min;  int64_t sqb;            /* [C] x rows (or NULL)      */
+  float scale;
+  float* g_out;                                /* optional, stride sgb      */
+  const float* h;      int64_t shb, ldh;       /* [C][rows][ldh]            */
+  const float* w;      int64_t swb;            /* [C][n]                    */
+  float* dz;           int64_t sdzb, lddz;     /* [C][rows][lddz]           */
+  float* dW;           int64_t sWs;            /* [splits][C][n] or NULL    */
+  float* db;           int64_t sbs;            /* [splits][C]                */
+  int64_t rows, n, splits;
+  int32_t C;
+} d3a_head1_bwd_desc;
+int d3a_head1_bwd(const d3a_head1_bwd_desc* desc, void* stream);
+
 /* ---- optimiser and target networks ------------------------------------- */
 
 /* One parameter tensor inside a flat buffer, with its gradient given as
@@ -110,10 +137,10 @@ typedef struct d3a_adam_segment {
  * amsgrad=False) as created by AdamFactory (d3rlpy/models/optimizers.py:106-138):
  *   m = lerp(m, g, 1-b1); v = v*b2 + (1-b2)*g*g; t = *step + 1
  *   p += -(lr/(1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
- * `segs` is a DEVICE array of n_seg segments; *step (device int64) is
- * incremented once per call after every block has read it. */
+ * `segs` is a DEVICE array of n_seg segments.  *step (device int64, the
+ * optimiser's completed steps) is only read; commit it with d3a_step_end. */
 int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg,
-                 int64_t max_numel, int64_t* step, unsigned int* ticket,
+                 int64_t max_numel, const int64_t* step,
                  double lr, double beta1, double beta2, double eps,
                  void* stream);
 
@@ -122,11 +149,17 @@ int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg,
 int d3a_soft_update_f32(float* targ, const float* src, int64_t n, double tau,
                         void* stream);
 
-/* Append metrics[0:n] to ring[(*ctr % cap)][0:n] and increment *ctr
- * (per-step loss history kept on device; read back once per epoch instead of
- * one device->host sync per update, cf. d3rlpy/base.py:645-657). */
-int d3a_metrics_push(const float* metrics, int32_t n, float* ring, int64_t cap,
-                     int64_t* ctr, void* stream);
+/* End of one update, one launch: (1) when targ != NULL the soft target
+ * update targ = targ*(1-tau) + tau*src over n_soft elements (soft_sync,
+ * d3rlpy/torch_utility.py:27-33, bit-exact as d3a_soft_update_f32);
+ * (2) when ring != NULL append metrics[0:n] to ring[(*ring_ctr % cap)] and
+ * increment *ring_ctr (per-step loss history kept on device and read once per
+ * epoch instead of one device->host sync per update, cf. base.py:645-657);
+ * (3) increment counters[i] for every bit i of inc_mask (optimiser steps). */
+int d3a_step_end(const float* metrics, int32_t n, float* ring, int64_t cap,
+                 int64_t* ring_ctr, int64_t* counters, uint32_t inc_mask,
+                 float* targ, const float* src, int64_t n_soft, double tau,
+                 void* stream);
 
 /* ---- random numbers ----------------------------------------------------- */
 

@@ -125,6 +125,7 @@ def test_adam_matches_torch(dev):
     gs = GradSpace(dev)
     gw = gs.add("w", (300, 7), 3)
     gb = gs.add("b", (5,), 1)
+    from d3rlpy_amd import ops
     from d3rlpy_amd.nets import OptimState
     opt = AdamGroup(OptimState(store, ["w", "b"], lr=3e-4), gs)
     pw = torch.nn.Parameter(w0.clone())
@@ -136,6 +137,7 @@ def test_adam_matches_torch(dev):
         gw.copy_(parts)
         gb.copy_(gbv.view(1, 5))
         opt.launch()
+        ops.step_end(opt.step, 1)
         # the kernel sums split-K partials in fp64 (then rounds once)
         pw.grad = parts.double().sum(0).float()
         pb.grad = gbv.clone()
