@@ -44,6 +44,7 @@ class GemmDesc(C.Structure):
 class Head1BwdDesc(C.Structure):
     _fields_ = [
         ("g", vp), ("sgb", C.c_int64),
+        ("gscale", vp), ("n_scaled", C.c_int64),
         ("q_min", vp), ("sqb", C.c_int64),
         ("scale", C.c_float),
         ("g_out", vp),
@@ -72,6 +73,7 @@ class CqlSampleDesc(C.Structure):
         ("x_q", vp), ("x_targ", vp), ("x_actor", vp),
         ("logp_temp", vp), ("logp_is", vp), ("actor_u", vp), ("actor_logp", vp),
         ("B", C.c_int32), ("D", C.c_int32), ("A", C.c_int32), ("N", C.c_int32),
+        ("ldx", C.c_int32),
         ("min_logstd", C.c_float), ("max_logstd", C.c_float),
     ]
 

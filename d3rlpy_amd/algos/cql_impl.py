@@ -361,6 +361,9 @@ class _Workspace:
         self.NB = NB
         self.R = 6 * NB + B
         DA = D + A
+        # Q-input rows padded to a multiple of 4 floats: 16-byte aligned rows let
+        # the first-layer GEMMs use vector loads (the pad columns stay zero)
+        self.LDX = LDX = (DA + 3) // 4 * 4
         z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
         # staged batch: obs2 = [obs; next_obs]
         self.obs2 = z(2 * B, D)
@@ -383,9 +386,9 @@ class _Workspace:
         # policy forward on 2B rows
         self.pacts = mlp.Acts.alloc(impl.policy, 2 * B, dev)
         # sample outputs
-        self.x_q = z(self.R, DA)
-        self.x_targ = z(B, DA)
-        self.x_actor = z(B, DA)
+        self.x_q = z(self.R, LDX)
+        self.x_targ = z(B, LDX)
+        self.x_actor = z(B, LDX)
         self.logp_temp = z(B)
         self.logp_is = z(4 * NB)
         self.actor_u = z(B, A)
@@ -437,6 +440,7 @@ class _Workspace:
         s.logp_temp, s.logp_is = self.logp_temp.data_ptr(), self.logp_is.data_ptr()
         s.actor_u, s.actor_logp = self.actor_u.data_ptr(), self.actor_logp.data_ptr()
         s.B, s.D, s.A, s.N = self.B, self.D, self.A, self.N
+        s.ldx = self.LDX
         s.min_logstd, s.max_logstd = impl._min_logstd, impl._max_logstd
         self.sample_desc = s
 
@@ -551,7 +555,7 @@ class _Workspace:
     def _enqueue(self, temp: bool, alpha: bool, critic: bool, actor: bool, targets: bool) -> None:
         impl = self.impl
         B, D, A, C, N, NB, R = self.B, self.D, self.A, self.C, self.N, self.NB, self.R
-        DA = D + A
+        DA = self.LDX  # row stride of the (padded) Q-input matrices
         if not self._external_noise:
             ops.philox_fill(self.noise, self.n_normal, self.n_uniform, -1.0, 1.0, self.seed,
                             self.rng_ctr, self.rng_ticket)
@@ -573,8 +577,11 @@ class _Workspace:
         if critic:
             # 5. critic backward on rows [3NB, R) and Adam
             r0 = 3 * NB
+            # dq of the 3NB importance-sampled rows is scaled by scalars[2]
+            # (alpha-dependent factor from the loss kernel) as it is read
             mlp.backward(self.cbwd, impl.store, self.x_q.data_ptr(), True, DA, self.qacts,
-                         self.dq.data_ptr() + 4 * r0, 1, R, r0, self.Rc)
+                         self.dq.data_ptr() + 4 * r0, 1, R, r0, self.Rc,
+                         g_scale=self.scalars.data_ptr() + 8, n_scaled=3 * NB)
             self.critic_opt.launch()
         if actor:
             if not (temp or alpha or critic):

@@ -44,7 +44,7 @@ __device__ __forceinline__ float squashed_sample(const float* mu, const float* l
 __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) {
   const int64_t B = d.B, N = d.N, A = d.A, D = d.D;
   const int64_t NB = N * B;
-  const int64_t DA = D + A;
+  const int64_t DA = d.ldx;  // row stride of the Q-input matrices (>= D + A, padded)
   const int64_t R = 6 * NB + B;           // x_q rows
   const int64_t total = R + 3 * B;         // + temp, target, actor rows
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -238,12 +238,9 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
     s_l += d.lse[(C + c) * B + b];
     d.dq[c * d.R + 6 * NB + b] = 2.f * diff / (float)B - gcons;
   }
-  // critic-set IS rows: softmax weight * gcons; alpha-set rows: no critic gradient
-  for (int64_t p = tid; p < C * 6 * NB; p += nt) {
-    const int64_t c = p / (6 * NB), r = p % (6 * NB);
-    float* q = d.dq + c * d.R + r;
-    *q = (r < 3 * NB) ? 0.f : gcons * (*q);
-  }
+  // critic-set IS rows keep the unscaled softmax weights of stage A; the
+  // backward (d3a_head1_bwd) multiplies them by scalars[2] = gcons on read.
+  if (tid == 0) d.scalars[2] = gcons;
   const float td = block_sum(s_td, scratch) / (float)B;
   const float lsum = block_sum(s_l, scratch);
   const float dsum = block_sum(s_d, scratch);
@@ -315,6 +312,7 @@ extern "C" int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream) {
   D3A_CHECK_ARG(d, "d3a_cql_sample: null desc");
   D3A_CHECK_ARG(d->A >= 1 && d->A <= 16, "d3a_cql_sample: action size must be in [1,16]");
   D3A_CHECK_ARG(d->B >= 1 && d->N >= 1 && d->D >= 1, "d3a_cql_sample: bad sizes");
+  D3A_CHECK_ARG(d->ldx >= d->D + d->A, "d3a_cql_sample: ldx < D + A");
   const int64_t total = 6LL * d->N * d->B + 4LL * d->B;
   hipLaunchKernelGGL(cql_sample_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, *d);

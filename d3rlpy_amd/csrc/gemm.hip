@@ -218,6 +218,9 @@ constexpr Variant kVariants[] = {
     {1, 1, 2, 2, 32},  // 3: 64x64   BK32
     {2, 2, 2, 2, 32},  // 4: 128x128 BK32
     {1, 2, 2, 2, 16},  // 5: 64x128  BK16
+    {1, 1, 1, 1, 16},  // 6: 32x32   BK16, one wave
+    {1, 1, 1, 1, 64},  // 7: 32x32   BK64, one wave (small, latency-bound problems)
+    {1, 1, 2, 2, 64},  // 8: 64x64   BK64
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -239,17 +242,26 @@ void launch_modes(const Params& p, int variant, hipStream_t st) {
     case 3: launch_v<AM, BMd, 3>(p, st); break;
     case 4: launch_v<AM, BMd, 4>(p, st); break;
     case 5: launch_v<AM, BMd, 5>(p, st); break;
+    case 6: launch_v<AM, BMd, 6>(p, st); break;
+    case 7: launch_v<AM, BMd, 7>(p, st); break;
+    case 8: launch_v<AM, BMd, 8>(p, st); break;
     default: launch_v<AM, BMd, 0>(p, st); break;
   }
 }
 
-// Tile choice: the largest tile that still gives >= ~2 workgroups per CU.
+// Tile choice.  Measured on MI355X (tools/bench_gemm.py, profiles/r01_gemm_sweep.log):
+// at this engine's shapes (K <= 256 per pass, or split-K slices of ~256 rows)
+// the 64x64 tile is within 3 % of the best variant everywhere and 10-50 %
+// faster than 128-wide tiles on the backward shapes, so it is the default.
+// Problems that give fewer than ~one 64x64 workgroup per 2 CUs (the 256-row
+// policy / actor passes) use one-wave 32x32 tiles: 4x the workgroups, same
+// per-wave work, lower latency.
 int choose_variant(const Params& p) {
-  const int64_t big = ((p.M + 127) / 128) * ((p.N + 127) / 128) * p.batch * p.splits;
-  if (p.N >= 128 && p.M >= 128 && big >= 384) return 1;
-  const int64_t mid = ((p.M + 127) / 128) * ((p.N + 63) / 64) * p.batch * p.splits;
-  if (p.M >= 128 && mid >= 384) return 2;
-  return 0;
+  const int64_t blocks64 = ((p.M + 63) / 64) * ((p.N + 63) / 64) * p.batch * p.splits;
+  if (blocks64 >= 128) return 0;
+  // few workgroups: the K loop's load latency dominates -> deeper K tiles
+  const int64_t kslice = (p.K + p.splits - 1) / p.splits;
+  return kslice >= 128 ? 7 : 6;
 }
 
 int env_variant() {

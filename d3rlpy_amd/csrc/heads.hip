@@ -20,9 +20,10 @@
 namespace d3a {
 namespace {
 
-__global__ __launch_bounds__(256) void head1_bwd_kernel(d3a_head1_bwd_desc d) {
-  __shared__ double sw[4][64];
-  __shared__ double sb[4];
+__global__ __launch_bounds__(1024) void head1_bwd_kernel(d3a_head1_bwd_desc d) {
+  constexpr int NW = 16;  // waves per workgroup (latency hiding: many rows in flight)
+  __shared__ double sw[NW][64];
+  __shared__ double sb[NW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t j = (int64_t)blockIdx.x * 64 + lane;
   const int64_t s = blockIdx.y, c = blockIdx.z;
@@ -33,28 +34,46 @@ __global__ __launch_bounds__(256) void head1_bwd_kernel(d3a_head1_bwd_desc d) {
   const float wj = colok ? d.w[c * d.swb + j] : 0.f;
   const float* h = d.h + c * d.shb;
   float* dz = d.dz + c * d.sdzb;
+  const float gs = d.gscale ? *d.gscale : 1.f;
   double accw = 0.0, accb = 0.0;
-  for (int64_t r = r0 + w; r < r1; r += 4) {
-    float g;
-    if (d.q_min) {
-      // first argmin over members of q[.][r]
-      int arg = 0;
-      float mn = d.q_min[r];
-      for (int k = 1; k < d.C; ++k) {
-        const float v = d.q_min[k * d.sqb + r];
-        if (v < mn) { mn = v; arg = k; }
+  // 8 rows per wave per iteration: all loads issued before any use
+  constexpr int U = 8;
+  for (int64_t rb = r0 + w; rb < r1; rb += NW * U) {
+    float g[U], hv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = rb + NW * u;
+      g[u] = 0.f;
+      hv[u] = 0.f;
+      if (r < r1) {
+        if (d.q_min) {
+          // first argmin over members of q[.][r]
+          int arg = 0;
+          float mn = d.q_min[r];
+          for (int k = 1; k < d.C; ++k) {
+            const float v = d.q_min[k * d.sqb + r];
+            if (v < mn) { mn = v; arg = k; }
+          }
+          g[u] = (arg == c) ? d.scale : 0.f;
+        } else {
+          g[u] = d.g[c * d.sgb + r];
+          if (r < d.n_scaled) g[u] *= gs;
+        }
+        if (colok) hv[u] = h[r * d.ldh + j];
       }
-      g = (arg == c) ? d.scale : 0.f;
-      if (d.g_out && lane == 0 && blockIdx.x == 0) d.g_out[c * d.sgb + r] = g;
-    } else {
-      g = d.g[c * d.sgb + r];
     }
-    if (colok) {
-      const float hv = h[r * d.ldh + j];
-      dz[r * d.lddz + j] = hv > 0.f ? g * wj : 0.f;
-      accw += (double)(g * hv);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = rb + NW * u;
+      if (r < r1) {
+        if (d.q_min && d.g_out && lane == 0 && blockIdx.x == 0) d.g_out[c * d.sgb + r] = g[u];
+        if (colok) {
+          dz[r * d.lddz + j] = hv[u] > 0.f ? g[u] * wj : 0.f;
+          accw += (double)(g[u] * hv[u]);
+        }
+        accb += (double)g[u];
+      }
     }
-    accb += (double)g;
   }
   if (d.dW) {
     sw[w][lane] = accw;
@@ -62,11 +81,16 @@ __global__ __launch_bounds__(256) void head1_bwd_kernel(d3a_head1_bwd_desc d) {
     __syncthreads();
     if (w == 0) {
       if (colok) {
-        const double t = sw[0][lane] + sw[1][lane] + sw[2][lane] + sw[3][lane];
+        double t = 0.0;
+        for (int q = 0; q < NW; ++q) t += sw[q][lane];
         d.dW[s * d.sWs + c * d.n + j] = (float)t;
       }
       if (lane == 0 && blockIdx.x == 0 && d.db)
-        d.db[s * d.sbs + c] = (float)(sb[0] + sb[1] + sb[2] + sb[3]);
+      {
+        double tb = 0.0;
+        for (int q = 0; q < NW; ++q) tb += sb[q];
+        d.db[s * d.sbs + c] = (float)tb;
+      }
     }
   }
 }
@@ -85,7 +109,7 @@ extern "C" int d3a_head1_bwd(const d3a_head1_bwd_desc* d, void* stream) {
   D3A_CHECK_ARG(!d->dW || d->db, "d3a_head1_bwd: dW requires db");
   if (d->rows == 0) return 0;
   dim3 grid((unsigned)((d->n + 63) / 64), (unsigned)d->splits, (unsigned)d->C);
-  hipLaunchKernelGGL(head1_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, *d);
+  hipLaunchKernelGGL(head1_bwd_kernel, grid, dim3(1024), 0, (hipStream_t)stream, *d);
   D3A_LAUNCH_CHECK("d3a_head1_bwd");
   return 0;
 }

@@ -27,7 +27,9 @@ from . import ops
 from .nets import EnsembleMLP, GradSpace, ParamStore
 
 
-def n_splits(rows: int, min_rows: int = 256, max_splits: int = 32) -> int:
+def n_splits(rows: int, min_rows: int = 32, max_splits: int = 32) -> int:
+    """Split-K slices for weight gradients: >= min_rows rows per slice, at most
+    max_splits slices (the Adam kernel sums the slices in a fixed order)."""
     return max(1, min(max_splits, rows // min_rows))
 
 
@@ -104,7 +106,8 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
              acts: Acts, dout: int, ld_dout: int, sdout_b: int, r0: int, n: int,
              weight_grads: bool = True, dx: Optional[torch.Tensor] = None,
              sxb: Optional[int] = None, q_min: Optional[int] = None, sq_b: int = 0,
-             q_scale: float = 0.0, g_out: Optional[int] = None) -> None:
+             q_scale: float = 0.0, g_out: Optional[int] = None,
+             g_scale: Optional[int] = None, n_scaled: int = 0) -> None:
     """Backward of rows [r0, r0+n) given dL/d(output) (``dout`` points at row r0).
 
     dout layout: [C] x rows, member stride sdout_b, row stride ld_dout (1 for a
@@ -149,6 +152,8 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
             d.g_out, d.sgb = g_out, sdout_b
         else:
             d.g, d.sgb = dout, sdout_b
+            if g_scale is not None:
+                d.gscale, d.n_scaled = g_scale, n_scaled
         d.h, d.shb, d.ldh = hin, sh, ld_h
         d.w, d.swb = net.W(L - 1, store), Hin
         d.dz, d.sdzb, d.lddz = cur.data_ptr(), scur, ld_cur
@@ -156,7 +161,8 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
             gW, gb = gs.get(net.wname(L - 1)), gs.get(net.bname(L - 1))
             d.dW, d.sWs = gW.data_ptr(), C * Hin
             d.db, d.sbs = gb.data_ptr(), C
-        d.rows, d.n, d.splits, d.C = n, Hin, S if weight_grads else 1, C
+        d.rows, d.n, d.C = n, Hin, C
+        d.splits = S if weight_grads else max(1, n // 64)
         ops.call_desc("d3a_head1_bwd", d)
     else:
         assert q_min is None

@@ -104,6 +104,8 @@ int d3a_outer_mask_f32(const float* g, int64_t sgb, const float* w,
  * dW/db may be NULL (input gradient only). */
 typedef struct d3a_head1_bwd_desc {
   const float* g;      int64_t sgb;            /* [C] x rows (or NULL)      */
+  const float* gscale; int64_t n_scaled;       /* g[r] *= *gscale for r < n_scaled
+                                                  (gscale may be NULL)      */
   const float* q_min;  int64_t sqb;            /* [C] x rows (or NULL)      */
   float scale;
   float* g_out;                                /* optional, stride sgb      */
@@ -198,6 +200,8 @@ typedef struct d3a_cql_sample_desc {
   float* actor_u;         /* [B][A]  pre-tanh actor sample                */
   float* actor_logp;      /* [B]                                         */
   int32_t B, D, A, N;
+  int32_t ldx;            /* row stride of x_q / x_targ / x_actor (>= D + A;
+                             padded to a multiple of 4 for 16-byte rows)   */
   float min_logstd, max_logstd;
 } d3a_cql_sample_desc;
 int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream);

@@ -45,7 +45,7 @@ def main():
             sB=(H * H, 1, H), sC=(R * H, H, 1), bias=b.data_ptr(), sbias=H, relu=True,
             variant=v)),
     }
-    variants = list(range(6))
+    variants = list(range(9))
     res = {k: {v: [] for v in variants} for k in shapes}
     reps = 20
     for rnd in range(5):
