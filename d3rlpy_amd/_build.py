@@ -28,7 +28,9 @@ CFLAGS = [
     "-O3",
     "-fPIC",
     "-std=c++17",
-    "-ffp-contract=fast",
+    # no implicit a*b+c -> fma: elementwise stages round like the reference's
+    # separate torch ops; fused multiply-adds are written as fmaf explicitly
+    "-ffp-contract=off",
     "-Wall",
     "-Wno-unused-function",
     f"-I{ROOT / 'include'}",

@@ -121,6 +121,41 @@ class GatherDesc(C.Structure):
     ]
 
 
+class Td3PrepDesc(C.Structure):
+    _fields_ = [
+        ("obs", vp), ("next_obs", vp), ("act", vp), ("mean", vp), ("std", vp),
+        ("eps", C.c_float), ("x_q", vp), ("x_targ", vp),
+        ("B", C.c_int32), ("D", C.c_int32), ("A", C.c_int32), ("ldx", C.c_int32),
+    ]
+
+
+class Td3TargetDesc(C.Structure):
+    _fields_ = [
+        ("head", vp), ("noise", vp), ("sigma", C.c_float), ("clip", C.c_float),
+        ("x_targ", vp), ("ldx", C.c_int32), ("D", C.c_int32), ("B", C.c_int32),
+        ("A", C.c_int32),
+    ]
+
+
+class Td3CriticLossDesc(C.Structure):
+    _fields_ = [
+        ("q", vp), ("q_targ", vp), ("rew", vp), ("term", vp), ("n_steps", vp),
+        ("dq", vp), ("metrics", vp), ("B", C.c_int32), ("C", C.c_int32),
+        ("gamma", C.c_float), ("actor_step", C.c_int32),
+    ]
+
+
+class Td3bcActorDesc(C.Structure):
+    _fields_ = [
+        ("head", vp), ("x_q", vp), ("x_actor", vp), ("pi_act", vp),
+        ("q0", vp), ("g", vp), ("scalars", vp),
+        ("dq_da", vp), ("ld_da", C.c_int32), ("da_off", C.c_int32),
+        ("act", vp), ("dhead", vp), ("metrics", vp),
+        ("alpha", C.c_float),
+        ("B", C.c_int32), ("D", C.c_int32), ("A", C.c_int32), ("ldx", C.c_int32),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "d3a_abi_version": (C.c_int, []),
@@ -146,6 +181,12 @@ _SIGNATURES = {
     "d3a_sac_actor_dq": (C.c_int, [vp, C.c_int64, C.c_int32, C.c_int32, vp, C.c_int64, vp]),
     "d3a_sac_actor_head": (C.c_int, [C.POINTER(SacActorHeadDesc), vp]),
     "d3a_gather_batch": (C.c_int, [C.POINTER(GatherDesc), vp]),
+    "d3a_td3_prep": (C.c_int, [C.POINTER(Td3PrepDesc), vp]),
+    "d3a_td3_target": (C.c_int, [C.POINTER(Td3TargetDesc), vp]),
+    "d3a_td3_critic_loss": (C.c_int, [C.POINTER(Td3CriticLossDesc), vp]),
+    "d3a_td3bc_actor_input": (C.c_int, [C.POINTER(Td3bcActorDesc), vp]),
+    "d3a_td3bc_actor_seed": (C.c_int, [C.POINTER(Td3bcActorDesc), vp]),
+    "d3a_td3bc_actor_head": (C.c_int, [C.POINTER(Td3bcActorDesc), vp]),
 }
 
 EXPORTED = tuple(_SIGNATURES)

@@ -1,0 +1,19 @@
+"""Algorithms on the HIP update engine (reference: d3rlpy/algos/__init__.py).
+
+Only the algorithms on the accelerated hot path are provided.
+"""
+from .cql import CQL
+from .td3_plus_bc import TD3PlusBC
+
+__all__ = ["CQL", "TD3PlusBC", "get_algo"]
+
+ALGO_LIST = {"cql": CQL, "td3_plus_bc": TD3PlusBC}
+
+
+def get_algo(name: str, discrete: bool):
+    """algos/__init__.py:66-85 for the algorithms available here."""
+    if discrete:
+        raise ValueError(f"discrete {name} is not available on the HIP engine")
+    if name not in ALGO_LIST:
+        raise ValueError(f"{name} is not available on the HIP engine")
+    return ALGO_LIST[name]

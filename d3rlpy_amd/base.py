@@ -36,6 +36,11 @@ IMPL_NOT_INITIALIZED_ERROR = "The neural network parameters are not initialized.
     "Pleaes call build_with_dataset, build_with_env, or directly call fit method."
 
 
+def _mean_present(col: np.ndarray) -> float:
+    present = col[~np.isnan(col)]
+    return float(np.mean(present)) if present.size else float("nan")
+
+
 def _serialize(v: Any) -> Any:
     if isinstance(v, (EncoderFactory, QFunctionFactory)):
         return {"type": v.get_type(), "params": v.get_params()}
@@ -253,7 +258,10 @@ class LearnableBase:
                     callback(self, epoch, total_step)
             names, values = self._impl.read_metrics_ring(ring)
             elapsed = time.perf_counter() - t0
-            epoch_loss = {n: float(np.mean(values[:, i])) for i, n in enumerate(names)}
+            # NaN marks "not computed at this step" (e.g. TD3's delayed actor
+            # loss); the reference logs such a metric only on the steps that
+            # produce it, so the epoch mean skips those rows
+            epoch_loss = {n: _mean_present(values[:, i]) for i, n in enumerate(names)}
             logger.add_epoch(epoch, total_step, epoch_loss,
                              {"time_step": elapsed / max(1, len(iterator))})
             self._loss_history["epoch"].append(epoch)

@@ -37,10 +37,10 @@ __global__ __launch_bounds__(256) void rowdot_kernel(const float* X, int64_t sXb
     for (int64_t j = (int64_t)lane * 4; j < n; j += 256) {
       const float4 a = *reinterpret_cast<const float4*>(x + j);
       const float4 c = *reinterpret_cast<const float4*>(wb + j);
-      acc += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
+      acc = fmaf(a.w, c.w, fmaf(a.z, c.z, fmaf(a.y, c.y, fmaf(a.x, c.x, acc))));
     }
   } else {
-    for (int64_t j = lane; j < n; j += 64) acc += x[j] * wb[j];
+    for (int64_t j = lane; j < n; j += 64) acc = fmaf(x[j], wb[j], acc);
   }
   acc = wave_sum(acc);
   if (lane == 0) out[b * sOb + r] = acc + (bias ? bias[b * sbb] : 0.f);

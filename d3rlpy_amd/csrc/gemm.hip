@@ -207,6 +207,145 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32_kernel(Params
   }
 }
 
+// ---- register-direct split-K kernel for small problems ---------------------
+// The 256-row layers of the policy / target / actor passes (M, N <= 256,
+// K <= 256) give only tens of 64x64 workgroups, and the LDS pipeline above
+// then waits one global-load latency per K tile.  Here each wave of a
+// workgroup owns the same 32 x (32*WN) output tile over a different K slice
+// and loads its MFMA operands straight into registers (no LDS, no barrier in
+// the K loop): lane l covers row/col l&31 and k = k0 + 4*(l>>5) + {0..3} (one
+// 16-byte load along a unit-stride k, or four coalesced loads across lanes),
+// feeding four v_mfma_f32_32x32x2_f32 per 8 k.  U such groups are loaded
+// before any is multiplied, so a wave has U loads per operand in flight.  The
+// KW partial tiles are summed in wave order through LDS (deterministic).
+template <int MODE>
+__device__ __forceinline__ float4 rd_load(const float* base, int64_t sx, int64_t sk, int64_t x,
+                                          int64_t X, int64_t k, int64_t kend) {
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (x >= X) return r;
+  if (MODE == MODE_KCONTIG) {
+    const float* p = base + x * sx + k;
+    if (k + 3 < kend && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
+      r = *reinterpret_cast<const float4*>(p);
+    } else {
+      if (k + 0 < kend) r.x = p[0];
+      if (k + 1 < kend) r.y = p[1];
+      if (k + 2 < kend) r.z = p[2];
+      if (k + 3 < kend) r.w = p[3];
+    }
+  } else {
+    const float* p = base + k * sk + x * sx;
+    if (k + 0 < kend) r.x = p[0];
+    if (k + 1 < kend) r.y = p[sk];
+    if (k + 2 < kend) r.z = p[2 * sk];
+    if (k + 3 < kend) r.w = p[3 * sk];
+  }
+  return r;
+}
+
+template <int AMODE, int BMODE, int KW, int WN, int U>
+__global__ __launch_bounds__(64 * KW) void gemm_rd_kernel(Params p) {
+  __shared__ float red[(KW > 1 ? KW - 1 : 1) * WN * 16 * 64];
+  __shared__ double rsum[KW * 32];
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  const int li = lane & 31, lg = lane >> 5;
+  const int64_t n0 = (int64_t)blockIdx.x * (32 * WN);
+  const int64_t m0 = (int64_t)blockIdx.y * 32;
+  const int64_t bz = blockIdx.z;
+  const int64_t b = bz / p.splits, s = bz % p.splits;
+  const int64_t sbeg = s * p.kchunk;
+  const int64_t send = (sbeg + p.kchunk < p.K) ? sbeg + p.kchunk : p.K;
+  // this wave's K slice (multiple of 8 so every lane group starts aligned)
+  int64_t wch = (send - sbeg + KW - 1) / KW;
+  wch = (wch + 7) / 8 * 8;
+  const int64_t kb = sbeg + w * wch;
+  const int64_t ke = (kb + wch < send) ? kb + wch : send;
+  const float* Ab = p.A + b * p.sAb;
+  const float* Bb = p.B + b * p.sBb;
+  const int64_t m = m0 + li;
+  const bool do_rowsum = p.rowsum != nullptr && blockIdx.x == 0;
+
+  f32x16 acc[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  double rs = 0.0;
+
+  for (int64_t k0 = kb; k0 < ke; k0 += 8 * U) {
+    float4 ra[U], rb[U][WN];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = k0 + 8 * u + 4 * lg;
+      ra[u] = rd_load<AMODE>(Ab, p.sAm, p.sAk, m, p.M, k, ke);
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        rb[u][j] = rd_load<BMODE>(Bb, p.sBn, p.sBk, n0 + 32 * j + li, p.N, k, ke);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (do_rowsum) rs += (double)ra[u].x + (double)ra[u].y + (double)ra[u].z + (double)ra[u].w;
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[u].x, rb[u][j].x, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[u].y, rb[u][j].y, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[u].z, rb[u][j].z, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[u].w, rb[u][j].w, acc[j], 0, 0, 0);
+      }
+    }
+  }
+
+  if (KW > 1) {
+    if (w > 0) {
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(((w - 1) * WN + j) * 16 + r) * 64 + lane] = acc[j][r];
+    }
+  }
+  if (do_rowsum) {
+    rs += __shfl_xor(rs, 32, 64);
+    if (lg == 0) rsum[w * 32 + li] = rs;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  if (KW > 1) {
+#pragma unroll
+    for (int v = 1; v < KW; ++v)
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] += red[(((v - 1) * WN + j) * 16 + r) * 64 + lane];
+  }
+  if (do_rowsum && lg == 0 && m < p.M) {
+    double tot = 0.0;
+    for (int v = 0; v < KW; ++v) tot += rsum[v * 32 + li];
+    p.rowsum[b * p.sRb + s * p.sRs + m] = (float)tot;
+  }
+  float* Cb = p.C + b * p.sCb + s * p.sCs;
+  const float* biasb = p.bias ? p.bias + b * p.sbias_b : nullptr;
+  const float* maskb = p.mask ? p.mask + b * p.sMb : nullptr;
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int64_t n = n0 + 32 * j + li;
+    if (n >= p.N) continue;
+    const float bn = biasb ? biasb[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * lg;
+      if (mm < p.M) {
+        float v = acc[j][r] * p.alpha;
+        if (biasb) v += bn;
+        if (p.relu) v = fmaxf(v, 0.f);
+        if (maskb && !(maskb[mm * p.sMm + n * p.sMn] > 0.f)) v = 0.f;
+        float* dst = Cb + mm * p.sCm + n * p.sCn;
+        if (p.accumulate) *dst += v; else *dst = v;
+      }
+    }
+  }
+}
+
 struct Variant {
   int wm_t, wn_t, waves_m, waves_n, bk;
 };
@@ -221,7 +360,10 @@ constexpr Variant kVariants[] = {
     {1, 1, 1, 1, 16},  // 6: 32x32   BK16, one wave
     {1, 1, 1, 1, 64},  // 7: 32x32   BK64, one wave (small, latency-bound problems)
     {1, 1, 2, 2, 64},  // 8: 64x64   BK64
+    {1, 1, 1, 1, 8},   // 9: register-direct 32x32, K split over waves (gemm_rd_kernel)
+    {1, 2, 1, 1, 8},   // 10: register-direct 32x64
 };
+constexpr int kFirstRd = 9;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 template <int AM, int BMd, int V>
@@ -234,9 +376,37 @@ void launch_v(const Params& p, hipStream_t st) {
                      dim3(64 * v.waves_m * v.waves_n), 0, st, p);
 }
 
+// waves per workgroup for the register-direct kernel: ~2048 waves in flight,
+// at least 32 k (one U=4 group of loads) per wave
+int rd_waves(const Params& p, int wn) {
+  const int64_t tiles = ((p.N + 32 * wn - 1) / (32 * wn)) * ((p.M + 31) / 32) * p.batch * p.splits;
+  int kw = 8;
+  while (kw > 1 && (tiles * kw > 4096 || p.kchunk / kw < 32)) kw >>= 1;
+  return kw;
+}
+
+template <int AM, int BMd, int KW, int WN>
+void launch_rd_kw(const Params& p, hipStream_t st) {
+  dim3 grid((unsigned)((p.N + 32 * WN - 1) / (32 * WN)), (unsigned)((p.M + 31) / 32),
+            (unsigned)(p.batch * p.splits));
+  hipLaunchKernelGGL((gemm_rd_kernel<AM, BMd, KW, WN, 4>), grid, dim3(64 * KW), 0, st, p);
+}
+
+template <int AM, int BMd, int WN>
+void launch_rd(const Params& p, hipStream_t st) {
+  switch (rd_waves(p, WN)) {
+    case 8: launch_rd_kw<AM, BMd, 8, WN>(p, st); break;
+    case 4: launch_rd_kw<AM, BMd, 4, WN>(p, st); break;
+    case 2: launch_rd_kw<AM, BMd, 2, WN>(p, st); break;
+    default: launch_rd_kw<AM, BMd, 1, WN>(p, st); break;
+  }
+}
+
 template <int AM, int BMd>
 void launch_modes(const Params& p, int variant, hipStream_t st) {
   switch (variant) {
+    case 9: launch_rd<AM, BMd, 1>(p, st); break;
+    case 10: launch_rd<AM, BMd, 2>(p, st); break;
     case 1: launch_v<AM, BMd, 1>(p, st); break;
     case 2: launch_v<AM, BMd, 2>(p, st); break;
     case 3: launch_v<AM, BMd, 3>(p, st); break;
@@ -249,19 +419,22 @@ void launch_modes(const Params& p, int variant, hipStream_t st) {
   }
 }
 
-// Tile choice.  Measured on MI355X (tools/bench_gemm.py, profiles/r01_gemm_sweep.log):
-// at this engine's shapes (K <= 256 per pass, or split-K slices of ~256 rows)
-// the 64x64 tile is within 3 % of the best variant everywhere and 10-50 %
-// faster than 128-wide tiles on the backward shapes, so it is the default.
-// Problems that give fewer than ~one 64x64 workgroup per 2 CUs (the 256-row
-// policy / actor passes) use one-wave 32x32 tiles: 4x the workgroups, same
-// per-wave work, lower latency.
+// Tile choice, from per-call sweeps of every GEMM of a K2 CQL and a K1 TD3+BC
+// update (tools/gemm_pipeline_sweep.py, graph-captured timings,
+// profiles/r01_pipe_sweep_*.log):
+//  - few output tiles (< 128 64x64 workgroups, or a 32-wide output) with at
+//    least 32 k per split: the register-direct split-K kernel (9), 1.7-2.6x
+//    faster than any LDS tile on the 256-row policy / target / actor layers
+//    and the narrow first-layer input gradients;
+//  - otherwise the 64x64 LDS tile (0), within 5 % of the best LDS variant on
+//    the large critic passes;
+//  - tiny K (the first layer's 11-17 inputs): one-wave 32x32 tile (6).
 int choose_variant(const Params& p) {
   const int64_t blocks64 = ((p.M + 63) / 64) * ((p.N + 63) / 64) * p.batch * p.splits;
-  if (blocks64 >= 128) return 0;
-  // few workgroups: the K loop's load latency dominates -> deeper K tiles
   const int64_t kslice = (p.K + p.splits - 1) / p.splits;
-  return kslice >= 128 ? 7 : 6;
+  if (kslice >= 32 && (blocks64 < 128 || p.M <= 32 || p.N <= 32)) return 9;
+  if (blocks64 >= 128) return 0;
+  return 6;
 }
 
 int env_variant() {

@@ -51,14 +51,16 @@ class Acts:
 
 
 def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: int, acts: Acts,
-            r0: int = 0, r1: Optional[int] = None, sxb: Optional[int] = None) -> None:
-    """Forward rows [r0, r1) of x (row stride ldx) through the ensemble."""
+            r0: int = 0, r1: Optional[int] = None, sxb: Optional[int] = None,
+            members: Optional[int] = None) -> None:
+    """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
+    (through its first ``members`` members only, when given)."""
     R = acts.R
     r1 = R if r1 is None else r1
     n = r1 - r0
     if n <= 0:
         return
-    C = net.C
+    C = net.C if members is None else members
     sizes = net.sizes
     L = net.n_layers
     inp, ld_in = x + 4 * r0 * ldx, ldx
@@ -107,7 +109,8 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
              weight_grads: bool = True, dx: Optional[torch.Tensor] = None,
              sxb: Optional[int] = None, q_min: Optional[int] = None, sq_b: int = 0,
              q_scale: float = 0.0, g_out: Optional[int] = None,
-             g_scale: Optional[int] = None, n_scaled: int = 0) -> None:
+             g_scale: Optional[int] = None, n_scaled: int = 0,
+             members: Optional[int] = None) -> None:
     """Backward of rows [r0, r0+n) given dL/d(output) (``dout`` points at row r0).
 
     dout layout: [C] x rows, member stride sdout_b, row stride ld_dout (1 for a
@@ -117,6 +120,9 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
     """
     net = bs.net
     C, L, sizes, R = net.C, net.n_layers, net.sizes, acts.R
+    if members is not None:
+        assert not weight_grads, "member subsets are for input gradients only"
+        C = members
     S = bs.splits
     assert n <= bs.rows
     sxb_ = (0 if x_shared else R * ldx) if sxb is None else sxb

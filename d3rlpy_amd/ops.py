@@ -8,6 +8,7 @@ and contiguous where a row-major layout is implied.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -15,6 +16,7 @@ import torch
 from . import _native as N
 
 _F32 = 4
+_TRACE = os.environ.get("D3A_GEMM_TRACE") == "1"  # print GEMM shapes as they are enqueued
 
 
 def _stream() -> int:
@@ -55,6 +57,10 @@ def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
     d.sMb, d.sMm, d.sMn = sM
     d.splits, d.sCs = splits, sCs
     d.alpha, d.relu, d.accumulate = alpha, int(relu), int(accumulate)
+    if _TRACE:
+        print(f"gemm M={M} N={Nn} K={K} batch={batch} splits={splits} sA={tuple(sA)} "
+              f"sB={tuple(sB)} sC={tuple(sC)} mask={mask is not None} relu={relu} "
+              f"rowsum={rowsum is not None} variant={variant}", flush=True)
     N.check(N.lib().d3a_gemm_f32(C.byref(d), _stream()), "d3a_gemm_f32")
 
 

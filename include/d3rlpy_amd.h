@@ -295,6 +295,63 @@ typedef struct d3a_gather_desc {
 } d3a_gather_desc;
 int d3a_gather_batch(const d3a_gather_desc* d, void* stream);
 
+/* ---- TD3+BC stages (K1).  The layer GEMMs use d3a_gemm_f32 / d3a_rowdot_f32
+ * / d3a_head1_bwd; these produce the layer inputs and loss gradients. ---- */
+
+/* Standard-scaled Q inputs (replaces scaler.transform in TorchMiniBatch,
+ * torch_utility.py:179-181 / preprocessing/scalers.py:350-354, plus the
+ * torch.cat([x, action]) of ContinuousQFunction.forward):
+ * x_q[b] = ((obs_b - mean) / (std + eps), act_b); x_targ[b][0:D) = scaled
+ * next_obs_b.  mean == NULL: no scaler. */
+typedef struct d3a_td3_prep_desc {
+  const float* obs; const float* next_obs; const float* act;
+  const float* mean; const float* std; float eps;
+  float* x_q; float* x_targ;
+  int32_t B, D, A, ldx;
+} d3a_td3_prep_desc;
+int d3a_td3_prep(const d3a_td3_prep_desc* d, void* stream);
+
+/* Target policy smoothing (replaces TD3Impl.compute_target,
+ * algos/torch/td3_impl.py:61-78): x_targ[b][D+j] =
+ * clamp(tanh(head) + clamp(sigma * noise, -clip, clip), -1, 1). */
+typedef struct d3a_td3_target_desc {
+  const float* head; const float* noise; float sigma, clip;
+  float* x_targ; int32_t ldx, D, B, A;
+} d3a_td3_target_desc;
+int d3a_td3_target(const d3a_td3_target_desc* d, void* stream);
+
+/* Critic TD loss (replaces DDPGBaseImpl.compute_critic_loss,
+ * algos/torch/ddpg_impl.py:154-167 -> EnsembleQFunction.compute_error with
+ * the mean Q function's mse): dq[c][b] = dL/dq, metrics[0] = critic loss;
+ * metrics[1] (actor loss) is set to NaN when actor_step == 0 (no actor
+ * update at this step: TD3PlusBC._update, algos/td3_plus_bc.py:177-192). */
+typedef struct d3a_td3_critic_loss_desc {
+  const float* q; const float* q_targ;   /* [C][B] */
+  const float* rew; const float* term; const float* n_steps;
+  float* dq; float* metrics;
+  int32_t B, C; float gamma; int32_t actor_step;
+} d3a_td3_critic_loss_desc;
+int d3a_td3_critic_loss(const d3a_td3_critic_loss_desc* d, void* stream);
+
+/* TD3+BC actor loss (replaces TD3PlusBCImpl.compute_actor_loss,
+ * algos/torch/td3_plus_bc_impl.py:64-70), in three stages around the
+ * critic-0 forward / input backward:
+ *   d3a_td3bc_actor_input  x_actor = (x_q[:, :D], tanh(head)), pi_act = tanh(head)
+ *   d3a_td3bc_actor_seed   scalars[0] = lam = alpha / mean|q0|,
+ *                          scalars[1] = -lam mean(q0), g = -lam / B
+ *   d3a_td3bc_actor_head   dhead = (dq_da + d mse/da)(1 - a^2), metrics[1] = loss */
+typedef struct d3a_td3bc_actor_desc {
+  const float* head; const float* x_q; float* x_actor; float* pi_act;
+  const float* q0; float* g; float* scalars;
+  const float* dq_da; int32_t ld_da, da_off;
+  const float* act; float* dhead; float* metrics;
+  float alpha;
+  int32_t B, D, A, ldx;
+} d3a_td3bc_actor_desc;
+int d3a_td3bc_actor_input(const d3a_td3bc_actor_desc* d, void* stream);
+int d3a_td3bc_actor_seed(const d3a_td3bc_actor_desc* d, void* stream);
+int d3a_td3bc_actor_head(const d3a_td3bc_actor_desc* d, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

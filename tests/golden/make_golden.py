@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 from oracle.cql import Batch, CQLNoise, CQLOracle  # noqa: E402
 from oracle import gather as og  # noqa: E402
+from oracle.td3bc import StandardScalerT, TD3PlusBCOracle  # noqa: E402
 
 STATE_KEYS = ("_q_func", "_targ_q_func", "_policy", "_targ_policy", "_log_temp", "_log_alpha")
 
@@ -64,6 +65,44 @@ def cql_small():
     np.savez_compressed(os.path.join(HERE, "cql_small.npz"), **data)
 
 
+TD3_KEYS = ("_q_func", "_targ_q_func", "_policy", "_targ_policy")
+
+
+def td3bc_small():
+    """Two TD3PlusBC._update steps (grad_step 0: critic + actor + targets;
+    grad_step 1: critic only) with a standard scaler and n-step targets."""
+    D, A, H, B = 6, 2, [32, 32], 16
+    rs = np.random.RandomState(21)
+    mean = rs.randn(D) * 0.5
+    std = np.abs(rs.randn(D)) + 0.5
+    orc = TD3PlusBCOracle(D, A, n_critics=2, hidden_units=H, scaler=StandardScalerT(mean, std),
+                          seed=321)
+    data = {"cfg": np.array([D, A, H[0], len(H), B], dtype=np.int64),
+            "scaler_mean": mean, "scaler_std": std}
+    for k in TD3_KEYS:
+        for n, t in getattr(orc, k).state_dict().items():
+            data[f"init/{k}/{n}"] = t.detach().numpy().copy()
+    metrics = []
+    for step in range(2):
+        obs = (rs.randn(B, D) * 2).astype(np.float32)
+        act = rs.uniform(-1, 1, (B, A)).astype(np.float32)
+        rew = rs.randn(B).astype(np.float32)
+        nobs = (rs.randn(B, D) * 2).astype(np.float32)
+        term = (rs.rand(B) < 0.2).astype(np.float32)
+        nst = rs.randint(1, 3, size=B).astype(np.float32)
+        noise = torch.randn(B, A, generator=torch.Generator().manual_seed(30 + step))
+        for k, v in (("obs", obs), ("act", act), ("rew", rew), ("next_obs", nobs),
+                     ("term", term), ("n_steps", nst), ("noise", noise.numpy())):
+            data[f"step{step}/{k}"] = v
+        m = orc.update(Batch.from_numpy(obs, act, rew, nobs, term, nst), noise, grad_step=step)
+        metrics.append([m["critic_loss"], m.get("actor_loss", np.nan)])
+    data["metrics"] = np.array(metrics, dtype=np.float32)
+    for k in TD3_KEYS:
+        for n, t in getattr(orc, k).state_dict().items():
+            data[f"final/{k}/{n}"] = t.detach().numpy().copy()
+    np.savez_compressed(os.path.join(HERE, "td3bc_small.npz"), **data)
+
+
 def gather_small():
     """Transitions of two episodes (one terminal, one not) gathered with the
     reference semantics: vector obs n_steps 1 and 3; image obs n_frames 4."""
@@ -99,4 +138,5 @@ def gather_small():
 if __name__ == "__main__":
     cql_small()
     gather_small()
+    td3bc_small()
     print("golden fixtures written to", HERE)

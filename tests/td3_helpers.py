@@ -1,0 +1,54 @@
+"""Shared helpers for TD3+BC parity tests: oracle + HIP impl with equal state."""
+import numpy as np
+import torch
+
+from oracle.td3bc import StandardScalerT, TD3PlusBCOracle
+
+TD3_STATE_KEYS = ("_q_func", "_targ_q_func", "_policy", "_targ_policy", "_critic_optim",
+                  "_actor_optim")
+
+
+def make_scaler_stats(rs: np.random.RandomState, D):
+    mean = rs.randn(D) * 0.5
+    std = np.abs(rs.randn(D)) + 0.5
+    return mean, std
+
+
+def make_td3_impl(D, A, hidden, C=2, scaler_stats=None, **kw):
+    from d3rlpy_amd.algos.td3_plus_bc_impl import TD3PlusBCImpl
+    from d3rlpy_amd.factories import AdamFactory, MeanQFunctionFactory, VectorEncoderFactory
+    from d3rlpy_amd.preprocessing import StandardScaler
+    args = dict(actor_learning_rate=3e-4, critic_learning_rate=3e-4, gamma=0.99, tau=0.005,
+                target_smoothing_sigma=0.2, target_smoothing_clip=0.5, alpha=2.5)
+    args.update(kw)
+    scaler = None
+    if scaler_stats is not None:
+        scaler = StandardScaler(mean=scaler_stats[0], std=scaler_stats[1])
+    impl = TD3PlusBCImpl(
+        observation_shape=(D,), action_size=A,
+        actor_optim_factory=AdamFactory(), critic_optim_factory=AdamFactory(),
+        actor_encoder_factory=VectorEncoderFactory(hidden),
+        critic_encoder_factory=VectorEncoderFactory(hidden),
+        q_func_factory=MeanQFunctionFactory(), n_critics=C, use_gpu=0, scaler=scaler,
+        action_scaler=None, reward_scaler=None, **args)
+    impl.build()
+    return impl
+
+
+def make_td3_oracle(D, A, hidden, C=2, seed=0, scaler_stats=None, **kw):
+    scaler = None if scaler_stats is None else StandardScalerT(*scaler_stats)
+    return TD3PlusBCOracle(D, A, n_critics=C, hidden_units=hidden, scaler=scaler, seed=seed, **kw)
+
+
+def td3_oracle_state(orc):
+    return {k: getattr(orc, k).state_dict() for k in TD3_STATE_KEYS}
+
+
+def make_td3_batch(rs: np.random.RandomState, B, D, A, n_steps=1):
+    obs = (rs.randn(B, D) * 2 + 0.3).astype(np.float32)
+    act = rs.uniform(-1, 1, size=(B, A)).astype(np.float32)
+    rew = rs.randn(B).astype(np.float32)
+    nobs = (rs.randn(B, D) * 2 + 0.3).astype(np.float32)
+    term = (rs.rand(B) < 0.1).astype(np.float32)
+    nst = rs.randint(1, n_steps + 1, size=B).astype(np.float32)
+    return obs, act, rew, nobs, term, nst

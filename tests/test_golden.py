@@ -137,3 +137,73 @@ def test_hip_cql_update_vs_fixture():
     for k, d in _state_from(g, "final/").items():
         for n, t in d.items():
             assert float((sd[k][n].view(-1) - t.view(-1)).abs().max()) <= 1e-5, (k, n)
+
+
+def _td3_from_fixture(g, prefix):
+    keys = ("_q_func", "_targ_q_func", "_policy", "_targ_policy")
+    sd = {k: {} for k in keys}
+    for f in g.files:
+        if f.startswith(prefix):
+            k, n = f[len(prefix):].split("/", 1)
+            sd[k][n] = torch.from_numpy(g[f])
+    return sd
+
+
+def _td3_oracle(g):
+    from oracle.td3bc import StandardScalerT, TD3PlusBCOracle
+    D, A, H, L, B = (int(v) for v in g["cfg"])
+    orc = TD3PlusBCOracle(D, A, n_critics=2, hidden_units=[H] * L,
+                          scaler=StandardScalerT(g["scaler_mean"], g["scaler_std"]), seed=0)
+    for k, v in _td3_from_fixture(g, "init/").items():
+        getattr(orc, k).load_state_dict(v)
+    # fresh Adam state, as in the fixture (built right before its first update)
+    orc._critic_optim = torch.optim.Adam(orc._q_func.parameters(), lr=3e-4)
+    orc._actor_optim = torch.optim.Adam(orc._policy.parameters(), lr=3e-4)
+    return orc, (D, A, H, L, B)
+
+
+def _td3_step_batch(g, step):
+    return [g[f"step{step}/{k}"] for k in ("obs", "act", "rew", "next_obs", "term", "n_steps")]
+
+
+def test_oracle_reproduces_td3bc_fixture():
+    g = _load("td3bc_small.npz")
+    orc, _ = _td3_oracle(g)
+    got = []
+    for step in range(2):
+        m = orc.update(Batch.from_numpy(*_td3_step_batch(g, step)),
+                       torch.from_numpy(g[f"step{step}/noise"]), grad_step=step)
+        got.append([m["critic_loss"], m.get("actor_loss", np.nan)])
+    assert np.array_equal(np.array(got, dtype=np.float32), g["metrics"], equal_nan=True)
+    for k, sd in _td3_from_fixture(g, "final/").items():
+        for n, t in sd.items():
+            assert torch.equal(getattr(orc, k).state_dict()[n], t), (k, n)
+
+
+@pytest.mark.gpu
+def test_hip_td3bc_updates_vs_fixture():
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from cql_helpers import HostBatch
+    from td3_helpers import make_td3_impl
+    g = _load("td3bc_small.npz")
+    D, A, H, L, B = (int(v) for v in g["cfg"])
+    impl = make_td3_impl(D, A, [H] * L, scaler_stats=(g["scaler_mean"], g["scaler_std"]))
+    cr, pr = impl._critic_refs(), impl._policy_refs()
+    from d3rlpy_amd import checkpoint as ckpt
+    init = _td3_from_fixture(g, "init/")
+    ckpt.load_module_state(impl.store, cr, init["_q_func"])
+    ckpt.load_module_state(impl.targ, cr, init["_targ_q_func"])
+    ckpt.load_module_state(impl.store, pr, init["_policy"])
+    ckpt.load_module_state(impl.targ, pr, init["_targ_policy"])
+    for step in range(2):
+        m = impl.update_step(HostBatch(*_td3_step_batch(g, step)), update_actor=step == 0,
+                             noise=g[f"step{step}/noise"])
+        exp = g["metrics"][step]
+        assert abs(m["critic_loss"] - exp[0]) <= 1e-5 * max(1.0, abs(exp[0]))
+        if step == 0:
+            assert abs(m["actor_loss"] - exp[1]) <= 1e-5 * max(1.0, abs(exp[1]))
+    sd = impl.get_state_dict()
+    for k, d in _td3_from_fixture(g, "final/").items():
+        for n, t in d.items():
+            assert float((sd[k][n].view(-1) - t.view(-1)).abs().max()) <= 1e-5, (k, n)

@@ -69,6 +69,61 @@ def test_linear_backward(dev, R, Nin, Nout, C, splits):
     assert _rel_err(dx, ref_dx) < 5e-6
 
 
+@pytest.mark.parametrize("variant", list(range(11)))
+def test_gemm_every_variant(dev, variant):
+    """Every tile variant (LDS-tiled 0-8, register-direct 9-10) on all four
+    operand-layout combinations with row sums, bias, relu, mask and
+    accumulate; fp64 reference, tolerance 5e-6 relative (exact-f32 chains)."""
+    from d3rlpy_amd import ops
+    g = torch.Generator().manual_seed(variant)
+    splits = 1
+    for (M, N, K, batch) in [(256, 256, 256, 2), (37, 70, 300, 1), (130, 6, 11, 3),
+                             (256, 14, 1000, 2)]:
+        for a_k, b_k in [(True, True), (True, False), (False, True), (False, False)]:
+            A = torch.randn(batch, M, K, generator=g).to(dev)
+            Bm = torch.randn(batch, K, N, generator=g).to(dev)
+            # storage: k-contiguous or x-contiguous copies of the same operand
+            As = A.contiguous() if a_k else A.transpose(1, 2).contiguous()
+            Bs = Bm.transpose(1, 2).contiguous() if b_k else Bm.contiguous()
+            sA = (M * K, K, 1) if a_k else (M * K, 1, M)
+            sB = (K * N, 1, K) if b_k else (K * N, N, 1)
+            bias = torch.randn(batch, N, generator=g).to(dev)
+            mask = torch.randn(batch, M, N, generator=g).to(dev)
+            Cb = torch.randn(splits, batch, M, N, generator=g).to(dev)
+            C0 = Cb.clone()
+            rs = torch.zeros(splits, batch, M, device=dev)
+            ops.gemm(As.data_ptr(), Bs.data_ptr(), Cb.data_ptr(), M, N, K, batch=batch, sA=sA,
+                     sB=sB, sC=(M * N, N, 1), splits=splits, sCs=batch * M * N,
+                     bias=bias.data_ptr(), sbias=N, relu=True, mask=mask.data_ptr(),
+                     sM=(M * N, N, 1), accumulate=True, rowsum=rs.data_ptr(), sR=(M, batch * M),
+                     variant=variant)
+            torch.cuda.synchronize()
+            tot = (Cb - C0).double().sum(0)
+            ref = torch.einsum("bmk,bkn->bmn", A.double(), Bm.double()) + bias.double()[:, None]
+            ref = ref.clamp_min(0) * (mask.double() > 0)
+            assert _rel_err(tot, ref) < 5e-6, (variant, M, N, K, a_k, b_k)
+            assert _rel_err(rs[0], A.double().sum(2)) < 5e-6, (variant, M, N, K, a_k, b_k)
+
+
+@pytest.mark.parametrize("variant", list(range(11)))
+def test_gemm_split_k_sum(dev, variant):
+    """Split-K partials (no epilogue) sum to the full product for every variant."""
+    from d3rlpy_amd import ops
+    g = torch.Generator().manual_seed(100 + variant)
+    M, N, K, batch, splits = 256, 256, 7936 // 4, 2, 8
+    A = torch.randn(batch, K, M, generator=g).to(dev)  # dY^T layout: A[m][k] = dY[k][m]
+    X = torch.randn(batch, K, N, generator=g).to(dev)
+    out = torch.zeros(splits, batch, M, N, device=dev)
+    rs = torch.zeros(splits, batch, M, device=dev)
+    ops.gemm(A.data_ptr(), X.data_ptr(), out.data_ptr(), M, N, K, batch=batch,
+             sA=(K * M, 1, M), sB=(K * N, N, 1), sC=(M * N, N, 1), splits=splits,
+             sCs=batch * M * N, rowsum=rs.data_ptr(), sR=(M, batch * M), variant=variant)
+    torch.cuda.synchronize()
+    ref = torch.einsum("bkm,bkn->bmn", A.double(), X.double())
+    assert _rel_err(out.double().sum(0), ref) < 5e-6
+    assert _rel_err(rs.double().sum(0), A.double().sum(1)) < 5e-6
+
+
 def test_rowdot_colreduce_outer(dev):
     from d3rlpy_amd import ops
     g = torch.Generator().manual_seed(3)

@@ -45,23 +45,41 @@ def test_argument_errors_are_reported_without_a_gpu():
         N.check(rc, "d3a_gemm_f32")
 
 
-def test_struct_layouts_match_header():
-    """ctypes structure sizes equal the C sizes compiled into the library's view:
-    field count of each typedef struct in the header == ctypes field count."""
+STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_adam_segment", "AdamSegment"),
+           ("d3a_head1_bwd_desc", "Head1BwdDesc"),
+           ("d3a_cql_sample_desc", "CqlSampleDesc"), ("d3a_cql_loss_desc", "CqlLossDesc"),
+           ("d3a_sac_actor_head_desc", "SacActorHeadDesc"), ("d3a_gather_desc", "GatherDesc"),
+           ("d3a_td3_prep_desc", "Td3PrepDesc"), ("d3a_td3_target_desc", "Td3TargetDesc"),
+           ("d3a_td3_critic_loss_desc", "Td3CriticLossDesc"),
+           ("d3a_td3bc_actor_desc", "Td3bcActorDesc"))
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """Every ctypes descriptor has the C struct's size and field offsets:
+    a small C program compiled with gcc against include/d3rlpy_amd.h prints
+    sizeof / offsetof, compared field by field with the ctypes layout."""
+    import shutil
+    import subprocess
     from d3rlpy_amd import _native as N
-    text = HEADER.read_text()
-    for cname, cls in (("d3a_gemm_desc", N.GemmDesc), ("d3a_adam_segment", N.AdamSegment),
-                       ("d3a_cql_sample_desc", N.CqlSampleDesc),
-                       ("d3a_cql_loss_desc", N.CqlLossDesc),
-                       ("d3a_sac_actor_head_desc", N.SacActorHeadDesc),
-                       ("d3a_gather_desc", N.GatherDesc)):
-        m = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), text, re.S)
-        assert m, cname
-        body = re.sub(r"/\*.*?\*/", "", m.group(1), flags=re.S)
-        n = 0
-        for decl in body.split(";"):
-            decl = decl.strip()
-            if not decl:
-                continue
-            n += decl.count(",") + 1
-        assert n == len(cls._fields_), (cname, n, len(cls._fields_))
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
+    for cname, pyname in STRUCTS:
+        cls = getattr(N, pyname)
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run([cc, str(src), "-o", str(exe)], check=True)
+    out = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True,
+                                                         text=True, check=True).stdout.split("\n")
+               if l)
+    for cname, pyname in STRUCTS:
+        cls = getattr(N, pyname)
+        assert int(out[cname]) == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert int(out[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)
