@@ -61,19 +61,40 @@ def _max_over_ranks(x: float, ws: int) -> float:
     return float(t.item())
 
 
-def build_workload(rank: int, n_transitions: int):
-    from d3rlpy_amd.algos.cql import CQL
+# workload per --algo: (dataset shape name, batch size, algo factory, description)
+WORKLOADS = {
+    "cql": ("hopper-medium-v0", 256,
+            "CQL K2 (configs[1]): obs 11, act 3, batch 256, n_critics 2, n_action_samples 10, "
+            "hidden [256,256], reference defaults"),
+    "td3bc": ("pendulum-random", 100,
+              "TD3+BC K1 (configs[0]) on 1xMI355X: obs 3, act 1, batch 100, n_critics 2, "
+              "actor every 2 steps, standard scaler, hidden [256,256], reference defaults"),
+}
+
+
+def _make_algo(name: str, batch: int):
+    if name == "cql":
+        from d3rlpy_amd.algos.cql import CQL
+        return CQL(batch_size=batch, n_critics=2, n_action_samples=10)
+    from d3rlpy_amd.algos.td3_plus_bc import TD3PlusBC
+    return TD3PlusBC(batch_size=batch)
+
+
+def build_workload(rank: int, n_transitions: int, name: str = "cql"):
     from d3rlpy_amd.dataset import DeviceDataset
     from d3rlpy_amd.datasets import get_synthetic_d4rl
     from d3rlpy_amd.iterators import RandomIterator
-    ds = get_synthetic_d4rl("hopper-medium-v0", n=n_transitions, seed=0)
+    shape, batch, _ = WORKLOADS[name]
+    ds = get_synthetic_d4rl(shape, n=n_transitions, seed=0)
     import torch
     torch.manual_seed(rank)
-    algo = CQL(batch_size=256, n_critics=2, n_action_samples=10)
+    algo = _make_algo(name, batch)
+    if algo.scaler is not None:
+        algo.scaler.fit_dataset(ds)  # as fit() does before building the impl
     algo.build_with_dataset(ds)
     ddata = DeviceDataset(ds)
-    it = RandomIterator(ddata, n_steps_per_epoch=1 << 40, batch_size=256,
-                        out=algo.impl.staging_batch(256), seed=1000 + rank)
+    it = RandomIterator(ddata, n_steps_per_epoch=1 << 40, batch_size=batch,
+                        out=algo.impl.staging_batch(batch), seed=1000 + rank)
     return algo, it
 
 
@@ -81,6 +102,7 @@ def gpu_steps(algo, it, n):
     for _ in range(n):
         batch = next(it)
         algo._update_async(batch)
+        algo._grad_step += 1  # as fit() does (drives TD3+BC's delayed actor)
 
 
 def measure_kernel(ws_obj, reps: int = 50):
@@ -101,28 +123,42 @@ def measure_kernel(ws_obj, reps: int = 50):
     return avg_s, flops, desc
 
 
-def cpu_baseline(seconds: float, threads: int):
-    """The oracle CQL update (torch CPU, op for op) + the reference's host
-    sampler restated (per-sample np.random.randint + TransitionMiniBatch gather)."""
+def cpu_baseline(seconds: float, threads: int, name: str = "cql"):
+    """The oracle update (torch CPU, op for op) + the reference's host sampler
+    restated (per-sample np.random.randint + TransitionMiniBatch gather)."""
     import torch
     from oracle.cql import Batch, CQLNoise, CQLOracle
     from oracle.gather import gather, random_indices, synthetic_dataset, to_episodes, to_transitions
     torch.set_num_threads(threads)
     n = 100_000
-    obs, act, rew, term = synthetic_dataset(n, 11, 3, episode_len=1000, seed=0)
+    D, A = (11, 3) if name == "cql" else (3, 1)
+    B = WORKLOADS[name][1]
+    obs, act, rew, term = synthetic_dataset(n, D, A, episode_len=1000, seed=0)
     trans = []
     for o, a, r, t in to_episodes(obs, act, rew, term):
         trans += to_transitions(o, a, r, t)
-    orc = CQLOracle(11, 3, n_critics=2, n_action_samples=10, seed=0)
     gen = torch.Generator().manual_seed(0)
     np.random.seed(0)
+    if name == "cql":
+        orc = CQLOracle(D, A, n_critics=2, n_action_samples=10, seed=0)
+
+        def update(batch, k):
+            orc.update(batch, CQLNoise.draw(gen, B, A, 10))
+    else:
+        from oracle.td3bc import StandardScalerT, TD3PlusBCOracle, fit_standard_scaler
+        orc = TD3PlusBCOracle(D, A, scaler=StandardScalerT(*fit_standard_scaler(obs)), seed=0)
+
+        def update(batch, k):
+            orc.update(batch, torch.randn(B, A, generator=gen), grad_step=k)
+    cnt = [0]
 
     def step():
-        idx = random_indices(len(trans), 256)
+        idx = random_indices(len(trans), B)
         b = gather([trans[i] for i in idx])
         batch = Batch.from_numpy(b["observations"], b["actions"], b["rewards"],
                                  b["next_observations"], b["terminals"], b["n_steps"])
-        orc.update(batch, CQLNoise.draw(gen, 256, 3, 10))
+        update(batch, cnt[0])
+        cnt[0] += 1
 
     for _ in range(2):
         step()
@@ -144,6 +180,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--transitions", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--algo", choices=sorted(WORKLOADS), default="cql",
+                    help="cql = the BASELINE.json headline (K2); td3bc = K1 shapes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(os.path.dirname(
         os.path.abspath(__file__)), "profiles", "r01_pmc_traffic.json"))
@@ -152,7 +190,7 @@ def main():
     import torch
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     ws, rank, local = _dist_setup()
-    algo, it = build_workload(rank, args.transitions)
+    algo, it = build_workload(rank, args.transitions, args.algo)
 
     gpu_steps(algo, it, args.warmup)
     torch.cuda.synchronize()
@@ -166,9 +204,12 @@ def main():
     elapsed = _max_over_ranks(t1 - t0, ws)
     # sanity: the losses are finite
     names, vals = algo.impl.read_metrics_ring(None)
-    finite = bool(np.isfinite(vals).all())
+    # NaN in a column marks "not computed at this step" (TD3+BC's delayed
+    # actor); every step computes critic_loss
+    ci = names.index("critic_loss")
+    finite = bool(np.isfinite(vals[:, ci]).all() and np.isfinite(vals[~np.isnan(vals)]).all())
 
-    wsp = algo.impl._last_ws()
+    wsp = next(iter(algo.impl._ws.values()))
     kern_s, kflops, kdesc = measure_kernel(wsp)
     if rank != 0:
         if ws > 1:
@@ -188,17 +229,23 @@ def main():
     cpu = None
     if not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        sps, k, el = cpu_baseline(args.cpu_seconds, threads)
+        sps, k, el = cpu_baseline(args.cpu_seconds, threads, args.algo)
+        what = ("CQL update (torch CPU, op-for-op restatement of cql_impl.py/sac_impl.py/"
+                "ddpg_impl.py)" if args.algo == "cql" else
+                "TD3+BC update (torch CPU, op-for-op restatement of td3_plus_bc_impl.py/"
+                "td3_impl.py/ddpg_impl.py, standard scaler)")
         cpu = {"value": round(sps, 3), "unit": "gradient-steps/s", "cores": threads,
                "kind": "port",
-               "sample": f"oracle CQL update (torch CPU, op-for-op restatement of "
-                         f"cql_impl.py/sac_impl.py/ddpg_impl.py) + reference host sampler "
-                         f"restated (np.random.randint per sample + TransitionMiniBatch "
-                         f"gather) on a 100k-transition synthetic dataset; {k} steps in "
-                         f"{el:.1f}s, {threads} threads"}
+               "sample": f"oracle {what} + reference host sampler restated "
+                         f"(np.random.randint per sample + TransitionMiniBatch gather) on a "
+                         f"100k-transition synthetic dataset; {k} steps in {el:.1f}s, "
+                         f"{threads} threads"}
     value = ws * args.steps / elapsed
+    shape, batch, wdesc = WORKLOADS[args.algo]
+    metric = ("gradient-steps/sec (CQL, batch=256, obs=11 act=3) at 1/2/4/8 GPU"
+              if args.algo == "cql" else "gradient-steps/sec (TD3+BC, batch=100, obs=3 act=1)")
     out = {
-        "metric": "gradient-steps/sec (CQL, batch=256, obs=11 act=3) at 1/2/4/8 GPU",
+        "metric": metric,
         "value": round(value, 2),
         "unit": "gradient-steps/s",
         "n_gpus": ws,
@@ -209,10 +256,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (D4RL hopper-medium-v0 shapes, 1M transitions, HBM-resident)",
-        "config": {"workload": "CQL K2 (configs[1]): obs 11, act 3, batch 256, n_critics 2, "
-                               "n_action_samples 10, hidden [256,256], reference defaults",
-                   "global_batch": 256 * ws, "parallelism": f"replicas x{ws}",
+        "data": f"synthetic (D4RL {shape} shapes, {args.transitions} transitions, "
+                "HBM-resident)",
+        "config": {"workload": wdesc,
+                   "global_batch": batch * ws, "parallelism": f"replicas x{ws}",
                    "losses_finite": finite},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak_tflops,
                      "unit": "TFLOP/s", "frac": round(achieved / peak_tflops, 4),

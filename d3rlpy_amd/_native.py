@@ -91,6 +91,7 @@ class CqlLossDesc(C.Structure):
         ("beta1", C.c_double), ("beta2", C.c_double), ("adam_eps", C.c_double),
         ("alpha_threshold", C.c_float), ("conservative_weight", C.c_float),
         ("update_temp", C.c_int32), ("update_alpha", C.c_int32), ("update_critic", C.c_int32),
+        ("dp_phase", C.c_int32), ("scalar_grads", vp), ("grad_scale", C.c_float),
     ]
 
 
@@ -117,7 +118,7 @@ class GatherDesc(C.Structure):
         ("B", C.c_int32),
         ("o_obs", vp), ("o_frames", vp), ("o_act", vp), ("o_act_i", vp),
         ("o_rew", vp), ("o_next_obs", vp), ("o_next_frames", vp),
-        ("o_term", vp), ("o_n_steps", vp),
+        ("o_term", vp), ("o_n_steps", vp), ("row_offset", C.c_int64),
     ]
 
 
@@ -169,10 +170,11 @@ _SIGNATURES = {
     "d3a_outer_mask_f32": (C.c_int, [vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
                                      C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
     "d3a_adam_f32": (C.c_int, [vp, C.c_int32, C.c_int64, vp, C.c_double, C.c_double,
-                               C.c_double, C.c_double, vp]),
+                               C.c_double, C.c_double, C.c_double, vp]),
+    "d3a_grad_reduce_f32": (C.c_int, [vp, C.c_int32, C.c_int64, vp]),
     "d3a_soft_update_f32": (C.c_int, [vp, vp, C.c_int64, C.c_double, vp]),
     "d3a_step_end": (C.c_int, [vp, C.c_int32, vp, C.c_int64, vp, vp, C.c_uint32, vp, vp,
-                               C.c_int64, C.c_double, vp]),
+                               C.c_int64, C.c_double, C.c_float, vp]),
     "d3a_philox_fill": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_float, C.c_float, C.c_uint64,
                                   vp, vp, vp]),
     "d3a_head1_bwd": (C.c_int, [C.POINTER(Head1BwdDesc), vp]),

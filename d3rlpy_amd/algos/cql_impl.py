@@ -108,6 +108,7 @@ class CQLImpl(ImplBase):
         self._min_logstd, self._max_logstd = -20.0, 2.0
         self._built = False
         self._ws: Dict[int, "_Workspace"] = {}
+        self._dp = None
 
     # ------------------------------------------------------------------ build
     def build(self) -> None:
@@ -232,6 +233,19 @@ class CQLImpl(ImplBase):
                 bh[:A].copy_(mu.bias)
                 bh[A:].copy_(ls.bias)
 
+    # ------------------------------------------------------- data parallel
+    def enable_data_parallel(self, dp) -> None:
+        """Average every gradient over the ranks of ``dp`` (d3rlpy_amd.dp,
+        K4): call after build() on every rank, before the first update.
+        Rank 0's parameters are broadcast so all replicas start identical."""
+        if self._ws:
+            raise RuntimeError("enable_data_parallel must precede the first update")
+        self._dp = dp
+        dp.broadcast_(self.store.data)
+        dp.broadcast_(self.targ.data)
+        dp.broadcast_(self.log_temp)
+        dp.broadcast_(self.log_alpha)
+
     # ------------------------------------------------------------- workspace
     def _workspace(self, B: int) -> "_Workspace":
         ws = self._ws.get(B)
@@ -279,6 +293,8 @@ class CQLImpl(ImplBase):
         if not sync:
             return None
         vals = ws.metrics.cpu().numpy()
+        if self._dp is not None:
+            vals = vals * np.float32(self._dp.scale)  # summed over ranks in the pipeline
         return {k: float(v) for k, v in zip(METRIC_NAMES, vals)}
 
     # ------------------------------------------------- device-side batches
@@ -404,6 +420,7 @@ class _Workspace:
         self.dhead = z(B, 2 * A)
         self.metrics = z(len(METRIC_NAMES))
         self.scalars = z(4)
+        self.scalar_grads = z(2)  # data parallel: temp / alpha gradients
         # per-step metric history (read back once per epoch by the fitter)
         self.ring = z(1 << 16, len(METRIC_NAMES))
         self.ring_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -468,6 +485,8 @@ class _Workspace:
         l.beta1, l.beta2, l.adam_eps = tf.betas[0], tf.betas[1], tf.eps
         l.alpha_threshold = impl._alpha_threshold
         l.conservative_weight = impl._conservative_weight
+        l.scalar_grads = self.scalar_grads.data_ptr()
+        l.grad_scale = 1.0 if impl._dp is None else impl._dp.scale
         self.loss_desc = l
 
         h = NAT.SacActorHeadDesc()
@@ -570,10 +589,20 @@ class _Workspace:
             mlp.forward(impl.critic, impl.store, self.x_q.data_ptr(), True, DA, self.qacts, r0, R)
         if critic:
             mlp.forward(impl.critic, impl.targ, self.x_targ.data_ptr(), True, DA, self.tacts)
+        dp = impl._dp
         if temp or alpha or critic:
             l = self.loss_desc
             l.update_temp, l.update_alpha, l.update_critic = int(temp), int(alpha), int(critic)
-            ops.call_desc("d3a_cql_loss", l)
+            if dp is not None and (temp or alpha):
+                # scalar gradients -> all-reduce -> Adam + critic stage
+                l.dp_phase = 1
+                ops.call_desc("d3a_cql_loss", l)
+                dp.all_reduce_sum(self.scalar_grads)
+                l.dp_phase = 2
+                ops.call_desc("d3a_cql_loss", l)
+                l.dp_phase = 0
+            else:
+                ops.call_desc("d3a_cql_loss", l)
         if critic:
             # 5. critic backward on rows [3NB, R) and Adam
             r0 = 3 * NB
@@ -582,7 +611,7 @@ class _Workspace:
             mlp.backward(self.cbwd, impl.store, self.x_q.data_ptr(), True, DA, self.qacts,
                          self.dq.data_ptr() + 4 * r0, 1, R, r0, self.Rc,
                          g_scale=self.scalars.data_ptr() + 8, n_scaled=3 * NB)
-            self.critic_opt.launch()
+            self._apply(self.critic_opt, dp)
         if actor:
             if not (temp or alpha or critic):
                 # scalars[0] = exp(log_temp) is produced by the loss kernel
@@ -599,8 +628,22 @@ class _Workspace:
             ops.call_desc("d3a_sac_actor_head", self.head_desc)
             mlp.backward(self.pbwd, impl.store, self.obs2.data_ptr(), True, D, self.pacts,
                          self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B)
-            self.actor_opt.launch()
+            self._apply(self.actor_opt, dp)
         # 7. soft update of both targets + metric ring + optimiser step counters
+        if dp is not None:
+            dp.all_reduce_sum(self.metrics)  # logged losses: mean over ranks
         ops.step_end(impl.counters, (1 if critic else 0) | (2 if actor else 0), self.metrics,
                      self.ring, self.ring_ctr, impl.targ.data if targets else None,
-                     impl.store.data if targets else None, impl._tau)
+                     impl.store.data if targets else None, impl._tau,
+                     metric_scale=1.0 if dp is None else dp.scale)
+
+    @staticmethod
+    def _apply(opt: AdamGroup, dp) -> None:
+        """Adam; with data parallelism: reduce the split-K partials, SUM
+        all-reduce the one gradient copy, Adam on it scaled by 1/world."""
+        if dp is None:
+            opt.launch()
+            return
+        opt.reduce()
+        dp.all_reduce_sum(opt.grad_span())
+        opt.launch(reduced=True, grad_scale=dp.scale)

@@ -112,6 +112,8 @@ class TD3PlusBCImpl(ImplBase):
         self.actor_state = OptimState(store, self.policy.names(), self._actor_learning_rate,
                                       f.betas, f.eps, step=self.counters[1:2])
         if self._scaler is not None:
+            if self._scaler.mean is None:
+                raise ValueError("the standard scaler is not fitted (fit_dataset / fit)")
             D_ = self._observation_shape[0]
             self.scaler_mean = torch.as_tensor(np.asarray(self._scaler.mean).reshape(D_),
                                                dtype=torch.float32).to(dev)

@@ -169,48 +169,76 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const int64_t B = d.B, C = d.C, N = d.N, NB = N * B;
 
+  // dp_phase 0: compute the scalar gradients and apply Adam here; 1: only
+  // compute them (-> scalar_grads, for the data-parallel all-reduce) and
+  // stop; 2: apply Adam to the all-reduced scalar_grads * grad_scale, then
+  // continue with the critic.
+  const int phase = d.dp_phase;
+
   // ---- update_temp (sac_impl.py:123-146) ----
   if (d.update_temp) {
-    float s = 0.f;
-    for (int64_t b = tid; b < B; b += nt) s += d.logp_temp[b] - (float)d.A;
-    const float tsum = block_sum(s, scratch);
+    float tsum = 0.f;
+    if (phase != 2) {
+      float s = 0.f;
+      for (int64_t b = tid; b < B; b += nt) s += d.logp_temp[b] - (float)d.A;
+      tsum = block_sum(s, scratch);
+    }
     if (tid == 0) {
-      const float e = expf(*d.log_temp);
-      // loss = -(exp(log_temp) * targ_temp).mean()
-      const float loss = -(e * tsum) / (float)B;
-      const float g = (-1.f / (float)B) * tsum * e;
-      const float ln = adam_scalar(d.log_temp, d.temp_m, d.temp_v, d.temp_step, g, d.temp_lr,
-                                   d.beta1, d.beta2, d.adam_eps);
-      d.metrics[0] = loss;
-      d.metrics[1] = expf(ln);
+      float g = 0.f;
+      if (phase != 2) {
+        const float e = expf(*d.log_temp);
+        // loss = -(exp(log_temp) * targ_temp).mean()
+        d.metrics[0] = -(e * tsum) / (float)B;
+        g = (-1.f / (float)B) * tsum * e;
+      }
+      if (phase == 1) {
+        d.scalar_grads[0] = g;
+      } else {
+        if (phase == 2) g = d.scalar_grads[0] * d.grad_scale;
+        const float ln = adam_scalar(d.log_temp, d.temp_m, d.temp_v, d.temp_step, g, d.temp_lr,
+                                     d.beta1, d.beta2, d.adam_eps);
+        d.metrics[1] = expf(ln);
+      }
     }
   }
   __syncthreads();
 
   // ---- update_alpha (cql_impl.py:119-141) on sample set 0 ----
   if (d.update_alpha) {
-    float sl = 0.f, sd = 0.f;
-    for (int64_t p = tid; p < C * B; p += nt) {
-      const int64_t c = p / B, b = p % B;
-      sl += d.lse[c * B + b];
-      sd += d.q[c * d.R + 6 * NB + b];
+    float lsum = 0.f, dsum = 0.f;
+    if (phase != 2) {
+      float sl = 0.f, sd = 0.f;
+      for (int64_t p = tid; p < C * B; p += nt) {
+        const int64_t c = p / B, b = p % B;
+        sl += d.lse[c * B + b];
+        sd += d.q[c * d.R + 6 * NB + b];
+      }
+      lsum = block_sum(sl, scratch);
+      dsum = block_sum(sd, scratch);
     }
-    const float lsum = block_sum(sl, scratch);
-    const float dsum = block_sum(sd, scratch);
     if (tid == 0) {
-      const float loss = lsum / (float)(C * B) - dsum / (float)(C * B);
-      const float scaled = d.conservative_weight * loss;
-      const float e = expf(*d.log_alpha);
-      const float ca = fminf(fmaxf(e, 0.f), 1e6f);
-      const float cons = ca * (scaled - d.alpha_threshold);
-      const bool pass = (e >= 0.f) && (e <= 1e6f);
-      const float g = pass ? -(scaled - d.alpha_threshold) * e : 0.f;
-      const float ln = adam_scalar(d.log_alpha, d.alpha_m, d.alpha_v, d.alpha_step, g,
-                                   d.alpha_lr, d.beta1, d.beta2, d.adam_eps);
-      d.metrics[2] = -cons;
-      d.metrics[3] = expf(ln);
+      float g = 0.f;
+      if (phase != 2) {
+        const float loss = lsum / (float)(C * B) - dsum / (float)(C * B);
+        const float scaled = d.conservative_weight * loss;
+        const float e = expf(*d.log_alpha);
+        const float ca = fminf(fmaxf(e, 0.f), 1e6f);
+        const float cons = ca * (scaled - d.alpha_threshold);
+        const bool pass = (e >= 0.f) && (e <= 1e6f);
+        g = pass ? -(scaled - d.alpha_threshold) * e : 0.f;
+        d.metrics[2] = -cons;
+      }
+      if (phase == 1) {
+        d.scalar_grads[1] = g;
+      } else {
+        if (phase == 2) g = d.scalar_grads[1] * d.grad_scale;
+        const float ln = adam_scalar(d.log_alpha, d.alpha_m, d.alpha_v, d.alpha_step, g,
+                                     d.alpha_lr, d.beta1, d.beta2, d.adam_eps);
+        d.metrics[3] = expf(ln);
+      }
     }
   }
+  if (phase == 1) return;
   __syncthreads();
   if (tid == 0) {
     sh[0] = fminf(fmaxf(expf(*d.log_alpha), 0.f), 1e6f);
@@ -324,7 +352,11 @@ extern "C" int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream) {
   D3A_CHECK_ARG(d, "d3a_cql_loss: null desc");
   D3A_CHECK_ARG(d->R == 6LL * d->N * d->B + d->B, "d3a_cql_loss: R must be 6NB+B");
   D3A_CHECK_ARG(d->lse != nullptr, "d3a_cql_loss: lse workspace required");
-  if (d->update_alpha || d->update_critic) {
+  D3A_CHECK_ARG(d->dp_phase >= 0 && d->dp_phase <= 2, "d3a_cql_loss: bad dp_phase");
+  D3A_CHECK_ARG(d->dp_phase == 0 || d->scalar_grads != nullptr,
+                "d3a_cql_loss: dp_phase needs scalar_grads");
+  // phase 2 reuses the logsumexp / softmax weights phase 1 wrote
+  if ((d->update_alpha || d->update_critic) && d->dp_phase != 2) {
     const int64_t waves = 2LL * d->C * d->B;
     hipLaunchKernelGGL(cql_lse_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, *d);

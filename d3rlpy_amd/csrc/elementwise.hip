@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void outer_mask_kernel(const float* g, int64_t
 // ---- Adam (torch.optim.adam._single_tensor_adam, weight_decay = 0) ---------
 __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
                                                    const int64_t* step, double lr, double beta1,
-                                                   double beta2, double eps) {
+                                                   double beta2, double eps, float grad_scale) {
   __shared__ float s_step_size, s_bc2_sqrt;
   const d3a_adam_segment sg = segs[blockIdx.y];
   const int64_t t = *step + 1;  // read by every block before the last one commits
@@ -133,7 +133,9 @@ __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
   if (i < sg.numel) {
     double gd = 0.0;  // split-K partials summed in a fixed order, in fp64
     for (int64_t q = 0; q < sg.n_partials; ++q) gd += (double)sg.grad[q * sg.partial_stride + i];
-    const float g = (float)gd;
+    // grad_scale: 1, or 1/world after a data-parallel SUM all-reduce (exact
+    // for power-of-two worlds)
+    const float g = grad_scale == 1.f ? (float)gd : __fmul_rn((float)gd, grad_scale);
     if (sg.grad_out) sg.grad_out[i] = g;
     // exp_avg.lerp_(grad, 1 - beta1): weight < 0.5 -> self + w * (end - self)
     // (ATen's vectorised CPU lerp: fmadd(weight, end - self, self))
@@ -153,6 +155,17 @@ __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
     sg.param[i] = pnew;
   }
   // the step counter is committed by d3a_step_end after the update
+}
+
+// ---- split-K partials -> one gradient (the data-parallel path reduces
+// before the all-reduce, so the collective moves one copy, not S partials)
+__global__ __launch_bounds__(256) void grad_reduce_kernel(const d3a_adam_segment* segs) {
+  const d3a_adam_segment sg = segs[blockIdx.y];
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= sg.numel) return;
+  double gd = 0.0;  // same fixed order and fp64 accumulation as adam_kernel
+  for (int64_t q = 0; q < sg.n_partials; ++q) gd += (double)sg.grad[q * sg.partial_stride + i];
+  sg.grad_out[i] = (float)gd;
 }
 
 // ---- soft update: fl(fl(p_t * (1 - tau)) + fl(tau * p)) -------------------
@@ -209,13 +222,14 @@ __global__ __launch_bounds__(256) void step_end_kernel(const float* m, int n, fl
                                                        int64_t cap, int64_t* ctr,
                                                        int64_t* counters, unsigned inc_mask,
                                                        float* targ, const float* src, int64_t ns,
-                                                       float omt, float tau) {
+                                                       float omt, float tau, float mscale) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (targ && i < ns) targ[i] = __fadd_rn(__fmul_rn(targ[i], omt), __fmul_rn(tau, src[i]));
   if (blockIdx.x != 0) return;
   if (ring) {
     const int64_t slot = *ctr % cap;
-    for (int k = threadIdx.x; k < n; k += blockDim.x) ring[slot * n + k] = m[k];
+    for (int k = threadIdx.x; k < n; k += blockDim.x)
+      ring[slot * n + k] = mscale == 1.f ? m[k] : m[k] * mscale;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -232,7 +246,8 @@ using namespace d3a;
 
 extern "C" int d3a_step_end(const float* metrics, int32_t n, float* ring, int64_t cap,
                             int64_t* ring_ctr, int64_t* counters, uint32_t inc_mask, float* targ,
-                            const float* src, int64_t n_soft, double tau, void* stream) {
+                            const float* src, int64_t n_soft, double tau, float metric_scale,
+                            void* stream) {
   D3A_CHECK_ARG(!ring || (metrics && ring_ctr && n > 0 && cap > 0), "d3a_step_end: bad ring");
   D3A_CHECK_ARG(!inc_mask || counters, "d3a_step_end: counters required");
   D3A_CHECK_ARG(!targ || (src && n_soft >= 0), "d3a_step_end: bad soft-update operands");
@@ -240,7 +255,7 @@ extern "C" int d3a_step_end(const float* metrics, int32_t n, float* ring, int64_
   const unsigned blocks = (unsigned)(ns > 0 ? (ns + 255) / 256 : 1);
   hipLaunchKernelGGL(step_end_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, metrics,
                      n, ring, cap, ring_ctr, counters, inc_mask, targ, src, ns,
-                     (float)(1.0 - tau), (float)tau);
+                     (float)(1.0 - tau), (float)tau, metric_scale);
   D3A_LAUNCH_CHECK("d3a_step_end");
   return 0;
 }
@@ -302,14 +317,25 @@ extern "C" int d3a_outer_mask_f32(const float* g, int64_t sgb, const float* w, i
 
 extern "C" int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg, int64_t max_numel,
                             const int64_t* step, double lr, double beta1, double beta2,
-                            double eps, void* stream) {
+                            double eps, double grad_scale, void* stream) {
   D3A_CHECK_ARG(segs && step, "d3a_adam_f32: null pointer");
   D3A_CHECK_ARG(n_seg > 0 && n_seg < 65536, "d3a_adam_f32: bad segment count");
   D3A_CHECK_ARG(max_numel > 0, "d3a_adam_f32: bad max_numel");
   dim3 grid((unsigned)((max_numel + 255) / 256), (unsigned)n_seg);
   hipLaunchKernelGGL(adam_kernel, grid, dim3(256), 0, (hipStream_t)stream, segs, step, lr, beta1,
-                     beta2, eps);
+                     beta2, eps, (float)grad_scale);
   D3A_LAUNCH_CHECK("d3a_adam_f32");
+  return 0;
+}
+
+extern "C" int d3a_grad_reduce_f32(const d3a_adam_segment* segs, int32_t n_seg,
+                                   int64_t max_numel, void* stream) {
+  D3A_CHECK_ARG(segs, "d3a_grad_reduce_f32: null pointer");
+  D3A_CHECK_ARG(n_seg > 0 && n_seg < 65536, "d3a_grad_reduce_f32: bad segment count");
+  D3A_CHECK_ARG(max_numel > 0, "d3a_grad_reduce_f32: bad max_numel");
+  dim3 grid((unsigned)((max_numel + 255) / 256), (unsigned)n_seg);
+  hipLaunchKernelGGL(grad_reduce_kernel, grid, dim3(256), 0, (hipStream_t)stream, segs);
+  D3A_LAUNCH_CHECK("d3a_grad_reduce_f32");
   return 0;
 }
 

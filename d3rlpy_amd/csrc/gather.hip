@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
       t = d.idx[b];
     } else {
       uint32_t r[4];
-      Philox::gen(d.seed, (uint64_t)(*d.ctr), (uint64_t)b, r);
+      Philox::gen(d.seed, (uint64_t)(*d.ctr), (uint64_t)(d.row_offset + b), r);
       const uint64_t x = ((uint64_t)r[0] << 32) | r[1];
       t = (int64_t)(x % (uint64_t)d.n_trans);
       d.idx_out[b] = t;

@@ -321,10 +321,12 @@ class DeviceDataset:
 
     def gather(self, out, indices: Optional[torch.Tensor] = None, n_steps: int = 1,
                gamma: float = 0.99, n_frames: int = 1, seed: int = 0,
-               idx_out: Optional[torch.Tensor] = None) -> None:
+               idx_out: Optional[torch.Tensor] = None, row_offset: int = 0) -> None:
         """Fill ``out`` (DeviceBatch) with the transitions ``indices`` (device
         int64), or with indices drawn on device (Philox, ``seed``, advancing
-        this dataset's sampler counter) when ``indices`` is None."""
+        this dataset's sampler counter) when ``indices`` is None; drawn row b
+        is draw ``row_offset + b`` of the step (a data-parallel shard of one
+        global index stream)."""
         from . import _native as N
         from . import ops
         B = out.batch_size
@@ -353,6 +355,7 @@ class DeviceDataset:
             d.seed = C.c_uint64(seed & 0xFFFFFFFFFFFFFFFF).value
             d.ctr = ops.ptr(self.ctr)
             d.ticket = ops.ptr(self.ticket)
+            d.row_offset = row_offset
         d.B = B
         if self.is_image:
             d.o_frames, d.o_next_frames = ops.ptr(out.obs), ops.ptr(out.next_obs)

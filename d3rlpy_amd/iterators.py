@@ -20,7 +20,7 @@ Index streams:
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import Tuple, Optional
 
 import numpy as np
 import torch
@@ -87,9 +87,16 @@ class RandomIterator(TransitionIterator):
     def __init__(self, dataset: DeviceDataset, n_steps_per_epoch: int, batch_size: int,
                  n_steps: int = 1, gamma: float = 0.99, n_frames: int = 1,
                  real_ratio: float = 1.0, generated_maxlen: int = 100000,
-                 index_source: str = "device", seed: Optional[int] = None, out=None):
+                 index_source: str = "device", seed: Optional[int] = None, out=None,
+                 shard: Tuple[int, int] = (0, 1)):
+        """``shard=(rank, world)``: this learner's slice [rank*B, (rank+1)*B)
+        of one global stream of world*B indices per step (every rank must use
+        the same ``seed``) — the data-parallel sampler of SURVEY §8e."""
         super().__init__(dataset, batch_size, n_steps, gamma, n_frames, real_ratio,
                          generated_maxlen, out)
+        self._rank, self._world = int(shard[0]), int(shard[1])
+        if not 0 <= self._rank < self._world:
+            raise ValueError("shard must be (rank, world) with 0 <= rank < world")
         self._n_steps_per_epoch = n_steps_per_epoch
         if index_source not in ("device", "numpy"):
             raise ValueError("index_source must be 'device' or 'numpy'")
@@ -100,12 +107,14 @@ class RandomIterator(TransitionIterator):
     def _gather(self, out) -> None:
         if self._index_source == "numpy":
             idx = np.array([np.random.randint(len(self._dataset))
-                            for _ in range(self._batch_size)], dtype=np.int64)
+                            for _ in range(self._batch_size * self._world)], dtype=np.int64)
+            idx = idx[self._rank * self._batch_size:(self._rank + 1) * self._batch_size]
             self.indices.copy_(torch.from_numpy(idx), non_blocking=False)
             self._dataset.gather(out, self.indices, self._n_steps, self._gamma, self._n_frames)
         else:
             self._dataset.gather(out, None, self._n_steps, self._gamma, self._n_frames,
-                                 seed=self._seed, idx_out=self.indices)
+                                 seed=self._seed, idx_out=self.indices,
+                                 row_offset=self._rank * self._batch_size)
 
     def _has_finished(self) -> bool:
         return self._count >= self._n_steps_per_epoch

@@ -204,11 +204,40 @@ class AdamGroup:
         raw = bytes(segs)
         self.seg_table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
         self._segs = segs
+        self.seg_table_reduced = None
+        if self.grad_store is not None:
+            # the same segments reading the already-reduced gradient (one
+            # partial) from grad_store: the data-parallel path's Adam
+            red = (N.AdamSegment * len(self.names))()
+            for i, n in enumerate(self.names):
+                red[i].param, red[i].exp_avg = segs[i].param, segs[i].exp_avg
+                red[i].exp_avg_sq = segs[i].exp_avg_sq
+                red[i].grad = self.grad_store.ptr(n)
+                red[i].numel, red[i].n_partials = segs[i].numel, 1
+                red[i].partial_stride = segs[i].numel
+                red[i].grad_out = None
+            self.seg_table_reduced = torch.frombuffer(bytearray(bytes(red)),
+                                                      dtype=torch.uint8).to(dev)
 
-    def launch(self) -> None:
+    def launch(self, reduced: bool = False, grad_scale: float = 1.0) -> None:
+        """Adam over every segment; ``reduced``: from grad_store (after
+        ``reduce`` and an all-reduce) scaled by ``grad_scale``."""
         from . import ops
-        ops.adam(self.seg_table, len(self.names), self.max_numel, self.step,
-                 self.lr, self.beta1, self.beta2, self.eps)
+        table = self.seg_table_reduced if reduced else self.seg_table
+        assert table is not None
+        ops.adam(table, len(self.names), self.max_numel, self.step,
+                 self.lr, self.beta1, self.beta2, self.eps, grad_scale)
+
+    def reduce(self) -> None:
+        """grad_store <- sum of the split-K partials (no parameter update)."""
+        from . import ops
+        assert self.grad_store is not None
+        ops.grad_reduce(self.seg_table, len(self.names), self.max_numel)
+
+    def grad_span(self) -> torch.Tensor:
+        """The contiguous slice of grad_store holding this group's gradients."""
+        s, e = self.store.span(self.names)
+        return self.grad_store.data[s:e]
 
     def grad(self, name: str) -> torch.Tensor:
         assert self.grad_store is not None

@@ -83,15 +83,20 @@ def outer_mask(g: int, sgb: int, w: int, swb: int, h: int, shb: int, out: int, s
 
 
 def adam(segs: torch.Tensor, n_seg: int, max_numel: int, step: torch.Tensor, lr: float,
-         beta1: float, beta2: float, eps: float) -> None:
+         beta1: float, beta2: float, eps: float, grad_scale: float = 1.0) -> None:
     N.check(N.lib().d3a_adam_f32(ptr(segs), n_seg, max_numel, ptr(step), lr, beta1, beta2, eps,
-                                 _stream()), "d3a_adam_f32")
+                                 grad_scale, _stream()), "d3a_adam_f32")
+
+
+def grad_reduce(segs: torch.Tensor, n_seg: int, max_numel: int) -> None:
+    N.check(N.lib().d3a_grad_reduce_f32(ptr(segs), n_seg, max_numel, _stream()),
+            "d3a_grad_reduce_f32")
 
 
 def step_end(counters: Optional[torch.Tensor], inc_mask: int, metrics: Optional[torch.Tensor] = None,
              ring: Optional[torch.Tensor] = None, ring_ctr: Optional[torch.Tensor] = None,
              targ: Optional[torch.Tensor] = None, src: Optional[torch.Tensor] = None,
-             tau: float = 0.0) -> None:
+             tau: float = 0.0, metric_scale: float = 1.0) -> None:
     """Soft target update (optional) + metric ring push + step counters, one launch."""
     n = metrics.numel() if metrics is not None else 0
     cap = ring.shape[0] if ring is not None else 0
@@ -99,7 +104,8 @@ def step_end(counters: Optional[torch.Tensor], inc_mask: int, metrics: Optional[
     if targ is not None:
         assert src is not None and src.numel() == ns
     N.check(N.lib().d3a_step_end(ptr(metrics), n, ptr(ring), cap, ptr(ring_ctr), ptr(counters),
-                                 inc_mask, ptr(targ), ptr(src), ns, float(tau), _stream()),
+                                 inc_mask, ptr(targ), ptr(src), ns, float(tau),
+                                 float(metric_scale), _stream()),
             "d3a_step_end")
 
 

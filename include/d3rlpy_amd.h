@@ -140,11 +140,19 @@ typedef struct d3a_adam_segment {
  *   m = lerp(m, g, 1-b1); v = v*b2 + (1-b2)*g*g; t = *step + 1
  *   p += -(lr/(1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
  * `segs` is a DEVICE array of n_seg segments.  *step (device int64, the
- * optimiser's completed steps) is only read; commit it with d3a_step_end. */
+ * optimiser's completed steps) is only read; commit it with d3a_step_end.
+ * The reduced gradient is multiplied by grad_scale (1, or 1/world after a
+ * data-parallel SUM all-reduce). */
 int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg,
                  int64_t max_numel, const int64_t* step,
                  double lr, double beta1, double beta2, double eps,
-                 void* stream);
+                 double grad_scale, void* stream);
+
+/* grad_out = sum of the n_partials split-K partials of each segment (fp64
+ * accumulation, same order as d3a_adam_f32) — the data-parallel path's
+ * reduction before the gradient all-reduce. */
+int d3a_grad_reduce_f32(const d3a_adam_segment* segs, int32_t n_seg,
+                        int64_t max_numel, void* stream);
 
 /* soft_sync (d3rlpy/torch_utility.py:27-33): targ = targ*(1-tau) + tau*src,
  * three separately rounded fp32 ops (mul_, tau*p, add_), bit-exact. */
@@ -157,11 +165,13 @@ int d3a_soft_update_f32(float* targ, const float* src, int64_t n, double tau,
  * (2) when ring != NULL append metrics[0:n] to ring[(*ring_ctr % cap)] and
  * increment *ring_ctr (per-step loss history kept on device and read once per
  * epoch instead of one device->host sync per update, cf. base.py:645-657);
- * (3) increment counters[i] for every bit i of inc_mask (optimiser steps). */
+ * (3) increment counters[i] for every bit i of inc_mask (optimiser steps).
+ * Ring entries are metrics * metric_scale (1, or 1/world for metrics summed
+ * over data-parallel ranks). */
 int d3a_step_end(const float* metrics, int32_t n, float* ring, int64_t cap,
                  int64_t* ring_ctr, int64_t* counters, uint32_t inc_mask,
                  float* targ, const float* src, int64_t n_soft, double tau,
-                 void* stream);
+                 float metric_scale, void* stream);
 
 /* ---- random numbers ----------------------------------------------------- */
 
@@ -235,6 +245,12 @@ typedef struct d3a_cql_loss_desc {
   double temp_lr, alpha_lr, beta1, beta2, adam_eps;
   float alpha_threshold, conservative_weight;
   int32_t update_temp, update_alpha, update_critic;
+  /* data parallel (K4): 0 = single device; 1 = write the temp /
+   * alpha gradients to scalar_grads[0:2] and stop; 2 = Adam on the
+   * all-reduced scalar_grads * grad_scale, then the critic stage */
+  int32_t dp_phase;
+  float* scalar_grads;
+  float grad_scale;
 } d3a_cql_loss_desc;
 int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream);
 
@@ -292,6 +308,9 @@ typedef struct d3a_gather_desc {
   float* o_act; int32_t* o_act_i;
   float* o_rew; float* o_next_obs; uint8_t* o_next_frames;
   float* o_term; float* o_n_steps;
+  /* drawn indices: row b takes draw number row_offset + b of the step, so
+   * data-parallel ranks slice one global index stream */
+  int64_t row_offset;
 } d3a_gather_desc;
 int d3a_gather_batch(const d3a_gather_desc* d, void* stream);
 
