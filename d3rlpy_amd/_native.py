@@ -157,6 +157,38 @@ class Td3bcActorDesc(C.Structure):
     ]
 
 
+MLP_MAX_HIDDEN = 4
+
+
+class MlpFwdDesc(C.Structure):
+    _fields_ = [
+        ("x", vp), ("ldx", C.c_int64), ("sxb", C.c_int64),
+        ("n_in", C.c_int32), ("n_hidden", C.c_int32), ("H", C.c_int32), ("n_out", C.c_int32),
+        ("W", vp * (MLP_MAX_HIDDEN + 1)), ("b", vp * (MLP_MAX_HIDDEN + 1)),
+        ("sW", C.c_int64 * (MLP_MAX_HIDDEN + 1)), ("sb", C.c_int64 * (MLP_MAX_HIDDEN + 1)),
+        ("h", vp * MLP_MAX_HIDDEN), ("sh", C.c_int64),
+        ("out", vp), ("sout", C.c_int64), ("ldout", C.c_int64),
+        ("r0", C.c_int64), ("rows", C.c_int64),
+        ("C", C.c_int32), ("block_rows", C.c_int32),
+    ]
+
+
+class MlpBwdDesc(C.Structure):
+    _fields_ = [
+        ("n_in", C.c_int32), ("n_hidden", C.c_int32), ("H", C.c_int32), ("n_out", C.c_int32),
+        ("C", C.c_int32),
+        ("W", vp * (MLP_MAX_HIDDEN + 1)), ("sW", C.c_int64 * (MLP_MAX_HIDDEN + 1)),
+        ("h", vp * MLP_MAX_HIDDEN), ("sh", C.c_int64), ("ldh", C.c_int64),
+        ("g", vp), ("sgb", C.c_int64), ("gscale", vp), ("n_scaled", C.c_int64),
+        ("q_min", vp), ("sqb", C.c_int64), ("scale", C.c_float),
+        ("g_eff", vp), ("sgeb", C.c_int64),
+        ("dhead", vp), ("sdhb", C.c_int64), ("lddh", C.c_int64),
+        ("dz", vp * MLP_MAX_HIDDEN), ("sdz", C.c_int64),
+        ("dx", vp), ("sdxb", C.c_int64), ("lddx", C.c_int64),
+        ("rows", C.c_int64), ("block_rows", C.c_int32),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "d3a_abi_version": (C.c_int, []),
@@ -183,6 +215,8 @@ _SIGNATURES = {
     "d3a_sac_actor_dq": (C.c_int, [vp, C.c_int64, C.c_int32, C.c_int32, vp, C.c_int64, vp]),
     "d3a_sac_actor_head": (C.c_int, [C.POINTER(SacActorHeadDesc), vp]),
     "d3a_gather_batch": (C.c_int, [C.POINTER(GatherDesc), vp]),
+    "d3a_mlp_fwd": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
+    "d3a_mlp_bwd": (C.c_int, [C.POINTER(MlpBwdDesc), vp]),
     "d3a_td3_prep": (C.c_int, [C.POINTER(Td3PrepDesc), vp]),
     "d3a_td3_target": (C.c_int, [C.POINTER(Td3TargetDesc), vp]),
     "d3a_td3_critic_loss": (C.c_int, [C.POINTER(Td3CriticLossDesc), vp]),

@@ -535,14 +535,21 @@ class _Workspace:
 
     # ------------------------------------------------------------ roofline
     def dominant_kernel(self):
-        """(launch_fn, flops_per_launch, description) of the critic hidden-layer
-        forward GEMM over all Q rows of the step (the MFMA-bound hot kernel):
-        C x R x H x H MACs, R = 6NB+B (update_alpha on) rows."""
+        """(launch_fn, flops_per_launch, description) of the MFMA-bound hot
+        kernel: the critic-ensemble forward over all R = 6NB+B Q rows of the
+        step (update_alpha on) — one d3a_mlp_fwd launch (every layer + head),
+        or its hidden-layer GEMM when the per-layer path is in use."""
         impl = self.impl
         net, st = impl.critic, impl.store
-        H = net.sizes[2]
-        Hin = net.sizes[1]
-        R, C = self.R, self.C
+        s = net.sizes
+        R, C, DA = self.R, self.C, self.LDX
+        if mlp.fused_ok(net, R):
+            def launch():
+                mlp.forward(net, st, self.x_q.data_ptr(), True, DA, self.qacts)
+            flops = 2 * C * R * sum(s[l] * s[l + 1] for l in range(len(s) - 1))
+            return launch, flops, (f"d3a_mlp_fwd critic ensemble: C={C} x {R} rows x "
+                                   f"{'-'.join(map(str, s))}")
+        H, Hin = s[2], s[1]
         h0, h1 = self.qacts.h[0], self.qacts.h[1]
 
         def launch():
@@ -588,7 +595,8 @@ class _Workspace:
             r0 = 0 if alpha else 3 * NB
             mlp.forward(impl.critic, impl.store, self.x_q.data_ptr(), True, DA, self.qacts, r0, R)
         if critic:
-            mlp.forward(impl.critic, impl.targ, self.x_targ.data_ptr(), True, DA, self.tacts)
+            mlp.forward(impl.critic, impl.targ, self.x_targ.data_ptr(), True, DA, self.tacts,
+                        keep_h=False)
         dp = impl._dp
         if temp or alpha or critic:
             l = self.loss_desc

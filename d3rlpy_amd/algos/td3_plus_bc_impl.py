@@ -375,11 +375,19 @@ class _Workspace:
             self.noise.copy_(torch.as_tensor(np.asarray(noise), dtype=torch.float32).view(-1))
 
     def dominant_kernel(self):
-        """Critic hidden-layer forward GEMM over the B data rows (C x B x H x H)."""
+        """The critic-ensemble forward over the B data rows (one d3a_mlp_fwd
+        launch, or the hidden-layer GEMM on the per-layer path)."""
         impl = self.impl
         net, st = impl.critic, impl.store
-        Hin, H = net.sizes[1], net.sizes[2]
+        s = net.sizes
         B, C = self.B, self.C
+        if mlp.fused_ok(net, B):
+            def launch():
+                mlp.forward(net, st, self.x_q.data_ptr(), True, self.LDX, self.qacts)
+            flops = 2 * C * B * sum(s[l] * s[l + 1] for l in range(len(s) - 1))
+            return launch, flops, (f"d3a_mlp_fwd critic ensemble: C={C} x {B} rows x "
+                                   f"{'-'.join(map(str, s))}")
+        Hin, H = s[1], s[2]
         h0, h1 = self.qacts.h[0], self.qacts.h[1]
 
         def launch():
@@ -415,10 +423,12 @@ class _Workspace:
                 ops.philox_fill(self.noise, B * A, 0, -1.0, 1.0, self.seed, self.rng_ctr,
                                 self.rng_ticket)
             # target action: targ_policy(s') + clipped noise (td3_impl.py:61-78)
-            mlp.forward(impl.policy, tg, self.x_targ.data_ptr(), True, LDX, self.tpacts)
+            mlp.forward(impl.policy, tg, self.x_targ.data_ptr(), True, LDX, self.tpacts,
+                        keep_h=False)
             ops.call_desc("d3a_td3_target", self.target_desc)
             mlp.forward(impl.critic, st, self.x_q.data_ptr(), True, LDX, self.qacts)
-            mlp.forward(impl.critic, tg, self.x_targ.data_ptr(), True, LDX, self.tacts)
+            mlp.forward(impl.critic, tg, self.x_targ.data_ptr(), True, LDX, self.tacts,
+                        keep_h=False)
             self.loss_desc.actor_step = int(actor)
             ops.call_desc("d3a_td3_critic_loss", self.loss_desc)
             mlp.backward(self.cbwd, st, self.x_q.data_ptr(), True, LDX, self.qacts,

@@ -17,6 +17,7 @@ order inside the Adam kernel), so every reduction is deterministic.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -50,11 +51,36 @@ class Acts:
         return Acts(hs, out, R)
 
 
+# one-launch forward (d3a_mlp_fwd) unless D3A_FUSED_MLP=0 (per-layer GEMMs,
+# kept for A/B measurement and as the path for shapes the fused kernel rejects)
+_FUSED = os.environ.get("D3A_FUSED_MLP", "1") != "0"
+
+
+# below this many rows x members the per-layer GEMMs win: a fused workgroup
+# computes every output column of its rows on one CU, so small passes leave
+# most CUs idle (measured: 100-512-row passes 10-60 % slower fused, the
+# 2 x 15616-row critic pass 12 % faster: 72 vs 82 us)
+FUSED_MIN_ROWS = int(os.environ.get("D3A_FUSED_MIN_ROWS", "4096"))
+# the fused backward-data kernel is opt-in: its weight operand is read across
+# rows (four loads per lane per 8 k) and it measured 67 us against 52 us for
+# the per-layer head backward + input-gradient GEMM on the K2 critic pass
+_FUSED_BWD = os.environ.get("D3A_FUSED_BWD", "0") == "1"
+
+
+def fused_ok(net: EnsembleMLP, rows: Optional[int] = None, backward: bool = False) -> bool:
+    hidden = net.sizes[1:-1]
+    return (_FUSED and 1 <= len(hidden) <= N.MLP_MAX_HIDDEN and len(set(hidden)) == 1
+            and hidden[0] % 32 == 0 and 32 <= hidden[0] <= 256 and net.sizes[0] <= 256
+            and net.sizes[-1] <= (64 if backward else 1024)
+            and (rows is None or rows * net.C >= FUSED_MIN_ROWS))
+
+
 def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: int, acts: Acts,
             r0: int = 0, r1: Optional[int] = None, sxb: Optional[int] = None,
-            members: Optional[int] = None) -> None:
+            members: Optional[int] = None, keep_h: bool = True) -> None:
     """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
-    (through its first ``members`` members only, when given)."""
+    (through its first ``members`` members only, when given).  ``keep_h``:
+    store the hidden activations in ``acts.h`` (needed by a backward pass)."""
     R = acts.R
     r1 = R if r1 is None else r1
     n = r1 - r0
@@ -62,6 +88,23 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         return
     C = net.C if members is None else members
     sizes = net.sizes
+    if fused_ok(net, n * C // net.C):
+        d = N.MlpFwdDesc()
+        d.x, d.ldx = x, ldx
+        d.sxb = (0 if x_shared else R * ldx) if sxb is None else sxb
+        L = net.n_layers
+        d.n_in, d.n_hidden, d.H, d.n_out = sizes[0], L - 1, sizes[1], sizes[-1]
+        for l in range(L):
+            d.W[l], d.b[l] = net.W(l, store), net.b(l, store)
+            d.sW[l], d.sb[l] = sizes[l + 1] * sizes[l], sizes[l + 1]
+        for l in range(L - 1):
+            d.h[l] = acts.h[l].data_ptr() if keep_h else None
+        d.sh = R * sizes[1]
+        d.out = acts.out.data_ptr()
+        d.sout, d.ldout = R * sizes[-1], sizes[-1]
+        d.r0, d.rows, d.C = r0, n, C
+        ops.call_desc("d3a_mlp_fwd", d)
+        return
     L = net.n_layers
     inp, ld_in = x + 4 * r0 * ldx, ldx
     sxb_ = (0 if x_shared else R * ldx) if sxb is None else sxb
@@ -94,7 +137,13 @@ class BackwardSpace:
         if len(set(hidden)) > 1:
             raise NotImplementedError("hidden layers of unequal width are not supported")
         Hmax = hidden[0] if hidden else 1
-        self.dz = [torch.zeros(net.C, rows, Hmax, device=device) for _ in range(2)]
+        self.fused = _FUSED_BWD and fused_ok(net, rows, backward=True)
+        # fused path: one dz buffer per hidden layer (written by d3a_mlp_bwd,
+        # read by the weight-gradient GEMMs) + the effective head gradient;
+        # per-layer path: two ping-pong buffers
+        n_dz = len(hidden) if self.fused else 2
+        self.dz = [torch.zeros(net.C, rows, Hmax, device=device) for _ in range(max(2, n_dz))]
+        self.g_eff = torch.zeros(net.C, rows, device=device) if self.fused else None
         self.splits = n_splits(rows) if splits is None else splits
         self.grads = grads
         if grads is not None:
@@ -127,6 +176,10 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
     assert n <= bs.rows
     sxb_ = (0 if x_shared else R * ldx) if sxb is None else sxb
     gs = bs.grads
+    if bs.fused:
+        _backward_fused(bs, store, x, ldx, sxb_, acts, dout, ld_dout, sdout_b, r0, n,
+                        weight_grads, dx, q_min, sq_b, q_scale, g_out, g_scale, n_scaled, C)
+        return
 
     def h_ptr(l):  # input activation of layer l at row r0
         if l == 0:
@@ -197,3 +250,60 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
             ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(0, store), dx.data_ptr(), Hin,
                              n * Hin, C, n, Hin, Hout)
 
+
+
+def _backward_fused(bs: BackwardSpace, store: ParamStore, x: int, ldx: int, sxb: int, acts: Acts,
+                    dout: int, ld_dout: int, sdout_b: int, r0: int, n: int, weight_grads: bool,
+                    dx: Optional[torch.Tensor], q_min: Optional[int], sq_b: int, q_scale: float,
+                    g_out: Optional[int], g_scale: Optional[int], n_scaled: int, C: int) -> None:
+    """d3a_mlp_bwd (the dz chain and dx in one launch) + one split-K weight
+    gradient GEMM per layer (with the bias gradient as its row sums)."""
+    net = bs.net
+    L, sizes, R = net.n_layers, net.sizes, acts.R
+    H, J = sizes[1], sizes[-1]
+    rows = bs.rows
+    d = N.MlpBwdDesc()
+    d.n_in, d.n_hidden, d.H, d.n_out, d.C = sizes[0], L - 1, H, J, C
+    for l in range(L):
+        d.W[l], d.sW[l] = net.W(l, store), sizes[l + 1] * sizes[l]
+    for l in range(L - 1):
+        d.h[l] = acts.h[l].data_ptr() + 4 * r0 * H
+        d.dz[l] = bs.dz[l].data_ptr()
+    d.sh, d.ldh, d.sdz = R * H, H, rows * H
+    if J == 1:
+        if q_min is not None:
+            d.q_min, d.sqb, d.scale = q_min, sq_b, q_scale
+        else:
+            d.g, d.sgb = dout, sdout_b
+            if g_scale is not None:
+                d.gscale, d.n_scaled = g_scale, n_scaled
+        if g_out is not None:  # caller wants the effective row gradient (e.g. argmin mask)
+            assert not weight_grads
+            d.g_eff, d.sgeb = g_out, sdout_b
+        else:
+            d.g_eff, d.sgeb = bs.g_eff.data_ptr(), rows
+    else:
+        d.dhead, d.sdhb, d.lddh = dout, sdout_b, ld_dout
+    if dx is not None:
+        d.dx, d.sdxb, d.lddx = dx.data_ptr(), n * sizes[0], sizes[0]
+    d.rows = n
+    ops.call_desc("d3a_mlp_bwd", d)
+    if not weight_grads:
+        return
+    gs, S = bs.grads, bs.splits
+    hin_last = acts.h[L - 2].data_ptr() + 4 * r0 * H
+    gW, gb = gs.get(net.wname(L - 1)), gs.get(net.bname(L - 1))
+    if J == 1:
+        ops.linear_bwd_w(bs.g_eff.data_ptr(), 1, rows, hin_last, H, R * H, gW.data_ptr(), C, n,
+                         H, 1, S, db=gb.data_ptr())
+    else:
+        ops.linear_bwd_w(dout, ld_dout, sdout_b, hin_last, H, R * H, gW.data_ptr(), C, n, H, J,
+                         S, db=gb.data_ptr())
+    for l in range(L - 2, -1, -1):
+        if l == 0:
+            hin, ld_h, sh = x + 4 * r0 * ldx, ldx, sxb
+        else:
+            hin, ld_h, sh = acts.h[l - 1].data_ptr() + 4 * r0 * H, H, R * H
+        gW, gb = gs.get(net.wname(l)), gs.get(net.bname(l))
+        ops.linear_bwd_w(bs.dz[l].data_ptr(), H, rows * H, hin, ld_h, sh, gW.data_ptr(), C, n,
+                         sizes[l], H, S, db=gb.data_ptr())

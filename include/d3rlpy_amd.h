@@ -119,6 +119,62 @@ typedef struct d3a_head1_bwd_desc {
 } d3a_head1_bwd_desc;
 int d3a_head1_bwd(const d3a_head1_bwd_desc* desc, void* stream);
 
+/* Whole-MLP forward, one launch (replaces the per-layer nn.Linear + ReLU
+ * chain of VectorEncoder / VectorEncoderWithAction, encoders.py:265-275,
+ * 328-339, and the linear head: mean_q_function.py:255-256 `_fc`,
+ * policies.py:57-59 / 170-176).  Per member c < C, rows r in [r0, r0+rows):
+ *   a_0 = x[c*sxb + r*ldx + 0:n_in]
+ *   a_l = relu(a_{l-1} W_{l-1}^T + b_{l-1}),  l = 1..n_hidden   (width H)
+ *   out[c*sout + r*ldout + j] = a_{n_hidden} . W_head[j] + b_head[j]
+ * W[l] row-major [out][in] (member stride sW[l]), W[n_hidden] is the head
+ * (16-byte aligned).  h[l] (optional) receives a_{l+1} as [C][R][H] (member
+ * stride sh, absolute row index) for the backward pass.  Activations stay in
+ * LDS between layers; block_rows (0 = automatic, 32 or 64) rows per
+ * workgroup.  Heads wider than 64 (quantile heads) run on MFMA as well. */
+#define D3A_MLP_MAX_HIDDEN 4
+typedef struct d3a_mlp_fwd_desc {
+  const float* x; int64_t ldx, sxb;
+  int32_t n_in, n_hidden, H, n_out;
+  const float* W[D3A_MLP_MAX_HIDDEN + 1];
+  const float* b[D3A_MLP_MAX_HIDDEN + 1];
+  int64_t sW[D3A_MLP_MAX_HIDDEN + 1], sb[D3A_MLP_MAX_HIDDEN + 1];
+  float* h[D3A_MLP_MAX_HIDDEN]; int64_t sh;
+  float* out; int64_t sout, ldout;
+  int64_t r0, rows;
+  int32_t C, block_rows;
+} d3a_mlp_fwd_desc;
+int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);
+
+/* Backward-data of the same MLP, one launch (the autograd backward of the
+ * encoder / head chain up to the weight gradients).  Rows r < rows of each
+ * member c (all row pointers already at the first row):
+ *   head, n_out == 1:  g_eff = g (* *gscale for r < n_scaled), or with
+ *                      q_min: `scale` on the first argmin member of
+ *                      q_min[.][r] (backward of min over the ensemble,
+ *                      sac_impl.py:114-121), 0 on the others; stored to
+ *                      g_eff when given;  dz_{L-1} = g_eff w_head * [h > 0]
+ *   head, n_out > 1:   dz_{L-1} = dhead W_head * [h_{L-1} > 0]
+ *   trunk:             dz_{l-1} = dz_l W_l * [h_{l-1} > 0]
+ *   input (dx given):  dx = dz_0 W_0
+ * dz[l] is [C][rows][H] (member stride sdz); h[l] the forward activations
+ * (member stride sh, row stride ldh).  Weight gradients are not formed here:
+ * they are split-K GEMMs over all rows (d3a_gemm_f32 with row sums). */
+typedef struct d3a_mlp_bwd_desc {
+  int32_t n_in, n_hidden, H, n_out, C;
+  const float* W[D3A_MLP_MAX_HIDDEN + 1];
+  int64_t sW[D3A_MLP_MAX_HIDDEN + 1];
+  const float* h[D3A_MLP_MAX_HIDDEN]; int64_t sh, ldh;
+  const float* g; int64_t sgb; const float* gscale; int64_t n_scaled;
+  const float* q_min; int64_t sqb; float scale;
+  float* g_eff; int64_t sgeb;
+  const float* dhead; int64_t sdhb, lddh;
+  float* dz[D3A_MLP_MAX_HIDDEN]; int64_t sdz;
+  float* dx; int64_t sdxb, lddx;
+  int64_t rows;
+  int32_t block_rows;
+} d3a_mlp_bwd_desc;
+int d3a_mlp_bwd(const d3a_mlp_bwd_desc* d, void* stream);
+
 /* ---- optimiser and target networks ------------------------------------- */
 
 /* One parameter tensor inside a flat buffer, with its gradient given as

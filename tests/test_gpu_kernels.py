@@ -222,3 +222,115 @@ def test_philox_statistics(dev):
     assert abs(float(n.mean())) < 0.01 and abs(float(n.std()) - 1) < 0.01
     assert float(u.min()) >= -1.0 and float(u.max()) < 1.0 and abs(float(u.mean())) < 0.01
     assert not torch.equal(first, out)  # the counter advanced -> fresh draws
+
+
+@pytest.mark.parametrize("C,R,r0,n,K0,H,L,J,x_shared", [
+    (2, 15616, 0, 15616, 14, 256, 2, 1, True),   # K2 critic pass (padded input rows)
+    (2, 15616, 7680, 7936, 14, 256, 2, 1, True),  # critic rows only (r0 > 0)
+    (1, 512, 0, 512, 11, 256, 2, 6, True),        # policy on [obs; next_obs]
+    (2, 100, 0, 100, 4, 64, 3, 1, True),          # odd rows, 3 hidden layers, H = 64
+    (3, 77, 0, 77, 37, 96, 1, 5, False),          # per-member inputs, one hidden layer
+    (2, 3000, 0, 3000, 23, 256, 2, 200, True),    # QR critic (200-quantile MFMA head)
+])
+def test_fused_mlp_forward(dev, C, R, r0, n, K0, H, L, J, x_shared, monkeypatch):
+    """d3a_mlp_fwd (every layer + head in one launch) against an fp64 torch
+    MLP; hidden activations (kept for the backward) checked too.
+    Tolerance 2e-6 relative (exact-f32 MFMA chains, K <= 256)."""
+    from d3rlpy_amd import mlp
+    from d3rlpy_amd.nets import EnsembleMLP, ParamStore
+    monkeypatch.setattr(mlp, "FUSED_MIN_ROWS", 0)  # fused kernel at every size
+    g = torch.Generator().manual_seed(R + K0)
+    st = ParamStore()
+    net = EnsembleMLP(st, "m", C, [K0] + [H] * L + [J])
+    st.allocate(dev)
+    with torch.no_grad():
+        st.data.copy_(torch.randn(st.data.numel(), generator=g) * 0.1)
+    ldx = (K0 + 3) // 4 * 4 + 4
+    x = torch.randn((1 if x_shared else C), R, ldx, generator=g).to(dev)
+    acts = mlp.Acts.alloc(net, R, dev)
+    assert mlp.fused_ok(net)
+    mlp.forward(net, st, x.data_ptr(), x_shared, ldx, acts, r0, r0 + n)
+    torch.cuda.synchronize()
+    for c in range(C):
+        a = x[0 if x_shared else c, r0:r0 + n, :K0].double()
+        for l in range(L + 1):
+            W, b = net.export_linear(l, c, st)
+            a = a @ W.double().T + b.double()
+            if l < L:
+                a = a.clamp_min(0)
+                assert _rel_err(acts.h[l][c, r0:r0 + n], a) < 2e-6, (c, l)
+        out = acts.out[c, r0:r0 + n] if J == 1 else acts.out[c, r0:r0 + n]
+        assert _rel_err(out.reshape(n, J), a) < 2e-6, c
+
+
+@pytest.mark.parametrize("C,R,r0,n,K0,H,L,J,mode", [
+    (2, 15616, 7680, 7936, 14, 256, 2, 1, "gscale"),  # K2 critic backward (IS rows scaled)
+    (2, 256, 0, 256, 14, 256, 2, 1, "qmin"),          # actor: argmin critic, dQ/dx only
+    (1, 512, 0, 256, 11, 256, 2, 6, "vector"),        # policy head backward (first half rows)
+    (2, 100, 0, 100, 4, 64, 3, 1, "plain"),           # odd rows, 3 hidden layers
+    (1, 77, 0, 77, 37, 96, 1, 5, "vector"),           # one hidden layer
+])
+def test_fused_mlp_backward(dev, C, R, r0, n, K0, H, L, J, mode, monkeypatch):
+    """d3a_mlp_bwd (dz chain + dx in one launch) + split-K weight-gradient
+    GEMMs against torch autograd in fp64 on the same forward activations.
+    Tolerance 5e-6 relative (max-normalised) per tensor."""
+    from d3rlpy_amd import mlp
+    from d3rlpy_amd.nets import EnsembleMLP, GradSpace, ParamStore
+    monkeypatch.setattr(mlp, "FUSED_MIN_ROWS", 0)
+    monkeypatch.setattr(mlp, "_FUSED_BWD", True)
+    g = torch.Generator().manual_seed(n + H)
+    st = ParamStore()
+    net = EnsembleMLP(st, "m", C, [K0] + [H] * L + [J])
+    st.allocate(dev)
+    with torch.no_grad():
+        st.data.copy_(torch.randn(st.data.numel(), generator=g) * 0.1)
+    ldx = (K0 + 3) // 4 * 4
+    x = torch.randn(R, ldx, generator=g).to(dev)
+    acts = mlp.Acts.alloc(net, R, dev)
+    mlp.forward(net, st, x.data_ptr(), True, ldx, acts)
+    grads = GradSpace(dev) if mode != "qmin" else None
+    bs = mlp.BackwardSpace(net, n, grads, dev)
+    assert bs.fused
+    dout = torch.randn(C, n, J, generator=g).to(dev).squeeze(-1).contiguous()
+    gscale = torch.tensor([0.37], device=dev)
+    dx = torch.zeros(C, n, K0, device=dev)
+    kw = {}
+    if mode == "gscale":
+        kw = dict(g_scale=gscale.data_ptr(), n_scaled=n // 3)
+    if mode == "qmin":
+        kw = dict(q_min=acts.out.data_ptr() + 4 * r0, sq_b=R, q_scale=-1.0 / n)
+    mlp.backward(bs, st, x.data_ptr(), True, ldx, acts, dout.data_ptr(), J, n * J, r0, n,
+                 weight_grads=mode != "qmin", dx=dx, **kw)
+    torch.cuda.synchronize()
+    # fp64 autograd reference
+    xs = x[r0:r0 + n, :K0].double().cpu()
+    for c in range(C):
+        params = []
+        a = xs.clone().requires_grad_(True)
+        h = a
+        for l in range(L + 1):
+            W, b = (t.double().cpu().clone().requires_grad_(True)
+                    for t in net.export_linear(l, c, st))
+            params.append((W, b))
+            h = h @ W.T + b
+            if l < L:
+                h = h.clamp_min(0)
+        if mode == "qmin":
+            qall = acts.out[:, r0:r0 + n].double().cpu()
+            arg = qall.argmin(0)
+            go = torch.where(arg == c, torch.tensor(-1.0 / n, dtype=torch.float64),
+                             torch.tensor(0.0, dtype=torch.float64)).view(n, 1)
+        else:
+            go = dout[c].double().cpu().view(n, J)
+            if mode == "gscale":
+                go = go.clone()
+                go[: n // 3] *= 0.37
+        h.backward(go)
+        assert _rel_err(dx[c], a.grad) < 5e-6, (c, "dx")
+        if mode == "qmin":
+            continue
+        for l, (W, b) in enumerate(params):
+            gW = grads.get(net.wname(l)).sum(0)[c]
+            gb = grads.get(net.bname(l)).sum(0)[c]
+            assert _rel_err(gW, W.grad) < 5e-6, (c, l, "W")
+            assert _rel_err(gb, b.grad) < 5e-6, (c, l, "b")
