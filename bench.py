@@ -69,6 +69,9 @@ WORKLOADS = {
     "td3bc": ("pendulum-random", 100,
               "TD3+BC K1 (configs[0]) on 1xMI355X: obs 3, act 1, batch 100, n_critics 2, "
               "actor every 2 steps, standard scaler, hidden [256,256], reference defaults"),
+    "bcq": ("halfcheetah-medium-v0", 256,
+            "BCQ K3 (configs[2]): obs 17, act 6, batch 256, QR critics n_quantiles 200, "
+            "n_critics 2, n_action_samples 100, hidden [256,256], reference defaults"),
 }
 
 
@@ -76,6 +79,10 @@ def _make_algo(name: str, batch: int):
     if name == "cql":
         from d3rlpy_amd.algos.cql import CQL
         return CQL(batch_size=batch, n_critics=2, n_action_samples=10)
+    if name == "bcq":
+        from d3rlpy_amd.algos.bcq import BCQ
+        from d3rlpy_amd.factories import QRQFunctionFactory
+        return BCQ(batch_size=batch, q_func_factory=QRQFunctionFactory(n_quantiles=200))
     from d3rlpy_amd.algos.td3_plus_bc import TD3PlusBC
     return TD3PlusBC(batch_size=batch)
 
@@ -131,7 +138,7 @@ def cpu_baseline(seconds: float, threads: int, name: str = "cql"):
     from oracle.gather import gather, random_indices, synthetic_dataset, to_episodes, to_transitions
     torch.set_num_threads(threads)
     n = 100_000
-    D, A = (11, 3) if name == "cql" else (3, 1)
+    D, A = {"cql": (11, 3), "td3bc": (3, 1), "bcq": (17, 6)}[name]
     B = WORKLOADS[name][1]
     obs, act, rew, term = synthetic_dataset(n, D, A, episode_len=1000, seed=0)
     trans = []
@@ -144,6 +151,12 @@ def cpu_baseline(seconds: float, threads: int, name: str = "cql"):
 
         def update(batch, k):
             orc.update(batch, CQLNoise.draw(gen, B, A, 10))
+    elif name == "bcq":
+        from oracle.bcq import BCQNoise, BCQOracle
+        orc = BCQOracle(D, A, n_quantiles=200, seed=0)
+
+        def update(batch, k):
+            orc.update(batch, BCQNoise.draw(gen, B, A, 100))
     else:
         from oracle.td3bc import StandardScalerT, TD3PlusBCOracle, fit_standard_scaler
         orc = TD3PlusBCOracle(D, A, scaler=StandardScalerT(*fit_standard_scaler(obs)), seed=0)
@@ -230,10 +243,12 @@ def main():
     if not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         sps, k, el = cpu_baseline(args.cpu_seconds, threads, args.algo)
-        what = ("CQL update (torch CPU, op-for-op restatement of cql_impl.py/sac_impl.py/"
-                "ddpg_impl.py)" if args.algo == "cql" else
-                "TD3+BC update (torch CPU, op-for-op restatement of td3_plus_bc_impl.py/"
-                "td3_impl.py/ddpg_impl.py, standard scaler)")
+        what = {"cql": "CQL update (torch CPU, op-for-op restatement of cql_impl.py/"
+                       "sac_impl.py/ddpg_impl.py)",
+                "td3bc": "TD3+BC update (torch CPU, op-for-op restatement of "
+                         "td3_plus_bc_impl.py/td3_impl.py/ddpg_impl.py, standard scaler)",
+                "bcq": "BCQ update (torch CPU, op-for-op restatement of bcq_impl.py/"
+                       "ddpg_impl.py, QR critics)"}[args.algo]
         cpu = {"value": round(sps, 3), "unit": "gradient-steps/s", "cores": threads,
                "kind": "port",
                "sample": f"oracle {what} + reference host sampler restated "
@@ -242,8 +257,9 @@ def main():
                          f"{threads} threads"}
     value = ws * args.steps / elapsed
     shape, batch, wdesc = WORKLOADS[args.algo]
-    metric = ("gradient-steps/sec (CQL, batch=256, obs=11 act=3) at 1/2/4/8 GPU"
-              if args.algo == "cql" else "gradient-steps/sec (TD3+BC, batch=100, obs=3 act=1)")
+    metric = {"cql": "gradient-steps/sec (CQL, batch=256, obs=11 act=3) at 1/2/4/8 GPU",
+              "td3bc": "gradient-steps/sec (TD3+BC, batch=100, obs=3 act=1)",
+              "bcq": "gradient-steps/sec (BCQ QR-200, batch=256, obs=17 act=6)"}[args.algo]
     out = {
         "metric": metric,
         "value": round(value, 2),

@@ -189,6 +189,52 @@ class MlpBwdDesc(C.Structure):
     ]
 
 
+class BcqRowsDesc(C.Structure):
+    _fields_ = [
+        ("obs", vp), ("D", C.c_int32), ("rep", C.c_int32),
+        ("a", vp), ("E", C.c_int32), ("lda", C.c_int64),
+        ("base", vp), ("mode", C.c_int32), ("clip", C.c_float), ("scale", C.c_float),
+        ("x", vp), ("ldx", C.c_int64), ("e_out", vp), ("rows", C.c_int64),
+    ]
+
+
+class BcqVaeDesc(C.Structure):
+    _fields_ = [
+        ("obs", vp), ("act", vp), ("eps", vp),
+        ("head_e", vp), ("std_out", vp), ("x_dec", vp), ("ldx", C.c_int64),
+        ("head_d", vp), ("dhead_d", vp),
+        ("dx_dec", vp), ("lddx", C.c_int64), ("dhead_e", vp),
+        ("scalars", vp), ("metrics", vp),
+        ("B", C.c_int32), ("D", C.c_int32), ("A", C.c_int32), ("L", C.c_int32),
+        ("beta", C.c_float), ("min_logstd", C.c_float), ("max_logstd", C.c_float),
+    ]
+
+
+class BcqTargetDesc(C.Structure):
+    _fields_ = [
+        ("q", vp), ("target", vp),
+        ("B", C.c_int32), ("N", C.c_int32), ("K", C.c_int32), ("C", C.c_int32),
+        ("lam", C.c_float),
+    ]
+
+
+class BcqQrDesc(C.Structure):
+    _fields_ = [
+        ("q", vp), ("target", vp), ("rew", vp), ("term", vp), ("n_steps", vp),
+        ("dq", vp), ("loss_cb", vp),
+        ("B", C.c_int32), ("K", C.c_int32), ("C", C.c_int32), ("gamma", C.c_float),
+    ]
+
+
+class BcqActorDesc(C.Structure):
+    _fields_ = [
+        ("head", vp), ("a_dec", vp), ("dq_da", vp), ("ld_da", C.c_int32),
+        ("da_off", C.c_int32), ("dhead", vp), ("q0", vp), ("loss_cb", vp), ("metrics", vp),
+        ("B", C.c_int32), ("A", C.c_int32), ("K", C.c_int32), ("C", C.c_int32),
+        ("scale", C.c_float),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "d3a_abi_version": (C.c_int, []),
@@ -216,6 +262,13 @@ _SIGNATURES = {
     "d3a_sac_actor_head": (C.c_int, [C.POINTER(SacActorHeadDesc), vp]),
     "d3a_gather_batch": (C.c_int, [C.POINTER(GatherDesc), vp]),
     "d3a_mlp_fwd": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
+    "d3a_bcq_rows": (C.c_int, [C.POINTER(BcqRowsDesc), vp]),
+    "d3a_bcq_vae_sample": (C.c_int, [C.POINTER(BcqVaeDesc), vp]),
+    "d3a_bcq_vae_loss": (C.c_int, [C.POINTER(BcqVaeDesc), vp]),
+    "d3a_bcq_vae_enc_grad": (C.c_int, [C.POINTER(BcqVaeDesc), vp]),
+    "d3a_bcq_target": (C.c_int, [C.POINTER(BcqTargetDesc), vp]),
+    "d3a_bcq_qr_loss": (C.c_int, [C.POINTER(BcqQrDesc), vp]),
+    "d3a_bcq_actor_head": (C.c_int, [C.POINTER(BcqActorDesc), vp]),
     "d3a_mlp_bwd": (C.c_int, [C.POINTER(MlpBwdDesc), vp]),
     "d3a_td3_prep": (C.c_int, [C.POINTER(Td3PrepDesc), vp]),
     "d3a_td3_target": (C.c_int, [C.POINTER(Td3TargetDesc), vp]),

@@ -2,12 +2,13 @@
 
 Only the algorithms on the accelerated hot path are provided.
 """
+from .bcq import BCQ
 from .cql import CQL
 from .td3_plus_bc import TD3PlusBC
 
-__all__ = ["CQL", "TD3PlusBC", "get_algo"]
+__all__ = ["BCQ", "CQL", "TD3PlusBC", "get_algo"]
 
-ALGO_LIST = {"cql": CQL, "td3_plus_bc": TD3PlusBC}
+ALGO_LIST = {"bcq": BCQ, "cql": CQL, "td3_plus_bc": TD3PlusBC}
 
 
 def get_algo(name: str, discrete: bool):

@@ -1,0 +1,603 @@
+"""BCQImpl on HIP kernels — drop-in for d3rlpy/algos/torch/bcq_impl.py:25-226
+(continuous BCQ; quantile-regression critics as in K3).
+
+Same constructor arguments and ``update_imitator / update_critic /
+update_actor / update_critic_target / update_actor_target`` methods; plus
+``update_step`` = one ``BCQ._update`` (algos/bcq.py:261-279 with the
+defaults rl_start_step 0, update_actor_interval 1) as one device pipeline
+(a HIP-graph replay after the first call).
+
+Pipeline of one update_step:
+  imitator  x = (s, a) -> VAE encoder -> d3a_bcq_vae_sample (z = mu + eps std,
+            KL) -> VAE decoder -> d3a_bcq_vae_loss -> decoder backward (with
+            dL/dz) -> d3a_bcq_vae_enc_grad -> encoder backward -> Adam
+  critic    target over N sampled actions per next state (B*N rows):
+            (s', clamp(z)) -> decoder -> (s', tanh) -> target residual policy
+            -> (s', clamp(a + 0.05 tanh)) -> target QR critics -> d3a_bcq_target
+            (compute_max_with_n_actions); critics on (s, a) ->
+            d3a_bcq_qr_loss (quantile Huber) -> backward -> Adam
+  actor     (s, clamp(z)) -> decoder -> residual policy -> critic 0 ->
+            dQ0/da -> d3a_bcq_actor_head -> policy backward -> Adam
+  targets   one soft update over the contiguous critic + policy parameters
+The B*N-row target passes (25,600 rows at K3) run through the one-launch
+fused MLP forward (d3a_mlp_fwd, MFMA quantile head).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+import torch
+from torch import nn
+
+from .. import _native as NAT
+from .. import checkpoint as ckpt
+from .. import mlp, ops
+from ..nets import AdamGroup, EnsembleMLP, GradSpace, OptimState, ParamStore
+from .impl_base import DeviceBatch, ImplBase, as_device_batch
+
+METRIC_NAMES = ("imitator_loss", "critic_loss", "actor_loss")
+
+
+def _pad4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
+class BCQImpl(ImplBase):
+    def __init__(
+        self,
+        observation_shape: Sequence[int],
+        action_size: int,
+        actor_learning_rate: float,
+        critic_learning_rate: float,
+        imitator_learning_rate: float,
+        actor_optim_factory,
+        critic_optim_factory,
+        imitator_optim_factory,
+        actor_encoder_factory,
+        critic_encoder_factory,
+        imitator_encoder_factory,
+        q_func_factory,
+        gamma: float,
+        tau: float,
+        n_critics: int,
+        lam: float,
+        n_action_samples: int,
+        action_flexibility: float,
+        beta: float,
+        use_gpu,
+        scaler,
+        action_scaler,
+        reward_scaler,
+    ):
+        super().__init__(observation_shape, action_size, scaler, action_scaler, reward_scaler,
+                         use_gpu)
+        if q_func_factory.get_type() != "qr":
+            raise NotImplementedError("BCQ on HIP implements the quantile-regression critics of "
+                                      "K3 (q_func_factory='qr')")
+        if len(observation_shape) != 1:
+            raise NotImplementedError("BCQ on HIP supports vector observations")
+        if scaler is not None or action_scaler is not None or reward_scaler is not None:
+            raise NotImplementedError("scalers are not supported by the HIP BCQImpl yet")
+        self._actor_learning_rate = actor_learning_rate
+        self._critic_learning_rate = critic_learning_rate
+        self._imitator_learning_rate = imitator_learning_rate
+        self._actor_optim_factory = actor_optim_factory
+        self._critic_optim_factory = critic_optim_factory
+        self._imitator_optim_factory = imitator_optim_factory
+        self._actor_encoder_factory = actor_encoder_factory
+        self._critic_encoder_factory = critic_encoder_factory
+        self._imitator_encoder_factory = imitator_encoder_factory
+        self._q_func_factory = q_func_factory
+        self._gamma = gamma
+        self._tau = tau
+        self._n_critics = n_critics
+        self._lam = lam
+        self._n_action_samples = n_action_samples
+        self._action_flexibility = action_flexibility
+        self._beta = beta
+        self._n_quantiles = q_func_factory.n_quantiles
+        self._ws: Dict[int, "_Workspace"] = {}
+
+    # ------------------------------------------------------------------ build
+    def build(self) -> None:
+        dev = self.torch_device
+        D, A, C, K = self._observation_shape[0], self._action_size, self._n_critics, \
+            self._n_quantiles
+        L = 2 * A
+        hi = list(self._imitator_encoder_factory.hidden_units)
+        hq = list(self._critic_encoder_factory.hidden_units)
+        hp = list(self._actor_encoder_factory.hidden_units)
+        store = ParamStore()
+        # imitator first (bcq_impl.py:101-105), then critic and actor: the
+        # critic and policy segments are contiguous (one soft-update span)
+        self.vae_enc = EnsembleMLP(store, "ve", 1, [D + A] + hi + [2 * L])
+        self.vae_dec = EnsembleMLP(store, "vd", 1, [D + L] + hi + [A])
+        self.critic = EnsembleMLP(store, "q", C, [D + A] + hq + [K])
+        self.policy = EnsembleMLP(store, "pi", 1, [D + A] + hp + [A])
+        store.allocate(dev)
+        self.store = store
+        self._init_like_reference()
+        self.targ = store.like()
+        self.targ.data.copy_(store.data)
+        self.counters = torch.zeros(8, dtype=torch.int64, device=dev)  # critic, actor, imitator
+        f = self._critic_optim_factory
+        self.critic_state = OptimState(store, self.critic.names(), self._critic_learning_rate,
+                                       f.betas, f.eps, step=self.counters[0:1])
+        f = self._actor_optim_factory
+        self.actor_state = OptimState(store, self.policy.names(), self._actor_learning_rate,
+                                      f.betas, f.eps, step=self.counters[1:2])
+        f = self._imitator_optim_factory
+        self.imitator_state = OptimState(store, self.vae_enc.names() + self.vae_dec.names(),
+                                         self._imitator_learning_rate, f.betas, f.eps,
+                                         step=self.counters[2:3])
+        s0, _ = store.span(self.critic.names())
+        _, e1 = store.span(self.policy.names())
+        self.soft_span = (s0, e1)
+
+    def _init_like_reference(self) -> None:
+        """nn.Linear default init in the reference construction order."""
+        D, A, C, K = self._observation_shape[0], self._action_size, self._n_critics, \
+            self._n_quantiles
+        L = 2 * A
+        hi = list(self._imitator_encoder_factory.hidden_units)
+        hq = list(self._critic_encoder_factory.hidden_units)
+        hp = list(self._actor_encoder_factory.hidden_units)
+        for net, d_in in ((self.vae_enc, D + A), (self.vae_dec, D + L)):
+            sizes = [d_in] + hi
+            for l in range(len(hi)):
+                net.load_linear(l, 0, nn.Linear(sizes[l], sizes[l + 1]))
+        mu, ls, fc = nn.Linear(hi[-1], L), nn.Linear(hi[-1], L), nn.Linear(hi[-1], A)
+        W, b = self.vae_enc.export_linear(len(hi), 0)
+        with torch.no_grad():
+            W[:L].copy_(mu.weight)
+            W[L:].copy_(ls.weight)
+            b[:L].copy_(mu.bias)
+            b[L:].copy_(ls.bias)
+        self.vae_dec.load_linear(len(hi), 0, fc)
+        for c in range(C):
+            sizes = [D + A] + hq
+            for l in range(len(hq)):
+                self.critic.load_linear(l, c, nn.Linear(sizes[l], sizes[l + 1]))
+            self.critic.load_linear(len(hq), c, nn.Linear(hq[-1], K))
+        sizes = [D + A] + hp
+        for l in range(len(hp)):
+            self.policy.load_linear(l, 0, nn.Linear(sizes[l], sizes[l + 1]))
+        self.policy.load_linear(len(hp), 0, nn.Linear(hp[-1], A))
+
+    # ---------------------------------------------------------- checkpoints
+    def _critic_refs(self):
+        refs, L = [], self.critic.n_layers
+        for c in range(self._n_critics):
+            for l in range(L - 1):
+                refs.append((f"_q_funcs.{c}._encoder._fcs.{l}.weight", self.critic.wname(l), c, None))
+                refs.append((f"_q_funcs.{c}._encoder._fcs.{l}.bias", self.critic.bname(l), c, None))
+            refs.append((f"_q_funcs.{c}._fc.weight", self.critic.wname(L - 1), c, None))
+            refs.append((f"_q_funcs.{c}._fc.bias", self.critic.bname(L - 1), c, None))
+        return refs
+
+    def _policy_refs(self):
+        """DeterministicResidualPolicy.parameters(): encoder fcs, _fc."""
+        refs, L = [], self.policy.n_layers
+        for l in range(L - 1):
+            refs.append((f"_encoder._fcs.{l}.weight", self.policy.wname(l), 0, None))
+            refs.append((f"_encoder._fcs.{l}.bias", self.policy.bname(l), 0, None))
+        refs.append(("_fc.weight", self.policy.wname(L - 1), 0, None))
+        refs.append(("_fc.bias", self.policy.bname(L - 1), 0, None))
+        return refs
+
+    def _imitator_refs(self):
+        """ConditionalVAE.parameters(): encoder fcs, decoder fcs, _mu, _logstd, _fc."""
+        refs = []
+        for pre, net in (("_encoder_encoder", self.vae_enc), ("_decoder_encoder", self.vae_dec)):
+            for l in range(net.n_layers - 1):
+                refs.append((f"{pre}._fcs.{l}.weight", net.wname(l), 0, None))
+                refs.append((f"{pre}._fcs.{l}.bias", net.bname(l), 0, None))
+        L, Le = 2 * self._action_size, self.vae_enc.n_layers - 1
+        mu, ls = slice(0, L), slice(L, 2 * L)
+        refs += [("_mu.weight", self.vae_enc.wname(Le), 0, mu),
+                 ("_mu.bias", self.vae_enc.bname(Le), 0, mu),
+                 ("_logstd.weight", self.vae_enc.wname(Le), 0, ls),
+                 ("_logstd.bias", self.vae_enc.bname(Le), 0, ls),
+                 ("_fc.weight", self.vae_dec.wname(self.vae_dec.n_layers - 1), 0, None),
+                 ("_fc.bias", self.vae_dec.bname(self.vae_dec.n_layers - 1), 0, None)]
+        return refs
+
+    def get_state_dict(self) -> Dict[str, dict]:
+        """torch_utility.get_state_dict layout of the reference BCQImpl."""
+        torch.cuda.synchronize()
+        cr, pr, ir = self._critic_refs(), self._policy_refs(), self._imitator_refs()
+        return {
+            "_q_func": ckpt.module_state(self.store, cr),
+            "_targ_q_func": ckpt.module_state(self.targ, cr),
+            "_policy": ckpt.module_state(self.store, pr),
+            "_targ_policy": ckpt.module_state(self.targ, pr),
+            "_imitator": ckpt.module_state(self.store, ir),
+            "_critic_optim": ckpt.adam_state(self.critic_state, cr),
+            "_actor_optim": ckpt.adam_state(self.actor_state, pr),
+            "_imitator_optim": ckpt.adam_state(self.imitator_state, ir),
+        }
+
+    def set_state_dict(self, sd: Dict[str, dict]) -> None:
+        cr, pr, ir = self._critic_refs(), self._policy_refs(), self._imitator_refs()
+        ckpt.load_module_state(self.store, cr, sd["_q_func"])
+        ckpt.load_module_state(self.targ, cr, sd["_targ_q_func"])
+        ckpt.load_module_state(self.store, pr, sd["_policy"])
+        ckpt.load_module_state(self.targ, pr, sd["_targ_policy"])
+        ckpt.load_module_state(self.store, ir, sd["_imitator"])
+        ckpt.load_adam_state(self.critic_state, cr, sd["_critic_optim"])
+        ckpt.load_adam_state(self.actor_state, pr, sd["_actor_optim"])
+        ckpt.load_adam_state(self.imitator_state, ir, sd["_imitator_optim"])
+        torch.cuda.synchronize()
+
+    def save_model(self, fname: str) -> None:
+        torch.save(self.get_state_dict(), fname)
+
+    def load_model(self, fname: str) -> None:
+        self.set_state_dict(torch.load(fname, map_location="cpu", weights_only=True))
+
+    # --------------------------------------------------------------- updates
+    def _workspace(self, B: int) -> "_Workspace":
+        ws = self._ws.get(B)
+        if ws is None:
+            if self._ws:
+                raise NotImplementedError("one batch size per BCQImpl is supported")
+            ws = _Workspace(self, B)
+            self._ws[B] = ws
+        return ws
+
+    def update_step(self, batch, noise: Optional[Dict[str, np.ndarray]] = None,
+                    sync: bool = True, use_graph: bool = True):
+        """One BCQ._update: imitator, critic, actor, both soft target updates."""
+        return self._run(batch, (True, True, True, True), noise, sync, use_graph)
+
+    def update_imitator(self, batch) -> np.ndarray:
+        return np.float32(self._run(batch, (True, False, False, False), None, True,
+                                    False)["imitator_loss"])
+
+    def update_critic(self, batch) -> np.ndarray:
+        return np.float32(self._run(batch, (False, True, False, False), None, True,
+                                    False)["critic_loss"])
+
+    def update_actor(self, batch) -> np.ndarray:
+        return np.float32(self._run(batch, (False, False, True, False), None, True,
+                                    False)["actor_loss"])
+
+    def update_critic_target(self) -> None:
+        s, e = self.store.span(self.critic.names())
+        ops.soft_update(self.targ.data[s:e], self.store.data[s:e], self._tau)
+
+    def update_actor_target(self) -> None:
+        s, e = self.store.span(self.policy.names())
+        ops.soft_update(self.targ.data[s:e], self.store.data[s:e], self._tau)
+
+    def _run(self, batch, flags, noise, sync, use_graph):
+        db = as_device_batch(batch, self.torch_device)
+        ws = self._workspace(db.batch_size)
+        ws.stage(db, noise)
+        ws.execute(flags, use_graph=use_graph and noise is None)
+        if not sync:
+            return None
+        vals = ws.metrics.cpu().numpy()
+        out = {k: float(v) for k, v in zip(METRIC_NAMES, vals)}
+        if flags[1] and not flags[2]:
+            # the critic-loss reduction runs inside the actor stage; without
+            # it, reduce the per-row losses here (method-level call only)
+            out["critic_loss"] = float(ws.loss_cb.double().sum().item() / ws.B)
+        return out
+
+    # ------------------------------------------------- device-side batches
+    def staging_batch(self, batch_size: int) -> DeviceBatch:
+        ws = self._workspace(batch_size)
+        B = batch_size
+        return DeviceBatch(ws.obs2[:B], ws.act, ws.rew, ws.obs2[B:], ws.term, ws.nsteps)
+
+    def active_metric_names(self):
+        return list(METRIC_NAMES)
+
+    def metrics_ring(self, n_steps: int):
+        for ws in self._ws.values():
+            ws.ring_ctr.zero_()
+        return n_steps
+
+    def read_metrics_ring(self, handle):
+        names = self.active_metric_names()
+        if not self._ws:
+            return names, np.zeros((0, len(names)), dtype=np.float32)
+        ws = next(iter(self._ws.values()))
+        k = min(int(ws.ring_ctr.item()), ws.ring.shape[0])
+        return names, ws.ring[:k].cpu().numpy()
+
+    # ------------------------------------------------------------- inference
+    def _mlp(self, net, x: torch.Tensor, store=None) -> torch.Tensor:
+        x = x.contiguous().float()
+        acts = mlp.Acts.alloc(net, x.shape[0], self.torch_device)
+        mlp.forward(net, store or self.store, x.data_ptr(), True, x.shape[1], acts,
+                    keep_h=False)
+        return acts.out
+
+    def _predict_best_action(self, x: torch.Tensor) -> torch.Tensor:
+        """bcq_impl.py:204-210: N sampled actions per state, argmax of Q_0."""
+        N, A = self._n_action_samples, self._action_size
+        B = x.shape[0]
+        rx = x.repeat_interleave(N, dim=0)
+        z = torch.randn(B * N, 2 * A, device=x.device).clamp(-0.5, 0.5)
+        a_dec = torch.tanh(self._mlp(self.vae_dec, torch.cat([rx, z], 1))[0])
+        res = self._mlp(self.policy, torch.cat([rx, a_dec], 1))[0]
+        act = (a_dec + self._action_flexibility * torch.tanh(res)).clamp(-1.0, 1.0)
+        q0 = self._mlp(self.critic, torch.cat([rx, act], 1))[0].mean(dim=1)
+        idx = q0.view(B, N).argmax(dim=1)
+        return act.view(B, N, A)[torch.arange(B, device=x.device), idx]
+
+    def _sample_action(self, x: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError("BCQ does not support sampling action")
+
+    def _predict_value(self, x: torch.Tensor, action: torch.Tensor) -> torch.Tensor:
+        q = self._mlp(self.critic, torch.cat([x.float(), action.float()], 1))
+        return q.mean(dim=2)  # [C][B] quantile means (ContinuousQRQFunction.forward)
+
+    # ------------------------------------------------------------ inspection
+    def critic_grad(self, name: str) -> torch.Tensor:
+        return next(iter(self._ws.values())).critic_opt.grad(name)
+
+    def policy_grad(self, name: str) -> torch.Tensor:
+        return next(iter(self._ws.values())).actor_opt.grad(name)
+
+    def imitator_grad(self, name: str) -> torch.Tensor:
+        return next(iter(self._ws.values())).imitator_opt.grad(name)
+
+
+class _Workspace:
+    """Every device buffer of one BCQ update at batch size B."""
+
+    def __init__(self, impl: BCQImpl, B: int):
+        dev = impl.torch_device
+        self.impl = impl
+        D, A, C, K, N = (impl._observation_shape[0], impl._action_size, impl._n_critics,
+                         impl._n_quantiles, impl._n_action_samples)
+        L = 2 * A
+        self.B, self.D, self.A, self.C, self.K, self.N, self.L = B, D, A, C, K, N, L
+        BN = B * N
+        self.LX1, self.LX2 = _pad4(D + A), _pad4(D + L)
+        z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        self.obs2 = z(2 * B, D)
+        self.act = z(B, A)
+        self.rew = z(B)
+        self.term = z(B)
+        self.nsteps = z(B)
+        self.obs, self.next_obs = self.obs2[:B], self.obs2[B:]
+        # noise: [eps_vae (B L) | z_target (B N L) | z_actor (B L)]
+        self.noise = z((B + BN + B) * L)
+        self.eps_vae = self.noise[:B * L]
+        self.z_target = self.noise[B * L:(B + BN) * L]
+        self.z_actor = self.noise[(B + BN) * L:]
+        self.rng_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.rng_ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.seed = int(torch.randint(0, 2**62, (1,)).item())
+        # imitator
+        self.x_q = z(B, self.LX1)                       # (s, a): VAE encoder + critic rows
+        self.ve_acts = mlp.Acts.alloc(impl.vae_enc, B, dev)
+        self.std = z(B * L)
+        self.x_vd = z(B, self.LX2)
+        self.vd_acts = mlp.Acts.alloc(impl.vae_dec, B, dev)
+        self.dhead_d = z(B, A)
+        self.dx_vd = z(1, B, D + L)
+        self.dhead_e = z(B, 2 * L)
+        self.igrads = GradSpace(dev)
+        self.ve_bwd = mlp.BackwardSpace(impl.vae_enc, B, self.igrads, dev)
+        self.vd_bwd = mlp.BackwardSpace(impl.vae_dec, B, self.igrads, dev)
+        # critic target over B*N sampled actions
+        self.x_td = z(BN, self.LX2)
+        self.td_acts = mlp.Acts.alloc(impl.vae_dec, BN, dev)
+        self.a_dec_t = z(BN, A)
+        self.x_tp = z(BN, self.LX1)
+        self.tp_acts = mlp.Acts.alloc(impl.policy, BN, dev)
+        self.x_tq = z(BN, self.LX1)
+        self.tq_acts = mlp.Acts.alloc(impl.critic, BN, dev)
+        self.target = z(B, K)
+        self.q_acts = mlp.Acts.alloc(impl.critic, B, dev)
+        self.dq = z(C, B, K)
+        self.loss_cb = z(C, B)
+        self.cgrads = GradSpace(dev)
+        self.cbwd = mlp.BackwardSpace(impl.critic, B, self.cgrads, dev)
+        # actor
+        self.x_ad = z(B, self.LX2)
+        self.ad_acts = mlp.Acts.alloc(impl.vae_dec, B, dev)
+        self.a_dec_a = z(B, A)
+        self.x_pa = z(B, self.LX1)
+        self.pa_acts = mlp.Acts.alloc(impl.policy, B, dev)
+        self.x_qa = z(B, self.LX1)
+        self.qa_acts = mlp.Acts.alloc(impl.critic, B, dev)
+        # d(-mean_b mean_k q0)/dq0 is a constant
+        self.dconst = torch.full((1, B, K), -1.0 / (B * K), dtype=torch.float32, device=dev)
+        self.abwd = mlp.BackwardSpace(impl.critic, B, None, dev)
+        self.adx = z(1, B, D + A)
+        self.dhead_pi = z(B, A)
+        self.pgrads = GradSpace(dev)
+        self.pbwd = mlp.BackwardSpace(impl.policy, B, self.pgrads, dev)
+        self.metrics = z(len(METRIC_NAMES))
+        self.scalars = z(4)
+        self.ring = z(1 << 16, len(METRIC_NAMES))
+        self.ring_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.imitator_opt = AdamGroup(impl.imitator_state, self.igrads)
+        self.critic_opt = AdamGroup(impl.critic_state, self.cgrads)
+        self.actor_opt = AdamGroup(impl.actor_state, self.pgrads)
+        self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._ran_eager = set()
+        self._external_noise = False
+        self._build_descs()
+
+    def _rows(self, obs, rep, a, E, lda, mode, x, ldx, rows, base=None, e_out=None, clip=0.0,
+              scale=0.0):
+        d = NAT.BcqRowsDesc()
+        d.obs, d.D, d.rep = obs.data_ptr(), self.D, rep
+        d.a, d.E, d.lda = a, E, lda
+        d.base = base.data_ptr() if base is not None else None
+        d.mode, d.clip, d.scale = mode, clip, scale
+        d.x, d.ldx = x.data_ptr(), ldx
+        d.e_out = e_out.data_ptr() if e_out is not None else None
+        d.rows = rows
+        return d
+
+    def _build_descs(self):
+        impl = self.impl
+        B, D, A, C, K, N, L = self.B, self.D, self.A, self.C, self.K, self.N, self.L
+        BN = B * N
+        flex = impl._action_flexibility
+        self.r_q = self._rows(self.obs, 1, self.act.data_ptr(), A, A, 0, self.x_q, self.LX1, B)
+        # target: (s', clamp(z)) -> (s', tanh(dec)) -> (s', clamp(a_dec + flex tanh(pi)))
+        self.r_td = self._rows(self.next_obs, N, self.z_target.data_ptr(), L, L, 1, self.x_td,
+                               self.LX2, BN, clip=0.5)
+        self.r_tp = self._rows(self.next_obs, N, self.td_acts.out.data_ptr(), A, A, 2, self.x_tp,
+                               self.LX1, BN, e_out=self.a_dec_t)
+        self.r_tq = self._rows(self.next_obs, N, self.tp_acts.out.data_ptr(), A, A, 3, self.x_tq,
+                               self.LX1, BN, base=self.a_dec_t, scale=flex)
+        # actor: the same chain on (s, z_actor) with the online policy
+        self.r_ad = self._rows(self.obs, 1, self.z_actor.data_ptr(), L, L, 1, self.x_ad,
+                               self.LX2, B, clip=0.5)
+        self.r_pa = self._rows(self.obs, 1, self.ad_acts.out.data_ptr(), A, A, 2, self.x_pa,
+                               self.LX1, B, e_out=self.a_dec_a)
+        self.r_qa = self._rows(self.obs, 1, self.pa_acts.out.data_ptr(), A, A, 3, self.x_qa,
+                               self.LX1, B, base=self.a_dec_a, scale=flex)
+
+        v = NAT.BcqVaeDesc()
+        v.obs, v.act, v.eps = self.obs.data_ptr(), self.act.data_ptr(), self.eps_vae.data_ptr()
+        v.head_e, v.std_out = self.ve_acts.out.data_ptr(), self.std.data_ptr()
+        v.x_dec, v.ldx = self.x_vd.data_ptr(), self.LX2
+        v.head_d, v.dhead_d = self.vd_acts.out.data_ptr(), self.dhead_d.data_ptr()
+        v.dx_dec, v.lddx, v.dhead_e = self.dx_vd.data_ptr(), D + L, self.dhead_e.data_ptr()
+        v.scalars, v.metrics = self.scalars.data_ptr(), self.metrics.data_ptr()
+        v.B, v.D, v.A, v.L = B, D, A, L
+        v.beta, v.min_logstd, v.max_logstd = impl._beta, -4.0, 15.0
+        self.vae_desc = v
+
+        t = NAT.BcqTargetDesc()
+        t.q, t.target = self.tq_acts.out.data_ptr(), self.target.data_ptr()
+        t.B, t.N, t.K, t.C, t.lam = B, N, K, C, impl._lam
+        self.target_desc = t
+
+        q = NAT.BcqQrDesc()
+        q.q, q.target = self.q_acts.out.data_ptr(), self.target.data_ptr()
+        q.rew, q.term, q.n_steps = self.rew.data_ptr(), self.term.data_ptr(), self.nsteps.data_ptr()
+        q.dq, q.loss_cb = self.dq.data_ptr(), self.loss_cb.data_ptr()
+        q.B, q.K, q.C, q.gamma = B, K, C, impl._gamma
+        self.qr_desc = q
+
+        a = NAT.BcqActorDesc()
+        a.head, a.a_dec = self.pa_acts.out.data_ptr(), self.a_dec_a.data_ptr()
+        a.dq_da, a.ld_da, a.da_off = self.adx.data_ptr(), D + A, D
+        a.dhead, a.q0 = self.dhead_pi.data_ptr(), self.qa_acts.out.data_ptr()
+        a.loss_cb, a.metrics = self.loss_cb.data_ptr(), self.metrics.data_ptr()
+        a.B, a.A, a.K, a.C, a.scale = B, A, K, C, flex
+        self.actor_desc = a
+
+    def stage(self, db: DeviceBatch, noise) -> None:
+        B, D = self.B, self.D
+        if db.obs.data_ptr() != self.obs2.data_ptr():
+            self.obs2[:B].copy_(db.obs.view(B, D), non_blocking=True)
+            self.obs2[B:].copy_(db.next_obs.view(B, D), non_blocking=True)
+            self.act.copy_(db.act.view(B, self.A), non_blocking=True)
+            self.rew.copy_(db.rew.view(B), non_blocking=True)
+            self.term.copy_(db.term.view(B), non_blocking=True)
+            self.nsteps.copy_(db.n_steps.view(B), non_blocking=True)
+        self._external_noise = noise is not None
+        if noise is not None:
+            g = lambda k: torch.as_tensor(np.asarray(noise[k]), dtype=torch.float32).view(-1)  # noqa
+            self.eps_vae.copy_(g("eps_vae"))
+            self.z_target.copy_(g("z_target"))
+            self.z_actor.copy_(g("z_actor"))
+
+    def dominant_kernel(self):
+        """The target QR-critic ensemble forward over the B*N sampled actions
+        (d3a_mlp_fwd; MFMA 200-quantile head): the bulk of K3's FLOPs."""
+        impl = self.impl
+        net = impl.critic
+        s = net.sizes
+        BN = self.B * self.N
+
+        def launch():
+            mlp.forward(net, impl.targ, self.x_tq.data_ptr(), True, self.LX1, self.tq_acts,
+                        keep_h=False)
+        flops = 2 * self.C * BN * sum(s[l] * s[l + 1] for l in range(len(s) - 1))
+        return launch, flops, (f"d3a_mlp_fwd target QR critics: C={self.C} x {BN} rows x "
+                               f"{'-'.join(map(str, s))}")
+
+    def execute(self, flags, use_graph: bool) -> None:
+        key = tuple(bool(f) for f in flags) + (self._external_noise,)
+        if not use_graph:
+            self._enqueue(*flags)
+            return
+        g = self._graphs.get(key)
+        if g is None:
+            if key not in self._ran_eager:
+                self._ran_eager.add(key)
+                self._enqueue(*flags)
+                return
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g):
+                self._enqueue(*flags)
+            self._graphs[key] = g
+        g.replay()
+
+    def _enqueue(self, imitator: bool, critic: bool, actor: bool, targets: bool) -> None:
+        impl = self.impl
+        B, D, A, K, L = self.B, self.D, self.A, self.K, self.L
+        st, tg = impl.store, impl.targ
+        if not self._external_noise:
+            ops.philox_fill(self.noise, self.noise.numel(), 0, -1.0, 1.0, self.seed,
+                            self.rng_ctr, self.rng_ticket)
+        ops.call_desc("d3a_bcq_rows", self.r_q)
+        if imitator:
+            # update_imitator (bcq_impl.py:148-161)
+            mlp.forward(impl.vae_enc, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts)
+            ops.call_desc("d3a_bcq_vae_sample", self.vae_desc)
+            mlp.forward(impl.vae_dec, st, self.x_vd.data_ptr(), True, self.LX2, self.vd_acts)
+            ops.call_desc("d3a_bcq_vae_loss", self.vae_desc)
+            mlp.backward(self.vd_bwd, st, self.x_vd.data_ptr(), True, self.LX2, self.vd_acts,
+                         self.dhead_d.data_ptr(), A, B * A, 0, B, dx=self.dx_vd)
+            ops.call_desc("d3a_bcq_vae_enc_grad", self.vae_desc)
+            mlp.backward(self.ve_bwd, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts,
+                         self.dhead_e.data_ptr(), 2 * L, B * 2 * L, 0, B)
+            self.imitator_opt.launch()
+        if critic:
+            # compute_target (bcq_impl.py:215-226) over B*N sampled actions
+            ops.call_desc("d3a_bcq_rows", self.r_td)
+            mlp.forward(impl.vae_dec, st, self.x_td.data_ptr(), True, self.LX2, self.td_acts,
+                        keep_h=False)
+            ops.call_desc("d3a_bcq_rows", self.r_tp)
+            mlp.forward(impl.policy, tg, self.x_tp.data_ptr(), True, self.LX1, self.tp_acts,
+                        keep_h=False)
+            ops.call_desc("d3a_bcq_rows", self.r_tq)
+            mlp.forward(impl.critic, tg, self.x_tq.data_ptr(), True, self.LX1, self.tq_acts,
+                        keep_h=False)
+            ops.call_desc("d3a_bcq_target", self.target_desc)
+            # update_critic (ddpg_impl.py:138-165) with the quantile Huber loss
+            mlp.forward(impl.critic, st, self.x_q.data_ptr(), True, self.LX1, self.q_acts)
+            ops.call_desc("d3a_bcq_qr_loss", self.qr_desc)
+            mlp.backward(self.cbwd, st, self.x_q.data_ptr(), True, self.LX1, self.q_acts,
+                         self.dq.data_ptr(), K, B * K, 0, B)
+            self.critic_opt.launch()
+        if actor:
+            # compute_actor_loss (bcq_impl.py:132-146)
+            ops.call_desc("d3a_bcq_rows", self.r_ad)
+            mlp.forward(impl.vae_dec, st, self.x_ad.data_ptr(), True, self.LX2, self.ad_acts,
+                        keep_h=False)
+            ops.call_desc("d3a_bcq_rows", self.r_pa)
+            mlp.forward(impl.policy, st, self.x_pa.data_ptr(), True, self.LX1, self.pa_acts)
+            ops.call_desc("d3a_bcq_rows", self.r_qa)
+            mlp.forward(impl.critic, st, self.x_qa.data_ptr(), True, self.LX1, self.qa_acts,
+                        members=1)
+            mlp.backward(self.abwd, st, self.x_qa.data_ptr(), True, self.LX1, self.qa_acts,
+                         self.dconst.data_ptr(), K, B * K, 0, B, weight_grads=False, dx=self.adx,
+                         members=1)
+            ops.call_desc("d3a_bcq_actor_head", self.actor_desc)
+            mlp.backward(self.pbwd, st, self.x_pa.data_ptr(), True, self.LX1, self.pa_acts,
+                         self.dhead_pi.data_ptr(), A, B * A, 0, B)
+            self.actor_opt.launch()
+        s0, s1 = impl.soft_span
+        mask = (1 if critic else 0) | (2 if actor else 0) | (4 if imitator else 0)
+        ops.step_end(impl.counters, mask, self.metrics, self.ring, self.ring_ctr,
+                     tg.data[s0:s1] if targets else None, st.data[s0:s1] if targets else None,
+                     impl._tau)

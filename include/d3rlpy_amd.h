@@ -427,6 +427,80 @@ int d3a_td3bc_actor_input(const d3a_td3bc_actor_desc* d, void* stream);
 int d3a_td3bc_actor_seed(const d3a_td3bc_actor_desc* d, void* stream);
 int d3a_td3bc_actor_head(const d3a_td3bc_actor_desc* d, void* stream);
 
+/* ---- BCQ stages (K3: continuous BCQ, quantile-regression critics).  The MLP
+ * layers use d3a_mlp_fwd / d3a_gemm_f32; these build their input rows and
+ * the loss gradients. ---- */
+
+/* x[r] = (obs[r / rep], f(a[r])), r < rows; f by mode: 0 copy, 1 clamp(a,
+ * -clip, clip) (the clipped latent of bcq_impl.py:139,180), 2 tanh(a)
+ * (ConditionalVAE.decode, imitators.py:70-72), 3 clamp(base + scale *
+ * tanh(a), -1, 1) (DeterministicResidualPolicy.forward, policies.py:94-97);
+ * e_out (optional) also receives f(a).  Replaces _repeat_observation +
+ * torch.cat of VectorEncoderWithAction (bcq_impl.py:163-187). */
+typedef struct d3a_bcq_rows_desc {
+  const float* obs; int32_t D, rep;
+  const float* a; int32_t E; int64_t lda;
+  const float* base;
+  int32_t mode; float clip, scale;
+  float* x; int64_t ldx;
+  float* e_out;
+  int64_t rows;
+} d3a_bcq_rows_desc;
+int d3a_bcq_rows(const d3a_bcq_rows_desc* d, void* stream);
+
+/* ConditionalVAE.compute_error (imitators.py:80-86) around the encoder /
+ * decoder MLPs, three stages:
+ *   d3a_bcq_vae_sample    head_e = [mu | logstd] -> std = exp(clamp(logstd)),
+ *                         z = mu + eps std, x_dec = (obs, z), scalars[0] = mean KL
+ *   d3a_bcq_vae_loss      head_d -> y = tanh, metrics[0] = mse(y, act) + beta KL,
+ *                         dhead_d = dL/dhead_d
+ *   d3a_bcq_vae_enc_grad  dhead_e from dz = dx_dec[:, D:] and the KL term */
+typedef struct d3a_bcq_vae_desc {
+  const float* obs; const float* act; const float* eps;
+  const float* head_e; float* std_out; float* x_dec; int64_t ldx;
+  const float* head_d; float* dhead_d;
+  const float* dx_dec; int64_t lddx; float* dhead_e;
+  float* scalars; float* metrics;
+  int32_t B, D, A, L;
+  float beta, min_logstd, max_logstd;
+} d3a_bcq_vae_desc;
+int d3a_bcq_vae_sample(const d3a_bcq_vae_desc* d, void* stream);
+int d3a_bcq_vae_loss(const d3a_bcq_vae_desc* d, void* stream);
+int d3a_bcq_vae_enc_grad(const d3a_bcq_vae_desc* d, void* stream);
+
+/* compute_max_with_n_actions (q_functions/__init__.py:8-72): q = target
+ * quantiles [C][B*N][K] (row b*N + n) -> target[b] = (1 - lam) q[cmax][b, n*]
+ * + lam q[cmin][b, n*], n* = argmax_n mix of the per-critic quantile means. */
+typedef struct d3a_bcq_target_desc {
+  const float* q; float* target;
+  int32_t B, N, K, C; float lam;
+} d3a_bcq_target_desc;
+int d3a_bcq_target(const d3a_bcq_target_desc* d, void* stream);
+
+/* Quantile Huber TD loss of every critic (ContinuousQRQFunction.compute_error,
+ * qr_q_function.py:130-150, q_functions/utility.py:27-61): dq = dL/dq
+ * [C][B][K], loss_cb[c][b] = per-row loss (summed over critics and averaged
+ * over rows by d3a_bcq_actor_head into metrics[1]). */
+typedef struct d3a_bcq_qr_desc {
+  const float* q; const float* target;
+  const float* rew; const float* term; const float* n_steps;
+  float* dq; float* loss_cb;
+  int32_t B, K, C; float gamma;
+} d3a_bcq_qr_desc;
+int d3a_bcq_qr_loss(const d3a_bcq_qr_desc* d, void* stream);
+
+/* BCQImpl.compute_actor_loss backward through the residual policy
+ * (bcq_impl.py:132-146): dhead = dq_da[:, da_off:] * [clamp pass] * scale *
+ * (1 - tanh(head)^2); metrics[2] = -mean q0 (q0: member-0 quantiles [B][K]),
+ * metrics[1] = sum_c mean_b loss_cb. */
+typedef struct d3a_bcq_actor_desc {
+  const float* head; const float* a_dec;
+  const float* dq_da; int32_t ld_da, da_off;
+  float* dhead; const float* q0; const float* loss_cb; float* metrics;
+  int32_t B, A, K, C; float scale;
+} d3a_bcq_actor_desc;
+int d3a_bcq_actor_head(const d3a_bcq_actor_desc* d, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

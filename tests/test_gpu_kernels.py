@@ -334,3 +334,42 @@ def test_fused_mlp_backward(dev, C, R, r0, n, K0, H, L, J, mode, monkeypatch):
             gb = grads.get(net.bname(l)).sum(0)[c]
             assert _rel_err(gW, W.grad) < 5e-6, (c, l, "W")
             assert _rel_err(gb, b.grad) < 5e-6, (c, l, "b")
+
+
+@pytest.mark.parametrize("C,R,K0,H,J,members", [(2, 256, 23, 256, 200, 1), (2, 256, 23, 256, 200, 2),
+                                                (2, 256, 14, 256, 1, 1), (2, 32, 7, 64, 16, 1)])
+def test_mlp_input_gradient_member_subset(dev, C, R, K0, H, J, members):
+    """Per-layer path: forward + input-gradient backward through the first
+    ``members`` ensemble members (the actor's dQ_0/da) against fp64 autograd."""
+    from d3rlpy_amd import mlp
+    from d3rlpy_amd.nets import EnsembleMLP, ParamStore
+    g = torch.Generator().manual_seed(R + J)
+    st = ParamStore()
+    net = EnsembleMLP(st, "m", C, [K0, H, H, J])
+    st.allocate(dev)
+    with torch.no_grad():
+        st.data.copy_(torch.randn(st.data.numel(), generator=g) * 0.1)
+    ldx = (K0 + 3) // 4 * 4
+    x = torch.randn(R, ldx, generator=g).to(dev)
+    acts = mlp.Acts.alloc(net, R, dev)
+    mlp.forward(net, st, x.data_ptr(), True, ldx, acts, members=members)
+    bs = mlp.BackwardSpace(net, R, None, dev)
+    dout = torch.randn(C, R, J, generator=g).to(dev).squeeze(-1).contiguous()
+    dx = torch.zeros(members, R, K0, device=dev)
+    if J == 1:
+        mlp.backward(bs, st, x.data_ptr(), True, ldx, acts, dout.data_ptr(), 1, R, 0, R,
+                     weight_grads=False, dx=dx, members=members)
+    else:
+        mlp.backward(bs, st, x.data_ptr(), True, ldx, acts, dout.data_ptr(), J, R * J, 0, R,
+                     weight_grads=False, dx=dx, members=members)
+    torch.cuda.synchronize()
+    for c in range(members):
+        a = x[:, :K0].double().cpu().requires_grad_(True)
+        h = a
+        for l in range(3):
+            W, b = (t.double().cpu() for t in net.export_linear(l, c, st))
+            h = h @ W.T + b
+            if l < 2:
+                h = h.clamp_min(0)
+        h.backward(dout[c].double().cpu().view(R, J))
+        assert _rel_err(dx[c], a.grad) < 5e-6, (c, _rel_err(dx[c], a.grad))

@@ -52,7 +52,9 @@ STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_adam_segment", "AdamSegment"),
            ("d3a_td3_prep_desc", "Td3PrepDesc"), ("d3a_td3_target_desc", "Td3TargetDesc"),
            ("d3a_td3_critic_loss_desc", "Td3CriticLossDesc"),
            ("d3a_td3bc_actor_desc", "Td3bcActorDesc"), ("d3a_mlp_fwd_desc", "MlpFwdDesc"),
-           ("d3a_mlp_bwd_desc", "MlpBwdDesc"))
+           ("d3a_mlp_bwd_desc", "MlpBwdDesc"), ("d3a_bcq_rows_desc", "BcqRowsDesc"),
+           ("d3a_bcq_vae_desc", "BcqVaeDesc"), ("d3a_bcq_target_desc", "BcqTargetDesc"),
+           ("d3a_bcq_qr_desc", "BcqQrDesc"), ("d3a_bcq_actor_desc", "BcqActorDesc"))
 
 
 def test_struct_layouts_match_header(tmp_path):
