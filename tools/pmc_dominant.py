@@ -1,0 +1,37 @@
+"""Launch only the bench's dominant kernel (for a rocprofv3 --pmc pass).
+
+    rocprofv3 --pmc FETCH_SIZE -d OUT -o run --output-format csv -- \
+        python3 tools/pmc_dominant.py [--algo cql] [--reps 20]
+
+Builds the same workload as bench.py, runs a few warm updates (so every
+buffer holds real data), then launches the dominant kernel --reps times.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--algo", default="cql")
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--transitions", type=int, default=200_000)
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    algo, it = bench.build_workload(0, a.transitions, a.algo)
+    bench.gpu_steps(algo, it, 5)
+    torch.cuda.synchronize()
+    launch, flops, desc = next(iter(algo.impl._ws.values())).dominant_kernel()
+    for _ in range(a.reps):
+        launch()
+    torch.cuda.synchronize()
+    print(desc, flops)
+
+
+if __name__ == "__main__":
+    main()
