@@ -72,6 +72,10 @@ WORKLOADS = {
     "bcq": ("halfcheetah-medium-v0", 256,
             "BCQ K3 (configs[2]): obs 17, act 6, batch 256, QR critics n_quantiles 200, "
             "n_critics 2, n_action_samples 100, hidden [256,256], reference defaults"),
+    "dcql": ("atari", 512,
+             "DiscreteCQL K5 (configs[4]): 4x84x84 uint8 frame stacks (n_frames 4), IQN "
+             "(64 quantiles, embed 64), batch 512, 4 actions, pixel scaler, Nature-DQN "
+             "encoder, reference defaults"),
 }
 
 
@@ -79,6 +83,9 @@ def _make_algo(name: str, batch: int):
     if name == "cql":
         from d3rlpy_amd.algos.cql import CQL
         return CQL(batch_size=batch, n_critics=2, n_action_samples=10)
+    if name == "dcql":
+        from d3rlpy_amd.algos.cql import DiscreteCQL
+        return DiscreteCQL(batch_size=batch, n_frames=4, q_func_factory="iqn", scaler="pixel")
     if name == "bcq":
         from d3rlpy_amd.algos.bcq import BCQ
         from d3rlpy_amd.factories import QRQFunctionFactory
@@ -92,7 +99,11 @@ def build_workload(rank: int, n_transitions: int, name: str = "cql"):
     from d3rlpy_amd.datasets import get_synthetic_d4rl
     from d3rlpy_amd.iterators import RandomIterator
     shape, batch, _ = WORKLOADS[name]
-    ds = get_synthetic_d4rl(shape, n=n_transitions, seed=0)
+    if shape == "atari":
+        from d3rlpy_amd.datasets import get_synthetic_atari
+        ds = get_synthetic_atari(n_frames_total=n_transitions, action_size=4, seed=0)
+    else:
+        ds = get_synthetic_d4rl(shape, n=n_transitions, seed=0)
     import torch
     torch.manual_seed(rank)
     algo = _make_algo(name, batch)
@@ -101,7 +112,8 @@ def build_workload(rank: int, n_transitions: int, name: str = "cql"):
     algo.build_with_dataset(ds)
     ddata = DeviceDataset(ds)
     it = RandomIterator(ddata, n_steps_per_epoch=1 << 40, batch_size=batch,
-                        out=algo.impl.staging_batch(batch), seed=1000 + rank)
+                        n_frames=algo.n_frames, out=algo.impl.staging_batch(batch),
+                        seed=1000 + rank)
     return algo, it
 
 
@@ -137,14 +149,16 @@ def cpu_baseline(seconds: float, threads: int, name: str = "cql"):
     from oracle.cql import Batch, CQLNoise, CQLOracle
     from oracle.gather import gather, random_indices, synthetic_dataset, to_episodes, to_transitions
     torch.set_num_threads(threads)
+    B = WORKLOADS[name][1]
+    gen = torch.Generator().manual_seed(0)
+    if name == "dcql":
+        return _cpu_baseline_dcql(seconds, B, gen)
     n = 100_000
     D, A = {"cql": (11, 3), "td3bc": (3, 1), "bcq": (17, 6)}[name]
-    B = WORKLOADS[name][1]
     obs, act, rew, term = synthetic_dataset(n, D, A, episode_len=1000, seed=0)
     trans = []
     for o, a, r, t in to_episodes(obs, act, rew, term):
         trans += to_transitions(o, a, r, t)
-    gen = torch.Generator().manual_seed(0)
     np.random.seed(0)
     if name == "cql":
         orc = CQLOracle(D, A, n_critics=2, n_action_samples=10, seed=0)
@@ -186,6 +200,46 @@ def cpu_baseline(seconds: float, threads: int, name: str = "cql"):
     return k / el, k, el
 
 
+def _cpu_baseline_dcql(seconds: float, B: int, gen):
+    """K5 on the host: the oracle DiscreteCQL-IQN update + the reference
+    sampler restated (4-frame stacks) over 20k synthetic 84x84 frames."""
+    import torch
+    from oracle.discrete_cql import DiscreteCQLIQNOracle, IQNTaus, PixelBatch
+    from oracle.gather import gather, random_indices, to_episodes, to_transitions
+    rs = np.random.RandomState(0)
+    n = 20_000
+    frames = rs.randint(0, 256, size=(n, 1, 84, 84), dtype=np.uint8)
+    act = rs.randint(4, size=n).astype(np.int32)
+    rew = rs.randint(-1, 2, size=n).astype(np.float32)
+    term = np.zeros(n, dtype=np.float32)
+    term[1999::2000] = 1.0
+    trans = []
+    for o, a, r, t in to_episodes(frames, act, rew, term):
+        trans += to_transitions(o, a, r, t)
+    orc = DiscreteCQLIQNOracle((4, 84, 84), 4, seed=0)
+    np.random.seed(0)
+
+    def step():
+        idx = random_indices(len(trans), B)
+        b = gather([trans[i] for i in idx], n_frames=4)
+        pb = PixelBatch(torch.from_numpy(b["observations"]),
+                        torch.from_numpy(np.asarray(b["actions"])).long().view(-1),
+                        torch.from_numpy(b["rewards"]), torch.from_numpy(b["next_observations"]),
+                        torch.from_numpy(b["terminals"]), torch.from_numpy(b["n_steps"]))
+        orc.update(pb, IQNTaus.draw(gen, B, 64))
+
+    step()
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        step()
+        k += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return k / el, k, el
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -196,8 +250,9 @@ def main():
     ap.add_argument("--algo", choices=sorted(WORKLOADS), default="cql",
                     help="cql = the BASELINE.json headline (K2); td3bc = K1 shapes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(os.path.dirname(
-        os.path.abspath(__file__)), "profiles", "r01_pmc_traffic.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary of the dominant kernel (tools/pmc_pass.sh); default "
+                         "profiles/r01_pmc_traffic_<algo>.json")
     args = ap.parse_args()
 
     import torch
@@ -219,7 +274,7 @@ def main():
     names, vals = algo.impl.read_metrics_ring(None)
     # NaN in a column marks "not computed at this step" (TD3+BC's delayed
     # actor); every step computes critic_loss
-    ci = names.index("critic_loss")
+    ci = names.index("critic_loss") if "critic_loss" in names else names.index("loss")
     finite = bool(np.isfinite(vals[:, ci]).all() and np.isfinite(vals[~np.isnan(vals)]).all())
 
     wsp = next(iter(algo.impl._ws.values()))
@@ -233,6 +288,9 @@ def main():
     peak_tflops = 157.3  # MI355X FP32 MFMA dense peak (MI355X_MICROARCH.md)
     achieved = kflops / kern_s / 1e12
     traffic = None
+    if args.traffic_json is None:
+        args.traffic_json = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                         f"r01_pmc_traffic_{args.algo}.json")
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
@@ -248,7 +306,9 @@ def main():
                 "td3bc": "TD3+BC update (torch CPU, op-for-op restatement of "
                          "td3_plus_bc_impl.py/td3_impl.py/ddpg_impl.py, standard scaler)",
                 "bcq": "BCQ update (torch CPU, op-for-op restatement of bcq_impl.py/"
-                       "ddpg_impl.py, QR critics)"}[args.algo]
+                       "ddpg_impl.py, QR critics)",
+                "dcql": "DiscreteCQL-IQN update (torch CPU, op-for-op restatement of "
+                        "dqn_impl.py/cql_impl.py/iqn_q_function.py, pixel encoder)"}[args.algo]
         cpu = {"value": round(sps, 3), "unit": "gradient-steps/s", "cores": threads,
                "kind": "port",
                "sample": f"oracle {what} + reference host sampler restated "
@@ -259,7 +319,8 @@ def main():
     shape, batch, wdesc = WORKLOADS[args.algo]
     metric = {"cql": "gradient-steps/sec (CQL, batch=256, obs=11 act=3) at 1/2/4/8 GPU",
               "td3bc": "gradient-steps/sec (TD3+BC, batch=100, obs=3 act=1)",
-              "bcq": "gradient-steps/sec (BCQ QR-200, batch=256, obs=17 act=6)"}[args.algo]
+              "bcq": "gradient-steps/sec (BCQ QR-200, batch=256, obs=17 act=6)",
+              "dcql": "gradient-steps/sec (DiscreteCQL-IQN, batch=512, 4x84x84 pixels)"}[args.algo]
     out = {
         "metric": metric,
         "value": round(value, 2),
@@ -272,8 +333,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": f"synthetic (D4RL {shape} shapes, {args.transitions} transitions, "
-                "HBM-resident)",
+        "data": (f"synthetic (D4RL {shape} shapes, {args.transitions} transitions, "
+                 "HBM-resident)" if shape != "atari" else
+                 f"synthetic Atari-shaped uint8 frames ({args.transitions} x 1x84x84, "
+                 "HBM-resident, 4-frame stacks gathered on device)"),
         "config": {"workload": wdesc,
                    "global_batch": batch * ws, "parallelism": f"replicas x{ws}",
                    "losses_finite": finite},

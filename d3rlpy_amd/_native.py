@@ -235,6 +235,66 @@ class BcqActorDesc(C.Structure):
     ]
 
 
+IQN_MAX_ACTIONS = 18
+IQN_MAX_GROUPS = 8
+
+
+class Im2colDesc(C.Structure):
+    _fields_ = [
+        ("x_u8", vp), ("x_f32", vp),
+        ("B", C.c_int32), ("C", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
+        ("KH", C.c_int32), ("KW", C.c_int32), ("S", C.c_int32), ("OH", C.c_int32),
+        ("OW", C.c_int32), ("col", vp), ("ldcol", C.c_int64),
+    ]
+
+
+class Col2imDesc(C.Structure):
+    _fields_ = [
+        ("dcol", vp), ("ldcol", C.c_int64), ("mask", vp), ("dx", vp),
+        ("B", C.c_int32), ("C", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
+        ("KH", C.c_int32), ("KW", C.c_int32), ("S", C.c_int32), ("OH", C.c_int32),
+        ("OW", C.c_int32),
+    ]
+
+
+class TransposeDesc(C.Structure):
+    _fields_ = [
+        ("src", vp), ("dst", vp), ("mask", vp),
+        ("B", C.c_int32), ("P", C.c_int32), ("C", C.c_int32), ("to_cp", C.c_int32),
+    ]
+
+
+class IqnPriorDesc(C.Structure):
+    _fields_ = [("taus", vp), ("prior", vp), ("rows", C.c_int64), ("E", C.c_int32)]
+
+
+class IqnHeadDesc(C.Structure):
+    _fields_ = [
+        ("h", vp * IQN_MAX_GROUPS), ("phi", vp), ("Wf", vp), ("bf", vp), ("q", vp),
+        ("rows", C.c_int64), ("group_rows", C.c_int64),
+        ("K", C.c_int32), ("F", C.c_int32), ("A", C.c_int32),
+    ]
+
+
+class IqnLossDesc(C.Structure):
+    _fields_ = [
+        ("q_loss", vp), ("q_next", vp), ("q_targ", vp),
+        ("act", vp), ("rew", vp), ("term", vp), ("n_steps", vp), ("taus_loss", vp),
+        ("dq", vp), ("loss_b", vp), ("cons_b", vp), ("metrics", vp),
+        ("B", C.c_int32), ("K", C.c_int32), ("A", C.c_int32),
+        ("gamma", C.c_float), ("alpha", C.c_float),
+    ]
+
+
+class IqnHeadBwdDesc(C.Structure):
+    _fields_ = [
+        ("h", vp), ("phi", vp), ("dq", vp), ("Wf", vp),
+        ("dphi", vp), ("dh", vp), ("dWf_part", vp), ("dbf_part", vp),
+        ("B", C.c_int32), ("K", C.c_int32), ("F", C.c_int32), ("A", C.c_int32),
+        ("G", C.c_int32),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "d3a_abi_version": (C.c_int, []),
@@ -262,6 +322,13 @@ _SIGNATURES = {
     "d3a_sac_actor_head": (C.c_int, [C.POINTER(SacActorHeadDesc), vp]),
     "d3a_gather_batch": (C.c_int, [C.POINTER(GatherDesc), vp]),
     "d3a_mlp_fwd": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
+    "d3a_im2col": (C.c_int, [C.POINTER(Im2colDesc), vp]),
+    "d3a_col2im": (C.c_int, [C.POINTER(Col2imDesc), vp]),
+    "d3a_iqn_transpose": (C.c_int, [C.POINTER(TransposeDesc), vp]),
+    "d3a_iqn_prior": (C.c_int, [C.POINTER(IqnPriorDesc), vp]),
+    "d3a_iqn_head_fwd": (C.c_int, [C.POINTER(IqnHeadDesc), vp]),
+    "d3a_iqn_loss": (C.c_int, [C.POINTER(IqnLossDesc), vp]),
+    "d3a_iqn_head_bwd": (C.c_int, [C.POINTER(IqnHeadBwdDesc), vp]),
     "d3a_bcq_rows": (C.c_int, [C.POINTER(BcqRowsDesc), vp]),
     "d3a_bcq_vae_sample": (C.c_int, [C.POINTER(BcqVaeDesc), vp]),
     "d3a_bcq_vae_loss": (C.c_int, [C.POINTER(BcqVaeDesc), vp]),

@@ -3,18 +3,23 @@
 Only the algorithms on the accelerated hot path are provided.
 """
 from .bcq import BCQ
-from .cql import CQL
+from .cql import CQL, DiscreteCQL
 from .td3_plus_bc import TD3PlusBC
 
-__all__ = ["BCQ", "CQL", "TD3PlusBC", "get_algo"]
+__all__ = ["BCQ", "CQL", "DiscreteCQL", "TD3PlusBC", "get_algo"]
 
 ALGO_LIST = {"bcq": BCQ, "cql": CQL, "td3_plus_bc": TD3PlusBC}
+
+
+DISCRETE_ALGO_LIST = {"cql": DiscreteCQL}
 
 
 def get_algo(name: str, discrete: bool):
     """algos/__init__.py:66-85 for the algorithms available here."""
     if discrete:
-        raise ValueError(f"discrete {name} is not available on the HIP engine")
+        if name not in DISCRETE_ALGO_LIST:
+            raise ValueError(f"discrete {name} is not available on the HIP engine")
+        return DISCRETE_ALGO_LIST[name]
     if name not in ALGO_LIST:
         raise ValueError(f"{name} is not available on the HIP engine")
     return ALGO_LIST[name]

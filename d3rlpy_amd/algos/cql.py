@@ -13,6 +13,7 @@ from ..constants import ActionSpace
 from ..factories import AdamFactory, OptimizerFactory, check_encoder, check_q_func, check_use_gpu
 from .base import AlgoBase
 from .cql_impl import CQLImpl
+from .discrete_cql_impl import DiscreteCQLImpl
 
 
 class CQL(AlgoBase):
@@ -121,6 +122,77 @@ class CQL(AlgoBase):
 
     def get_action_type(self) -> ActionSpace:
         return ActionSpace.CONTINUOUS
+
+
+class DiscreteCQL(AlgoBase):
+    """algos/cql.py:265-375 with the HIP DiscreteCQLImpl (IQN Q-function on
+    pixels, K5).  Constructor defaults are the reference's (:316-333);
+    ``_update`` = DQN._update (algos/dqn.py:127-132): one update, and the
+    target hard sync every ``target_update_interval`` steps (folded into the
+    update's last launch)."""
+
+    def __init__(
+        self,
+        *,
+        learning_rate: float = 6.25e-5,
+        optim_factory: OptimizerFactory = AdamFactory(),
+        encoder_factory="default",
+        q_func_factory="mean",
+        batch_size: int = 32,
+        n_frames: int = 1,
+        n_steps: int = 1,
+        gamma: float = 0.99,
+        n_critics: int = 1,
+        target_update_interval: int = 8000,
+        alpha: float = 1.0,
+        use_gpu=False,
+        scaler=None,
+        reward_scaler=None,
+        impl: Optional[DiscreteCQLImpl] = None,
+        **kwargs: Any,
+    ):
+        super().__init__(batch_size=batch_size, n_frames=n_frames, n_steps=n_steps, gamma=gamma,
+                         scaler=scaler, action_scaler=None, reward_scaler=reward_scaler,
+                         kwargs=kwargs)
+        self._learning_rate = learning_rate
+        self._optim_factory = optim_factory
+        self._encoder_factory = check_encoder(encoder_factory)
+        self._q_func_factory = check_q_func(q_func_factory)
+        self._n_critics = n_critics
+        self._target_update_interval = target_update_interval
+        self._alpha = alpha
+        self._use_gpu = use_gpu
+        self._impl = impl
+
+    def _create_impl(self, observation_shape: Sequence[int], action_size: int) -> None:
+        self._impl = DiscreteCQLImpl(
+            observation_shape=observation_shape,
+            action_size=action_size,
+            learning_rate=self._learning_rate,
+            optim_factory=self._optim_factory,
+            encoder_factory=_resolve(self._encoder_factory, observation_shape),
+            q_func_factory=self._q_func_factory,
+            gamma=self._gamma,
+            n_critics=self._n_critics,
+            alpha=self._alpha,
+            use_gpu=self._use_gpu,
+            scaler=self._scaler,
+            reward_scaler=self._reward_scaler,
+        )
+        self._impl.build()
+
+    def _sync_target(self) -> bool:
+        return self._grad_step % self._target_update_interval == 0
+
+    def _update(self, batch) -> Dict[str, float]:
+        m = self._impl.update_step(batch, update_target=self._sync_target(), sync=True)
+        return {"loss": m["loss"]}
+
+    def _update_async(self, batch) -> None:
+        self._impl.update_step(batch, update_target=self._sync_target(), sync=False)
+
+    def get_action_type(self) -> ActionSpace:
+        return ActionSpace.DISCRETE
 
 
 def _resolve(factory, observation_shape):

@@ -1,0 +1,527 @@
+"""DiscreteCQLImpl on HIP kernels with an IQN Q-function on pixels — drop-in for
+d3rlpy/algos/torch/cql_impl.py:246-302 (DiscreteCQLImpl) and what it inherits
+(DoubleDQNImpl / DQNImpl, algos/torch/dqn_impl.py:27-171), for the K5
+configuration: Nature-DQN PixelEncoder, DiscreteIQNQFunction
+(n_quantiles 64, embed 64), n_critics 1, pixel scaler.
+
+One ``update`` (dqn_impl.py:97-111) on the device:
+  1  Philox taus for the five IQN evaluations of the step
+     (next-online argmax, next-target, loss, logsumexp, data values)
+  2  online encoder over [obs; next_obs] (2B samples), target encoder over
+     next_obs: im2col (uint8 -> /255 fused) + GEMM per conv, NHWC -> NCHW
+     flatten, fc
+  3  IQN head: cos prior, embed GEMM + ReLU, (h * phi) . W_fc per row —
+     online rows [loss | lse | data | next] in one pass, target rows in another
+  4  d3a_iqn_loss: Double-DQN target, per-sample-tau quantile Huber loss,
+     conservative logsumexp term, dL/dq
+  5  head backward (d3a_iqn_head_bwd), embed weight gradient, encoder backward
+     (fc, conv3, conv2 via col2im, conv1 weight gradient), Adam
+  6  d3a_step_end: metrics ring, step counter, and on target-update steps the
+     hard sync (tau = 1 copy, dqn_impl.py:146-149)
+Encoder forwards on identical (params, input) are evaluated once: the three
+online evaluations of obs share one encoder pass and its one backward.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+from torch import nn
+
+from .. import _native as NAT
+from .. import checkpoint as ckpt
+from .. import mlp, ops
+from ..nets import AdamGroup, GradSpace, OptimState, ParamStore
+from .impl_base import DeviceBatch, ImplBase, as_device_batch
+
+METRIC_NAMES = ("loss", "td_loss", "conservative_loss")
+FILTERS = ((32, 8, 4), (64, 4, 2), (64, 3, 1))
+
+
+def _geometry(obs_shape: Sequence[int]) -> List[Tuple[int, int, int, int, int, int, int]]:
+    """Per conv: (C_in, H, W, C_out, K, S, OH) with square inputs/kernels."""
+    c, h, w = obs_shape
+    out = []
+    for co, k, s in FILTERS:
+        oh, ow = (h - k) // s + 1, (w - k) // s + 1
+        out.append((c, h, w, co, k, s, oh, ow))
+        c, h, w = co, oh, ow
+    return out
+
+
+class DiscreteCQLImpl(ImplBase):
+    def __init__(
+        self,
+        observation_shape: Sequence[int],
+        action_size: int,
+        learning_rate: float,
+        optim_factory,
+        encoder_factory,
+        q_func_factory,
+        gamma: float,
+        n_critics: int,
+        alpha: float,
+        use_gpu,
+        scaler,
+        reward_scaler,
+    ):
+        super().__init__(observation_shape, action_size, scaler, None, reward_scaler, use_gpu)
+        if q_func_factory.get_type() != "iqn":
+            raise NotImplementedError("DiscreteCQL on HIP implements the IQN Q-function of K5")
+        if len(observation_shape) != 3:
+            raise NotImplementedError("DiscreteCQL on HIP supports pixel observations")
+        if scaler is None or scaler.get_type() != "pixel":
+            raise NotImplementedError("DiscreteCQL on HIP expects the pixel scaler")
+        if n_critics != 1 or reward_scaler is not None:
+            raise NotImplementedError("n_critics = 1 and no reward scaler (K5)")
+        if action_size > NAT.IQN_MAX_ACTIONS:
+            raise NotImplementedError(f"at most {NAT.IQN_MAX_ACTIONS} actions")
+        if getattr(encoder_factory, "TYPE", "pixel") != "pixel" or \
+                [list(f) for f in encoder_factory.filters] != [list(f) for f in FILTERS] or \
+                getattr(encoder_factory, "_use_batch_norm", False) or \
+                getattr(encoder_factory, "_dropout_rate", None) is not None:
+            raise NotImplementedError("the Nature-DQN PixelEncoder without batch norm / "
+                                      "dropout (K5) is implemented")
+        self._learning_rate = learning_rate
+        self._optim_factory = optim_factory
+        self._encoder_factory = encoder_factory
+        self._q_func_factory = q_func_factory
+        self._gamma = gamma
+        self._n_critics = n_critics
+        self._alpha = alpha
+        self._K = q_func_factory.n_quantiles
+        self._K_greedy = q_func_factory.n_greedy_quantiles
+        self._E = q_func_factory.embed_size
+        self._F = encoder_factory.feature_size
+        self._ws: Dict[int, "_Workspace"] = {}
+
+    # ------------------------------------------------------------------ build
+    def build(self) -> None:
+        dev = self.torch_device
+        A, F, E = self._action_size, self._F, self._E
+        self.geom = _geometry(self._observation_shape)
+        st = ParamStore()
+        self.conv_names = []
+        for l, (ci, h, w, co, k, s, oh, ow) in enumerate(self.geom):
+            st.add(f"enc.c{l}.W", (1, co, ci, k, k))
+            st.add(f"enc.c{l}.b", (1, co))
+            self.conv_names.append((f"enc.c{l}.W", f"enc.c{l}.b"))
+        ci, h, w, co, k, s, oh, ow = self.geom[-1]
+        self.flat = co * oh * ow
+        st.add("enc.fc.W", (1, F, self.flat))
+        st.add("enc.fc.b", (1, F))
+        st.add("q.fc.W", (1, A, F))
+        st.add("q.fc.b", (1, A))
+        st.add("q.embed.W", (1, F, E))
+        st.add("q.embed.b", (1, F))
+        st.allocate(dev)
+        self.store = st
+        self._init_like_reference()
+        self.targ = st.like()
+        self.targ.data.copy_(st.data)
+        self.counters = torch.zeros(8, dtype=torch.int64, device=dev)
+        f = self._optim_factory
+        self.names = list(st.specs)
+        self.optim_state = OptimState(st, self.names, self._learning_rate, f.betas, f.eps,
+                                      step=self.counters[0:1])
+
+    def _init_like_reference(self) -> None:
+        """nn.Conv2d / nn.Linear default init in the reference construction order
+        (PixelEncoder convs, its fc, then the IQN _fc and _embed)."""
+        st = self.store
+        with torch.no_grad():
+            for l, (ci, h, w, co, k, s, oh, ow) in enumerate(self.geom):
+                conv = nn.Conv2d(ci, co, kernel_size=k, stride=s)
+                st.view(f"enc.c{l}.W")[0].copy_(conv.weight)
+                st.view(f"enc.c{l}.b")[0].copy_(conv.bias)
+            for name, (o, i) in (("enc.fc", (self._F, self.flat)),
+                                 ("q.fc", (self._action_size, self._F)),
+                                 ("q.embed", (self._F, self._E))):
+                lin = nn.Linear(i, o)
+                st.view(f"{name}.W")[0].copy_(lin.weight)
+                st.view(f"{name}.b")[0].copy_(lin.bias)
+
+    # ---------------------------------------------------------- checkpoints
+    def _refs(self):
+        """EnsembleDiscreteQFunction(DiscreteIQNQFunction).parameters() order."""
+        p = "_q_funcs.0."
+        refs = []
+        for l in range(len(self.geom)):
+            refs += [(f"{p}_encoder._convs.{l}.weight", f"enc.c{l}.W", 0, None),
+                     (f"{p}_encoder._convs.{l}.bias", f"enc.c{l}.b", 0, None)]
+        refs += [(f"{p}_encoder._fc.weight", "enc.fc.W", 0, None),
+                 (f"{p}_encoder._fc.bias", "enc.fc.b", 0, None),
+                 (f"{p}_fc.weight", "q.fc.W", 0, None), (f"{p}_fc.bias", "q.fc.b", 0, None),
+                 (f"{p}_embed.weight", "q.embed.W", 0, None),
+                 (f"{p}_embed.bias", "q.embed.b", 0, None)]
+        return refs
+
+    def get_state_dict(self) -> Dict[str, dict]:
+        torch.cuda.synchronize()
+        r = self._refs()
+        return {"_q_func": ckpt.module_state(self.store, r),
+                "_targ_q_func": ckpt.module_state(self.targ, r),
+                "_optim": ckpt.adam_state(self.optim_state, r)}
+
+    def set_state_dict(self, sd: Dict[str, dict]) -> None:
+        r = self._refs()
+        ckpt.load_module_state(self.store, r, sd["_q_func"])
+        ckpt.load_module_state(self.targ, r, sd["_targ_q_func"])
+        ckpt.load_adam_state(self.optim_state, r, sd["_optim"])
+        torch.cuda.synchronize()
+
+    def save_model(self, fname: str) -> None:
+        torch.save(self.get_state_dict(), fname)
+
+    def load_model(self, fname: str) -> None:
+        self.set_state_dict(torch.load(fname, map_location="cpu", weights_only=True))
+
+    # --------------------------------------------------------------- updates
+    def _workspace(self, B: int) -> "_Workspace":
+        ws = self._ws.get(B)
+        if ws is None:
+            if self._ws:
+                raise NotImplementedError("one batch size per DiscreteCQLImpl is supported")
+            ws = _Workspace(self, B)
+            self._ws[B] = ws
+        return ws
+
+    def update_step(self, batch, update_target: bool = False,
+                    taus: Optional[Dict[str, np.ndarray]] = None, sync: bool = True,
+                    use_graph: bool = True):
+        db = as_device_batch(batch, self.torch_device)
+        ws = self._workspace(db.batch_size)
+        ws.stage(db, taus)
+        ws.execute((bool(update_target),), use_graph=use_graph and taus is None)
+        if not sync:
+            return None
+        return {k: float(v) for k, v in zip(METRIC_NAMES, ws.metrics.cpu().numpy())}
+
+    def update(self, batch) -> np.ndarray:
+        """DQNImpl.update (dqn_impl.py:97-111): returns the loss."""
+        return np.float32(self.update_step(batch)["loss"])
+
+    def update_target(self) -> None:
+        """hard_sync (torch_utility.py:36-41)."""
+        self.targ.data.copy_(self.store.data)
+
+    # ------------------------------------------------- device-side batches
+    def staging_batch(self, batch_size: int) -> DeviceBatch:
+        ws = self._workspace(batch_size)
+        B = batch_size
+        return DeviceBatch(ws.obs2[:B], ws.act, ws.rew, ws.obs2[B:], ws.term, ws.nsteps)
+
+    def active_metric_names(self):
+        return ["loss"]
+
+    def metrics_ring(self, n_steps: int):
+        for ws in self._ws.values():
+            ws.ring_ctr.zero_()
+        return n_steps
+
+    def read_metrics_ring(self, handle):
+        if not self._ws:
+            return ["loss"], np.zeros((0, 1), dtype=np.float32)
+        ws = next(iter(self._ws.values()))
+        k = min(int(ws.ring_ctr.item()), ws.ring.shape[0])
+        return ["loss"], ws.ring[:k, :1].cpu().numpy()
+
+    # ------------------------------------------------------------- inference
+    def _as_input(self, x) -> torch.Tensor:
+        t = torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x)
+        assert t.ndim == 4, "Input must have batch dimension."
+        return t.to(self.torch_device).to(torch.uint8).contiguous()
+
+    def _q_values(self, x_u8: torch.Tensor) -> torch.Tensor:
+        """DiscreteIQNQFunction.forward in eval mode (n_greedy_quantiles
+        linspace taus, iqn_q_function.py:16-30): mean over quantiles, [B][A]."""
+        B = x_u8.shape[0]
+        Kg = self._K_greedy
+        enc = _EncoderPass(self, B, self.torch_device, keep=False)
+        enc.forward(x_u8.data_ptr(), self.store)
+        taus = torch.linspace(0, 1, Kg, device=x_u8.device).repeat(B)
+        head = _HeadPass(self, B * Kg, self.torch_device)
+        q = head.forward(taus, [enc.h.data_ptr()], B * Kg, Kg, self.store)
+        return q.view(B, Kg, -1).mean(dim=1)
+
+    def predict_best_action(self, x) -> np.ndarray:
+        with torch.no_grad():
+            return self._q_values(self._as_input(x)).argmax(dim=1).cpu().numpy()
+
+    def sample_action(self, x) -> np.ndarray:
+        return self.predict_best_action(x)
+
+    def predict_value(self, x, action, with_std: bool = False):
+        with torch.no_grad():
+            q = self._q_values(self._as_input(x))
+            a = torch.as_tensor(np.asarray(action), device=q.device).long().view(-1)
+            v = q[torch.arange(q.shape[0], device=q.device), a].cpu().numpy()
+            return (v, np.zeros_like(v)) if with_std else v
+
+    # ------------------------------------------------------------ inspection
+    def grad(self, name: str) -> torch.Tensor:
+        return next(iter(self._ws.values())).opt.grad(name)
+
+
+class _EncoderPass:
+    """Buffers + launches of one PixelEncoder forward over n samples (NHWC
+    activations, NCHW flatten), and its backward for the first nb samples."""
+
+    def __init__(self, impl: DiscreteCQLImpl, n: int, dev, keep: bool = True):
+        self.impl, self.n = impl, n
+        z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        self.cols, self.ys = [], []
+        for (ci, h, w, co, k, s, oh, ow) in impl.geom:
+            self.cols.append(z(n * oh * ow, ci * k * k))
+            self.ys.append(z(n * oh * ow, co))
+        self.yt = z(n, impl.flat)
+        self.h = z(n, impl._F)
+
+    def forward(self, x_u8: int, store: ParamStore) -> None:
+        impl = self.impl
+        n = self.n
+        for l, (ci, h, w, co, k, s, oh, ow) in enumerate(impl.geom):
+            d = NAT.Im2colDesc()
+            if l == 0:
+                d.x_u8 = x_u8
+            else:
+                d.x_f32 = self.ys[l - 1].data_ptr()
+            d.B, d.C, d.H, d.W, d.KH, d.KW, d.S, d.OH, d.OW = n, ci, h, w, k, k, s, oh, ow
+            d.col, d.ldcol = self.cols[l].data_ptr(), ci * k * k
+            ops.call_desc("d3a_im2col", d)
+            Wn, bn = impl.conv_names[l]
+            ops.linear_fwd(self.cols[l].data_ptr(), True, ci * k * k, store.ptr(Wn), store.ptr(bn),
+                           self.ys[l].data_ptr(), 1, n * oh * ow, ci * k * k, co, relu=True)
+        ci, h, w, co, k, s, oh, ow = impl.geom[-1]
+        t = NAT.TransposeDesc()
+        t.src, t.dst = self.ys[-1].data_ptr(), self.yt.data_ptr()
+        t.B, t.P, t.C, t.to_cp = n, oh * ow, co, 1
+        ops.call_desc("d3a_iqn_transpose", t)
+        ops.linear_fwd(self.yt.data_ptr(), True, impl.flat, store.ptr("enc.fc.W"),
+                       store.ptr("enc.fc.b"), self.h.data_ptr(), 1, n, impl.flat, impl._F,
+                       relu=True)
+
+
+class _HeadPass:
+    """IQN head forward buffers over `rows` quantile rows."""
+
+    def __init__(self, impl: DiscreteCQLImpl, rows: int, dev):
+        self.impl = impl
+        z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        self.prior = z(rows, impl._E)
+        self.phi = z(rows, impl._F)
+        self.q = z(rows, impl._action_size)
+        self.rows = rows
+
+    def launch(self, taus_ptr: int, h_groups: List[int], group_rows: int, K: int,
+               store: ParamStore) -> None:
+        impl = self.impl
+        p = NAT.IqnPriorDesc()
+        p.taus, p.prior, p.rows, p.E = taus_ptr, self.prior.data_ptr(), self.rows, impl._E
+        ops.call_desc("d3a_iqn_prior", p)
+        ops.linear_fwd(self.prior.data_ptr(), True, impl._E, store.ptr("q.embed.W"),
+                       store.ptr("q.embed.b"), self.phi.data_ptr(), 1, self.rows, impl._E,
+                       impl._F, relu=True)
+        d = NAT.IqnHeadDesc()
+        for g, hp in enumerate(h_groups):
+            d.h[g] = hp
+        d.phi, d.Wf, d.bf, d.q = (self.phi.data_ptr(), store.ptr("q.fc.W"), store.ptr("q.fc.b"),
+                                  self.q.data_ptr())
+        d.rows, d.group_rows = self.rows, group_rows
+        d.K, d.F, d.A = K, impl._F, impl._action_size
+        ops.call_desc("d3a_iqn_head_fwd", d)
+
+    def forward(self, taus: torch.Tensor, h_groups: List[int], group_rows: int, K: int,
+                store: ParamStore) -> torch.Tensor:
+        self.launch(taus.contiguous().data_ptr(), h_groups, group_rows, K, store)
+        return self.q
+
+
+class _Workspace:
+    def __init__(self, impl: DiscreteCQLImpl, B: int):
+        dev = impl.torch_device
+        self.impl = impl
+        self.B = B
+        K, A, F, E = impl._K, impl._action_size, impl._F, impl._E
+        BK = B * K
+        obs_shape = impl._observation_shape
+        self.obs2 = torch.zeros((2 * B,) + tuple(obs_shape), dtype=torch.uint8, device=dev)
+        self.act = torch.zeros(B, dtype=torch.int32, device=dev)
+        z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        self.rew, self.term, self.nsteps = z(B), z(B), z(B)
+        # taus [5][B][K]: loss | cons_lse | cons_data | next_online | next_target
+        self.taus = z(5, B, K)
+        self.rng_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.rng_ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.seed = int(torch.randint(0, 2**62, (1,)).item())
+        self.enc = _EncoderPass(impl, 2 * B, dev)      # online: [obs; next_obs]
+        self.enc_t = _EncoderPass(impl, B, dev)        # target: next_obs
+        self.head = _HeadPass(impl, 4 * BK, dev)       # online rows [loss|lse|data|next]
+        self.head_t = _HeadPass(impl, BK, dev)         # target rows
+        self.dq = z(3 * BK, A)
+        self.loss_b, self.cons_b = z(B), z(B)
+        self.metrics = z(len(METRIC_NAMES))
+        self.ring = z(1 << 16, len(METRIC_NAMES))
+        self.ring_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        # backward buffers (obs samples only)
+        self.dphi = z(3 * BK, F)
+        self.dzfc = z(B, F)
+        self.dyt = z(B, impl.flat)
+        self.dys = [z(B * oh * ow, co) for (ci, h, w, co, k, s, oh, ow) in impl.geom]
+        self.dcols = [None] + [z(B * oh * ow, ci * k * k)
+                               for (ci, h, w, co, k, s, oh, ow) in impl.geom[1:]]
+        # gradients: split-K partials for the GEMM weight gradients, per-row
+        # partials (B) for the IQN fc
+        self.grads = GradSpace(dev)
+        self.splits = {}
+        for l, (ci, h, w, co, k, s, oh, ow) in enumerate(impl.geom):
+            S = mlp.n_splits(B * oh * ow)
+            self.splits[l] = S
+            self.grads.add(f"enc.c{l}.W", (1, co, ci, k, k), S)
+            self.grads.add(f"enc.c{l}.b", (1, co), S)
+        self.S_fc = mlp.n_splits(B)
+        self.grads.add("enc.fc.W", (1, F, impl.flat), self.S_fc)
+        self.grads.add("enc.fc.b", (1, F), self.S_fc)
+        self.grads.add("q.fc.W", (1, A, F), B)
+        self.grads.add("q.fc.b", (1, A), B)
+        self.S_emb = mlp.n_splits(3 * BK)
+        self.grads.add("q.embed.W", (1, F, E), self.S_emb)
+        self.grads.add("q.embed.b", (1, F), self.S_emb)
+        self.opt = AdamGroup(impl.optim_state, self.grads)
+        self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._ran_eager = set()
+        self._external_taus = False
+        self._build_descs()
+
+    def _build_descs(self):
+        impl = self.impl
+        B, K, A, F = self.B, impl._K, impl._action_size, impl._F
+        BK = B * K
+        l = NAT.IqnLossDesc()
+        q = self.head.q
+        l.q_loss = q.data_ptr()                       # rows [0, 3BK)
+        l.q_next = q.data_ptr() + 4 * 3 * BK * A      # rows [3BK, 4BK)
+        l.q_targ = self.head_t.q.data_ptr()
+        l.act, l.rew, l.term, l.n_steps = (self.act.data_ptr(), self.rew.data_ptr(),
+                                           self.term.data_ptr(), self.nsteps.data_ptr())
+        l.taus_loss = self.taus.data_ptr()
+        l.dq, l.loss_b, l.cons_b, l.metrics = (self.dq.data_ptr(), self.loss_b.data_ptr(),
+                                               self.cons_b.data_ptr(), self.metrics.data_ptr())
+        l.B, l.K, l.A, l.gamma, l.alpha = B, K, A, impl._gamma, impl._alpha
+        self.loss_desc = l
+        hb = NAT.IqnHeadBwdDesc()
+        hb.h, hb.phi, hb.dq = self.enc.h.data_ptr(), self.head.phi.data_ptr(), self.dq.data_ptr()
+        hb.Wf = impl.store.ptr("q.fc.W")
+        hb.dphi, hb.dh = self.dphi.data_ptr(), self.dzfc.data_ptr()
+        hb.dWf_part = self.grads.get("q.fc.W").data_ptr()
+        hb.dbf_part = self.grads.get("q.fc.b").data_ptr()
+        hb.B, hb.K, hb.F, hb.A, hb.G = B, K, F, A, 3
+        self.head_bwd_desc = hb
+
+    def stage(self, db: DeviceBatch, taus) -> None:
+        B = self.B
+        if db.obs.data_ptr() != self.obs2.data_ptr():
+            self.obs2[:B].copy_(db.obs.view_as(self.obs2[:B]), non_blocking=True)
+            self.obs2[B:].copy_(db.next_obs.view_as(self.obs2[B:]), non_blocking=True)
+            self.act.copy_(db.act.view(B).to(torch.int32), non_blocking=True)
+            self.rew.copy_(db.rew.view(B), non_blocking=True)
+            self.term.copy_(db.term.view(B), non_blocking=True)
+            self.nsteps.copy_(db.n_steps.view(B), non_blocking=True)
+        self._external_taus = taus is not None
+        if taus is not None:
+            order = ("loss", "cons_lse", "cons_data", "next_online", "next_target")
+            for i, k in enumerate(order):
+                self.taus[i].copy_(torch.as_tensor(np.asarray(taus[k]), dtype=torch.float32)
+                                   .view(B, -1))
+
+    def dominant_kernel(self):
+        """The first conv GEMM of the online encoder over [obs; next_obs]
+        (2B x 400 output positions x 32 filters x 256 taps): the largest GEMM
+        of the step."""
+        impl = self.impl
+        ci, h, w, co, k, s, oh, ow = impl.geom[0]
+        rows = 2 * self.B * oh * ow
+        col, y = self.enc.cols[0], self.enc.ys[0]
+        Wn, bn = impl.conv_names[0]
+
+        def launch():
+            ops.linear_fwd(col.data_ptr(), True, ci * k * k, impl.store.ptr(Wn),
+                           impl.store.ptr(bn), y.data_ptr(), 1, rows, ci * k * k, co, relu=True)
+        return launch, 2 * rows * ci * k * k * co, (f"gemm_f32 conv1 (im2col): [{rows}x"
+                                                    f"{ci * k * k}]@[{ci * k * k}x{co}]")
+
+    def execute(self, flags, use_graph: bool) -> None:
+        key = tuple(flags) + (self._external_taus,)
+        if not use_graph:
+            self._enqueue(*flags)
+            return
+        g = self._graphs.get(key)
+        if g is None:
+            if key not in self._ran_eager:
+                self._ran_eager.add(key)
+                self._enqueue(*flags)
+                return
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g):
+                self._enqueue(*flags)
+            self._graphs[key] = g
+        g.replay()
+
+    def _enqueue(self, sync_target: bool) -> None:
+        impl = self.impl
+        B, K, A, F, E = self.B, impl._K, impl._action_size, impl._F, impl._E
+        BK = B * K
+        st, tg = impl.store, impl.targ
+        if not self._external_taus:
+            ops.philox_fill(self.taus, 0, self.taus.numel(), 0.0, 1.0, self.seed, self.rng_ctr,
+                            self.rng_ticket)
+        # encoders
+        self.enc.forward(self.obs2.data_ptr(), st)
+        self.enc_t.forward(self.obs2.data_ptr() + self.obs2[0].numel() * B, tg)
+        h_obs = self.enc.h.data_ptr()
+        h_next = h_obs + 4 * B * F
+        # IQN heads: online rows [loss | lse | data | next], target rows
+        self.head.launch(self.taus.data_ptr(), [h_obs, h_obs, h_obs, h_next], BK, K, st)
+        self.head_t.launch(self.taus.data_ptr() + 4 * 4 * BK, [self.enc_t.h.data_ptr()], BK, K,
+                           tg)
+        ops.call_desc("d3a_iqn_loss", self.loss_desc)
+        # backward: head, embed, encoder (obs samples)
+        ops.call_desc("d3a_iqn_head_bwd", self.head_bwd_desc)
+        g = self.grads
+        ops.linear_bwd_w(self.dphi.data_ptr(), F, 3 * BK * F, self.head.prior.data_ptr(), E,
+                         3 * BK * E, g.get("q.embed.W").data_ptr(), 1, 3 * BK, E, F, self.S_emb,
+                         db=g.get("q.embed.b").data_ptr())
+        ops.linear_bwd_w(self.dzfc.data_ptr(), F, B * F, self.enc.yt.data_ptr(), impl.flat,
+                         B * impl.flat, g.get("enc.fc.W").data_ptr(), 1, B, impl.flat, F,
+                         self.S_fc, db=g.get("enc.fc.b").data_ptr())
+        ops.linear_bwd_x(self.dzfc.data_ptr(), F, B * F, st.ptr("enc.fc.W"), self.dyt.data_ptr(),
+                         impl.flat, B * impl.flat, 1, B, impl.flat, F)
+        ci, h, w, co, k, s, oh, ow = impl.geom[-1]
+        t = NAT.TransposeDesc()
+        t.src, t.dst, t.mask = self.dyt.data_ptr(), self.dys[-1].data_ptr(), \
+            self.enc.ys[-1].data_ptr()
+        t.B, t.P, t.C, t.to_cp = B, oh * ow, co, 0
+        ops.call_desc("d3a_iqn_transpose", t)
+        for l in range(len(impl.geom) - 1, -1, -1):
+            ci, h, w, co, k, s, oh, ow = impl.geom[l]
+            rows, Kc = B * oh * ow, ci * k * k
+            Wn, bn = impl.conv_names[l]
+            ops.linear_bwd_w(self.dys[l].data_ptr(), co, rows * co, self.enc.cols[l].data_ptr(),
+                             Kc, rows * Kc, g.get(Wn).data_ptr(), 1, rows, Kc, co,
+                             self.splits[l], db=g.get(bn).data_ptr())
+            if l > 0:
+                ops.linear_bwd_x(self.dys[l].data_ptr(), co, rows * co, st.ptr(Wn),
+                                 self.dcols[l].data_ptr(), Kc, rows * Kc, 1, rows, Kc, co)
+                c2 = NAT.Col2imDesc()
+                c2.dcol, c2.ldcol = self.dcols[l].data_ptr(), Kc
+                c2.mask = self.enc.ys[l - 1].data_ptr()
+                c2.dx = self.dys[l - 1].data_ptr()
+                c2.B, c2.C, c2.H, c2.W = B, ci, h, w
+                c2.KH, c2.KW, c2.S, c2.OH, c2.OW = k, k, s, oh, ow
+                ops.call_desc("d3a_col2im", c2)
+        self.opt.launch()
+        ops.step_end(impl.counters, 1, self.metrics, self.ring, self.ring_ctr,
+                     tg.data if sync_target else None, st.data if sync_target else None,
+                     1.0)

@@ -116,6 +116,14 @@ class PixelEncoderFactory(EncoderFactory):
         self._use_batch_norm = use_batch_norm
         self._dropout_rate = dropout_rate
 
+    @property
+    def filters(self):
+        return [list(f) for f in self._filters]
+
+    @property
+    def feature_size(self) -> int:
+        return self._feature_size
+
     def get_params(self, deep: bool = False) -> Dict[str, Any]:
         return {"filters": copy.deepcopy(self._filters), "feature_size": self._feature_size,
                 "activation": self._activation, "use_batch_norm": self._use_batch_norm,

@@ -501,6 +501,88 @@ typedef struct d3a_bcq_actor_desc {
 } d3a_bcq_actor_desc;
 int d3a_bcq_actor_head(const d3a_bcq_actor_desc* d, void* stream);
 
+/* ---- DiscreteCQL + IQN on pixels (K5).  Convolutions are d3a_gemm_f32 over
+ * im2col matrices; activations are NHWC (the GEMM's row-major output). ---- */
+
+/* col[(b, oy, ox)][c*KH*KW + kh*KW + kw] = x[b, c, S*oy + kh, S*ox + kw]:
+ * x_u8 NCHW uint8 scaled by 1/255 (PixelScaler.transform, scalers.py:109-110;
+ * the first conv of PixelEncoder, encoders.py:130-136) or x_f32 NHWC. */
+typedef struct d3a_im2col_desc {
+  const uint8_t* x_u8; const float* x_f32;
+  int32_t B, C, H, W, KH, KW, S, OH, OW;
+  float* col; int64_t ldcol;
+} d3a_im2col_desc;
+int d3a_im2col(const d3a_im2col_desc* d, void* stream);
+
+/* Deterministic (gather-form) col2im: dx[b][y][x][c] = sum of the dcol
+ * entries whose window covers (y, x), times [mask > 0] (the producing
+ * layer's ReLU) — the autograd of nn.Conv2d's input (encoders.py:130-136). */
+typedef struct d3a_col2im_desc {
+  const float* dcol; int64_t ldcol;
+  const float* mask;
+  float* dx;
+  int32_t B, C, H, W, KH, KW, S, OH, OW;
+} d3a_col2im_desc;
+int d3a_col2im(const d3a_col2im_desc* d, void* stream);
+
+/* Per-sample [P][C] (NHWC) <-> [C][P] (NCHW) transpose, optional [mask > 0]
+ * in the destination layout: the flatten before PixelEncoder._fc
+ * (encoders.py:157) and its gradient. */
+typedef struct d3a_transpose_desc {
+  const float* src; float* dst; const float* mask;
+  int32_t B, P, C, to_cp;
+} d3a_transpose_desc;
+int d3a_iqn_transpose(const d3a_transpose_desc* d, void* stream);
+
+/* prior[r][i] = cos(pi (i + 1) tau[r]), i < E (compute_iqn_feature,
+ * iqn_q_function.py:33-44). */
+typedef struct d3a_iqn_prior_desc {
+  const float* taus; float* prior; int64_t rows; int32_t E;
+} d3a_iqn_prior_desc;
+int d3a_iqn_prior(const d3a_iqn_prior_desc* d, void* stream);
+
+#define D3A_IQN_MAX_ACTIONS 18
+#define D3A_IQN_MAX_GROUPS 8
+/* q[r][a] = (h[b] * phi[r]) . Wf[a] + bf[a] (compute_iqn_feature's product
+ * + DiscreteIQNQFunction._fc, iqn_q_function.py:45-47, 82-88).  Rows come in
+ * groups of group_rows = B*K; group g reads its features from h[g]
+ * (b = (r mod group_rows) / K). */
+typedef struct d3a_iqn_head_desc {
+  const float* h[D3A_IQN_MAX_GROUPS];
+  const float* phi; const float* Wf; const float* bf; float* q;
+  int64_t rows, group_rows;
+  int32_t K, F, A;
+} d3a_iqn_head_desc;
+int d3a_iqn_head_fwd(const d3a_iqn_head_desc* d, void* stream);
+
+/* DiscreteCQL loss on IQN quantiles, one workgroup per row b
+ * (DoubleDQNImpl.compute_target dqn_impl.py:162-171; DiscreteIQNQFunction.
+ * compute_error iqn_q_function.py:95-118 with per-sample taus; DiscreteCQLImpl.
+ * compute_loss / _compute_conservative_loss cql_impl.py:279-302):
+ *   q_loss [3][B*K][A] online quantiles on obs (loss | logsumexp | data taus)
+ *   q_next [B*K][A] online on next_obs (argmax), q_targ [B*K][A] target
+ * -> dq [3][B*K][A], loss_b / cons_b per row, metrics[0] = loss,
+ * metrics[1] = td, metrics[2] = conservative term. */
+typedef struct d3a_iqn_loss_desc {
+  const float* q_loss; const float* q_next; const float* q_targ;
+  const int32_t* act; const float* rew; const float* term; const float* n_steps;
+  const float* taus_loss;
+  float* dq; float* loss_b; float* cons_b; float* metrics;
+  int32_t B, K, A; float gamma, alpha;
+} d3a_iqn_loss_desc;
+int d3a_iqn_loss(const d3a_iqn_loss_desc* d, void* stream);
+
+/* Backward of the IQN head over G gradient passes (rows g*B*K + b*K + k),
+ * one workgroup per b: dphi = (dq Wf) * h * [phi > 0] (the embed ReLU),
+ * dh = (sum_r (dq Wf) * phi) * [h > 0] (the encoder fc ReLU), and per-b
+ * partials of dWf / dbf (summed in order by d3a_adam_f32). */
+typedef struct d3a_iqn_head_bwd_desc {
+  const float* h; const float* phi; const float* dq; const float* Wf;
+  float* dphi; float* dh; float* dWf_part; float* dbf_part;
+  int32_t B, K, F, A, G;
+} d3a_iqn_head_bwd_desc;
+int d3a_iqn_head_bwd(const d3a_iqn_head_bwd_desc* d, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

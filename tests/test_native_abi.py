@@ -54,7 +54,11 @@ STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_adam_segment", "AdamSegment"),
            ("d3a_td3bc_actor_desc", "Td3bcActorDesc"), ("d3a_mlp_fwd_desc", "MlpFwdDesc"),
            ("d3a_mlp_bwd_desc", "MlpBwdDesc"), ("d3a_bcq_rows_desc", "BcqRowsDesc"),
            ("d3a_bcq_vae_desc", "BcqVaeDesc"), ("d3a_bcq_target_desc", "BcqTargetDesc"),
-           ("d3a_bcq_qr_desc", "BcqQrDesc"), ("d3a_bcq_actor_desc", "BcqActorDesc"))
+           ("d3a_bcq_qr_desc", "BcqQrDesc"), ("d3a_bcq_actor_desc", "BcqActorDesc"),
+           ("d3a_im2col_desc", "Im2colDesc"), ("d3a_col2im_desc", "Col2imDesc"),
+           ("d3a_transpose_desc", "TransposeDesc"), ("d3a_iqn_prior_desc", "IqnPriorDesc"),
+           ("d3a_iqn_head_desc", "IqnHeadDesc"), ("d3a_iqn_loss_desc", "IqnLossDesc"),
+           ("d3a_iqn_head_bwd_desc", "IqnHeadBwdDesc"))
 
 
 def test_struct_layouts_match_header(tmp_path):
