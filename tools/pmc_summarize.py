@@ -14,15 +14,18 @@ import statistics
 import sys
 
 
-def per_dispatch(d, counter, sub):
+def per_dispatch(d, counter, sub, last=20):
+    """Counter value per matching dispatch, the last `last` dispatches only
+    (tools/pmc_dominant.py launches the dominant kernel last, after warm-up
+    updates that may run kernels with the same name)."""
     files = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
     vals = {}
     for f in files:
         for r in csv.DictReader(open(f)):
             if sub in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
-                key = r.get("Dispatch_Id") or r.get("Correlation_Id")
+                key = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
                 vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
-    return list(vals.values())
+    return [vals[k] for k in sorted(vals)[-last:]]
 
 
 def main():
