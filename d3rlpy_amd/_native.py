@@ -168,7 +168,7 @@ class MlpFwdDesc(C.Structure):
         ("sW", C.c_int64 * (MLP_MAX_HIDDEN + 1)), ("sb", C.c_int64 * (MLP_MAX_HIDDEN + 1)),
         ("h", vp * MLP_MAX_HIDDEN), ("sh", C.c_int64),
         ("out", vp), ("sout", C.c_int64), ("ldout", C.c_int64),
-        ("r0", C.c_int64), ("rows", C.c_int64),
+        ("r0", C.c_int64), ("rows", C.c_int64), ("h_from", C.c_int64),
         ("C", C.c_int32), ("block_rows", C.c_int32),
     ]
 

@@ -593,7 +593,9 @@ class _Workspace:
         if alpha or critic:
             # 3. critic forward (alpha set only when update_alpha runs)
             r0 = 0 if alpha else 3 * NB
-            mlp.forward(impl.critic, impl.store, self.x_q.data_ptr(), True, DA, self.qacts, r0, R)
+            # the critic backward reads the activations of rows [3NB, R) only
+            mlp.forward(impl.critic, impl.store, self.x_q.data_ptr(), True, DA, self.qacts, r0, R,
+                        h_from=3 * NB)
         if critic:
             mlp.forward(impl.critic, impl.targ, self.x_targ.data_ptr(), True, DA, self.tacts,
                         keep_h=False)

@@ -20,6 +20,7 @@
 // is one ds_read_b128 per 32-row tile, the weight operand one 16-byte global
 // load (W rows are k-contiguous, L2-resident across workgroups), four MFMAs
 // per 8 k.
+#include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
 
@@ -28,33 +29,80 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// W[n][k] row-major (row stride ldw), k..k+3 (zero beyond kend / n >= N)
-__device__ __forceinline__ float4 wload(const float* W, int64_t ldw, int n, int N, int k,
-                                        int kend) {
-  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (n >= N) return r;
-  const float* p = W + (int64_t)n * ldw + k;
-  if (k + 3 < kend && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
-    r = *reinterpret_cast<const float4*>(p);
-  } else {
-    if (k + 0 < kend) r.x = p[0];
-    if (k + 1 < kend) r.y = p[1];
-    if (k + 2 < kend) r.z = p[2];
-    if (k + 3 < kend) r.w = p[3];
-  }
-  return r;
-}
-
 // LDS row stride: widest input (256) + 4 floats, so consecutive rows start 4
 // banks apart and the ds_read_b128 lane groups are conflict-free
 constexpr int LDK = 260;
 
-template <int BM, int NW>
-__global__ __launch_bounds__(64 * NW) void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
+// One 32-column output tile over all RT row tiles:
+//   acc[i] += A[i*32.., 0:Kin] (LDS, row stride LDK) x B[0:Kin][this column]
+// Kin is a multiple of 32 (the LDS operand is zero-padded up to it);
+// load(k) returns the lane's B operand B[k..k+3][column].  The B operand is
+// double-buffered in registers: the loads of the next 32-deep k slice are
+// issued before the MFMAs of the current one.  Loaders must be
+// unconditional (clamped addresses, no guarded loads) so the compiler can
+// keep them in flight across the MFMAs -- a guarded load makes it drain the
+// whole queue first.
+template <int RT, class LoadB>
+__device__ __forceinline__ void tile_mfma(f32x16* acc, const float* A, int Kin, int li, int lg,
+                                          LoadB load) {
+  constexpr int U = 4;
+  // multiply one 32-deep slice at k0 with its weights b; every activation
+  // operand of the slice is read before its MFMAs
+  auto slice = [&](int k0, const float4* b) {
+    float4 av[U][RT];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < RT; ++i)
+        av[u][i] = *reinterpret_cast<const float4*>(&A[(i * 32 + li) * LDK + k0 + 8 * u + 4 * lg]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int i = 0; i < RT; ++i) {
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][i].x, b[u].x, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][i].y, b[u].y, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][i].z, b[u].z, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][i].w, b[u].w, acc[i], 0, 0, 0);
+      }
+    }
+  };
+  // ping-pong between two register sets (no copies, so no wait on the
+  // prefetch before its slice); prefetch addresses past the end clamp to
+  // the last slice and are never used
+  float4 b0[U], b1[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) b0[u] = load(8 * u + 4 * lg);
+  const int klast = Kin - 8 * U;
+  int k0 = 0;
+  for (; k0 + 16 * U <= Kin; k0 += 16 * U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) b1[u] = load(k0 + 8 * U + 8 * u + 4 * lg);
+    __builtin_amdgcn_sched_barrier(0);
+    slice(k0, b0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) b0[u] = load(min(k0 + 16 * U, klast) + 8 * u + 4 * lg);
+    __builtin_amdgcn_sched_barrier(0);
+    slice(k0 + 8 * U, b1);
+  }
+  if (k0 < Kin) slice(k0, b0);  // odd number of 32-deep slices
+}
+
+// RTW = 32-row tiles per wave: the waves split the BM rows into RT / RTW
+// groups and each group's waves split the output columns.  32-row blocks use
+// half the LDS, so two workgroups share a CU.
+template <int BM, int NW, int RTW>
+__global__ __launch_bounds__(64 * NW)
+__attribute__((amdgpu_waves_per_eu((NW / 4) * (BM == 32 ? 2 : 1))))
+void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
   constexpr int NT = 64 * NW;
   constexpr int RT = BM / 32;  // 32-row MFMA tiles per workgroup
-  constexpr int U = 4;         // 8-k groups whose weight loads are in flight together
-  __shared__ __attribute__((aligned(16))) float lds[2 * BM * LDK];
+  constexpr int RG = RT / RTW;  // row groups
+  constexpr int NCW = NW / RG;  // waves per row group
+  static_assert(RT % RTW == 0 && NW % RG == 0, "bad wave split");
+  // 128-row blocks keep one activation buffer (133 KB) and update it in place
+  constexpr bool INPLACE = BM == 128;
+  static_assert(!INPLACE || (RG == 1 && NW * 32 >= 256), "in-place needs a column tile per wave");
+  __shared__ __attribute__((aligned(16))) float lds[(INPLACE ? 1 : 2) * BM * LDK];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int li = lane & 31, lg = lane >> 5;
   const int c = blockIdx.z;
@@ -62,9 +110,9 @@ __global__ __launch_bounds__(64 * NW) void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
   const int64_t rend = d.r0 + d.rows;
   const int H = d.H;
   const int K0 = d.n_in;
-  const int K0p = (K0 + 7) / 8 * 8;
+  const int K0p = (K0 + 31) / 32 * 32;  // zero-padded to whole 32-deep k slices
   float* bufA = lds;
-  float* bufB = lds + BM * LDK;
+  float* bufB = INPLACE ? lds : lds + BM * LDK;
 
   // stage the input rows (zero-padded to a multiple of 8 columns)
   const float* xb = d.x + c * d.sxb;
@@ -79,6 +127,23 @@ __global__ __launch_bounds__(64 * NW) void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
   // J > 64 columns go through the MFMA loop, narrow heads through VALU dots)
   const int J = d.n_out;
   const int n_mfma = d.n_hidden + (J > 64 ? 1 : 0);
+  // per-lane row-validity bit masks over the RTW x 16 accumulator rows:
+  // v_out rows < rend, v_h rows also >= h_from (activations kept)
+  uint64_t v_out = 0, v_h = 0;
+  {
+    const int64_t lr = m0 + (w % RG) * RTW * 32 + 4 * lg;
+#pragma unroll
+    for (int i = 0; i < RTW; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = lr + i * 32 + (r & 3) + 8 * (r >> 2);
+        const uint64_t bit = uint64_t(1) << (i * 16 + r);
+        if (row < rend) {
+          v_out |= bit;
+          if (row >= d.h_from) v_h |= bit;
+        }
+      }
+  }
   for (int l = 0; l < n_mfma; ++l) {
     const bool head = l == d.n_hidden;
     const int N = head ? J : H;
@@ -87,58 +152,79 @@ __global__ __launch_bounds__(64 * NW) void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
     const float* W = d.W[l] + c * d.sW[l];
     const float* bias = d.b[l] + c * d.sb[l];
     float* gout = head ? d.out + c * d.sout : (d.h[l] ? d.h[l] + c * d.sh : nullptr);
-    const int64_t ldg = head ? d.ldout : H;
-    for (int ct = w; ct < (N + 31) / 32; ct += NW) {
-      const int n = ct * 32 + li;
-      f32x16 acc[RT];
+    const int ldg = head ? (int)d.ldout : H;
+    const int rg = w % RG;
+    const float* Ag = bufA + rg * RTW * 32 * LDK;
+    auto mma = [&](f32x16* acc, int n) {
 #pragma unroll
-      for (int i = 0; i < RT; ++i)
+      for (int i = 0; i < RTW; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
-      // weight operand double-buffered in registers: the loads of the next
-      // 8U-deep k slice are in flight while the current one is multiplied
-      float4 bv[U], bnx[U];
+      // columns >= N are computed from a clamped row and dropped; 32-bit
+      // offsets from the uniform base keep the addresses in one VGPR each
+      const int wo = min(n, N - 1) * Kreal;
+      if (l == 0) {
+        // k beyond the real inputs clamps to the last one; its product with
+        // the zero padding of the LDS operand is an exact zero
+        tile_mfma<RTW>(acc, Ag, Kin, li, lg, [&](int k) {
+          float4 r;
+          r.x = W[wo + min(k + 0, Kreal - 1)];
+          r.y = W[wo + min(k + 1, Kreal - 1)];
+          r.z = W[wo + min(k + 2, Kreal - 1)];
+          r.w = W[wo + min(k + 3, Kreal - 1)];
+          return r;
+        });
+      } else {
+        tile_mfma<RTW>(acc, Ag, Kin, li, lg,
+                       [&](int k) { return *reinterpret_cast<const float4*>(W + (wo + k)); });
+      }
+    };
+    auto epi = [&](const f32x16* acc, int n, float* dst) {
+      if (n >= N) return;
+      const float bn = bias[n];
+      // this lane's rows: lrow + mo(i, r); row validity from the masks
+      const int lrow = rg * RTW * 32 + 4 * lg;
+      float* gp = gout ? gout + (int64_t)(m0 + lrow) * ldg + n : nullptr;
+      const uint64_t vm = head ? v_out : v_h;
 #pragma unroll
-      for (int u = 0; u < U; ++u) bv[u] = wload(W, Kreal, n, N, 8 * u + 4 * lg, Kreal);
-      for (int k0 = 0; k0 < Kin; k0 += 8 * U) {
-        if (k0 + 8 * U < Kin) {
+      for (int i = 0; i < RTW; ++i) {
 #pragma unroll
-          for (int u = 0; u < U; ++u)
-            bnx[u] = wload(W, Kreal, n, N, k0 + 8 * U + 8 * u + 4 * lg, Kreal);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int k = k0 + 8 * u + 4 * lg;
-          if (k0 + 8 * u >= Kin) break;
-#pragma unroll
-          for (int i = 0; i < RT; ++i) {
-            const float4 av = *reinterpret_cast<const float4*>(&bufA[(i * 32 + li) * LDK + k]);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv[u].x, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv[u].y, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv[u].z, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv[u].w, acc[i], 0, 0, 0);
+        for (int r = 0; r < 16; ++r) {
+          const int mo = i * 32 + (r & 3) + 8 * (r >> 2);
+          const bool ok = (vm >> (i * 16 + r)) & 1;
+          if (head) {
+            if (ok) gp[mo * ldg] = acc[i][r] + bn;
+          } else {
+            const float v = fmaxf(acc[i][r] + bn, 0.f);
+            dst[(lrow + mo) * LDK + n] = v;
+            // the global copy for the backward pass leaves with the
+            // epilogue (overlapping the other waves' MFMAs)
+            if (gp && ok) gp[mo * ldg] = v;
           }
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) bv[u] = bnx[u];
       }
-      if (n < N) {
-        const float bn = bias[n];
-#pragma unroll
-        for (int i = 0; i < RT; ++i) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int m = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lg;
-            const float v = head ? acc[i][r] + bn : fmaxf(acc[i][r] + bn, 0.f);
-            if (!head) bufB[m * LDK + n] = v;
-            if (gout && m0 + m < rend) gout[(m0 + m) * ldg + n] = v;
-          }
-        }
-      }
+    };
+    if (INPLACE && !head) {
+      // one column tile per wave (H <= 32 * NW); the layer's output
+      // overwrites its input once every wave has finished reading it
+      const int n = w * 32 + li;
+      const bool act = w * 32 < N;
+      f32x16 acc[RTW];
+      if (act) mma(acc, n);
+      __syncthreads();
+      if (act) epi(acc, n, bufA);
+      __syncthreads();
+      continue;
+    }
+    for (int ct = w / RG; ct < (N + 31) / 32; ct += NCW) {
+      const int n = ct * 32 + li;
+      f32x16 acc[RTW];
+      mma(acc, n);
+      epi(acc, n, bufB);
     }
     if (head) return;
     __syncthreads();
-    float* tmp = bufA; bufA = bufB; bufB = tmp;
+    float* tmp = bufA; bufA = bufB; bufB = tmp;  // (INPLACE never gets here for hidden layers)
   }
 
   // narrow head: out[r][j] = h[r] . Wh[j] + bh[j]
@@ -195,22 +281,36 @@ extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
   D3A_CHECK_ARG(d.n_in >= 1 && d.n_in <= 256, "d3a_mlp_fwd: n_in must be 1..256");
   D3A_CHECK_ARG(d.n_out >= 1 && d.n_out <= 1024, "d3a_mlp_fwd: n_out must be 1..1024");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0, "d3a_mlp_fwd: bad sizes");
+  D3A_CHECK_ARG(d.h_from >= 0, "d3a_mlp_fwd: h_from must be >= 0");
   for (int l = 0; l <= d.n_hidden; ++l)
     D3A_CHECK_ARG(d.W[l] && d.b[l], "d3a_mlp_fwd: null layer parameters");
-  // the head reads W rows with 16-byte loads
-  D3A_CHECK_ARG((reinterpret_cast<uintptr_t>(d.W[d.n_hidden]) & 15) == 0 && d.sW[d.n_hidden] % 4 == 0,
-                "d3a_mlp_fwd: head weights must be 16-byte aligned");
+  // layers after the first (and the head) read W rows with 16-byte loads
+  for (int l = 1; l <= d.n_hidden; ++l)
+    D3A_CHECK_ARG((reinterpret_cast<uintptr_t>(d.W[l]) & 15) == 0 && d.sW[l] % 4 == 0,
+                  "d3a_mlp_fwd: weights after layer 0 must be 16-byte aligned");
+  // in-kernel row offsets are 32-bit
+  D3A_CHECK_ARG((d.r0 + d.rows) * (int64_t)(d.ldout > d.H ? d.ldout : d.H) < (int64_t(1) << 31),
+                "d3a_mlp_fwd: rows x row stride exceeds 2^31");
   if (d.rows == 0) return 0;
-  // 64-row blocks for the large critic passes (each weight load feeds two
-  // row tiles), 32-row blocks otherwise (more workgroups for 100-256 rows);
-  // 8 waves: one 32-column tile per wave at H = 256
-  const int bm = d.block_rows > 0 ? d.block_rows : (d.rows * d.C >= 4096 ? 64 : 32);
-  D3A_CHECK_ARG(bm == 32 || bm == 64, "d3a_mlp_fwd: block_rows must be 0, 32 or 64");
+  // Rows per workgroup, from bench A/B runs (profiles/r01_fused_ab.log):
+  // 128 (in-place activations, four row tiles per weight load) for large
+  // passes with narrow heads -- 55.8 us against 69.5 (32) / 77.6 (64) on the
+  // K2 critic pass, 2 x 15616 rows; 32 (two workgroups per CU) otherwise --
+  // 164.9 us against 173.5 (128) / 194.9 (64) on the K3 200-quantile target
+  // pass, 2 x 25600 rows, and more workgroups for the 100-2560-row passes
+  const int bm = d.block_rows > 0
+                     ? d.block_rows
+                     : (d.n_out <= 64 && d.rows * d.C >= 16384 ? 128 : 32);
+  D3A_CHECK_ARG(bm == 32 || bm == 64 || bm == 128,
+                "d3a_mlp_fwd: block_rows must be 0, 32, 64 or 128");
   dim3 grid((unsigned)((d.rows + bm - 1) / bm), 1, (unsigned)d.C);
-  if (bm == 32)
-    hipLaunchKernelGGL((mlp_fwd_kernel<32, 8>), grid, dim3(512), 0, (hipStream_t)stream, d);
+  hipStream_t st = (hipStream_t)stream;
+  if (bm == 128)
+    hipLaunchKernelGGL((mlp_fwd_kernel<128, 8, 4>), grid, dim3(512), 0, st, d);
+  else if (bm == 64)
+    hipLaunchKernelGGL((mlp_fwd_kernel<64, 8, 2>), grid, dim3(512), 0, st, d);
   else
-    hipLaunchKernelGGL((mlp_fwd_kernel<64, 8>), grid, dim3(512), 0, (hipStream_t)stream, d);
+    hipLaunchKernelGGL((mlp_fwd_kernel<32, 8, 1>), grid, dim3(512), 0, st, d);
   D3A_LAUNCH_CHECK("d3a_mlp_fwd");
   return 0;
 }
@@ -228,7 +328,6 @@ template <int BM, int NW>
 __global__ __launch_bounds__(64 * NW) void mlp_bwd_kernel(d3a_mlp_bwd_desc d) {
   constexpr int NT = 64 * NW;
   constexpr int RT = BM / 32;
-  constexpr int U = 4;
   __shared__ __attribute__((aligned(16))) float lds[2 * BM * LDK];
   __shared__ float s_g[BM];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -298,6 +397,7 @@ __global__ __launch_bounds__(64 * NW) void mlp_bwd_kernel(d3a_mlp_bwd_desc d) {
     const int ldw = to_x ? d.n_in : H;
     const float* hm = to_x ? nullptr : d.h[l - 1] + c * d.sh;
     float* dzo = to_x ? nullptr : d.dz[l - 1] + c * d.sdz;
+    float* dxb = to_x ? d.dx + c * d.sdxb : nullptr;
     for (int ct = w; ct < (Kout + 31) / 32; ct += NW) {
       const int k = ct * 32 + li;
       f32x16 acc[RT];
@@ -306,38 +406,16 @@ __global__ __launch_bounds__(64 * NW) void mlp_bwd_kernel(d3a_mlp_bwd_desc d) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
       // B(n, k) = W[n][k]: four rows, one column per lane (coalesced over
-      // lanes); double-buffered like the forward's weight operand
-      auto bload = [&](int n0_, float4* dst) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int n = n0_ + 8 * u + 4 * lg;
-          const float* p = W + (int64_t)n * ldw + k;
-          const bool ok = k < Kout;
-          dst[u].x = ok ? p[0] : 0.f;
-          dst[u].y = ok ? p[ldw] : 0.f;
-          dst[u].z = ok ? p[2 * ldw] : 0.f;
-          dst[u].w = ok ? p[3 * ldw] : 0.f;
-        }
-      };
-      float4 bv[U], bnx[U];
-      bload(0, bv);
-      for (int n0 = 0; n0 < H; n0 += 8 * U) {
-        if (n0 + 8 * U < H) bload(n0 + 8 * U, bnx);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int n = n0 + 8 * u + 4 * lg;
-#pragma unroll
-          for (int i = 0; i < RT; ++i) {
-            const float4 av = *reinterpret_cast<const float4*>(&bufA[(i * 32 + li) * LDK + n]);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv[u].x, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv[u].y, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv[u].z, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv[u].w, acc[i], 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) bv[u] = bnx[u];
-      }
+      // lanes); columns >= Kout read a clamped column and are dropped
+      const int kc = min(k, Kout - 1);
+      tile_mfma<RT>(acc, bufA, H, li, lg, [&](int n) {
+        float4 r;
+        r.x = W[kc + (n + 0) * ldw];
+        r.y = W[kc + (n + 1) * ldw];
+        r.z = W[kc + (n + 2) * ldw];
+        r.w = W[kc + (n + 3) * ldw];
+        return r;
+      });
       if (k < Kout) {
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
@@ -346,11 +424,11 @@ __global__ __launch_bounds__(64 * NW) void mlp_bwd_kernel(d3a_mlp_bwd_desc d) {
             const int m = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lg;
             const int64_t row = m0 + m;
             if (to_x) {
-              if (row < rows) d.dx[c * d.sdxb + row * d.lddx + k] = acc[i][r];
+              if (row < rows) dxb[(int)(row * d.lddx) + k] = acc[i][r];
             } else {
-              const float v = (row < rows && hm[row * d.ldh + k] > 0.f) ? acc[i][r] : 0.f;
+              const float v = (row < rows && hm[(int)(row * d.ldh) + k] > 0.f) ? acc[i][r] : 0.f;
               bufB[m * LDK + k] = v;
-              if (row < rows) dzo[row * H + k] = v;
+              if (row < rows) dzo[(int)row * H + k] = v;
             }
           }
         }
@@ -377,6 +455,13 @@ extern "C" int d3a_mlp_bwd(const d3a_mlp_bwd_desc* dp, void* stream) {
     D3A_CHECK_ARG(d.h[l] && d.dz[l], "d3a_mlp_bwd: activations and dz outputs required");
   D3A_CHECK_ARG(d.n_out == 1 ? (d.g != nullptr || d.q_min != nullptr) : d.dhead != nullptr,
                 "d3a_mlp_bwd: missing output gradient");
+  // in-kernel row offsets are 32-bit
+  {
+    int64_t ld = d.H;
+    if (d.ldh > ld) ld = d.ldh;
+    if (d.dx && d.lddx > ld) ld = d.lddx;
+    D3A_CHECK_ARG(d.rows * ld < (int64_t(1) << 31), "d3a_mlp_bwd: rows x row stride exceeds 2^31");
+  }
   if (d.rows <= 0) return 0;
   const int bm = d.block_rows > 0 ? d.block_rows : (d.rows * d.C >= 4096 ? 64 : 32);
   D3A_CHECK_ARG(bm == 32 || bm == 64, "d3a_mlp_bwd: block_rows must be 0, 32 or 64");

@@ -65,6 +65,8 @@ FUSED_MIN_ROWS = int(os.environ.get("D3A_FUSED_MIN_ROWS", "4096"))
 # rows (four loads per lane per 8 k) and it measured 67 us against 52 us for
 # the per-layer head backward + input-gradient GEMM on the K2 critic pass
 _FUSED_BWD = os.environ.get("D3A_FUSED_BWD", "0") == "1"
+# rows per fused workgroup (32 or 64; 0 = the library's choice)
+_FUSED_BM = int(os.environ.get("D3A_FUSED_BM", "0"))
 
 
 def fused_ok(net: EnsembleMLP, rows: Optional[int] = None, backward: bool = False) -> bool:
@@ -77,10 +79,13 @@ def fused_ok(net: EnsembleMLP, rows: Optional[int] = None, backward: bool = Fals
 
 def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: int, acts: Acts,
             r0: int = 0, r1: Optional[int] = None, sxb: Optional[int] = None,
-            members: Optional[int] = None, keep_h: bool = True) -> None:
+            members: Optional[int] = None, keep_h: bool = True,
+            h_from: Optional[int] = None) -> None:
     """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
     (through its first ``members`` members only, when given).  ``keep_h``:
-    store the hidden activations in ``acts.h`` (needed by a backward pass)."""
+    store the hidden activations in ``acts.h`` (needed by a backward pass),
+    for rows >= ``h_from`` only when given (the fused kernel skips the rest;
+    the per-layer path stores every row)."""
     R = acts.R
     r1 = R if r1 is None else r1
     n = r1 - r0
@@ -90,6 +95,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     sizes = net.sizes
     if fused_ok(net, n * C // net.C):
         d = N.MlpFwdDesc()
+        d.block_rows = _FUSED_BM
         d.x, d.ldx = x, ldx
         d.sxb = (0 if x_shared else R * ldx) if sxb is None else sxb
         L = net.n_layers
@@ -103,6 +109,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         d.out = acts.out.data_ptr()
         d.sout, d.ldout = R * sizes[-1], sizes[-1]
         d.r0, d.rows, d.C = r0, n, C
+        d.h_from = r0 if h_from is None else max(r0, h_from)
         ops.call_desc("d3a_mlp_fwd", d)
         return
     L = net.n_layers

@@ -127,10 +127,12 @@ int d3a_head1_bwd(const d3a_head1_bwd_desc* desc, void* stream);
  *   a_l = relu(a_{l-1} W_{l-1}^T + b_{l-1}),  l = 1..n_hidden   (width H)
  *   out[c*sout + r*ldout + j] = a_{n_hidden} . W_head[j] + b_head[j]
  * W[l] row-major [out][in] (member stride sW[l]), W[n_hidden] is the head
- * (16-byte aligned).  h[l] (optional) receives a_{l+1} as [C][R][H] (member
- * stride sh, absolute row index) for the backward pass.  Activations stay in
- * LDS between layers; block_rows (0 = automatic, 32 or 64) rows per
- * workgroup.  Heads wider than 64 (quantile heads) run on MFMA as well. */
+ * (16-byte aligned; every layer after the first too).  h[l] (optional)
+ * receives a_{l+1} as [C][R][H] (member stride sh, absolute row index) for
+ * the backward pass, for rows r >= h_from only (rows no backward reads are
+ * not stored).  Activations stay in LDS between layers; block_rows (0 =
+ * automatic, 32, 64 or 128) rows per workgroup.  Heads wider than 64
+ * (quantile heads) run on MFMA as well. */
 #define D3A_MLP_MAX_HIDDEN 4
 typedef struct d3a_mlp_fwd_desc {
   const float* x; int64_t ldx, sxb;
@@ -140,7 +142,7 @@ typedef struct d3a_mlp_fwd_desc {
   int64_t sW[D3A_MLP_MAX_HIDDEN + 1], sb[D3A_MLP_MAX_HIDDEN + 1];
   float* h[D3A_MLP_MAX_HIDDEN]; int64_t sh;
   float* out; int64_t sout, ldout;
-  int64_t r0, rows;
+  int64_t r0, rows, h_from;
   int32_t C, block_rows;
 } d3a_mlp_fwd_desc;
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);

@@ -232,13 +232,17 @@ def test_philox_statistics(dev):
     (3, 77, 0, 77, 37, 96, 1, 5, False),          # per-member inputs, one hidden layer
     (2, 3000, 0, 3000, 23, 256, 2, 200, True),    # QR critic (200-quantile MFMA head)
 ])
-def test_fused_mlp_forward(dev, C, R, r0, n, K0, H, L, J, x_shared, monkeypatch):
+@pytest.mark.parametrize("bm", [0, 32, 64, 128])
+def test_fused_mlp_forward(dev, C, R, r0, n, K0, H, L, J, x_shared, bm, monkeypatch):
     """d3a_mlp_fwd (every layer + head in one launch) against an fp64 torch
-    MLP; hidden activations (kept for the backward) checked too.
+    MLP; hidden activations (kept for the backward) checked too, and rows
+    below h_from must be left untouched.  Every workgroup shape (bm = rows
+    per workgroup; 0 = the library's choice).
     Tolerance 2e-6 relative (exact-f32 MFMA chains, K <= 256)."""
     from d3rlpy_amd import mlp
     from d3rlpy_amd.nets import EnsembleMLP, ParamStore
     monkeypatch.setattr(mlp, "FUSED_MIN_ROWS", 0)  # fused kernel at every size
+    monkeypatch.setattr(mlp, "_FUSED_BM", bm)
     g = torch.Generator().manual_seed(R + K0)
     st = ParamStore()
     net = EnsembleMLP(st, "m", C, [K0] + [H] * L + [J])
@@ -248,9 +252,13 @@ def test_fused_mlp_forward(dev, C, R, r0, n, K0, H, L, J, x_shared, monkeypatch)
     ldx = (K0 + 3) // 4 * 4 + 4
     x = torch.randn((1 if x_shared else C), R, ldx, generator=g).to(dev)
     acts = mlp.Acts.alloc(net, R, dev)
+    for h in acts.h:
+        h.fill_(float("nan"))
+    h_from = r0 + n // 3
     assert mlp.fused_ok(net)
-    mlp.forward(net, st, x.data_ptr(), x_shared, ldx, acts, r0, r0 + n)
+    mlp.forward(net, st, x.data_ptr(), x_shared, ldx, acts, r0, r0 + n, h_from=h_from)
     torch.cuda.synchronize()
+    k = h_from - r0
     for c in range(C):
         a = x[0 if x_shared else c, r0:r0 + n, :K0].double()
         for l in range(L + 1):
@@ -258,7 +266,8 @@ def test_fused_mlp_forward(dev, C, R, r0, n, K0, H, L, J, x_shared, monkeypatch)
             a = a @ W.double().T + b.double()
             if l < L:
                 a = a.clamp_min(0)
-                assert _rel_err(acts.h[l][c, r0:r0 + n], a) < 2e-6, (c, l)
+                assert _rel_err(acts.h[l][c, h_from:r0 + n], a[k:]) < 2e-6, (c, l)
+                assert torch.isnan(acts.h[l][c, r0:h_from]).all(), (c, l)
         out = acts.out[c, r0:r0 + n] if J == 1 else acts.out[c, r0:r0 + n]
         assert _rel_err(out.reshape(n, J), a) < 2e-6, c
 
