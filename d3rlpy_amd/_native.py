@@ -257,6 +257,16 @@ class Col2imDesc(C.Structure):
     ]
 
 
+class ConvDesc(C.Structure):
+    _fields_ = [
+        ("x_u8", vp), ("x_f32", vp), ("weight", vp), ("bias", vp), ("y", vp), ("wpack", vp),
+        ("dy", vp), ("dW", vp), ("db", vp),
+        ("B", C.c_int32), ("C", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
+        ("KH", C.c_int32), ("KW", C.c_int32), ("S", C.c_int32), ("OH", C.c_int32),
+        ("OW", C.c_int32), ("CO", C.c_int32), ("relu", C.c_int32), ("splits", C.c_int32),
+    ]
+
+
 class TransposeDesc(C.Structure):
     _fields_ = [
         ("src", vp), ("dst", vp), ("mask", vp),
@@ -325,6 +335,8 @@ _SIGNATURES = {
     "d3a_im2col": (C.c_int, [C.POINTER(Im2colDesc), vp]),
     "d3a_col2im": (C.c_int, [C.POINTER(Col2imDesc), vp]),
     "d3a_iqn_transpose": (C.c_int, [C.POINTER(TransposeDesc), vp]),
+    "d3a_conv_fwd": (C.c_int, [C.POINTER(ConvDesc), vp]),
+    "d3a_conv_bwd_w": (C.c_int, [C.POINTER(ConvDesc), vp]),
     "d3a_iqn_prior": (C.c_int, [C.POINTER(IqnPriorDesc), vp]),
     "d3a_iqn_head_fwd": (C.c_int, [C.POINTER(IqnHeadDesc), vp]),
     "d3a_iqn_loss": (C.c_int, [C.POINTER(IqnLossDesc), vp]),

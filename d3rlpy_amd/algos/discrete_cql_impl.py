@@ -8,14 +8,15 @@ One ``update`` (dqn_impl.py:97-111) on the device:
   1  Philox taus for the five IQN evaluations of the step
      (next-online argmax, next-target, loss, logsumexp, data values)
   2  online encoder over [obs; next_obs] (2B samples), target encoder over
-     next_obs: im2col (uint8 -> /255 fused) + GEMM per conv, NHWC -> NCHW
-     flatten, fc
+     next_obs: implicit-GEMM convs (uint8 -> /255 fused into the loads, no
+     im2col matrix), NHWC -> NCHW flatten, fc
   3  IQN head: cos prior, embed GEMM + ReLU, (h * phi) . W_fc per row —
      online rows [loss | lse | data | next] in one pass, target rows in another
   4  d3a_iqn_loss: Double-DQN target, per-sample-tau quantile Huber loss,
      conservative logsumexp term, dL/dq
   5  head backward (d3a_iqn_head_bwd), embed weight gradient, encoder backward
-     (fc, conv3, conv2 via col2im, conv1 weight gradient), Adam
+     (fc; per conv an implicit-GEMM weight gradient; conv3 / conv2 input
+     gradients via GEMM + col2im), Adam
   6  d3a_step_end: metrics ring, step counter, and on target-update steps the
      hard sync (tau = 1 copy, dqn_impl.py:146-149)
 Encoder forwards on identical (params, input) are evaluated once: the three
@@ -264,43 +265,53 @@ class DiscreteCQLImpl(ImplBase):
         return next(iter(self._ws.values())).opt.grad(name)
 
 
+def _conv_desc(geom, l: int, n: int, store: ParamStore, names) -> "NAT.ConvDesc":
+    ci, h, w, co, k, s, oh, ow = geom[l]
+    d = NAT.ConvDesc()
+    d.B, d.C, d.H, d.W, d.KH, d.KW, d.S, d.OH, d.OW, d.CO = n, ci, h, w, k, k, s, oh, ow, co
+    Wn, bn = names[l]
+    d.weight, d.bias = store.ptr(Wn), store.ptr(bn)
+    d.relu = 1
+    return d
+
+
 class _EncoderPass:
     """Buffers + launches of one PixelEncoder forward over n samples (NHWC
-    activations, NCHW flatten), and its backward for the first nb samples."""
+    activations, NCHW flatten): implicit-GEMM convs (d3a_conv_fwd, the pixel
+    scaler fused into the first layer's loads) — no im2col matrix."""
 
     def __init__(self, impl: DiscreteCQLImpl, n: int, dev, keep: bool = True):
         self.impl, self.n = impl, n
         z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
-        self.cols, self.ys = [], []
-        for (ci, h, w, co, k, s, oh, ow) in impl.geom:
-            self.cols.append(z(n * oh * ow, ci * k * k))
-            self.ys.append(z(n * oh * ow, co))
+        self.ys = [z(n * oh * ow, co) for (ci, h, w, co, k, s, oh, ow) in impl.geom]
+        # walk-ordered weight scratch of the fp32-input convs (d3a_conv_fwd)
+        self.wpack = [z(co * ci * k * k) for (ci, h, w, co, k, s, oh, ow) in impl.geom]
         self.yt = z(n, impl.flat)
         self.h = z(n, impl._F)
 
     def forward(self, x_u8: int, store: ParamStore) -> None:
         impl = self.impl
         n = self.n
-        for l, (ci, h, w, co, k, s, oh, ow) in enumerate(impl.geom):
-            d = NAT.Im2colDesc()
+        for l in range(len(impl.geom)):
+            d = _conv_desc(impl.geom, l, n, store, impl.conv_names)
             if l == 0:
                 d.x_u8 = x_u8
             else:
                 d.x_f32 = self.ys[l - 1].data_ptr()
-            d.B, d.C, d.H, d.W, d.KH, d.KW, d.S, d.OH, d.OW = n, ci, h, w, k, k, s, oh, ow
-            d.col, d.ldcol = self.cols[l].data_ptr(), ci * k * k
-            ops.call_desc("d3a_im2col", d)
-            Wn, bn = impl.conv_names[l]
-            ops.linear_fwd(self.cols[l].data_ptr(), True, ci * k * k, store.ptr(Wn), store.ptr(bn),
-                           self.ys[l].data_ptr(), 1, n * oh * ow, ci * k * k, co, relu=True)
+                d.wpack = self.wpack[l].data_ptr()
+            d.y = self.ys[l].data_ptr()
+            ops.call_desc("d3a_conv_fwd", d)
         ci, h, w, co, k, s, oh, ow = impl.geom[-1]
         t = NAT.TransposeDesc()
         t.src, t.dst = self.ys[-1].data_ptr(), self.yt.data_ptr()
         t.B, t.P, t.C, t.to_cp = n, oh * ow, co, 1
         ops.call_desc("d3a_iqn_transpose", t)
+        # K = 3136, few output tiles: over 2B = 1024 rows the register-direct
+        # 32x64 tile with K split over waves (tools/bench_gemm_k5.py: 98 us vs
+        # 139 for 64x64 LDS); at 512 rows the library's 32x32 choice (58 vs 96)
         ops.linear_fwd(self.yt.data_ptr(), True, impl.flat, store.ptr("enc.fc.W"),
                        store.ptr("enc.fc.b"), self.h.data_ptr(), 1, n, impl.flat, impl._F,
-                       relu=True)
+                       relu=True, variant=10 if n > 512 else -1)
 
 
 class _HeadPass:
@@ -380,7 +391,10 @@ class _Workspace:
             self.splits[l] = S
             self.grads.add(f"enc.c{l}.W", (1, co, ci, k, k), S)
             self.grads.add(f"enc.c{l}.b", (1, co), S)
-        self.S_fc = mlp.n_splits(B)
+        # weight-gradient splits / tiles from tools/bench_gemm_k5.py
+        # (profiles/r01_gemm_sweep_k5.log): fc 4 splits (38 us vs 53 at 16),
+        # embed 32 splits on the register-direct 32x64 tile (112 us vs 244)
+        self.S_fc = min(4, mlp.n_splits(B))
         self.grads.add("enc.fc.W", (1, F, impl.flat), self.S_fc)
         self.grads.add("enc.fc.b", (1, F), self.S_fc)
         self.grads.add("q.fc.W", (1, A, F), B)
@@ -442,14 +456,14 @@ class _Workspace:
         impl = self.impl
         ci, h, w, co, k, s, oh, ow = impl.geom[0]
         rows = 2 * self.B * oh * ow
-        col, y = self.enc.cols[0], self.enc.ys[0]
-        Wn, bn = impl.conv_names[0]
+        d = _conv_desc(impl.geom, 0, 2 * self.B, impl.store, impl.conv_names)
+        d.x_u8, d.y = self.obs2.data_ptr(), self.enc.ys[0].data_ptr()
 
         def launch():
-            ops.linear_fwd(col.data_ptr(), True, ci * k * k, impl.store.ptr(Wn),
-                           impl.store.ptr(bn), y.data_ptr(), 1, rows, ci * k * k, co, relu=True)
-        return launch, 2 * rows * ci * k * k * co, (f"gemm_f32 conv1 (im2col): [{rows}x"
-                                                    f"{ci * k * k}]@[{ci * k * k}x{co}]")
+            ops.call_desc("d3a_conv_fwd", d)
+        return launch, 2 * rows * ci * k * k * co, (f"d3a_conv_fwd conv1 (implicit GEMM, u8 "
+                                                    f"input): [{rows}x{ci * k * k}]@"
+                                                    f"[{ci * k * k}x{co}]")
 
     def execute(self, flags, use_graph: bool) -> None:
         key = tuple(flags) + (self._external_taus,)
@@ -492,7 +506,7 @@ class _Workspace:
         g = self.grads
         ops.linear_bwd_w(self.dphi.data_ptr(), F, 3 * BK * F, self.head.prior.data_ptr(), E,
                          3 * BK * E, g.get("q.embed.W").data_ptr(), 1, 3 * BK, E, F, self.S_emb,
-                         db=g.get("q.embed.b").data_ptr())
+                         db=g.get("q.embed.b").data_ptr(), variant=10)
         ops.linear_bwd_w(self.dzfc.data_ptr(), F, B * F, self.enc.yt.data_ptr(), impl.flat,
                          B * impl.flat, g.get("enc.fc.W").data_ptr(), 1, B, impl.flat, F,
                          self.S_fc, db=g.get("enc.fc.b").data_ptr())
@@ -508,9 +522,16 @@ class _Workspace:
             ci, h, w, co, k, s, oh, ow = impl.geom[l]
             rows, Kc = B * oh * ow, ci * k * k
             Wn, bn = impl.conv_names[l]
-            ops.linear_bwd_w(self.dys[l].data_ptr(), co, rows * co, self.enc.cols[l].data_ptr(),
-                             Kc, rows * Kc, g.get(Wn).data_ptr(), 1, rows, Kc, co,
-                             self.splits[l], db=g.get(bn).data_ptr())
+            # weight gradient over the obs samples (the first B of the online pass)
+            cd = _conv_desc(impl.geom, l, B, st, impl.conv_names)
+            if l == 0:
+                cd.x_u8 = self.obs2.data_ptr()
+            else:
+                cd.x_f32 = self.enc.ys[l - 1].data_ptr()
+            cd.dy, cd.dW, cd.db = self.dys[l].data_ptr(), g.get(Wn).data_ptr(), \
+                g.get(bn).data_ptr()
+            cd.splits = self.splits[l]
+            ops.call_desc("d3a_conv_bwd_w", cd)
             if l > 0:
                 ops.linear_bwd_x(self.dys[l].data_ptr(), co, rows * co, st.ptr(Wn),
                                  self.dcols[l].data_ptr(), Kc, rows * Kc, 1, rows, Kc, co)

@@ -1,0 +1,426 @@
+// Implicit-GEMM convolutions of the Nature-DQN PixelEncoder on the gfx950
+// f32-input matrix cores: no im2col matrix is ever written to HBM.
+//
+// Replaces nn.Conv2d forward and weight gradient in PixelEncoder._conv_encode
+// (d3rlpy/models/torch/encoders.py:130-162; no padding, square stride), with
+// PixelScaler.transform (preprocessing/scalers.py:109-110, x.float() / 255)
+// fused into the first layer's operand load.
+//
+// A conv is the GEMM  y[row][co] = sum_k col(row, k) * W[co][k] + b[co], with
+// row = (b, oy, ox) and k = (c, kh, kw).  Here col(row, k) is read straight
+// from the layer input when the MFMA operand is loaded:
+//   * uint8 NCHW frames (first layer): k in the reference's (c, kh, kw) order;
+//     four consecutive kw of one kernel row are one aligned 32-bit load
+//     (KW % 4 == 0, W % 4 == 0, S % 4 == 0) scaled by 1/255 (correctly
+//     rounded, as the reference's fp32 division);
+//   * fp32 NHWC activations (later layers): k walked in (kh, kw, c) order so
+//     that four consecutive k are four consecutive channels (one 16-byte
+//     load); the weight is first re-laid in that order (conv_pack_kernel).
+// The sum over k is a reduction, so walking it in another order only changes
+// the fp32 rounding order (the reference's CPU conv has its own order too).
+//
+// Forward: a wave owns 32 output rows x CO channels (CO = 32 * WN),
+// v_mfma_f32_32x32x2_f32; lane l covers row / channel l & 31 and
+// k = 4 * (l >> 5) + {0..3} of each 8-k group.  The input operand goes
+// straight into registers; the weight is staged per 32-k chunk in LDS and
+// shared by the workgroup's four waves.  The per-k-group input offsets are
+// tabulated in LDS once per workgroup.
+//
+// Weight gradient: dW[co][k] = sum_rows dy[row][co] * col(row, k) and
+// db[co] = sum_rows dy[row][co] (ReLU already applied to dy).  A wave owns a
+// 32 (co) x 32*WNK (k) tile over a slice of rows; KWV waves of a workgroup
+// take consecutive slices of the split and are summed through LDS in wave
+// order; the split's partial goes to dW[split] (summed in order by the Adam
+// kernel), so the result is run-to-run deterministic.
+#include "common.hpp"
+#include "../../include/d3rlpy_amd.h"
+
+namespace d3a {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kMaxKGroups = 1024;  // C*KH*KW <= 4096
+
+// x / 255 correctly rounded (== torch's x.float() / 255.0) for x in 0..255
+// without a full IEEE division: q = x * fl(1/255), one Newton residual step
+// with exact fma (checked exhaustively, tests/test_gpu_conv.py)
+__device__ __forceinline__ float px(uint32_t byte) {
+  const float x = (float)byte, r = 1.f / 255.f;
+  const float q = __fmul_rn(x, r);
+  const float e = fmaf(-q, 255.f, x);
+  return fmaf(e, r, q);
+}
+
+// input offset of k-group g (4 consecutive k) relative to the row's window
+// origin (walk order: (c, kh, kw) for uint8 input, (kh, kw, c) for fp32)
+template <bool U8>
+__device__ __forceinline__ int kgroup_offset(const d3a_conv_desc& d, int g) {
+  const int k = 4 * g, KK = d.KH * d.KW;
+  if (U8) {
+    const int c = k / KK, r = k - c * KK, kh = r / d.KW, kw = r - kh * d.KW;
+    return (c * d.H + kh) * d.W + kw;
+  }
+  const int c = k % d.C, t = k / d.C, kw = t % d.KW, kh = t / d.KW;
+  return (kh * d.W + kw) * d.C + c;
+}
+
+template <bool U8>
+__device__ __forceinline__ int64_t window_origin(const d3a_conv_desc& d, int64_t b, int oy, int ox) {
+  if (U8) return (b * d.C * d.H + (int64_t)oy * d.S) * d.W + (int64_t)ox * d.S;
+  return ((b * d.H + (int64_t)oy * d.S) * d.W + (int64_t)ox * d.S) * d.C;
+}
+
+// weight [CO][C][KH][KW] -> wpack [CO][KH][KW][C] (the fp32 walk order)
+__global__ __launch_bounds__(256) void conv_pack_kernel(const float* __restrict__ w,
+                                                        float* __restrict__ wp, int C, int KH,
+                                                        int KW, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int Kc = C * KH * KW;
+  const int64_t co = i / Kc;
+  const int kp = (int)(i - co * Kc);
+  const int c = kp % C, t = kp / C, kw = t % KW, kh = t / KW;
+  wp[i] = w[co * Kc + (c * KH + kh) * KW + kw];
+}
+
+// Forward.  Workgroup: 4 waves x 32 rows; each wave 32 rows x CO channels.
+// K is walked in chunks of 32: the workgroup stages the chunk's weights
+// (CO x 32, from the walk-ordered weight, coalesced) into LDS, double
+// buffered, one barrier per chunk; the input operand is loaded straight into
+// registers one chunk ahead.
+template <int WN, bool U8, bool ALIGNED>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(d3a_conv_desc d, const float* __restrict__ wk) {
+  constexpr int CO = 32 * WN, BK = 32, LDW = BK + 4, U = BK / 8;
+  __shared__ int ta[kMaxKGroups];
+  __shared__ __attribute__((aligned(16))) float Ws[2][CO * LDW];
+  const int KK = d.KH * d.KW;
+  const int Kc = d.C * KK;
+  const int G = Kc / 4;
+  for (int g = threadIdx.x; g < G; g += 256) ta[g] = kgroup_offset<U8>(d, g);
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  const int li = lane & 31, lg = lane >> 5;
+  const int P = d.OH * d.OW;
+  const int64_t M = (int64_t)d.B * P;
+  const int64_t m0 = ((int64_t)blockIdx.x * 4 + w) * 32;
+  const int64_t m = m0 + li;
+  const bool valid = m < M;
+  int64_t org = 0;
+  if (valid) {
+    const int64_t b = m / P;
+    const int p = (int)(m - b * P);
+    const int oy = p / d.OW, ox = p - oy * d.OW;
+    org = window_origin<U8>(d, b, oy, ox);
+  }
+
+  // weight chunk loader: WN float4 per thread (CO rows x 8 float4)
+  float4 wr[WN];
+  auto wload = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int v = t + 256 * j, co = v >> 3, q = v & 7;
+      const int k = k0 + 4 * q;
+      wr[j] = k < Kc ? *reinterpret_cast<const float4*>(wk + (int64_t)co * Kc + k)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto wstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int v = t + 256 * j, co = v >> 3, q = v & 7;
+      *reinterpret_cast<float4*>(&Ws[buf][co * LDW + 4 * q]) = wr[j];
+    }
+  };
+  float4 ra[U];
+  auto aload = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int g = k0 / 4 + 2 * u + lg;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (valid && g < G) {
+        if (U8) {
+          const uint8_t* s = d.x_u8 + org + ta[g];
+          if (ALIGNED) {
+            const uint32_t x = *reinterpret_cast<const uint32_t*>(s);
+            a = make_float4(px(x & 255u), px((x >> 8) & 255u), px((x >> 16) & 255u), px(x >> 24));
+          } else {
+            a = make_float4(px(s[0]), px(s[1]), px(s[2]), px(s[3]));
+          }
+        } else {
+          a = *reinterpret_cast<const float4*>(d.x_f32 + org + ta[g]);
+        }
+      }
+      ra[u] = a;
+    }
+  };
+
+  f32x16 acc[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+  wload(0);
+  wstore(0);
+  __syncthreads();  // also publishes the offset table
+  aload(0);
+  int cur = 0;
+  for (int k0 = 0; k0 < Kc; k0 += BK) {
+    const bool more = k0 + BK < Kc;
+    if (more) wload(k0 + BK);
+    float4 ca[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ca[u] = ra[u];
+    if (more) aload(k0 + BK);
+    const float* Wc = Ws[cur];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        const float4 bv = *reinterpret_cast<const float4*>(&Wc[(32 * j + li) * LDW + 8 * u + 4 * lg]);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[u].x, bv.x, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[u].y, bv.y, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[u].z, bv.z, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[u].w, bv.w, acc[j], 0, 0, 0);
+      }
+    }
+    if (more) wstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  if (m0 >= M) return;
+  // epilogue: acc[j][r] -> row m0 + (r&3) + 8*(r>>2) + 4*lg, channel 32*j + li
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int n = 32 * j + li;
+    const float bn = d.bias ? d.bias[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * lg;
+      if (mm < M) {
+        float v = acc[j][r] + bn;
+        if (d.relu) v = fmaxf(v, 0.f);
+        d.y[mm * CO + n] = v;
+      }
+    }
+  }
+}
+
+// row -> (b, oy, ox) cursor that advances one row at a time
+struct RowCursor {
+  int64_t b;
+  int oy, ox;
+  __device__ __forceinline__ void set(int64_t row, int P, int OW) {
+    b = row / P;
+    const int p = (int)(row - b * P);
+    oy = p / OW;
+    ox = p - oy * OW;
+  }
+  __device__ __forceinline__ void next(int OH, int OW) {
+    if (++ox == OW) {
+      ox = 0;
+      if (++oy == OH) { oy = 0; ++b; }
+    }
+  }
+};
+
+template <int WNK, int KWV, bool U8>
+__global__ __launch_bounds__(64 * KWV) void conv_bwd_w_kernel(d3a_conv_desc d) {
+  __shared__ float red[(KWV - 1) * WNK * 16 * 64];
+  __shared__ double rsum[KWV * 32];
+  constexpr int U = 2;  // 8-row steps loaded before any is multiplied
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 31, lg = lane >> 5;
+  const int KK = d.KH * d.KW;
+  const int Kc = d.C * KK;
+  const int P = d.OH * d.OW;
+  const int64_t M = (int64_t)d.B * P;
+  const int k0 = blockIdx.x * 32 * WNK;
+  const int co0 = blockIdx.y * 32;
+  const int s = blockIdx.z;
+  // split s: rows [sb, se); wave w: a multiple-of-8 sub-slice
+  const int64_t chunk = (M + d.splits - 1) / d.splits;
+  const int64_t sb = s * chunk;
+  const int64_t se = sb + chunk < M ? sb + chunk : M;
+  int64_t wch = (se - sb + KWV - 1) / KWV;
+  wch = (wch + 7) / 8 * 8;
+  const int64_t rb = sb + w * wch;
+  const int64_t re = rb + wch < se ? rb + wch : se;
+  const bool do_bias = d.db != nullptr && blockIdx.x == 0;
+
+  // this lane's k columns (walk order) -> input offset and output column
+  int koff[WNK], kout[WNK];
+  bool kok[WNK];
+#pragma unroll
+  for (int j = 0; j < WNK; ++j) {
+    const int k = k0 + 32 * j + li;
+    kok[j] = k < Kc;
+    const int kk = kok[j] ? k : 0;
+    if (U8) {
+      const int c = kk / KK, r = kk - c * KK, kh = r / d.KW, kw = r - kh * d.KW;
+      koff[j] = (c * d.H + kh) * d.W + kw;
+      kout[j] = kk;
+    } else {
+      const int c = kk % d.C, t = kk / d.C, kw = t % d.KW, kh = t / d.KW;
+      koff[j] = (kh * d.W + kw) * d.C + c;
+      kout[j] = c * KK + kh * d.KW + kw;
+    }
+  }
+
+  f32x16 acc[WNK];
+#pragma unroll
+  for (int j = 0; j < WNK; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  double bs = 0.0;
+
+  RowCursor cur;
+  if (rb < re) cur.set(rb + 4 * lg, P, d.OW);
+  for (int64_t r0 = rb; r0 < re; r0 += 8 * U) {
+    float ra[U][4], rv[U][WNK][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      RowCursor c = cur;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = r0 + 8 * u + 4 * lg + q;
+        const bool ok = row < re;
+        ra[u][q] = ok ? d.dy[row * d.CO + co0 + li] : 0.f;
+        const int64_t org = window_origin<U8>(d, c.b, c.oy, c.ox);
+#pragma unroll
+        for (int j = 0; j < WNK; ++j) {
+          float v = 0.f;
+          if (ok && kok[j]) v = U8 ? px(d.x_u8[org + koff[j]]) : d.x_f32[org + koff[j]];
+          rv[u][j][q] = v;
+        }
+        c.next(d.OH, d.OW);
+      }
+      // advance the cursor by 8 rows (4 consumed above + 4 of the other lane group)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) c.next(d.OH, d.OW);
+      cur = c;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (do_bias) bs += (double)ra[u][0] + (double)ra[u][1] + (double)ra[u][2] + (double)ra[u][3];
+#pragma unroll
+      for (int j = 0; j < WNK; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[u][q], rv[u][j][q], acc[j], 0, 0, 0);
+    }
+  }
+
+  if (w > 0) {
+#pragma unroll
+    for (int j = 0; j < WNK; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(((w - 1) * WNK + j) * 16 + r) * 64 + lane] = acc[j][r];
+  }
+  if (do_bias) {
+    bs += __shfl_xor(bs, 32, 64);
+    if (lg == 0) rsum[w * 32 + li] = bs;
+  }
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int v = 1; v < KWV; ++v)
+#pragma unroll
+    for (int j = 0; j < WNK; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] += red[(((v - 1) * WNK + j) * 16 + r) * 64 + lane];
+  float* dW = d.dW + (int64_t)s * d.CO * Kc;
+#pragma unroll
+  for (int j = 0; j < WNK; ++j) {
+    if (!kok[j]) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * lg;
+      dW[(int64_t)co * Kc + kout[j]] = acc[j][r];
+    }
+  }
+  if (do_bias && lg == 0) {
+    double tot = 0.0;
+    for (int v = 0; v < KWV; ++v) tot += rsum[v * 32 + li];
+    d.db[(int64_t)s * d.CO + co0 + li] = (float)tot;
+  }
+}
+
+int check_geometry(const d3a_conv_desc* d, const char* name) {
+  D3A_CHECK_ARG(d != nullptr, "%s: null descriptor", name);
+  D3A_CHECK_ARG((d->x_u8 != nullptr) != (d->x_f32 != nullptr),
+                "%s: exactly one of x_u8 / x_f32 must be set", name);
+  D3A_CHECK_ARG(d->weight, "%s: null weight", name);
+  D3A_CHECK_ARG(d->B >= 0 && d->C >= 1 && d->KH >= 1 && d->KW >= 1 && d->S >= 1 &&
+                    d->H >= d->KH && d->W >= d->KW,
+                "%s: bad geometry", name);
+  D3A_CHECK_ARG(d->OH == (d->H - d->KH) / d->S + 1 && d->OW == (d->W - d->KW) / d->S + 1,
+                "%s: inconsistent output size", name);
+  D3A_CHECK_ARG(d->CO == 32 || d->CO == 64, "%s: CO must be 32 or 64", name);
+  const int64_t Kc = (int64_t)d->C * d->KH * d->KW;
+  D3A_CHECK_ARG(Kc % 4 == 0 && Kc / 4 <= kMaxKGroups, "%s: C*KH*KW must be a multiple of 4, <= 4096",
+                name);
+  if (d->x_u8) D3A_CHECK_ARG(d->KW % 4 == 0, "%s: uint8 input needs KW %% 4 == 0", name);
+  else D3A_CHECK_ARG(d->C % 4 == 0, "%s: fp32 NHWC input needs C %% 4 == 0", name);
+  return 0;
+}
+
+}  // namespace
+}  // namespace d3a
+
+extern "C" int d3a_conv_fwd(const d3a_conv_desc* d, void* stream) {
+  using namespace d3a;
+  if (check_geometry(d, "d3a_conv_fwd")) return -1;
+  D3A_CHECK_ARG(d->y, "d3a_conv_fwd: null output");
+  D3A_CHECK_ARG(d->x_u8 || d->wpack, "d3a_conv_fwd: fp32 input needs the wpack scratch");
+  const int64_t M = (int64_t)d->B * d->OH * d->OW;
+  if (M == 0) return 0;
+  const int64_t blocks = (M + 127) / 128;
+  D3A_CHECK_ARG(blocks < (1ll << 31), "d3a_conv_fwd: too many rows");
+  D3A_CHECK_ARG((reinterpret_cast<uintptr_t>(d->weight) & 15) == 0,
+                "d3a_conv_fwd: weight must be 16-byte aligned");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)blocks), block(256);
+  if (d->x_u8) {
+    const bool aligned = d->W % 4 == 0 && d->S % 4 == 0 &&
+                         (reinterpret_cast<uintptr_t>(d->x_u8) & 3) == 0;
+    const float* wk = d->weight;  // (c, kh, kw) walk order == nn.Conv2d layout
+    if (d->CO == 32) {
+      if (aligned) hipLaunchKernelGGL((conv_fwd_kernel<1, true, true>), grid, block, 0, st, *d, wk);
+      else hipLaunchKernelGGL((conv_fwd_kernel<1, true, false>), grid, block, 0, st, *d, wk);
+    } else {
+      if (aligned) hipLaunchKernelGGL((conv_fwd_kernel<2, true, true>), grid, block, 0, st, *d, wk);
+      else hipLaunchKernelGGL((conv_fwd_kernel<2, true, false>), grid, block, 0, st, *d, wk);
+    }
+  } else {
+    D3A_CHECK_ARG((reinterpret_cast<uintptr_t>(d->x_f32) & 15) == 0 &&
+                      (reinterpret_cast<uintptr_t>(d->wpack) & 15) == 0,
+                  "d3a_conv_fwd: fp32 input and wpack must be 16-byte aligned");
+    const int64_t n = (int64_t)d->CO * d->C * d->KH * d->KW;
+    hipLaunchKernelGGL(conv_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       d->weight, d->wpack, d->C, d->KH, d->KW, n);
+    if (d->CO == 32)
+      hipLaunchKernelGGL((conv_fwd_kernel<1, false, true>), grid, block, 0, st, *d, d->wpack);
+    else
+      hipLaunchKernelGGL((conv_fwd_kernel<2, false, true>), grid, block, 0, st, *d, d->wpack);
+  }
+  D3A_LAUNCH_CHECK("d3a_conv_fwd");
+  return 0;
+}
+
+extern "C" int d3a_conv_bwd_w(const d3a_conv_desc* d, void* stream) {
+  using namespace d3a;
+  if (check_geometry(d, "d3a_conv_bwd_w")) return -1;
+  D3A_CHECK_ARG(d->dy && d->dW, "d3a_conv_bwd_w: null dy / dW");
+  D3A_CHECK_ARG(d->splits >= 1 && d->splits < 65536, "d3a_conv_bwd_w: bad splits");
+  const int64_t Kc = (int64_t)d->C * d->KH * d->KW;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // 32 (co) x 32 (k) per wave, 16 waves per workgroup over consecutive row slices
+  const dim3 grid((unsigned)((Kc + 31) / 32), (unsigned)(d->CO / 32), (unsigned)d->splits);
+  if (d->x_u8) hipLaunchKernelGGL((conv_bwd_w_kernel<1, 16, true>), grid, dim3(1024), 0, st, *d);
+  else hipLaunchKernelGGL((conv_bwd_w_kernel<1, 16, false>), grid, dim3(1024), 0, st, *d);
+  D3A_LAUNCH_CHECK("d3a_conv_bwd_w");
+  return 0;
+}

@@ -114,14 +114,57 @@ __global__ __launch_bounds__(256) void outer_mask_kernel(const float* g, int64_t
   }
 }
 
+// ---- split-K partials: sum_q grad[q][i] in fp64 in a fixed order (run-to-run
+// bit-identical).  A segment with many partials (>= 64, e.g. one per batch
+// row) gives each element a group of L = 16 lanes: lane j sums partials
+// q = j, j + L, ... in order, then the group is summed by a fixed butterfly.
+// Loads are issued 8 at a time so a lane has 8 independent requests in flight.
+__host__ __device__ __forceinline__ int seg_lanes(int64_t n_partials) {
+  return n_partials >= 64 ? 16 : 1;
+}
+
+__device__ __forceinline__ double sum_partials(const float* g, int64_t n, int64_t stride,
+                                               int64_t i, int j, int L) {
+  double gd = 0.0;
+  int64_t q = j;
+  for (; q + 7 * L < n; q += 8 * L) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = g[(q + u * L) * stride + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) gd += (double)v[u];
+  }
+  for (; q < n; q += L) gd += (double)g[q * stride + i];
+  for (int o = L >> 1; o > 0; o >>= 1) gd += __shfl_xor(gd, o, 64);
+  return gd;
+}
+
 // ---- Adam (torch.optim.adam._single_tensor_adam, weight_decay = 0) ---------
-__global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
+// The grid is flat over the segments: segment s owns ceil(numel_s * L_s / 256)
+// consecutive blocks, in table order (no idle blocks for small segments).
+__device__ __forceinline__ void locate_block(const d3a_adam_segment* segs, int n_seg, int* s_seg,
+                                             int64_t* s_first) {
+  if (threadIdx.x == 0) {
+    int64_t first = 0;
+    int s = 0;
+    for (; s < n_seg - 1; ++s) {
+      const int64_t nb = (segs[s].numel * seg_lanes(segs[s].n_partials) + 255) / 256;
+      if ((int64_t)blockIdx.x < first + nb) break;
+      first += nb;
+    }
+    *s_seg = s;
+    *s_first = first;
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs, int n_seg,
                                                    const int64_t* step, double lr, double beta1,
                                                    double beta2, double eps, float grad_scale) {
   __shared__ float s_step_size, s_bc2_sqrt;
-  const d3a_adam_segment sg = segs[blockIdx.y];
+  __shared__ int s_seg;
+  __shared__ int64_t s_first;
+  locate_block(segs, n_seg, &s_seg, &s_first);
   const int64_t t = *step + 1;  // read by every block before the last one commits
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (threadIdx.x == 0) {
     // bias corrections in fp64 exactly as torch computes them in Python floats
     const double bc1 = 1.0 - pow(beta1, (double)t);
@@ -130,9 +173,13 @@ __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
     s_bc2_sqrt = (float)sqrt(bc2);
   }
   __syncthreads();
-  if (i < sg.numel) {
-    double gd = 0.0;  // split-K partials summed in a fixed order, in fp64
-    for (int64_t q = 0; q < sg.n_partials; ++q) gd += (double)sg.grad[q * sg.partial_stride + i];
+  const d3a_adam_segment sg = segs[s_seg];
+  const int L = seg_lanes(sg.n_partials);
+  const int64_t lt = ((int64_t)blockIdx.x - s_first) * 256 + threadIdx.x;
+  const int64_t i = lt / L;
+  if (i < sg.numel) {  // uniform over each lane group
+    const double gd = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i, (int)(lt % L), L);
+    if (lt % L) return;
     // grad_scale: 1, or 1/world after a data-parallel SUM all-reduce (exact
     // for power-of-two worlds)
     const float g = grad_scale == 1.f ? (float)gd : __fmul_rn((float)gd, grad_scale);
@@ -159,12 +206,19 @@ __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
 
 // ---- split-K partials -> one gradient (the data-parallel path reduces
 // before the all-reduce, so the collective moves one copy, not S partials)
-__global__ __launch_bounds__(256) void grad_reduce_kernel(const d3a_adam_segment* segs) {
-  const d3a_adam_segment sg = segs[blockIdx.y];
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= sg.numel) return;
-  double gd = 0.0;  // same fixed order and fp64 accumulation as adam_kernel
-  for (int64_t q = 0; q < sg.n_partials; ++q) gd += (double)sg.grad[q * sg.partial_stride + i];
+__global__ __launch_bounds__(256) void grad_reduce_kernel(const d3a_adam_segment* segs,
+                                                          int n_seg) {
+  __shared__ int s_seg;
+  __shared__ int64_t s_first;
+  locate_block(segs, n_seg, &s_seg, &s_first);
+  __syncthreads();
+  const d3a_adam_segment sg = segs[s_seg];
+  const int L = seg_lanes(sg.n_partials);
+  const int64_t lt = ((int64_t)blockIdx.x - s_first) * 256 + threadIdx.x;
+  const int64_t i = lt / L;
+  if (i >= sg.numel) return;  // uniform over each lane group
+  const double gd = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i, (int)(lt % L), L);
+  if (lt % L) return;
   sg.grad_out[i] = (float)gd;
 }
 
@@ -315,26 +369,25 @@ extern "C" int d3a_outer_mask_f32(const float* g, int64_t sgb, const float* w, i
   return 0;
 }
 
-extern "C" int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg, int64_t max_numel,
+extern "C" int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg, int64_t n_blocks,
                             const int64_t* step, double lr, double beta1, double beta2,
                             double eps, double grad_scale, void* stream) {
   D3A_CHECK_ARG(segs && step, "d3a_adam_f32: null pointer");
   D3A_CHECK_ARG(n_seg > 0 && n_seg < 65536, "d3a_adam_f32: bad segment count");
-  D3A_CHECK_ARG(max_numel > 0, "d3a_adam_f32: bad max_numel");
-  dim3 grid((unsigned)((max_numel + 255) / 256), (unsigned)n_seg);
-  hipLaunchKernelGGL(adam_kernel, grid, dim3(256), 0, (hipStream_t)stream, segs, step, lr, beta1,
-                     beta2, eps, (float)grad_scale);
+  D3A_CHECK_ARG(n_blocks >= n_seg && n_blocks < (1ll << 31), "d3a_adam_f32: bad n_blocks");
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)n_blocks), dim3(256), 0, (hipStream_t)stream,
+                     segs, (int)n_seg, step, lr, beta1, beta2, eps, (float)grad_scale);
   D3A_LAUNCH_CHECK("d3a_adam_f32");
   return 0;
 }
 
 extern "C" int d3a_grad_reduce_f32(const d3a_adam_segment* segs, int32_t n_seg,
-                                   int64_t max_numel, void* stream) {
+                                   int64_t n_blocks, void* stream) {
   D3A_CHECK_ARG(segs, "d3a_grad_reduce_f32: null pointer");
   D3A_CHECK_ARG(n_seg > 0 && n_seg < 65536, "d3a_grad_reduce_f32: bad segment count");
-  D3A_CHECK_ARG(max_numel > 0, "d3a_grad_reduce_f32: bad max_numel");
-  dim3 grid((unsigned)((max_numel + 255) / 256), (unsigned)n_seg);
-  hipLaunchKernelGGL(grad_reduce_kernel, grid, dim3(256), 0, (hipStream_t)stream, segs);
+  D3A_CHECK_ARG(n_blocks >= n_seg && n_blocks < (1ll << 31), "d3a_grad_reduce_f32: bad n_blocks");
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3((unsigned)n_blocks), dim3(256), 0,
+                     (hipStream_t)stream, segs, (int)n_seg);
   D3A_LAUNCH_CHECK("d3a_grad_reduce_f32");
   return 0;
 }

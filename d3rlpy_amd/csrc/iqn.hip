@@ -1,7 +1,8 @@
 // DiscreteCQL with an IQN Q-function on pixel observations (K5): the conv
-// encoder's data movement (im2col / col2im / layout transposes) and the IQN
-// head, loss and head backward.  The convolutions themselves are GEMMs
-// (d3a_gemm_f32) over the im2col matrices.
+// encoder's data movement (col2im / layout transposes; im2col is kept in the
+// ABI for reference-layout checks) and the IQN head, loss and head backward.
+// The conv forward and weight gradient are implicit GEMMs (conv.hip); the
+// conv input gradient is a GEMM into the column matrix + col2im.
 //
 // Reference (restated op for op, fp32):
 //   PixelEncoder._conv_encode / forward      models/torch/encoders.py:130-162
@@ -144,6 +145,46 @@ __global__ __launch_bounds__(256) void iqn_head_fwd_kernel(d3a_iqn_head_desc d) 
   }
 }
 
+// Same head, 16 lanes per row and 16-byte loads (F % 4 == 0): Wf staged in
+// LDS once per workgroup, each lane multiplies 4 features per load and the 16
+// lanes of a row are summed with a butterfly.  Bandwidth-bound on phi.
+__global__ __launch_bounds__(256) void iqn_head_fwd4_kernel(d3a_iqn_head_desc d) {
+  __shared__ __attribute__((aligned(16))) float sW[D3A_IQN_MAX_ACTIONS * 512];
+  const int F = d.F, A = d.A;
+  for (int i = threadIdx.x; i < A * F; i += 256) sW[i] = d.Wf[i];
+  __syncthreads();
+  const int sl = threadIdx.x & 15;
+  const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (r >= d.rows) return;
+  const int g = (int)(r / d.group_rows);
+  const int64_t b = (r - (int64_t)g * d.group_rows) / d.K;
+  const float4* h = reinterpret_cast<const float4*>(d.h[g] + b * F);
+  const float4* phi = reinterpret_cast<const float4*>(d.phi + r * F);
+  float acc[D3A_IQN_MAX_ACTIONS];
+#pragma unroll
+  for (int a = 0; a < D3A_IQN_MAX_ACTIONS; ++a) acc[a] = 0.f;
+  for (int n4 = sl; n4 < F / 4; n4 += 16) {
+    const float4 hv = h[n4], pv4 = phi[n4];
+    const float p0 = __fmul_rn(hv.x, pv4.x), p1 = __fmul_rn(hv.y, pv4.y);
+    const float p2 = __fmul_rn(hv.z, pv4.z), p3 = __fmul_rn(hv.w, pv4.w);
+#pragma unroll
+    for (int a = 0; a < D3A_IQN_MAX_ACTIONS; ++a) {
+      if (a < A) {
+        const float4 wv = *reinterpret_cast<const float4*>(&sW[a * F + 4 * n4]);
+        acc[a] = fmaf(p3, wv.w, fmaf(p2, wv.z, fmaf(p1, wv.y, fmaf(p0, wv.x, acc[a]))));
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < D3A_IQN_MAX_ACTIONS; ++a) {
+    if (a >= A) break;
+    float v = acc[a];
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (sl == 0) d.q[r * A + a] = v + d.bf[a];
+  }
+}
+
 // One workgroup per batch row b: Double-DQN target, quantile Huber TD loss
 // with the sample's taus, conservative term; dL/dq of the three gradient
 // passes (rows [0, 3BK) of dq: loss | logsumexp | data), per-row loss.
@@ -273,41 +314,63 @@ __global__ __launch_bounds__(1024) void iqn_loss_reduce_kernel(d3a_iqn_loss_desc
 //   dh[b][n] = (sum_r dprod * phi[r][n]) * [h[b][n] > 0]   (encoder fc ReLU)
 //   dWf partial[b][a][n] = sum_r dq[r][a] h[b][n] phi[r][n], dbf partial[b][a]
 __global__ __launch_bounds__(512) void iqn_head_bwd_kernel(d3a_iqn_head_bwd_desc d) {
+  // dq rows of this b (G passes x K quantiles x A), staged once: every thread
+  // reads them as LDS broadcasts
+  __shared__ float sdq[D3A_IQN_HEAD_BWD_MAX_ROWS * D3A_IQN_MAX_ACTIONS];
   const int64_t b = blockIdx.x;
-  const int K = d.K, A = d.A;
+  const int K = d.K, A = d.A, F = d.F;
   const int64_t BK = (int64_t)d.B * K;
-  for (int n = threadIdx.x; n < d.F; n += 512) {
-    const float hv = d.h[b * d.F + n];
+  const float* __restrict__ phi = d.phi;
+  float* __restrict__ dphi = d.dphi;
+  for (int i = threadIdx.x; i < d.G * K * A; i += 512) {
+    const int gk = i / A, a = i - gk * A;
+    const int g = gk / K, k = gk - g * K;
+    sdq[i] = d.dq[(g * BK + b * K + k) * A + a];
+  }
+  __syncthreads();
+  constexpr int UR = 8;  // rows loaded before any is processed
+  for (int n = threadIdx.x; n < F; n += 512) {
+    const float hv = d.h[b * F + n];
+    float wv[D3A_IQN_MAX_ACTIONS];
+#pragma unroll
+    for (int a = 0; a < D3A_IQN_MAX_ACTIONS; ++a) wv[a] = a < A ? d.Wf[(int64_t)a * F + n] : 0.f;
     float dh = 0.f;
     float dw[D3A_IQN_MAX_ACTIONS];
 #pragma unroll
     for (int a = 0; a < D3A_IQN_MAX_ACTIONS; ++a) dw[a] = 0.f;
     for (int g = 0; g < d.G; ++g) {
-      for (int k = 0; k < K; ++k) {
-        const int64_t r = g * BK + b * K + k;
-        const float ph = d.phi[r * d.F + n];
-        float dp = 0.f;
+      const int64_t rbase = g * BK + b * K;
+      for (int k0 = 0; k0 < K; k0 += UR) {
+        float ph[UR];
 #pragma unroll
-        for (int a = 0; a < D3A_IQN_MAX_ACTIONS; ++a) {
-          if (a >= A) break;
-          const float q = d.dq[r * A + a];
-          dp = fmaf(q, d.Wf[(int64_t)a * d.F + n], dp);
-          dw[a] = fmaf(q, __fmul_rn(hv, ph), dw[a]);
+        for (int u = 0; u < UR; ++u) ph[u] = k0 + u < K ? phi[(rbase + k0 + u) * F + n] : 0.f;
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+          if (k0 + u >= K) break;
+          const int64_t r = rbase + k0 + u;
+          const float* sq = &sdq[(g * K + k0 + u) * A];
+          float dp = 0.f;
+#pragma unroll
+          for (int a = 0; a < D3A_IQN_MAX_ACTIONS; ++a) {
+            if (a >= A) break;
+            const float q = sq[a];
+            dp = fmaf(q, wv[a], dp);
+            dw[a] = fmaf(q, __fmul_rn(hv, ph[u]), dw[a]);
+          }
+          dphi[r * F + n] = ph[u] > 0.f ? __fmul_rn(dp, hv) : 0.f;
+          dh = fmaf(dp, ph[u], dh);
         }
-        d.dphi[r * d.F + n] = ph > 0.f ? __fmul_rn(dp, hv) : 0.f;
-        dh = fmaf(dp, ph, dh);
       }
     }
-    d.dh[b * d.F + n] = hv > 0.f ? dh : 0.f;
+    d.dh[b * F + n] = hv > 0.f ? dh : 0.f;
 #pragma unroll
     for (int a = 0; a < D3A_IQN_MAX_ACTIONS; ++a)
-      if (a < A) d.dWf_part[(b * A + a) * d.F + n] = dw[a];
+      if (a < A) d.dWf_part[(b * A + a) * F + n] = dw[a];
   }
   if (threadIdx.x < (unsigned)A) {
     const int a = threadIdx.x;
     double s = 0.0;
-    for (int g = 0; g < d.G; ++g)
-      for (int k = 0; k < K; ++k) s += (double)d.dq[(g * BK + b * K + k) * A + a];
+    for (int gk = 0; gk < d.G * K; ++gk) s += (double)sdq[gk * A + a];
     d.dbf_part[b * A + a] = (float)s;
   }
 }
@@ -362,8 +425,17 @@ extern "C" int d3a_iqn_head_fwd(const d3a_iqn_head_desc* d, void* stream) {
   const int64_t groups = (d->rows + d->group_rows - 1) / d->group_rows;
   D3A_CHECK_ARG(groups <= D3A_IQN_MAX_GROUPS, "d3a_iqn_head_fwd: too many row groups");
   for (int64_t g = 0; g < groups; ++g) D3A_CHECK_ARG(d->h[g], "d3a_iqn_head_fwd: null h group");
-  hipLaunchKernelGGL(iqn_head_fwd_kernel, dim3((unsigned)((d->rows + 3) / 4)), dim3(256), 0,
-                     (hipStream_t)stream, *d);
+  const bool vec = d->F % 4 == 0 && d->F <= 512 &&
+                   (reinterpret_cast<uintptr_t>(d->phi) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(d->Wf) & 15) == 0;
+  bool hvec = true;
+  for (int64_t g = 0; g < groups; ++g) hvec = hvec && (reinterpret_cast<uintptr_t>(d->h[g]) & 15) == 0;
+  if (vec && hvec)
+    hipLaunchKernelGGL(iqn_head_fwd4_kernel, dim3((unsigned)((d->rows + 15) / 16)), dim3(256), 0,
+                       (hipStream_t)stream, *d);
+  else
+    hipLaunchKernelGGL(iqn_head_fwd_kernel, dim3((unsigned)((d->rows + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, *d);
   D3A_LAUNCH_CHECK("d3a_iqn_head_fwd");
   return 0;
 }
@@ -384,6 +456,8 @@ extern "C" int d3a_iqn_head_bwd(const d3a_iqn_head_bwd_desc* d, void* stream) {
   D3A_CHECK_ARG(d && d->h && d->phi && d->dq && d->Wf && d->dphi && d->dh && d->dWf_part &&
                 d->dbf_part, "d3a_iqn_head_bwd: null pointer");
   D3A_CHECK_ARG(d->A >= 1 && d->A <= D3A_IQN_MAX_ACTIONS && d->G >= 1, "d3a_iqn_head_bwd: bad sizes");
+  D3A_CHECK_ARG((int64_t)d->G * d->K <= D3A_IQN_HEAD_BWD_MAX_ROWS,
+                "d3a_iqn_head_bwd: G * K exceeds D3A_IQN_HEAD_BWD_MAX_ROWS");
   hipLaunchKernelGGL(iqn_head_bwd_kernel, dim3((unsigned)d->B), dim3(512), 0, (hipStream_t)stream,
                      *d);
   D3A_LAUNCH_CHECK("d3a_iqn_head_bwd");

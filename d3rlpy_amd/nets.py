@@ -187,7 +187,8 @@ class AdamGroup:
         self.step = state.step
         self.grad_store = store.like() if keep_grads else None
         segs = (N.AdamSegment * len(self.names))()
-        self.max_numel = 1
+        self.n_blocks = 0  # flat launch over the segments (d3a_adam_f32)
+        self.n_blocks_reduced = 0
         for i, n in enumerate(self.names):
             gt, parts = grads.parts[n]
             numel = store.numel(n)
@@ -200,7 +201,9 @@ class AdamGroup:
             segs[i].n_partials = parts
             segs[i].partial_stride = numel
             segs[i].grad_out = self.grad_store.ptr(n) if self.grad_store is not None else None
-            self.max_numel = max(self.max_numel, numel)
+            lanes = 16 if parts >= 64 else 1  # lanes per element (elementwise.hip seg_lanes)
+            self.n_blocks += (numel * lanes + 255) // 256
+            self.n_blocks_reduced += (numel + 255) // 256
         raw = bytes(segs)
         self.seg_table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
         self._segs = segs
@@ -225,14 +228,15 @@ class AdamGroup:
         from . import ops
         table = self.seg_table_reduced if reduced else self.seg_table
         assert table is not None
-        ops.adam(table, len(self.names), self.max_numel, self.step,
+        ops.adam(table, len(self.names), self.n_blocks_reduced if reduced else self.n_blocks,
+                 self.step,
                  self.lr, self.beta1, self.beta2, self.eps, grad_scale)
 
     def reduce(self) -> None:
         """grad_store <- sum of the split-K partials (no parameter update)."""
         from . import ops
         assert self.grad_store is not None
-        ops.grad_reduce(self.seg_table, len(self.names), self.max_numel)
+        ops.grad_reduce(self.seg_table, len(self.names), self.n_blocks)
 
     def grad_span(self) -> torch.Tensor:
         """The contiguous slice of grad_store holding this group's gradients."""

@@ -82,14 +82,14 @@ def outer_mask(g: int, sgb: int, w: int, swb: int, h: int, shb: int, out: int, s
                                        _stream()), "d3a_outer_mask_f32")
 
 
-def adam(segs: torch.Tensor, n_seg: int, max_numel: int, step: torch.Tensor, lr: float,
+def adam(segs: torch.Tensor, n_seg: int, n_blocks: int, step: torch.Tensor, lr: float,
          beta1: float, beta2: float, eps: float, grad_scale: float = 1.0) -> None:
-    N.check(N.lib().d3a_adam_f32(ptr(segs), n_seg, max_numel, ptr(step), lr, beta1, beta2, eps,
+    N.check(N.lib().d3a_adam_f32(ptr(segs), n_seg, n_blocks, ptr(step), lr, beta1, beta2, eps,
                                  grad_scale, _stream()), "d3a_adam_f32")
 
 
-def grad_reduce(segs: torch.Tensor, n_seg: int, max_numel: int) -> None:
-    N.check(N.lib().d3a_grad_reduce_f32(ptr(segs), n_seg, max_numel, _stream()),
+def grad_reduce(segs: torch.Tensor, n_seg: int, n_blocks: int) -> None:
+    N.check(N.lib().d3a_grad_reduce_f32(ptr(segs), n_seg, n_blocks, _stream()),
             "d3a_grad_reduce_f32")
 
 
@@ -135,13 +135,13 @@ def call_desc(fn_name: str, desc: C.Structure) -> None:
 # ---------------------------------------------------------------------------
 def linear_fwd(x: int, x_shared: bool, ldx: int, W: int, b: int, y: int, C_: int, R: int,
                n_in: int, n_out: int, relu: bool, ldy: Optional[int] = None,
-               sxb: Optional[int] = None, syb: Optional[int] = None) -> None:
+               sxb: Optional[int] = None, syb: Optional[int] = None, variant: int = -1) -> None:
     """y[c] = act(x[c] @ W[c]^T + b[c]); x rows have stride ldx; y is [C][R][n_out]."""
     ldy = n_out if ldy is None else ldy
     sxb = (0 if x_shared else R * ldx) if sxb is None else sxb
     syb = R * ldy if syb is None else syb
     gemm(x, W, y, R, n_out, n_in, batch=C_, sA=(sxb, ldx, 1), sB=(n_out * n_in, 1, n_in),
-         sC=(syb, ldy, 1), bias=b, sbias=n_out, relu=relu)
+         sC=(syb, ldy, 1), bias=b, sbias=n_out, relu=relu, variant=variant)
 
 
 def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: int, C_: int,

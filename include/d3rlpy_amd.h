@@ -197,20 +197,23 @@ typedef struct d3a_adam_segment {
  * amsgrad=False) as created by AdamFactory (d3rlpy/models/optimizers.py:106-138):
  *   m = lerp(m, g, 1-b1); v = v*b2 + (1-b2)*g*g; t = *step + 1
  *   p += -(lr/(1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
- * `segs` is a DEVICE array of n_seg segments.  *step (device int64, the
+ * `segs` is a DEVICE array of n_seg segments; the launch is flat over them:
+ * n_blocks = sum_s ceil(numel_s * L_s / 256), L_s = 16 if n_partials_s >= 64
+ * else 1 (segment s owns the next ceil(numel_s * L_s / 256) blocks, in table
+ * order; L_s lanes share one element's partial sum).  *step (device int64, the
  * optimiser's completed steps) is only read; commit it with d3a_step_end.
  * The reduced gradient is multiplied by grad_scale (1, or 1/world after a
  * data-parallel SUM all-reduce). */
 int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg,
-                 int64_t max_numel, const int64_t* step,
+                 int64_t n_blocks, const int64_t* step,
                  double lr, double beta1, double beta2, double eps,
                  double grad_scale, void* stream);
 
 /* grad_out = sum of the n_partials split-K partials of each segment (fp64
- * accumulation, same order as d3a_adam_f32) — the data-parallel path's
+ * accumulation, same order and flat grid as d3a_adam_f32) — the data-parallel path's
  * reduction before the gradient all-reduce. */
 int d3a_grad_reduce_f32(const d3a_adam_segment* segs, int32_t n_seg,
-                        int64_t max_numel, void* stream);
+                        int64_t n_blocks, void* stream);
 
 /* soft_sync (d3rlpy/torch_utility.py:27-33): targ = targ*(1-tau) + tau*src,
  * three separately rounded fp32 ops (mul_, tau*p, add_), bit-exact. */
@@ -527,6 +530,32 @@ typedef struct d3a_col2im_desc {
 } d3a_col2im_desc;
 int d3a_col2im(const d3a_col2im_desc* d, void* stream);
 
+/* Implicit-GEMM convolution (nn.Conv2d without padding) of PixelEncoder
+ * (encoders.py:130-136): no im2col matrix in HBM.  Input x_u8 NCHW uint8,
+ * scaled by 1/255 on load (PixelScaler.transform, scalers.py:109-110; needs
+ * KW % 4 == 0) or x_f32 NHWC (the previous conv's output; needs C % 4 == 0);
+ * weight [CO][C][KH][KW] (nn.Conv2d layout), CO = 32 or 64.
+ *   d3a_conv_fwd:   y[(b, oy, ox)][co] = act(conv(x, weight) + bias)
+ *                   (act = ReLU when relu != 0), NHWC.  fp32 input needs
+ *                   `wpack`, CO*C*KH*KW floats of scratch (the weight is
+ *                   re-laid [CO][KH][KW][C] there first, in the same stream).
+ *   d3a_conv_bwd_w: dW[s][co][c][kh][kw] = sum over rows of split s of
+ *                   dy[row][co] * x-window(row)[c][kh][kw]; db[s][co] (optional)
+ *                   = sum of dy over the split's rows.  dy is the gradient at
+ *                   the pre-activation, NHWC [B*OH*OW][CO]; rows are cut into
+ *                   `splits` equal consecutive chunks (the Adam kernel sums the
+ *                   split partials in order). */
+typedef struct d3a_conv_desc {
+  const uint8_t* x_u8; const float* x_f32;
+  const float* weight; const float* bias;
+  float* y; float* wpack;
+  const float* dy; float* dW; float* db;
+  int32_t B, C, H, W, KH, KW, S, OH, OW, CO;
+  int32_t relu, splits;
+} d3a_conv_desc;
+int d3a_conv_fwd(const d3a_conv_desc* d, void* stream);
+int d3a_conv_bwd_w(const d3a_conv_desc* d, void* stream);
+
 /* Per-sample [P][C] (NHWC) <-> [C][P] (NCHW) transpose, optional [mask > 0]
  * in the destination layout: the flatten before PixelEncoder._fc
  * (encoders.py:157) and its gradient. */
@@ -545,6 +574,7 @@ int d3a_iqn_prior(const d3a_iqn_prior_desc* d, void* stream);
 
 #define D3A_IQN_MAX_ACTIONS 18
 #define D3A_IQN_MAX_GROUPS 8
+#define D3A_IQN_HEAD_BWD_MAX_ROWS 512 /* G * K of d3a_iqn_head_bwd */
 /* q[r][a] = (h[b] * phi[r]) . Wf[a] + bf[a] (compute_iqn_feature's product
  * + DiscreteIQNQFunction._fc, iqn_q_function.py:45-47, 82-88).  Rows come in
  * groups of group_rows = B*K; group g reads its features from h[g]

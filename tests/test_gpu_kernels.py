@@ -166,7 +166,9 @@ def test_soft_update_bit_exact(dev):
 
 
 def test_adam_matches_torch(dev):
-    """torch.optim.Adam single-tensor step (the oracle's CPU Adam), 3 steps."""
+    """torch.optim.Adam single-tensor step (the oracle's CPU Adam), 3 steps;
+    11 split-K partials (one unrolled batch of 8 + a remainder) over a
+    multi-block segment followed by a one-block segment (flat grid)."""
     from d3rlpy_amd.nets import AdamGroup, GradSpace, ParamStore
     store = ParamStore()
     store.add("w", (300, 7))
@@ -178,7 +180,7 @@ def test_adam_matches_torch(dev):
     store.view("w").copy_(w0)
     store.view("b").copy_(b0)
     gs = GradSpace(dev)
-    gw = gs.add("w", (300, 7), 3)
+    gw = gs.add("w", (300, 7), 11)
     gb = gs.add("b", (5,), 1)
     from d3rlpy_amd import ops
     from d3rlpy_amd.nets import OptimState
@@ -187,7 +189,7 @@ def test_adam_matches_torch(dev):
     pb = torch.nn.Parameter(b0.clone())
     topt = torch.optim.Adam([pw, pb], lr=3e-4)
     for it in range(3):
-        parts = torch.randn(3, 300, 7, generator=g) * 10 ** (-it)
+        parts = torch.randn(11, 300, 7, generator=g) * 10 ** (-it)
         gbv = torch.randn(5, generator=g)
         gw.copy_(parts)
         gb.copy_(gbv.view(1, 5))
@@ -204,6 +206,42 @@ def test_adam_matches_torch(dev):
     torch.testing.assert_close(store.view("b").cpu(), pb.detach(), rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(opt.exp_avg_sq.view("w").cpu(), topt.state[pw]["exp_avg_sq"],
                                rtol=1e-6, atol=1e-12)
+
+
+def test_adam_many_partials_matches_torch(dev):
+    """A segment with >= 64 partials (one per batch row, e.g. the IQN head's
+    weight gradient) is summed by 16-lane groups in a fixed order: 3 Adam
+    steps vs torch.optim.Adam on the fp64 sum of the partials."""
+    from d3rlpy_amd import ops
+    from d3rlpy_amd.nets import AdamGroup, GradSpace, OptimState, ParamStore
+    store = ParamStore()
+    store.add("w", (4, 517))
+    store.add("b", (3,))
+    store.allocate(dev)
+    g = torch.Generator().manual_seed(9)
+    w0, b0 = torch.randn(4, 517, generator=g), torch.randn(3, generator=g)
+    store.view("w").copy_(w0)
+    store.view("b").copy_(b0)
+    gs = GradSpace(dev)
+    gw = gs.add("w", (4, 517), 203)
+    gb = gs.add("b", (3,), 70)
+    opt = AdamGroup(OptimState(store, ["w", "b"], lr=1e-3), gs)
+    pw, pb = torch.nn.Parameter(w0.clone()), torch.nn.Parameter(b0.clone())
+    topt = torch.optim.Adam([pw, pb], lr=1e-3)
+    for it in range(3):
+        parts = torch.randn(203, 4, 517, generator=g)
+        pbv = torch.randn(70, 3, generator=g)
+        gw.copy_(parts)
+        gb.copy_(pbv)
+        opt.launch()
+        ops.step_end(opt.step, 1)
+        pw.grad = parts.double().sum(0).float()
+        pb.grad = pbv.double().sum(0).float()
+        topt.step()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(store.view("w").cpu(), pw.detach(), rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(store.view("b").cpu(), pb.detach(), rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(opt.grad("w").cpu(), pw.grad, rtol=1e-6, atol=1e-6)
 
 
 def test_philox_statistics(dev):
