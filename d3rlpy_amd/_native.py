@@ -154,6 +154,7 @@ class Td3bcActorDesc(C.Structure):
         ("act", vp), ("dhead", vp), ("metrics", vp),
         ("alpha", C.c_float),
         ("B", C.c_int32), ("D", C.c_int32), ("A", C.c_int32), ("ldx", C.c_int32),
+        ("bc", C.c_int32),
     ]
 
 

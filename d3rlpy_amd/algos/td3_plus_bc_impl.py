@@ -42,6 +42,10 @@ METRIC_NAMES = ("critic_loss", "actor_loss")
 
 
 class TD3PlusBCImpl(ImplBase):
+    # behaviour-cloning actor loss (td3_plus_bc_impl.py:64-70); TD3Impl /
+    # DDPGImpl (algos/td3.py) clear it for -mean Q_0 (ddpg_impl.py:244-249)
+    _BC = True
+
     def __init__(
         self,
         observation_shape: Sequence[int],
@@ -67,11 +71,11 @@ class TD3PlusBCImpl(ImplBase):
         super().__init__(observation_shape, action_size, scaler, action_scaler, reward_scaler,
                          use_gpu)
         if q_func_factory.get_type() != "mean":
-            raise NotImplementedError("TD3+BC on HIP supports the 'mean' Q function")
+            raise NotImplementedError(f"{self._name()} on HIP supports the 'mean' Q function")
         if len(observation_shape) != 1:
-            raise NotImplementedError("TD3+BC on HIP supports vector observations")
+            raise NotImplementedError(f"{self._name()} on HIP supports vector observations")
         if scaler is not None and scaler.get_type() != "standard":
-            raise NotImplementedError("TD3+BC on HIP supports the 'standard' scaler")
+            raise NotImplementedError(f"{self._name()} on HIP supports the 'standard' scaler")
         if action_scaler is not None or reward_scaler is not None:
             raise NotImplementedError("action/reward scalers are out of scope (SURVEY §2 #4)")
         self._actor_learning_rate = actor_learning_rate
@@ -88,6 +92,10 @@ class TD3PlusBCImpl(ImplBase):
         self._target_smoothing_clip = target_smoothing_clip
         self._alpha = alpha
         self._ws: Dict[int, "_Workspace"] = {}
+
+    @classmethod
+    def _name(cls) -> str:
+        return cls.__name__.replace("Impl", "")
 
     # ------------------------------------------------------------------ build
     def build(self) -> None:
@@ -260,8 +268,8 @@ class TD3PlusBCImpl(ImplBase):
         return torch.tanh(acts.out[0])
 
     def _sample_action(self, x: torch.Tensor) -> torch.Tensor:
-        # DeterministicPolicy.sample_with_log_prob (policies.py:64-69)
-        raise NotImplementedError("deterministic policy does not support sample")
+        # DDPGImpl._sample_action (ddpg_impl.py:262-263): the greedy action
+        return self._predict_best_action(x)
 
     def _predict_value(self, x: torch.Tensor, action: torch.Tensor) -> torch.Tensor:
         xa = torch.cat([x.float(), action.float()], dim=1).contiguous()
@@ -359,6 +367,7 @@ class _Workspace:
         a.act, a.dhead, a.metrics = self.act.data_ptr(), self.dhead.data_ptr(), self.metrics.data_ptr()
         a.alpha = impl._alpha
         a.B, a.D, a.A, a.ldx = B, D, A, LDX
+        a.bc = int(impl._BC)
         self.actor_desc = a
 
     def stage(self, db: DeviceBatch, noise) -> None:
@@ -419,7 +428,9 @@ class _Workspace:
         st, tg = impl.store, impl.targ
         ops.call_desc("d3a_td3_prep", self.prep_desc)
         if critic:
-            if not self._external_noise:
+            # DDPG (sigma = 0) draws no smoothing noise: the zero buffer leaves
+            # clamp(tanh(mu') + 0, -1, 1) = tanh(mu') (ddpg_impl.py:251-260)
+            if not self._external_noise and impl._target_smoothing_sigma != 0.0:
                 ops.philox_fill(self.noise, B * A, 0, -1.0, 1.0, self.seed, self.rng_ctr,
                                 self.rng_ticket)
             # target action: targ_policy(s') + clipped noise (td3_impl.py:61-78)

@@ -7,6 +7,7 @@
 //                q_functions/mean_q_function.py:74-87   sum_c mean((q_c - y)^2)
 //   actor loss   algos/torch/td3_plus_bc_impl.py:64-70
 //                lam = alpha / mean|Q_0(s, pi(s))|;  L = -lam mean Q_0 + mean((a - pi(s))^2)
+//                (bc = 0: the TD3 / DDPG loss -mean Q_0, ddpg_impl.py:244-249)
 //
 // The GEMM-shaped work (policy / critic layers and their backward) runs in
 // gemm.hip / heads.hip; these kernels produce the layer inputs and the
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(1024) void td3bc_actor_seed_kernel(d3a_td3bc_actor_
     double t = 0.0;
     for (int w = 0; w < (nt >> 6); ++w) t += sd[w];
     const float mabs = (float)(t / d.B);
-    s_lam = __fdiv_rn(d.alpha, mabs);
+    s_lam = d.bc ? __fdiv_rn(d.alpha, mabs) : 1.f;
   }
   __syncthreads();
   if (lane == 0) sd[wid] = sq;
@@ -147,12 +148,15 @@ __global__ __launch_bounds__(1024) void td3bc_actor_head_kernel(d3a_td3bc_actor_
     const int64_t b = i / d.A;
     const int j = (int)(i - b * d.A);
     const float a = d.pi_act[i];
-    const float diff = __fsub_rn(d.act[i], a);
-    s += (double)__fmul_rn(diff, diff);
-    // (actions - action) ** 2 -> d/d action = -(gm * 2 * diff)
-    const float g_bc = -__fmul_rn(gm, __fmul_rn(2.f, diff));
     const float g_q = d.dq_da[b * d.ld_da + d.da_off + j];
-    const float ga = __fadd_rn(g_q, g_bc);
+    float ga = g_q;
+    if (d.bc) {
+      const float diff = __fsub_rn(d.act[i], a);
+      s += (double)__fmul_rn(diff, diff);
+      // (actions - action) ** 2 -> d/d action = -(gm * 2 * diff)
+      const float g_bc = -__fmul_rn(gm, __fmul_rn(2.f, diff));
+      ga = __fadd_rn(g_q, g_bc);
+    }
     d.dhead[i] = __fmul_rn(ga, __fsub_rn(1.f, __fmul_rn(a, a)));
   }
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -161,7 +165,7 @@ __global__ __launch_bounds__(1024) void td3bc_actor_head_kernel(d3a_td3bc_actor_
   if (tid == 0) {
     double t = 0.0;
     for (int w = 0; w < (nt >> 6); ++w) t += sd[w];
-    d.metrics[1] = __fadd_rn(d.scalars[1], (float)(t / (double)n));
+    d.metrics[1] = d.bc ? __fadd_rn(d.scalars[1], (float)(t / (double)n)) : d.scalars[1];
   }
 }
 

@@ -427,6 +427,9 @@ typedef struct d3a_td3bc_actor_desc {
   const float* act; float* dhead; float* metrics;
   float alpha;
   int32_t B, D, A, ldx;
+  /* 1: TD3+BC loss (lam = alpha / mean|Q0|, + BC term); 0: the DDPG / TD3
+   * actor loss -mean Q0 (ddpg_impl.py:244-249), lam = 1, no BC term */
+  int32_t bc;
 } d3a_td3bc_actor_desc;
 int d3a_td3bc_actor_input(const d3a_td3bc_actor_desc* d, void* stream);
 int d3a_td3bc_actor_seed(const d3a_td3bc_actor_desc* d, void* stream);

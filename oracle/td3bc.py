@@ -6,7 +6,10 @@ Follows, op for op and in the same order:
   d3rlpy/algos/torch/td3_plus_bc_impl.py:64-70 (BC actor loss)
   d3rlpy/algos/td3_plus_bc.py:177-192      (TD3PlusBC._update schedule)
   d3rlpy/torch_utility.py:179-181 + preprocessing/scalers.py:350-354 (standard scaler)
-with the target-smoothing noise passed in explicitly.
+with the target-smoothing noise passed in explicitly.  TD3Oracle / DDPGOracle
+restate the parents: DDPGImpl.compute_actor_loss (ddpg_impl.py:244-249) and,
+for DDPG, DDPGImpl.compute_target (ddpg_impl.py:251-260) with the schedules of
+algos/td3.py:182-203 and algos/ddpg.py:167-174.
 """
 from __future__ import annotations
 
@@ -48,6 +51,8 @@ def fit_standard_scaler(observations: np.ndarray):
 
 
 class TD3PlusBCOracle:
+    _BC = True
+
     def __init__(self, observation_size: int, action_size: int,
                  actor_learning_rate: float = 3e-4, critic_learning_rate: float = 3e-4,
                  gamma: float = 0.99, tau: float = 0.005, n_critics: int = 2,
@@ -108,6 +113,8 @@ class TD3PlusBCOracle:
         """td3_plus_bc_impl.py:64-70."""
         action = self._policy(batch.observations)
         q_t = self._q_func(batch.observations, action, "none")[0]
+        if not self._BC:
+            return -q_t.mean()  # ddpg_impl.py:244-249
         lam = self._alpha / (q_t.abs().mean()).detach()
         return lam * -q_t.mean() + ((batch.actions - action) ** 2).mean()
 
@@ -134,4 +141,38 @@ class TD3PlusBCOracle:
             metrics["actor_loss"] = float(self.update_actor(batch))
             self.update_critic_target()
             self.update_actor_target()
+        return metrics
+
+
+class TD3Oracle(TD3PlusBCOracle):
+    """TD3Impl (td3_impl.py:14-78): DDPG actor loss, smoothed target."""
+
+    _BC = False
+
+    def __init__(self, observation_size: int, action_size: int, **kw):
+        kw.setdefault("alpha", 0.0)
+        super().__init__(observation_size, action_size, **kw)
+
+
+class DDPGOracle(TD3Oracle):
+    """DDPGImpl (ddpg_impl.py:232-263) with the DDPG._update schedule."""
+
+    def __init__(self, observation_size: int, action_size: int, n_critics: int = 1, **kw):
+        super().__init__(observation_size, action_size, n_critics=n_critics,
+                         target_smoothing_sigma=0.0, target_smoothing_clip=0.0, **kw)
+
+    def compute_target(self, batch: Batch, noise: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """ddpg_impl.py:251-260 (no smoothing noise)."""
+        with torch.no_grad():
+            action = self._targ_policy(batch.next_observations)
+            return self._targ_q_func.compute_target(batch.next_observations,
+                                                    action.clamp(-1.0, 1.0), reduction="min")
+
+    def update(self, batch: Batch, noise: Optional[torch.Tensor] = None, grad_step: int = 0,
+               update_actor_interval: int = 1) -> Dict[str, float]:
+        """algos/ddpg.py:167-174."""
+        metrics = {"critic_loss": float(self.update_critic(batch, noise))}
+        metrics["actor_loss"] = float(self.update_actor(batch))
+        self.update_critic_target()
+        self.update_actor_target()
         return metrics

@@ -2,7 +2,7 @@
 import numpy as np
 import torch
 
-from oracle.td3bc import StandardScalerT, TD3PlusBCOracle
+from oracle.td3bc import DDPGOracle, StandardScalerT, TD3Oracle, TD3PlusBCOracle
 
 TD3_STATE_KEYS = ("_q_func", "_targ_q_func", "_policy", "_targ_policy", "_critic_optim",
                   "_actor_optim")
@@ -35,9 +35,33 @@ def make_td3_impl(D, A, hidden, C=2, scaler_stats=None, **kw):
     return impl
 
 
-def make_td3_oracle(D, A, hidden, C=2, seed=0, scaler_stats=None, **kw):
+def make_td3_oracle(D, A, hidden, C=2, seed=0, scaler_stats=None, kind="td3_plus_bc", **kw):
     scaler = None if scaler_stats is None else StandardScalerT(*scaler_stats)
-    return TD3PlusBCOracle(D, A, n_critics=C, hidden_units=hidden, scaler=scaler, seed=seed, **kw)
+    cls = {"td3_plus_bc": TD3PlusBCOracle, "td3": TD3Oracle, "ddpg": DDPGOracle}[kind]
+    return cls(D, A, n_critics=C, hidden_units=hidden, scaler=scaler, seed=seed, **kw)
+
+
+def make_family_impl(kind, D, A, hidden, C, scaler_stats=None):
+    """TD3Impl / DDPGImpl (d3rlpy_amd.algos.td3) with the reference defaults."""
+    from d3rlpy_amd.algos.td3 import DDPGImpl, TD3Impl
+    from d3rlpy_amd.factories import AdamFactory, MeanQFunctionFactory, VectorEncoderFactory
+    from d3rlpy_amd.preprocessing import StandardScaler
+    scaler = None
+    if scaler_stats is not None:
+        scaler = StandardScaler(mean=scaler_stats[0], std=scaler_stats[1])
+    args = dict(observation_shape=(D,), action_size=A, actor_learning_rate=3e-4,
+                critic_learning_rate=3e-4, actor_optim_factory=AdamFactory(),
+                critic_optim_factory=AdamFactory(),
+                actor_encoder_factory=VectorEncoderFactory(hidden),
+                critic_encoder_factory=VectorEncoderFactory(hidden),
+                q_func_factory=MeanQFunctionFactory(), gamma=0.99, tau=0.005, n_critics=C,
+                use_gpu=0, scaler=scaler, action_scaler=None, reward_scaler=None)
+    if kind == "td3":
+        impl = TD3Impl(target_smoothing_sigma=0.2, target_smoothing_clip=0.5, **args)
+    else:
+        impl = DDPGImpl(**args)
+    impl.build()
+    return impl
 
 
 def td3_oracle_state(orc):

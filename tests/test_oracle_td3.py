@@ -86,3 +86,30 @@ def test_delayed_actor_schedule():
     m = orc.update(b, n, grad_step=2)
     assert set(m) == {"critic_loss", "actor_loss"}
     assert not all(torch.equal(a, b_) for a, b_ in zip(t0, orc._targ_q_func.parameters()))
+
+
+def test_td3_ddpg_oracle_parents():
+    """TD3Oracle / DDPGOracle restate the parents of TD3PlusBCImpl:
+    the DDPG actor loss is -mean Q_0(s, pi(s)) (ddpg_impl.py:244-249), and
+    DDPG's unsmoothed target (ddpg_impl.py:251-260) equals TD3's target with
+    sigma = clip = 0 (what the HIP DDPGImpl runs) bit for bit."""
+    import torch
+    from oracle.cql import Batch
+    from oracle.td3bc import DDPGOracle, TD3Oracle
+    rs = np.random.RandomState(3)
+    B, D, A = 16, 4, 2
+    arrs = (rs.randn(B, D).astype(np.float32), rs.uniform(-1, 1, (B, A)).astype(np.float32),
+            rs.randn(B).astype(np.float32), rs.randn(B, D).astype(np.float32),
+            np.zeros(B, np.float32), np.ones(B, np.float32))
+    tb = Batch.from_numpy(*arrs)
+    td3 = TD3Oracle(D, A, hidden_units=(32, 32), seed=1)
+    with torch.no_grad():
+        act = td3._policy(tb.observations)
+        q0 = td3._q_func(tb.observations, act, "none")[0]
+        assert torch.equal(td3.compute_actor_loss(tb), -q0.mean())
+    ddpg = DDPGOracle(D, A, hidden_units=(32, 32), seed=1)
+    assert len(ddpg._q_func.q_funcs) == 1
+    ref = TD3Oracle(D, A, n_critics=1, hidden_units=(32, 32), seed=1,
+                    target_smoothing_sigma=0.0, target_smoothing_clip=0.0)
+    noise = torch.randn(B, A, generator=torch.Generator().manual_seed(0))
+    assert torch.equal(ddpg.compute_target(tb), ref.compute_target(tb, noise))
