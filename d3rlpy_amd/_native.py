@@ -75,6 +75,7 @@ class CqlSampleDesc(C.Structure):
         ("B", C.c_int32), ("D", C.c_int32), ("A", C.c_int32), ("N", C.c_int32),
         ("ldx", C.c_int32),
         ("min_logstd", C.c_float), ("max_logstd", C.c_float),
+        ("eps_targ", vp), ("logp_targ", vp), ("soft_target", C.c_int32),
     ]
 
 
@@ -92,6 +93,7 @@ class CqlLossDesc(C.Structure):
         ("alpha_threshold", C.c_float), ("conservative_weight", C.c_float),
         ("update_temp", C.c_int32), ("update_alpha", C.c_int32), ("update_critic", C.c_int32),
         ("dp_phase", C.c_int32), ("scalar_grads", vp), ("grad_scale", C.c_float),
+        ("logp_targ", vp), ("soft_target", C.c_int32), ("conservative", C.c_int32),
     ]
 
 

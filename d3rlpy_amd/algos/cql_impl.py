@@ -46,6 +46,9 @@ METRIC_NAMES = ("temp_loss", "temp", "alpha_loss", "alpha", "critic_loss", "acto
 
 
 class CQLImpl(ImplBase):
+    # conservative term + alpha (cql_impl.py); SACImpl (algos/sac.py) clears it
+    _CONSERVATIVE = True
+
     def __init__(
         self,
         observation_shape: Sequence[int],
@@ -77,8 +80,6 @@ class CQLImpl(ImplBase):
     ):
         super().__init__(observation_shape, action_size, scaler, action_scaler, reward_scaler,
                          use_gpu)
-        if soft_q_backup:
-            raise NotImplementedError("soft_q_backup=True is not supported by the HIP CQLImpl")
         if q_func_factory.get_type() != "mean":
             raise NotImplementedError("CQL on HIP supports the 'mean' Q function")
         if len(observation_shape) != 1:
@@ -370,9 +371,11 @@ class _Workspace:
     def __init__(self, impl: CQLImpl, B: int):
         dev = impl.torch_device
         self.impl = impl
-        D, A, C, N = impl._observation_shape[0], impl._action_size, impl._n_critics, \
-            impl._n_action_samples
+        D, A, C = impl._observation_shape[0], impl._action_size, impl._n_critics
+        # SAC (no conservative term) draws no importance samples: N = 0
+        N = impl._n_action_samples if impl._CONSERVATIVE else 0
         self.B, self.D, self.A, self.C, self.N = B, D, A, C, N
+        self.soft = bool(impl._soft_q_backup)
         NB = N * B
         self.NB = NB
         self.R = 6 * NB + B
@@ -387,14 +390,17 @@ class _Workspace:
         self.rew = z(B)
         self.term = z(B)
         self.nsteps = z(B)
-        # noise: [eps_temp | eps_pi (2 sets x 2 x N x B x A) | eps_actor | u_rand (2 x NB x A)]
-        self.n_normal = (B + 4 * NB + B) * A
+        # noise: [eps_temp | eps_pi (2 sets x 2 x N x B x A) | eps_actor | eps_targ
+        # (soft target only) | u_rand (2 x NB x A)]
+        nt = B * A if self.soft else 0
+        self.n_normal = (B + 4 * NB + B) * A + nt
         self.n_uniform = 2 * NB * A
         self.noise = z(self.n_normal + self.n_uniform)
         o = 0
         self.eps_temp = self.noise[o:o + B * A]; o += B * A
         self.eps_pi = self.noise[o:o + 4 * NB * A]; o += 4 * NB * A
         self.eps_actor = self.noise[o:o + B * A]; o += B * A
+        self.eps_targ = self.noise[o:o + nt]; o += nt
         self.u_rand = self.noise[o:o + 2 * NB * A]
         self.rng_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         self.rng_ticket = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -409,6 +415,7 @@ class _Workspace:
         self.logp_is = z(4 * NB)
         self.actor_u = z(B, A)
         self.actor_logp = z(B)
+        self.logp_targ = z(B)
         # critic / target / actor-critic activations
         self.qacts = mlp.Acts.alloc(impl.critic, self.R, dev)
         self.tacts = mlp.Acts.alloc(impl.critic, B, dev)
@@ -459,6 +466,9 @@ class _Workspace:
         s.B, s.D, s.A, s.N = self.B, self.D, self.A, self.N
         s.ldx = self.LDX
         s.min_logstd, s.max_logstd = impl._min_logstd, impl._max_logstd
+        s.soft_target = int(self.soft)
+        if self.soft:
+            s.eps_targ, s.logp_targ = self.eps_targ.data_ptr(), self.logp_targ.data_ptr()
         self.sample_desc = s
 
         l = NAT.CqlLossDesc()
@@ -487,6 +497,8 @@ class _Workspace:
         l.conservative_weight = impl._conservative_weight
         l.scalar_grads = self.scalar_grads.data_ptr()
         l.grad_scale = 1.0 if impl._dp is None else impl._dp.scale
+        l.soft_target, l.conservative = int(self.soft), int(impl._CONSERVATIVE)
+        l.logp_targ = self.logp_targ.data_ptr()
         self.loss_desc = l
 
         h = NAT.SacActorHeadDesc()
@@ -532,6 +544,8 @@ class _Workspace:
         ur[0].copy_(g("alpha_rand").view(NB, A))
         ur[1].copy_(g("critic_rand").view(NB, A))
         self.eps_actor.copy_(g("eps_actor").view(-1))
+        if self.soft:
+            self.eps_targ.copy_(g("eps_targ").view(-1))
 
     # ------------------------------------------------------------ roofline
     def dominant_kernel(self):

@@ -86,12 +86,19 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
     d.logp_temp[b] = squashed_sample(hrow, hrow + A, d.eps_temp + b * A, (int)A, d.min_logstd,
                                      d.max_logstd, nullptr, nullptr);
   } else if (i < R + 2 * B) {
-    // deterministic target action tanh(mu(s_t+1)) (NormalPolicy.best_action)
     const int64_t b = i - R - B;
     const float* hrow = d.head + (B + b) * H;
     float* x = d.x_targ + b * DA;
     for (int64_t j = 0; j < D; ++j) x[j] = d.next_obs[b * D + j];
-    for (int64_t j = 0; j < A; ++j) x[D + j] = tanhf(hrow[j]);
+    if (d.soft_target) {
+      // SACImpl.compute_target: policy.sample_with_log_prob(next_obs)
+      d.logp_targ[b] = squashed_sample(hrow, hrow + A, d.eps_targ + b * A, (int)A, d.min_logstd,
+                                       d.max_logstd, act, nullptr);
+      for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
+    } else {
+      // deterministic target action tanh(mu(s_t+1)) (NormalPolicy.best_action)
+      for (int64_t j = 0; j < A; ++j) x[D + j] = tanhf(hrow[j]);
+    }
   } else {
     // actor sample (rsample, with gradient later)
     const int64_t b = i - R - 2 * B;
@@ -242,28 +249,33 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   __syncthreads();
   if (tid == 0) {
     sh[0] = fminf(fmaxf(expf(*d.log_alpha), 0.f), 1e6f);
-    d.scalars[0] = expf(*d.log_temp);
+    sh[1] = expf(*d.log_temp);  // the temperature after update_temp
+    d.scalars[0] = sh[1];
     d.scalars[1] = sh[0];
   }
   __syncthreads();
   const float ca = sh[0];
+  const float temp = sh[1];
+  const bool cons_on = d.conservative != 0;
 
   if (!d.update_critic) return;
   // ---- update_critic loss and dL/dQ (ddpg_impl.py:138-165, cql_impl.py:110-117) ----
-  const float gcons = ca * d.conservative_weight / (float)(C * B);
+  const float gcons = cons_on ? ca * d.conservative_weight / (float)(C * B) : 0.f;
   float s_td = 0.f, s_l = 0.f, s_d = 0.f;
   for (int64_t p = tid; p < C * B; p += nt) {
     const int64_t c = p / B, b = p % B;
-    // deterministic target: min over target critics
+    // target: min over target critics
     float tq = d.q_targ[b];
     for (int64_t k = 1; k < C; ++k) tq = fminf(tq, d.q_targ[k * B + b]);
+    // soft backup: target - exp(log_temp) * log_prob (sac_impl.py:156-162)
+    if (d.soft_target) tq = tq - temp * d.logp_targ[b];
     const float gam = powf(d.gamma, d.n_steps[b]);
     const float y = d.rew[b] + gam * tq * (1.f - d.term[b]);
     const float qd = d.q[c * d.R + 6 * NB + b];
     const float diff = qd - y;
     s_td += diff * diff;
     s_d += qd;
-    s_l += d.lse[(C + c) * B + b];
+    if (cons_on) s_l += d.lse[(C + c) * B + b];
     d.dq[c * d.R + 6 * NB + b] = 2.f * diff / (float)B - gcons;
   }
   // critic-set IS rows keep the unscaled softmax weights of stage A; the
@@ -274,8 +286,8 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   const float dsum = block_sum(s_d, scratch);
   if (tid == 0) {
     const float loss = lsum / (float)(C * B) - dsum / (float)(C * B);
-    const float cons = ca * (d.conservative_weight * loss - d.alpha_threshold);
-    d.metrics[4] = td + cons;
+    const float cons = cons_on ? ca * (d.conservative_weight * loss - d.alpha_threshold) : 0.f;
+    d.metrics[4] = cons_on ? td + cons : td;
     d.metrics[6] = td;
     d.metrics[7] = cons;
   }
@@ -339,7 +351,9 @@ using namespace d3a;
 extern "C" int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream) {
   D3A_CHECK_ARG(d, "d3a_cql_sample: null desc");
   D3A_CHECK_ARG(d->A >= 1 && d->A <= 16, "d3a_cql_sample: action size must be in [1,16]");
-  D3A_CHECK_ARG(d->B >= 1 && d->N >= 1 && d->D >= 1, "d3a_cql_sample: bad sizes");
+  D3A_CHECK_ARG(d->B >= 1 && d->N >= 0 && d->D >= 1, "d3a_cql_sample: bad sizes");
+  D3A_CHECK_ARG(!d->soft_target || (d->eps_targ && d->logp_targ),
+                "d3a_cql_sample: soft_target needs eps_targ and logp_targ");
   D3A_CHECK_ARG(d->ldx >= d->D + d->A, "d3a_cql_sample: ldx < D + A");
   const int64_t total = 6LL * d->N * d->B + 4LL * d->B;
   hipLaunchKernelGGL(cql_sample_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
@@ -355,8 +369,12 @@ extern "C" int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream) {
   D3A_CHECK_ARG(d->dp_phase >= 0 && d->dp_phase <= 2, "d3a_cql_loss: bad dp_phase");
   D3A_CHECK_ARG(d->dp_phase == 0 || d->scalar_grads != nullptr,
                 "d3a_cql_loss: dp_phase needs scalar_grads");
+  D3A_CHECK_ARG(!d->soft_target || d->logp_targ, "d3a_cql_loss: soft_target needs logp_targ");
+  D3A_CHECK_ARG(d->conservative || !d->update_alpha,
+                "d3a_cql_loss: update_alpha needs the conservative term");
+  D3A_CHECK_ARG(!d->conservative || d->N >= 1, "d3a_cql_loss: the conservative term needs N >= 1");
   // phase 2 reuses the logsumexp / softmax weights phase 1 wrote
-  if ((d->update_alpha || d->update_critic) && d->dp_phase != 2) {
+  if (d->conservative && (d->update_alpha || d->update_critic) && d->dp_phase != 2) {
     const int64_t waves = 2LL * d->C * d->B;
     hipLaunchKernelGGL(cql_lse_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, *d);

@@ -274,6 +274,14 @@ typedef struct d3a_cql_sample_desc {
   int32_t ldx;            /* row stride of x_q / x_targ / x_actor (>= D + A;
                              padded to a multiple of 4 for 16-byte rows)   */
   float min_logstd, max_logstd;
+  /* soft_target != 0: the target action is a policy sample at next_obs
+   * (SACImpl.compute_target, sac_impl.py:148-162; CQL soft_q_backup,
+   * cql_impl.py:225-230) from eps_targ [B][A], its log-prob -> logp_targ [B];
+   * otherwise tanh(mu(next_obs)) (cql_impl.py:232-243).  N = 0 (SAC: no
+   * conservative samples) leaves x_q = the B data rows. */
+  const float* eps_targ;
+  float* logp_targ;
+  int32_t soft_target;
 } d3a_cql_sample_desc;
 int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream);
 
@@ -312,6 +320,11 @@ typedef struct d3a_cql_loss_desc {
   int32_t dp_phase;
   float* scalar_grads;
   float grad_scale;
+  /* soft_target: y uses min_c Q_targ - exp(log_temp_new) * logp_targ[b]
+   * (sac_impl.py:148-162); conservative = 0: plain TD loss (SACImpl, no
+   * logsumexp stage, no alpha) */
+  const float* logp_targ;
+  int32_t soft_target, conservative;
 } d3a_cql_loss_desc;
 int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream);
 

@@ -6,6 +6,8 @@ same order:
   d3rlpy/algos/torch/sac_impl.py:92-162   (SACImpl: build, actor loss, update_temp)
   d3rlpy/algos/torch/ddpg_impl.py:95-209  (update_critic / update_actor / targets)
   d3rlpy/algos/cql.py:234-258             (CQL._update schedule)
+  d3rlpy/algos/torch/sac_impl.py:148-162  (SACImpl.compute_target: soft_q_backup, SACOracle)
+  d3rlpy/algos/sac.py:195-214             (SAC._update schedule, SACOracle)
 with every random draw passed in explicitly (``CQLNoise``).
 """
 from __future__ import annotations
@@ -55,6 +57,8 @@ class CQLNoise:
     alpha_rand:      (B*N, A)   update_alpha       uniform_(-1, 1)
     critic_pi_t / critic_pi_tp1 / critic_rand:     same, inside update_critic
     eps_actor:       (B, A)     update_actor       policy.sample_with_log_prob
+    eps_targ:        (B, A)     update_critic      soft target sample_with_log_prob(next_obs)
+                                                   (soft_q_backup / SAC only; else None)
     """
 
     eps_temp: torch.Tensor
@@ -65,13 +69,23 @@ class CQLNoise:
     critic_pi_tp1: torch.Tensor
     critic_rand: torch.Tensor
     eps_actor: torch.Tensor
+    eps_targ: Optional[torch.Tensor] = None
+
+    def tensors(self) -> Dict[str, torch.Tensor]:
+        """The draws that exist (eps_targ only for a soft target)."""
+        return {k: getattr(self, k) for k in self.__dataclass_fields__
+                if getattr(self, k) is not None}
 
     @staticmethod
-    def draw(gen: torch.Generator, B: int, A: int, N: int) -> "CQLNoise":
+    def draw(gen: torch.Generator, B: int, A: int, N: int,
+             soft_target: bool = False) -> "CQLNoise":
         n = lambda *s: torch.randn(*s, generator=gen)  # noqa: E731
         u = lambda *s: torch.rand(*s, generator=gen) * 2.0 - 1.0  # noqa: E731
-        return CQLNoise(n(B, A), n(N, B, A), n(N, B, A), u(B * N, A),
-                        n(N, B, A), n(N, B, A), u(B * N, A), n(B, A))
+        nz = CQLNoise(n(B, A), n(N, B, A), n(N, B, A), u(B * N, A),
+                      n(N, B, A), n(N, B, A), u(B * N, A), n(B, A))
+        if soft_target:  # drawn last: the other draws keep their stream
+            nz.eps_targ = n(B, A)
+        return nz
 
 
 class CQLOracle:
@@ -93,6 +107,7 @@ class CQLOracle:
         alpha_threshold: float = 10.0,
         conservative_weight: float = 5.0,
         n_action_samples: int = 10,
+        soft_q_backup: bool = False,
         hidden_units: Sequence[int] = (256, 256),
         betas=(0.9, 0.999),
         eps: float = 1e-8,
@@ -107,6 +122,7 @@ class CQLOracle:
         self._alpha_threshold = alpha_threshold
         self._conservative_weight = conservative_weight
         self._n_action_samples = n_action_samples
+        self._soft_q_backup = soft_q_backup
         self._temp_learning_rate = temp_learning_rate
         self._alpha_learning_rate = alpha_learning_rate
         # build order: CQLImpl.build -> _build_alpha, SACImpl.build -> _build_temperature,
@@ -186,23 +202,38 @@ class CQLOracle:
         cur_alpha = self._log_alpha().exp().cpu().detach().numpy()[0][0]
         return loss.cpu().detach().numpy(), cur_alpha
 
-    def compute_target(self, batch: Batch):
-        """cql_impl.py:225-243 (soft_q_backup=False)."""
+    def compute_target(self, batch: Batch, noise: Optional[CQLNoise] = None):
+        """cql_impl.py:225-243."""
+        if self._soft_q_backup:
+            return self._compute_soft_target(batch, noise.eps_targ)
         with torch.no_grad():
             action = self._policy.best_action(batch.next_observations)
             return self._targ_q_func.compute_target(batch.next_observations, action,
                                                     reduction="min")
 
-    def update_critic(self, batch: Batch, noise: CQLNoise):
-        """ddpg_impl.py:138-165 + cql_impl.py:110-117."""
-        self._critic_optim.zero_grad()
-        q_tpn = self.compute_target(batch)
+    def _compute_soft_target(self, batch: Batch, eps: torch.Tensor):
+        """SACImpl.compute_target (sac_impl.py:148-162), sample noise supplied."""
+        with torch.no_grad():
+            action, log_prob = self._policy.sample_with_log_prob(batch.next_observations, eps)
+            entropy = self._log_temp().exp() * log_prob
+            target = self._targ_q_func.compute_target(batch.next_observations, action,
+                                                      reduction="min")
+            return target - entropy
+
+    def compute_critic_loss(self, batch: Batch, q_tpn: torch.Tensor, noise: CQLNoise):
+        """cql_impl.py:110-117 (DDPGBaseImpl's TD error + conservative loss)."""
         loss = self._q_func.compute_error(
             observations=batch.observations, actions=batch.actions, rewards=batch.rewards,
             target=q_tpn, terminals=batch.terminals, gamma=self._gamma ** batch.n_steps)
-        loss = loss + self._compute_conservative_loss(
+        return loss + self._compute_conservative_loss(
             batch.observations, batch.actions, batch.next_observations,
             noise.critic_pi_t, noise.critic_pi_tp1, noise.critic_rand)
+
+    def update_critic(self, batch: Batch, noise: CQLNoise):
+        """ddpg_impl.py:138-165."""
+        self._critic_optim.zero_grad()
+        q_tpn = self.compute_target(batch, noise)
+        loss = self.compute_critic_loss(batch, q_tpn, noise)
         loss.backward()
         self._critic_optim.step()
         return loss.cpu().detach().numpy()
@@ -251,3 +282,36 @@ class CQLOracle:
         for name, p in self._policy.named_parameters():
             out["pi." + name] = p.grad.detach().clone() if p.grad is not None else None
         return out
+
+
+class SACOracle(CQLOracle):
+    """SACImpl (sac_impl.py:27-162) with the reference defaults
+    (algos/sac.py:118-140): no conservative term, no alpha, soft target.
+    Construction draws the same weights as CQLOracle with the same seed
+    (the log_alpha parameter of CQLImpl consumes no random numbers)."""
+
+    def __init__(self, observation_size: int, action_size: int,
+                 actor_learning_rate: float = 3e-4, critic_learning_rate: float = 3e-4,
+                 temp_learning_rate: float = 3e-4, **kw):
+        super().__init__(observation_size, action_size, actor_learning_rate=actor_learning_rate,
+                         critic_learning_rate=critic_learning_rate,
+                         temp_learning_rate=temp_learning_rate, alpha_learning_rate=0.0,
+                         n_action_samples=0, soft_q_backup=True, **kw)
+
+    def compute_critic_loss(self, batch: Batch, q_tpn: torch.Tensor, noise: CQLNoise):
+        """DDPGBaseImpl.compute_critic_loss (ddpg_impl.py:154-167)."""
+        return self._q_func.compute_error(
+            observations=batch.observations, actions=batch.actions, rewards=batch.rewards,
+            target=q_tpn, terminals=batch.terminals, gamma=self._gamma ** batch.n_steps)
+
+    def update(self, batch: Batch, noise: CQLNoise) -> Dict[str, float]:
+        """algos/sac.py:195-214 (SAC._update)."""
+        metrics = {}
+        if self._temp_learning_rate > 0:
+            temp_loss, temp = self.update_temp(batch, noise.eps_temp)
+            metrics.update({"temp_loss": float(temp_loss), "temp": float(temp)})
+        metrics["critic_loss"] = float(self.update_critic(batch, noise))
+        metrics["actor_loss"] = float(self.update_actor(batch, noise.eps_actor))
+        self.update_critic_target()
+        self.update_actor_target()
+        return metrics

@@ -10,7 +10,8 @@ def make_impl(D, A, hidden, N, C=2, **kw):
     from d3rlpy_amd.factories import AdamFactory, MeanQFunctionFactory, VectorEncoderFactory
     args = dict(actor_learning_rate=1e-4, critic_learning_rate=3e-4, temp_learning_rate=1e-4,
                 alpha_learning_rate=1e-4, gamma=0.99, tau=0.005, initial_temperature=1.0,
-                initial_alpha=1.0, alpha_threshold=10.0, conservative_weight=5.0)
+                initial_alpha=1.0, alpha_threshold=10.0, conservative_weight=5.0,
+                soft_q_backup=False)
     args.update(kw)
     impl = CQLImpl(
         observation_shape=(D,), action_size=A,
@@ -19,8 +20,26 @@ def make_impl(D, A, hidden, N, C=2, **kw):
         actor_encoder_factory=VectorEncoderFactory(hidden),
         critic_encoder_factory=VectorEncoderFactory(hidden),
         q_func_factory=MeanQFunctionFactory(), n_critics=C, n_action_samples=N,
-        soft_q_backup=False, use_gpu=0, scaler=None, action_scaler=None, reward_scaler=None,
+        use_gpu=0, scaler=None, action_scaler=None, reward_scaler=None,
         **args)
+    impl.build()
+    return impl
+
+
+def make_sac_impl(D, A, hidden, C=2, **kw):
+    from d3rlpy_amd.algos.sac import SACImpl
+    from d3rlpy_amd.factories import AdamFactory, MeanQFunctionFactory, VectorEncoderFactory
+    args = dict(actor_learning_rate=3e-4, critic_learning_rate=3e-4, temp_learning_rate=3e-4,
+                gamma=0.99, tau=0.005, initial_temperature=1.0)
+    args.update(kw)
+    impl = SACImpl(
+        observation_shape=(D,), action_size=A,
+        actor_optim_factory=AdamFactory(), critic_optim_factory=AdamFactory(),
+        temp_optim_factory=AdamFactory(),
+        actor_encoder_factory=VectorEncoderFactory(hidden),
+        critic_encoder_factory=VectorEncoderFactory(hidden),
+        q_func_factory=MeanQFunctionFactory(), n_critics=C, use_gpu=0, scaler=None,
+        action_scaler=None, reward_scaler=None, **args)
     impl.build()
     return impl
 
@@ -101,7 +120,7 @@ class HostBatch:
 
 
 def noise_dict(nz: CQLNoise):
-    return {k: getattr(nz, k) for k in nz.__dataclass_fields__}
+    return nz.tensors()
 
 
 def max_rel(a, b):

@@ -46,7 +46,7 @@ def cql_small():
     data = {"cfg": np.array([D, A, H[0], len(H), N, B], dtype=np.int64),
             "obs": obs, "act": act, "rew": rew, "next_obs": nobs, "term": term, "n_steps": nst}
     data.update(flat_state(orc, "init/"))
-    for k in nz.__dataclass_fields__:
+    for k in nz.tensors():
         data[f"noise/{k}"] = getattr(nz, k).numpy()
     batch = Batch.from_numpy(obs, act, rew, nobs, term, nst)
     tl, t = orc.update_temp(batch, nz.eps_temp)

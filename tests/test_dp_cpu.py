@@ -55,7 +55,7 @@ def test_gloo_two_ranks_equal_global_batch(tmp_path):
         steps.append((arrs, nz))
         np.savez(tmp_path / f"step{s}.npz", obs=arrs[0], act=arrs[1], rew=arrs[2],
                  next_obs=arrs[3], term=arrs[4], n_steps=arrs[5],
-                 **{f"noise/{k}": getattr(nz, k).numpy() for k in nz.__dataclass_fields__})
+                 **{f"noise/{k}": v.numpy() for k, v in nz.tensors().items()})
     port = _free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", CUDA_VISIBLE_DEVICES="")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_cpu_worker.py"), str(r),

@@ -42,7 +42,8 @@ def test_oracle_reproduces_cql_fixture():
     g = _load("cql_small.npz")
     orc, (D, A, H, L, N, B) = _oracle_from_fixture(g)
     batch = Batch.from_numpy(g["obs"], g["act"], g["rew"], g["next_obs"], g["term"], g["n_steps"])
-    nz = CQLNoise(**{k: torch.from_numpy(g[f"noise/{k}"]) for k in CQLNoise.__dataclass_fields__})
+    nz = CQLNoise(**{k: torch.from_numpy(g[f"noise/{k}"]) for k in CQLNoise.__dataclass_fields__
+                     if f"noise/{k}" in g})
     m = orc.update(batch, nz)
     got = np.array([m["temp_loss"], m["temp"], m["alpha_loss"], m["alpha"], m["critic_loss"],
                     m["actor_loss"]], dtype=np.float32)
@@ -127,7 +128,7 @@ def test_hip_cql_update_vs_fixture():
     orc, (D, A, H, L, N, B) = _oracle_from_fixture(g)
     impl = make_impl(D, A, [H] * L, N)
     impl.set_state_dict(oracle_state(orc))
-    noise = {k: g[f"noise/{k}"] for k in CQLNoise.__dataclass_fields__}
+    noise = {k: g[f"noise/{k}"] for k in CQLNoise.__dataclass_fields__ if f"noise/{k}" in g}
     m = impl.update_step(HostBatch(g["obs"], g["act"], g["rew"], g["next_obs"], g["term"],
                                    g["n_steps"]), noise=noise)
     got = np.array([m["temp_loss"], m["temp"], m["alpha_loss"], m["alpha"], m["critic_loss"],
