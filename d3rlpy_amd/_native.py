@@ -173,6 +173,9 @@ class MlpFwdDesc(C.Structure):
         ("out", vp), ("sout", C.c_int64), ("ldout", C.c_int64),
         ("r0", C.c_int64), ("rows", C.c_int64), ("h_from", C.c_int64),
         ("C", C.c_int32), ("block_rows", C.c_int32),
+        ("aux_x", vp), ("aux_ldx", C.c_int64), ("aux_sxb", C.c_int64),
+        ("aux_wdelta", C.c_int64), ("aux_out", vp), ("aux_sout", C.c_int64),
+        ("aux_rows", C.c_int64),
     ]
 
 

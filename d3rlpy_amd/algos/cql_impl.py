@@ -607,12 +607,12 @@ class _Workspace:
         if alpha or critic:
             # 3. critic forward (alpha set only when update_alpha runs)
             r0 = 0 if alpha else 3 * NB
-            # the critic backward reads the activations of rows [3NB, R) only
+            # the critic backward reads the activations of rows [3NB, R) only;
+            # the target ensemble over the B next-state rows rides in the same
+            # launch (aux pass) when the critic is updated
+            targ = (impl.targ, self.x_targ.data_ptr(), DA, self.tacts) if critic else None
             mlp.forward(impl.critic, impl.store, self.x_q.data_ptr(), True, DA, self.qacts, r0, R,
-                        h_from=3 * NB)
-        if critic:
-            mlp.forward(impl.critic, impl.targ, self.x_targ.data_ptr(), True, DA, self.tacts,
-                        keep_h=False)
+                        h_from=3 * NB, aux=targ)
         dp = impl._dp
         if temp or alpha or critic:
             l = self.loss_desc

@@ -106,8 +106,15 @@ void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int li = lane & 31, lg = lane >> 5;
   const int c = blockIdx.z;
-  const int64_t m0 = d.r0 + (int64_t)blockIdx.x * BM;
-  const int64_t rend = d.r0 + d.rows;
+  // workgroups past the main pass's row blocks run the aux pass (the same
+  // network at W + aux_wdelta over aux_rows rows of aux_x, no activations kept)
+  const int64_t nb_main = (d.rows + BM - 1) / BM;
+  const bool aux = (int64_t)blockIdx.x >= nb_main;
+  const int64_t m0 = aux ? ((int64_t)blockIdx.x - nb_main) * BM : d.r0 + (int64_t)blockIdx.x * BM;
+  const int64_t rend = aux ? d.aux_rows : d.r0 + d.rows;
+  const int64_t h_from = aux ? rend : d.h_from;
+  const int64_t wdel = aux ? d.aux_wdelta : 0;
+  float* const outp = aux ? d.aux_out + c * d.aux_sout : d.out + c * d.sout;
   const int H = d.H;
   const int K0 = d.n_in;
   const int K0p = (K0 + 31) / 32 * 32;  // zero-padded to whole 32-deep k slices
@@ -115,11 +122,12 @@ void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
   float* bufB = INPLACE ? lds : lds + BM * LDK;
 
   // stage the input rows (zero-padded to a multiple of 8 columns)
-  const float* xb = d.x + c * d.sxb;
+  const float* xb = aux ? d.aux_x + c * d.aux_sxb : d.x + c * d.sxb;
+  const int64_t ldx = aux ? d.aux_ldx : d.ldx;
   for (int i = t; i < BM * K0p; i += NT) {
     const int m = i / K0p, k = i - m * K0p;
     const int64_t r = m0 + m;
-    bufA[m * LDK + k] = (r < rend && k < K0) ? xb[r * d.ldx + k] : 0.f;
+    bufA[m * LDK + k] = (r < rend && k < K0) ? xb[r * ldx + k] : 0.f;
   }
   __syncthreads();
 
@@ -140,7 +148,7 @@ void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
         const uint64_t bit = uint64_t(1) << (i * 16 + r);
         if (row < rend) {
           v_out |= bit;
-          if (row >= d.h_from) v_h |= bit;
+          if (row >= h_from) v_h |= bit;
         }
       }
   }
@@ -149,9 +157,9 @@ void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
     const int N = head ? J : H;
     const int Kin = l == 0 ? K0p : H;
     const int Kreal = l == 0 ? K0 : H;
-    const float* W = d.W[l] + c * d.sW[l];
-    const float* bias = d.b[l] + c * d.sb[l];
-    float* gout = head ? d.out + c * d.sout : (d.h[l] ? d.h[l] + c * d.sh : nullptr);
+    const float* W = d.W[l] + wdel + c * d.sW[l];
+    const float* bias = d.b[l] + wdel + c * d.sb[l];
+    float* gout = head ? outp : (!aux && d.h[l] ? d.h[l] + c * d.sh : nullptr);
     const int ldg = head ? (int)d.ldout : H;
     const int rg = w % RG;
     const float* Ag = bufA + rg * RTW * 32 * LDK;
@@ -228,9 +236,9 @@ void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
   }
 
   // narrow head: out[r][j] = h[r] . Wh[j] + bh[j]
-  const float* Wh = d.W[d.n_hidden] + c * d.sW[d.n_hidden];
-  const float* bh = d.b[d.n_hidden] + c * d.sb[d.n_hidden];
-  float* outb = d.out + c * d.sout;
+  const float* Wh = d.W[d.n_hidden] + wdel + c * d.sW[d.n_hidden];
+  const float* bh = d.b[d.n_hidden] + wdel + c * d.sb[d.n_hidden];
+  float* outb = outp;
   if (J == 1) {
     // TPR lanes per row, interleaved columns, then a shuffle reduction
     constexpr int TPR = NT / BM;
@@ -291,7 +299,14 @@ extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
   // in-kernel row offsets are 32-bit
   D3A_CHECK_ARG((d.r0 + d.rows) * (int64_t)(d.ldout > d.H ? d.ldout : d.H) < (int64_t(1) << 31),
                 "d3a_mlp_fwd: rows x row stride exceeds 2^31");
-  if (d.rows == 0) return 0;
+  D3A_CHECK_ARG(d.aux_rows >= 0, "d3a_mlp_fwd: aux_rows must be >= 0");
+  if (d.aux_rows > 0) {
+    D3A_CHECK_ARG(d.aux_x && d.aux_out, "d3a_mlp_fwd: aux pass needs aux_x and aux_out");
+    D3A_CHECK_ARG(d.aux_wdelta % 4 == 0, "d3a_mlp_fwd: aux_wdelta must keep 16-byte alignment");
+    D3A_CHECK_ARG(d.aux_rows * (int64_t)(d.ldout > d.H ? d.ldout : d.H) < (int64_t(1) << 31),
+                  "d3a_mlp_fwd: aux rows x row stride exceeds 2^31");
+  }
+  if (d.rows == 0 && d.aux_rows == 0) return 0;
   // Rows per workgroup, from bench A/B runs (profiles/r01_fused_ab.log):
   // 128 (in-place activations, four row tiles per weight load) for large
   // passes with narrow heads -- 55.8 us against 69.5 (32) / 77.6 (64) on the
@@ -303,7 +318,7 @@ extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
                      : (d.n_out <= 64 && d.rows * d.C >= 16384 ? 128 : 32);
   D3A_CHECK_ARG(bm == 32 || bm == 64 || bm == 128,
                 "d3a_mlp_fwd: block_rows must be 0, 32, 64 or 128");
-  dim3 grid((unsigned)((d.rows + bm - 1) / bm), 1, (unsigned)d.C);
+  dim3 grid((unsigned)((d.rows + bm - 1) / bm + (d.aux_rows + bm - 1) / bm), 1, (unsigned)d.C);
   hipStream_t st = (hipStream_t)stream;
   if (bm == 128)
     hipLaunchKernelGGL((mlp_fwd_kernel<128, 8, 4>), grid, dim3(512), 0, st, d);

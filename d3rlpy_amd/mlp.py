@@ -80,12 +80,19 @@ def fused_ok(net: EnsembleMLP, rows: Optional[int] = None, backward: bool = Fals
 def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: int, acts: Acts,
             r0: int = 0, r1: Optional[int] = None, sxb: Optional[int] = None,
             members: Optional[int] = None, keep_h: bool = True,
-            h_from: Optional[int] = None) -> None:
+            h_from: Optional[int] = None, aux: Optional[tuple] = None) -> None:
     """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
     (through its first ``members`` members only, when given).  ``keep_h``:
     store the hidden activations in ``acts.h`` (needed by a backward pass),
     for rows >= ``h_from`` only when given (the fused kernel skips the rest;
-    the per-layer path stores every row)."""
+    the per-layer path stores every row).
+
+    ``aux = (store2, x2, ldx2, acts2)``: a second, independent forward of the
+    same network with the parameters of ``store2`` (same layout, e.g. the
+    targets) over all acts2.R rows of x2 (shared by the members), no
+    activations kept.  On the fused path it rides in the same launch (its
+    workgroups use the CUs the main pass leaves idle); otherwise it is a
+    separate forward."""
     R = acts.R
     r1 = R if r1 is None else r1
     n = r1 - r0
@@ -110,7 +117,16 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         d.sout, d.ldout = R * sizes[-1], sizes[-1]
         d.r0, d.rows, d.C = r0, n, C
         d.h_from = r0 if h_from is None else max(r0, h_from)
+        if aux is not None and members is None:
+            ast, ax, aldx, aacts = aux
+            assert ast.size == store.size and list(ast.specs) == list(store.specs)
+            d.aux_x, d.aux_ldx, d.aux_sxb = ax, aldx, 0
+            d.aux_wdelta = (ast.data.data_ptr() - store.data.data_ptr()) // 4
+            d.aux_out, d.aux_sout, d.aux_rows = aacts.out.data_ptr(), aacts.R * sizes[-1], aacts.R
+            aux = None
         ops.call_desc("d3a_mlp_fwd", d)
+        if aux is not None:
+            forward(net, aux[0], aux[1], True, aux[2], aux[3], keep_h=False)
         return
     L = net.n_layers
     inp, ld_in = x + 4 * r0 * ldx, ldx
@@ -131,6 +147,8 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         ops.linear_fwd(inp, False, ld_in, net.W(L - 1, store), net.b(L - 1, store),
                        acts.out.data_ptr() + 4 * r0 * out_dim, C, n, Hl, out_dim, relu=False,
                        ldy=out_dim, sxb=R * Hl if L > 1 else sxb_, syb=R * out_dim)
+    if aux is not None:
+        forward(net, aux[0], aux[1], True, aux[2], aux[3], keep_h=False)
 
 
 class BackwardSpace:

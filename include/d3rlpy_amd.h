@@ -144,6 +144,16 @@ typedef struct d3a_mlp_fwd_desc {
   float* out; int64_t sout, ldout;
   int64_t r0, rows, h_from;
   int32_t C, block_rows;
+  /* Optional second, independent pass in the same launch (aux_rows > 0):
+   * the same network shape with its parameters at W[l] + aux_wdelta and
+   * b[l] + aux_wdelta (a second parameter buffer of the same layout, e.g.
+   * the target networks of DDPGBaseImpl._targ_q_func), input rows
+   * [0, aux_rows) of aux_x (row stride aux_ldx, member stride aux_sxb),
+   * output aux_out (member stride aux_sout, row stride ldout), no
+   * activations kept.  Its workgroups follow the main pass's in the grid and
+   * run on the CUs the main pass leaves idle. */
+  const float* aux_x; int64_t aux_ldx, aux_sxb, aux_wdelta;
+  float* aux_out; int64_t aux_sout, aux_rows;
 } d3a_mlp_fwd_desc;
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);
 

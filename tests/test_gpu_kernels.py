@@ -310,6 +310,47 @@ def test_fused_mlp_forward(dev, C, R, r0, n, K0, H, L, J, x_shared, bm, monkeypa
         assert _rel_err(out.reshape(n, J), a) < 2e-6, c
 
 
+@pytest.mark.parametrize("bm", [0, 32, 128])
+@pytest.mark.parametrize("R,n_aux", [(15616, 256), (4096, 100), (300, 1000)])
+def test_fused_mlp_forward_aux_pass(dev, R, n_aux, bm, monkeypatch):
+    """d3a_mlp_fwd with an aux pass (a second parameter buffer of the same
+    layout over other rows, e.g. the target critics over next-state rows) in
+    the same launch: both passes against fp64 torch, the main pass's kept
+    activations unchanged by the aux workgroups (2e-6 relative)."""
+    from d3rlpy_amd import mlp
+    from d3rlpy_amd.nets import EnsembleMLP, ParamStore
+    monkeypatch.setattr(mlp, "FUSED_MIN_ROWS", 0)
+    monkeypatch.setattr(mlp, "_FUSED_BM", bm)
+    g = torch.Generator().manual_seed(R + n_aux)
+    C, K0, H, L = 2, 14, 256, 2
+    st = ParamStore()
+    net = EnsembleMLP(st, "m", C, [K0] + [H] * L + [1])
+    st.allocate(dev)
+    targ = st.like()
+    with torch.no_grad():
+        st.data.copy_(torch.randn(st.data.numel(), generator=g) * 0.1)
+        targ.data.copy_(torch.randn(st.data.numel(), generator=g) * 0.1)
+    ldx = 16
+    x = torch.randn(1, R, ldx, generator=g).to(dev)
+    x2 = torch.randn(1, n_aux, ldx, generator=g).to(dev)
+    acts = mlp.Acts.alloc(net, R, dev)
+    acts2 = mlp.Acts.alloc(net, n_aux, dev)
+    acts2.out.fill_(float("nan"))
+    mlp.forward(net, st, x.data_ptr(), True, ldx, acts, aux=(targ, x2.data_ptr(), ldx, acts2))
+    torch.cuda.synchronize()
+    for store, xx, a_, rows in ((st, x, acts, R), (targ, x2, acts2, n_aux)):
+        for c in range(C):
+            a = xx[0, :, :K0].double()
+            for l in range(L + 1):
+                W, b = net.export_linear(l, c, store)
+                a = a @ W.double().T + b.double()
+                if l < L:
+                    a = a.clamp_min(0)
+                    if a_ is acts:
+                        assert _rel_err(acts.h[l][c], a) < 2e-6, (c, l)
+            assert _rel_err(a_.out[c].reshape(rows, 1), a) < 2e-6, (rows, c)
+
+
 @pytest.mark.parametrize("C,R,r0,n,K0,H,L,J,mode", [
     (2, 15616, 7680, 7936, 14, 256, 2, 1, "gscale"),  # K2 critic backward (IS rows scaled)
     (2, 256, 0, 256, 14, 256, 2, 1, "qmin"),          # actor: argmin critic, dQ/dx only
