@@ -88,21 +88,29 @@ __device__ __forceinline__ void store4(float* lds, int xl, int kl, float4 v) {
   }
 }
 
+template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK>
+struct TileLds {
+  static constexpr int BM = 32 * WM_T * WAVES_M, BN = 32 * WN_T * WAVES_N;
+  float As[2][BK * (BM + 4)];
+  float Bs[2][BK * (BN + 4)];
+};
+
+// One BM x BN output tile (block coordinates bx, by, bz) of the GEMM p.
 template <int AMODE, int BMODE, int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32_kernel(Params p) {
+__device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64_t by, int64_t bz,
+                                              TileLds<WM_T, WN_T, WAVES_M, WAVES_N, BK>& L) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int BM = 32 * WM_T * WAVES_M, BN = 32 * WN_T * WAVES_N;
   constexpr int LDA = BM + 4, LDB = BN + 4;
   constexpr int AV = BM * BK / 4 / NT, BV = BN * BK / 4 / NT;  // float4 per thread
   static_assert(AV >= 1 && BV >= 1, "tile too small for the thread count");
-  __shared__ __attribute__((aligned(16))) float As[2][BK * LDA];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB];
+  auto& As = L.As;
+  auto& Bs = L.Bs;
 
   const int t = threadIdx.x;
   const int lane = t & 63, wid = t >> 6;
-  const int64_t n0 = (int64_t)blockIdx.x * BN;
-  const int64_t m0 = (int64_t)blockIdx.y * BM;
-  const int64_t bz = blockIdx.z;
+  const int64_t n0 = bx * BN;
+  const int64_t m0 = by * BM;
   const int64_t b = bz / p.splits, s = bz % p.splits;
   const int64_t kbeg = s * p.kchunk;
   const int64_t kend = (kbeg + p.kchunk < p.K) ? kbeg + p.kchunk : p.K;
@@ -125,7 +133,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32_kernel(Params
 
   const int wm = (wid / WAVES_N) * (32 * WM_T), wn = (wid % WAVES_N) * (32 * WN_T);
   const int li = lane & 31, lk = lane >> 5;
-  const bool do_rowsum = p.rowsum != nullptr && blockIdx.x == 0;
+  const bool do_rowsum = p.rowsum != nullptr && bx == 0;
   double rs = 0.0;
 
   float4 ra[AV], rb[BV];
@@ -205,6 +213,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32_kernel(Params
       }
     }
   }
+}
+
+template <int AMODE, int BMODE, int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32_kernel(Params p) {
+  __shared__ __attribute__((aligned(16))) TileLds<WM_T, WN_T, WAVES_M, WAVES_N, BK> lds;
+  gemm_f32_tile<AMODE, BMODE, WM_T, WN_T, WAVES_M, WAVES_N, BK>(p, blockIdx.x, blockIdx.y,
+                                                                blockIdx.z, lds);
 }
 
 // ---- register-direct split-K kernel for small problems ---------------------
@@ -448,16 +463,19 @@ int env_variant() {
 }  // namespace
 }  // namespace d3a
 
-extern "C" int d3a_gemm_f32(const d3a_gemm_desc* d, void* stream) {
-  using namespace d3a;
+namespace d3a {
+namespace {
+
+// Validate a descriptor and fill the kernel parameters; *skip = the problem is empty.
+int make_params(const d3a_gemm_desc* d, Params& p, int& variant, int& am, int& bm, bool& skip) {
   D3A_CHECK_ARG(d != nullptr, "d3a_gemm_f32: null descriptor");
   D3A_CHECK_ARG(d->A && d->B && d->C, "d3a_gemm_f32: null operand");
   D3A_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0 && d->batch >= 0,
                 "d3a_gemm_f32: negative size");
   D3A_CHECK_ARG(d->splits >= 1, "d3a_gemm_f32: splits must be >= 1");
   D3A_CHECK_ARG(d->variant >= -1 && d->variant < kNumVariants, "d3a_gemm_f32: bad variant");
-  if (d->M == 0 || d->N == 0 || d->batch == 0) return 0;
-  Params p;
+  skip = d->M == 0 || d->N == 0 || d->batch == 0;
+  if (skip) return 0;
   p.A = d->A; p.B = d->B; p.C = d->C; p.bias = d->bias; p.mask = d->mask;
   p.rowsum = d->rowsum;
   p.M = d->M; p.N = d->N; p.K = d->K; p.batch = d->batch;
@@ -467,7 +485,7 @@ extern "C" int d3a_gemm_f32(const d3a_gemm_desc* d, void* stream) {
   p.sbias_b = d->sbias_b; p.sMb = d->sMb; p.sMm = d->sMm; p.sMn = d->sMn;
   p.splits = d->splits; p.sCs = d->sCs; p.sRb = d->sRb; p.sRs = d->sRs;
   p.alpha = d->alpha; p.relu = d->relu; p.accumulate = d->accumulate;
-  int variant = d->variant >= 0 ? d->variant : env_variant();
+  variant = d->variant >= 0 ? d->variant : env_variant();
   if (variant < 0) variant = choose_variant(p);
   const int bk = kVariants[variant].bk;
   // split K in BK multiples (every split starts on a K-tile boundary)
@@ -476,10 +494,12 @@ extern "C" int d3a_gemm_f32(const d3a_gemm_desc* d, void* stream) {
   p.kchunk = kc > 0 ? kc : bk;
   D3A_CHECK_ARG(d->batch * d->splits < 65536, "d3a_gemm_f32: batch*splits too large");
   D3A_CHECK_ARG((d->M + 31) / 32 < 65536, "d3a_gemm_f32: M too large");
+  am = (d->sAk == 1) ? MODE_KCONTIG : (d->sAm == 1 ? MODE_XCONTIG : MODE_GENERIC);
+  bm = (d->sBk == 1) ? MODE_KCONTIG : (d->sBn == 1 ? MODE_XCONTIG : MODE_GENERIC);
+  return 0;
+}
 
-  const int am = (d->sAk == 1) ? MODE_KCONTIG : (d->sAm == 1 ? MODE_XCONTIG : MODE_GENERIC);
-  const int bm = (d->sBk == 1) ? MODE_KCONTIG : (d->sBn == 1 ? MODE_XCONTIG : MODE_GENERIC);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+void launch_params(const Params& p, int variant, int am, int bm, hipStream_t st) {
   if (am == MODE_GENERIC || bm == MODE_GENERIC) {
     // strided fallback: smallest tile, scalar loads
     if (am == MODE_GENERIC && bm == MODE_GENERIC) launch_v<MODE_GENERIC, MODE_GENERIC, 0>(p, st);
@@ -499,6 +519,19 @@ extern "C" int d3a_gemm_f32(const d3a_gemm_desc* d, void* stream) {
   } else {
     launch_modes<MODE_XCONTIG, MODE_XCONTIG>(p, variant, st);
   }
+}
+
+}  // namespace
+}  // namespace d3a
+
+extern "C" int d3a_gemm_f32(const d3a_gemm_desc* d, void* stream) {
+  using namespace d3a;
+  Params p;
+  int variant, am, bm;
+  bool skip;
+  if (make_params(d, p, variant, am, bm, skip) != 0) return -1;
+  if (skip) return 0;
+  launch_params(p, variant, am, bm, reinterpret_cast<hipStream_t>(stream));
   D3A_LAUNCH_CHECK("d3a_gemm_f32");
   return 0;
 }
