@@ -24,7 +24,9 @@ class AlgoBase(LearnableBase):
         return self._impl.sample_action(x)
 
     def save_policy(self, fname: str) -> None:
-        raise NotImplementedError("save_policy (TorchScript/ONNX export) is not implemented yet")
+        """algos/base.py:77-103: greedy policy as TorchScript (.pt) or ONNX (.onnx)."""
+        assert self._impl is not None, IMPL_NOT_INITIALIZED_ERROR
+        self._impl.save_policy(fname)
 
     def copy_policy_from(self, algo: "AlgoBase") -> None:
         assert self._impl is not None and algo.impl is not None, IMPL_NOT_INITIALIZED_ERROR

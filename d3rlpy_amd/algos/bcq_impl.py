@@ -317,6 +317,12 @@ class BCQImpl(ImplBase):
                     keep_h=False)
         return acts.out
 
+    def _policy_module(self) -> nn.Module:
+        from ..export import BCQGreedy, mlp_module
+        return BCQGreedy(mlp_module(self.vae_dec, self.store), mlp_module(self.policy, self.store),
+                         mlp_module(self.critic, self.store, 0), self._action_size,
+                         self._n_action_samples, self._action_flexibility)
+
     def _predict_best_action(self, x: torch.Tensor) -> torch.Tensor:
         """bcq_impl.py:204-210: N sampled actions per state, argmax of Q_0."""
         N, A = self._n_action_samples, self._action_size

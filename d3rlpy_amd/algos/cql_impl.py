@@ -338,6 +338,10 @@ class CQLImpl(ImplBase):
         mlp.forward(self.policy, self.store, x.data_ptr(), True, x.shape[1], acts)
         return acts.out[0]
 
+    def _policy_module(self) -> nn.Module:
+        from ..export import TanhMeanPolicy, mlp_module
+        return TanhMeanPolicy(mlp_module(self.policy, self.store), self._action_size)
+
     def _predict_best_action(self, x: torch.Tensor) -> torch.Tensor:
         A = self._action_size
         return torch.tanh(self._policy_head(x)[:, :A])

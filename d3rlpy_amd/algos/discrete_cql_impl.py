@@ -246,6 +246,17 @@ class DiscreteCQLImpl(ImplBase):
         q = head.forward(taus, [enc.h.data_ptr()], B * Kg, Kg, self.store)
         return q.view(B, Kg, -1).mean(dim=1)
 
+    def _policy_module(self) -> nn.Module:
+        from ..export import IQNGreedy, conv_from, linear_from
+        st = self.store
+        convs = nn.ModuleList(
+            conv_from(st.view(wn)[0], st.view(bn)[0], g[5])
+            for (wn, bn), g in zip(self.conv_names, self.geom))
+        return IQNGreedy(convs, linear_from(st.view("enc.fc.W")[0], st.view("enc.fc.b")[0]),
+                         linear_from(st.view("q.embed.W")[0], st.view("q.embed.b")[0]),
+                         linear_from(st.view("q.fc.W")[0], st.view("q.fc.b")[0]),
+                         self._K_greedy, self._E)
+
     def predict_best_action(self, x) -> np.ndarray:
         with torch.no_grad():
             return self._q_values(self._as_input(x)).argmax(dim=1).cpu().numpy()

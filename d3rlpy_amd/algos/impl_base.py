@@ -143,6 +143,16 @@ class ImplBase:
             return mean_values, stds
         return mean_values
 
+    def save_policy(self, fname: str) -> None:
+        """algos/torch/base.py:87-127: the greedy policy (behind the scalers)
+        as TorchScript ``.pt`` or ``.onnx``, built by ``_policy_module``."""
+        from ..export import save_traced
+        save_traced(self._policy_module(), self._observation_shape, self.torch_device, fname,
+                    self._scaler, self._action_scaler)
+
+    def _policy_module(self) -> torch.nn.Module:
+        raise NotImplementedError
+
     def _predict_best_action(self, x: torch.Tensor) -> torch.Tensor:
         raise NotImplementedError
 

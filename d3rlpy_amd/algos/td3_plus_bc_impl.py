@@ -261,6 +261,10 @@ class TD3PlusBCImpl(ImplBase):
         return names, ws.ring[:k].cpu().numpy()
 
     # ------------------------------------------------------------- inference
+    def _policy_module(self) -> nn.Module:
+        from ..export import DeterministicPolicy, mlp_module
+        return DeterministicPolicy(mlp_module(self.policy, self.store))
+
     def _predict_best_action(self, x: torch.Tensor) -> torch.Tensor:
         acts = mlp.Acts.alloc(self.policy, x.shape[0], self.torch_device)
         x = x.contiguous().float()
