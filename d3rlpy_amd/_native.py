@@ -105,6 +105,8 @@ class SacActorHeadDesc(C.Structure):
         ("dhead", vp), ("metrics", vp),
         ("B", C.c_int32), ("A", C.c_int32), ("C", C.c_int32),
         ("min_logstd", C.c_float), ("max_logstd", C.c_float),
+        ("w_head", vp), ("h", vp), ("ldh", C.c_int64), ("dz", vp), ("lddz", C.c_int64),
+        ("H", C.c_int32),
     ]
 
 

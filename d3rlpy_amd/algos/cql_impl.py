@@ -517,6 +517,16 @@ class _Workspace:
         h.dhead, h.metrics = self.dhead.data_ptr(), self.metrics.data_ptr()
         h.B, h.A, h.C = self.B, self.A, self.C
         h.min_logstd, h.max_logstd = impl._min_logstd, impl._max_logstd
+        # the policy head's input gradient goes straight into the trunk
+        # backward's first dz buffer (per-layer backward path)
+        self.head_dz = not self.pbwd.fused and impl.policy.sizes[-2] <= 256
+        if self.head_dz:
+            pol = impl.policy
+            Lp = pol.n_layers
+            h.w_head = pol.W(Lp - 1, impl.store)
+            h.h, h.ldh = self.pacts.h[Lp - 2].data_ptr(), pol.sizes[Lp - 1]
+            h.dz, h.lddz = self.pbwd.dz[0].data_ptr(), self.pbwd.dz[0].shape[2]
+            h.H = pol.sizes[Lp - 1]
         self.head_desc = h
 
     # ---------------------------------------------------------------- inputs
@@ -655,7 +665,8 @@ class _Workspace:
                          g_out=self.adq.data_ptr())
             ops.call_desc("d3a_sac_actor_head", self.head_desc)
             mlp.backward(self.pbwd, impl.store, self.obs2.data_ptr(), True, D, self.pacts,
-                         self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B)
+                         self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B,
+                         head_dz_ready=self.head_dz)
             self._apply(self.actor_opt, dp)
         # 7. soft update of both targets + metric ring + optimiser step counters
         if dp is not None:

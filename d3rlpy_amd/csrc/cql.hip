@@ -306,41 +306,71 @@ __global__ __launch_bounds__(256) void sac_actor_dq_kernel(const float* q, int64
   for (int c = 0; c < C; ++c) dq[c * sdq + b] = (c == arg) ? -1.f / (float)B : 0.f;
 }
 
+// Workgroups 0..B-1: one batch row b each -- the policy-head gradient of row
+// b (threads j < A), then, when dz is given, the head's input gradient
+// dz[b][n] = (sum_k dhead[b][k] W_head[k][n]) * [h[b][n] > 0] for the trunk
+// backward (autograd of the `_mu` / `_logstd` Linear layers, policies.py:
+// 170-176; thread n, H <= 256, operands loaded before the head math).
+// Workgroup B: the actor loss mean(exp(log_temp) * logp - min_c Q) into
+// metrics[5] (rows summed in a fixed order).
 __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_desc d) {
   __shared__ float scratch[4];
+  __shared__ float s_dh[32];
   const int tid = threadIdx.x;
   const int A = d.A, B = d.B, C = d.C;
+  const int64_t b = blockIdx.x;
   const float et = d.scalars[0];
-  const float dlogp = et / (float)B;
-  float lsum = 0.f;
-  for (int b = tid; b < B; b += blockDim.x) {
-    const float* hrow = d.head + (int64_t)b * 2 * A;
-    float qmin = d.q[b];
-    for (int c = 1; c < C; ++c) qmin = fminf(qmin, d.q[c * d.sqc + b]);
-    lsum += et * d.logp[b] - qmin;
-    for (int j = 0; j < A; ++j) {
-      float da = 0.f;
-      for (int c = 0; c < C; ++c) da += d.dq_da[c * d.sda_c + (int64_t)b * d.ld_da + d.da_off + j];
-      const float mu = hrow[j], lsr = hrow[A + j];
-      const float l = fminf(fmaxf(lsr, d.min_logstd), d.max_logstd);
-      const float sd = expf(l);
-      const float u = d.u[b * A + j];
-      const float e = d.eps[b * A + j];
-      const float th = tanhf(u);
-      const float dm = u - mu;
-      const float var = sd * sd;
-      // d logp / d u (direct): -(u-mu)/var + 2 - 4 sigmoid(-2u)
-      const float dlp_du = -dm / var + 2.f - 4.f * sigmoidf_t(-2.f * u);
-      const float du = da * (1.f - th * th) + dlogp * dlp_du;
-      const float dmu = du + dlogp * (dm / var);
-      const float dsd = du * e + dlogp * ((dm * dm) / (var * sd) - 1.f / sd);
-      const bool pass = (lsr >= d.min_logstd) && (lsr <= d.max_logstd);
-      d.dhead[(int64_t)b * 2 * A + j] = dmu;
-      d.dhead[(int64_t)b * 2 * A + A + j] = pass ? dsd * sd : 0.f;
+  if (b == B) {
+    float lsum = 0.f;
+    for (int r = tid; r < B; r += blockDim.x) {
+      float qmin = d.q[r];
+      for (int c = 1; c < C; ++c) qmin = fminf(qmin, d.q[c * d.sqc + r]);
+      lsum += et * d.logp[r] - qmin;
     }
+    const float tot = block_sum(lsum, scratch);
+    if (tid == 0) d.metrics[5] = tot / (float)B;
+    return;
   }
-  const float tot = block_sum(lsum, scratch);
-  if (tid == 0) d.metrics[5] = tot / (float)B;
+  const float dlogp = et / (float)B;
+  const float* hrow = d.head + b * 2 * A;
+  // input-gradient operands of this thread's column
+  const bool col = d.dz != nullptr && tid < d.H;
+  float hv = 0.f, wk[32];
+  if (col) {
+    hv = d.h[b * d.ldh + tid];
+    for (int k = 0; k < 2 * A; ++k) wk[k] = d.w_head[(int64_t)k * d.H + tid];
+  }
+  if (tid < A) {
+    const int j = tid;
+    float da = 0.f;
+    for (int c = 0; c < C; ++c) da += d.dq_da[c * d.sda_c + b * d.ld_da + d.da_off + j];
+    const float mu = hrow[j], lsr = hrow[A + j];
+    const float l = fminf(fmaxf(lsr, d.min_logstd), d.max_logstd);
+    const float sd = expf(l);
+    const float u = d.u[b * A + j];
+    const float e = d.eps[b * A + j];
+    const float th = tanhf(u);
+    const float dm = u - mu;
+    const float var = sd * sd;
+    // d logp / d u (direct): -(u-mu)/var + 2 - 4 sigmoid(-2u)
+    const float dlp_du = -dm / var + 2.f - 4.f * sigmoidf_t(-2.f * u);
+    const float du = da * (1.f - th * th) + dlogp * dlp_du;
+    const float dmu = du + dlogp * (dm / var);
+    const float dsd = du * e + dlogp * ((dm * dm) / (var * sd) - 1.f / sd);
+    const bool pass = (lsr >= d.min_logstd) && (lsr <= d.max_logstd);
+    const float dls = pass ? dsd * sd : 0.f;
+    d.dhead[b * 2 * A + j] = dmu;
+    d.dhead[b * 2 * A + A + j] = dls;
+    s_dh[j] = dmu;
+    s_dh[A + j] = dls;
+  }
+  if (d.dz == nullptr) return;
+  __syncthreads();
+  if (col) {
+    float v = 0.f;
+    for (int k = 0; k < 2 * A; ++k) v = fmaf(s_dh[k], wk[k], v);
+    d.dz[b * d.lddz + tid] = hv > 0.f ? v : 0.f;
+  }
 }
 
 }  // namespace
@@ -394,8 +424,12 @@ extern "C" int d3a_sac_actor_dq(const float* q, int64_t sqc, int32_t C, int32_t 
 }
 
 extern "C" int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream) {
-  D3A_CHECK_ARG(d && d->B >= 1 && d->A >= 1 && d->C >= 1, "d3a_sac_actor_head: bad args");
-  hipLaunchKernelGGL(sac_actor_head_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *d);
+  D3A_CHECK_ARG(d && d->B >= 1 && d->A >= 1 && d->A <= 16 && d->C >= 1,
+                "d3a_sac_actor_head: bad args");
+  D3A_CHECK_ARG(!d->dz || (d->h && d->w_head && d->H >= 1 && d->H <= 256),
+                "d3a_sac_actor_head: dz needs h, w_head and 1 <= H <= 256");
+  hipLaunchKernelGGL(sac_actor_head_kernel, dim3((unsigned)d->B + 1), dim3(256), 0,
+                     (hipStream_t)stream, *d);
   D3A_LAUNCH_CHECK("d3a_sac_actor_head");
   return 0;
 }

@@ -360,6 +360,14 @@ typedef struct d3a_sac_actor_head_desc {
   float* metrics;         /* metrics[5] = actor_loss                       */
   int32_t B, A, C;
   float min_logstd, max_logstd;
+  /* optional (dz != NULL): the head's input gradient for the trunk backward,
+   * dz[b*lddz + n] = (sum_k dhead[b][k] w_head[k*H + n]) * [h[b*ldh + n] > 0] */
+  const float* w_head;    /* [2A][H] head weight (_mu rows, then _logstd)   */
+  const float* h;         /* [B][ldh] last hidden activation of the policy  */
+  int64_t ldh;
+  float* dz;
+  int64_t lddz;
+  int32_t H;              /* <= 256 */
 } d3a_sac_actor_head_desc;
 int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream);
 
