@@ -72,6 +72,11 @@ WORKLOADS = {
     "bcq": ("halfcheetah-medium-v0", 256,
             "BCQ K3 (configs[2]): obs 17, act 6, batch 256, QR critics n_quantiles 200, "
             "n_critics 2, n_action_samples 100, hidden [256,256], reference defaults"),
+    "cqldp": ("antmaze-umaze-v0", 256,
+              "CQL K4 (configs[3]) data parallel: obs 29, act 8, 256 rows per GPU (global batch "
+              "256 x n_gpus), n_critics 2, n_action_samples 10, hidden [256,256], reference "
+              "defaults; per step three RCCL SUM all-reduces (scalar, critic, actor gradients) "
+              "captured in the update graph"),
     "dcql": ("atari", 512,
              "DiscreteCQL K5 (configs[4]): 4x84x84 uint8 frame stacks (n_frames 4), IQN "
              "(64 quantiles, embed 64), batch 512, 4 actions, pixel scaler, Nature-DQN "
@@ -80,7 +85,7 @@ WORKLOADS = {
 
 
 def _make_algo(name: str, batch: int):
-    if name == "cql":
+    if name in ("cql", "cqldp"):
         from d3rlpy_amd.algos.cql import CQL
         return CQL(batch_size=batch, n_critics=2, n_action_samples=10)
     if name == "dcql":
@@ -94,7 +99,7 @@ def _make_algo(name: str, batch: int):
     return TD3PlusBC(batch_size=batch)
 
 
-def build_workload(rank: int, n_transitions: int, name: str = "cql"):
+def build_workload(rank: int, n_transitions: int, name: str = "cql", world: int = 1):
     from d3rlpy_amd.dataset import DeviceDataset
     from d3rlpy_amd.datasets import get_synthetic_d4rl
     from d3rlpy_amd.iterators import RandomIterator
@@ -111,9 +116,18 @@ def build_workload(rank: int, n_transitions: int, name: str = "cql"):
         algo.scaler.fit_dataset(ds)  # as fit() does before building the impl
     algo.build_with_dataset(ds)
     ddata = DeviceDataset(ds)
+    shard = (0, 1)
+    seed = 1000 + rank
+    if name == "cqldp" and world > 1:
+        # K4: one global index stream (same seed on every rank), rank k
+        # gathers rows [256k, 256k+256) of each global batch; gradients are
+        # all-reduced inside the update graph (d3rlpy_amd/dp.py)
+        from d3rlpy_amd.dp import DataParallel
+        algo.impl.enable_data_parallel(DataParallel())
+        shard, seed = (rank, world), 1000
     it = RandomIterator(ddata, n_steps_per_epoch=1 << 40, batch_size=batch,
                         n_frames=algo.n_frames, out=algo.impl.staging_batch(batch),
-                        seed=1000 + rank)
+                        seed=seed, shard=shard)
     return algo, it
 
 
@@ -154,13 +168,13 @@ def cpu_baseline(seconds: float, threads: int, name: str = "cql"):
     if name == "dcql":
         return _cpu_baseline_dcql(seconds, B, gen)
     n = 100_000
-    D, A = {"cql": (11, 3), "td3bc": (3, 1), "bcq": (17, 6)}[name]
+    D, A = {"cql": (11, 3), "cqldp": (29, 8), "td3bc": (3, 1), "bcq": (17, 6)}[name]
     obs, act, rew, term = synthetic_dataset(n, D, A, episode_len=1000, seed=0)
     trans = []
     for o, a, r, t in to_episodes(obs, act, rew, term):
         trans += to_transitions(o, a, r, t)
     np.random.seed(0)
-    if name == "cql":
+    if name in ("cql", "cqldp"):
         orc = CQLOracle(D, A, n_critics=2, n_action_samples=10, seed=0)
 
         def update(batch, k):
@@ -258,7 +272,7 @@ def main():
     import torch
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     ws, rank, local = _dist_setup()
-    algo, it = build_workload(rank, args.transitions, args.algo)
+    algo, it = build_workload(rank, args.transitions, args.algo, ws)
 
     gpu_steps(algo, it, args.warmup)
     torch.cuda.synchronize()
@@ -303,6 +317,8 @@ def main():
         sps, k, el = cpu_baseline(args.cpu_seconds, threads, args.algo)
         what = {"cql": "CQL update (torch CPU, op-for-op restatement of cql_impl.py/"
                        "sac_impl.py/ddpg_impl.py)",
+                "cqldp": "CQL update at antmaze shapes, batch 256 (torch CPU, op-for-op "
+                         "restatement of cql_impl.py/sac_impl.py/ddpg_impl.py)",
                 "td3bc": "TD3+BC update (torch CPU, op-for-op restatement of "
                          "td3_plus_bc_impl.py/td3_impl.py/ddpg_impl.py, standard scaler)",
                 "bcq": "BCQ update (torch CPU, op-for-op restatement of bcq_impl.py/"
@@ -315,9 +331,13 @@ def main():
                          f"(np.random.randint per sample + TransitionMiniBatch gather) on a "
                          f"100k-transition synthetic dataset; {k} steps in {el:.1f}s, "
                          f"{threads} threads"}
-    value = ws * args.steps / elapsed
+    # replicas: every rank's steps count; data parallel: one global step per
+    # step of all ranks together
+    dp = args.algo == "cqldp"
+    value = (1 if dp else ws) * args.steps / elapsed
     shape, batch, wdesc = WORKLOADS[args.algo]
     metric = {"cql": "gradient-steps/sec (CQL, batch=256, obs=11 act=3) at 1/2/4/8 GPU",
+              "cqldp": "gradient-steps/sec (CQL data-parallel, 256 rows per GPU, obs=29 act=8)",
               "td3bc": "gradient-steps/sec (TD3+BC, batch=100, obs=3 act=1)",
               "bcq": "gradient-steps/sec (BCQ QR-200, batch=256, obs=17 act=6)",
               "dcql": "gradient-steps/sec (DiscreteCQL-IQN, batch=512, 4x84x84 pixels)"}[args.algo]
@@ -338,7 +358,9 @@ def main():
                  f"synthetic Atari-shaped uint8 frames ({args.transitions} x 1x84x84, "
                  "HBM-resident, 4-frame stacks gathered on device)"),
         "config": {"workload": wdesc,
-                   "global_batch": batch * ws, "parallelism": f"replicas x{ws}",
+                   "global_batch": batch * ws,
+                   "parallelism": (f"dp{ws} (RCCL all-reduce)" if dp and ws > 1 else
+                                   "single learner" if dp else f"replicas x{ws}"),
                    "losses_finite": finite},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak_tflops,
                      "unit": "TFLOP/s", "frac": round(achieved / peak_tflops, 4),
