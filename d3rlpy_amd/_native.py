@@ -294,6 +294,15 @@ class IqnHeadDesc(C.Structure):
     ]
 
 
+class DqnLossDesc(C.Structure):
+    _fields_ = [
+        ("q", vp), ("q_next", vp), ("q_targ", vp), ("act", vp), ("rew", vp), ("term", vp),
+        ("n_steps", vp), ("dq", vp), ("metrics", vp),
+        ("B", C.c_int32), ("A", C.c_int32), ("double_q", C.c_int32),
+        ("gamma", C.c_float), ("alpha", C.c_float),
+    ]
+
+
 class IqnLossDesc(C.Structure):
     _fields_ = [
         ("q_loss", vp), ("q_next", vp), ("q_targ", vp),
@@ -348,6 +357,7 @@ _SIGNATURES = {
     "d3a_iqn_prior": (C.c_int, [C.POINTER(IqnPriorDesc), vp]),
     "d3a_iqn_head_fwd": (C.c_int, [C.POINTER(IqnHeadDesc), vp]),
     "d3a_iqn_loss": (C.c_int, [C.POINTER(IqnLossDesc), vp]),
+    "d3a_dqn_loss": (C.c_int, [C.POINTER(DqnLossDesc), vp]),
     "d3a_iqn_head_bwd": (C.c_int, [C.POINTER(IqnHeadBwdDesc), vp]),
     "d3a_bcq_rows": (C.c_int, [C.POINTER(BcqRowsDesc), vp]),
     "d3a_bcq_vae_sample": (C.c_int, [C.POINTER(BcqVaeDesc), vp]),

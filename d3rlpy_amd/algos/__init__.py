@@ -4,16 +4,17 @@ Only the algorithms on the accelerated hot path are provided.
 """
 from .bcq import BCQ
 from .cql import CQL, DiscreteCQL
+from .dqn import DQN, DoubleDQN
 from .sac import SAC
 from .td3 import DDPG, TD3
 from .td3_plus_bc import TD3PlusBC
 
-__all__ = ["BCQ", "CQL", "DDPG", "DiscreteCQL", "SAC", "TD3", "TD3PlusBC", "get_algo"]
+__all__ = ["BCQ", "CQL", "DDPG", "DQN", "DiscreteCQL", "DoubleDQN", "SAC", "TD3", "TD3PlusBC", "get_algo"]
 
 ALGO_LIST = {"bcq": BCQ, "cql": CQL, "ddpg": DDPG, "sac": SAC, "td3": TD3, "td3_plus_bc": TD3PlusBC}
 
 
-DISCRETE_ALGO_LIST = {"cql": DiscreteCQL}
+DISCRETE_ALGO_LIST = {"cql": DiscreteCQL, "dqn": DQN, "double_dqn": DoubleDQN}
 
 
 def get_algo(name: str, discrete: bool):

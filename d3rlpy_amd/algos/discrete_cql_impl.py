@@ -1,8 +1,10 @@
-"""DiscreteCQLImpl on HIP kernels with an IQN Q-function on pixels — drop-in for
+"""DiscreteCQLImpl on HIP kernels on pixels — drop-in for
 d3rlpy/algos/torch/cql_impl.py:246-302 (DiscreteCQLImpl) and what it inherits
-(DoubleDQNImpl / DQNImpl, algos/torch/dqn_impl.py:27-171), for the K5
-configuration: Nature-DQN PixelEncoder, DiscreteIQNQFunction
-(n_quantiles 64, embed 64), n_critics 1, pixel scaler.
+(DoubleDQNImpl / DQNImpl, algos/torch/dqn_impl.py:27-171; the DQN and
+DoubleDQN Impls of algos/dqn.py are this class with alpha = 0): Nature-DQN
+PixelEncoder, n_critics 1, pixel scaler, and either the K5 configuration's
+DiscreteIQNQFunction (n_quantiles 64, embed 64) or the reference's default
+DiscreteMeanQFunction (a linear head, Huber TD loss in d3a_dqn_loss).
 
 One ``update`` (dqn_impl.py:97-111) on the device:
   1  Philox taus for the five IQN evaluations of the step
@@ -52,6 +54,9 @@ def _geometry(obs_shape: Sequence[int]) -> List[Tuple[int, int, int, int, int, i
 
 
 class DiscreteCQLImpl(ImplBase):
+    # DoubleDQN target (online argmax, dqn_impl.py:162-171); DQNImpl clears it
+    _DOUBLE = True
+
     def __init__(
         self,
         observation_shape: Sequence[int],
@@ -68,15 +73,20 @@ class DiscreteCQLImpl(ImplBase):
         reward_scaler,
     ):
         super().__init__(observation_shape, action_size, scaler, None, reward_scaler, use_gpu)
-        if q_func_factory.get_type() != "iqn":
-            raise NotImplementedError("DiscreteCQL on HIP implements the IQN Q-function of K5")
+        self._q_type = q_func_factory.get_type()
+        if self._q_type not in ("iqn", "mean"):
+            raise NotImplementedError("the discrete HIP Impls implement the mean and IQN "
+                                      "Q-functions")
+        if self._q_type == "iqn" and not self._DOUBLE:
+            raise NotImplementedError("DQN (target-network argmax) with the IQN Q-function is "
+                                      "not implemented; DoubleDQN / DiscreteCQL are")
         if len(observation_shape) != 3:
             raise NotImplementedError("DiscreteCQL on HIP supports pixel observations")
         if scaler is None or scaler.get_type() != "pixel":
             raise NotImplementedError("DiscreteCQL on HIP expects the pixel scaler")
         if n_critics != 1 or reward_scaler is not None:
             raise NotImplementedError("n_critics = 1 and no reward scaler (K5)")
-        if action_size > NAT.IQN_MAX_ACTIONS:
+        if self._q_type == "iqn" and action_size > NAT.IQN_MAX_ACTIONS:
             raise NotImplementedError(f"at most {NAT.IQN_MAX_ACTIONS} actions")
         if getattr(encoder_factory, "TYPE", "pixel") != "pixel" or \
                 [list(f) for f in encoder_factory.filters] != [list(f) for f in FILTERS] or \
@@ -91,9 +101,10 @@ class DiscreteCQLImpl(ImplBase):
         self._gamma = gamma
         self._n_critics = n_critics
         self._alpha = alpha
-        self._K = q_func_factory.n_quantiles
-        self._K_greedy = q_func_factory.n_greedy_quantiles
-        self._E = q_func_factory.embed_size
+        iqn = self._q_type == "iqn"
+        self._K = q_func_factory.n_quantiles if iqn else 1
+        self._K_greedy = q_func_factory.n_greedy_quantiles if iqn else 1
+        self._E = q_func_factory.embed_size if iqn else 0
         self._F = encoder_factory.feature_size
         self._ws: Dict[int, "_Workspace"] = {}
 
@@ -114,8 +125,9 @@ class DiscreteCQLImpl(ImplBase):
         st.add("enc.fc.b", (1, F))
         st.add("q.fc.W", (1, A, F))
         st.add("q.fc.b", (1, A))
-        st.add("q.embed.W", (1, F, E))
-        st.add("q.embed.b", (1, F))
+        if self._q_type == "iqn":
+            st.add("q.embed.W", (1, F, E))
+            st.add("q.embed.b", (1, F))
         st.allocate(dev)
         self.store = st
         self._init_like_reference()
@@ -136,16 +148,17 @@ class DiscreteCQLImpl(ImplBase):
                 conv = nn.Conv2d(ci, co, kernel_size=k, stride=s)
                 st.view(f"enc.c{l}.W")[0].copy_(conv.weight)
                 st.view(f"enc.c{l}.b")[0].copy_(conv.bias)
-            for name, (o, i) in (("enc.fc", (self._F, self.flat)),
-                                 ("q.fc", (self._action_size, self._F)),
-                                 ("q.embed", (self._F, self._E))):
+            layers = [("enc.fc", (self._F, self.flat)), ("q.fc", (self._action_size, self._F))]
+            if self._q_type == "iqn":
+                layers.append(("q.embed", (self._F, self._E)))
+            for name, (o, i) in layers:
                 lin = nn.Linear(i, o)
                 st.view(f"{name}.W")[0].copy_(lin.weight)
                 st.view(f"{name}.b")[0].copy_(lin.bias)
 
     # ---------------------------------------------------------- checkpoints
     def _refs(self):
-        """EnsembleDiscreteQFunction(DiscreteIQNQFunction).parameters() order."""
+        """EnsembleDiscreteQFunction(DiscreteIQN / DiscreteMeanQFunction).parameters() order."""
         p = "_q_funcs.0."
         refs = []
         for l in range(len(self.geom)):
@@ -153,9 +166,10 @@ class DiscreteCQLImpl(ImplBase):
                      (f"{p}_encoder._convs.{l}.bias", f"enc.c{l}.b", 0, None)]
         refs += [(f"{p}_encoder._fc.weight", "enc.fc.W", 0, None),
                  (f"{p}_encoder._fc.bias", "enc.fc.b", 0, None),
-                 (f"{p}_fc.weight", "q.fc.W", 0, None), (f"{p}_fc.bias", "q.fc.b", 0, None),
-                 (f"{p}_embed.weight", "q.embed.W", 0, None),
-                 (f"{p}_embed.bias", "q.embed.b", 0, None)]
+                 (f"{p}_fc.weight", "q.fc.W", 0, None), (f"{p}_fc.bias", "q.fc.b", 0, None)]
+        if self._q_type == "iqn":
+            refs += [(f"{p}_embed.weight", "q.embed.W", 0, None),
+                     (f"{p}_embed.bias", "q.embed.b", 0, None)]
         return refs
 
     def get_state_dict(self) -> Dict[str, dict]:
@@ -236,8 +250,17 @@ class DiscreteCQLImpl(ImplBase):
 
     def _q_values(self, x_u8: torch.Tensor) -> torch.Tensor:
         """DiscreteIQNQFunction.forward in eval mode (n_greedy_quantiles
-        linspace taus, iqn_q_function.py:16-30): mean over quantiles, [B][A]."""
+        linspace taus, iqn_q_function.py:16-30): mean over quantiles, [B][A];
+        DiscreteMeanQFunction.forward (mean_q_function.py:22-23)."""
         B = x_u8.shape[0]
+        if self._q_type == "mean":
+            enc = _EncoderPass(self, B, self.torch_device, keep=False)
+            enc.forward(x_u8.data_ptr(), self.store)
+            q = torch.zeros(B, self._action_size, device=x_u8.device)
+            ops.linear_fwd(enc.h.data_ptr(), True, self._F, self.store.ptr("q.fc.W"),
+                           self.store.ptr("q.fc.b"), q.data_ptr(), 1, B, self._F,
+                           self._action_size, relu=False)
+            return q
         Kg = self._K_greedy
         enc = _EncoderPass(self, B, self.torch_device, keep=False)
         enc.forward(x_u8.data_ptr(), self.store)
@@ -247,11 +270,14 @@ class DiscreteCQLImpl(ImplBase):
         return q.view(B, Kg, -1).mean(dim=1)
 
     def _policy_module(self) -> nn.Module:
-        from ..export import IQNGreedy, conv_from, linear_from
+        from ..export import IQNGreedy, MeanQGreedy, conv_from, linear_from
         st = self.store
         convs = nn.ModuleList(
             conv_from(st.view(wn)[0], st.view(bn)[0], g[5])
             for (wn, bn), g in zip(self.conv_names, self.geom))
+        if self._q_type == "mean":
+            return MeanQGreedy(convs, linear_from(st.view("enc.fc.W")[0], st.view("enc.fc.b")[0]),
+                               linear_from(st.view("q.fc.W")[0], st.view("q.fc.b")[0]))
         return IQNGreedy(convs, linear_from(st.view("enc.fc.W")[0], st.view("enc.fc.b")[0]),
                          linear_from(st.view("q.embed.W")[0], st.view("q.embed.b")[0]),
                          linear_from(st.view("q.fc.W")[0], st.view("q.fc.b")[0]),
@@ -379,15 +405,21 @@ class _Workspace:
         self.seed = int(torch.randint(0, 2**62, (1,)).item())
         self.enc = _EncoderPass(impl, 2 * B, dev)      # online: [obs; next_obs]
         self.enc_t = _EncoderPass(impl, B, dev)        # target: next_obs
-        self.head = _HeadPass(impl, 4 * BK, dev)       # online rows [loss|lse|data|next]
-        self.head_t = _HeadPass(impl, BK, dev)         # target rows
-        self.dq = z(3 * BK, A)
+        self.mean = impl._q_type == "mean"
+        if self.mean:
+            # linear head: online Q over [obs; next_obs], target Q over next_obs
+            self.q_on, self.q_t = z(2 * B, A), z(B, A)
+            self.dq = z(B, A)
+        else:
+            self.head = _HeadPass(impl, 4 * BK, dev)   # online rows [loss|lse|data|next]
+            self.head_t = _HeadPass(impl, BK, dev)     # target rows
+            self.dq = z(3 * BK, A)
+            self.dphi = z(3 * BK, F)
         self.loss_b, self.cons_b = z(B), z(B)
         self.metrics = z(len(METRIC_NAMES))
         self.ring = z(1 << 16, len(METRIC_NAMES))
         self.ring_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         # backward buffers (obs samples only)
-        self.dphi = z(3 * BK, F)
         self.dzfc = z(B, F)
         self.dyt = z(B, impl.flat)
         self.dys = [z(B * oh * ow, co) for (ci, h, w, co, k, s, oh, ow) in impl.geom]
@@ -408,11 +440,16 @@ class _Workspace:
         self.S_fc = min(4, mlp.n_splits(B))
         self.grads.add("enc.fc.W", (1, F, impl.flat), self.S_fc)
         self.grads.add("enc.fc.b", (1, F), self.S_fc)
-        self.grads.add("q.fc.W", (1, A, F), B)
-        self.grads.add("q.fc.b", (1, A), B)
-        self.S_emb = mlp.n_splits(3 * BK)
-        self.grads.add("q.embed.W", (1, F, E), self.S_emb)
-        self.grads.add("q.embed.b", (1, F), self.S_emb)
+        if self.mean:
+            self.S_head = mlp.n_splits(B)
+            self.grads.add("q.fc.W", (1, A, F), self.S_head)
+            self.grads.add("q.fc.b", (1, A), self.S_head)
+        else:
+            self.grads.add("q.fc.W", (1, A, F), B)
+            self.grads.add("q.fc.b", (1, A), B)
+            self.S_emb = mlp.n_splits(3 * BK)
+            self.grads.add("q.embed.W", (1, F, E), self.S_emb)
+            self.grads.add("q.embed.b", (1, F), self.S_emb)
         self.opt = AdamGroup(impl.optim_state, self.grads)
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._ran_eager = set()
@@ -423,6 +460,17 @@ class _Workspace:
         impl = self.impl
         B, K, A, F = self.B, impl._K, impl._action_size, impl._F
         BK = B * K
+        if self.mean:
+            l = NAT.DqnLossDesc()
+            l.q, l.q_next, l.q_targ = (self.q_on.data_ptr(), self.q_on.data_ptr() + 4 * B * A,
+                                       self.q_t.data_ptr())
+            l.act, l.rew, l.term, l.n_steps = (self.act.data_ptr(), self.rew.data_ptr(),
+                                               self.term.data_ptr(), self.nsteps.data_ptr())
+            l.dq, l.metrics = self.dq.data_ptr(), self.metrics.data_ptr()
+            l.B, l.A, l.double_q = B, A, int(impl._DOUBLE)
+            l.gamma, l.alpha = impl._gamma, impl._alpha
+            self.loss_desc = l
+            return
         l = NAT.IqnLossDesc()
         q = self.head.q
         l.q_loss = q.data_ptr()                       # rows [0, 3BK)
@@ -499,7 +547,7 @@ class _Workspace:
         B, K, A, F, E = self.B, impl._K, impl._action_size, impl._F, impl._E
         BK = B * K
         st, tg = impl.store, impl.targ
-        if not self._external_taus:
+        if not self._external_taus and not self.mean:
             ops.philox_fill(self.taus, 0, self.taus.numel(), 0.0, 1.0, self.seed, self.rng_ctr,
                             self.rng_ticket)
         # encoders
@@ -507,17 +555,31 @@ class _Workspace:
         self.enc_t.forward(self.obs2.data_ptr() + self.obs2[0].numel() * B, tg)
         h_obs = self.enc.h.data_ptr()
         h_next = h_obs + 4 * B * F
-        # IQN heads: online rows [loss | lse | data | next], target rows
-        self.head.launch(self.taus.data_ptr(), [h_obs, h_obs, h_obs, h_next], BK, K, st)
-        self.head_t.launch(self.taus.data_ptr() + 4 * 4 * BK, [self.enc_t.h.data_ptr()], BK, K,
-                           tg)
-        ops.call_desc("d3a_iqn_loss", self.loss_desc)
-        # backward: head, embed, encoder (obs samples)
-        ops.call_desc("d3a_iqn_head_bwd", self.head_bwd_desc)
         g = self.grads
-        ops.linear_bwd_w(self.dphi.data_ptr(), F, 3 * BK * F, self.head.prior.data_ptr(), E,
-                         3 * BK * E, g.get("q.embed.W").data_ptr(), 1, 3 * BK, E, F, self.S_emb,
-                         db=g.get("q.embed.b").data_ptr(), variant=10)
+        if self.mean:
+            # linear heads (mean_q_function.py:22-23), the TD (+ conservative)
+            # loss with dL/dQ, then the head's weight and masked input gradients
+            ops.linear_fwd(h_obs, True, F, st.ptr("q.fc.W"), st.ptr("q.fc.b"),
+                           self.q_on.data_ptr(), 1, 2 * B, F, A, relu=False)
+            ops.linear_fwd(self.enc_t.h.data_ptr(), True, F, tg.ptr("q.fc.W"), tg.ptr("q.fc.b"),
+                           self.q_t.data_ptr(), 1, B, F, A, relu=False)
+            ops.call_desc("d3a_dqn_loss", self.loss_desc)
+            ops.linear_bwd_w(self.dq.data_ptr(), A, B * A, h_obs, F, B * F,
+                             g.get("q.fc.W").data_ptr(), 1, B, F, A, self.S_head,
+                             db=g.get("q.fc.b").data_ptr())
+            ops.linear_bwd_x(self.dq.data_ptr(), A, B * A, st.ptr("q.fc.W"), self.dzfc.data_ptr(),
+                             F, B * F, 1, B, F, A, mask=h_obs, ldm=F, smb=B * F)
+        else:
+            # IQN heads: online rows [loss | lse | data | next], target rows
+            self.head.launch(self.taus.data_ptr(), [h_obs, h_obs, h_obs, h_next], BK, K, st)
+            self.head_t.launch(self.taus.data_ptr() + 4 * 4 * BK, [self.enc_t.h.data_ptr()], BK,
+                               K, tg)
+            ops.call_desc("d3a_iqn_loss", self.loss_desc)
+            # backward: head, embed, encoder (obs samples)
+            ops.call_desc("d3a_iqn_head_bwd", self.head_bwd_desc)
+            ops.linear_bwd_w(self.dphi.data_ptr(), F, 3 * BK * F, self.head.prior.data_ptr(), E,
+                             3 * BK * E, g.get("q.embed.W").data_ptr(), 1, 3 * BK, E, F,
+                             self.S_emb, db=g.get("q.embed.b").data_ptr(), variant=10)
         ops.linear_bwd_w(self.dzfc.data_ptr(), F, B * F, self.enc.yt.data_ptr(), impl.flat,
                          B * impl.flat, g.get("enc.fc.W").data_ptr(), 1, B, impl.flat, F,
                          self.S_fc, db=g.get("enc.fc.b").data_ptr())

@@ -124,6 +124,23 @@ class IQNGreedy(nn.Module):
         return q.mean(dim=1).argmax(dim=1)
 
 
+class MeanQGreedy(nn.Module):
+    """argmax_a of DiscreteMeanQFunction.forward (mean_q_function.py:22-23):
+    PixelEncoder (encoders.py:130-162) then the linear head (DQNImpl.
+    _predict_best_action, dqn_impl.py:139-141)."""
+
+    def __init__(self, convs: nn.ModuleList, fc: nn.Linear, head: nn.Linear):
+        super().__init__()
+        self.convs, self.fc, self.head = convs, fc, head
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h = x
+        for conv in self.convs:
+            h = torch.relu(conv(h))
+        h = torch.relu(self.fc(h.reshape(h.shape[0], -1)))
+        return self.head(h).argmax(dim=1)
+
+
 def linear_from(W: torch.Tensor, b: torch.Tensor) -> nn.Linear:
     lin = nn.Linear(W.shape[1], W.shape[0], device=W.device)
     with torch.no_grad():

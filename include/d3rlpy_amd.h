@@ -606,6 +606,28 @@ typedef struct d3a_iqn_prior_desc {
 } d3a_iqn_prior_desc;
 int d3a_iqn_prior(const d3a_iqn_prior_desc* d, void* stream);
 
+/* TD loss + gradient of the DQN family with the mean Q-function
+ * (DiscreteMeanQFunction.compute_error, mean_q_function.py:25-40, Huber,
+ * beta 1; DQNImpl / DoubleDQNImpl.compute_target, dqn_impl.py:128-171;
+ * DiscreteCQLImpl.compute_loss, cql_impl.py:279-302, when alpha != 0).
+ * q [B][A] = Q(s, .), q_next [B][A] = Q(s', .) (online; read when double_q),
+ * q_targ [B][A] = Q_targ(s', .).  dq [B][A] = dL/dQ(s, .);
+ * metrics[0..2] = loss, td loss, conservative loss. */
+typedef struct d3a_dqn_loss_desc {
+  const float* q;
+  const float* q_next;
+  const float* q_targ;
+  const int32_t* act;
+  const float* rew;
+  const float* term;
+  const float* n_steps;
+  float* dq;
+  float* metrics;
+  int32_t B, A, double_q;
+  float gamma, alpha;
+} d3a_dqn_loss_desc;
+int d3a_dqn_loss(const d3a_dqn_loss_desc* d, void* stream);
+
 #define D3A_IQN_MAX_ACTIONS 18
 #define D3A_IQN_MAX_GROUPS 8
 #define D3A_IQN_HEAD_BWD_MAX_ROWS 512 /* G * K of d3a_iqn_head_bwd */

@@ -1,4 +1,4 @@
-"""CPU restatement of DiscreteCQLImpl with an IQN Q-function on pixels — TEST INFRASTRUCTURE.
+"""CPU restatement of DiscreteCQLImpl (IQN) and DQN / DoubleDQN / DiscreteCQL (mean Q) on pixels — TEST INFRASTRUCTURE.
 
 Follows, op for op and in the same order:
   d3rlpy/algos/torch/dqn_impl.py:97-171          (update, DoubleDQN target, hard sync)
@@ -172,6 +172,104 @@ class DiscreteCQLIQNOracle:
         one_hot = F.one_hot(act.view(-1), num_classes=self._action_size)
         data_values = (self._q_func(obs, taus.cons_data) * one_hot).sum(dim=1, keepdim=True)
         loss = loss + self._alpha * (logsumexp - data_values).mean()
+        loss.backward()
+        self._optim.step()
+        return float(loss.detach())
+
+    def update_target(self):
+        hard_sync(self._targ_q_func, self._q_func)
+
+
+# ---------------------------------------------------------------------------
+# DQN / DoubleDQN / DiscreteCQL with the mean Q-function (the reference's
+# default q_func_factory="mean") on pixels
+#   d3rlpy/models/torch/q_functions/mean_q_function.py:13-55  (DiscreteMeanQFunction)
+#   d3rlpy/models/torch/q_functions/utility.py:9-32          (pick_value_by_action, huber)
+#   d3rlpy/algos/torch/dqn_impl.py:97-171                    (DQN / DoubleDQN target, update)
+#   d3rlpy/algos/torch/cql_impl.py:279-302                   (DiscreteCQL loss)
+# ---------------------------------------------------------------------------
+def compute_huber_loss(y, target, beta: float = 1.0):
+    """q_functions/utility.py:27-32."""
+    diff = target - y
+    cond = diff.detach().abs() < beta
+    return torch.where(cond, 0.5 * diff ** 2, beta * (diff.abs() - 0.5 * beta))
+
+
+def pick_value_by_action(values, action, keepdim: bool = False):
+    """q_functions/utility.py:9-15."""
+    one_hot = F.one_hot(action.view(-1), num_classes=values.shape[1])
+    masked_values = values * one_hot.float()
+    return masked_values.sum(dim=1, keepdim=keepdim)
+
+
+class DiscreteMeanQFunction(nn.Module):
+    """mean_q_function.py:13-55 (reduction 'mean' of compute_error)."""
+
+    def __init__(self, encoder: PixelEncoder, action_size: int):
+        super().__init__()
+        self._encoder = encoder
+        self._action_size = action_size
+        self._fc = nn.Linear(encoder.get_feature_size(), action_size)
+
+    def forward(self, x):
+        return self._fc(self._encoder(x))
+
+    def compute_error(self, observations, actions, rewards, target, terminals, gamma=0.99):
+        one_hot = F.one_hot(actions.view(-1), num_classes=self._action_size)
+        value = (self.forward(observations) * one_hot.float()).sum(dim=1, keepdim=True)
+        y = rewards + gamma * target * (1 - terminals)
+        return compute_huber_loss(value, y).mean()
+
+    def compute_target(self, x, action=None):
+        if action is None:
+            return self.forward(x)
+        return pick_value_by_action(self.forward(x), action, keepdim=True)
+
+
+class DiscreteMeanOracle:
+    """DQNImpl (variant 'dqn'), DoubleDQNImpl ('double_dqn') or DiscreteCQLImpl
+    ('cql') with n_critics 1, the mean Q-function and the pixel scaler."""
+
+    def __init__(self, observation_shape: Sequence[int], action_size: int, variant: str = "dqn",
+                 learning_rate: float = 6.25e-5, gamma: float = 0.99, alpha: float = 1.0,
+                 feature_size: int = 512, seed: int = 0):
+        assert variant in ("dqn", "double_dqn", "cql")
+        torch.manual_seed(seed)
+        self._variant = variant
+        self._gamma, self._alpha = gamma, alpha
+        self._action_size = action_size
+        self._q_func = DiscreteMeanQFunction(PixelEncoder(observation_shape, feature_size),
+                                             action_size)
+        self._targ_q_func = copy.deepcopy(self._q_func)
+        self._optim = torch.optim.Adam(self._q_func.parameters(), lr=learning_rate)
+
+    _scale = staticmethod(DiscreteCQLIQNOracle._scale)
+
+    def compute_target(self, batch: PixelBatch):
+        """DQNImpl.compute_target (dqn_impl.py:128-137) / DoubleDQNImpl's
+        (:162-171)."""
+        with torch.no_grad():
+            nobs = self._scale(batch.next_observations)
+            if self._variant == "dqn":
+                action = self._targ_q_func(nobs).argmax(dim=1)
+            else:
+                action = self._q_func(nobs).argmax(dim=1)
+            return self._targ_q_func.compute_target(nobs, action)
+
+    def update(self, batch: PixelBatch) -> float:
+        """DQNImpl.update (dqn_impl.py:97-126) [+ DiscreteCQLImpl.compute_loss]."""
+        self._optim.zero_grad()
+        q_tpn = self.compute_target(batch)
+        obs = self._scale(batch.observations)
+        act = batch.actions.long()
+        loss = self._q_func.compute_error(obs, act, batch.rewards, q_tpn, batch.terminals,
+                                          gamma=self._gamma ** batch.n_steps)
+        if self._variant == "cql":
+            policy_values = self._q_func(obs)
+            logsumexp = torch.logsumexp(policy_values, dim=1, keepdim=True)
+            one_hot = F.one_hot(act.view(-1), num_classes=self._action_size)
+            data_values = (self._q_func(obs) * one_hot).sum(dim=1, keepdim=True)
+            loss = loss + self._alpha * (logsumexp - data_values).mean()
         loss.backward()
         self._optim.step()
         return float(loss.detach())
