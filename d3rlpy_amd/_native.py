@@ -338,6 +338,8 @@ _SIGNATURES = {
                                C.c_double, C.c_double, C.c_double, vp]),
     "d3a_grad_reduce_f32": (C.c_int, [vp, C.c_int32, C.c_int64, vp]),
     "d3a_soft_update_f32": (C.c_int, [vp, vp, C.c_int64, C.c_double, vp]),
+    "d3a_standardize_f32": (C.c_int, [vp, vp, C.c_int64, C.c_int32, C.c_int64, vp, vp, C.c_float,
+                                      vp]),
     "d3a_step_end": (C.c_int, [vp, C.c_int32, vp, C.c_int64, vp, vp, C.c_uint32, vp, vp,
                                C.c_int64, C.c_double, C.c_float, vp]),
     "d3a_philox_fill": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_float, C.c_float, C.c_uint64,

@@ -84,8 +84,10 @@ class CQLImpl(ImplBase):
             raise NotImplementedError("CQL on HIP supports the 'mean' Q function")
         if len(observation_shape) != 1:
             raise NotImplementedError("CQL on HIP supports vector observations")
-        if scaler is not None or action_scaler is not None or reward_scaler is not None:
-            raise NotImplementedError("scalers are not supported by the HIP CQLImpl yet")
+        if scaler is not None and scaler.get_type() != "standard":
+            raise NotImplementedError("the HIP CQLImpl supports the 'standard' scaler")
+        if action_scaler is not None or reward_scaler is not None:
+            raise NotImplementedError("action/reward scalers are out of scope (SURVEY §2 #4)")
         self._actor_learning_rate = actor_learning_rate
         self._critic_learning_rate = critic_learning_rate
         self._temp_learning_rate = temp_learning_rate
@@ -388,8 +390,21 @@ class _Workspace:
         # the first-layer GEMMs use vector loads (the pad columns stay zero)
         self.LDX = LDX = (DA + 3) // 4 * 4
         z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
-        # staged batch: obs2 = [obs; next_obs]
+        # staged batch: obs2 = [obs; next_obs]; with a standard scaler the
+        # pipeline reads its transform xobs2 (d3a_standardize_f32, the
+        # TorchMiniBatch scaling of torch_utility.py:179-181), else obs2 itself
         self.obs2 = z(2 * B, D)
+        sc = impl._scaler
+        if sc is not None:
+            assert sc._mean is not None, "fit the scaler before the first update"
+            self.sc_mean = torch.as_tensor(np.asarray(sc._mean, dtype=np.float32).reshape(-1),
+                                           device=dev)
+            self.sc_std = torch.as_tensor(np.asarray(sc._std, dtype=np.float32).reshape(-1),
+                                          device=dev)
+            self.sc_eps = float(sc._eps)
+            self.xobs2 = z(2 * B, D)
+        else:
+            self.xobs2 = self.obs2
         self.act = z(B, A)
         self.rew = z(B)
         self.term = z(B)
@@ -456,8 +471,8 @@ class _Workspace:
         impl = self.impl
         s = NAT.CqlSampleDesc()
         s.head = self.pacts.out.data_ptr()
-        s.obs = self.obs2.data_ptr()
-        s.next_obs = self.obs2.data_ptr() + 4 * self.B * self.D
+        s.obs = self.xobs2.data_ptr()
+        s.next_obs = self.xobs2.data_ptr() + 4 * self.B * self.D
         s.act = self.act.data_ptr()
         s.eps_temp = self.eps_temp.data_ptr()
         s.eps_pi = self.eps_pi.data_ptr()
@@ -613,9 +628,11 @@ class _Workspace:
         if not self._external_noise:
             ops.philox_fill(self.noise, self.n_normal, self.n_uniform, -1.0, 1.0, self.seed,
                             self.rng_ctr, self.rng_ticket)
+        if impl._scaler is not None:
+            ops.standardize(self.obs2, self.xobs2, self.sc_mean, self.sc_std, self.sc_eps)
         if temp or alpha or critic or actor:
             # 1. policy on [obs; next_obs]
-            mlp.forward(impl.policy, impl.store, self.obs2.data_ptr(), True, D, self.pacts)
+            mlp.forward(impl.policy, impl.store, self.xobs2.data_ptr(), True, D, self.pacts)
             # 2. samples and Q inputs
             ops.call_desc("d3a_cql_sample", self.sample_desc)
         if alpha or critic:
@@ -664,7 +681,7 @@ class _Workspace:
                          q_min=self.aacts.out.data_ptr(), sq_b=B, q_scale=-1.0 / B,
                          g_out=self.adq.data_ptr())
             ops.call_desc("d3a_sac_actor_head", self.head_desc)
-            mlp.backward(self.pbwd, impl.store, self.obs2.data_ptr(), True, D, self.pacts,
+            mlp.backward(self.pbwd, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
                          self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B,
                          head_dz_ready=self.head_dz)
             self._apply(self.actor_opt, dp)

@@ -229,6 +229,18 @@ __global__ __launch_bounds__(256) void soft_update_kernel(float* targ, const flo
   if (i < n) targ[i] = __fadd_rn(__fmul_rn(targ[i], omt), __fmul_rn(tau, src[i]));
 }
 
+// ---- StandardScaler.transform: y = (x - mean) / (std + eps), each op rounded
+// as torch's separate fp32 ops (scalers.py:350-354) --------------------------
+__global__ __launch_bounds__(256) void standardize_kernel(const float* x, float* y, int64_t rows,
+                                                          int D, int64_t ldx, const float* mean,
+                                                          const float* std, float eps) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * D) return;
+  const int64_t r = i / D;
+  const int j = (int)(i - r * D);
+  y[r * ldx + j] = __fdiv_rn(__fsub_rn(x[r * ldx + j], mean[j]), __fadd_rn(std[j], eps));
+}
+
 // ---- Philox noise ----------------------------------------------------------
 __global__ __launch_bounds__(256) void philox_kernel(float* out, int64_t n_normal,
                                                      int64_t n_uniform, float lo, float hi,
@@ -389,6 +401,18 @@ extern "C" int d3a_grad_reduce_f32(const d3a_adam_segment* segs, int32_t n_seg,
   hipLaunchKernelGGL(grad_reduce_kernel, dim3((unsigned)n_blocks), dim3(256), 0,
                      (hipStream_t)stream, segs, (int)n_seg);
   D3A_LAUNCH_CHECK("d3a_grad_reduce_f32");
+  return 0;
+}
+
+extern "C" int d3a_standardize_f32(const float* x, float* y, int64_t rows, int32_t D,
+                                   int64_t ldx, const float* mean, const float* std, float eps,
+                                   void* stream) {
+  D3A_CHECK_ARG(x && y && mean && std, "d3a_standardize_f32: null pointer");
+  D3A_CHECK_ARG(D >= 1 && ldx >= D && rows >= 0, "d3a_standardize_f32: bad sizes");
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(standardize_kernel, dim3((unsigned)((rows * D + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, x, y, rows, D, ldx, mean, std, eps);
+  D3A_LAUNCH_CHECK("d3a_standardize_f32");
   return 0;
 }
 

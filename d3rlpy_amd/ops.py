@@ -109,6 +109,16 @@ def step_end(counters: Optional[torch.Tensor], inc_mask: int, metrics: Optional[
             "d3a_step_end")
 
 
+def standardize(x: torch.Tensor, y: torch.Tensor, mean: torch.Tensor, std: torch.Tensor,
+                eps: float) -> None:
+    """y = (x - mean) / (std + eps) row-wise (StandardScaler.transform)."""
+    _need_gpu(x, y, mean, std)
+    assert x.shape == y.shape and x.dim() == 2 and x.stride(1) == 1 and y.stride() == x.stride()
+    N.check(N.lib().d3a_standardize_f32(ptr(x), ptr(y), x.shape[0], x.shape[1], x.stride(0),
+                                        ptr(mean), ptr(std), float(eps), _stream()),
+            "d3a_standardize_f32")
+
+
 def soft_update(targ: torch.Tensor, src: torch.Tensor, tau: float) -> None:
     _need_gpu(targ, src)
     assert targ.numel() == src.numel() and targ.dtype == src.dtype == torch.float32

@@ -225,6 +225,13 @@ int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg,
 int d3a_grad_reduce_f32(const d3a_adam_segment* segs, int32_t n_seg,
                         int64_t n_blocks, void* stream);
 
+/* StandardScaler.transform (preprocessing/scalers.py:350-354) as applied to a
+ * minibatch by TorchMiniBatch (torch_utility.py:179-181): y[r][j] =
+ * (x[r][j] - mean[j]) / (std[j] + eps), separately rounded fp32 ops; x and y
+ * rows of stride ldx (may alias). */
+int d3a_standardize_f32(const float* x, float* y, int64_t rows, int32_t D, int64_t ldx,
+                        const float* mean, const float* std, float eps, void* stream);
+
 /* soft_sync (d3rlpy/torch_utility.py:27-33): targ = targ*(1-tau) + tau*src,
  * three separately rounded fp32 ops (mul_, tau*p, add_), bit-exact. */
 int d3a_soft_update_f32(float* targ, const float* src, int64_t n, double tau,

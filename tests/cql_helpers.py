@@ -11,7 +11,7 @@ def make_impl(D, A, hidden, N, C=2, **kw):
     args = dict(actor_learning_rate=1e-4, critic_learning_rate=3e-4, temp_learning_rate=1e-4,
                 alpha_learning_rate=1e-4, gamma=0.99, tau=0.005, initial_temperature=1.0,
                 initial_alpha=1.0, alpha_threshold=10.0, conservative_weight=5.0,
-                soft_q_backup=False)
+                soft_q_backup=False, scaler=None)
     args.update(kw)
     impl = CQLImpl(
         observation_shape=(D,), action_size=A,
@@ -20,7 +20,7 @@ def make_impl(D, A, hidden, N, C=2, **kw):
         actor_encoder_factory=VectorEncoderFactory(hidden),
         critic_encoder_factory=VectorEncoderFactory(hidden),
         q_func_factory=MeanQFunctionFactory(), n_critics=C, n_action_samples=N,
-        use_gpu=0, scaler=None, action_scaler=None, reward_scaler=None,
+        use_gpu=0, action_scaler=None, reward_scaler=None,
         **args)
     impl.build()
     return impl

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from cql_helpers import (HostBatch, make_batch, make_impl, make_oracle, make_sac_impl,
+from cql_helpers import (HostBatch, make_batch, make_impl, make_oracle, make_sac_impl, max_rel,
                          noise_dict, oracle_policy_grads, oracle_state)
 from oracle.cql import Batch, CQLNoise, SACOracle
 from test_gpu_cql_parity import _compare_step, _oracle_step
@@ -75,6 +75,75 @@ def test_cql_soft_q_backup_parity(case):
         torch.cuda.synchronize()
         _compare_step("cql-soft-" + case, step, impl, orc, m_hip, m_orc, cgrads, pgrads, A,
                       grad_tol=2e-5)
+
+
+def test_cql_standard_scaler_parity():
+    """CQL with scaler='standard': the HIP pipeline standardises the staged
+    batch on device (d3a_standardize_f32); the oracle receives the batch
+    transformed as TorchMiniBatch does (torch_utility.py:179-181).  Metrics
+    within 1e-5 of the fp32 oracle; each gradient tensor within 1e-5 (max-
+    normalised) of an fp64 evaluation of the same update, or no further from it
+    than 3x the fp32 oracle's own distance (a critic's head-bias gradient is
+    one sum of ~8k cancelling row terms: both fp32 paths land ~2-5e-5 from
+    exact on it here, at an absolute error of ~1e-9)."""
+    from d3rlpy_amd.preprocessing import StandardScaler
+    from oracle.td3bc import StandardScalerT
+    from cql_helpers import copy_oracle_to_impl, oracle_critic_params
+    D, A, H, B, N = 11, 3, [256, 256], 256, 10
+    rs = np.random.RandomState(8)
+    # statistics of the data below (obs ~ 3 N(0,1) + 1), slightly off as a
+    # fitted scaler's would be
+    mean = (1.0 + 0.1 * rs.randn(D)).astype(np.float32)
+    std = (3.0 * (1.0 + 0.1 * rs.rand(D))).astype(np.float32)
+    orc = make_oracle(D, A, H, N, seed=19)
+    o64 = make_oracle(D, A, H, N, seed=19)
+    for m in (o64._q_func, o64._policy, o64._targ_q_func, o64._targ_policy, o64._log_temp,
+              o64._log_alpha):
+        m.double()
+    impl = make_impl(D, A, H, N, scaler=StandardScaler(mean=mean, std=std))
+    copy_oracle_to_impl(orc, impl)
+    sc = StandardScalerT(mean, std)
+    obs, act, rew, nobs, term, nst = make_batch(rs, B, D, A)
+    obs, nobs = obs * 3 + 1, nobs * 3 + 1
+    nz = CQLNoise.draw(torch.Generator().manual_seed(8), B, A, N)
+    tb = Batch.from_numpy(sc.transform(torch.from_numpy(obs)).numpy(), act, rew,
+                          sc.transform(torch.from_numpy(nobs)).numpy(), term, nst)
+    tb64 = Batch(*(getattr(tb, f).double() for f in tb.__dataclass_fields__))
+    nz64 = CQLNoise(**{k: v.double() for k, v in noise_dict(nz).items()})
+    m32 = None
+    grads = []
+    for o, b, n in ((orc, tb, nz), (o64, tb64, nz64)):
+        tl, t = o.update_temp(b, n.eps_temp)
+        al, a = o.update_alpha(b, n)
+        cl = o.update_critic(b, n)
+        grads.append([[(fc.weight.grad.clone(), fc.bias.grad.clone())
+                       for fc in list(qf._encoder._fcs) + [qf._fc]] for qf in o._q_func.q_funcs])
+        actl = o.update_actor(b, n.eps_actor)
+        grads[-1].append(oracle_policy_grads(o._policy, A))
+        if m32 is None:
+            m32 = dict(temp_loss=float(tl), temp=float(t), alpha_loss=float(al), alpha=float(a),
+                       critic_loss=float(cl), actor_loss=float(actl))
+    m_hip = impl.update_step(HostBatch(obs, act, rew, nobs, term, nst), noise=noise_dict(nz))
+    torch.cuda.synchronize()
+    for k, v in m32.items():
+        assert abs(m_hip[k] - v) <= 1e-5 * max(1.0, abs(v)), (k, m_hip[k], v)
+    for c in range(3):
+        net = impl.critic if c < 2 else impl.policy
+        for l in range(net.n_layers):
+            for k, nm in enumerate((net.wname(l), net.bname(l))):
+                g = impl.critic_grad(nm)[c] if c < 2 else impl.policy_grad(nm)[0]
+                e_hip = max_rel(g, grads[1][c][l][k])
+                e_orc = max_rel(grads[0][c][l][k], grads[1][c][l][k])
+                print(f"[cql-scaler] {c} {nm}: hip-vs-fp64 {e_hip:.1e} oracle32-vs-fp64 "
+                      f"{e_orc:.1e}")
+                assert e_hip <= max(1e-5, 3 * e_orc), (c, nm, e_hip, e_orc)
+    # post-Adam parameters against the fp32 oracle
+    perr = 0.0
+    for c in range(2):
+        for (W, b), (Wo, bo) in zip([impl.critic.export_linear(l, c) for l in
+                                     range(impl.critic.n_layers)], oracle_critic_params(orc, c)):
+            perr = max(perr, float((W.cpu() - Wo).abs().max()), float((b.cpu() - bo).abs().max()))
+    assert perr <= 1e-5, perr
 
 
 def test_sac_fit_and_predict():
