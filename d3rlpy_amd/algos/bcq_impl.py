@@ -78,8 +78,10 @@ class BCQImpl(ImplBase):
                                       "K3 (q_func_factory='qr')")
         if len(observation_shape) != 1:
             raise NotImplementedError("BCQ on HIP supports vector observations")
-        if scaler is not None or action_scaler is not None or reward_scaler is not None:
-            raise NotImplementedError("scalers are not supported by the HIP BCQImpl yet")
+        if scaler is not None and scaler.get_type() != "standard":
+            raise NotImplementedError("the HIP BCQImpl supports the 'standard' scaler")
+        if action_scaler is not None or reward_scaler is not None:
+            raise NotImplementedError("action/reward scalers are out of scope (SURVEY §2 #4)")
         self._actor_learning_rate = actor_learning_rate
         self._critic_learning_rate = critic_learning_rate
         self._imitator_learning_rate = imitator_learning_rate
@@ -372,7 +374,20 @@ class _Workspace:
         self.rew = z(B)
         self.term = z(B)
         self.nsteps = z(B)
-        self.obs, self.next_obs = self.obs2[:B], self.obs2[B:]
+        # with a standard scaler every row builder reads the transform xobs2
+        # (d3a_standardize_f32, TorchMiniBatch scaling, torch_utility.py:179-181)
+        sc = impl._scaler
+        if sc is not None:
+            assert sc._mean is not None, "fit the scaler before the first update"
+            self.sc_mean = torch.as_tensor(np.asarray(sc._mean, dtype=np.float32).reshape(-1),
+                                           device=dev)
+            self.sc_std = torch.as_tensor(np.asarray(sc._std, dtype=np.float32).reshape(-1),
+                                          device=dev)
+            self.sc_eps = float(sc._eps)
+            self.xobs2 = z(2 * B, D)
+        else:
+            self.xobs2 = self.obs2
+        self.obs, self.next_obs = self.xobs2[:B], self.xobs2[B:]
         # noise: [eps_vae (B L) | z_target (B N L) | z_actor (B L)]
         self.noise = z((B + BN + B) * L)
         self.eps_vae = self.noise[:B * L]
@@ -554,6 +569,8 @@ class _Workspace:
         if not self._external_noise:
             ops.philox_fill(self.noise, self.noise.numel(), 0, -1.0, 1.0, self.seed,
                             self.rng_ctr, self.rng_ticket)
+        if impl._scaler is not None:
+            ops.standardize(self.obs2, self.xobs2, self.sc_mean, self.sc_std, self.sc_eps)
         ops.call_desc("d3a_bcq_rows", self.r_q)
         if imitator:
             # update_imitator (bcq_impl.py:148-161)

@@ -26,7 +26,7 @@ CASES = {
 }
 
 
-def make_bcq_impl(D, A, hidden, N, K, C=2):
+def make_bcq_impl(D, A, hidden, N, K, C=2, scaler=None):
     from d3rlpy_amd.algos.bcq_impl import BCQImpl
     from d3rlpy_amd.factories import AdamFactory, QRQFunctionFactory, VectorEncoderFactory
     impl = BCQImpl(
@@ -38,7 +38,7 @@ def make_bcq_impl(D, A, hidden, N, K, C=2):
         imitator_encoder_factory=VectorEncoderFactory(hidden),
         q_func_factory=QRQFunctionFactory(n_quantiles=K), gamma=0.99, tau=0.005, n_critics=C,
         lam=0.75, n_action_samples=N, action_flexibility=0.05, beta=0.5, use_gpu=0,
-        scaler=None, action_scaler=None, reward_scaler=None)
+        scaler=scaler, action_scaler=None, reward_scaler=None)
     impl.build()
     return impl
 
@@ -154,6 +154,35 @@ def test_bcq_full_step_equals_stages():
         assert torch.equal(a.store.data, b.store.data)
         s0, s1 = a.soft_span
         assert torch.equal(a.targ.data[s0:s1], b.targ.data[s0:s1])
+
+
+def test_bcq_standard_scaler_matches_prescaled_batch():
+    """scaler='standard': the on-device transform (d3a_standardize_f32) of a
+    raw batch gives bit-identical updates to an unscaled Impl fed the batch
+    transformed by torch as TorchMiniBatch does (torch_utility.py:179-181):
+    sub, add and div are correctly rounded either way."""
+    from d3rlpy_amd.preprocessing import StandardScaler
+    from oracle.td3bc import StandardScalerT
+    D, A, H, N, K, B = 17, 6, [256, 256], 100, 200, 256
+    rs = np.random.RandomState(6)
+    mean = (1.0 + 0.1 * rs.randn(D)).astype(np.float32)
+    std = (3.0 * (1.0 + 0.1 * rs.rand(D))).astype(np.float32)
+    a = make_bcq_impl(D, A, H, N, K, scaler=StandardScaler(mean=mean, std=std))
+    b = make_bcq_impl(D, A, H, N, K)
+    b.set_state_dict(a.get_state_dict())
+    sc = StandardScalerT(mean, std)
+    for step in range(2):
+        obs, act, rew, nobs, term, nst = _batch(rs, B, D, A)
+        obs, nobs = obs * 3 + 1, nobs * 3 + 1
+        nz = BCQNoise.draw(torch.Generator().manual_seed(step), B, A, N)
+        noise = {k: getattr(nz, k).numpy() for k in ("eps_vae", "z_target", "z_actor")}
+        ma = a.update_step(HostBatch(obs, act, rew, nobs, term, nst), noise=noise)
+        mb = b.update_step(HostBatch(sc.transform(torch.from_numpy(obs)).numpy(), act, rew,
+                                     sc.transform(torch.from_numpy(nobs)).numpy(), term, nst),
+                           noise=noise)
+        assert ma == mb, (step, ma, mb)
+    torch.cuda.synchronize()
+    assert torch.equal(a.store.data, b.store.data)
 
 
 def test_bcq_graph_replay_matches_eager():
