@@ -106,7 +106,7 @@ class SacActorHeadDesc(C.Structure):
         ("B", C.c_int32), ("A", C.c_int32), ("C", C.c_int32),
         ("min_logstd", C.c_float), ("max_logstd", C.c_float),
         ("w_head", vp), ("h", vp), ("ldh", C.c_int64), ("dz", vp), ("lddz", C.c_int64),
-        ("H", C.c_int32),
+        ("H", C.c_int32), ("dW_part", vp), ("db_part", vp),
     ]
 
 

@@ -456,7 +456,12 @@ class _Workspace:
         self.cbwd = mlp.BackwardSpace(impl.critic, self.Rc, self.cgrads, dev)
         self.abwd = mlp.BackwardSpace(impl.critic, B, None, dev)
         self.pgrads = GradSpace(dev)
-        self.pbwd = mlp.BackwardSpace(impl.policy, B, self.pgrads, dev)
+        # the policy head's weight / bias gradients come from
+        # d3a_sac_actor_head as one partial per batch row (see head_dz below)
+        self.head_dz = not mlp._FUSED_BWD and impl.policy.sizes[-2] <= 256
+        self.pbwd = mlp.BackwardSpace(impl.policy, B, self.pgrads, dev,
+                                      head_partials=B if self.head_dz else None)
+        assert not (self.head_dz and self.pbwd.fused)
         self.critic_opt = AdamGroup(impl.critic_state, self.cgrads)
         self.actor_opt = AdamGroup(impl.actor_state, self.pgrads)
         # share optimiser state across workspaces of other batch sizes
@@ -534,7 +539,6 @@ class _Workspace:
         h.min_logstd, h.max_logstd = impl._min_logstd, impl._max_logstd
         # the policy head's input gradient goes straight into the trunk
         # backward's first dz buffer (per-layer backward path)
-        self.head_dz = not self.pbwd.fused and impl.policy.sizes[-2] <= 256
         if self.head_dz:
             pol = impl.policy
             Lp = pol.n_layers
@@ -542,6 +546,8 @@ class _Workspace:
             h.h, h.ldh = self.pacts.h[Lp - 2].data_ptr(), pol.sizes[Lp - 1]
             h.dz, h.lddz = self.pbwd.dz[0].data_ptr(), self.pbwd.dz[0].shape[2]
             h.H = pol.sizes[Lp - 1]
+            h.dW_part = self.pgrads.get(pol.wname(Lp - 1)).data_ptr()
+            h.db_part = self.pgrads.get(pol.bname(Lp - 1)).data_ptr()
         self.head_desc = h
 
     # ---------------------------------------------------------------- inputs
@@ -683,7 +689,7 @@ class _Workspace:
             ops.call_desc("d3a_sac_actor_head", self.head_desc)
             mlp.backward(self.pbwd, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
                          self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B,
-                         head_dz_ready=self.head_dz)
+                         head_ready=self.head_dz)
             self._apply(self.actor_opt, dp)
         # 7. soft update of both targets + metric ring + optimiser step counters
         if dp is not None:

@@ -370,7 +370,13 @@ __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_
     float v = 0.f;
     for (int k = 0; k < 2 * A; ++k) v = fmaf(s_dh[k], wk[k], v);
     d.dz[b * d.lddz + tid] = hv > 0.f ? v : 0.f;
+    // this row's partial of the head weight gradient dW[k][n] = dhead[k] h[n]
+    if (d.dW_part) {
+      float* pw = d.dW_part + b * 2 * A * d.H + tid;
+      for (int k = 0; k < 2 * A; ++k) pw[(int64_t)k * d.H] = s_dh[k] * hv;
+    }
   }
+  if (d.db_part && tid < 2 * A) d.db_part[b * 2 * A + tid] = s_dh[tid];
 }
 
 }  // namespace

@@ -155,7 +155,10 @@ class BackwardSpace:
     """dz ping-pong buffers + weight-gradient partial workspaces for one net."""
 
     def __init__(self, net: EnsembleMLP, rows: int, grads: Optional[GradSpace], device,
-                 splits: Optional[int] = None):
+                 splits: Optional[int] = None, head_partials: Optional[int] = None):
+        """``head_partials``: partial count of the head layer's weight / bias
+        gradients when a caller's kernel writes them (one per row, say)
+        instead of the split-K GEMM (``backward(..., head_ready=True)``)."""
         self.net = net
         self.rows = rows
         hidden = net.sizes[1:-1]
@@ -174,8 +177,10 @@ class BackwardSpace:
         if grads is not None:
             for l in range(net.n_layers):
                 o, i = net.sizes[l + 1], net.sizes[l]
-                grads.add(net.wname(l), (net.C, o, i), self.splits)
-                grads.add(net.bname(l), (net.C, o), self.splits)
+                parts = head_partials if (head_partials and l == net.n_layers - 1) \
+                    else self.splits
+                grads.add(net.wname(l), (net.C, o, i), parts)
+                grads.add(net.bname(l), (net.C, o), parts)
 
 
 def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: int,
@@ -184,16 +189,16 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
              sxb: Optional[int] = None, q_min: Optional[int] = None, sq_b: int = 0,
              q_scale: float = 0.0, g_out: Optional[int] = None,
              g_scale: Optional[int] = None, n_scaled: int = 0,
-             members: Optional[int] = None, head_dz_ready: bool = False) -> None:
+             members: Optional[int] = None, head_ready: bool = False) -> None:
     """Backward of rows [r0, r0+n) given dL/d(output) (``dout`` points at row r0).
 
     dout layout: [C] x rows, member stride sdout_b, row stride ld_dout (1 for a
     single-output head).  ``dx`` (if given) receives dL/dx as [C][n][in].
     With ``q_min`` (single-output heads only) the row gradient is ``q_scale`` on
     the argmin member of q_min[.][r] (backward of a min over the ensemble).
-    ``head_dz_ready``: the head's input gradient is already in ``bs.dz[0]``
-    (written by the caller's head kernel, per-layer path only); only the head's
-    weight gradient is computed for it.
+    ``head_ready``: the caller's head kernel already wrote the head's input
+    gradient into ``bs.dz[0]`` and its weight / bias gradient partials (per-
+    layer path only); the backward starts at the trunk.
     """
     net = bs.net
     C, L, sizes, R = net.C, net.n_layers, net.sizes, acts.R
@@ -205,7 +210,7 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
     sxb_ = (0 if x_shared else R * ldx) if sxb is None else sxb
     gs = bs.grads
     if bs.fused:
-        assert not head_dz_ready
+        assert not head_ready
         _backward_fused(bs, store, x, ldx, sxb_, acts, dout, ld_dout, sdout_b, r0, n,
                         weight_grads, dx, q_min, sq_b, q_scale, g_out, g_scale, n_scaled, C)
         return
@@ -254,11 +259,11 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         ops.call_desc("d3a_head1_bwd", d)
     else:
         assert q_min is None
-        if weight_grads:
+        if weight_grads and not head_ready:
             gW, gb = gs.get(net.wname(L - 1)), gs.get(net.bname(L - 1))
             ops.linear_bwd_w(dout, ld_dout, sdout_b, hin, ld_h, sh, gW.data_ptr(), C, n, Hin,
                              out_dim, S, db=gb.data_ptr())
-        if not head_dz_ready:
+        if not head_ready:
             ops.linear_bwd_x(dout, ld_dout, sdout_b, net.W(L - 1, store), cur.data_ptr(), ld_cur,
                              scur, C, n, Hin, out_dim, mask=hin, ldm=ld_h, smb=sh)
     # ---- trunk layers L-2 .. 0

@@ -375,6 +375,11 @@ typedef struct d3a_sac_actor_head_desc {
   float* dz;
   int64_t lddz;
   int32_t H;              /* <= 256 */
+  /* optional (with dz): one partial per row of the head's weight / bias
+   * gradients, dW_part[b][k][n] = dhead[b][k] h[b][n], db_part[b][k] =
+   * dhead[b][k] (summed over b, in row order, by d3a_adam_f32) */
+  float* dW_part;
+  float* db_part;
 } d3a_sac_actor_head_desc;
 int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream);
 
