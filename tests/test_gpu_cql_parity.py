@@ -35,6 +35,9 @@ CASES = {
     "small": dict(D=5, A=2, hidden=[64, 64], N=4, B=32),
     "hopper": dict(D=11, A=3, hidden=[256, 256], N=10, B=256),   # K2 shapes
     "deep": dict(D=7, A=2, hidden=[128, 128, 128], N=3, B=64),   # 3 hidden layers
+    # n-step returns (gather n_steps 3): gamma ** n_steps per row
+    # (ddpg_impl.py:160, cql_impl.py:110-117) with n in {1, 2, 3}
+    "nstep": dict(D=11, A=3, hidden=[256, 256], N=10, B=256, nstep=True),
 }
 
 
@@ -110,6 +113,8 @@ def test_cql_update_parity(case):
     for step in range(3):
         impl.set_state_dict(oracle_state(orc))
         arrs = make_batch(rs, B, D, A)
+        if cfg.get("nstep"):
+            arrs = arrs[:5] + (rs.randint(1, 4, size=B).astype(np.float32),)
         nz = CQLNoise.draw(gen, B, A, N)
         m_orc, cgrads, pgrads = _oracle_step(orc, Batch.from_numpy(*arrs), nz, A)
         m_hip = impl.update_step(HostBatch(*arrs), noise=noise_dict(nz))
