@@ -38,6 +38,8 @@ class GemmDesc(C.Structure):
         ("sRb", C.c_int64), ("sRs", C.c_int64),
         ("alpha", C.c_float), ("relu", C.c_int32), ("accumulate", C.c_int32),
         ("variant", C.c_int32),
+        ("batch2", C.c_int64), ("sAb2", C.c_int64), ("sBb2", C.c_int64), ("sCb2", C.c_int64),
+        ("sbias_b2", C.c_int64), ("sMb2", C.c_int64),
     ]
 
 
@@ -330,6 +332,9 @@ _SIGNATURES = {
     "d3a_gemm_f32": (C.c_int, [C.POINTER(GemmDesc), vp]),
     "d3a_rowdot_f32": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
                                  C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
+    "d3a_rowdot2_f32": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
+                                  C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                  C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
     "d3a_colreduce_f32": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64,
                                     C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
     "d3a_outer_mask_f32": (C.c_int, [vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,

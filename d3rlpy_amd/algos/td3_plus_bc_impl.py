@@ -441,9 +441,10 @@ class _Workspace:
             mlp.forward(impl.policy, tg, self.x_targ.data_ptr(), True, LDX, self.tpacts,
                         keep_h=False)
             ops.call_desc("d3a_td3_target", self.target_desc)
-            mlp.forward(impl.critic, st, self.x_q.data_ptr(), True, LDX, self.qacts)
-            mlp.forward(impl.critic, tg, self.x_targ.data_ptr(), True, LDX, self.tacts,
-                        keep_h=False)
+            # critic ensemble on (s, a) and, in the same launches, the target
+            # ensemble on (s', a') (aux pass)
+            mlp.forward(impl.critic, st, self.x_q.data_ptr(), True, LDX, self.qacts,
+                        aux=(tg, self.x_targ.data_ptr(), LDX, self.tacts))
             self.loss_desc.actor_step = int(actor)
             ops.call_desc("d3a_td3_critic_loss", self.loss_desc)
             mlp.backward(self.cbwd, st, self.x_q.data_ptr(), True, LDX, self.qacts,

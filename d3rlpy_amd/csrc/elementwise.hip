@@ -23,13 +23,17 @@ namespace {
 __global__ __launch_bounds__(256) void rowdot_kernel(const float* X, int64_t sXb, int64_t sXr,
                                                      const float* w, int64_t swb,
                                                      const float* bias, int64_t sbb, float* out,
-                                                     int64_t sOb, int64_t rows, int64_t n) {
+                                                     int64_t sOb, int64_t rows, int64_t n,
+                                                     int64_t dX, int64_t dw, int64_t dbias,
+                                                     int64_t dout) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int64_t b = blockIdx.y;
+  const int64_t b = blockIdx.y, t = blockIdx.z;
   if (r >= rows) return;
-  const float* x = X + b * sXb + r * sXr;
-  const float* wb = w + b * swb;
+  const float* x = X + b * sXb + t * dX + r * sXr;
+  const float* wb = w + b * swb + t * dw;
+  out += t * dout;
+  if (bias) bias += t * dbias;
   float acc = 0.f;
   const bool vec = ((n & 3) == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0) &&
                    ((reinterpret_cast<uintptr_t>(wb) & 15) == 0);
@@ -343,12 +347,22 @@ extern "C" int d3a_rowdot_f32(const float* X, int64_t sXb, int64_t sXr, const fl
                               int64_t swb, const float* bias, int64_t sbb, float* out,
                               int64_t sOb, int64_t batch, int64_t rows, int64_t n,
                               void* stream) {
+  return d3a_rowdot2_f32(X, sXb, sXr, w, swb, bias, sbb, out, sOb, batch, rows, n, 1, 0, 0, 0, 0,
+                         stream);
+}
+
+extern "C" int d3a_rowdot2_f32(const float* X, int64_t sXb, int64_t sXr, const float* w,
+                               int64_t swb, const float* bias, int64_t sbb, float* out,
+                               int64_t sOb, int64_t batch, int64_t rows, int64_t n,
+                               int64_t batch2, int64_t dX, int64_t dw, int64_t dbias,
+                               int64_t dout, void* stream) {
   D3A_CHECK_ARG(X && w && out, "d3a_rowdot_f32: null pointer");
+  D3A_CHECK_ARG(batch2 >= 1, "d3a_rowdot2_f32: batch2 >= 1");
   if (batch <= 0 || rows <= 0) return 0;
-  dim3 grid((unsigned)((rows + 3) / 4), (unsigned)batch);
+  dim3 grid((unsigned)((rows + 3) / 4), (unsigned)batch, (unsigned)batch2);
   hipLaunchKernelGGL(rowdot_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, sXb, sXr, w, swb,
-                     bias, sbb, out, sOb, rows, n);
-  D3A_LAUNCH_CHECK("d3a_rowdot_f32");
+                     bias, sbb, out, sOb, rows, n, dX, dw, dbias, dout);
+  D3A_LAUNCH_CHECK("d3a_rowdot2_f32");
   return 0;
 }
 

@@ -35,6 +35,9 @@ struct Params {
   int64_t splits, sCs, kchunk, sRb, sRs;
   float alpha;
   int relu, accumulate;
+  // second batch dimension (an independent pass of the same shape, e.g. the
+  // target networks): z = (t * batch + b) * splits + s, offsets t * s?b2
+  int64_t batch2, sAb2, sBb2, sCb2, sbias_b2, sMb2;
 };
 
 // Load a 4-vector of a tile at non-k coordinate x and reduction coordinate k.
@@ -111,11 +114,12 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
   const int lane = t & 63, wid = t >> 6;
   const int64_t n0 = bx * BN;
   const int64_t m0 = by * BM;
-  const int64_t b = bz / p.splits, s = bz % p.splits;
+  const int64_t bb = bz / p.splits, s = bz % p.splits;
+  const int64_t b = bb % p.batch, t2 = bb / p.batch;
   const int64_t kbeg = s * p.kchunk;
   const int64_t kend = (kbeg + p.kchunk < p.K) ? kbeg + p.kchunk : p.K;
-  const float* Ab = p.A + b * p.sAb;
-  const float* Bb = p.B + b * p.sBb;
+  const float* Ab = p.A + b * p.sAb + t2 * p.sAb2;
+  const float* Bb = p.B + b * p.sBb + t2 * p.sBb2;
 
   int axl[AV], akl[AV], bxl[BV], bkl[BV];
 #pragma unroll
@@ -189,9 +193,9 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
     p.rowsum[b * p.sRb + s * p.sRs + m0 + t] = (float)rs;
 
   // epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  float* Cb = p.C + b * p.sCb + s * p.sCs;
-  const float* biasb = p.bias ? p.bias + b * p.sbias_b : nullptr;
-  const float* maskb = p.mask ? p.mask + b * p.sMb : nullptr;
+  float* Cb = p.C + b * p.sCb + t2 * p.sCb2 + s * p.sCs;
+  const float* biasb = p.bias ? p.bias + b * p.sbias_b + t2 * p.sbias_b2 : nullptr;
+  const float* maskb = p.mask ? p.mask + b * p.sMb + t2 * p.sMb2 : nullptr;
 #pragma unroll
   for (int j = 0; j < WN_T; ++j) {
     const int64_t n = n0 + wn + 32 * j + li;
@@ -268,7 +272,8 @@ __global__ __launch_bounds__(64 * KW) void gemm_rd_kernel(Params p) {
   const int64_t n0 = (int64_t)blockIdx.x * (32 * WN);
   const int64_t m0 = (int64_t)blockIdx.y * 32;
   const int64_t bz = blockIdx.z;
-  const int64_t b = bz / p.splits, s = bz % p.splits;
+  const int64_t bb = bz / p.splits, s = bz % p.splits;
+  const int64_t b = bb % p.batch, t2 = bb / p.batch;
   const int64_t sbeg = s * p.kchunk;
   const int64_t send = (sbeg + p.kchunk < p.K) ? sbeg + p.kchunk : p.K;
   // this wave's K slice (multiple of 8 so every lane group starts aligned)
@@ -276,8 +281,8 @@ __global__ __launch_bounds__(64 * KW) void gemm_rd_kernel(Params p) {
   wch = (wch + 7) / 8 * 8;
   const int64_t kb = sbeg + w * wch;
   const int64_t ke = (kb + wch < send) ? kb + wch : send;
-  const float* Ab = p.A + b * p.sAb;
-  const float* Bb = p.B + b * p.sBb;
+  const float* Ab = p.A + b * p.sAb + t2 * p.sAb2;
+  const float* Bb = p.B + b * p.sBb + t2 * p.sBb2;
   const int64_t m = m0 + li;
   const bool do_rowsum = p.rowsum != nullptr && blockIdx.x == 0;
 
@@ -338,9 +343,9 @@ __global__ __launch_bounds__(64 * KW) void gemm_rd_kernel(Params p) {
     for (int v = 0; v < KW; ++v) tot += rsum[v * 32 + li];
     p.rowsum[b * p.sRb + s * p.sRs + m] = (float)tot;
   }
-  float* Cb = p.C + b * p.sCb + s * p.sCs;
-  const float* biasb = p.bias ? p.bias + b * p.sbias_b : nullptr;
-  const float* maskb = p.mask ? p.mask + b * p.sMb : nullptr;
+  float* Cb = p.C + b * p.sCb + t2 * p.sCb2 + s * p.sCs;
+  const float* biasb = p.bias ? p.bias + b * p.sbias_b + t2 * p.sbias_b2 : nullptr;
+  const float* maskb = p.mask ? p.mask + b * p.sMb + t2 * p.sMb2 : nullptr;
 #pragma unroll
   for (int j = 0; j < WN; ++j) {
     const int64_t n = n0 + 32 * j + li;
@@ -386,7 +391,7 @@ void launch_v(const Params& p, hipStream_t st) {
   constexpr Variant v = kVariants[V];
   constexpr int BM = 32 * v.wm_t * v.waves_m, BN = 32 * v.wn_t * v.waves_n;
   dim3 grid((unsigned)((p.N + BN - 1) / BN), (unsigned)((p.M + BM - 1) / BM),
-            (unsigned)(p.batch * p.splits));
+            (unsigned)(p.batch * p.batch2 * p.splits));
   hipLaunchKernelGGL((gemm_f32_kernel<AM, BMd, v.wm_t, v.wn_t, v.waves_m, v.waves_n, v.bk>), grid,
                      dim3(64 * v.waves_m * v.waves_n), 0, st, p);
 }
@@ -394,7 +399,8 @@ void launch_v(const Params& p, hipStream_t st) {
 // waves per workgroup for the register-direct kernel: ~2048 waves in flight,
 // at least 32 k (one U=4 group of loads) per wave
 int rd_waves(const Params& p, int wn) {
-  const int64_t tiles = ((p.N + 32 * wn - 1) / (32 * wn)) * ((p.M + 31) / 32) * p.batch * p.splits;
+  const int64_t tiles =
+      ((p.N + 32 * wn - 1) / (32 * wn)) * ((p.M + 31) / 32) * p.batch * p.batch2 * p.splits;
   int kw = 8;
   while (kw > 1 && (tiles * kw > 4096 || p.kchunk / kw < 32)) kw >>= 1;
   return kw;
@@ -403,7 +409,7 @@ int rd_waves(const Params& p, int wn) {
 template <int AM, int BMd, int KW, int WN>
 void launch_rd_kw(const Params& p, hipStream_t st) {
   dim3 grid((unsigned)((p.N + 32 * WN - 1) / (32 * WN)), (unsigned)((p.M + 31) / 32),
-            (unsigned)(p.batch * p.splits));
+            (unsigned)(p.batch * p.batch2 * p.splits));
   hipLaunchKernelGGL((gemm_rd_kernel<AM, BMd, KW, WN, 4>), grid, dim3(64 * KW), 0, st, p);
 }
 
@@ -445,7 +451,8 @@ void launch_modes(const Params& p, int variant, hipStream_t st) {
 //    the large critic passes;
 //  - tiny K (the first layer's 11-17 inputs): one-wave 32x32 tile (6).
 int choose_variant(const Params& p) {
-  const int64_t blocks64 = ((p.M + 63) / 64) * ((p.N + 63) / 64) * p.batch * p.splits;
+  const int64_t blocks64 =
+      ((p.M + 63) / 64) * ((p.N + 63) / 64) * p.batch * p.batch2 * p.splits;
   const int64_t kslice = (p.K + p.splits - 1) / p.splits;
   if (kslice >= 32 && (blocks64 < 128 || p.M <= 32 || p.N <= 32)) return 9;
   if (blocks64 >= 128) return 0;
@@ -485,6 +492,11 @@ int make_params(const d3a_gemm_desc* d, Params& p, int& variant, int& am, int& b
   p.sbias_b = d->sbias_b; p.sMb = d->sMb; p.sMm = d->sMm; p.sMn = d->sMn;
   p.splits = d->splits; p.sCs = d->sCs; p.sRb = d->sRb; p.sRs = d->sRs;
   p.alpha = d->alpha; p.relu = d->relu; p.accumulate = d->accumulate;
+  // batch2 0 (a zero-initialised descriptor) means 1
+  p.batch2 = d->batch2 > 0 ? d->batch2 : 1;
+  p.sAb2 = d->sAb2; p.sBb2 = d->sBb2; p.sCb2 = d->sCb2;
+  p.sbias_b2 = d->sbias_b2; p.sMb2 = d->sMb2;
+  D3A_CHECK_ARG(p.batch2 == 1 || d->rowsum == nullptr, "d3a_gemm_f32: rowsum needs batch2 = 1");
   variant = d->variant >= 0 ? d->variant : env_variant();
   if (variant < 0) variant = choose_variant(p);
   const int bk = kVariants[variant].bk;
@@ -492,7 +504,8 @@ int make_params(const d3a_gemm_desc* d, Params& p, int& variant, int& am, int& b
   int64_t kc = (d->K + d->splits - 1) / d->splits;
   kc = ((kc + bk - 1) / bk) * bk;
   p.kchunk = kc > 0 ? kc : bk;
-  D3A_CHECK_ARG(d->batch * d->splits < 65536, "d3a_gemm_f32: batch*splits too large");
+  D3A_CHECK_ARG(d->batch * p.batch2 * d->splits < 65536,
+                "d3a_gemm_f32: batch*batch2*splits too large");
   D3A_CHECK_ARG((d->M + 31) / 32 < 65536, "d3a_gemm_f32: M too large");
   am = (d->sAk == 1) ? MODE_KCONTIG : (d->sAm == 1 ? MODE_XCONTIG : MODE_GENERIC);
   bm = (d->sBk == 1) ? MODE_KCONTIG : (d->sBn == 1 ? MODE_XCONTIG : MODE_GENERIC);

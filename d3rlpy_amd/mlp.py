@@ -91,8 +91,10 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     same network with the parameters of ``store2`` (same layout, e.g. the
     targets) over all acts2.R rows of x2 (shared by the members), no
     activations kept.  On the fused path it rides in the same launch (its
-    workgroups use the CUs the main pass leaves idle); otherwise it is a
-    separate forward."""
+    workgroups use the CUs the main pass leaves idle); on the per-layer path
+    each layer's launch carries it as a second batch dimension when its shape
+    equals the main pass's (acts2.R == acts.R rows, same ldx); otherwise it is
+    a separate forward."""
     R = acts.R
     r1 = R if r1 is None else r1
     n = r1 - r0
@@ -131,23 +133,37 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     L = net.n_layers
     inp, ld_in = x + 4 * r0 * ldx, ldx
     sxb_ = (0 if x_shared else R * ldx) if sxb is None else sxb
+    # the aux pass rides in the same launches (second batch dimension, element
+    # offsets from the main pass's operands) when it has the main pass's shape
+    pair = aux is not None and members is None and x_shared and sxb is None and r0 == 0 \
+        and n == R and aux[3].R == R and aux[2] == ldx
+    if pair:
+        ast, ax, _, aacts = aux
+        assert ast.size == store.size and list(ast.specs) == list(store.specs)
+        dW = (ast.data.data_ptr() - store.data.data_ptr()) // 4
+        dx = (ax - inp) // 4
     for l in range(L - 1):
         h = acts.h[l]
         H = sizes[l + 1]
+        dy = (aacts.h[l].data_ptr() - h.data_ptr()) // 4 if pair else 0
         ops.linear_fwd(inp, False, ld_in, net.W(l, store), net.b(l, store), h.data_ptr() + 4 * r0 * H,
                        C, n, sizes[l], H, relu=True, ldy=H, sxb=sxb_ if l == 0 else R * ld_in,
-                       syb=R * H)
+                       syb=R * H, pair=(dx, dW, dy) if pair else None)
         inp, ld_in = h.data_ptr() + 4 * r0 * H, H
+        dx = dy
     out_dim = sizes[-1]
     Hl = sizes[-2]
+    dout = (aacts.out.data_ptr() - acts.out.data_ptr()) // 4 if pair else 0
     if out_dim == 1:
         ops.rowdot(inp, R * Hl if L > 1 else sxb_, ld_in, net.W(L - 1, store), Hl,
-                   net.b(L - 1, store), 1, acts.out.data_ptr() + 4 * r0, R, C, n, Hl)
+                   net.b(L - 1, store), 1, acts.out.data_ptr() + 4 * r0, R, C, n, Hl,
+                   pair=(dx, dW, dW, dout) if pair else None)
     else:
         ops.linear_fwd(inp, False, ld_in, net.W(L - 1, store), net.b(L - 1, store),
                        acts.out.data_ptr() + 4 * r0 * out_dim, C, n, Hl, out_dim, relu=False,
-                       ldy=out_dim, sxb=R * Hl if L > 1 else sxb_, syb=R * out_dim)
-    if aux is not None:
+                       ldy=out_dim, sxb=R * Hl if L > 1 else sxb_, syb=R * out_dim,
+                       pair=(dx, dW, dout) if pair else None)
+    if aux is not None and not pair:
         forward(net, aux[0], aux[1], True, aux[2], aux[3], keep_h=False)
 
 

@@ -42,8 +42,10 @@ def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
          mask: Optional[int] = None, sM: Sequence[int] = (0, 0, 0),
          relu: bool = False, accumulate: bool = False, splits: int = 1, sCs: int = 0,
          alpha: float = 1.0, rowsum: Optional[int] = None, sR: Sequence[int] = (0, 0),
-         variant: int = -1) -> None:
-    """C_b,s(m,n) = epi(alpha * sum_k A_b(m,k) B_b(k,n)); strides (batch, row, col)."""
+         variant: int = -1, pair: Optional[Sequence[int]] = None) -> None:
+    """C_b,s(m,n) = epi(alpha * sum_k A_b(m,k) B_b(k,n)); strides (batch, row, col).
+    ``pair = (dA, dB, dC, dbias)``: a second pass of the same shape at those
+    element offsets in the same launch (d3a_gemm_desc.batch2 = 2)."""
     d = N.GemmDesc()
     d.A, d.B, d.C, d.bias, d.mask = A, B, Cp, bias, mask
     d.rowsum = rowsum
@@ -57,6 +59,9 @@ def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
     d.sMb, d.sMm, d.sMn = sM
     d.splits, d.sCs = splits, sCs
     d.alpha, d.relu, d.accumulate = alpha, int(relu), int(accumulate)
+    if pair is not None:
+        d.batch2 = 2
+        d.sAb2, d.sBb2, d.sCb2, d.sbias_b2 = pair
     if _TRACE:
         print(f"gemm M={M} N={Nn} K={K} batch={batch} splits={splits} sA={tuple(sA)} "
               f"sB={tuple(sB)} sC={tuple(sC)} mask={mask is not None} relu={relu} "
@@ -65,9 +70,15 @@ def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
 
 
 def rowdot(X: int, sXb: int, sXr: int, w: int, swb: int, bias: Optional[int], sbb: int,
-           out: int, sOb: int, batch: int, rows: int, n: int) -> None:
-    N.check(N.lib().d3a_rowdot_f32(X, sXb, sXr, w, swb, bias, sbb, out, sOb, batch, rows, n,
-                                   _stream()), "d3a_rowdot_f32")
+           out: int, sOb: int, batch: int, rows: int, n: int,
+           pair: Optional[Sequence[int]] = None) -> None:
+    """``pair = (dX, dw, dbias, dout)``: a second pass at those element offsets."""
+    if pair is None:
+        N.check(N.lib().d3a_rowdot_f32(X, sXb, sXr, w, swb, bias, sbb, out, sOb, batch, rows, n,
+                                       _stream()), "d3a_rowdot_f32")
+        return
+    N.check(N.lib().d3a_rowdot2_f32(X, sXb, sXr, w, swb, bias, sbb, out, sOb, batch, rows, n, 2,
+                                    *pair, _stream()), "d3a_rowdot2_f32")
 
 
 def colreduce(X: int, sXb: int, sXr: int, w: Optional[int], swb: int, out: int, sOb: int,
@@ -145,13 +156,17 @@ def call_desc(fn_name: str, desc: C.Structure) -> None:
 # ---------------------------------------------------------------------------
 def linear_fwd(x: int, x_shared: bool, ldx: int, W: int, b: int, y: int, C_: int, R: int,
                n_in: int, n_out: int, relu: bool, ldy: Optional[int] = None,
-               sxb: Optional[int] = None, syb: Optional[int] = None, variant: int = -1) -> None:
-    """y[c] = act(x[c] @ W[c]^T + b[c]); x rows have stride ldx; y is [C][R][n_out]."""
+               sxb: Optional[int] = None, syb: Optional[int] = None, variant: int = -1,
+               pair: Optional[Sequence[int]] = None) -> None:
+    """y[c] = act(x[c] @ W[c]^T + b[c]); x rows have stride ldx; y is [C][R][n_out].
+    ``pair = (dx, dW, dy)`` element offsets of a second pass of the same shape
+    (its bias at b + dW) in the same launch."""
     ldy = n_out if ldy is None else ldy
     sxb = (0 if x_shared else R * ldx) if sxb is None else sxb
     syb = R * ldy if syb is None else syb
     gemm(x, W, y, R, n_out, n_in, batch=C_, sA=(sxb, ldx, 1), sB=(n_out * n_in, 1, n_in),
-         sC=(syb, ldy, 1), bias=b, sbias=n_out, relu=relu, variant=variant)
+         sC=(syb, ldy, 1), bias=b, sbias=n_out, relu=relu, variant=variant,
+         pair=None if pair is None else (pair[0], pair[1], pair[2], pair[1]))
 
 
 def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: int, C_: int,

@@ -69,6 +69,12 @@ typedef struct d3a_gemm_desc {
   int32_t relu;
   int32_t accumulate;
   int32_t variant;    /* tile configuration, -1 = automatic */
+  /* Optional second batch dimension t < batch2 (0 or 1 = none): operands of
+   * (b, t) at A + b*sAb + t*sAb2, B + b*sBb + t*sBb2, C + b*sCb + t*sCb2,
+   * bias + b*sbias_b + t*sbias_b2, mask + b*sMb + t*sMb2 -- an independent
+   * pass of the same shape in the same launch (the target networks beside
+   * the online ones, DDPGBaseImpl._targ_q_func).  Not with rowsum. */
+  int64_t batch2, sAb2, sBb2, sCb2, sbias_b2, sMb2;
 } d3a_gemm_desc;
 int d3a_gemm_f32(const d3a_gemm_desc* desc, void* stream);
 
@@ -78,6 +84,12 @@ int d3a_rowdot_f32(const float* X, int64_t sXb, int64_t sXr, const float* w,
                    int64_t swb, const float* bias, int64_t sbb, float* out,
                    int64_t sOb, int64_t batch, int64_t rows, int64_t n,
                    void* stream);
+/* the same over a second batch dimension t < batch2, offsets t * (dX, dw,
+ * dbias, dout) on top of the above (an independent pass of the same shape) */
+int d3a_rowdot2_f32(const float* X, int64_t sXb, int64_t sXr, const float* w,
+                    int64_t swb, const float* bias, int64_t sbb, float* out,
+                    int64_t sOb, int64_t batch, int64_t rows, int64_t n, int64_t batch2,
+                    int64_t dX, int64_t dw, int64_t dbias, int64_t dout, void* stream);
 
 /* out[b*sOb + s*sOs + j] = sum_{r in split s} (w ? w[b*swb + r] : 1) *
  *                          X[b*sXb + r*sXr + j]

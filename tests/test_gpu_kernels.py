@@ -351,6 +351,45 @@ def test_fused_mlp_forward_aux_pass(dev, R, n_aux, bm, monkeypatch):
             assert _rel_err(a_.out[c].reshape(rows, 1), a) < 2e-6, (rows, c)
 
 
+@pytest.mark.parametrize("R,J,C", [(256, 1, 2), (100, 1, 2), (256, 6, 1), (64, 200, 2)])
+def test_per_layer_mlp_forward_aux_pair(dev, R, J, C, monkeypatch):
+    """Per-layer forward with an aux pass of the same shape: every layer's GEMM
+    (and the row-dot head) carries it as a second batch dimension
+    (d3a_gemm_desc.batch2, d3a_rowdot2_f32).  Both passes against fp64 torch
+    (2e-6 relative), and bit-identical to the two passes run separately."""
+    from d3rlpy_amd import mlp
+    from d3rlpy_amd.nets import EnsembleMLP, ParamStore
+    monkeypatch.setattr(mlp, "_FUSED", False)
+    g = torch.Generator().manual_seed(R + J)
+    K0, H, L = 14, 256, 2
+    st = ParamStore()
+    net = EnsembleMLP(st, "m", C, [K0] + [H] * L + [J])
+    st.allocate(dev)
+    targ = st.like()
+    with torch.no_grad():
+        st.data.copy_(torch.randn(st.data.numel(), generator=g) * 0.1)
+        targ.data.copy_(torch.randn(st.data.numel(), generator=g) * 0.1)
+    ldx = 16
+    x = torch.randn(1, R, ldx, generator=g).to(dev)
+    x2 = torch.randn(1, R, ldx, generator=g).to(dev)
+    acts, acts2 = mlp.Acts.alloc(net, R, dev), mlp.Acts.alloc(net, R, dev)
+    mlp.forward(net, st, x.data_ptr(), True, ldx, acts, aux=(targ, x2.data_ptr(), ldx, acts2))
+    s1, s2 = mlp.Acts.alloc(net, R, dev), mlp.Acts.alloc(net, R, dev)
+    mlp.forward(net, st, x.data_ptr(), True, ldx, s1)
+    mlp.forward(net, targ, x2.data_ptr(), True, ldx, s2)
+    torch.cuda.synchronize()
+    for store, xx, a_, ref in ((st, x, acts, s1), (targ, x2, acts2, s2)):
+        for c in range(C):
+            a = xx[0, :, :K0].double()
+            for l in range(L + 1):
+                W, b = net.export_linear(l, c, store)
+                a = a @ W.double().T + b.double()
+                if l < L:
+                    a = a.clamp_min(0)
+            assert _rel_err(a_.out[c].reshape(R, J), a) < 2e-6, c
+        assert torch.equal(a_.out, ref.out)
+
+
 @pytest.mark.parametrize("C,R,r0,n,K0,H,L,J,mode", [
     (2, 15616, 7680, 7936, 14, 256, 2, 1, "gscale"),  # K2 critic backward (IS rows scaled)
     (2, 256, 0, 256, 14, 256, 2, 1, "qmin"),          # actor: argmin critic, dQ/dx only
