@@ -112,14 +112,15 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
 }
 
 // Adam on a single scalar parameter (torch single-tensor path); returns new p.
+// bc = {1 - b1^t, 1 - b2^t} for t = *step + 1 (precomputed, see adam_bias_corrections).
 __device__ float adam_scalar(float* p, float* m, float* v, int64_t* step, float g, double lr,
-                             double b1, double b2, double eps) {
+                             double b1, double b2, double eps, const double* bc) {
   const int64_t t = *step + 1;
   float mm = fmaf((float)(1.0 - b1), __fsub_rn(g, *m), *m);
   float vv = __fmul_rn(*v, (float)b2);
   vv = __fadd_rn(vv, __fmul_rn(__fmul_rn((float)(1.0 - b2), g), g));
-  const double bc1 = 1.0 - pow(b1, (double)t);
-  const double bc2 = 1.0 - pow(b2, (double)t);
+  const double bc1 = bc[0];
+  const double bc2 = bc[1];
   const float step_size = (float)(lr / bc1);
   const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vv), (float)sqrt(bc2)), (float)eps);
   const float pn = __fadd_rn(*p, __fmul_rn(-step_size, __fdiv_rn(mm, denom)));
@@ -182,6 +183,21 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   // continue with the critic.
   const int phase = d.dp_phase;
 
+  // Adam bias corrections 1 - beta^t of the temperature and alpha steps (fp64
+  // pow, as torch computes them in Python floats), one per wave so the four
+  // library pows run concurrently instead of in thread 0's serial path
+  __shared__ double s_bc[4];
+  {
+    const bool apply = phase != 1;
+    const int w = tid >> 6;
+    if ((tid & 63) == 0 && w < 4 && apply &&
+        (w < 2 ? d.update_temp : d.update_alpha)) {
+      const int64_t t = (w < 2 ? *d.temp_step : *d.alpha_step) + 1;
+      s_bc[w] = 1.0 - pow((w & 1) ? d.beta2 : d.beta1, (double)t);
+    }
+    __syncthreads();
+  }
+
   // ---- update_temp (sac_impl.py:123-146) ----
   if (d.update_temp) {
     float tsum = 0.f;
@@ -203,7 +219,7 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
       } else {
         if (phase == 2) g = d.scalar_grads[0] * d.grad_scale;
         const float ln = adam_scalar(d.log_temp, d.temp_m, d.temp_v, d.temp_step, g, d.temp_lr,
-                                     d.beta1, d.beta2, d.adam_eps);
+                                     d.beta1, d.beta2, d.adam_eps, s_bc);
         d.metrics[1] = expf(ln);
       }
     }
@@ -240,7 +256,7 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
       } else {
         if (phase == 2) g = d.scalar_grads[1] * d.grad_scale;
         const float ln = adam_scalar(d.log_alpha, d.alpha_m, d.alpha_v, d.alpha_step, g,
-                                     d.alpha_lr, d.beta1, d.beta2, d.adam_eps);
+                                     d.alpha_lr, d.beta1, d.beta2, d.adam_eps, s_bc + 2);
         d.metrics[3] = expf(ln);
       }
     }
