@@ -312,7 +312,8 @@ def main():
         except Exception:
             traffic = None
     cpu = None
-    if not args.no_cpu_baseline:
+    # the CPU baseline is a rank-0, single-GPU-run measurement (not repeated per N)
+    if not args.no_cpu_baseline and ws == 1:
         threads = min(16, os.cpu_count() or 1)
         sps, k, el = cpu_baseline(args.cpu_seconds, threads, args.algo)
         what = {"cql": "CQL update (torch CPU, op-for-op restatement of cql_impl.py/"
