@@ -65,28 +65,34 @@ __global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
       t = (int64_t)(x % (uint64_t)d.n_trans);
       d.idx_out[b] = t;
     }
+    // every table entry of transition t is requested at once (one memory
+    // round trip instead of one per field)
+    const int64_t row_t = d.t_row[t], last_t = d.t_ep_last[t], ep_t = d.t_ep_start[t];
+    const uint8_t term_t = d.t_terminal[t];
     // n-step return (dataset.pyx:1323-1330)
     float ret = 0.f;
-    int64_t nt_i = t;
+    int64_t nt_i = t, row_i = row_t, last_i = last_t;
     int k = 0;
     for (k = 0; k < d.n_steps; ++k) {
       // n_step_return += reward * gamma ** i   (dataset.pyx:1325); gamma**i is
       // evaluated as the fp32 rounding of the fp64 power, then one fp32
       // multiply and one fp32 add (no contraction), matching oracle/gather.py
-      const float gp = (float)pow((double)d.gamma, (double)k);
-      ret = __fadd_rn(ret, __fmul_rn(d.rew[d.t_row[nt_i]], gp));
-      if (nt_i == d.t_ep_last[nt_i] || k == d.n_steps - 1) break;
+      const float gp = k == 0 ? 1.f : (float)pow((double)d.gamma, (double)k);
+      ret = __fadd_rn(ret, __fmul_rn(d.rew[row_i], gp));
+      if (nt_i == last_i || k == d.n_steps - 1) break;
       nt_i += 1;
+      row_i = d.t_row[nt_i];
+      last_i = d.t_ep_last[nt_i];
     }
     d.o_rew[b] = ret;
-    const bool term = d.t_terminal[nt_i] != 0;
+    const bool term = (nt_i == t ? term_t : d.t_terminal[nt_i]) != 0;
     d.o_term[b] = term ? 1.f : 0.f;
     d.o_n_steps[b] = (float)(k + 1);
     meta.t = t;
-    meta.row = d.t_row[t];
-    meta.ep_start = d.t_ep_start[t];
+    meta.row = row_t;
+    meta.ep_start = ep_t;
     meta.next_t = nt_i;
-    meta.next_row = term ? -1 : d.t_row[nt_i] + 1;
+    meta.next_row = term ? -1 : row_i + 1;
     // actions
     if (d.act_i) d.o_act_i[b] = d.act_i[meta.row];
   }
