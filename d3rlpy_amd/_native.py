@@ -78,6 +78,8 @@ class CqlSampleDesc(C.Structure):
         ("ldx", C.c_int32),
         ("min_logstd", C.c_float), ("max_logstd", C.c_float),
         ("eps_targ", vp), ("logp_targ", vp), ("soft_target", C.c_int32),
+        ("noise_base", vp), ("rng_ctr", vp), ("eps_actor_out", vp), ("seed", C.c_uint64),
+        ("n_normal", C.c_int64), ("gen_noise", C.c_int32),
     ]
 
 

@@ -421,8 +421,9 @@ class _Workspace:
         self.eps_actor = self.noise[o:o + B * A]; o += B * A
         self.eps_targ = self.noise[o:o + nt]; o += nt
         self.u_rand = self.noise[o:o + 2 * NB * A]
-        self.rng_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.rng_ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        # Philox counter of the step's draws (d3a_cql_sample draws them; the
+        # step-end kernel advances it as counter slot 4)
+        self.rng_ctr = impl.counters[4:5]
         self.seed = int(torch.randint(0, 2**62, (1,)).item())
         # policy forward on 2B rows
         self.pacts = mlp.Acts.alloc(impl.policy, 2 * B, dev)
@@ -491,6 +492,8 @@ class _Workspace:
         s.ldx = self.LDX
         s.min_logstd, s.max_logstd = impl._min_logstd, impl._max_logstd
         s.soft_target = int(self.soft)
+        s.noise_base, s.rng_ctr = self.noise.data_ptr(), self.rng_ctr.data_ptr()
+        s.eps_actor_out, s.seed, s.n_normal = self.eps_actor.data_ptr(), self.seed, self.n_normal
         if self.soft:
             s.eps_targ, s.logp_targ = self.eps_targ.data_ptr(), self.logp_targ.data_ptr()
         self.sample_desc = s
@@ -635,12 +638,13 @@ class _Workspace:
         impl = self.impl
         B, D, A, C, N, NB, R = self.B, self.D, self.A, self.C, self.N, self.NB, self.R
         DA = self.LDX  # row stride of the (padded) Q-input matrices
-        if not self._external_noise:
-            ops.philox_fill(self.noise, self.n_normal, self.n_uniform, -1.0, 1.0, self.seed,
-                            self.rng_ctr, self.rng_ticket)
+        sampled = temp or alpha or critic or actor
+        # the sample stage draws the step's noise itself unless it was injected
+        self.sample_desc.gen_noise = int(not self._external_noise)
+        self.sample_desc.seed = self.seed
         if impl._scaler is not None:
             ops.standardize(self.obs2, self.xobs2, self.sc_mean, self.sc_std, self.sc_eps)
-        if temp or alpha or critic or actor:
+        if sampled:
             # 1. policy on [obs; next_obs]
             mlp.forward(impl.policy, impl.store, self.xobs2.data_ptr(), True, D, self.pacts)
             # 2. samples and Q inputs
@@ -698,7 +702,8 @@ class _Workspace:
         # 7. soft update of both targets + metric ring + optimiser step counters
         if dp is not None:
             dp.all_reduce_sum(self.metrics)  # logged losses: mean over ranks
-        ops.step_end(impl.counters, (1 if critic else 0) | (2 if actor else 0), self.metrics,
+        rng = 16 if sampled and not self._external_noise else 0  # counters[4] += 1
+        ops.step_end(impl.counters, (1 if critic else 0) | (2 if actor else 0) | rng, self.metrics,
                      self.ring, self.ring_ctr, impl.targ.data if targets else None,
                      impl.store.data if targets else None, impl._tau,
                      metric_scale=1.0 if dp is None else dp.scale)

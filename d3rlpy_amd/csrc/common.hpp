@@ -100,4 +100,22 @@ __device__ __forceinline__ float u01(uint32_t x) {
   return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
 }
 
+// Element e of the d3a_philox_fill stream (seed, counter ctr): elements
+// [0, n_normal) standard normal (Box-Muller over the 4 words of Philox call
+// e / 4), the rest uniform in [lo, hi) -- bit-identical to what
+// d3a_philox_fill writes at out[e], so a consumer can draw its own values.
+__device__ __forceinline__ float philox_elem(uint64_t seed, uint64_t ctr, int64_t e,
+                                             int64_t n_normal, float lo, float hi) {
+  uint32_t r[4];
+  Philox::gen(seed, ctr, (uint64_t)(e >> 2), r);
+  const int q = (int)(e & 3);
+  if (e < n_normal) {
+    const int p = q & ~1;
+    const float u1 = u01(r[p]), u2 = u01(r[p + 1]);
+    const float rad = sqrtf(-2.f * logf(u1));
+    return (q & 1) ? rad * sinf(6.283185307179586f * u2) : rad * cosf(6.283185307179586f * u2);
+  }
+  return lo + (hi - lo) * (u01(r[q]) - 0x1p-24f);
+}
+
 }  // namespace d3a

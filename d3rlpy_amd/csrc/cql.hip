@@ -50,7 +50,15 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const int64_t H = 2 * A;                 // head row width
-  float act[16];
+  float act[16], ev[16];
+  // the step's noise: drawn here from the Philox stream (gen_noise) or read
+  // from the buffers the caller filled (parity mode)
+  const uint64_t ctr = d.gen_noise ? (uint64_t)*d.rng_ctr : 0;
+  auto noise = [&](const float* p, int n, float* out) {
+    for (int j = 0; j < n; ++j)
+      out[j] = d.gen_noise ? philox_elem(d.seed, ctr, (p + j) - d.noise_base, d.n_normal, -1.f, 1.f)
+                           : p[j];
+  };
 
   if (i < 6 * NB) {
     const int64_t s = i / (3 * NB);        // 0 = alpha set, 1 = critic set
@@ -64,14 +72,14 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
     if (blk < 2) {
       // policy rows: head row b (obs) or B + b (next_obs); noise [s][blk][n][b]
       const float* hrow = d.head + (blk * B + b) * H;
-      const float* e = d.eps_pi + (((s * 2 + blk) * N + n) * B + b) * A;
-      const float lp = squashed_sample(hrow, hrow + A, e, (int)A, d.min_logstd, d.max_logstd,
+      noise(d.eps_pi + (((s * 2 + blk) * N + n) * B + b) * A, (int)A, ev);
+      const float lp = squashed_sample(hrow, hrow + A, ev, (int)A, d.min_logstd, d.max_logstd,
                                        act, nullptr);
       d.logp_is[(s * 2 + blk) * NB + r] = lp;
       for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
     } else {
-      const float* u = d.u_rand + (s * NB + r) * A;
-      for (int64_t j = 0; j < A; ++j) x[D + j] = u[j];
+      noise(d.u_rand + (s * NB + r) * A, (int)A, ev);
+      for (int64_t j = 0; j < A; ++j) x[D + j] = ev[j];
     }
   } else if (i < R) {
     // data rows (obs_t, a_t)
@@ -83,8 +91,9 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
     // update_temp sample: log-prob only
     const int64_t b = i - R;
     const float* hrow = d.head + b * H;
-    d.logp_temp[b] = squashed_sample(hrow, hrow + A, d.eps_temp + b * A, (int)A, d.min_logstd,
-                                     d.max_logstd, nullptr, nullptr);
+    noise(d.eps_temp + b * A, (int)A, ev);
+    d.logp_temp[b] = squashed_sample(hrow, hrow + A, ev, (int)A, d.min_logstd, d.max_logstd,
+                                     nullptr, nullptr);
   } else if (i < R + 2 * B) {
     const int64_t b = i - R - B;
     const float* hrow = d.head + (B + b) * H;
@@ -92,8 +101,9 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
     for (int64_t j = 0; j < D; ++j) x[j] = d.next_obs[b * D + j];
     if (d.soft_target) {
       // SACImpl.compute_target: policy.sample_with_log_prob(next_obs)
-      d.logp_targ[b] = squashed_sample(hrow, hrow + A, d.eps_targ + b * A, (int)A, d.min_logstd,
-                                       d.max_logstd, act, nullptr);
+      noise(d.eps_targ + b * A, (int)A, ev);
+      d.logp_targ[b] = squashed_sample(hrow, hrow + A, ev, (int)A, d.min_logstd, d.max_logstd,
+                                       act, nullptr);
       for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
     } else {
       // deterministic target action tanh(mu(s_t+1)) (NormalPolicy.best_action)
@@ -105,8 +115,12 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
     const float* hrow = d.head + b * H;
     float* x = d.x_actor + b * DA;
     for (int64_t j = 0; j < D; ++j) x[j] = d.obs[b * D + j];
-    d.actor_logp[b] = squashed_sample(hrow, hrow + A, d.eps_actor + b * A, (int)A, d.min_logstd,
-                                      d.max_logstd, act, d.actor_u + b * A);
+    noise(d.eps_actor + b * A, (int)A, ev);
+    // the actor head (d3a_sac_actor_head) reads these draws again
+    if (d.gen_noise)
+      for (int64_t j = 0; j < A; ++j) d.eps_actor_out[b * A + j] = ev[j];
+    d.actor_logp[b] = squashed_sample(hrow, hrow + A, ev, (int)A, d.min_logstd, d.max_logstd,
+                                      act, d.actor_u + b * A);
     for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
   }
 }
@@ -407,6 +421,8 @@ extern "C" int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream) {
   D3A_CHECK_ARG(!d->soft_target || (d->eps_targ && d->logp_targ),
                 "d3a_cql_sample: soft_target needs eps_targ and logp_targ");
   D3A_CHECK_ARG(d->ldx >= d->D + d->A, "d3a_cql_sample: ldx < D + A");
+  D3A_CHECK_ARG(!d->gen_noise || (d->noise_base && d->rng_ctr && d->eps_actor_out),
+                "d3a_cql_sample: gen_noise needs noise_base, rng_ctr and eps_actor_out");
   const int64_t total = 6LL * d->N * d->B + 4LL * d->B;
   hipLaunchKernelGGL(cql_sample_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, *d);

@@ -255,24 +255,9 @@ __global__ __launch_bounds__(256) void philox_kernel(float* out, int64_t n_norma
   const int64_t total = n_normal + n_uniform;
   const int64_t e0 = g * 4;
   if (e0 < total) {
-    uint32_t r[4];
-    Philox::gen(seed, (uint64_t)step, (uint64_t)g, r);
-    float v[4];
-    // Box-Muller pairs
-    {
-      const float u1 = u01(r[0]), u2 = u01(r[1]);
-      const float rad = sqrtf(-2.f * logf(u1));
-      v[0] = rad * cosf(6.283185307179586f * u2);
-      v[1] = rad * sinf(6.283185307179586f * u2);
-      const float u3 = u01(r[2]), u4 = u01(r[3]);
-      const float rad2 = sqrtf(-2.f * logf(u3));
-      v[2] = rad2 * cosf(6.283185307179586f * u4);
-      v[3] = rad2 * sinf(6.283185307179586f * u4);
-    }
     for (int q = 0; q < 4; ++q) {
       const int64_t e = e0 + q;
-      if (e < n_normal) out[e] = v[q];
-      else if (e < total) out[e] = lo + (hi - lo) * (u01(r[q]) - 0x1p-24f);
+      if (e < total) out[e] = philox_elem(seed, (uint64_t)step, e, n_normal, lo, hi);
     }
   }
   __syncthreads();

@@ -311,6 +311,17 @@ typedef struct d3a_cql_sample_desc {
   const float* eps_targ;
   float* logp_targ;
   int32_t soft_target;
+  /* gen_noise != 0: the draws are not read from eps_* / u_rand but computed
+   * here as the elements (pointer - noise_base) of the d3a_philox_fill stream
+   * (seed, *rng_ctr; the first n_normal normal, the rest uniform in [-1, 1)),
+   * bit-identical to filling the buffer first; the actor draws are written
+   * to eps_actor_out for d3a_sac_actor_head.  The caller advances *rng_ctr. */
+  const float* noise_base;
+  const int64_t* rng_ctr;
+  float* eps_actor_out;
+  uint64_t seed;
+  int64_t n_normal;
+  int32_t gen_noise;
 } d3a_cql_sample_desc;
 int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream);
 

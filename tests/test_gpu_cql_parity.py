@@ -248,3 +248,30 @@ def test_cql_grad_accuracy_vs_fp64():
                 print(f"critic {c} {nm}: hip-vs-fp64 {e_hip:.1e}  oracle32-vs-fp64 {e_orc:.1e}")
                 worst_hip, worst_orc = max(worst_hip, e_hip), max(worst_orc, e_orc)
     assert worst_hip <= 1e-5, (worst_hip, worst_orc)
+
+
+def test_cql_sample_draws_equal_philox_fill():
+    """d3a_cql_sample drawing its own noise (the default) is bit-identical to
+    filling the noise buffer with d3a_philox_fill (same seed and counter)
+    and reading it: sampled Q-input rows, log-probs and the actor draws."""
+    from d3rlpy_amd import mlp, ops
+    D, A, H, N, B = 11, 3, [64, 64], 10, 256
+    impl = make_impl(D, A, H, N)
+    ws = impl._workspace(B)
+    arrs = make_batch(np.random.RandomState(2), B, D, A)
+    from d3rlpy_amd.algos.impl_base import as_device_batch
+    ws.stage(as_device_batch(HostBatch(*arrs), impl.torch_device), None)
+    impl.counters[4] = 7
+    mlp.forward(impl.policy, impl.store, ws.xobs2.data_ptr(), True, D, ws.pacts)
+    ws.sample_desc.gen_noise = 1
+    ops.call_desc("d3a_cql_sample", ws.sample_desc)
+    got = [t.clone() for t in (ws.x_q, ws.logp_is, ws.logp_temp, ws.actor_logp, ws.eps_actor)]
+    ws.noise.zero_()
+    ctr = torch.full((1,), 7, dtype=torch.int64, device="cuda")
+    ticket = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ops.philox_fill(ws.noise, ws.n_normal, ws.n_uniform, -1.0, 1.0, ws.seed, ctr, ticket)
+    ws.sample_desc.gen_noise = 0
+    ops.call_desc("d3a_cql_sample", ws.sample_desc)
+    torch.cuda.synchronize()
+    for a, b in zip(got, (ws.x_q, ws.logp_is, ws.logp_temp, ws.actor_logp, ws.eps_actor)):
+        assert torch.equal(a, b)
