@@ -335,7 +335,8 @@ _SIGNATURES = {
     "d3a_rowdot_f32": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
                                  C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
     "d3a_rowdot2_f32": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
-                                  C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                  C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int32,
+                                  C.c_int64,
                                   C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
     "d3a_colreduce_f32": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64,
                                     C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),

@@ -20,10 +20,12 @@ void set_error(const char* fmt, ...) {
 namespace {
 
 // ---- rowdot: one wave per row, 4 floats per lane per step -------------------
+// out[r][j] = x[r] . w[j] + bias[j] for the J (<= 16) outputs of a narrow head;
+// w is [J][n] (nn.Linear layout), out rows have stride J.
 __global__ __launch_bounds__(256) void rowdot_kernel(const float* X, int64_t sXb, int64_t sXr,
                                                      const float* w, int64_t swb,
                                                      const float* bias, int64_t sbb, float* out,
-                                                     int64_t sOb, int64_t rows, int64_t n,
+                                                     int64_t sOb, int64_t rows, int64_t n, int J,
                                                      int64_t dX, int64_t dw, int64_t dbias,
                                                      int64_t dout) {
   const int lane = threadIdx.x & 63;
@@ -34,20 +36,37 @@ __global__ __launch_bounds__(256) void rowdot_kernel(const float* X, int64_t sXb
   const float* wb = w + b * swb + t * dw;
   out += t * dout;
   if (bias) bias += t * dbias;
-  float acc = 0.f;
+  float acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
   const bool vec = ((n & 3) == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0) &&
                    ((reinterpret_cast<uintptr_t>(wb) & 15) == 0);
   if (vec) {
-    for (int64_t j = (int64_t)lane * 4; j < n; j += 256) {
-      const float4 a = *reinterpret_cast<const float4*>(x + j);
-      const float4 c = *reinterpret_cast<const float4*>(wb + j);
-      acc = fmaf(a.w, c.w, fmaf(a.z, c.z, fmaf(a.y, c.y, fmaf(a.x, c.x, acc))));
+    for (int64_t k = (int64_t)lane * 4; k < n; k += 256) {
+      const float4 a = *reinterpret_cast<const float4*>(x + k);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (j >= J) break;
+        const float4 c = *reinterpret_cast<const float4*>(wb + j * n + k);
+        acc[j] = fmaf(a.w, c.w, fmaf(a.z, c.z, fmaf(a.y, c.y, fmaf(a.x, c.x, acc[j]))));
+      }
     }
   } else {
-    for (int64_t j = lane; j < n; j += 64) acc = fmaf(x[j], wb[j], acc);
+    for (int64_t k = lane; k < n; k += 64) {
+      const float a = x[k];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (j >= J) break;
+        acc[j] = fmaf(a, wb[j * n + k], acc[j]);
+      }
+    }
   }
-  acc = wave_sum(acc);
-  if (lane == 0) out[b * sOb + r] = acc + (bias ? bias[b * sbb] : 0.f);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (j >= J) break;
+    const float v = wave_sum(acc[j]);
+    if (lane == 0) out[b * sOb + r * J + j] = v + (bias ? bias[b * sbb + j] : 0.f);
+  }
 }
 
 // ---- colreduce: column tile of TW columns x RL row lanes per 256-thread block
@@ -332,21 +351,22 @@ extern "C" int d3a_rowdot_f32(const float* X, int64_t sXb, int64_t sXr, const fl
                               int64_t swb, const float* bias, int64_t sbb, float* out,
                               int64_t sOb, int64_t batch, int64_t rows, int64_t n,
                               void* stream) {
-  return d3a_rowdot2_f32(X, sXb, sXr, w, swb, bias, sbb, out, sOb, batch, rows, n, 1, 0, 0, 0, 0,
-                         stream);
+  return d3a_rowdot2_f32(X, sXb, sXr, w, swb, bias, sbb, out, sOb, batch, rows, n, 1, 1, 0, 0, 0,
+                         0, stream);
 }
 
 extern "C" int d3a_rowdot2_f32(const float* X, int64_t sXb, int64_t sXr, const float* w,
                                int64_t swb, const float* bias, int64_t sbb, float* out,
-                               int64_t sOb, int64_t batch, int64_t rows, int64_t n,
+                               int64_t sOb, int64_t batch, int64_t rows, int64_t n, int32_t J,
                                int64_t batch2, int64_t dX, int64_t dw, int64_t dbias,
                                int64_t dout, void* stream) {
   D3A_CHECK_ARG(X && w && out, "d3a_rowdot_f32: null pointer");
   D3A_CHECK_ARG(batch2 >= 1, "d3a_rowdot2_f32: batch2 >= 1");
+  D3A_CHECK_ARG(J >= 1 && J <= 16, "d3a_rowdot2_f32: 1 <= J <= 16");
   if (batch <= 0 || rows <= 0) return 0;
   dim3 grid((unsigned)((rows + 3) / 4), (unsigned)batch, (unsigned)batch2);
   hipLaunchKernelGGL(rowdot_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, sXb, sXr, w, swb,
-                     bias, sbb, out, sOb, rows, n, dX, dw, dbias, dout);
+                     bias, sbb, out, sOb, rows, n, (int)J, dX, dw, dbias, dout);
   D3A_LAUNCH_CHECK("d3a_rowdot2_f32");
   return 0;
 }

@@ -154,10 +154,12 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     out_dim = sizes[-1]
     Hl = sizes[-2]
     dout = (aacts.out.data_ptr() - acts.out.data_ptr()) // 4 if pair else 0
-    if out_dim == 1:
-        ops.rowdot(inp, R * Hl if L > 1 else sxb_, ld_in, net.W(L - 1, store), Hl,
-                   net.b(L - 1, store), 1, acts.out.data_ptr() + 4 * r0, R, C, n, Hl,
-                   pair=(dx, dW, dW, dout) if pair else None)
+    if out_dim <= 16:
+        # narrow heads (Q values, policy mu|logstd): one wave per row beats a
+        # 32-wide MFMA tile that is mostly padding
+        ops.rowdot(inp, R * Hl if L > 1 else sxb_, ld_in, net.W(L - 1, store), Hl * out_dim,
+                   net.b(L - 1, store), out_dim, acts.out.data_ptr() + 4 * r0 * out_dim,
+                   R * out_dim, C, n, Hl, pair=(dx, dW, dW, dout) if pair else None, J=out_dim)
     else:
         ops.linear_fwd(inp, False, ld_in, net.W(L - 1, store), net.b(L - 1, store),
                        acts.out.data_ptr() + 4 * r0 * out_dim, C, n, Hl, out_dim, relu=False,

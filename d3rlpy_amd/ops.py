@@ -71,14 +71,16 @@ def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
 
 def rowdot(X: int, sXb: int, sXr: int, w: int, swb: int, bias: Optional[int], sbb: int,
            out: int, sOb: int, batch: int, rows: int, n: int,
-           pair: Optional[Sequence[int]] = None) -> None:
-    """``pair = (dX, dw, dbias, dout)``: a second pass at those element offsets."""
-    if pair is None:
+           pair: Optional[Sequence[int]] = None, J: int = 1) -> None:
+    """``J`` outputs per row (w [J][n], out rows of stride J); ``pair = (dX, dw,
+    dbias, dout)``: a second pass at those element offsets."""
+    if pair is None and J == 1:
         N.check(N.lib().d3a_rowdot_f32(X, sXb, sXr, w, swb, bias, sbb, out, sOb, batch, rows, n,
                                        _stream()), "d3a_rowdot_f32")
         return
-    N.check(N.lib().d3a_rowdot2_f32(X, sXb, sXr, w, swb, bias, sbb, out, sOb, batch, rows, n, 2,
-                                    *pair, _stream()), "d3a_rowdot2_f32")
+    p = (1, 0, 0, 0, 0) if pair is None else (2,) + tuple(pair)
+    N.check(N.lib().d3a_rowdot2_f32(X, sXb, sXr, w, swb, bias, sbb, out, sOb, batch, rows, n, J,
+                                    *p, _stream()), "d3a_rowdot2_f32")
 
 
 def colreduce(X: int, sXb: int, sXr: int, w: Optional[int], swb: int, out: int, sOb: int,

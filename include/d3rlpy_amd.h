@@ -84,12 +84,16 @@ int d3a_rowdot_f32(const float* X, int64_t sXb, int64_t sXr, const float* w,
                    int64_t swb, const float* bias, int64_t sbb, float* out,
                    int64_t sOb, int64_t batch, int64_t rows, int64_t n,
                    void* stream);
-/* the same over a second batch dimension t < batch2, offsets t * (dX, dw,
- * dbias, dout) on top of the above (an independent pass of the same shape) */
+/* the same for a narrow head of J <= 16 outputs (w [J][n], bias [J], out
+ * rows of stride J: out[b*sOb + r*J + j]; the nn.Linear heads of
+ * policies.py:57-59 / 170-176) over a second batch dimension t < batch2,
+ * offsets t * (dX, dw, dbias, dout) on top of the above (an independent pass
+ * of the same shape, e.g. the target networks) */
 int d3a_rowdot2_f32(const float* X, int64_t sXb, int64_t sXr, const float* w,
                     int64_t swb, const float* bias, int64_t sbb, float* out,
-                    int64_t sOb, int64_t batch, int64_t rows, int64_t n, int64_t batch2,
-                    int64_t dX, int64_t dw, int64_t dbias, int64_t dout, void* stream);
+                    int64_t sOb, int64_t batch, int64_t rows, int64_t n, int32_t J,
+                    int64_t batch2, int64_t dX, int64_t dw, int64_t dbias, int64_t dout,
+                    void* stream);
 
 /* out[b*sOb + s*sOs + j] = sum_{r in split s} (w ? w[b*swb + r] : 1) *
  *                          X[b*sXb + r*sXr + j]
