@@ -208,3 +208,32 @@ def test_hip_td3bc_updates_vs_fixture():
     for k, d in _td3_from_fixture(g, "final/").items():
         for n, t in d.items():
             assert float((sd[k][n].view(-1) - t.view(-1)).abs().max()) <= 1e-5, (k, n)
+
+
+@pytest.mark.gpu
+def test_round_iterator_epoch_semantics():
+    """RoundIterator (iterators/round_iterator.py:39-53): len = n // batch,
+    one epoch visits np.random.shuffle's permutation of the transitions in
+    order (global numpy RNG, as the reference), gathered bit-exactly."""
+    from d3rlpy_amd.dataset import DeviceDataset, MDPDataset
+    from d3rlpy_amd.iterators import RoundIterator
+    from oracle.gather import gather, to_episodes, to_transitions
+    g = _load("gather_small.npz")
+    ds = MDPDataset(g["obs"], g["act"], g["rew"], g["term"], episode_terminals=g["ep_term"])
+    dd = DeviceDataset(ds)
+    B = 8
+    it = RoundIterator(dd, batch_size=B, shuffle=True)
+    np.random.seed(5)
+    batches = [(b.obs.cpu().numpy().copy(), b.rew.cpu().numpy().copy()) for b in it]
+    n = len(dd)
+    assert len(it) == n // B and len(batches) == n // B
+    np.random.seed(5)
+    perm = np.arange(n)
+    np.random.shuffle(perm)
+    trans = []
+    for o, a, r, t in to_episodes(g["obs"], g["act"], g["rew"], g["term"], g["ep_term"]):
+        trans += to_transitions(o, a, r, t)
+    for k, (obs, rew) in enumerate(batches):
+        ref = gather([trans[i] for i in perm[k * B:(k + 1) * B]])
+        assert np.array_equal(obs, ref["observations"])
+        assert np.array_equal(rew, ref["rewards"].ravel())
