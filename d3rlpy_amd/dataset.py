@@ -113,6 +113,10 @@ class Episode:
     def get_action_size(self):
         return self.action_size
 
+    def compute_return(self) -> float:
+        """Undiscounted episode return (dataset.pyx:763-774)."""
+        return float(np.sum(self._rewards))
+
     def n_transitions(self) -> int:
         L = len(self._observations)
         return L if self._terminal else max(L - 1, 0)
@@ -236,6 +240,109 @@ class MDPDataset:
 
     def __iter__(self):
         return iter(self.episodes)
+
+    def __getitem__(self, index):
+        return self.episodes[index]
+
+    def build_episodes(self) -> None:
+        """Rebuild the episode view (dataset.pyx:552-566)."""
+        self._episodes = None
+        _ = self.episodes
+
+    # -- growing the dataset (dataset.pyx:424-509) ------------------------------
+    def append(self, observations, actions, rewards, terminals, episode_terminals=None):
+        """Append flat arrays; episodes are re-derived from the new terminals."""
+        observations = np.asarray(observations)
+        shape = self.get_observation_shape()
+        assert observations.shape[1:] == shape, f"Observation shape must be {shape}."
+        if self.discrete_action:
+            actions = np.asarray(actions).reshape(-1)
+            if actions.size and int(actions.max()) >= self.get_action_size():
+                import warnings
+                warnings.warn(f"New action size is higher than {self.get_action_size()}.")
+            self._actions = np.concatenate([self._actions, actions.astype(np.int32)])
+        else:
+            actions = np.asarray(actions, dtype=np.float32)
+            assert actions.shape[1:] == (self.get_action_size(),), \
+                f"Action size must be {self.get_action_size()}."
+            self._actions = np.concatenate([self._actions, actions])
+        if observations.dtype != self._observations.dtype:
+            observations = observations.astype(self._observations.dtype)
+        self._observations = np.concatenate([self._observations, observations])
+        terminals = np.asarray(terminals, dtype=np.float32).reshape(-1)
+        self._rewards = np.concatenate(
+            [self._rewards, np.asarray(rewards, dtype=np.float32).reshape(-1)])
+        self._terminals = np.concatenate([self._terminals, terminals])
+        ep_terms = terminals if episode_terminals is None else \
+            np.asarray(episode_terminals, dtype=np.float32).reshape(-1)
+        self._episode_terminals = np.concatenate([self._episode_terminals, ep_terms])
+        self._episodes = None
+
+    def extend(self, dataset: "MDPDataset") -> None:
+        """dataset.pyx:488-509."""
+        assert self.is_action_discrete() == dataset.is_action_discrete(), \
+            "Dataset must have discrete action-space."
+        assert self.get_observation_shape() == dataset.get_observation_shape(), \
+            f"Observation shape must be {self.get_observation_shape()}"
+        self.append(dataset.observations, dataset.actions, dataset.rewards,
+                    dataset.terminals, dataset.episode_terminals)
+
+    # -- statistics (dataset.pyx:330-422) ---------------------------------------
+    def compute_stats(self) -> dict:
+        """Return / reward / action / observation summaries with 20-bin histograms."""
+        def summary(x, axis=None):
+            return {"mean": np.mean(x, axis=axis), "std": np.std(x, axis=axis),
+                    "min": np.min(x, axis=axis), "max": np.max(x, axis=axis)}
+
+        returns = np.array([ep.compute_return() for ep in self.episodes])
+        stats = {"return": dict(summary(returns), histogram=np.histogram(returns, bins=20)),
+                 "reward": dict(summary(self._rewards),
+                                histogram=np.histogram(self._rewards, bins=20))}
+        n_act = self.get_action_size()
+        if self.discrete_action:
+            counts = [int(np.count_nonzero(self._actions == a)) for a in range(n_act)]
+            stats["action"] = {"histogram": [counts, np.arange(n_act)]}
+        else:
+            stats["action"] = dict(summary(self._actions, axis=0), histogram=[
+                np.histogram(self._actions[:, j], bins=20) for j in range(n_act)])
+        stats["observation"] = summary(self._observations, axis=0)
+        return stats
+
+    # -- persistence (dataset.pyx:511-550) --------------------------------------
+    _FIELDS = ("observations", "actions", "rewards", "terminals", "episode_terminals")
+
+    def dump(self, fname: str) -> None:
+        """HDF5 (same dataset names as the reference) when h5py is importable and
+        the name ends in .h5/.hdf5; otherwise an uncompressed .npz with the same keys."""
+        arrays = {k: getattr(self, "_" + k) for k in self._FIELDS}
+        if str(fname).endswith((".h5", ".hdf5")):
+            try:
+                import h5py
+            except ImportError as e:
+                raise ImportError("h5py is required for .h5 files; use a .npz name") from e
+            with h5py.File(fname, "w") as f:
+                for k, v in arrays.items():
+                    f.create_dataset(k, data=v)
+                f.create_dataset("discrete_action", data=self.discrete_action)
+                f.create_dataset("version", data="1.0")
+            return
+        with open(fname, "wb") as fh:
+            np.savez(fh, discrete_action=np.array(self.discrete_action),
+                     version=np.array("1.0"), **arrays)
+
+    @classmethod
+    def load(cls, fname: str) -> "MDPDataset":
+        if str(fname).endswith((".h5", ".hdf5")):
+            import h5py
+            with h5py.File(fname, "r") as f:
+                data = {k: f[k][()] for k in cls._FIELDS if k in f}
+                discrete = bool(f["discrete_action"][()])
+        else:
+            with np.load(fname, allow_pickle=False) as f:
+                data = {k: f[k] for k in cls._FIELDS if k in f.files}
+                discrete = bool(f["discrete_action"])
+        return cls(data["observations"], data["actions"], data["rewards"], data["terminals"],
+                   episode_terminals=data.get("episode_terminals"), discrete_action=discrete)
 
 
 def transition_table(bounds: Sequence[Tuple[int, int, bool]]) -> Tuple[np.ndarray, ...]:
