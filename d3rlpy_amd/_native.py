@@ -127,6 +127,7 @@ class GatherDesc(C.Structure):
         ("o_obs", vp), ("o_frames", vp), ("o_act", vp), ("o_act_i", vp),
         ("o_rew", vp), ("o_next_obs", vp), ("o_next_frames", vp),
         ("o_term", vp), ("o_n_steps", vp), ("row_offset", C.c_int64),
+        ("t_term_value", vp),
     ]
 
 

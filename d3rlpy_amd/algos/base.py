@@ -23,6 +23,38 @@ class AlgoBase(LearnableBase):
         assert self._impl is not None, IMPL_NOT_INITIALIZED_ERROR
         return self._impl.sample_action(x)
 
+    def build_with_env(self, env) -> None:
+        """algos/base.py build_with_env: shapes from the env's spaces."""
+        from ..online import get_action_size_from_env
+        self.create_impl(self._process_observation_shape(env.observation_space.shape),
+                         get_action_size_from_env(env))
+
+    def fit_online(self, env, buffer=None, explorer=None, n_steps: int = 1000000,
+                   n_steps_per_epoch: int = 10000, update_interval: int = 1,
+                   update_start_step: int = 0, random_steps: int = 0, eval_env=None,
+                   eval_epsilon: float = 0.0, save_metrics: bool = True,
+                   save_interval: int = 1, experiment_name: Optional[str] = None,
+                   with_timestamp: bool = True, logdir: str = "d3rlpy_logs",
+                   verbose: bool = True, show_progress: bool = True,
+                   tensorboard_dir: Optional[str] = None, timelimit_aware: bool = True,
+                   callback=None):
+        """algos/base.py:187-260: online training on a gym-style env (old
+        ``reset() -> obs`` / ``step(a) -> (obs, r, done, info)`` API) with the
+        HBM-resident ReplayBuffer (default maxlen 1,000,000)."""
+        from ..online import ReplayBuffer, train_single_env
+        if buffer is None:
+            buffer = ReplayBuffer(1000000, env=env)
+        return train_single_env(self, env, buffer, explorer, n_steps=n_steps,
+                                n_steps_per_epoch=n_steps_per_epoch,
+                                update_interval=update_interval,
+                                update_start_step=update_start_step,
+                                random_steps=random_steps, eval_env=eval_env,
+                                eval_epsilon=eval_epsilon, save_metrics=save_metrics,
+                                save_interval=save_interval, experiment_name=experiment_name,
+                                with_timestamp=with_timestamp, logdir=logdir, verbose=verbose,
+                                show_progress=show_progress, tensorboard_dir=tensorboard_dir,
+                                timelimit_aware=timelimit_aware, callback=callback)
+
     def save_policy(self, fname: str) -> None:
         """algos/base.py:77-103: greedy policy as TorchScript (.pt) or ONNX (.onnx)."""
         assert self._impl is not None, IMPL_NOT_INITIALIZED_ERROR

@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
     }
     d.o_rew[b] = ret;
     const bool term = (nt_i == t ? term_t : d.t_terminal[nt_i]) != 0;
-    d.o_term[b] = term ? 1.f : 0.f;
+    d.o_term[b] = d.t_term_value ? d.t_term_value[nt_i] : (term ? 1.f : 0.f);
     d.o_n_steps[b] = (float)(k + 1);
     meta.t = t;
     meta.row = row_t;

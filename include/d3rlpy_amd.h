@@ -442,6 +442,10 @@ typedef struct d3a_gather_desc {
   /* drawn indices: row b takes draw number row_offset + b of the step, so
    * data-parallel ranks slice one global index stream */
   int64_t row_offset;
+  /* optional [n_trans] terminal flag reported in o_term (NULL: t_terminal).
+   * The online ReplayBuffer needs it: its transition into the terminal state
+   * has terminal = 1 but a real next observation (online/buffers.py:268-281) */
+  const float* t_term_value;
 } d3a_gather_desc;
 int d3a_gather_batch(const d3a_gather_desc* d, void* stream);
 
