@@ -80,7 +80,9 @@ __global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
       const float gp = k == 0 ? 1.f : (float)pow((double)d.gamma, (double)k);
       ret = __fadd_rn(ret, __fmul_rn(d.rew[row_i], gp));
       if (nt_i == last_i || k == d.n_steps - 1) break;
-      nt_i += 1;
+      // successor slot; wraps at n_trans for the online replay ring (an
+      // offline table never steps past its last transition here)
+      nt_i = nt_i + 1 == d.n_trans ? 0 : nt_i + 1;
       row_i = d.t_row[nt_i];
       last_i = d.t_ep_last[nt_i];
     }

@@ -11,7 +11,8 @@ transition table handed to the gather kernel (``d3a_gather_batch``) is then
 ``t_row[s] = 2s``, ``t_ep_start[s] = 2s``, ``t_terminal[s] = 0`` (the zero
 next observation is stored), ``t_term_value[s]`` = the transition's terminal
 flag, and ``t_ep_last[s] = s`` iff the transition has no successor in the next
-slot, so the kernel's n-step walk (``nt_i += 1`` until ``nt_i == t_ep_last``)
+slot (``(s+1) % maxlen``), so the kernel's n-step walk (successor slot until
+``nt_i == t_ep_last``)
 follows the reference's ``next_transition`` links and reads the next
 observation at ``2(s+k)+1``.  Appends land in the host mirror; ``sample``
 uploads only the slots written since the previous sample, then gathers on
@@ -22,8 +23,6 @@ numpy's global RNG over raw slot indices, the reference's stream
 Differences from the reference, by construction:
 * ``n_frames > 1`` (frame stacking across the ring) is not supported:
   ``sample`` raises ``NotImplementedError``.
-* An n-step chain that crosses the ring's wrap (slot ``maxlen-1`` -> slot 0)
-  is cut at the wrap.
 * ``to_mdp_dataset`` traces episodes through stored transitions only; the
   reference may also reach transitions already overwritten in the ring but
   still linked from a stored successor (buffers.py:115-121).
@@ -125,8 +124,8 @@ class ReplayBuffer:
         if prev_tid >= 0 and self._live(prev_tid):
             ps = prev_tid % self._maxlen
             self._next_id[ps] = tid
-            # the kernel's n-step walk steps to slot ps + 1; a wrap cuts it
-            self._h_last[ps] = ps if s != ps + 1 else s
+            # the kernel's n-step walk steps to slot (ps + 1) % maxlen
+            self._h_last[ps] = s if s == (ps + 1) % self._maxlen else ps
             self._dirty.add(ps)
         self._n_total += 1
         self._size = min(self._size + 1, self._maxlen)
