@@ -29,6 +29,18 @@ class AlgoBase(LearnableBase):
         self.create_impl(self._process_observation_shape(env.observation_space.shape),
                          get_action_size_from_env(env))
 
+    def collect(self, env, buffer=None, explorer=None, deterministic: bool = False,
+                n_steps: int = 1000000, show_progress: bool = True,
+                timelimit_aware: bool = True):
+        """algos/base.py collect: fill a ReplayBuffer from ``env`` without
+        updates; returns the buffer."""
+        from ..online import ReplayBuffer, collect
+        if buffer is None:
+            buffer = ReplayBuffer(1000000, env=env)
+        collect(self, env, buffer, explorer, deterministic=deterministic, n_steps=n_steps,
+                show_progress=show_progress, timelimit_aware=timelimit_aware)
+        return buffer
+
     def fit_online(self, env, buffer=None, explorer=None, n_steps: int = 1000000,
                    n_steps_per_epoch: int = 10000, update_interval: int = 1,
                    update_start_step: int = 0, random_steps: int = 0, eval_env=None,

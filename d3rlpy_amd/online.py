@@ -505,3 +505,35 @@ def train_single_env(algo, env, buffer: ReplayBuffer, explorer: Optional[Explore
     buffer.clip_episode()
     logger.close()
     return history
+
+
+def collect(algo, env, buffer: ReplayBuffer, explorer: Optional[Explorer] = None,
+            deterministic: bool = False, n_steps: int = 1000000,
+            show_progress: bool = True, timelimit_aware: bool = True) -> None:
+    """iterators.py:288-380: fill ``buffer`` by acting in ``env`` (greedy when
+    ``deterministic``, else the explorer or the policy's sample), no updates."""
+    if algo.n_frames > 1:
+        raise NotImplementedError("online collection with frame stacking is not supported")
+    _setup_algo(algo, env)
+    observation = env.reset()
+    for total_step in range(1, n_steps + 1):
+        observation = np.asarray(observation)
+        if observation.dtype != np.uint8:
+            observation = observation.astype("f4")
+        if deterministic:
+            action = algo.predict([observation])[0]
+        elif explorer:
+            action = explorer.sample(algo, observation.reshape((1,) + observation.shape),
+                                     total_step)[0]
+        else:
+            action = algo.sample_action([observation])[0]
+        next_observation, reward, terminal, info = env.step(action)
+        if timelimit_aware and "TimeLimit.truncated" in info:
+            clip_episode = True
+            terminal = False
+        else:
+            clip_episode = terminal
+        buffer.append(observation=observation, action=action, reward=reward,
+                      terminal=terminal, clip_episode=clip_episode)
+        observation = env.reset() if clip_episode else next_observation
+    buffer.clip_episode()
