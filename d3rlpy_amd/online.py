@@ -231,15 +231,19 @@ class ReplayBuffer:
         self._device = dev
         M = self._maxlen
         up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-        self._d_obs = up(self._h_obs)
-        self._d_act = up(self._h_act)
-        self._d_rew = up(self._h_rew)
+        # step rows start as zeros on the device; every slot written so far is
+        # still in the dirty set, so the first _sync uploads exactly those (a
+        # 1M-slot pixel ring never copies, or faults in, its unused host pages)
+        zeros = lambda a: torch.zeros(a.shape, dtype=torch.from_numpy(a[:1]).dtype,  # noqa: E731
+                                      device=dev)
+        self._d_obs = zeros(self._h_obs)
+        self._d_act = zeros(self._h_act)
+        self._d_rew = zeros(self._h_rew)
         self._d_last = up(self._h_last)
-        self._d_term = up(self._h_term)
+        self._d_term = zeros(self._h_term)
         self._d_row = torch.arange(0, 2 * M, 2, dtype=torch.int64, device=dev)
         self._d_ep_start = self._d_row
         self._d_terminal = torch.zeros(M, dtype=torch.uint8, device=dev)
-        self._dirty.clear()
 
     def _sync(self) -> None:
         """Upload the slots written since the last sample (one copy per field)."""
