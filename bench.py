@@ -11,9 +11,12 @@ CQL._update (temp, alpha, critic, actor, both target updates) — the inner
 loop of fit() with per-step losses kept on device.
 
 Multi-GPU: K2 does not shard: ``--gpus N`` runs N independent
-learners (one per GPU, distinct seeds, "replicas") launched by
-torch.distributed.run; value = steps completed by all ranks / max-over-ranks
-wall time (weak scaling).
+learners (one per GPU, distinct seeds, "replicas"); value = steps completed
+by all ranks / max-over-ranks wall time (weak scaling).  The ranks come from
+torch.distributed.run (RANK / LOCAL_RANK / WORLD_SIZE in the environment) or,
+when ``--gpus N > 1`` is given without them, from this script itself: the
+parent starts N child processes with those variables set before anything
+touches the GPU, waits for them, and relays rank 0's line (``launch_ranks``).
 
 Prints ONE JSON line (rank 0) with roofline (dominant kernel: the critic
 hidden-layer forward GEMM, fp32 MFMA) and cpu_baseline (the oracle's
@@ -30,11 +33,72 @@ import time
 import numpy as np
 
 
-def _dist_setup():
-    import torch
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv, timeout: float = None) -> int:
+    """Run this script as ``n`` ranks on one node (one process per GPU).
+
+    The parent never initialises the GPU (it does not even import torch): it
+    starts the children with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+    MASTER_PORT set, streams their stderr, relays rank 0's stdout, and
+    returns the first non-zero exit status (the others are then stopped)."""
+    import subprocess
+    import threading
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else
+                                      subprocess.DEVNULL))
+
+    def relay():
+        for line in procs[0].stdout:
+            sys.stdout.write(line.decode())
+            sys.stdout.flush()
+
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    rc = 0
+    deadline = None if timeout is None else time.monotonic() + timeout
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is not None:
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+        if rc != 0 or (deadline is not None and time.monotonic() > deadline):
+            rc = rc or 124
+            for p in pending:
+                p.kill()
+            for p in pending:
+                p.wait()
+            break
+        time.sleep(0.05)
+    t.join(timeout=5)
+    return rc
+
+
+def _dist_setup(backend: str = "nccl"):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "gloo":  # launcher self-test: CPU only
+        import torch.distributed as dist
+        if ws > 1:
+            dist.init_process_group("gloo")
+        return ws, rank, local
+    import torch
     if ws > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -56,7 +120,8 @@ def _max_over_ranks(x: float, ws: int) -> float:
         return x
     import torch
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -254,6 +319,52 @@ def _cpu_baseline_dcql(seconds: float, B: int, gen):
     return k / el, k, el
 
 
+def _selftest(args) -> None:
+    """The multi-rank bracket of main() over gloo with a host stand-in for
+    the step (tests/test_bench_launcher.py): rendezvous, barrier-bracketed
+    timing, max over ranks, rank-0 line with the whole-job value; for
+    ``cqldp`` each rank also reports its shard of the global index stream."""
+    ws, rank, _ = _dist_setup("gloo")
+    shape, batch, _ = WORKLOADS[args.algo]
+    dp = args.algo == "cqldp"
+    rs = np.random.RandomState(1000)
+    x = np.ones((64, 64), dtype=np.float32)
+
+    fail = os.environ.get("D3A_SELFTEST_FAIL_RANK")
+    if fail is not None and int(fail) == rank:
+        raise SystemExit(3)
+
+    def step():
+        g = rs.randint(1_000_000, size=batch * ws)  # one global draw per step
+        mine = g[rank * batch:(rank + 1) * batch] if dp else g[:batch]
+        time.sleep(0.001 * (1 + rank))  # ranks finish at different times
+        return int(mine.sum()) + int((x @ x)[0, 0])
+
+    for _ in range(args.warmup):
+        step()
+    _barrier(ws)
+    t0 = time.perf_counter()
+    chk = sum(step() for _ in range(args.steps))
+    _barrier(ws)
+    elapsed = _max_over_ranks(time.perf_counter() - t0, ws)
+    import torch
+    import torch.distributed as dist
+    sums = [chk]
+    if ws > 1:
+        t = torch.zeros(ws, dtype=torch.int64)
+        t[rank] = chk
+        dist.all_reduce(t)
+        sums = t.tolist()
+    if rank == 0:
+        value = (1 if dp else ws) * args.steps / elapsed
+        print(json.dumps({"metric": "selftest", "value": round(value, 2), "n_gpus": ws,
+                          "steps": args.steps, "ms_per_step": 1e3 * elapsed / args.steps,
+                          "scaling": "weak", "global_batch": batch * ws,
+                          "rank_checksums": sums}))
+    if ws > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -264,14 +375,27 @@ def main():
     ap.add_argument("--algo", choices=sorted(WORKLOADS), default="cql",
                     help="cql = the BASELINE.json headline (K2); td3bc = K1 shapes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="host threads of the all-cores CPU baseline (default: this "
+                         "process's CPU share)")
+    ap.add_argument("--selftest-gloo", action="store_true",
+                    help="launcher self-test without a GPU: gloo ranks, a host stand-in step")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary of the dominant kernel (tools/pmc_pass.sh); default "
                          "profiles/r01_pmc_traffic_<algo>.json")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's plain `bench.py --gpus N`: become N ranks (no GPU use here)
+        return launch_ranks(args.gpus, sys.argv[1:])
+    if args.selftest_gloo:
+        return _selftest(args)
 
     import torch
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     ws, rank, local = _dist_setup()
+    if ws != args.gpus:
+        print(f"bench: WORLD_SIZE={ws} but --gpus {args.gpus}; reporting n_gpus={ws}",
+              file=sys.stderr)
     algo, it = build_workload(rank, args.transitions, args.algo, ws)
 
     gpu_steps(algo, it, args.warmup)
@@ -378,4 +502,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -425,6 +425,9 @@ class _Workspace:
         # step-end kernel advances it as counter slot 4)
         self.rng_ctr = impl.counters[4:5]
         self.seed = int(torch.randint(0, 2**62, (1,)).item())
+        if impl._dp is not None:
+            # rank 0's seed with the rank folded in: distinct noise per shard
+            self.seed = impl._dp.rank_seed(self.seed)
         # policy forward on 2B rows
         self.pacts = mlp.Acts.alloc(impl.policy, 2 * B, dev)
         # sample outputs

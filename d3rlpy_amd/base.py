@@ -22,6 +22,7 @@ from __future__ import annotations
 import json
 import os
 import time
+import weakref
 from collections import defaultdict
 from typing import Any, Callable, DefaultDict, Dict, Generator, List, Optional, Sequence, Tuple
 
@@ -49,6 +50,17 @@ def _serialize(v: Any) -> Any:
     if hasattr(v, "get_type") and hasattr(v, "get_params"):  # scalers
         return {"type": v.get_type(), "params": v.get_params()}
     return v
+
+
+def _json_default(o: Any) -> Any:
+    """logger.py:21-28 (default_json_encoder)."""
+    if isinstance(o, np.integer):
+        return int(o)
+    if isinstance(o, np.floating):
+        return float(o)
+    if isinstance(o, np.ndarray):
+        return o.tolist()
+    raise ValueError(f"invalid object type: {type(o)}")
 
 
 def _deserialize(key: str, v: Any) -> Any:
@@ -89,7 +101,9 @@ class LearnableBase:
         self._loss_history: DefaultDict[str, List[float]] = defaultdict(list)
         self._active_logger = None
         self._grad_step = 0
-        self._device_dataset_cache: Dict[int, DeviceDataset] = {}
+        # (weakref to the MDPDataset, its version, the HBM copy): one entry, so
+        # a new or changed dataset releases the previous copy
+        self._device_dataset_cache: Optional[Tuple[Any, int, DeviceDataset]] = None
 
     def __setattr__(self, name: str, value: Any) -> None:
         super().__setattr__(name, value)
@@ -129,24 +143,42 @@ class LearnableBase:
         return self
 
     def save_params(self, logdir: str) -> None:
+        """params.json in the reference schema (base.py:823-850, logger.py:100-110):
+        every hyper-parameter, ``algorithm``, ``observation_shape``,
+        ``action_size``; factories / scalers as {"type", "params"}, optimiser
+        factories as their get_params(), ``use_gpu`` as a device id or null."""
         assert self._impl is not None, IMPL_NOT_INITIALIZED_ERROR
-        params = {"observation_shape": list(self._impl.observation_shape),
-                  "action_size": self._impl.action_size}
+        params: Dict[str, Any] = {}
         for k, v in self.get_params(deep=False).items():
-            if k in ("use_gpu", "impl"):
+            if k == "impl":
                 continue
+            if k == "use_gpu":
+                v = None if v is None or v is False else (0 if v is True else int(v))
             params[k] = _serialize(v)
+        params["algorithm"] = self.__class__.__name__
+        params["observation_shape"] = list(self._impl.observation_shape)
+        params["action_size"] = int(self._impl.action_size)
         with open(os.path.join(logdir, "params.json"), "w") as f:
-            json.dump(params, f, indent=2, default=lambda o: str(o))
+            json.dump(params, f, indent=2, default=_json_default)
 
     @classmethod
-    def from_json(cls, fname: str, use_gpu=False) -> "LearnableBase":
+    def params_from_json(cls, fname: str, use_gpu=False):
+        """(observation_shape, action_size, constructor kwargs) of a params.json
+        written by the reference or by save_params (base.py:186-232)."""
         with open(fname) as f:
             params = json.load(f)
         observation_shape = tuple(params.pop("observation_shape"))
         action_size = params.pop("action_size")
+        algorithm = params.pop("algorithm", None)
+        if algorithm is not None and algorithm != cls.__name__:
+            raise ValueError(f"params.json is for {algorithm}, not {cls.__name__}")
         params = {k: _deserialize(k, v) for k, v in params.items()}
         params["use_gpu"] = use_gpu
+        return observation_shape, action_size, params
+
+    @classmethod
+    def from_json(cls, fname: str, use_gpu=False) -> "LearnableBase":
+        observation_shape, action_size, params = cls.params_from_json(fname, use_gpu)
         algo = cls(**params)
         algo.create_impl(observation_shape, action_size)
         return algo
@@ -176,10 +208,13 @@ class LearnableBase:
         if not isinstance(dataset, MDPDataset):
             raise NotImplementedError(
                 "fit() on the HIP engine takes an MDPDataset (uploaded to HBM once)")
-        key = id(dataset)
-        if key not in self._device_dataset_cache:
-            self._device_dataset_cache[key] = DeviceDataset(dataset)
-        return self._device_dataset_cache[key]
+        c = self._device_dataset_cache
+        if c is not None and c[0]() is dataset and c[1] == dataset.version:
+            return c[2]
+        self._device_dataset_cache = None  # drop the stale copy before uploading
+        ddata = DeviceDataset(dataset)
+        self._device_dataset_cache = (weakref.ref(dataset), dataset.version, ddata)
+        return ddata
 
     def fit(self, dataset, n_epochs: Optional[int] = None, n_steps: Optional[int] = None,
             n_steps_per_epoch: int = 10000, save_metrics: bool = True,
@@ -203,6 +238,10 @@ class LearnableBase:
                save_interval: int = 1, scorers=None, shuffle: bool = True, callback=None
                ) -> Generator[Tuple[int, Dict[str, float]], None, None]:
         from .logger import OfflineLogger
+        if tensorboard_dir is not None:
+            raise NotImplementedError("tensorboard logging is out of scope (offline logger only)")
+        if wandb_project not in (None, "BASE"):
+            raise NotImplementedError("wandb logging is out of scope (no network access)")
         ddata = self._device_dataset(dataset)
         if isinstance(dataset, MDPDataset):
             discrete = dataset.is_action_discrete()
@@ -268,11 +307,27 @@ class LearnableBase:
             self._loss_history["step"].append(total_step)
             for k, v in epoch_loss.items():
                 self._loss_history[k].append(v)
+            if scorers and eval_episodes:
+                # base.py:806-821: scorer(algo, episodes) per named scorer
+                scores = self._evaluate(eval_episodes, scorers)
+                logger.add_epoch(epoch, total_step, scores, {})
+                epoch_loss.update(scores)
             if save_metrics and epoch % save_interval == 0:
                 logger.save_model(total_step, self)
             yield epoch, dict(epoch_loss)
         logger.close()
         self._active_logger = None
+
+    def _evaluate(self, episodes, scorers: Dict[str, Callable[[Any, Any], float]]
+                  ) -> Dict[str, float]:
+        """base.py:806-821."""
+        out = {}
+        for name, scorer in scorers.items():
+            score = scorer(self, episodes)
+            out[name] = score
+            if score is not None:
+                self._eval_results[name].append(score)
+        return out
 
     def update(self, batch) -> Dict[str, float]:
         """base.py:746-758: one gradient step on ``batch``; returns metrics."""

@@ -180,6 +180,12 @@ class MDPDataset:
         else:
             self._actions = np.asarray(actions, dtype=np.float32)
         self._episodes: Optional[List[Episode]] = None
+        # bumped by every in-place change; device copies are keyed by it
+        self._version = 0
+
+    @property
+    def version(self) -> int:
+        return self._version
 
     @property
     def observations(self):
@@ -277,6 +283,7 @@ class MDPDataset:
             np.asarray(episode_terminals, dtype=np.float32).reshape(-1)
         self._episode_terminals = np.concatenate([self._episode_terminals, ep_terms])
         self._episodes = None
+        self._version += 1
 
     def extend(self, dataset: "MDPDataset") -> None:
         """dataset.pyx:488-509."""

@@ -91,7 +91,9 @@ class RandomIterator(TransitionIterator):
                  shard: Tuple[int, int] = (0, 1)):
         """``shard=(rank, world)``: this learner's slice [rank*B, (rank+1)*B)
         of one global stream of world*B indices per step (every rank must use
-        the same ``seed``) — the data-parallel sampler of SURVEY §8e."""
+        the same ``seed``) — the data-parallel sampler of SURVEY §8e.  With
+        world > 1 and ``seed=None`` rank 0's seed is broadcast over the
+        initialised torch.distributed group (an error if there is none)."""
         super().__init__(dataset, batch_size, n_steps, gamma, n_frames, real_ratio,
                          generated_maxlen, out)
         self._rank, self._world = int(shard[0]), int(shard[1])
@@ -101,7 +103,16 @@ class RandomIterator(TransitionIterator):
         if index_source not in ("device", "numpy"):
             raise ValueError("index_source must be 'device' or 'numpy'")
         self._index_source = index_source
-        self._seed = int(np.random.randint(0, 2**62)) if seed is None else int(seed)
+        if seed is None:
+            seed = int(np.random.randint(0, 2**62))
+            if self._world > 1:
+                import torch.distributed as dist
+                if not dist.is_initialized():
+                    raise ValueError("shard world > 1 needs an explicit seed shared by every "
+                                     "rank, or an initialised torch.distributed group")
+                from .dp import broadcast_seed
+                seed = broadcast_seed(seed)
+        self._seed = int(seed)
         self.indices = torch.zeros(batch_size, dtype=torch.int64, device=dataset.device)
 
     def _gather(self, out) -> None:

@@ -121,7 +121,9 @@ class ReplayBuffer:
         self._prev_id[s] = prev_tid
         self._next_id[s] = -1
         self._dirty.add(s)
-        if prev_tid >= 0 and self._live(prev_tid):
+        # liveness in the post-push window [tid - maxlen + 1, tid]: with
+        # maxlen 1 the predecessor was just overwritten by this transition
+        if prev_tid >= 0 and prev_tid > tid - self._maxlen:
             ps = prev_tid % self._maxlen
             self._next_id[ps] = tid
             # the kernel's n-step walk steps to slot (ps + 1) % maxlen

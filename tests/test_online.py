@@ -99,12 +99,25 @@ def _check_host(buf: ReplayBuffer, ob: OReplayBuffer):
         assert (buf._h_last[s] != s) == cont, s
 
 
-@pytest.mark.parametrize("maxlen,n", [(5000, 700), (97, 700)])
+@pytest.mark.parametrize("maxlen,n", [(5000, 700), (97, 700), (2, 50), (1, 50)])
 def test_replay_host_mirror_matches_reference_buffer(maxlen, n):
     buf = ReplayBuffer(maxlen, env=ToyEnv())
     ob = OReplayBuffer(maxlen, (5,), 2)
     _fill([buf, ob], n)
     _check_host(buf, ob)
+
+
+def test_replay_maxlen1_keeps_the_stored_transition():
+    """maxlen 1: the newest transition must not link to itself (it replaced
+    its predecessor); to_mdp_dataset traces stored transitions only (the
+    reference also walks evicted objects it keeps reachable, module doc)."""
+    buf = ReplayBuffer(1, env=ToyEnv())
+    ob = OReplayBuffer(1, (5,), 2)
+    _fill([buf, ob], 500)
+    assert buf._h_last[0] == 0 and buf._next_id[0] == -1
+    ds = buf.to_mdp_dataset()
+    assert len(ds.observations) == 1
+    np.testing.assert_array_equal(ds.observations[0], np.asarray(ob.buf[0].observation))
 
 
 def test_replay_to_mdp_dataset_matches_reference():
