@@ -128,7 +128,32 @@ class GatherDesc(C.Structure):
         ("o_rew", vp), ("o_next_obs", vp), ("o_next_frames", vp),
         ("o_term", vp), ("o_n_steps", vp), ("row_offset", C.c_int64),
         ("t_term_value", vp),
+        ("gamma_pow", C.c_float * 64),
     ]
+
+    def set_gamma(self, gamma: float, n_steps: int) -> None:
+        """gamma and the powf(gamma, i) table of the n-step return."""
+        if not 1 <= n_steps <= 64:
+            raise ValueError("n_steps must be in [1, 64]")
+        self.gamma = gamma
+        for i, v in enumerate(gamma_powers(gamma, n_steps)):
+            self.gamma_pow[i] = v
+
+
+_LIBM = None
+
+
+def gamma_powers(gamma: float, n: int):
+    """[powf(gamma, (float)i) for i < n] with the C library's powf — the
+    arithmetic the reference's compiled n-step loop performs
+    (dataset.pyx:1325 under Cython 0.29: float gamma ** int i -> powf)."""
+    global _LIBM
+    if _LIBM is None:
+        import ctypes.util
+        _LIBM = C.CDLL(ctypes.util.find_library("m"))
+        _LIBM.powf.restype = C.c_float
+        _LIBM.powf.argtypes = [C.c_float, C.c_float]
+    return [_LIBM.powf(C.c_float(gamma), C.c_float(float(i))) for i in range(n)]
 
 
 class Td3PrepDesc(C.Structure):

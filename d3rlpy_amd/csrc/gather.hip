@@ -74,10 +74,10 @@ __global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
     int64_t nt_i = t, row_i = row_t, last_i = last_t;
     int k = 0;
     for (k = 0; k < d.n_steps; ++k) {
-      // n_step_return += reward * gamma ** i   (dataset.pyx:1325); gamma**i is
-      // evaluated as the fp32 rounding of the fp64 power, then one fp32
-      // multiply and one fp32 add (no contraction), matching oracle/gather.py
-      const float gp = k == 0 ? 1.f : (float)pow((double)d.gamma, (double)k);
+      // n_step_return += reward * gamma ** i   (dataset.pyx:1325): the host's
+      // powf(gamma, i) from the descriptor, then one fp32 multiply and one fp32
+      // add (no contraction) — the Cython 0.29 codegen, see d3a_gather_desc
+      const float gp = d.gamma_pow[k];
       ret = __fadd_rn(ret, __fmul_rn(d.rew[row_i], gp));
       if (nt_i == last_i || k == d.n_steps - 1) break;
       // successor slot; wraps at n_trans for the online replay ring (an
@@ -157,6 +157,7 @@ extern "C" int d3a_gather_batch(const d3a_gather_desc* d, void* stream) {
   D3A_CHECK_ARG((d->act != nullptr) != (d->act_i != nullptr),
                 "d3a_gather_batch: exactly one of act / act_i");
   D3A_CHECK_ARG(d->n_steps >= 1 && d->n_frames >= 1, "d3a_gather_batch: n_steps, n_frames >= 1");
+  D3A_CHECK_ARG(d->n_steps <= D3A_MAX_NSTEP, "d3a_gather_batch: n_steps > D3A_MAX_NSTEP");
   D3A_CHECK_ARG(d->idx || (d->idx_out && d->ctr && d->ticket),
                 "d3a_gather_batch: indices must be given or drawn (idx_out, ctr, ticket)");
   D3A_CHECK_ARG(d->obs ? (d->o_obs && d->o_next_obs) : (d->o_frames && d->o_next_frames),

@@ -458,7 +458,7 @@ class DeviceDataset:
         d.frame_bytes = self.frame_bytes
         d.n_frames = n_frames if self.is_image else 1
         d.n_steps = n_steps
-        d.gamma = gamma
+        d.set_gamma(gamma, n_steps)
         if indices is not None:
             assert indices.dtype == torch.int64 and indices.is_cuda and indices.numel() >= B
             d.idx = ops.ptr(indices)

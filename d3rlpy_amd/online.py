@@ -315,7 +315,7 @@ class ReplayBuffer:
         d.n_trans = self._maxlen
         d.n_frames = 1
         d.n_steps = n_steps
-        d.gamma = gamma
+        d.set_gamma(gamma, n_steps)
         d.idx = ops.ptr(idx)
         d.B = batch_size
         if self._is_image:

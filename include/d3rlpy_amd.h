@@ -413,6 +413,7 @@ int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream);
 /* ---- device-resident dataset gather (replaces TransitionMiniBatch /
  *      _assign_to_batch, d3rlpy/dataset.pyx:1139-1342, and the index draw of
  *      RandomIterator._next, d3rlpy/iterators/random_iterator.py:38-41) ---- */
+#define D3A_MAX_NSTEP 64
 typedef struct d3a_gather_desc {
   /* dataset (device resident, structure of arrays over all stored steps) */
   const float* obs;          /* [n_rows][D] float observations (or NULL)   */
@@ -446,6 +447,13 @@ typedef struct d3a_gather_desc {
    * The online ReplayBuffer needs it: its transition into the terminal state
    * has terminal = 1 but a real next observation (online/buffers.py:268-281) */
   const float* t_term_value;
+  /* gamma_pow[i] = powf(gamma, (float)i) for i < n_steps, filled by the host
+   * with its C library's powf: the reference's n-step accumulation
+   * `n_step_return += reward * gamma ** i` (dataset.pyx:1325; float gamma,
+   * int i) is compiled by its pinned Cython 0.29.21 into
+   * `acc = acc + reward * powf(gamma, (float)i)` — all fp32 — and powf is
+   * not always the correctly rounded power, so the kernel reads the host's */
+  float gamma_pow[D3A_MAX_NSTEP];
 } d3a_gather_desc;
 int d3a_gather_batch(const d3a_gather_desc* d, void* stream);
 

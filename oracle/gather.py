@@ -93,6 +93,21 @@ def _stack_frames(t: OTransition, n_frames: int, stack_next: bool) -> np.ndarray
     return stack
 
 
+_LIBM = None
+
+
+def _powf_table(g32: np.float32, n: int):
+    """powf(gamma, (float)i) for i < n from the C library (ctypes)."""
+    global _LIBM
+    if _LIBM is None:
+        import ctypes
+        import ctypes.util
+        _LIBM = ctypes.CDLL(ctypes.util.find_library("m"))
+        _LIBM.powf.restype = ctypes.c_float
+        _LIBM.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+    return [np.float32(_LIBM.powf(float(g32), float(i))) for i in range(n)]
+
+
 def gather(transitions: List[OTransition], n_frames: int = 1, n_steps: int = 1,
            gamma: float = 0.99):
     """TransitionMiniBatch(transitions, n_frames, n_steps, gamma) -> dict of arrays."""
@@ -102,14 +117,17 @@ def gather(transitions: List[OTransition], n_frames: int = 1, n_steps: int = 1,
     discrete = not isinstance(first.action, np.ndarray)
     obs, nobs, acts, rews, terms, nst = [], [], [], [], [], []
     g32 = np.float32(gamma)
+    gpow = _powf_table(g32, n_steps)
     for t in transitions:
         ret = np.float32(0.0)
         nxt = t
         i = 0
         for i in range(n_steps):
-            # n_step_return += reward * gamma ** i   (C float arithmetic; gamma**i
-            # taken as the fp32 rounding of the fp64 power)
-            gp = np.float32(np.float64(g32) ** i)
+            # n_step_return += reward * gamma ** i   (dataset.pyx:1325, float gamma,
+            # int i): Cython 0.29.21 (requirements.txt:8) emits
+            # `acc = acc + reward * powf(gamma, (float)i)` — fp32 throughout,
+            # powf from the C library (tests/golden/cython_pow_codegen.txt)
+            gp = gpow[i]
             ret = np.float32(ret + np.float32(np.float32(nxt.reward) * gp))
             if nxt.next is None or i == n_steps - 1:
                 break

@@ -53,6 +53,8 @@ def main():
         m = impl.update_step(HostBatch(*arrs), noise=nz)
         metrics.append([m[k] for k in sorted(m)])
     torch.cuda.synchronize()
+    # the Philox key this rank's workspace draws its own noise with
+    np.save(os.path.join(work, f"seed{rank}.npy"), np.array(impl._workspace(sl.stop - sl.start).seed))
     if rank == 0:
         torch.save(impl.get_state_dict(), os.path.join(work, "dp_state.pt"))
         np.save(os.path.join(work, "dp_metrics.npy"), np.array(metrics))

@@ -38,6 +38,9 @@ CASES = {
     # n-step returns (gather n_steps 3): gamma ** n_steps per row
     # (ddpg_impl.py:160, cql_impl.py:110-117) with n in {1, 2, 3}
     "nstep": dict(D=11, A=3, hidden=[256, 256], N=10, B=256, nstep=True),
+    # K4 shapes (antmaze obs 29 / act 8, 256 rows per GPU): Q-input rows of
+    # 37 floats padded to 40, 8-wide tanh-Gaussian sample / log-prob
+    "k4_antmaze": dict(D=29, A=8, hidden=[256, 256], N=10, B=256),
 }
 
 
@@ -199,14 +202,19 @@ def test_cql_graph_replay_matches_eager():
     assert len(impl_b._workspace(B)._graphs) == 1
 
 
-def test_cql_grad_accuracy_vs_fp64():
+@pytest.mark.parametrize("shape", [(11, 3), (29, 8)], ids=["k2_hopper", "k4_antmaze"])
+def test_cql_grad_accuracy_vs_fp64(shape):
     """Where the two fp32 implementations differ, which one is closer to exact?
 
-    Runs the K2-shaped first update in the fp32 oracle, in an fp64 copy of
-    the oracle, and on HIP.  HIP's critic gradients must be within 1e-5
-    (max-normalised) of the fp64 values, i.e. the residual HIP-vs-fp32-oracle
-    difference is fp32 rounding, not a formula difference."""
-    D, A, H, N, B = 11, 3, [256, 256], 10, 256
+    Runs the first update (K2 or K4 shapes) in the fp32 oracle, in an fp64
+    copy of the oracle, and on HIP.  HIP's critic and policy gradients must
+    be within 1e-5 (max-normalised) of the fp64 values, i.e. the residual
+    HIP-vs-fp32-oracle difference is fp32 rounding, not a formula difference;
+    parameters within 1e-5 of fp64 or proven Adam first-step amplification
+    (tests/arbiter_helpers.py)."""
+    from arbiter_helpers import check_params_adam1, hip_grads
+    D, A = shape
+    H, N, B = [256, 256], 10, 256
     orc = make_oracle(D, A, H, N, seed=11)
     o64 = make_oracle(D, A, H, N, seed=11)
     for m in (o64._q_func, o64._policy, o64._targ_q_func, o64._targ_policy, o64._log_temp,
@@ -214,6 +222,7 @@ def test_cql_grad_accuracy_vs_fp64():
         m.double()
     impl = make_impl(D, A, H, N)
     copy_oracle_to_impl(orc, impl)
+    sd0 = impl.get_state_dict()
     rs = np.random.RandomState(0)
     gen = torch.Generator().manual_seed(1)
     arrs = make_batch(rs, B, D, A)
@@ -248,6 +257,13 @@ def test_cql_grad_accuracy_vs_fp64():
                 print(f"critic {c} {nm}: hip-vs-fp64 {e_hip:.1e}  oracle32-vs-fp64 {e_orc:.1e}")
                 worst_hip, worst_orc = max(worst_hip, e_hip), max(worst_orc, e_orc)
     assert worst_hip <= 1e-5, (worst_hip, worst_orc)
+    sd1 = impl.get_state_dict()
+    for key, refs, getter, lr in (("_q_func", impl._critic_refs(), impl.critic_grad, 3e-4),
+                                  ("_policy", impl._policy_refs(), impl.policy_grad, 1e-4)):
+        g_hip = hip_grads(refs, getter)
+        p64 = {k: v.detach() for k, v in getattr(o64, key).named_parameters()}
+        pw, namp = check_params_adam1(key, sd0[key], sd1[key], p64, g_hip, lr=lr)
+        print(f"{key} params vs fp64: {pw:.1e} ({namp} amplified)")
 
 
 def test_cql_sample_draws_equal_philox_fill():

@@ -60,8 +60,17 @@ def test_dp_world1_rccl_graph_bit_identical():
         dist.destroy_process_group()
 
 
-def test_dp_two_ranks_match_global_batch(tmp_path):
-    D, A, H, L, N, B, S = 11, 3, 64, 2, 4, 64, 3
+DP_CASES = {
+    "small": (11, 3, 64, 2, 4, 64, 3),
+    # K4 shapes: antmaze obs 29 / act 8 (Q-input rows 37 padded to 40), 256
+    # rows per rank, N = 10
+    "k4_antmaze": (29, 8, 256, 2, 10, 512, 2),
+}
+
+
+@pytest.mark.parametrize("case", list(DP_CASES))
+def test_dp_two_ranks_match_global_batch(tmp_path, case):
+    D, A, H, L, N, B, S = DP_CASES[case]
     world = 2
     ref = make_impl(D, A, [H] * L, N)
     torch.save(ref.get_state_dict(), tmp_path / "init.pt")
@@ -106,3 +115,7 @@ def test_dp_two_ranks_match_global_batch(tmp_path):
     assert worst <= 1e-5
     for key in ("_log_temp", "_log_alpha"):
         assert abs(float(sd[key]["_parameter"]) - float(full[key]["_parameter"])) <= 1e-6
+    # device noise (gen_noise): rank 0's seed with the rank folded in — the
+    # two shards draw different policy noise
+    s0, s1 = (int(np.load(tmp_path / f"seed{r}.npy")) for r in range(world))
+    assert s0 != s1

@@ -23,8 +23,11 @@ from td3_helpers import (make_scaler_stats, make_td3_batch, make_td3_impl, make_
 pytestmark = pytest.mark.gpu
 
 CASES = {
+    # K1 = configs[0]: pendulum-random shapes, batch 100, standard scaler
+    # (td3_plus_bc.py:101-119); steps 0 and 2 include the delayed actor
+    "k1_pendulum": dict(D=3, A=1, hidden=[256, 256], B=100, scaler=True, n_steps=1),
     "small_scaled": dict(D=5, A=2, hidden=[64, 64], B=32, scaler=True, n_steps=1),
-    "k1_hopper": dict(D=11, A=3, hidden=[256, 256], B=256, scaler=True, n_steps=1),
+    "hopper_scaled": dict(D=11, A=3, hidden=[256, 256], B=256, scaler=True, n_steps=1),
     "halfcheetah_nstep": dict(D=17, A=6, hidden=[256, 256], B=256, scaler=True, n_steps=3),
     "deep_unscaled": dict(D=7, A=2, hidden=[128, 128, 128], B=64, scaler=False, n_steps=1),
 }
