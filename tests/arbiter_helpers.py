@@ -20,6 +20,7 @@ reference) from the SAME state HIP starts a stage from, and compares:
 """
 from __future__ import annotations
 
+import math
 from typing import Dict
 
 import torch
@@ -73,6 +74,57 @@ def check_grads(label: str, g_hip: Dict[str, torch.Tensor], g64: Dict[str, torch
         worst = max(worst, e)
     assert worst <= tol, (label, worst)
     return worst
+
+
+def adam_state_by_key(optim_sd: dict, keys) -> Dict[str, tuple]:
+    """torch.optim.Adam state_dict -> {param key: (exp_avg, exp_avg_sq, step)}
+    with ``keys`` in parameters() order (the reference checkpoint layout)."""
+    ids = optim_sd["param_groups"][0]["params"]
+    out = {}
+    for k, i in zip(keys, ids):
+        st = optim_sd["state"].get(i)
+        if st:
+            out[k] = (st["exp_avg"].double(), st["exp_avg_sq"].double(), int(st["step"]))
+    return out
+
+
+def adam_map(p0, g, lr, state=None, betas=(0.9, 0.999), eps=1e-8):
+    """torch.optim.Adam's update (weight_decay 0) in fp64 from the state
+    before the step (None: the first step)."""
+    b1, b2 = betas
+    g = g.double()
+    m0, v0, t0 = state if state is not None else (torch.zeros_like(g), torch.zeros_like(g), 0)
+    t = t0 + 1
+    m = b1 * m0 + (1 - b1) * g
+    v = b2 * v0 + (1 - b2) * g * g
+    denom = v.sqrt() / math.sqrt(1 - b2 ** t) + eps
+    return p0.double() - lr / (1 - b1 ** t) * m / denom
+
+
+def check_params_adam(label: str, p0: Dict[str, torch.Tensor], p_hip: Dict[str, torch.Tensor],
+                      p_ref: Dict[str, torch.Tensor], g_hip: Dict[str, torch.Tensor], lr: float,
+                      states: Dict[str, tuple] = None, tol: float = PARAM_TOL):
+    """Parameters after one Adam step from the state ``states`` (None: the
+    first step): within ``tol`` of the reference, or — entry by entry —
+    HIP's value is Adam applied to HIP's own (1e-5-checked) gradient.
+    Returns (max |p_hip - p_ref|, number of such entries)."""
+    worst, n_amp = 0.0, 0
+    for k, ref in p_ref.items():
+        ph, pr = p_hip[k].double().cpu(), ref.double().cpu()
+        d = (ph - pr).abs()
+        worst = max(worst, float(d.max()))
+        bad = d > tol
+        if bool(bad.any()):
+            g = g_hip[k]
+            st = None if states is None else states.get(k)
+            pred = adam_map(p0[k].cpu(), g, lr, st)
+            self_err = float((ph - pred).abs()[bad].max())
+            print(f"  {label} param {k}: {int(bad.sum())} entries differ by up to "
+                  f"{float(d.max()):.1e}; their |g| <= {float(g.abs()[bad].max()):.1e} "
+                  f"(tensor max {float(g.abs().max()):.1e}); HIP vs Adam(own grad) {self_err:.1e}")
+            assert self_err <= ADAM_SELF_TOL, (label, k, self_err)
+            n_amp += int(bad.sum())
+    return worst, n_amp
 
 
 def check_params_adam1(label: str, p0: Dict[str, torch.Tensor], p_hip: Dict[str, torch.Tensor],

@@ -4,8 +4,10 @@ Same initial state (loaded through the reference checkpoint layout), same
 minibatch, same injected draws (VAE rsample noise, the B*N target latents,
 the actor latents).  Compared per stage: imitator / critic / actor losses,
 the reduced gradients of the three optimisers, post-Adam parameters and
-targets.  Tolerances: losses 1e-5 relative, gradients 2e-5 max-normalised,
-parameters 3e-5 absolute (see test_bcq_update_parity).
+targets.  Tolerances: losses 1e-5 relative, gradients 2e-5 max-normalised
+between the two fp32 implementations (HIP itself is within 1e-5 of fp64:
+tests/test_gpu_arbiters.py), parameters 1e-5 absolute or proven Adam
+amplification of a near-zero gradient entry (tests/arbiter_helpers.py).
 """
 import numpy as np
 import pytest
@@ -69,10 +71,16 @@ def _grad_err(impl, refs, ref_g, getter, name):
     return e
 
 
-def _param_err(impl, orc, keys):
+def _param_check(label, impl, orc, key, optim_key, sd0, refs, getter):
+    """Parameters of ``key`` after its stage: 1e-5 of the oracle, or proven
+    Adam amplification of a near-zero gradient entry (arbiter_helpers)."""
+    from arbiter_helpers import adam_state_by_key, check_params_adam, hip_grads
     sd = impl.get_state_dict()
-    ref = oracle_state(orc)
-    return max(float((sd[k][n] - t).abs().max()) for k in keys for n, t in ref[k].items())
+    keys = [r[0] for r in refs]
+    states = adam_state_by_key(sd0[optim_key], keys)
+    w, n = check_params_adam(label, sd0[key], sd[key], oracle_state(orc)[key],
+                             hip_grads(refs, getter), lr=1e-3, states=states or None)
+    return w, n
 
 
 @pytest.mark.parametrize("case", list(CASES))
@@ -98,22 +106,27 @@ def test_bcq_update_parity(case):
         hb = HostBatch(*arrs)
         # imitator
         impl.set_state_dict(oracle_state(orc))
+        sd0 = impl.get_state_dict()
         lo = float(orc.update_imitator(tb, nz.eps_vae))
         ig = [p.grad.clone() for p in orc._imitator.parameters()]
         lh = impl._run(hb, (True, False, False, False), noise, True, False)["imitator_loss"]
         assert abs(lh - lo) <= 1e-5 * max(1.0, abs(lo)), (step, lh, lo)
         e_i = _grad_err(impl, impl._imitator_refs(), ig, impl.imitator_grad, "imitator")
-        p_i = _param_err(impl, orc, ("_imitator",))
+        p_i, a_i = _param_check("imitator", impl, orc, "_imitator", "_imitator_optim", sd0,
+                                impl._imitator_refs(), impl.imitator_grad)
         # critic
         impl.set_state_dict(oracle_state(orc))
+        sd0 = impl.get_state_dict()
         lo = float(orc.update_critic(tb, nz.z_target))
         cg = [p.grad.clone() for p in orc._q_func.parameters()]
         lh = impl._run(hb, (False, True, False, False), noise, True, False)["critic_loss"]
         assert abs(lh - lo) <= 1e-5 * max(1.0, abs(lo)), (step, lh, lo)
         e_c = _grad_err(impl, impl._critic_refs(), cg, impl.critic_grad, "critic")
-        p_c = _param_err(impl, orc, ("_q_func",))
+        p_c, a_c = _param_check("critic", impl, orc, "_q_func", "_critic_optim", sd0,
+                                impl._critic_refs(), impl.critic_grad)
         # actor + targets
         impl.set_state_dict(oracle_state(orc))
+        sd0 = impl.get_state_dict()
         lo = float(orc.update_actor(tb, nz.z_actor))
         pg = [p.grad.clone() for p in orc._policy.parameters()]
         soft_sync(orc._targ_policy, orc._policy, orc._tau)
@@ -121,15 +134,20 @@ def test_bcq_update_parity(case):
         m = impl._run(hb, (False, False, True, True), noise, True, False)
         assert abs(m["actor_loss"] - lo) <= 1e-5 * max(1.0, abs(lo)), (step, m, lo)
         e_p = _grad_err(impl, impl._policy_refs(), pg, impl.policy_grad, "policy")
-        p_p = _param_err(impl, orc, ("_policy", "_targ_policy", "_targ_q_func"))
+        p_p, a_p = _param_check("policy", impl, orc, "_policy", "_actor_optim", sd0,
+                                impl._policy_refs(), impl.policy_grad)
+        sd = impl.get_state_dict()
+        ref = oracle_state(orc)
+        p_t = max(float((sd[k][n] - t).abs().max()) for k in ("_targ_policy", "_targ_q_func")
+                  for n, t in ref[k].items())
         print(f"[{case}] step {step}: grad rel imitator {e_i:.1e} critic {e_c:.1e} policy "
-              f"{e_p:.1e}; param abs {max(p_i, p_c, p_p):.1e}")
+              f"{e_p:.1e}; param abs {max(p_i, p_c, p_p):.1e} ({a_i + a_c + a_p} entries "
+              f"proven Adam amplification), targets {p_t:.1e}")
         assert max(e_i, e_c, e_p) <= 2e-5
-        # parameters: 3e-5 absolute.  At Adam's first steps an entry moves by
-        # ~lr * g / (|g| + eps); for near-zero gradient entries (|g| ~ 1e-7 of
-        # a max ~1e-2) the 2e-5-relative gradient agreement becomes ~1e-5 of
-        # parameter difference at BCQ's lr = 1e-3 (3.3x CQL's critic lr)
-        assert max(p_i, p_c, p_p) <= 3e-5
+        # parameters: 1e-5 absolute, except entries where Adam amplifies a
+        # near-zero gradient (lr * g / (|g| + eps) at BCQ's lr = 1e-3), each of
+        # which is proven to be Adam applied to HIP's 2e-5-checked gradient
+        assert p_t <= 1e-5
 
 
 def test_bcq_full_step_equals_stages():
