@@ -222,12 +222,13 @@ class LearnableBase:
             logdir: str = "d3rlpy_logs", allow_overwrite: bool = False,
             wandb_project: str = "BASE", verbose: bool = True, show_progress: bool = True,
             tensorboard_dir: Optional[str] = None, eval_episodes=None, save_interval: int = 1,
-            scorers=None, shuffle: bool = True, callback=None
-            ) -> List[Tuple[int, Dict[str, float]]]:
+            scorers=None, shuffle: bool = True, callback=None, *,
+            index_source: str = "device") -> List[Tuple[int, Dict[str, float]]]:
         return list(self.fitter(dataset, n_epochs, n_steps, n_steps_per_epoch, save_metrics,
                                 experiment_name, with_timestamp, logdir, allow_overwrite,
                                 wandb_project, verbose, show_progress, tensorboard_dir,
-                                eval_episodes, save_interval, scorers, shuffle, callback))
+                                eval_episodes, save_interval, scorers, shuffle, callback,
+                                index_source=index_source))
 
     def fitter(self, dataset, n_epochs: Optional[int] = None, n_steps: Optional[int] = None,
                n_steps_per_epoch: int = 10000, save_metrics: bool = True,
@@ -235,8 +236,13 @@ class LearnableBase:
                logdir: str = "d3rlpy_logs", allow_overwrite: bool = False,
                wandb_project: str = "BASE", verbose: bool = True, show_progress: bool = True,
                tensorboard_dir: Optional[str] = None, eval_episodes=None,
-               save_interval: int = 1, scorers=None, shuffle: bool = True, callback=None
+               save_interval: int = 1, scorers=None, shuffle: bool = True, callback=None, *,
+               index_source: str = "device"
                ) -> Generator[Tuple[int, Dict[str, float]], None, None]:
+        """base.py:349-687.  Extension (keyword-only): ``index_source`` of the
+        n_steps mode's RandomIterator — "device" (Philox on the GPU, default)
+        or "numpy" (the reference's np.random.randint stream, uploaded per
+        step)."""
         from .logger import OfflineLogger
         if tensorboard_dir is not None:
             raise NotImplementedError("tensorboard logging is out of scope (offline logger only)")
@@ -264,7 +270,8 @@ class LearnableBase:
             iterator = RandomIterator(ddata, n_steps_per_epoch, batch_size=self._batch_size,
                                       n_steps=self._n_steps, gamma=self._gamma,
                                       n_frames=self._n_frames, real_ratio=self._real_ratio,
-                                      generated_maxlen=self._generated_maxlen, out=out)
+                                      generated_maxlen=self._generated_maxlen, out=out,
+                                      index_source=index_source)
         elif n_epochs is not None and n_steps is None:
             iterator = RoundIterator(ddata, batch_size=self._batch_size, n_steps=self._n_steps,
                                      gamma=self._gamma, n_frames=self._n_frames,

@@ -103,6 +103,10 @@ class RandomIterator(TransitionIterator):
         if index_source not in ("device", "numpy"):
             raise ValueError("index_source must be 'device' or 'numpy'")
         self._index_source = index_source
+        if seed is None and index_source == "numpy":
+            seed = 0  # unused: the numpy stream draws from numpy's global RNG,
+            # which must not be advanced here (the reference draws nothing at
+            # construction, random_iterator.py:18-36)
         if seed is None:
             seed = int(np.random.randint(0, 2**62))
             if self._world > 1:

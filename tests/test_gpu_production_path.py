@@ -1,0 +1,151 @@
+"""The production path end to end against the oracle (GPU only).
+
+``Algo.fit`` as shipped — the fitter loop (base.py:611-682), RandomIterator
+over the HBM dataset with the reference's index stream (index_source="numpy",
+random_iterator.py:38-41), the gather kernel, the update pipeline drawing its
+own Philox noise on device (gen_noise), the first step eager and every later
+step a HIP-graph replay, the per-step metric ring read back at the epoch end
+— for 12 steps, then replayed on the CPU oracle: the same numpy index draws
+gathered by the oracle's TransitionMiniBatch, and each step's device draws
+reproduced with d3a_philox_fill at that step's Philox counter (the sampler
+kernels draw bit-identically to it: test_cql_sample_draws_equal_philox_fill).
+
+Bars (a 12-step trajectory without re-synchronisation; relu masks and Adam's
+near-zero-gradient entries let the two fp32 trajectories separate slowly, as
+in test_cql_trajectory_drift): every logged loss within 1e-4 relative,
+parameters and targets within 1e-4 absolute; the index stream and the
+reproduced draws themselves are exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gather as og
+from oracle.cql import Batch
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 12
+
+
+def _transitions(ds):
+    trans = []
+    for o, a, r, t in og.to_episodes(ds.observations, ds.actions, ds.rewards, ds.terminals):
+        trans += og.to_transitions(o, a, r, t)
+    return trans
+
+
+def _oracle_batches(trans, B, seed):
+    np.random.seed(seed)
+    out = []
+    for _ in range(STEPS):
+        idx = [np.random.randint(len(trans)) for _ in range(B)]
+        b = og.gather([trans[i] for i in idx])
+        out.append(Batch.from_numpy(b["observations"], b["actions"], b["rewards"],
+                                    b["next_observations"], b["terminals"], b["n_steps"]))
+    return out
+
+
+def _philox(n_normal, n_uniform, seed, counter):
+    from d3rlpy_amd import ops
+    buf = torch.zeros(n_normal + n_uniform, device="cuda")
+    ctr = torch.full((1,), counter, dtype=torch.int64, device="cuda")
+    ticket = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ops.philox_fill(buf, n_normal, n_uniform, -1.0, 1.0, seed, ctr, ticket)
+    torch.cuda.synchronize()
+    return buf.cpu()
+
+
+def _compare_state(sd, ref, keys, tol):
+    worst = 0.0
+    for k in keys:
+        for n, t in ref[k].items():
+            worst = max(worst, float((sd[k][n] - t).abs().max()))
+    assert worst <= tol, worst
+    return worst
+
+
+def test_cql_fit_production_path_vs_oracle():
+    from cql_helpers import ORACLE_STATE_KEYS, make_oracle, oracle_state
+    from d3rlpy_amd.algos.cql import CQL
+    from d3rlpy_amd.datasets import get_synthetic_d4rl
+    from oracle.cql import CQLNoise
+    D, A, N, B = 11, 3, 10, 256
+    ds = get_synthetic_d4rl("hopper-medium-v0", n=5000, seed=2)
+    algo = CQL(batch_size=B)
+    algo.build_with_dataset(ds)
+    impl = algo.impl
+    orc = make_oracle(D, A, [256, 256], N, seed=0)
+    for k, v in impl.get_state_dict().items():
+        getattr(orc, k).load_state_dict(v)
+    np.random.seed(42)
+    algo.fit(ds, n_steps=STEPS, n_steps_per_epoch=STEPS, save_metrics=False, verbose=False,
+             show_progress=False, index_source="numpy")
+    ws = impl._last_ws()
+    assert len(ws._graphs) == 1  # steps 2..12 replayed the captured graph
+    names, ring = impl.read_metrics_ring(None)
+    assert ring.shape == (STEPS, len(names))
+    worst_m = 0.0
+    tmpl = CQLNoise.draw(torch.Generator(), B, A, N)
+    NB = N * B
+    for s, batch in enumerate(_oracle_batches(_transitions(ds), B, 42)):
+        buf = _philox(ws.n_normal, ws.n_uniform, ws.seed, s)
+        o = 0
+        eps_temp = buf[o:o + B * A]; o += B * A
+        ep = buf[o:o + 4 * NB * A].view(2, 2, N, B, A); o += 4 * NB * A
+        eps_actor = buf[o:o + B * A]; o += B * A
+        ur = buf[ws.n_normal:ws.n_normal + 2 * NB * A].view(2, NB, A)
+        f = dict(eps_temp=eps_temp, alpha_pi_t=ep[0, 0], alpha_pi_tp1=ep[0, 1],
+                 critic_pi_t=ep[1, 0], critic_pi_tp1=ep[1, 1], alpha_rand=ur[0],
+                 critic_rand=ur[1], eps_actor=eps_actor)
+        nz = CQLNoise(**{k: v.reshape(getattr(tmpl, k).shape).clone() for k, v in f.items()},
+                      **{k: getattr(tmpl, k) for k in tmpl.__dataclass_fields__ if k not in f})
+        m = orc.update(batch, nz)
+        for j, name in enumerate(names):
+            e = abs(ring[s, j] - m[name]) / max(1.0, abs(m[name]))
+            worst_m = max(worst_m, e)
+            assert e <= 1e-4, (s, name, ring[s, j], m[name])
+    w = _compare_state(impl.get_state_dict(), oracle_state(orc),
+                       ("_q_func", "_targ_q_func", "_policy", "_targ_policy"), 1e-4)
+    assert abs(float(impl.log_alpha.item()) - float(orc._log_alpha().item())) <= 1e-5
+    assert abs(float(impl.log_temp.item()) - float(orc._log_temp().item())) <= 1e-5
+    print(f"CQL fit production path: {STEPS} steps, max |param diff| {w:.2e}, max metric "
+          f"rel diff {worst_m:.2e}")
+
+
+def test_td3bc_fit_production_path_vs_oracle():
+    """K1 = configs[0]: TD3+BC at pendulum shapes (obs 3, act 1, batch 100,
+    standard scaler fitted by fit() itself), actor and targets every 2nd step."""
+    from d3rlpy_amd.algos.td3_plus_bc import TD3PlusBC
+    from d3rlpy_amd.datasets import get_synthetic_d4rl
+    from td3_helpers import make_td3_oracle, td3_oracle_state
+    D, A, B = 3, 1, 100
+    ds = get_synthetic_d4rl("pendulum-random", n=4000, episode_len=200, seed=4)
+    algo = TD3PlusBC(batch_size=B, scaler="standard")
+    algo.scaler.fit_dataset(ds)
+    algo.build_with_dataset(ds)
+    impl = algo.impl
+    mean = np.asarray(algo.scaler._mean, np.float64).reshape(-1)
+    std = np.asarray(algo.scaler._std, np.float64).reshape(-1)
+    orc = make_td3_oracle(D, A, [256, 256], seed=0, scaler_stats=(mean, std))
+    for k, v in impl.get_state_dict().items():
+        getattr(orc, k).load_state_dict(v)
+    np.random.seed(7)
+    algo.fit(ds, n_steps=STEPS, n_steps_per_epoch=STEPS, save_metrics=False, verbose=False,
+             show_progress=False, index_source="numpy")
+    # fit() re-fits the scaler on the same dataset: the same statistics
+    assert np.array_equal(np.asarray(algo.scaler._mean, np.float64).reshape(-1), mean)
+    ws = next(iter(impl._ws.values()))
+    names, ring = impl.read_metrics_ring(None)
+    for s, batch in enumerate(_oracle_batches(_transitions(ds), B, 7)):
+        noise = _philox(B * A, 0, ws.seed, s).view(B, A)
+        m = orc.update(batch, noise, grad_step=s)
+        for j, name in enumerate(names):
+            if name not in m:
+                assert np.isnan(ring[s, j]), (s, name)
+                continue
+            assert abs(ring[s, j] - m[name]) <= 1e-4 * max(1.0, abs(m[name])), \
+                (s, name, ring[s, j], m[name])
+    w = _compare_state(impl.get_state_dict(), td3_oracle_state(orc),
+                       ("_q_func", "_targ_q_func", "_policy", "_targ_policy"), 1e-4)
+    print(f"TD3+BC fit production path: {STEPS} steps, max |param diff| {w:.2e}")
