@@ -382,6 +382,14 @@ constexpr Variant kVariants[] = {
     {1, 1, 2, 2, 64},  // 8: 64x64   BK64
     {1, 1, 1, 1, 8},   // 9: register-direct 32x32, K split over waves (gemm_rd_kernel)
     {1, 2, 1, 1, 8},   // 10: register-direct 32x64
+    {1, 2, 1, 4, 32},  // 11: 32x256  BK32, 4 waves 32x64 (tall-skinny: A read once)
+    {1, 2, 2, 4, 32},  // 12: 64x256  BK32, 8 waves 32x64
+    {2, 2, 2, 4, 16},  // 13: 128x256 BK16, 8 waves 64x64
+    {1, 1, 4, 4, 32},  // 14: 128x128 BK32, 16 waves 32x32
+    {1, 2, 4, 2, 16},  // 15: 128x128 BK16, 8 waves 32x64
+    {2, 1, 2, 4, 16},  // 16: 128x128 BK16, 8 waves 64x32
+    {1, 1, 2, 4, 32},  // 17: 64x128  BK32, 8 waves 32x32
+    {1, 1, 4, 2, 32},  // 18: 128x64  BK32, 8 waves 32x32
 };
 constexpr int kFirstRd = 9;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
@@ -436,6 +444,14 @@ void launch_modes(const Params& p, int variant, hipStream_t st) {
     case 6: launch_v<AM, BMd, 6>(p, st); break;
     case 7: launch_v<AM, BMd, 7>(p, st); break;
     case 8: launch_v<AM, BMd, 8>(p, st); break;
+    case 11: launch_v<AM, BMd, 11>(p, st); break;
+    case 12: launch_v<AM, BMd, 12>(p, st); break;
+    case 13: launch_v<AM, BMd, 13>(p, st); break;
+    case 14: launch_v<AM, BMd, 14>(p, st); break;
+    case 15: launch_v<AM, BMd, 15>(p, st); break;
+    case 16: launch_v<AM, BMd, 16>(p, st); break;
+    case 17: launch_v<AM, BMd, 17>(p, st); break;
+    case 18: launch_v<AM, BMd, 18>(p, st); break;
     default: launch_v<AM, BMd, 0>(p, st); break;
   }
 }
@@ -447,14 +463,21 @@ void launch_modes(const Params& p, int variant, hipStream_t st) {
 //    least 32 k per split: the register-direct split-K kernel (9), 1.7-2.6x
 //    faster than any LDS tile on the 256-row policy / target / actor layers
 //    and the narrow first-layer input gradients;
-//  - otherwise the 64x64 LDS tile (0), within 5 % of the best LDS variant on
-//    the large critic passes;
+//  - large problems with both output dimensions >= 128 and >= 64 such tiles:
+//    the 128x128 tile of sixteen 32x32 waves, BK 32 (14) — four waves per
+//    SIMD hide the LDS and global latency the 4-wave tiles expose (K2 critic
+//    backward, profiles/r02_gemm_sweep.log: dW 33.8 vs 39.2 us, dX 35.2 vs
+//    40.6 us for the 64x64 tile);
+//  - otherwise the 64x64 LDS tile (0);
 //  - tiny K (the first layer's 11-17 inputs): one-wave 32x32 tile (6).
 int choose_variant(const Params& p) {
   const int64_t blocks64 =
       ((p.M + 63) / 64) * ((p.N + 63) / 64) * p.batch * p.batch2 * p.splits;
+  const int64_t blocks128 =
+      ((p.M + 127) / 128) * ((p.N + 127) / 128) * p.batch * p.batch2 * p.splits;
   const int64_t kslice = (p.K + p.splits - 1) / p.splits;
   if (kslice >= 32 && (blocks64 < 128 || p.M <= 32 || p.N <= 32)) return 9;
+  if (p.M >= 128 && p.N >= 128 && blocks128 >= 64 && kslice >= 192) return 14;
   if (blocks64 >= 128) return 0;
   return 6;
 }

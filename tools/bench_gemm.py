@@ -33,8 +33,8 @@ def main():
         "dW2[2x256x256x7936] s31": (2 * C * Rc * H * H, lambda v: ops.linear_bwd_w(
             dZ.data_ptr(), H, Rc * H, Xc.data_ptr(), H, Rc * H, dW.data_ptr(), C, Rc, H, H, 31,
             db=db.data_ptr(), variant=v)),
-        "dW2[2x256x256x7936] s8": (2 * C * Rc * H * H, lambda v: ops.linear_bwd_w(
-            dZ.data_ptr(), H, Rc * H, Xc.data_ptr(), H, Rc * H, dW.data_ptr(), C, Rc, H, H, 8,
+        "dW2[2x256x256x7936] s16": (2 * C * Rc * H * H, lambda v: ops.linear_bwd_w(
+            dZ.data_ptr(), H, Rc * H, Xc.data_ptr(), H, Rc * H, dW.data_ptr(), C, Rc, H, H, 16,
             db=db.data_ptr(), variant=v)),
         "dX[2x7936x256x256]+mask": (2 * C * Rc * H * H, lambda v: ops.gemm(
             dZ.data_ptr(), W.data_ptr(), out.data_ptr(), Rc, H, H, batch=C, sA=(Rc * H, H, 1),
@@ -45,10 +45,11 @@ def main():
             sB=(H * H, 1, H), sC=(R * H, H, 1), bias=b.data_ptr(), sbias=H, relu=True,
             variant=v)),
     }
-    variants = list(range(9))
+    variants = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else \
+        [0, 3, 5, 11, 12, 13, 14, 15, 16, 17, 18]
     res = {k: {v: [] for v in variants} for k in shapes}
     reps = 20
-    for rnd in range(5):
+    for rnd in range(3):
         for name, (flops, fn) in shapes.items():
             for v in variants:
                 for _ in range(2):
