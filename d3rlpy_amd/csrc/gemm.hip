@@ -264,7 +264,8 @@ __device__ __forceinline__ float4 rd_load(const float* base, int64_t sx, int64_t
 
 template <int AMODE, int BMODE, int KW, int WN, int U>
 __global__ __launch_bounds__(64 * KW) void gemm_rd_kernel(Params p) {
-  __shared__ float red[(KW > 1 ? KW - 1 : 1) * WN * 16 * 64];
+  // every wave's partial tile: red[w][j*16 + r][lane]
+  __shared__ float red[(KW > 1 ? KW : 1) * WN * 16 * 64];
   __shared__ double rsum[KW * 32];
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
@@ -316,29 +317,22 @@ __global__ __launch_bounds__(64 * KW) void gemm_rd_kernel(Params p) {
     }
   }
 
-  if (KW > 1) {
-    if (w > 0) {
-#pragma unroll
-      for (int j = 0; j < WN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) red[(((w - 1) * WN + j) * 16 + r) * 64 + lane] = acc[j][r];
-    }
-  }
   if (do_rowsum) {
     rs += __shfl_xor(rs, 32, 64);
     if (lg == 0) rsum[w * 32 + li] = rs;
   }
-  __syncthreads();
-  if (w != 0) return;
+  // The KW partial tiles are summed in wave order 0, 1, ..., KW-1 for every
+  // element (deterministic); the WN * 16 accumulator slots are shared out
+  // over the waves, so the reduction runs KW-wide instead of on wave 0 alone.
+  constexpr int SLOTS = WN * 16;
   if (KW > 1) {
 #pragma unroll
-    for (int v = 1; v < KW; ++v)
+    for (int j = 0; j < WN; ++j)
 #pragma unroll
-      for (int j = 0; j < WN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] += red[(((v - 1) * WN + j) * 16 + r) * 64 + lane];
+      for (int r = 0; r < 16; ++r) red[((w * WN + j) * 16 + r) * 64 + lane] = acc[j][r];
   }
-  if (do_rowsum && lg == 0 && m < p.M) {
+  __syncthreads();
+  if (do_rowsum && w == 0 && lg == 0 && m < p.M) {
     double tot = 0.0;
     for (int v = 0; v < KW; ++v) tot += rsum[v * 32 + li];
     p.rowsum[b * p.sRb + s * p.sRs + m] = (float)tot;
@@ -346,23 +340,30 @@ __global__ __launch_bounds__(64 * KW) void gemm_rd_kernel(Params p) {
   float* Cb = p.C + b * p.sCb + t2 * p.sCb2 + s * p.sCs;
   const float* biasb = p.bias ? p.bias + b * p.sbias_b + t2 * p.sbias_b2 : nullptr;
   const float* maskb = p.mask ? p.mask + b * p.sMb + t2 * p.sMb2 : nullptr;
-#pragma unroll
-  for (int j = 0; j < WN; ++j) {
+  auto emit = [&](int j, int r, float v) {
     const int64_t n = n0 + 32 * j + li;
-    if (n >= p.N) continue;
-    const float bn = biasb ? biasb[n] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * lg;
-      if (mm < p.M) {
-        float v = acc[j][r] * p.alpha;
-        if (biasb) v += bn;
-        if (p.relu) v = fmaxf(v, 0.f);
-        if (maskb && !(maskb[mm * p.sMm + n * p.sMn] > 0.f)) v = 0.f;
-        float* dst = Cb + mm * p.sCm + n * p.sCn;
-        if (p.accumulate) *dst += v; else *dst = v;
-      }
+    const int64_t mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * lg;
+    if (n < p.N && mm < p.M) {
+      v = v * p.alpha;
+      if (biasb) v += biasb[n];
+      if (p.relu) v = fmaxf(v, 0.f);
+      if (maskb && !(maskb[mm * p.sMm + n * p.sMn] > 0.f)) v = 0.f;
+      float* dst = Cb + mm * p.sCm + n * p.sCn;
+      if (p.accumulate) *dst += v; else *dst = v;
     }
+  };
+  if constexpr (KW > 1) {
+    for (int q = w; q < SLOTS; q += KW) {
+      const int j = q / 16, r = q % 16;
+      float v = red[(j * 16 + r) * 64 + lane];
+      for (int u = 1; u < KW; ++u) v += red[((u * WN + j) * 16 + r) * 64 + lane];
+      emit(j, r, v);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) emit(j, r, acc[j][r]);
   }
 }
 

@@ -57,6 +57,15 @@ def main():
     np.save(os.path.join(work, f"seed{rank}.npy"), np.array(impl._workspace(sl.stop - sl.start).seed))
     if rank == 0:
         torch.save(impl.get_state_dict(), os.path.join(work, "dp_state.pt"))
+        # the gradients the last Adam steps consumed: all-reduced SUM x 1/world
+        sc = impl._dp.scale
+        g = {}
+        for key, refs, getter in (("_q_func", impl._critic_refs(), impl.critic_grad),
+                                  ("_policy", impl._policy_refs(), impl.policy_grad)):
+            for k, seg, member, sl in refs:
+                t = getter(seg)[member]
+                g[f"{key}/{k}"] = ((t if sl is None else t[sl]) * sc).detach().cpu().clone()
+        torch.save(g, os.path.join(work, "dp_grads.pt"))
         np.save(os.path.join(work, "dp_metrics.npy"), np.array(metrics))
     dist.barrier()
     dist.destroy_process_group()
