@@ -125,21 +125,19 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
   }
 }
 
-// Adam on a single scalar parameter (torch single-tensor path); returns new p.
-// bc = {1 - b1^t, 1 - b2^t} for t = *step + 1 (precomputed, see adam_bias_corrections).
-__device__ float adam_scalar(float* p, float* m, float* v, int64_t* step, float g, double lr,
-                             double b1, double b2, double eps, const double* bc) {
-  const int64_t t = *step + 1;
-  float mm = fmaf((float)(1.0 - b1), __fsub_rn(g, *m), *m);
-  float vv = __fmul_rn(*v, (float)b2);
+// Adam on a single scalar parameter (torch single-tensor path) held in
+// registers; returns the new p, updates m / v (the caller stores them).
+// bc = {1 - b1^t, 1 - b2^t} for the step t being taken.
+__device__ __forceinline__ float adam_scalar_r(float p, float& m, float& v, float g, double lr,
+                                               double b1, double b2, double eps, const double* bc) {
+  float mm = fmaf((float)(1.0 - b1), __fsub_rn(g, m), m);
+  float vv = __fmul_rn(v, (float)b2);
   vv = __fadd_rn(vv, __fmul_rn(__fmul_rn((float)(1.0 - b2), g), g));
-  const double bc1 = bc[0];
-  const double bc2 = bc[1];
-  const float step_size = (float)(lr / bc1);
-  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vv), (float)sqrt(bc2)), (float)eps);
-  const float pn = __fadd_rn(*p, __fmul_rn(-step_size, __fdiv_rn(mm, denom)));
-  *m = mm; *v = vv; *p = pn; *step = t;
-  return pn;
+  const float step_size = (float)(lr / bc[0]);
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vv), (float)sqrt(bc[1])), (float)eps);
+  m = mm;
+  v = vv;
+  return __fadd_rn(p, __fmul_rn(-step_size, __fdiv_rn(mm, denom)));
 }
 
 // logsumexp over the 3N importance-sampled values of (c, b) in set s.
@@ -185,45 +183,72 @@ __global__ __launch_bounds__(256) void cql_lse_kernel(d3a_cql_loss_desc d) {
 
 // Stage B (one workgroup): temperature and alpha Adam steps, TD loss, and
 // final dL/dQ (scales stage A's softmax weights by the new clipped alpha).
+// Latency-bound (one CU): every input is loaded up front — the per-row values
+// into registers (LOSS_MP slots per thread, the same p = tid + i * nt order
+// the sums use), the scalar optimiser states by thread 0 — so the stage pays
+// about one global round trip instead of one per phase.
+constexpr int LOSS_MP = 8;
+
 __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   __shared__ float scratch[16];
   __shared__ float sh[4];
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int64_t B = d.B, C = d.C, N = d.N, NB = N * B;
-
-  // dp_phase 0: compute the scalar gradients and apply Adam here; 1: only
-  // compute them (-> scalar_grads, for the data-parallel all-reduce) and
-  // stop; 2: apply Adam to the all-reduced scalar_grads * grad_scale, then
-  // continue with the critic.
-  const int phase = d.dp_phase;
-
-  // Adam bias corrections 1 - beta^t of the temperature and alpha steps (fp64
-  // pow, as torch computes them in Python floats), one per wave so the four
-  // library pows run concurrently instead of in thread 0's serial path
   __shared__ double s_bc[4];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int64_t B = d.B, C = d.C, N = d.N, NB = N * B, CB = C * B;
+  const int phase = d.dp_phase;
+  const bool temp_on = d.update_temp != 0, alpha_on = d.update_alpha != 0;
+  const bool critic_on = d.update_critic != 0 && phase != 1;
+  const bool cons_on = d.conservative != 0;
+
+  // ---- prefetch ----
+  // Adam bias corrections 1 - beta^t (fp64 pow, as torch computes them in
+  // Python floats), one per wave so the four library pows run concurrently
   {
-    const bool apply = phase != 1;
     const int w = tid >> 6;
-    if ((tid & 63) == 0 && w < 4 && apply &&
-        (w < 2 ? d.update_temp : d.update_alpha)) {
+    if ((tid & 63) == 0 && w < 4 && phase != 1 && (w < 2 ? temp_on : alpha_on)) {
       const int64_t t = (w < 2 ? *d.temp_step : *d.alpha_step) + 1;
       s_bc[w] = 1.0 - pow((w & 1) ? d.beta2 : d.beta1, (double)t);
     }
-    __syncthreads();
   }
+  float r_lseA[LOSS_MP], r_qd[LOSS_MP], r_lseC[LOSS_MP], r_tq[LOSS_MP], r_rw[LOSS_MP],
+      r_tm[LOSS_MP], r_ns[LOSS_MP];
+  float ltemp = 0.f, tm_ = 0.f, tv_ = 0.f, lalpha = 0.f, am_ = 0.f, av_ = 0.f;
+  if (tid == 0) {
+    ltemp = *d.log_temp;
+    lalpha = *d.log_alpha;
+    if (temp_on) { tm_ = *d.temp_m; tv_ = *d.temp_v; }
+    if (alpha_on) { am_ = *d.alpha_m; av_ = *d.alpha_v; }
+  }
+  float s_temp = 0.f;
+  if (temp_on && phase != 2)
+    for (int64_t b = tid; b < B; b += nt) s_temp += d.logp_temp[b] - (float)d.A;
+#pragma unroll
+  for (int i = 0; i < LOSS_MP; ++i) {
+    const int64_t p = tid + (int64_t)i * nt;
+    r_lseA[i] = r_qd[i] = r_lseC[i] = r_tq[i] = r_rw[i] = r_tm[i] = r_ns[i] = 0.f;
+    if (p >= CB) continue;
+    const int64_t c = p / B, b = p % B;
+    if ((alpha_on && phase != 2) || critic_on) r_qd[i] = d.q[c * d.R + 6 * NB + b];
+    if (alpha_on && phase != 2) r_lseA[i] = d.lse[c * B + b];
+    if (critic_on) {
+      float tq = d.q_targ[b];
+      for (int64_t k = 1; k < C; ++k) tq = fminf(tq, d.q_targ[k * B + b]);
+      r_tq[i] = tq;
+      r_rw[i] = d.rew[b];
+      r_tm[i] = d.term[b];
+      r_ns[i] = d.n_steps[b];
+      if (cons_on) r_lseC[i] = d.lse[(C + c) * B + b];
+    }
+  }
+  __syncthreads();  // s_bc
 
   // ---- update_temp (sac_impl.py:123-146) ----
-  if (d.update_temp) {
-    float tsum = 0.f;
-    if (phase != 2) {
-      float s = 0.f;
-      for (int64_t b = tid; b < B; b += nt) s += d.logp_temp[b] - (float)d.A;
-      tsum = block_sum(s, scratch);
-    }
+  if (temp_on) {
+    const float tsum = phase != 2 ? block_sum(s_temp, scratch) : 0.f;
     if (tid == 0) {
       float g = 0.f;
       if (phase != 2) {
-        const float e = expf(*d.log_temp);
+        const float e = expf(ltemp);
         // loss = -(exp(log_temp) * targ_temp).mean()
         d.metrics[0] = -(e * tsum) / (float)B;
         g = (-1.f / (float)B) * tsum * e;
@@ -232,23 +257,25 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
         d.scalar_grads[0] = g;
       } else {
         if (phase == 2) g = d.scalar_grads[0] * d.grad_scale;
-        const float ln = adam_scalar(d.log_temp, d.temp_m, d.temp_v, d.temp_step, g, d.temp_lr,
-                                     d.beta1, d.beta2, d.adam_eps, s_bc);
+        float* pm = d.temp_m; float* pv = d.temp_v;
+        const float ln = adam_scalar_r(ltemp, tm_, tv_, g, d.temp_lr, d.beta1, d.beta2,
+                                       d.adam_eps, s_bc);
+        *pm = tm_; *pv = tv_; *d.log_temp = ln; *d.temp_step = *d.temp_step + 1;
+        ltemp = ln;
         d.metrics[1] = expf(ln);
       }
     }
   }
-  __syncthreads();
 
   // ---- update_alpha (cql_impl.py:119-141) on sample set 0 ----
-  if (d.update_alpha) {
+  if (alpha_on) {
     float lsum = 0.f, dsum = 0.f;
     if (phase != 2) {
       float sl = 0.f, sd = 0.f;
-      for (int64_t p = tid; p < C * B; p += nt) {
-        const int64_t c = p / B, b = p % B;
-        sl += d.lse[c * B + b];
-        sd += d.q[c * d.R + 6 * NB + b];
+#pragma unroll
+      for (int i = 0; i < LOSS_MP; ++i) {
+        sl += r_lseA[i];
+        sd += r_qd[i];
       }
       lsum = block_sum(sl, scratch);
       dsum = block_sum(sd, scratch);
@@ -256,9 +283,9 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
     if (tid == 0) {
       float g = 0.f;
       if (phase != 2) {
-        const float loss = lsum / (float)(C * B) - dsum / (float)(C * B);
+        const float loss = lsum / (float)CB - dsum / (float)CB;
         const float scaled = d.conservative_weight * loss;
-        const float e = expf(*d.log_alpha);
+        const float e = expf(lalpha);
         const float ca = fminf(fmaxf(e, 0.f), 1e6f);
         const float cons = ca * (scaled - d.alpha_threshold);
         const bool pass = (e >= 0.f) && (e <= 1e6f);
@@ -269,43 +296,45 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
         d.scalar_grads[1] = g;
       } else {
         if (phase == 2) g = d.scalar_grads[1] * d.grad_scale;
-        const float ln = adam_scalar(d.log_alpha, d.alpha_m, d.alpha_v, d.alpha_step, g,
-                                     d.alpha_lr, d.beta1, d.beta2, d.adam_eps, s_bc + 2);
+        float* pm = d.alpha_m; float* pv = d.alpha_v;
+        const float ln = adam_scalar_r(lalpha, am_, av_, g, d.alpha_lr, d.beta1, d.beta2,
+                                       d.adam_eps, s_bc + 2);
+        *pm = am_; *pv = av_; *d.log_alpha = ln; *d.alpha_step = *d.alpha_step + 1;
+        lalpha = ln;
         d.metrics[3] = expf(ln);
       }
     }
   }
   if (phase == 1) return;
-  __syncthreads();
   if (tid == 0) {
-    sh[0] = fminf(fmaxf(expf(*d.log_alpha), 0.f), 1e6f);
-    sh[1] = expf(*d.log_temp);  // the temperature after update_temp
+    sh[0] = fminf(fmaxf(expf(lalpha), 0.f), 1e6f);
+    sh[1] = expf(ltemp);  // the temperature after update_temp
     d.scalars[0] = sh[1];
     d.scalars[1] = sh[0];
   }
   __syncthreads();
   const float ca = sh[0];
   const float temp = sh[1];
-  const bool cons_on = d.conservative != 0;
 
-  if (!d.update_critic) return;
+  if (!critic_on) return;
   // ---- update_critic loss and dL/dQ (ddpg_impl.py:138-165, cql_impl.py:110-117) ----
-  const float gcons = cons_on ? ca * d.conservative_weight / (float)(C * B) : 0.f;
+  const float gcons = cons_on ? ca * d.conservative_weight / (float)CB : 0.f;
   float s_td = 0.f, s_l = 0.f, s_d = 0.f;
-  for (int64_t p = tid; p < C * B; p += nt) {
+#pragma unroll
+  for (int i = 0; i < LOSS_MP; ++i) {
+    const int64_t p = tid + (int64_t)i * nt;
+    if (p >= CB) continue;
     const int64_t c = p / B, b = p % B;
-    // target: min over target critics
-    float tq = d.q_targ[b];
-    for (int64_t k = 1; k < C; ++k) tq = fminf(tq, d.q_targ[k * B + b]);
+    float tq = r_tq[i];
     // soft backup: target - exp(log_temp) * log_prob (sac_impl.py:156-162)
     if (d.soft_target) tq = tq - temp * d.logp_targ[b];
-    const float gam = powf(d.gamma, d.n_steps[b]);
-    const float y = d.rew[b] + gam * tq * (1.f - d.term[b]);
-    const float qd = d.q[c * d.R + 6 * NB + b];
+    const float gam = powf(d.gamma, r_ns[i]);
+    const float y = r_rw[i] + gam * tq * (1.f - r_tm[i]);
+    const float qd = r_qd[i];
     const float diff = qd - y;
     s_td += diff * diff;
     s_d += qd;
-    if (cons_on) s_l += d.lse[(C + c) * B + b];
+    if (cons_on) s_l += r_lseC[i];
     d.dq[c * d.R + 6 * NB + b] = 2.f * diff / (float)B - gcons;
   }
   // critic-set IS rows keep the unscaled softmax weights of stage A; the
@@ -315,7 +344,7 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   const float lsum = block_sum(s_l, scratch);
   const float dsum = block_sum(s_d, scratch);
   if (tid == 0) {
-    const float loss = lsum / (float)(C * B) - dsum / (float)(C * B);
+    const float loss = lsum / (float)CB - dsum / (float)CB;
     const float cons = cons_on ? ca * (d.conservative_weight * loss - d.alpha_threshold) : 0.f;
     d.metrics[4] = cons_on ? td + cons : td;
     d.metrics[6] = td;
@@ -441,6 +470,8 @@ extern "C" int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream) {
   D3A_CHECK_ARG(d->conservative || !d->update_alpha,
                 "d3a_cql_loss: update_alpha needs the conservative term");
   D3A_CHECK_ARG(!d->conservative || d->N >= 1, "d3a_cql_loss: the conservative term needs N >= 1");
+  D3A_CHECK_ARG((int64_t)d->C * d->B <= (int64_t)LOSS_MP * 1024,
+                "d3a_cql_loss: n_critics * batch must be <= 8192");
   // phase 2 reuses the logsumexp / softmax weights phase 1 wrote
   if (d->conservative && (d->update_alpha || d->update_critic) && d->dp_phase != 2) {
     const int64_t waves = 2LL * d->C * d->B;
