@@ -221,17 +221,17 @@ def measure_kernel(ws_obj, reps: int = 50):
     return avg_s, flops, desc
 
 
-def cpu_baseline(seconds: float, threads: int, name: str = "cql"):
-    """The oracle update (torch CPU, op for op) + the reference's host sampler
-    restated (per-sample np.random.randint + TransitionMiniBatch gather)."""
+def cpu_step_fn(name: str = "cql"):
+    """One step of the CPU baseline: the oracle update (torch CPU, op for op)
+    + the reference's host sampler restated (per-sample np.random.randint +
+    TransitionMiniBatch gather).  Returns step() -> None."""
     import torch
     from oracle.cql import Batch, CQLNoise, CQLOracle
     from oracle.gather import gather, random_indices, synthetic_dataset, to_episodes, to_transitions
-    torch.set_num_threads(threads)
     B = WORKLOADS[name][1]
     gen = torch.Generator().manual_seed(0)
     if name == "dcql":
-        return _cpu_baseline_dcql(seconds, B, gen)
+        return _cpu_step_dcql(B, gen)
     n = 100_000
     D, A = {"cql": (11, 3), "cqldp": (29, 8), "td3bc": (3, 1), "bcq": (17, 6)}[name]
     obs, act, rew, term = synthetic_dataset(n, D, A, episode_len=1000, seed=0)
@@ -265,7 +265,15 @@ def cpu_baseline(seconds: float, threads: int, name: str = "cql"):
                                  b["next_observations"], b["terminals"], b["n_steps"])
         update(batch, cnt[0])
         cnt[0] += 1
+    return step
 
+
+def cpu_baseline(seconds: float, threads: int, name: str = "cql"):
+    """Bounded sample: steps/s of cpu_step_fn over ~``seconds`` after 2 warm-up
+    steps with ``threads`` torch threads -> (steps/s, steps, seconds)."""
+    import torch
+    torch.set_num_threads(threads)
+    step = cpu_step_fn(name)
     for _ in range(2):
         step()
     t0 = time.perf_counter()
@@ -279,7 +287,7 @@ def cpu_baseline(seconds: float, threads: int, name: str = "cql"):
     return k / el, k, el
 
 
-def _cpu_baseline_dcql(seconds: float, B: int, gen):
+def _cpu_step_dcql(B: int, gen):
     """K5 on the host: the oracle DiscreteCQL-IQN update + the reference
     sampler restated (4-frame stacks) over 20k synthetic 84x84 frames."""
     import torch
@@ -306,17 +314,27 @@ def _cpu_baseline_dcql(seconds: float, B: int, gen):
                         torch.from_numpy(b["rewards"]), torch.from_numpy(b["next_observations"]),
                         torch.from_numpy(b["terminals"]), torch.from_numpy(b["n_steps"]))
         orc.update(pb, IQNTaus.draw(gen, B, 64))
+    return step
 
-    step()
-    t0 = time.perf_counter()
-    k = 0
-    while True:
-        step()
-        k += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return k / el, k, el
+
+def host_cpu() -> dict:
+    """The host CPU as this process sees it: model, logical CPUs of the
+    machine, this process's CPU share (affinity) and the thread count the
+    all-cores baseline uses (OMP_NUM_THREADS when set, else the share)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    share = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(share, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else share
+    return {"model": model, "machine_cpus": os.cpu_count(), "process_cpus": share,
+            "threads": threads}
 
 
 def _selftest(args) -> None:
@@ -371,7 +389,8 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--transitions", type=int, default=1_000_000)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds-1t", type=float, default=6.0)
     ap.add_argument("--algo", choices=sorted(WORKLOADS), default="cql",
                     help="cql = the BASELINE.json headline (K2); td3bc = K1 shapes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -438,8 +457,10 @@ def main():
     cpu = None
     # the CPU baseline is a rank-0, single-GPU-run measurement (not repeated per N)
     if not args.no_cpu_baseline and ws == 1:
-        threads = min(16, os.cpu_count() or 1)
+        host = host_cpu()
+        threads = args.cpu_threads or host["threads"]
         sps, k, el = cpu_baseline(args.cpu_seconds, threads, args.algo)
+        sps1, k1, el1 = cpu_baseline(args.cpu_seconds_1t, 1, args.algo)
         what = {"cql": "CQL update (torch CPU, op-for-op restatement of cql_impl.py/"
                        "sac_impl.py/ddpg_impl.py)",
                 "cqldp": "CQL update at antmaze shapes, batch 256 (torch CPU, op-for-op "
@@ -454,8 +475,24 @@ def main():
                "kind": "port",
                "sample": f"oracle {what} + reference host sampler restated "
                          f"(np.random.randint per sample + TransitionMiniBatch gather) on a "
-                         f"100k-transition synthetic dataset; {k} steps in {el:.1f}s, "
-                         f"{threads} threads"}
+                         f"100k-transition synthetic dataset; bounded live sample: {k} steps "
+                         f"in {el:.1f}s on {threads} threads (this process's CPU share)",
+               "one_thread": {"value": round(sps1, 3), "cores": 1,
+                              "sample": f"{k1} steps in {el1:.1f}s"},
+               "host": host}
+        # BASELINE.md's full protocol (>= 1000 steps after 50 warm-up, median
+        # of 5, all cores and 1 thread), run by tools/cpu_baseline_protocol.py
+        proto = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                             f"r02_cpu_baseline_{args.algo}.json")
+        if os.path.exists(proto):
+            with open(proto) as f:
+                pr = json.load(f)
+            cpu["protocol"] = {"file": os.path.relpath(proto, os.path.dirname(
+                os.path.abspath(__file__))), "all_cores_median": round(pr["all_cores"]["median"], 3),
+                "all_cores_threads": pr["all_cores"]["threads"],
+                "one_thread_median": round(pr["one_thread"]["median"], 3),
+                "steps": pr["steps"], "warmup": pr["warmup"], "runs": pr["runs"],
+                "host_model": pr["host"]["model"]}
     # replicas: every rank's steps count; data parallel: one global step per
     # step of all ranks together
     dp = args.algo == "cqldp"

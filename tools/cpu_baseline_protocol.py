@@ -1,0 +1,88 @@
+"""BASELINE.md's CPU-baseline protocol on the GPU box's host (no GPU used).
+
+    python tools/cpu_baseline_protocol.py --algo cql --out profiles/r02_cpu_baseline_cql.json
+
+The step is bench.cpu_step_fn (the oracle's op-for-op CPU update + the
+reference's host sampler restated).  Protocol: `--warmup` (50) untimed steps,
+then `--steps` (1000) timed with time.perf_counter, median of `--runs` (5):
+  * all cores: torch.set_num_threads(<this process's CPU share, capped by
+    OMP_NUM_THREADS>), the runs one after another;
+  * 1 thread: torch.set_num_threads(1); the runs execute concurrently as
+    separate processes pinned to distinct cores of the share (a single-thread
+    run is compute bound, so pinning them apart keeps them independent while
+    the protocol fits one bounded call).
+Writes one JSON file with both medians, every run and the host description;
+bench.py reports it next to its live bounded sample.
+"""
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def timed_run(algo: str, threads: int, steps: int, warmup: int) -> float:
+    import torch
+    import bench
+    torch.set_num_threads(threads)
+    step = bench.cpu_step_fn(algo)
+    for _ in range(warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    return steps / (time.perf_counter() - t0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--algo", default="cql")
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--runs", type=int, default=5)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--single-on-core", type=int, default=None, help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.single_on_core is not None:
+        os.sched_setaffinity(0, {args.single_on_core})
+        print(json.dumps({"sps": timed_run(args.algo, 1, args.steps, args.warmup)}), flush=True)
+        return
+    import bench
+    host = bench.host_cpu()
+    print(f"host {host}", flush=True)
+    allc = []
+    for r in range(args.runs):
+        allc.append(timed_run(args.algo, host["threads"], args.steps, args.warmup))
+        print(f"all cores run {r}: {allc[-1]:.3f} steps/s", flush=True)
+    cores = sorted(os.sched_getaffinity(0))
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--algo", args.algo,
+                               "--steps", str(args.steps), "--warmup", str(args.warmup),
+                               "--single-on-core", str(cores[(2 * r) % len(cores)])],
+                              stdout=subprocess.PIPE, text=True)
+             for r in range(args.runs)]
+    one = []
+    for p in procs:
+        out, _ = p.communicate()
+        assert p.returncode == 0, out
+        one.append(json.loads(out.strip().splitlines()[-1])["sps"])
+    print(f"1-thread runs: {[round(v, 3) for v in one]}", flush=True)
+    res = {"algo": args.algo, "unit": "gradient-steps/s", "steps": args.steps,
+           "warmup": args.warmup, "runs": args.runs,
+           "all_cores": {"threads": host["threads"], "median": statistics.median(allc),
+                         "runs": allc},
+           "one_thread": {"threads": 1, "median": statistics.median(one), "runs": one,
+                          "note": "runs concurrent, pinned to distinct cores"},
+           "host": host}
+    print(json.dumps(res))
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
