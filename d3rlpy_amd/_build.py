@@ -60,7 +60,47 @@ def _compile(src: Path, hdr: str) -> Path:
     return obj
 
 
+TORCH_LIB = PKG / "libd3rlpy_amd_torch.so"
+TORCH_SRC = CSRC / "torch_ops.cpp"
+
+
+def build_torch_ops(verbose: bool = False) -> Path:
+    """libd3rlpy_amd_torch.so: the TORCH_LIBRARY registration of the C-ABI
+    (csrc/torch_ops.cpp), host C++ against the installed torch, linked to
+    libd3rlpy_amd.so (found next to it via $ORIGIN)."""
+    import torch
+    import torch.utils.cpp_extension as ce
+    cxx = shutil.which("g++") or "g++"
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    flags = ["-std=c++17", "-O2", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__=1",
+             "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+             *[f"-I{p}" for p in ce.include_paths()], "-I/opt/rocm/include",
+             f"-I{ROOT / 'include'}"]
+    libs = [*[f"-L{p}" for p in ce.library_paths()], "-ltorch", "-ltorch_cpu", "-lc10",
+            "-lc10_hip", "-ltorch_hip", f"-L{PKG}", "-ld3rlpy_amd", "-Wl,-rpath,$ORIGIN"]
+    h = hashlib.sha256(TORCH_SRC.read_bytes() + (ROOT / "include" / "d3rlpy_amd.h").read_bytes()
+                       + " ".join(flags + libs + [torch.__version__]).encode()).hexdigest()[:16]
+    stamp = BUILD / "torch_ops.stamp"
+    if TORCH_LIB.exists() and stamp.exists() and stamp.read_text() == h:
+        return TORCH_LIB
+    cmd = [cxx, *flags, str(TORCH_SRC), "-o", str(TORCH_LIB) + ".tmp", *libs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"torch op library build failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(str(TORCH_LIB) + ".tmp", TORCH_LIB)
+    stamp.write_text(h)
+    if verbose:
+        print(f"built {TORCH_LIB}")
+    return TORCH_LIB
+
+
 def build(verbose: bool = False) -> Path:
+    lib = _build_hip(verbose)
+    build_torch_ops(verbose)
+    return lib
+
+
+def _build_hip(verbose: bool = False) -> Path:
     BUILD.mkdir(exist_ok=True)
     hdr = _headers_digest()
     srcs = sorted(CSRC.glob("*.hip"))

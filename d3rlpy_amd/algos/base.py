@@ -67,10 +67,11 @@ class AlgoBase(LearnableBase):
                                 show_progress=show_progress, tensorboard_dir=tensorboard_dir,
                                 timelimit_aware=timelimit_aware, callback=callback)
 
-    def save_policy(self, fname: str) -> None:
-        """algos/base.py:77-103: greedy policy as TorchScript (.pt) or ONNX (.onnx)."""
+    def save_policy(self, fname: str, hip_ops: bool = False) -> None:
+        """algos/base.py:77-103: greedy policy as TorchScript (.pt) or ONNX (.onnx);
+        ``hip_ops`` (extension): MLPs through torch.ops.d3rlpy_amd.mlp_forward."""
         assert self._impl is not None, IMPL_NOT_INITIALIZED_ERROR
-        self._impl.save_policy(fname)
+        self._impl.save_policy(fname, hip_ops=hip_ops)
 
     def copy_policy_from(self, algo: "AlgoBase") -> None:
         assert self._impl is not None and algo.impl is not None, IMPL_NOT_INITIALIZED_ERROR

@@ -143,12 +143,20 @@ class ImplBase:
             return mean_values, stds
         return mean_values
 
-    def save_policy(self, fname: str) -> None:
+    def save_policy(self, fname: str, hip_ops: bool = False) -> None:
         """algos/torch/base.py:87-127: the greedy policy (behind the scalers)
-        as TorchScript ``.pt`` or ``.onnx``, built by ``_policy_module``."""
-        from ..export import save_traced
-        save_traced(self._policy_module(), self._observation_shape, self.torch_device, fname,
-                    self._scaler, self._action_scaler)
+        as TorchScript ``.pt`` or ``.onnx``, built by ``_policy_module``.
+        ``hip_ops=True`` (extension): MLP trunks call the registered HIP op
+        torch.ops.d3rlpy_amd.mlp_forward instead of plain torch layers."""
+        from .. import export
+        prev = export._HIP_OPS
+        export._HIP_OPS = bool(hip_ops)
+        try:
+            module = self._policy_module()
+        finally:
+            export._HIP_OPS = prev
+        export.save_traced(module, self._observation_shape, self.torch_device, fname,
+                           self._scaler, self._action_scaler)
 
     def _policy_module(self) -> torch.nn.Module:
         raise NotImplementedError

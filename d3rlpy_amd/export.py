@@ -18,10 +18,39 @@ from torch import nn
 
 from .nets import EnsembleMLP, ParamStore
 
+# save_policy(..., hip_ops=True): MLP trunks export as one call of the
+# registered custom op torch.ops.d3rlpy_amd.mlp_forward (the HIP GEMM kernels;
+# loading the program needs d3rlpy_amd.torch_ops.load() first) instead of the
+# portable plain-torch Linear / ReLU chain
+_HIP_OPS = False
 
-def mlp_module(net: EnsembleMLP, store: ParamStore, member: int = 0) -> nn.Sequential:
+
+class HipMLP(nn.Module):
+    """An ensemble member's ReLU MLP through torch.ops.d3rlpy_amd.mlp_forward
+    (scriptable / traceable: the op is registered with TORCH_LIBRARY)."""
+
+    def __init__(self, Ws, bs):
+        super().__init__()
+        from . import torch_ops
+        torch_ops.load()
+        self.Ws = nn.ParameterList([nn.Parameter(W.detach().clone(), requires_grad=False)
+                                    for W in Ws])
+        self.bs = nn.ParameterList([nn.Parameter(b.detach().clone(), requires_grad=False)
+                                    for b in bs])
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        Ws = [w for w in self.Ws]
+        bs = [b for b in self.bs]
+        return torch.ops.d3rlpy_amd.mlp_forward(x.contiguous(), Ws, bs)
+
+
+def mlp_module(net: EnsembleMLP, store: ParamStore, member: int = 0) -> nn.Module:
     """Member ``member`` of an ensemble as Linear / ReLU layers (encoders.py:265-275
-    + the linear head), weights copied from ``store``."""
+    + the linear head), weights copied from ``store`` (or, under
+    save_policy(hip_ops=True), as one HipMLP)."""
+    if _HIP_OPS:
+        pairs = [net.export_linear(l, member, store) for l in range(net.n_layers)]
+        return HipMLP([W for W, _ in pairs], [b for _, b in pairs])
     layers = []
     for l in range(net.n_layers):
         W, b = net.export_linear(l, member, store)
