@@ -111,6 +111,30 @@ class EnsembleQRQFunction(nn.Module):
         return self._q_funcs
 
 
+def gather_quantiles_by_indices(y: torch.Tensor, indices: torch.Tensor) -> torch.Tensor:
+    """ensemble_q_function.py:25-42 (the 3-D case: (N, batch, K) -> (batch, K))."""
+    assert y.dim() == 3
+    return y.transpose(0, 1)[torch.arange(y.shape[1]), indices]
+
+
+def reduce_quantile_ensemble(y: torch.Tensor, reduction: str = "min", dim: int = 0,
+                             lam: float = 0.75) -> torch.Tensor:
+    """ensemble_q_function.py:45-66: pick each row's member by the mean of its
+    quantiles (min / max), or mix the two picks."""
+    mean = y.mean(dim=-1)
+    if reduction == "min":
+        return gather_quantiles_by_indices(y, mean.min(dim=dim).indices)
+    if reduction == "max":
+        return gather_quantiles_by_indices(y, mean.max(dim=dim).indices)
+    if reduction == "none":
+        return y
+    if reduction == "mix":
+        mn = gather_quantiles_by_indices(y, mean.min(dim=dim).indices)
+        mx = gather_quantiles_by_indices(y, mean.max(dim=dim).indices)
+        return lam * mn + (1.0 - lam) * mx
+    raise ValueError("invalid reduction type.")
+
+
 def compute_max_with_n_actions(x, actions, q_func: EnsembleQRQFunction, lam: float):
     """q_functions/__init__.py:8-72 (first return value)."""
     batch_size = actions.shape[0]
