@@ -10,11 +10,14 @@ gathered by the oracle's TransitionMiniBatch, and each step's device draws
 reproduced with d3a_philox_fill at that step's Philox counter (the sampler
 kernels draw bit-identically to it: test_cql_sample_draws_equal_philox_fill).
 
-Bars (a 12-step trajectory without re-synchronisation; relu masks and Adam's
-near-zero-gradient entries let the two fp32 trajectories separate slowly, as
-in test_cql_trajectory_drift): every logged loss within 1e-4 relative,
-parameters and targets within 1e-4 absolute; the index stream and the
-reproduced draws themselves are exact.
+Bars (a 12-step trajectory without re-synchronisation): every logged loss
+within 1e-4 relative; parameters and targets: at least 99.9 % of the entries of
+every network within 1e-5 and all within 1e-3.  The two fp32 trajectories
+separate only where Adam's first steps amplify a near-zero gradient entry
+(lr * g / (|g| + eps): a rounding-level difference in g can move such an entry
+by up to 2 * lr; proven entry by entry for single steps in
+tests/test_gpu_arbiters.py) — isolated entries that then stay apart.  The index
+stream and the reproduced draws themselves are exact.
 """
 import numpy as np
 import pytest
@@ -56,13 +59,18 @@ def _philox(n_normal, n_uniform, seed, counter):
     return buf.cpu()
 
 
-def _compare_state(sd, ref, keys, tol):
-    worst = 0.0
+def _compare_state(sd, ref, keys):
+    """(max |diff|, fraction of entries beyond 1e-5) over the networks."""
+    worst, n_off, n_all = 0.0, 0, 0
     for k in keys:
         for n, t in ref[k].items():
-            worst = max(worst, float((sd[k][n] - t).abs().max()))
-    assert worst <= tol, worst
-    return worst
+            d = (sd[k][n] - t).abs()
+            worst = max(worst, float(d.max()))
+            n_off += int((d > 1e-5).sum())
+            n_all += d.numel()
+    frac = n_off / n_all
+    assert worst <= 1e-3 and frac <= 1e-3, (worst, frac)
+    return worst, frac
 
 
 def test_cql_fit_production_path_vs_oracle():
@@ -105,12 +113,12 @@ def test_cql_fit_production_path_vs_oracle():
             e = abs(ring[s, j] - m[name]) / max(1.0, abs(m[name]))
             worst_m = max(worst_m, e)
             assert e <= 1e-4, (s, name, ring[s, j], m[name])
-    w = _compare_state(impl.get_state_dict(), oracle_state(orc),
-                       ("_q_func", "_targ_q_func", "_policy", "_targ_policy"), 1e-4)
+    w, frac = _compare_state(impl.get_state_dict(), oracle_state(orc),
+                             ("_q_func", "_targ_q_func", "_policy", "_targ_policy"))
     assert abs(float(impl.log_alpha.item()) - float(orc._log_alpha().item())) <= 1e-5
     assert abs(float(impl.log_temp.item()) - float(orc._log_temp().item())) <= 1e-5
-    print(f"CQL fit production path: {STEPS} steps, max |param diff| {w:.2e}, max metric "
-          f"rel diff {worst_m:.2e}")
+    print(f"CQL fit production path: {STEPS} steps, max |param diff| {w:.2e} ({frac:.1e} of "
+          f"entries beyond 1e-5), max metric rel diff {worst_m:.2e}")
 
 
 def test_td3bc_fit_production_path_vs_oracle():
@@ -146,6 +154,7 @@ def test_td3bc_fit_production_path_vs_oracle():
                 continue
             assert abs(ring[s, j] - m[name]) <= 1e-4 * max(1.0, abs(m[name])), \
                 (s, name, ring[s, j], m[name])
-    w = _compare_state(impl.get_state_dict(), td3_oracle_state(orc),
-                       ("_q_func", "_targ_q_func", "_policy", "_targ_policy"), 1e-4)
-    print(f"TD3+BC fit production path: {STEPS} steps, max |param diff| {w:.2e}")
+    w, frac = _compare_state(impl.get_state_dict(), td3_oracle_state(orc),
+                             ("_q_func", "_targ_q_func", "_policy", "_targ_policy"))
+    print(f"TD3+BC fit production path: {STEPS} steps, max |param diff| {w:.2e} ({frac:.1e} "
+          f"of entries beyond 1e-5)")
