@@ -1,0 +1,175 @@
+// Split-bf16 GEMM: fp32 operands evaluated on the bf16 matrix cores.
+//
+// The throughput instantiation of the ensemble-Q layer GEMM (the nn.Linear of
+// encoders.py:265-275 over every critic at once; SURVEY §7 step 4, "fp32 for
+// parity, bf16 for throughput").  Each fp32 operand x is split into bf16
+// parts x = x0 + x1 (+ x2) — x0 = bf16(x), x1 = bf16(x - x0), x2 =
+// bf16(x - x0 - x1), each subtraction exact in fp32 — and a product is the sum
+// of the part products whose order is below fp32's resolution:
+//   TERMS 3 (hi/lo):      x0 y0 + x0 y1 + x1 y0                  ~2^-16 relative
+//   TERMS 6 (hi/mid/lo):  + x0 y2 + x1 y1 + x2 y0                ~2^-24 relative
+// on v_mfma_f32_32x32x16_bf16 (16 k per instruction, 32 cycles per SIMD:
+// 3 or 6 of them per 16 k against 8 x 64 cycles of v_mfma_f32_32x32x2_f32),
+// accumulated in fp32.
+//
+// Operands are split once, when a K tile is staged into LDS (one split per
+// element per workgroup, not per use): a 128x128 output tile, sixteen 32x32
+// waves, BK 32, LDS rows [m][k] of bf16 parts so that a lane's fragment
+// (A[row r][k = 8h + j], B[k = 8h + j][col r], j < 8) is one ds_read_b128 per
+// part.  A and B must be k-contiguous (the forward GEMM y = x W^T + b: x rows
+// and W rows both run along k); epilogue bias / ReLU as d3a_gemm_f32.
+#include "common.hpp"
+#include "../../include/d3rlpy_amd.h"
+
+namespace d3a {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int SB_BM = 128, SB_BN = 128, SB_BK = 32, SB_NT = 1024;
+constexpr int SB_LD = SB_BK + 8;  // bf16 row stride (80 B: 16-B aligned, bank-staggered)
+
+template <int PARTS>
+struct SbLds {
+  __bf16 A[2][PARTS][SB_BM * SB_LD];
+  __bf16 B[2][PARTS][SB_BN * SB_LD];
+};
+
+__device__ __forceinline__ void split4(float4 v, bf16x4* out, int parts) {
+  float x[4] = {v.x, v.y, v.z, v.w};
+  bf16x4 p0, p1, p2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const __bf16 h0 = (__bf16)x[i];
+    const float r1 = x[i] - (float)h0;  // exact
+    const __bf16 h1 = (__bf16)r1;
+    const float r2 = r1 - (float)h1;    // exact
+    p0[i] = h0;
+    p1[i] = h1;
+    p2[i] = (__bf16)r2;
+  }
+  out[0] = p0;
+  out[1] = p1;
+  if (parts > 2) out[2] = p2;
+}
+
+template <int TERMS>
+__global__ __launch_bounds__(SB_NT) void gemm_sbf16_kernel(d3a_gemm_desc p) {
+  constexpr int PARTS = TERMS == 3 ? 2 : 3;
+  __shared__ __attribute__((aligned(16))) SbLds<PARTS> L;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t n0 = (int64_t)blockIdx.x * SB_BN, m0 = (int64_t)blockIdx.y * SB_BM;
+  const int64_t b = blockIdx.z;
+  const float* A = p.A + b * p.sAb;
+  const float* B = p.B + b * p.sBb;
+  // staging: one float4 of A and one of B per thread per K tile
+  const int srow = t / (SB_BK / 4), sk = (t % (SB_BK / 4)) * 4;
+  const int wm = (w / 4) * 32, wn = (w % 4) * 32;
+
+  auto gload = [&](const float* base, int64_t ld, int64_t x, int64_t X, int64_t k) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (x < X) {
+      const float* q = base + x * ld + k;
+      if (k + 3 < p.K) {
+        v = *reinterpret_cast<const float4*>(q);
+      } else {
+        if (k + 0 < p.K) v.x = q[0];
+        if (k + 1 < p.K) v.y = q[1];
+        if (k + 2 < p.K) v.z = q[2];
+      }
+    }
+    return v;
+  };
+  auto stage = [&](int buf, float4 va, float4 vb) {
+    bf16x4 pa[3], pb[3];
+    split4(va, pa, PARTS);
+    split4(vb, pb, PARTS);
+#pragma unroll
+    for (int q = 0; q < PARTS; ++q) {
+      *reinterpret_cast<bf16x4*>(&L.A[buf][q][srow * SB_LD + sk]) = pa[q];
+      *reinterpret_cast<bf16x4*>(&L.B[buf][q][srow * SB_LD + sk]) = pb[q];
+    }
+  };
+
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+
+  float4 va = gload(A, p.sAm, m0 + srow, p.M, sk);
+  float4 vb = gload(B, p.sBn, n0 + srow, p.N, sk);
+  stage(0, va, vb);
+  __syncthreads();
+  int cur = 0;
+  for (int64_t k0 = 0; k0 < p.K; k0 += SB_BK) {
+    const bool more = k0 + SB_BK < p.K;
+    if (more) {
+      va = gload(A, p.sAm, m0 + srow, p.M, k0 + SB_BK + sk);
+      vb = gload(B, p.sBn, n0 + srow, p.N, k0 + SB_BK + sk);
+    }
+#pragma unroll
+    for (int ks = 0; ks < SB_BK; ks += 16) {
+      bf16x8 a[PARTS], bb[PARTS];
+#pragma unroll
+      for (int q = 0; q < PARTS; ++q) {
+        a[q] = *reinterpret_cast<const bf16x8*>(&L.A[cur][q][(wm + r) * SB_LD + ks + 8 * h]);
+        bb[q] = *reinterpret_cast<const bf16x8*>(&L.B[cur][q][(wn + r) * SB_LD + ks + 8 * h]);
+      }
+      // smallest terms first
+      if (TERMS == 6) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb[0], acc, 0, 0, 0);
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[0], acc, 0, 0, 0);
+    }
+    if (more) stage(cur ^ 1, va, vb);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  float* C = p.C + b * p.sCb;
+  const float* bias = p.bias ? p.bias + b * p.sbias_b : nullptr;
+  const int64_t n = n0 + wn + r;
+  if (n >= p.N) return;
+  const float bn = bias ? bias[n] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t m = m0 + wm + (i & 3) + 8 * (i >> 2) + 4 * h;
+    if (m < p.M) {
+      float v = acc[i] * p.alpha;
+      if (bias) v += bn;
+      if (p.relu) v = fmaxf(v, 0.f);
+      C[m * p.sCm + n * p.sCn] = v;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace d3a
+
+extern "C" int d3a_gemm_sbf16(const d3a_gemm_desc* d, int32_t terms, void* stream) {
+  using namespace d3a;
+  D3A_CHECK_ARG(d && d->A && d->B && d->C, "d3a_gemm_sbf16: null operand");
+  D3A_CHECK_ARG(terms == 3 || terms == 6, "d3a_gemm_sbf16: terms must be 3 or 6");
+  D3A_CHECK_ARG(d->sAk == 1 && d->sBk == 1, "d3a_gemm_sbf16: A and B must be k-contiguous");
+  D3A_CHECK_ARG(d->K % 4 == 0 && d->sAm % 4 == 0 && d->sBn % 4 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(d->A) | reinterpret_cast<uintptr_t>(d->B)) & 15) == 0,
+                "d3a_gemm_sbf16: 16-byte aligned rows, K % 4 == 0");
+  D3A_CHECK_ARG(d->splits <= 1 && !d->rowsum && !d->mask && !d->accumulate &&
+                    (d->batch2 <= 1),
+                "d3a_gemm_sbf16: no split-K / rowsum / mask / accumulate / batch2");
+  if (d->M == 0 || d->N == 0 || d->batch == 0) return 0;
+  const dim3 grid((unsigned)((d->N + SB_BN - 1) / SB_BN), (unsigned)((d->M + SB_BM - 1) / SB_BM),
+                  (unsigned)d->batch);
+  if (terms == 3)
+    hipLaunchKernelGGL(gemm_sbf16_kernel<3>, grid, dim3(SB_NT), 0, (hipStream_t)stream, *d);
+  else
+    hipLaunchKernelGGL(gemm_sbf16_kernel<6>, grid, dim3(SB_NT), 0, (hipStream_t)stream, *d);
+  D3A_LAUNCH_CHECK("d3a_gemm_sbf16");
+  return 0;
+}

@@ -139,6 +139,27 @@ def soft_update(targ: torch.Tensor, src: torch.Tensor, tau: float) -> None:
                                         _stream()), "d3a_soft_update_f32")
 
 
+def gemm_sbf16(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor], y: torch.Tensor,
+               terms: int = 6, relu: bool = False) -> None:
+    """y[c] = epi(x[c] @ W[c]^T + b[c]) on the bf16 matrix cores with split-bf16
+    operands (d3a_gemm_sbf16): x [C, R, in] (or [R, in] shared), W [C, out, in],
+    b [C, out], y [C, R, out]."""
+    _need_gpu(x, W, b, y)
+    C_, out, n_in = W.shape
+    shared = x.dim() == 2
+    R = x.shape[0] if shared else x.shape[1]
+    d = N.GemmDesc()
+    d.A, d.B, d.C = ptr(x), ptr(W), ptr(y)
+    d.bias = ptr(b)
+    d.M, d.N, d.K, d.batch = R, out, n_in, C_
+    d.sAb, d.sAm, d.sAk = (0 if shared else R * n_in), n_in, 1
+    d.sBb, d.sBk, d.sBn = out * n_in, 1, n_in
+    d.sCb, d.sCm, d.sCn = R * out, out, 1
+    d.sbias_b = out
+    d.splits, d.alpha, d.relu, d.variant, d.batch2 = 1, 1.0, int(relu), -1, 1
+    N.check(N.lib().d3a_gemm_sbf16(C.byref(d), terms, _stream()), "d3a_gemm_sbf16")
+
+
 def philox_fill(out: torch.Tensor, n_normal: int, n_uniform: int, lo: float, hi: float,
                 seed: int, ctr: torch.Tensor, ticket: torch.Tensor) -> None:
     _need_gpu(out, ctr, ticket)
