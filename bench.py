@@ -394,6 +394,10 @@ def main():
     ap.add_argument("--algo", choices=sorted(WORKLOADS), default="cql",
                     help="cql = the BASELINE.json headline (K2); td3bc = K1 shapes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", choices=["fp32", "sbf16x6"], default="fp32",
+                    help="sbf16x6: the large input-gradient GEMMs on the bf16 matrix cores "
+                         "with hi/mid/lo split operands (fp32-accurate; a separate line, "
+                         "never the headline)")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="host threads of the all-cores CPU baseline (default: this "
                          "process's CPU share)")
@@ -411,6 +415,9 @@ def main():
 
     import torch
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if args.precision == "sbf16x6":
+        from d3rlpy_amd import ops as _ops
+        _ops.set_sbf16(6)
     ws, rank, local = _dist_setup()
     if ws != args.gpus:
         print(f"bench: WORLD_SIZE={ws} but --gpus {args.gpus}; reporting n_gpus={ws}",
@@ -515,7 +522,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32" if args.precision == "fp32" else
+                 "fp32 (input-gradient GEMMs: split-bf16 x6 on bf16 MFMA)",
         "data": (f"synthetic (D4RL {shape} shapes, {args.transitions} transitions, "
                  "HBM-resident)" if shape != "atari" else
                  f"synthetic Atari-shaped uint8 frames ({args.transitions} x 1x84x84, "

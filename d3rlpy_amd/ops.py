@@ -192,10 +192,36 @@ def linear_fwd(x: int, x_shared: bool, ldx: int, W: int, b: int, y: int, C_: int
          pair=None if pair is None else (pair[0], pair[1], pair[2], pair[1]))
 
 
+# split-bf16 precision mode for the large input-gradient GEMMs (0 = fp32 MFMA,
+# the default and the parity / headline path; 6 = hi/mid/lo split-bf16, fp32-
+# accurate; 3 = hi/lo): set with set_sbf16() before the update graphs are captured
+SBF16_TERMS = int(os.environ.get("D3A_SBF16", "0"))
+SBF16_MIN_ROWS = 4096
+SBF16_W = os.environ.get("D3A_SBF16_W", "1") == "1"  # also the weight-gradient GEMMs
+
+
+def set_sbf16(terms: int) -> None:
+    global SBF16_TERMS
+    assert terms in (0, 3, 6)
+    SBF16_TERMS = terms
+
+
 def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: int, C_: int,
                  R: int, n_in: int, n_out: int, mask: Optional[int] = None,
                  ldm: int = 0, smb: int = 0) -> None:
     """dx[c] = (dy[c] @ W[c]) * [mask[c] > 0]."""
+    if SBF16_TERMS and R * C_ >= SBF16_MIN_ROWS and n_out % 4 == 0 and n_in % 4 == 0 \
+            and ldy % 4 == 0 and dy % 16 == 0 and W % 16 == 0:
+        d = N.GemmDesc()
+        d.A, d.B, d.C, d.mask = dy, W, dx, mask
+        d.M, d.N, d.K, d.batch = R, n_in, n_out, C_
+        d.sAb, d.sAm, d.sAk = sdyb, ldy, 1
+        d.sBb, d.sBk, d.sBn = n_out * n_in, n_in, 1
+        d.sCb, d.sCm, d.sCn = sdxb, ldx, 1
+        d.sMb, d.sMm, d.sMn = smb, ldm, 1
+        d.splits, d.alpha, d.variant, d.batch2 = 1, 1.0, -1, 1
+        N.check(N.lib().d3a_gemm_sbf16(C.byref(d), SBF16_TERMS, _stream()), "d3a_gemm_sbf16")
+        return
     gemm(dy, W, dx, R, n_in, n_out, batch=C_, sA=(sdyb, ldy, 1), sB=(n_out * n_in, n_in, 1),
          sC=(sdxb, ldx, 1), mask=mask, sM=(smb, ldm, 1))
 
@@ -205,6 +231,21 @@ def linear_bwd_w(dy: int, ldy: int, sdyb: int, x: int, ldx: int, sxb: int, dW: i
                  variant: int = -1) -> None:
     """dW[s][c] = sum_{r in split s} dy[c][r]^T x[c][r]  -> partials [splits][C][out][in];
     if ``db`` is given, also the bias-gradient partials db[s][c][out] = sum_r dy[c][r]."""
+    if SBF16_TERMS and SBF16_W and R * C_ >= SBF16_MIN_ROWS and n_out >= 128 and n_in >= 128 \
+            and n_out % 4 == 0 and n_in % 4 == 0 and ldy % 4 == 0 and ldx % 4 == 0 \
+            and dy % 16 == 0 and x % 16 == 0:
+        d = N.GemmDesc()
+        d.A, d.B, d.C = dy, x, dW
+        d.rowsum = db
+        d.sRb, d.sRs = n_out, C_ * n_out
+        d.M, d.N, d.K, d.batch = n_out, n_in, R, C_
+        d.sAb, d.sAm, d.sAk = sdyb, 1, ldy
+        d.sBb, d.sBk, d.sBn = sxb, ldx, 1
+        d.sCb, d.sCm, d.sCn = n_out * n_in, n_in, 1
+        d.splits, d.sCs = splits, C_ * n_out * n_in
+        d.alpha, d.variant, d.batch2 = 1.0, -1, 1
+        N.check(N.lib().d3a_gemm_sbf16(C.byref(d), SBF16_TERMS, _stream()), "d3a_gemm_sbf16")
+        return
     gemm(dy, x, dW, n_out, n_in, R, batch=C_, sA=(sdyb, 1, ldy), sB=(sxb, ldx, 1),
          sC=(n_out * n_in, n_in, 1), splits=splits, sCs=C_ * n_out * n_in,
          rowsum=db, sR=(n_out, C_ * n_out), variant=variant)

@@ -78,11 +78,11 @@ typedef struct d3a_gemm_desc {
 } d3a_gemm_desc;
 int d3a_gemm_f32(const d3a_gemm_desc* desc, void* stream);
 
-/* The same GEMM (k-contiguous A and B: y = x W^T (+ bias, ReLU)) evaluated on
- * the bf16 matrix cores with each fp32 operand split into bf16 parts:
- * terms = 3 (hi/lo, ~2^-16 relative per product) or 6 (hi/mid/lo, ~fp32).
- * The throughput instantiation of the ensemble-Q layer GEMM (SURVEY §7
- * step 4); no split-K / rowsum / mask / batch2. */
+/* The same GEMM (A k-contiguous; B k-contiguous, y = x W^T (+ bias, ReLU),
+ * or n-contiguous, dx = (dy W) * mask) evaluated on the bf16 matrix cores with
+ * each fp32 operand split into bf16 parts: terms = 3 (hi/lo, ~2^-16 relative
+ * per product) or 6 (hi/mid/lo, ~fp32).  The throughput instantiation of the
+ * ensemble-Q layer GEMMs; no split-K / rowsum / batch2. */
 int d3a_gemm_sbf16(const d3a_gemm_desc* desc, int32_t terms, void* stream);
 
 /* out[b*sOb + r] = sum_j X[b*sXb + r*sXr + j] * w[b*swb + j] + bias[b*sbb]
