@@ -80,6 +80,9 @@ def test_cql_fit_production_path_vs_oracle():
     from oracle.cql import CQLNoise
     D, A, N, B = 11, 3, 10, 256
     ds = get_synthetic_d4rl("hopper-medium-v0", n=5000, seed=2)
+    # parameter init and the device noise seed come from torch's global RNG:
+    # pin it so the trajectory does not depend on the tests run before this one
+    torch.manual_seed(67280421310721)
     algo = CQL(batch_size=B)
     algo.build_with_dataset(ds)
     impl = algo.impl
@@ -129,6 +132,7 @@ def test_td3bc_fit_production_path_vs_oracle():
     from td3_helpers import make_td3_oracle, td3_oracle_state
     D, A, B = 3, 1, 100
     ds = get_synthetic_d4rl("pendulum-random", n=4000, episode_len=200, seed=4)
+    torch.manual_seed(67280421310721)
     algo = TD3PlusBC(batch_size=B, scaler="standard")
     algo.scaler.fit_dataset(ds)
     algo.build_with_dataset(ds)
