@@ -40,6 +40,7 @@ class GemmDesc(C.Structure):
         ("variant", C.c_int32),
         ("batch2", C.c_int64), ("sAb2", C.c_int64), ("sBb2", C.c_int64), ("sCb2", C.c_int64),
         ("sbias_b2", C.c_int64), ("sMb2", C.c_int64),
+        ("agen", vp),
     ]
 
 

@@ -38,6 +38,14 @@ struct Params {
   // second batch dimension (an independent pass of the same shape, e.g. the
   // target networks): z = (t * batch + b) * splits + s, offsets t * s?b2
   int64_t batch2, sAb2, sBb2, sCb2, sbias_b2, sMb2;
+  // generated A (d3a_gemm_desc.agen): the single-output head's masked input
+  // gradient g'[r] * w[j] * [h[r][j] > 0], and its weight / bias gradients
+  const float* hg_h; int64_t hg_shb, hg_ldh;
+  const float* hg_g; int64_t hg_sgb;
+  const float* hg_gscale; int64_t hg_nscaled;
+  const float* hg_w; int64_t hg_swb;
+  float* hg_dW; int64_t hg_sWs;
+  float* hg_db; int64_t hg_sbs;
 };
 
 // Load a 4-vector of a tile at non-k coordinate x and reduction coordinate k.
@@ -99,7 +107,8 @@ struct TileLds {
 };
 
 // One BM x BN output tile (block coordinates bx, by, bz) of the GEMM p.
-template <int AMODE, int BMODE, int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK>
+template <int AMODE, int BMODE, int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK,
+          bool AGEN = false>
 __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64_t by, int64_t bz,
                                               TileLds<WM_T, WN_T, WAVES_M, WAVES_N, BK>& L) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
@@ -140,57 +149,177 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
   const bool do_rowsum = p.rowsum != nullptr && bx == 0;
   double rs = 0.0;
 
-  float4 ra[AV], rb[BV];
-  auto gload = [&](int64_t k0) {
+  // Global->register->LDS pipeline two K tiles deep: the loads of tile i+2
+  // are issued while tile i is multiplied and stored to LDS only at the end
+  // of tile i+1, so each load has two tiles' worth of MFMA work to land.
+  float4 ra0[AV], rb0[BV], ra1[AV], rb1[BV];
+  // Generated A (the head backward, AGEN): gload keeps the raw loads (h and,
+  // per K tile, w[j..j+3] (A k-contiguous) or g[r] and its scale (A
+  // m-contiguous)) in registers and lstore forms g'[r] * w[j] * [h > 0], so
+  // the loads stay in flight across the MFMA work like plain operands.
+  float4 rx0[AV], rx1[AV];
+  const float* hgH = AGEN ? p.hg_h + b * p.hg_shb : nullptr;
+  const float* hgG = AGEN ? p.hg_g + b * p.hg_sgb : nullptr;
+  const float* hgW = AGEN ? p.hg_w + b * p.hg_swb : nullptr;
+  const float hg_gs = (AGEN && p.hg_gscale) ? *p.hg_gscale : 1.f;
+  const bool hg_grads = AMODE == MODE_XCONTIG && AGEN && p.hg_dW != nullptr && bx == 0;
+  double hg_acc[AV][4], hg_accb = 0.0;
+  float hg_fix[AV][4];  // per-thread constants: g'[r] (k-contiguous A) or w[j..j+3]
 #pragma unroll
-    for (int i = 0; i < AV; ++i)
-      ra[i] = load4<AMODE>(Ab, p.sAm, p.sAk, m0 + axl[i], k0 + akl[i], p.M, kend);
+  for (int i = 0; i < AV; ++i) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hg_acc[i][q] = 0.0;
+    if constexpr (AGEN) {
+      if (AMODE == MODE_KCONTIG) {  // A(r, j): this thread's row r is fixed
+        const int64_t r = m0 + axl[i];
+        float g = 0.f;
+        if (r < p.M) {
+          g = hgG[r];
+          if (r < p.hg_nscaled) g *= hg_gs;  // as d3a_head1_bwd forms g'
+        }
+        hg_fix[i][0] = hg_fix[i][1] = hg_fix[i][2] = hg_fix[i][3] = g;
+      } else {  // A(j, r): this thread's hidden units j..j+3 are fixed
+        const float4 wv = load4<MODE_XCONTIG>(hgW, 1, 0, m0 + axl[i], 0, p.M, 1);
+        hg_fix[i][0] = wv.x; hg_fix[i][1] = wv.y; hg_fix[i][2] = wv.z; hg_fix[i][3] = wv.w;
+      }
+    }
+  }
+  auto gload = [&](float4* ra, float4* rx, float4* rb, int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      if constexpr (AGEN) {
+        if (AMODE == MODE_KCONTIG) {
+          const int64_t r = m0 + axl[i], j = k0 + akl[i];
+          ra[i] = load4<MODE_KCONTIG>(hgH, p.hg_ldh, 1, r, j, p.M, kend);
+          rx[i] = load4<MODE_KCONTIG>(hgW, 0, 1, 0, j, 1, kend);
+        } else {
+          const int64_t j = m0 + axl[i], r = k0 + akl[i];
+          ra[i] = load4<MODE_XCONTIG>(hgH, 1, p.hg_ldh, j, r, p.M, kend);
+          rx[i].x = r < kend ? hgG[r] : 0.f;
+          rx[i].y = r < p.hg_nscaled ? hg_gs : 1.f;
+        }
+      } else {
+        ra[i] = load4<AMODE>(Ab, p.sAm, p.sAk, m0 + axl[i], k0 + akl[i], p.M, kend);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < BV; ++i)
       rb[i] = load4<BMODE>(Bb, p.sBn, p.sBk, n0 + bxl[i], k0 + bkl[i], p.N, kend);
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](const float4* ra, const float4* rx, const float4* rb, int buf) {
 #pragma unroll
-    for (int i = 0; i < AV; ++i) store4<AMODE, LDA>(As[buf], axl[i], akl[i], ra[i]);
+    for (int i = 0; i < AV; ++i) {
+      if constexpr (AGEN) {
+        const float4 hv = ra[i];
+        float g[4], w[4];
+        if (AMODE == MODE_KCONTIG) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) g[q] = hg_fix[i][q];
+          w[0] = rx[i].x; w[1] = rx[i].y; w[2] = rx[i].z; w[3] = rx[i].w;
+        } else {
+          const float gr = rx[i].x * rx[i].y;  // scale 1 (exact) past n_scaled
+#pragma unroll
+          for (int q = 0; q < 4; ++q) { g[q] = gr; w[q] = hg_fix[i][q]; }
+          if (hg_grads) {
+            hg_acc[i][0] += (double)(gr * hv.x);
+            hg_acc[i][1] += (double)(gr * hv.y);
+            hg_acc[i][2] += (double)(gr * hv.z);
+            hg_acc[i][3] += (double)(gr * hv.w);
+            if (axl[i] == 0) hg_accb += (double)gr;
+          }
+        }
+        float4 a;
+        a.x = hv.x > 0.f ? g[0] * w[0] : 0.f;
+        a.y = hv.y > 0.f ? g[1] * w[1] : 0.f;
+        a.z = hv.z > 0.f ? g[2] * w[2] : 0.f;
+        a.w = hv.w > 0.f ? g[3] * w[3] : 0.f;
+        store4<AMODE, LDA>(As[buf], axl[i], akl[i], a);
+      } else {
+        store4<AMODE, LDA>(As[buf], axl[i], akl[i], ra[i]);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < BV; ++i) store4<BMODE, LDB>(Bs[buf], bxl[i], bkl[i], rb[i]);
   };
-
-  int cur = 0;
-  if (kbeg < kend) {
-    gload(kbeg);
-    lstore(0);
-  }
-  __syncthreads();
-  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
-    const bool more = k0 + BK < kend;
-    if (more) gload(k0 + BK);
-    const float* Ac = As[cur];
-    const float* Bc = Bs[cur];
+  auto compute = [&](int buf) {
+    const float* Ac = As[buf];
+    const float* Bc = Bs[buf];
+    // every operand of the K tile is read from LDS before the first MFMA, so
+    // the reads overlap each other instead of each MFMA waiting one LDS latency
+    float av[BK / 2][WM_T], bv[BK / 2][WN_T];
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
-      float av[WM_T], bv[WN_T];
 #pragma unroll
-      for (int i = 0; i < WM_T; ++i) av[i] = Ac[(kk + lk) * LDA + wm + 32 * i + li];
+      for (int i = 0; i < WM_T; ++i) av[kk / 2][i] = Ac[(kk + lk) * LDA + wm + 32 * i + li];
 #pragma unroll
-      for (int j = 0; j < WN_T; ++j) bv[j] = Bc[(kk + lk) * LDB + wn + 32 * j + li];
+      for (int j = 0; j < WN_T; ++j) bv[kk / 2][j] = Bc[(kk + lk) * LDB + wn + 32 * j + li];
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
 #pragma unroll
       for (int i = 0; i < WM_T; ++i)
 #pragma unroll
         for (int j = 0; j < WN_T; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk / 2][i], bv[kk / 2][j],
+                                                          acc[i][j], 0, 0, 0);
     }
     if (do_rowsum && t < BM) {
 #pragma unroll
       for (int kk = 0; kk < BK; ++kk) rs += (double)Ac[kk * LDA + t];
     }
-    if (more) lstore(cur ^ 1);
+  };
+
+  if (kbeg < kend) {
+    gload(ra0, rx0, rb0, kbeg);
+    lstore(ra0, rx0, rb0, 0);
+    if (kbeg + BK < kend) gload(ra1, rx1, rb1, kbeg + BK);
+  }
+  __syncthreads();
+  // even tiles in LDS buffer 0 / registers 0, odd tiles in buffer 1 / registers 1
+  for (int64_t k0 = kbeg; k0 < kend;) {
+    if (k0 + 2 * BK < kend) gload(ra0, rx0, rb0, k0 + 2 * BK);
+    compute(0);
+    if (k0 + BK >= kend) break;
+    lstore(ra1, rx1, rb1, 1);
     __syncthreads();
-    cur ^= 1;
+    k0 += BK;
+    if (k0 + 2 * BK < kend) gload(ra1, rx1, rb1, k0 + 2 * BK);
+    compute(1);
+    if (k0 + BK >= kend) break;
+    lstore(ra0, rx0, rb0, 0);
+    __syncthreads();
+    k0 += BK;
   }
 
   if (do_rowsum && t < BM && m0 + t < p.M)
     p.rowsum[b * p.sRb + s * p.sRs + m0 + t] = (float)rs;
+
+  if (hg_grads) {
+    // head weight / bias gradient partials of this split: every (k, m) slot
+    // of the staging tile holds one thread's running sum; slots are summed
+    // over k in a fixed order (deterministic)
+    static_assert(sizeof(L) >= sizeof(double) * (BK * BM + BK), "LDS reuse too small");
+    double* red = reinterpret_cast<double*>(&L);
+    double* redb = red + BK * BM;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[akl[i] * BM + axl[i] + q] = hg_acc[i][q];
+      if (axl[i] == 0) redb[akl[i]] = hg_accb;
+    }
+    __syncthreads();
+    if (t < BM && m0 + t < p.M) {
+      double v = 0.0;
+      for (int k = 0; k < BK; ++k) v += red[k * BM + t];
+      p.hg_dW[s * p.hg_sWs + b * p.M + m0 + t] = (float)v;
+    }
+    if (t == 0 && by == 0 && p.hg_db) {
+      double v = 0.0;
+      for (int k = 0; k < BK; ++k) v += redb[k];
+      p.hg_db[s * p.hg_sbs + b] = (float)v;
+    }
+  }
 
   // epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
   float* Cb = p.C + b * p.sCb + t2 * p.sCb2 + s * p.sCs;
@@ -219,11 +348,29 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
   }
 }
 
-template <int AMODE, int BMODE, int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK>
+// XCD-aware tile order: the dispatcher deals workgroups out to the 8 XCDs
+// round-robin, so neighbouring tiles (the column tiles of one row block, the
+// tiles of one split-K slice), which read the same operand rows, would each
+// fetch them into a different XCD's L2.  The bijective remap below gives each
+// XCD a contiguous run of logical tiles instead (cdna_hip_programming.md T1);
+// a wrong guess about placement costs speed, never correctness.
+__device__ __forceinline__ void xcd_tile(int64_t& bx, int64_t& by, int64_t& bz) {
+  const uint32_t gx = gridDim.x, gy = gridDim.y, nwg = gx * gy * gridDim.z;
+  const uint32_t orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const uint32_t xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+  const uint32_t id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  bx = id % gx;
+  by = (id / gx) % gy;
+  bz = id / (gx * gy);
+}
+
+template <int AMODE, int BMODE, int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK,
+          bool AGEN = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) TileLds<WM_T, WN_T, WAVES_M, WAVES_N, BK> lds;
-  gemm_f32_tile<AMODE, BMODE, WM_T, WN_T, WAVES_M, WAVES_N, BK>(p, blockIdx.x, blockIdx.y,
-                                                                blockIdx.z, lds);
+  int64_t bx, by, bz;
+  xcd_tile(bx, by, bz);
+  gemm_f32_tile<AMODE, BMODE, WM_T, WN_T, WAVES_M, WAVES_N, BK, AGEN>(p, bx, by, bz, lds);
 }
 
 // ---- register-direct split-K kernel for small problems ---------------------
@@ -395,13 +542,13 @@ constexpr Variant kVariants[] = {
 constexpr int kFirstRd = 9;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-template <int AM, int BMd, int V>
+template <int AM, int BMd, int V, bool AGEN = false>
 void launch_v(const Params& p, hipStream_t st) {
   constexpr Variant v = kVariants[V];
   constexpr int BM = 32 * v.wm_t * v.waves_m, BN = 32 * v.wn_t * v.waves_n;
   dim3 grid((unsigned)((p.N + BN - 1) / BN), (unsigned)((p.M + BM - 1) / BM),
             (unsigned)(p.batch * p.batch2 * p.splits));
-  hipLaunchKernelGGL((gemm_f32_kernel<AM, BMd, v.wm_t, v.wn_t, v.waves_m, v.waves_n, v.bk>), grid,
+  hipLaunchKernelGGL((gemm_f32_kernel<AM, BMd, v.wm_t, v.wn_t, v.waves_m, v.waves_n, v.bk, AGEN>), grid,
                      dim3(64 * v.waves_m * v.waves_n), 0, st, p);
 }
 
@@ -500,7 +647,7 @@ namespace {
 // Validate a descriptor and fill the kernel parameters; *skip = the problem is empty.
 int make_params(const d3a_gemm_desc* d, Params& p, int& variant, int& am, int& bm, bool& skip) {
   D3A_CHECK_ARG(d != nullptr, "d3a_gemm_f32: null descriptor");
-  D3A_CHECK_ARG(d->A && d->B && d->C, "d3a_gemm_f32: null operand");
+  D3A_CHECK_ARG((d->A || d->agen) && d->B && d->C, "d3a_gemm_f32: null operand");
   D3A_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0 && d->batch >= 0,
                 "d3a_gemm_f32: negative size");
   D3A_CHECK_ARG(d->splits >= 1, "d3a_gemm_f32: splits must be >= 1");
@@ -520,9 +667,29 @@ int make_params(const d3a_gemm_desc* d, Params& p, int& variant, int& am, int& b
   p.batch2 = d->batch2 > 0 ? d->batch2 : 1;
   p.sAb2 = d->sAb2; p.sBb2 = d->sBb2; p.sCb2 = d->sCb2;
   p.sbias_b2 = d->sbias_b2; p.sMb2 = d->sMb2;
+  p.hg_h = nullptr; p.hg_g = nullptr; p.hg_gscale = nullptr; p.hg_w = nullptr;
+  p.hg_dW = nullptr; p.hg_db = nullptr;
+  p.hg_shb = p.hg_ldh = p.hg_sgb = p.hg_nscaled = p.hg_swb = p.hg_sWs = p.hg_sbs = 0;
+  if (d->agen) {
+    const d3a_head1_bwd_desc* g = d->agen;
+    D3A_CHECK_ARG(g->h && g->g && g->w && !g->q_min,
+                  "d3a_gemm_f32: agen needs h, g, w (no argmin mode)");
+    D3A_CHECK_ARG(p.batch2 == 1 && !d->accumulate, "d3a_gemm_f32: agen with batch2 / accumulate");
+    D3A_CHECK_ARG((d->sAk == 1) != (d->sAm == 1), "d3a_gemm_f32: agen needs a contiguous A mode");
+    D3A_CHECK_ARG(!g->dW || (d->sAm == 1 && g->db), "d3a_gemm_f32: agen head grads need A^T and db");
+    D3A_CHECK_ARG(!g->dW || d->K >= 1, "d3a_gemm_f32: agen head grads need rows");
+    p.hg_h = g->h; p.hg_shb = g->shb; p.hg_ldh = g->ldh;
+    p.hg_g = g->g; p.hg_sgb = g->sgb;
+    p.hg_gscale = g->gscale; p.hg_nscaled = g->n_scaled;
+    p.hg_w = g->w; p.hg_swb = g->swb;
+    p.hg_dW = g->dW; p.hg_sWs = g->sWs;
+    p.hg_db = g->db; p.hg_sbs = g->sbs;
+  }
   D3A_CHECK_ARG(p.batch2 == 1 || d->rowsum == nullptr, "d3a_gemm_f32: rowsum needs batch2 = 1");
   variant = d->variant >= 0 ? d->variant : env_variant();
   if (variant < 0) variant = choose_variant(p);
+  // generated A: the LDS tiles launch_agen instantiates
+  if (d->agen) variant = (d->M >= 128 && d->N >= 128) ? 14 : 0;  // as launch_agen
   const int bk = kVariants[variant].bk;
   // split K in BK multiples (every split starts on a K-tile boundary)
   int64_t kc = (d->K + d->splits - 1) / d->splits;
@@ -536,7 +703,25 @@ int make_params(const d3a_gemm_desc* d, Params& p, int& variant, int& am, int& b
   return 0;
 }
 
+// generated-A launches (d3a_gemm_desc.agen): the 16-wave 128x128 tile where
+// both output dimensions reach 128, else the 64x64 tile
+template <int AM, int BMd>
+void launch_agen(const Params& p, hipStream_t st) {
+  if (p.M >= 128 && p.N >= 128) launch_v<AM, BMd, 14, true>(p, st);
+  else launch_v<AM, BMd, 0, true>(p, st);
+}
+
 void launch_params(const Params& p, int variant, int am, int bm, hipStream_t st) {
+  if (p.hg_h) {
+    if (am == MODE_KCONTIG) {
+      if (bm == MODE_KCONTIG) launch_agen<MODE_KCONTIG, MODE_KCONTIG>(p, st);
+      else launch_agen<MODE_KCONTIG, MODE_XCONTIG>(p, st);
+    } else {
+      if (bm == MODE_KCONTIG) launch_agen<MODE_XCONTIG, MODE_KCONTIG>(p, st);
+      else launch_agen<MODE_XCONTIG, MODE_XCONTIG>(p, st);
+    }
+    return;
+  }
   if (am == MODE_GENERIC || bm == MODE_GENERIC) {
     // strided fallback: smallest tile, scalar loads
     if (am == MODE_GENERIC && bm == MODE_GENERIC) launch_v<MODE_GENERIC, MODE_GENERIC, 0>(p, st);

@@ -233,6 +233,7 @@ extern "C" int d3a_gemm_sbf16(const d3a_gemm_desc* d, int32_t terms, void* strea
                     (bt ? d->sBk % 4 == 0 && d->N % 4 == 0 : d->sBn % 4 == 0 && d->K % 4 == 0) &&
                     ((reinterpret_cast<uintptr_t>(d->A) | reinterpret_cast<uintptr_t>(d->B)) & 15) == 0,
                 "d3a_gemm_sbf16: 16-byte aligned vectors along the contiguous dimensions");
+  D3A_CHECK_ARG(!d->agen, "d3a_gemm_sbf16: no generated A");
   D3A_CHECK_ARG(!d->accumulate && d->batch2 <= 1 && (!d->rowsum || at),
                 "d3a_gemm_sbf16: no accumulate / batch2; rowsum only with an m-contiguous A");
   if (d->M == 0 || d->N == 0 || d->batch == 0) return 0;

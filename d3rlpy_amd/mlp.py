@@ -65,6 +65,11 @@ FUSED_MIN_ROWS = int(os.environ.get("D3A_FUSED_MIN_ROWS", "4096"))
 # rows (four loads per lane per 8 k) and it measured 67 us against 52 us for
 # the per-layer head backward + input-gradient GEMM on the K2 critic pass
 _FUSED_BWD = os.environ.get("D3A_FUSED_BWD", "0") == "1"
+# head backward generated inside the trunk GEMMs (see backward); measured on
+# the K2 critic backward (7,936 rows x 2 members), off for small passes where
+# the register-direct GEMM + d3a_head1_bwd is faster
+_HEAD_GEN = os.environ.get("D3A_HEAD_GEN", "1") == "1"
+_HEAD_GEN_MIN_ROWS = 4096
 # rows per fused workgroup (32 or 64; 0 = the library's choice)
 _FUSED_BM = int(os.environ.get("D3A_FUSED_BM", "0"))
 
@@ -255,7 +260,26 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         return
     ld_cur = bs.dz[0].shape[2]
     scur = bs.rows * ld_cur
-    if out_dim == 1:
+    # large critic backward: the head's masked input gradient is generated
+    # inside the trunk's two GEMMs (d3a_gemm_desc.agen) instead of written by
+    # d3a_head1_bwd and read back; the weight-gradient GEMM also writes the
+    # head's weight / bias gradient partials
+    agen = None
+    if out_dim == 1 and q_min is None and weight_grads and _HEAD_GEN and not ops.SBF16_TERMS \
+            and n * C >= _HEAD_GEN_MIN_ROWS:
+        agen = N.Head1BwdDesc()
+        agen.g, agen.sgb = dout, sdout_b
+        if g_scale is not None:
+            agen.gscale, agen.n_scaled = g_scale, n_scaled
+        agen.h, agen.shb, agen.ldh = hin, sh, ld_h
+        agen.w, agen.swb = net.W(L - 1, store), Hin
+        gW, gb = gs.get(net.wname(L - 1)), gs.get(net.bname(L - 1))
+        agen.dW, agen.sWs = gW.data_ptr(), C * Hin
+        agen.db, agen.sbs = gb.data_ptr(), C
+        agen.rows, agen.n, agen.C, agen.splits = n, Hin, C, S
+    if agen is not None:
+        pass
+    elif out_dim == 1:
         # fused: masked input gradient + head weight/bias gradients, h read once
         d = N.Head1BwdDesc()
         if q_min is not None:
@@ -290,18 +314,19 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         Hin = sizes[l]
         hin, ld_h, sh = h_ptr(l)
         dz = cur
+        ag = agen if l == L - 2 else None  # the head's dz, generated
         if weight_grads:
             gW, gb = gs.get(net.wname(l)), gs.get(net.bname(l))
             ops.linear_bwd_w(dz.data_ptr(), ld_cur, scur, hin, ld_h, sh, gW.data_ptr(), C, n, Hin,
-                             Hout, S, db=gb.data_ptr())
+                             Hout, S, db=gb.data_ptr(), agen=ag)
         if l > 0:
             nxt = bs.dz[1] if cur is bs.dz[0] else bs.dz[0]
             ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(l, store), nxt.data_ptr(), ld_cur,
-                             scur, C, n, Hin, Hout, mask=hin, ldm=ld_h, smb=sh)
+                             scur, C, n, Hin, Hout, mask=hin, ldm=ld_h, smb=sh, agen=ag)
             cur = nxt
         elif dx is not None:
             ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(0, store), dx.data_ptr(), Hin,
-                             n * Hin, C, n, Hin, Hout)
+                             n * Hin, C, n, Hin, Hout, agen=ag)
 
 
 

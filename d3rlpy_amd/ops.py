@@ -42,8 +42,11 @@ def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
          mask: Optional[int] = None, sM: Sequence[int] = (0, 0, 0),
          relu: bool = False, accumulate: bool = False, splits: int = 1, sCs: int = 0,
          alpha: float = 1.0, rowsum: Optional[int] = None, sR: Sequence[int] = (0, 0),
-         variant: int = -1, pair: Optional[Sequence[int]] = None) -> None:
+         variant: int = -1, pair: Optional[Sequence[int]] = None,
+         agen: Optional[C.Structure] = None) -> None:
     """C_b,s(m,n) = epi(alpha * sum_k A_b(m,k) B_b(k,n)); strides (batch, row, col).
+    ``agen`` (a Head1BwdDesc): A is generated as that head's masked input
+    gradient instead of read (d3a_gemm_desc.agen).
     ``pair = (dA, dB, dC, dbias)``: a second pass of the same shape at those
     element offsets in the same launch (d3a_gemm_desc.batch2 = 2)."""
     d = N.GemmDesc()
@@ -62,6 +65,8 @@ def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
     if pair is not None:
         d.batch2 = 2
         d.sAb2, d.sBb2, d.sCb2, d.sbias_b2 = pair
+    if agen is not None:
+        d.agen = C.addressof(agen)
     if _TRACE:
         print(f"gemm M={M} N={Nn} K={K} batch={batch} splits={splits} sA={tuple(sA)} "
               f"sB={tuple(sB)} sC={tuple(sC)} mask={mask is not None} relu={relu} "
@@ -208,8 +213,17 @@ def set_sbf16(terms: int) -> None:
 
 def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: int, C_: int,
                  R: int, n_in: int, n_out: int, mask: Optional[int] = None,
-                 ldm: int = 0, smb: int = 0) -> None:
-    """dx[c] = (dy[c] @ W[c]) * [mask[c] > 0]."""
+                 ldm: int = 0, smb: int = 0, agen: Optional[C.Structure] = None) -> None:
+    """dx[c] = (dy[c] @ W[c]) * [mask[c] > 0]; with ``agen`` dy is generated
+    from that single-output head (d3a_gemm_desc.agen) and not read."""
+    if agen is not None:
+        if agen.dW:  # the head's weight gradients come from the dW launch only
+            agen = type(agen).from_buffer_copy(agen)
+            agen.dW = agen.db = None
+        gemm(None, W, dx, R, n_in, n_out, batch=C_, sA=(0, n_out, 1),
+             sB=(n_out * n_in, n_in, 1), sC=(sdxb, ldx, 1), mask=mask, sM=(smb, ldm, 1),
+             agen=agen)
+        return
     if SBF16_TERMS and R * C_ >= SBF16_MIN_ROWS and n_out % 4 == 0 and n_in % 4 == 0 \
             and ldy % 4 == 0 and dy % 16 == 0 and W % 16 == 0:
         d = N.GemmDesc()
@@ -228,9 +242,16 @@ def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: 
 
 def linear_bwd_w(dy: int, ldy: int, sdyb: int, x: int, ldx: int, sxb: int, dW: int, C_: int,
                  R: int, n_in: int, n_out: int, splits: int, db: Optional[int] = None,
-                 variant: int = -1) -> None:
+                 variant: int = -1, agen: Optional[C.Structure] = None) -> None:
     """dW[s][c] = sum_{r in split s} dy[c][r]^T x[c][r]  -> partials [splits][C][out][in];
-    if ``db`` is given, also the bias-gradient partials db[s][c][out] = sum_r dy[c][r]."""
+    if ``db`` is given, also the bias-gradient partials db[s][c][out] = sum_r dy[c][r].
+    With ``agen`` dy is generated from that single-output head, whose weight /
+    bias gradient partials the same launch writes (d3a_gemm_desc.agen)."""
+    if agen is not None:
+        gemm(None, x, dW, n_out, n_in, R, batch=C_, sA=(0, 1, n_out), sB=(sxb, ldx, 1),
+             sC=(n_out * n_in, n_in, 1), splits=splits, sCs=C_ * n_out * n_in,
+             rowsum=db, sR=(n_out, C_ * n_out), variant=variant, agen=agen)
+        return
     if SBF16_TERMS and SBF16_W and R * C_ >= SBF16_MIN_ROWS and n_out >= 128 and n_in >= 128 \
             and n_out % 4 == 0 and n_in % 4 == 0 and ldy % 4 == 0 and ldx % 4 == 0 \
             and dy % 16 == 0 and x % 16 == 0:

@@ -75,6 +75,17 @@ typedef struct d3a_gemm_desc {
    * pass of the same shape in the same launch (the target networks beside
    * the online ones, DDPGBaseImpl._targ_q_func).  Not with rowsum. */
   int64_t batch2, sAb2, sBb2, sCb2, sbias_b2, sMb2;
+  /* Optional (may be NULL): A is not read but generated as the masked input
+   * gradient of a single-output head, exactly as d3a_head1_bwd writes dz
+   * (its g / gscale / n_scaled / h / w fields; A = NULL, batch = members):
+   *   A_b(r, j) = g'[b][r] * w[b][j] * [h[b][r][j] > 0]     (A k-contiguous)
+   *   A_b(j, r) = the same                                  (A m-contiguous)
+   * With A m-contiguous (the weight-gradient GEMM dW = dz^T h_prev) and
+   * agen->dW / db set, the launch also writes the head's weight / bias
+   * gradient partials agen->dW[s][b][j] = sum_{r in split s} g'[r] h[r][j],
+   * agen->db[s][b] = sum g'[r] (fp64-accumulated, as d3a_head1_bwd does) —
+   * the head backward needs no launch of its own. */
+  const struct d3a_head1_bwd_desc* agen;
 } d3a_gemm_desc;
 int d3a_gemm_f32(const d3a_gemm_desc* desc, void* stream);
 

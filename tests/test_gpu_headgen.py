@@ -1,0 +1,91 @@
+"""Generated-A GEMMs (d3a_gemm_desc.agen) against d3a_head1_bwd + the plain
+GEMMs (GPU only).
+
+The critic backward of the large passes generates the Q head's masked input
+gradient g'[r] * w[j] * [h[r][j] > 0] inside the trunk's weight- and input-
+gradient GEMMs instead of writing it with d3a_head1_bwd and reading it back.
+The generated operand is the same fp32 product, so both GEMM outputs must be
+bit-identical to the two-launch path; the head's weight / bias gradients are
+fp64 sums over the same rows in a different split, so their split totals must
+agree to fp32 rounding.
+"""
+import ctypes as C
+
+import pytest
+import torch
+
+from d3rlpy_amd import _native as N
+from d3rlpy_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("rows,n_scaled", [(5000, 1234), (7936, 0)])
+def test_head_gradient_generated_in_gemms(rows, n_scaled):
+    g = torch.Generator(device="cuda").manual_seed(11)
+    Cm, H, Hp, S = 2, 256, 256, 32
+    dev = "cuda"
+    h2 = torch.relu(torch.randn(Cm, rows, H, device=dev, generator=g))
+    h1 = torch.relu(torch.randn(Cm, rows, Hp, device=dev, generator=g))
+    gr = torch.randn(Cm, rows, device=dev, generator=g) * 1e-2
+    w = torch.randn(Cm, H, device=dev, generator=g) * 0.06
+    W2 = torch.randn(Cm, H, Hp, device=dev, generator=g) * 0.06
+    gscale = torch.tensor([0.7], device=dev)
+
+    def head_desc(dz=None, dWh=None, dbh=None, splits=S):
+        d = N.Head1BwdDesc()
+        d.g, d.sgb = gr.data_ptr(), rows
+        if n_scaled:
+            d.gscale, d.n_scaled = gscale.data_ptr(), n_scaled
+        d.h, d.shb, d.ldh = h2.data_ptr(), rows * H, H
+        d.w, d.swb = w.data_ptr(), H
+        if dz is not None:
+            d.dz, d.sdzb, d.lddz = dz.data_ptr(), rows * H, H
+        if dWh is not None:
+            d.dW, d.sWs = dWh.data_ptr(), Cm * H
+            d.db, d.sbs = dbh.data_ptr(), Cm
+        d.rows, d.n, d.C, d.splits = rows, H, Cm, splits
+        return d
+
+    prev = ops.SBF16_TERMS
+    ops.set_sbf16(0)
+    try:
+        # two-launch reference: d3a_head1_bwd writes dz, the GEMMs read it
+        dz = torch.zeros(Cm, rows, H, device=dev)
+        dWh_ref = torch.zeros(S, Cm, H, device=dev)
+        dbh_ref = torch.zeros(S, Cm, device=dev)
+        ops.call_desc("d3a_head1_bwd", head_desc(dz, dWh_ref, dbh_ref))
+        dW_ref = torch.zeros(S, Cm, H, Hp, device=dev)
+        db_ref = torch.zeros(S, Cm, H, device=dev)
+        dx_ref = torch.zeros(Cm, rows, Hp, device=dev)
+        ops.linear_bwd_w(dz.data_ptr(), H, rows * H, h1.data_ptr(), Hp, rows * Hp,
+                         dW_ref.data_ptr(), Cm, rows, Hp, H, S, db=db_ref.data_ptr())
+        ops.linear_bwd_x(dz.data_ptr(), H, rows * H, W2.data_ptr(), dx_ref.data_ptr(), Hp,
+                         rows * Hp, Cm, rows, Hp, H, mask=h1.data_ptr(), ldm=Hp, smb=rows * Hp)
+        # generated path
+        dWh = torch.full((S, Cm, H), float("nan"), device=dev)
+        dbh = torch.full((S, Cm), float("nan"), device=dev)
+        dW = torch.full((S, Cm, H, Hp), float("nan"), device=dev)
+        db = torch.full((S, Cm, H), float("nan"), device=dev)
+        dx = torch.full((Cm, rows, Hp), float("nan"), device=dev)
+        ag = head_desc(None, dWh, dbh)
+        ops.linear_bwd_w(0, H, rows * H, h1.data_ptr(), Hp, rows * Hp, dW.data_ptr(), Cm, rows,
+                         Hp, H, S, db=db.data_ptr(), agen=ag)
+        ops.linear_bwd_x(0, H, rows * H, W2.data_ptr(), dx.data_ptr(), Hp, rows * Hp, Cm, rows,
+                         Hp, H, mask=h1.data_ptr(), ldm=Hp, smb=rows * Hp, agen=head_desc())
+        torch.cuda.synchronize()
+    finally:
+        ops.set_sbf16(prev)
+    assert torch.equal(dW, dW_ref)
+    assert torch.equal(db, db_ref)
+    assert torch.equal(dx, dx_ref)
+    # head gradients: fp64 totals over the same rows, split differently
+    gs = gr.clone()
+    gs[:, :n_scaled] = gr[:, :n_scaled] * gscale  # fp32, as the kernels form g'
+    gsf = gs.double()
+    ref_w = torch.einsum("cr,crj->cj", gsf, h2.double())
+    for tot, ref in ((dWh.double().sum(0), ref_w), (dWh_ref.double().sum(0), ref_w),
+                     (dbh.double().sum(0), gsf.sum(1)), (dbh_ref.double().sum(0), gsf.sum(1))):
+        e = float((tot - ref).abs().max()) / max(1e-30, float(ref.abs().max()))
+        assert e <= 1e-6, e
+    assert not torch.isnan(dWh).any() and not torch.isnan(dbh).any()
