@@ -40,7 +40,14 @@ class GemmDesc(C.Structure):
         ("variant", C.c_int32),
         ("batch2", C.c_int64), ("sAb2", C.c_int64), ("sBb2", C.c_int64), ("sCb2", C.c_int64),
         ("sbias_b2", C.c_int64), ("sMb2", C.c_int64),
-        ("agen", vp),
+        ("agen", vp), ("wnext", vp),
+    ]
+
+
+class GemmWnext(C.Structure):
+    _fields_ = [
+        ("x", vp), ("ldx", C.c_int64), ("sxb", C.c_int64), ("n_in", C.c_int64),
+        ("dW", vp), ("db", vp),
     ]
 
 

@@ -16,6 +16,7 @@
 // multiplied, one barrier per K tile.  Numerics: every output is an exact
 // fp32 fmaf chain over k (f32-input MFMA), no reduced precision.
 #include <cstdlib>
+#include <type_traits>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
 
@@ -46,6 +47,9 @@ struct Params {
   const float* hg_w; int64_t hg_swb;
   float* hg_dW; int64_t hg_sWs;
   float* hg_db; int64_t hg_sbs;
+  // next layer's weight-gradient epilogue (d3a_gemm_desc.wnext)
+  const float* ew_x; int64_t ew_ldx, ew_sxb, ew_nin;
+  float* ew_dW; float* ew_db;
 };
 
 // Load a 4-vector of a tile at non-k coordinate x and reduction coordinate k.
@@ -105,12 +109,17 @@ struct TileLds {
   float As[2][BK * (BM + 4)];
   float Bs[2][BK * (BN + 4)];
 };
+// + the input-row tile of the next layer's weight-gradient epilogue (EW)
+template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK>
+struct TileLdsEW : TileLds<WM_T, WN_T, WAVES_M, WAVES_N, BK> {
+  float Xs[32 * WM_T * WAVES_M * 32];
+};
 
 // One BM x BN output tile (block coordinates bx, by, bz) of the GEMM p.
 template <int AMODE, int BMODE, int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK,
-          bool AGEN = false>
+          bool AGEN = false, bool EW = false, class LdsT = TileLds<WM_T, WN_T, WAVES_M, WAVES_N, BK>>
 __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64_t by, int64_t bz,
-                                              TileLds<WM_T, WN_T, WAVES_M, WAVES_N, BK>& L) {
+                                              LdsT& L) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int BM = 32 * WM_T * WAVES_M, BN = 32 * WN_T * WAVES_N;
   constexpr int LDA = BM + 4, LDB = BN + 4;
@@ -321,6 +330,79 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
     }
   }
 
+  if constexpr (EW) {
+    // C = dz_{l-1} (this layer's masked input gradient) is not written: the
+    // tile goes to LDS and the previous layer's weight / bias gradient
+    // partials of this 128-row tile are formed from it,
+    //   dW[t][b][j][d] = sum_r C(r, j) x[r][d],  db[t][b][j] = sum_r C(r, j)
+    // (t = by), with x (<= 32 inputs) staged beside it.  Wave w multiplies
+    // the 32 j of block w&3 over rows 32*(w>>2)..+31; the four row quarters
+    // are summed in order (deterministic).
+    static_assert(BM == 128 && BN == 128 && NT == 1024 && WM_T == 1 && WN_T == 1,
+                  "EW epilogue: 128x128 tile of sixteen 32x32 waves");
+    constexpr int LT = BN + 4;
+    static_assert(sizeof(L.As) + sizeof(L.Bs) >= sizeof(float) * BM * LT, "T tile");
+    float* T = &L.As[0][0];  // [r][LT], spans As and Bs (contiguous)
+    float* X = L.Xs;         // [r][32]
+    const float* maskb = p.mask ? p.mask + b * p.sMb : nullptr;
+    __syncthreads();  // every wave is done with the last K tile
+    {
+      const int64_t n = n0 + wn + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        const int64_t m = m0 + ml;
+        float v = 0.f;
+        if (m < p.M && n < p.N) {
+          v = acc[0][0][r] * p.alpha;
+          if (maskb && !(maskb[m * p.sMm + n * p.sMn] > 0.f)) v = 0.f;
+        }
+        T[ml * LT + wn + li] = v;
+      }
+      const float* xb = p.ew_x + b * p.ew_sxb;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = t + q * NT, r = e >> 5, d = e & 31;
+        const int64_t m = m0 + r;
+        X[e] = (m < p.M && d < p.ew_nin) ? xb[m * p.ew_ldx + d] : 0.f;
+      }
+    }
+    __syncthreads();
+    const int64_t C_ = p.batch;
+    if (t < BN && n0 + t < p.N) {  // bias gradient partial: fp64 column sum
+      double v = 0.0;
+      for (int r = 0; r < BM; ++r) v += (double)T[r * LT + t];
+      p.ew_db[(by * C_ + b) * p.N + n0 + t] = (float)v;
+    }
+    const int jb = wid & 3, kq = wid >> 2;
+    f32x16 a2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a2[r] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 32; kk += 2) {
+      const int r = kq * 32 + kk + lk;
+      a2 = __builtin_amdgcn_mfma_f32_32x32x2f32(T[r * LT + jb * 32 + li], X[r * 32 + li], a2, 0,
+                                                0, 0);
+    }
+    __syncthreads();  // T is free: reuse it for the four row-quarter partials
+    float* red = T;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(wid * 16 + r) * 64 + lane] = a2[r];
+    __syncthreads();
+    if (wid < 4) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = red[(wid * 16 + r) * 64 + lane];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) v += red[((q * 4 + wid) * 16 + r) * 64 + lane];
+        const int64_t j = n0 + wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (li < p.ew_nin && j < p.N)
+          p.ew_dW[((by * C_ + b) * p.N + j) * p.ew_nin + li] = v;
+      }
+    }
+    return;
+  }
+
   // epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
   float* Cb = p.C + b * p.sCb + t2 * p.sCb2 + s * p.sCs;
   const float* biasb = p.bias ? p.bias + b * p.sbias_b + t2 * p.sbias_b2 : nullptr;
@@ -365,12 +447,15 @@ __device__ __forceinline__ void xcd_tile(int64_t& bx, int64_t& by, int64_t& bz) 
 }
 
 template <int AMODE, int BMODE, int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK,
-          bool AGEN = false>
+          bool AGEN = false, bool EW = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32_kernel(Params p) {
-  __shared__ __attribute__((aligned(16))) TileLds<WM_T, WN_T, WAVES_M, WAVES_N, BK> lds;
+  using LdsT = typename std::conditional<EW, TileLdsEW<WM_T, WN_T, WAVES_M, WAVES_N, BK>,
+                                         TileLds<WM_T, WN_T, WAVES_M, WAVES_N, BK>>::type;
+  __shared__ __attribute__((aligned(16))) LdsT lds;
   int64_t bx, by, bz;
   xcd_tile(bx, by, bz);
-  gemm_f32_tile<AMODE, BMODE, WM_T, WN_T, WAVES_M, WAVES_N, BK, AGEN>(p, bx, by, bz, lds);
+  gemm_f32_tile<AMODE, BMODE, WM_T, WN_T, WAVES_M, WAVES_N, BK, AGEN, EW, LdsT>(p, bx, by, bz,
+                                                                              lds);
 }
 
 // ---- register-direct split-K kernel for small problems ---------------------
@@ -542,13 +627,13 @@ constexpr Variant kVariants[] = {
 constexpr int kFirstRd = 9;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-template <int AM, int BMd, int V, bool AGEN = false>
+template <int AM, int BMd, int V, bool AGEN = false, bool EW = false>
 void launch_v(const Params& p, hipStream_t st) {
   constexpr Variant v = kVariants[V];
   constexpr int BM = 32 * v.wm_t * v.waves_m, BN = 32 * v.wn_t * v.waves_n;
   dim3 grid((unsigned)((p.N + BN - 1) / BN), (unsigned)((p.M + BM - 1) / BM),
             (unsigned)(p.batch * p.batch2 * p.splits));
-  hipLaunchKernelGGL((gemm_f32_kernel<AM, BMd, v.wm_t, v.wn_t, v.waves_m, v.waves_n, v.bk, AGEN>), grid,
+  hipLaunchKernelGGL((gemm_f32_kernel<AM, BMd, v.wm_t, v.wn_t, v.waves_m, v.waves_n, v.bk, AGEN, EW>), grid,
                      dim3(64 * v.waves_m * v.waves_n), 0, st, p);
 }
 
@@ -647,7 +732,7 @@ namespace {
 // Validate a descriptor and fill the kernel parameters; *skip = the problem is empty.
 int make_params(const d3a_gemm_desc* d, Params& p, int& variant, int& am, int& bm, bool& skip) {
   D3A_CHECK_ARG(d != nullptr, "d3a_gemm_f32: null descriptor");
-  D3A_CHECK_ARG((d->A || d->agen) && d->B && d->C, "d3a_gemm_f32: null operand");
+  D3A_CHECK_ARG((d->A || d->agen) && d->B && (d->C || d->wnext), "d3a_gemm_f32: null operand");
   D3A_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0 && d->batch >= 0,
                 "d3a_gemm_f32: negative size");
   D3A_CHECK_ARG(d->splits >= 1, "d3a_gemm_f32: splits must be >= 1");
@@ -690,6 +775,20 @@ int make_params(const d3a_gemm_desc* d, Params& p, int& variant, int& am, int& b
   if (variant < 0) variant = choose_variant(p);
   // generated A: the LDS tiles launch_agen instantiates
   if (d->agen) variant = (d->M >= 128 && d->N >= 128) ? 14 : 0;  // as launch_agen
+  p.ew_x = nullptr; p.ew_dW = nullptr; p.ew_db = nullptr;
+  p.ew_ldx = p.ew_sxb = p.ew_nin = 0;
+  if (d->wnext) {
+    const d3a_gemm_wnext* w = d->wnext;
+    D3A_CHECK_ARG(w->x && w->dW && w->db && w->n_in >= 1 && w->n_in <= 32,
+                  "d3a_gemm_f32: wnext needs x, dW, db and 1..32 inputs");
+    D3A_CHECK_ARG(d->sAk == 1 && d->sBk != 0 && d->splits == 1 && p.batch2 == 1 &&
+                      !d->rowsum && !d->accumulate && !d->bias && !d->relu,
+                  "d3a_gemm_f32: wnext on a plain input-gradient GEMM (A k-contiguous)");
+    D3A_CHECK_ARG(d->sBk == 1 || d->sBn == 1, "d3a_gemm_f32: wnext needs a contiguous B");
+    p.ew_x = w->x; p.ew_ldx = w->ldx; p.ew_sxb = w->sxb; p.ew_nin = w->n_in;
+    p.ew_dW = w->dW; p.ew_db = w->db;
+    variant = 14;
+  }
   const int bk = kVariants[variant].bk;
   // split K in BK multiples (every split starts on a K-tile boundary)
   int64_t kc = (d->K + d->splits - 1) / d->splits;
@@ -712,6 +811,16 @@ void launch_agen(const Params& p, hipStream_t st) {
 }
 
 void launch_params(const Params& p, int variant, int am, int bm, hipStream_t st) {
+  if (p.ew_x) {  // checked: A k-contiguous, 128x128 tile
+    if (p.hg_h) {
+      if (bm == MODE_KCONTIG) launch_v<MODE_KCONTIG, MODE_KCONTIG, 14, true, true>(p, st);
+      else launch_v<MODE_KCONTIG, MODE_XCONTIG, 14, true, true>(p, st);
+    } else {
+      if (bm == MODE_KCONTIG) launch_v<MODE_KCONTIG, MODE_KCONTIG, 14, false, true>(p, st);
+      else launch_v<MODE_KCONTIG, MODE_XCONTIG, 14, false, true>(p, st);
+    }
+    return;
+  }
   if (p.hg_h) {
     if (am == MODE_KCONTIG) {
       if (bm == MODE_KCONTIG) launch_agen<MODE_KCONTIG, MODE_KCONTIG>(p, st);

@@ -70,6 +70,9 @@ _FUSED_BWD = os.environ.get("D3A_FUSED_BWD", "0") == "1"
 # the register-direct GEMM + d3a_head1_bwd is faster
 _HEAD_GEN = os.environ.get("D3A_HEAD_GEN", "1") == "1"
 _HEAD_GEN_MIN_ROWS = 4096
+# the first layer's weight gradient formed in the epilogue of the second
+# layer's input-gradient GEMM (d3a_gemm_desc.wnext): same size gate
+_FIRST_LAYER_EPI = os.environ.get("D3A_W0_EPI", "1") == "1"
 # rows per fused workgroup (32 or 64; 0 = the library's choice)
 _FUSED_BM = int(os.environ.get("D3A_FUSED_BM", "0"))
 
@@ -197,11 +200,17 @@ class BackwardSpace:
         self.g_eff = torch.zeros(net.C, rows, device=device) if self.fused else None
         self.splits = n_splits(rows) if splits is None else splits
         self.grads = grads
+        # first-layer weight gradients as one partial per 128-row tile, from
+        # the second layer's input-gradient GEMM (backward's wnext path)
+        self.l0_tiles = None
+        if (grads is not None and _FIRST_LAYER_EPI and not self.fused and net.n_layers >= 2
+                and net.sizes[0] <= 32 and rows * net.C >= _HEAD_GEN_MIN_ROWS):
+            self.l0_tiles = (rows + 127) // 128
         if grads is not None:
             for l in range(net.n_layers):
                 o, i = net.sizes[l + 1], net.sizes[l]
                 parts = head_partials if (head_partials and l == net.n_layers - 1) \
-                    else self.splits
+                    else (self.l0_tiles if (l == 0 and self.l0_tiles) else self.splits)
                 grads.add(net.wname(l), (net.C, o, i), parts)
                 grads.add(net.bname(l), (net.C, o), parts)
 
@@ -309,16 +318,31 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
             ops.linear_bwd_x(dout, ld_dout, sdout_b, net.W(L - 1, store), cur.data_ptr(), ld_cur,
                              scur, C, n, Hin, out_dim, mask=hin, ldm=ld_h, smb=sh)
     # ---- trunk layers L-2 .. 0
+    # first layer's weight gradients from the second layer's dX epilogue
+    ew = (bs.l0_tiles is not None and weight_grads and dx is None and n == bs.rows
+          and not ops.SBF16_TERMS)
     for l in range(L - 2, -1, -1):
         Hout = sizes[l + 1]
         Hin = sizes[l]
         hin, ld_h, sh = h_ptr(l)
         dz = cur
         ag = agen if l == L - 2 else None  # the head's dz, generated
+        if l == 0 and ew:
+            break  # written by the l == 1 launch
         if weight_grads:
             gW, gb = gs.get(net.wname(l)), gs.get(net.bname(l))
+            S_l = bs.l0_tiles if (l == 0 and bs.l0_tiles) else S
             ops.linear_bwd_w(dz.data_ptr(), ld_cur, scur, hin, ld_h, sh, gW.data_ptr(), C, n, Hin,
-                             Hout, S, db=gb.data_ptr(), agen=ag)
+                             Hout, S_l, db=gb.data_ptr(), agen=ag)
+        if l == 1 and ew:
+            x0, ldx0, sx0 = h_ptr(0)
+            wn = N.GemmWnext()
+            wn.x, wn.ldx, wn.sxb, wn.n_in = x0, ldx0, sx0, sizes[0]
+            wn.dW = gs.get(net.wname(0)).data_ptr()
+            wn.db = gs.get(net.bname(0)).data_ptr()
+            ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(1, store), 0, ld_cur, scur, C, n,
+                             Hin, Hout, mask=hin, ldm=ld_h, smb=sh, agen=ag, wnext=wn)
+            continue
         if l > 0:
             nxt = bs.dz[1] if cur is bs.dz[0] else bs.dz[0]
             ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(l, store), nxt.data_ptr(), ld_cur,

@@ -43,7 +43,7 @@ def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
          relu: bool = False, accumulate: bool = False, splits: int = 1, sCs: int = 0,
          alpha: float = 1.0, rowsum: Optional[int] = None, sR: Sequence[int] = (0, 0),
          variant: int = -1, pair: Optional[Sequence[int]] = None,
-         agen: Optional[C.Structure] = None) -> None:
+         agen: Optional[C.Structure] = None, wnext: Optional[C.Structure] = None) -> None:
     """C_b,s(m,n) = epi(alpha * sum_k A_b(m,k) B_b(k,n)); strides (batch, row, col).
     ``agen`` (a Head1BwdDesc): A is generated as that head's masked input
     gradient instead of read (d3a_gemm_desc.agen).
@@ -67,6 +67,8 @@ def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
         d.sAb2, d.sBb2, d.sCb2, d.sbias_b2 = pair
     if agen is not None:
         d.agen = C.addressof(agen)
+    if wnext is not None:
+        d.wnext = C.addressof(wnext)
     if _TRACE:
         print(f"gemm M={M} N={Nn} K={K} batch={batch} splits={splits} sA={tuple(sA)} "
               f"sB={tuple(sB)} sC={tuple(sC)} mask={mask is not None} relu={relu} "
@@ -213,9 +215,21 @@ def set_sbf16(terms: int) -> None:
 
 def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: int, C_: int,
                  R: int, n_in: int, n_out: int, mask: Optional[int] = None,
-                 ldm: int = 0, smb: int = 0, agen: Optional[C.Structure] = None) -> None:
+                 ldm: int = 0, smb: int = 0, agen: Optional[C.Structure] = None,
+                 wnext: Optional[C.Structure] = None) -> None:
     """dx[c] = (dy[c] @ W[c]) * [mask[c] > 0]; with ``agen`` dy is generated
-    from that single-output head (d3a_gemm_desc.agen) and not read."""
+    from that single-output head (d3a_gemm_desc.agen) and not read; with
+    ``wnext`` (a GemmWnext) dx is not written but the layer below's weight /
+    bias gradient partials per 128-row tile (d3a_gemm_desc.wnext)."""
+    if wnext is not None:
+        if agen is not None and agen.dW:
+            agen = type(agen).from_buffer_copy(agen)
+            agen.dW = agen.db = None
+        gemm(None if agen is not None else dy, W, None, R, n_in, n_out, batch=C_,
+             sA=(0 if agen is not None else sdyb, n_out if agen is not None else ldy, 1),
+             sB=(n_out * n_in, n_in, 1), sC=(0, 0, 0), mask=mask, sM=(smb, ldm, 1),
+             agen=agen, wnext=wnext)
+        return
     if agen is not None:
         if agen.dW:  # the head's weight gradients come from the dW launch only
             agen = type(agen).from_buffer_copy(agen)

@@ -49,6 +49,15 @@ int d3a_device_count(int* count);
  *   C_b,s(m,n) = C[b*sCb + s*sCs + m*sCm + n*sCn].
  * A forward nn.Linear is (A = x [rows,in], B = W^T i.e. sBk=1,sBn=in),
  * dX = dY W is (A = dY, B = W), dW = dY^T X is (A = dY^T, B = X). */
+/* Next-layer weight-gradient epilogue of an input-gradient GEMM (see
+ * d3a_gemm_desc.wnext). */
+typedef struct d3a_gemm_wnext {
+  const float* x; int64_t ldx, sxb;  /* layer input rows x[b*sxb + r*ldx + d] */
+  int64_t n_in;                      /* d < n_in <= 32                       */
+  float* dW;  /* [ceil(M/128)][batch][N][n_in] partials                      */
+  float* db;  /* [ceil(M/128)][batch][N] partials                            */
+} d3a_gemm_wnext;
+
 typedef struct d3a_gemm_desc {
   const float* A;
   const float* B;
@@ -86,6 +95,15 @@ typedef struct d3a_gemm_desc {
    * agen->db[s][b] = sum g'[r] (fp64-accumulated, as d3a_head1_bwd does) —
    * the head backward needs no launch of its own. */
   const struct d3a_head1_bwd_desc* agen;
+  /* Optional (may be NULL) on an input-gradient GEMM whose output C_b(r, j)
+   * is the masked gradient dz of the layer below (A k-contiguous, no split,
+   * bias, ReLU or rowsum): C is not written (may be NULL); instead, per
+   * 128-row tile t, the weight / bias gradient partials of the layer whose
+   * input is x:  wnext->dW[t][b][j][d] = sum_{r in t} C_b(r, j) x[r][d],
+   * wnext->db[t][b][j] = sum_{r in t} C_b(r, j) (fp64-accumulated) — the
+   * first layer's weight gradient without a launch of its own or a dz
+   * round trip through HBM. */
+  const d3a_gemm_wnext* wnext;
 } d3a_gemm_desc;
 int d3a_gemm_f32(const d3a_gemm_desc* desc, void* stream);
 

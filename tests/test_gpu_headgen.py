@@ -89,3 +89,65 @@ def test_head_gradient_generated_in_gemms(rows, n_scaled):
         e = float((tot - ref).abs().max()) / max(1e-30, float(ref.abs().max()))
         assert e <= 1e-6, e
     assert not torch.isnan(dWh).any() and not torch.isnan(dbh).any()
+
+
+@pytest.mark.parametrize("generated", [False, True])
+def test_first_layer_weight_gradient_epilogue(generated):
+    """wnext: the layer-0 weight / bias gradient partials formed from the
+    layer-1 input-gradient tile (dz1 never written) against dz1 written by the
+    plain GEMM and reduced by linear_bwd_w: the 128-row-tile totals agree to
+    fp32 rounding (max-normalised 1e-6)."""
+    g = torch.Generator(device="cuda").manual_seed(12)
+    Cm, rows, H, n_in, ldx = 2, 7936 - 37, 256, 14, 16
+    dev = "cuda"
+    x = torch.randn(rows, ldx, device=dev, generator=g)
+    x[:, n_in:] = 0
+    h1 = torch.relu(torch.randn(Cm, rows, H, device=dev, generator=g))
+    h2 = torch.relu(torch.randn(Cm, rows, H, device=dev, generator=g))
+    dz2 = torch.randn(Cm, rows, H, device=dev, generator=g) * 1e-3
+    W2 = torch.randn(Cm, H, H, device=dev, generator=g) * 0.06
+    gr = torch.randn(Cm, rows, device=dev, generator=g) * 1e-2
+    w = torch.randn(Cm, H, device=dev, generator=g) * 0.06
+    ag = None
+    if generated:
+        ag = N.Head1BwdDesc()
+        ag.g, ag.sgb = gr.data_ptr(), rows
+        ag.h, ag.shb, ag.ldh = h2.data_ptr(), rows * H, H
+        ag.w, ag.swb = w.data_ptr(), H
+        ag.rows, ag.n, ag.C, ag.splits = rows, H, Cm, 1
+        dz2 = torch.where(h2 > 0, gr[:, :, None] * w[:, None, :], torch.zeros((), device=dev))
+    P = (rows + 127) // 128
+    prev = ops.SBF16_TERMS
+    ops.set_sbf16(0)
+    try:
+        dz1 = torch.zeros(Cm, rows, H, device=dev)
+        ops.linear_bwd_x(dz2.data_ptr(), H, rows * H, W2.data_ptr(), dz1.data_ptr(), H, rows * H,
+                         Cm, rows, H, H, mask=h1.data_ptr(), ldm=H, smb=rows * H)
+        dW_ref = torch.zeros(P, Cm, H, n_in, device=dev)
+        db_ref = torch.zeros(P, Cm, H, device=dev)
+        ops.linear_bwd_w(dz1.data_ptr(), H, rows * H, x.data_ptr(), ldx, 0, dW_ref.data_ptr(), Cm,
+                         rows, n_in, H, P, db=db_ref.data_ptr())
+        dW = torch.full((P, Cm, H, n_in), float("nan"), device=dev)
+        db = torch.full((P, Cm, H), float("nan"), device=dev)
+        wn = N.GemmWnext()
+        wn.x, wn.ldx, wn.sxb, wn.n_in = x.data_ptr(), ldx, 0, n_in
+        wn.dW, wn.db = dW.data_ptr(), db.data_ptr()
+        ops.linear_bwd_x(0 if generated else dz2.data_ptr(), H, rows * H, W2.data_ptr(), 0, H,
+                         rows * H, Cm, rows, H, H, mask=h1.data_ptr(), ldm=H, smb=rows * H,
+                         agen=ag, wnext=wn)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_sbf16(prev)
+    assert not torch.isnan(dW).any() and not torch.isnan(db).any()
+    ref_w = torch.einsum("crj,rd->cjd", dz1.double(), x[:, :n_in].double())
+    ref_b = dz1.double().sum(1)
+    for tot, ref in ((dW.double().sum(0), ref_w), (dW_ref.double().sum(0), ref_w),
+                     (db.double().sum(0), ref_b), (db_ref.double().sum(0), ref_b)):
+        e = float((tot - ref).abs().max()) / float(ref.abs().max())
+        assert e <= 1e-6, e
+    # per tile: the same 128 rows
+    tile_w = torch.stack([torch.einsum("crj,rd->cjd", dz1[:, t * 128:(t + 1) * 128].double(),
+                                       x[t * 128:(t + 1) * 128, :n_in].double())
+                          for t in range(P)])
+    e = float((dW.double() - tile_w).abs().max()) / float(tile_w.abs().max())
+    assert e <= 1e-6, e

@@ -45,7 +45,8 @@ def test_argument_errors_are_reported_without_a_gpu():
         N.check(rc, "d3a_gemm_f32")
 
 
-STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_adam_segment", "AdamSegment"),
+STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_gemm_wnext", "GemmWnext"),
+           ("d3a_adam_segment", "AdamSegment"),
            ("d3a_head1_bwd_desc", "Head1BwdDesc"),
            ("d3a_cql_sample_desc", "CqlSampleDesc"), ("d3a_cql_loss_desc", "CqlLossDesc"),
            ("d3a_sac_actor_head_desc", "SacActorHeadDesc"), ("d3a_gather_desc", "GatherDesc"),
