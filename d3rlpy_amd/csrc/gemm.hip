@@ -112,7 +112,7 @@ struct TileLds {
 // + the input-row tile of the next layer's weight-gradient epilogue (EW)
 template <int WM_T, int WN_T, int WAVES_M, int WAVES_N, int BK>
 struct TileLdsEW : TileLds<WM_T, WN_T, WAVES_M, WAVES_N, BK> {
-  float Xs[32 * WM_T * WAVES_M * 32];
+  float Xs[32 * WM_T * WAVES_M * 64];
 };
 
 // One BM x BN output tile (block coordinates bx, by, bz) of the GEMM p.
@@ -335,15 +335,15 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
     // tile goes to LDS and the previous layer's weight / bias gradient
     // partials of this 128-row tile are formed from it,
     //   dW[t][b][j][d] = sum_r C(r, j) x[r][d],  db[t][b][j] = sum_r C(r, j)
-    // (t = by), with x (<= 32 inputs) staged beside it.  Wave w multiplies
-    // the 32 j of block w&3 over rows 32*(w>>2)..+31; the four row quarters
-    // are summed in order (deterministic).
+    // (t = by), with x (<= 64 inputs, nd 32-wide blocks) staged beside it.
+    // Wave w multiplies the 32 j of block w&3 by input block (w>>2)%nd over
+    // one of 4/nd row slices; the slices are summed in order (deterministic).
     static_assert(BM == 128 && BN == 128 && NT == 1024 && WM_T == 1 && WN_T == 1,
                   "EW epilogue: 128x128 tile of sixteen 32x32 waves");
     constexpr int LT = BN + 4;
     static_assert(sizeof(L.As) + sizeof(L.Bs) >= sizeof(float) * BM * LT, "T tile");
     float* T = &L.As[0][0];  // [r][LT], spans As and Bs (contiguous)
-    float* X = L.Xs;         // [r][32]
+    float* X = L.Xs;         // [r][64]
     const float* maskb = p.mask ? p.mask + b * p.sMb : nullptr;
     __syncthreads();  // every wave is done with the last K tile
     {
@@ -360,11 +360,20 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
         T[ml * LT + wn + li] = v;
       }
       const float* xb = p.ew_x + b * p.ew_sxb;
+      if (p.ew_nin <= 32) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int e = t + q * NT, r = e >> 5, d = e & 31;
-        const int64_t m = m0 + r;
-        X[e] = (m < p.M && d < p.ew_nin) ? xb[m * p.ew_ldx + d] : 0.f;
+        for (int q = 0; q < 4; ++q) {
+          const int e = t + q * NT, r = e >> 5, d = e & 31;
+          const int64_t m = m0 + r;
+          X[r * 64 + d] = (m < p.M && d < p.ew_nin) ? xb[m * p.ew_ldx + d] : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int e = t + q * NT, r = e >> 6, d = e & 63;
+          const int64_t m = m0 + r;
+          X[e] = (m < p.M && d < p.ew_nin) ? xb[m * p.ew_ldx + d] : 0.f;
+        }
       }
     }
     __syncthreads();
@@ -374,30 +383,35 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
       for (int r = 0; r < BM; ++r) v += (double)T[r * LT + t];
       p.ew_db[(by * C_ + b) * p.N + n0 + t] = (float)v;
     }
-    const int jb = wid & 3, kq = wid >> 2;
+    const int nd = p.ew_nin > 32 ? 2 : 1, nkq = 4 / nd;
+    const int jb = wid & 3, dq = (wid >> 2) % nd, kq = (wid >> 2) / nd;
     f32x16 a2;
 #pragma unroll
     for (int r = 0; r < 16; ++r) a2[r] = 0.f;
+    auto ew_mma = [&](auto sl) {
+      constexpr int SL = decltype(sl)::value;
 #pragma unroll
-    for (int kk = 0; kk < 32; kk += 2) {
-      const int r = kq * 32 + kk + lk;
-      a2 = __builtin_amdgcn_mfma_f32_32x32x2f32(T[r * LT + jb * 32 + li], X[r * 32 + li], a2, 0,
-                                                0, 0);
-    }
+      for (int kk = 0; kk < SL; kk += 2) {
+        const int r = kq * SL + kk + lk;
+        a2 = __builtin_amdgcn_mfma_f32_32x32x2f32(T[r * LT + jb * 32 + li],
+                                                  X[r * 64 + dq * 32 + li], a2, 0, 0, 0);
+      }
+    };
+    if (nd == 1) ew_mma(std::integral_constant<int, BM / 4>());
+    else ew_mma(std::integral_constant<int, BM / 2>());
     __syncthreads();  // T is free: reuse it for the four row-quarter partials
     float* red = T;
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[(wid * 16 + r) * 64 + lane] = a2[r];
     __syncthreads();
-    if (wid < 4) {
+    if (kq == 0) {  // waves w < 4 * nd: sum the row slices of (jb, dq) in order
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float v = red[(wid * 16 + r) * 64 + lane];
-#pragma unroll
-        for (int q = 1; q < 4; ++q) v += red[((q * 4 + wid) * 16 + r) * 64 + lane];
-        const int64_t j = n0 + wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (li < p.ew_nin && j < p.N)
-          p.ew_dW[((by * C_ + b) * p.N + j) * p.ew_nin + li] = v;
+        for (int q = 1; q < nkq; ++q) v += red[((wid + 4 * nd * q) * 16 + r) * 64 + lane];
+        const int64_t j = n0 + jb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        const int d = dq * 32 + li;
+        if (d < p.ew_nin && j < p.N) p.ew_dW[((by * C_ + b) * p.N + j) * p.ew_nin + d] = v;
       }
     }
     return;
@@ -779,8 +793,8 @@ int make_params(const d3a_gemm_desc* d, Params& p, int& variant, int& am, int& b
   p.ew_ldx = p.ew_sxb = p.ew_nin = 0;
   if (d->wnext) {
     const d3a_gemm_wnext* w = d->wnext;
-    D3A_CHECK_ARG(w->x && w->dW && w->db && w->n_in >= 1 && w->n_in <= 32,
-                  "d3a_gemm_f32: wnext needs x, dW, db and 1..32 inputs");
+    D3A_CHECK_ARG(w->x && w->dW && w->db && w->n_in >= 1 && w->n_in <= 64,
+                  "d3a_gemm_f32: wnext needs x, dW, db and 1..64 inputs");
     D3A_CHECK_ARG(d->sAk == 1 && d->sBk != 0 && d->splits == 1 && p.batch2 == 1 &&
                       !d->rowsum && !d->accumulate && !d->bias && !d->relu,
                   "d3a_gemm_f32: wnext on a plain input-gradient GEMM (A k-contiguous)");

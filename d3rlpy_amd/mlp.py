@@ -204,7 +204,7 @@ class BackwardSpace:
         # the second layer's input-gradient GEMM (backward's wnext path)
         self.l0_tiles = None
         if (grads is not None and _FIRST_LAYER_EPI and not self.fused and net.n_layers >= 2
-                and net.sizes[0] <= 32 and rows * net.C >= _HEAD_GEN_MIN_ROWS):
+                and net.sizes[0] <= 64 and rows * net.C >= _HEAD_GEN_MIN_ROWS):
             self.l0_tiles = (rows + 127) // 128
         if grads is not None:
             for l in range(net.n_layers):

@@ -53,7 +53,7 @@ int d3a_device_count(int* count);
  * d3a_gemm_desc.wnext). */
 typedef struct d3a_gemm_wnext {
   const float* x; int64_t ldx, sxb;  /* layer input rows x[b*sxb + r*ldx + d] */
-  int64_t n_in;                      /* d < n_in <= 32                       */
+  int64_t n_in;                      /* d < n_in <= 64                       */
   float* dW;  /* [ceil(M/128)][batch][N][n_in] partials                      */
   float* db;  /* [ceil(M/128)][batch][N] partials                            */
 } d3a_gemm_wnext;

@@ -91,14 +91,15 @@ def test_head_gradient_generated_in_gemms(rows, n_scaled):
     assert not torch.isnan(dWh).any() and not torch.isnan(dbh).any()
 
 
-@pytest.mark.parametrize("generated", [False, True])
-def test_first_layer_weight_gradient_epilogue(generated):
+@pytest.mark.parametrize("generated,n_in,ldx", [(False, 14, 16), (True, 14, 16),
+                                                (True, 37, 40), (False, 64, 64)])
+def test_first_layer_weight_gradient_epilogue(generated, n_in, ldx):
     """wnext: the layer-0 weight / bias gradient partials formed from the
     layer-1 input-gradient tile (dz1 never written) against dz1 written by the
     plain GEMM and reduced by linear_bwd_w: the 128-row-tile totals agree to
     fp32 rounding (max-normalised 1e-6)."""
     g = torch.Generator(device="cuda").manual_seed(12)
-    Cm, rows, H, n_in, ldx = 2, 7936 - 37, 256, 14, 16
+    Cm, rows, H = 2, 7936 - 37, 256
     dev = "cuda"
     x = torch.randn(rows, ldx, device=dev, generator=g)
     x[:, n_in:] = 0
