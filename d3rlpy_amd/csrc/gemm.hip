@@ -283,6 +283,21 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
     lstore(ra0, rx0, rb0, 0);
     if (kbeg + BK < kend) gload(ra1, rx1, rb1, kbeg + BK);
   }
+  // one accumulator tile per wave: its ReLU-mask operand is loaded now and
+  // stays in registers, so the epilogue does not wait a memory round trip
+  constexpr bool kMaskPf = WM_T == 1 && WN_T == 1;
+  float mpf[16];
+  if constexpr (kMaskPf) {
+    if (p.mask) {
+      const float* mb = p.mask + b * p.sMb + t2 * p.sMb2;
+      const int64_t n = n0 + wn + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        mpf[r] = (m < p.M && n < p.N) ? mb[m * p.sMm + n * p.sMn] : 0.f;
+      }
+    }
+  }
   __syncthreads();
   // even tiles in LDS buffer 0 / registers 0, odd tiles in buffer 1 / registers 1
   for (int64_t k0 = kbeg; k0 < kend;) {
@@ -355,7 +370,7 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
         float v = 0.f;
         if (m < p.M && n < p.N) {
           v = acc[0][0][r] * p.alpha;
-          if (maskb && !(maskb[m * p.sMm + n * p.sMn] > 0.f)) v = 0.f;
+          if (maskb && !(mpf[r] > 0.f)) v = 0.f;
         }
         T[ml * LT + wn + li] = v;
       }
@@ -435,7 +450,7 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
           float v = acc[i][j][r] * p.alpha;
           if (biasb) v += bn;
           if (p.relu) v = fmaxf(v, 0.f);
-          if (maskb && !(maskb[m * p.sMm + n * p.sMn] > 0.f)) v = 0.f;
+          if (maskb && !((kMaskPf ? mpf[r] : maskb[m * p.sMm + n * p.sMn]) > 0.f)) v = 0.f;
           float* dst = Cb + m * p.sCm + n * p.sCn;
           if (p.accumulate) *dst += v; else *dst = v;
         }
