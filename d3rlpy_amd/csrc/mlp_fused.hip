@@ -187,7 +187,7 @@ void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
                        [&](int k) { return *reinterpret_cast<const float4*>(W + (wo + k)); });
       }
     };
-    auto epi = [&](const f32x16* acc, int n, float* dst) {
+    auto epi = [&](const f32x16* acc, int n, float* dst, bool store_h) {
       if (n >= N) return;
       const float bn = bias[n];
       // this lane's rows: lrow + mo(i, r); row validity from the masks
@@ -207,7 +207,7 @@ void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
             dst[(lrow + mo) * LDK + n] = v;
             // the global copy for the backward pass leaves with the
             // epilogue (overlapping the other waves' MFMAs)
-            if (gp && ok) gp[mo * ldg] = v;
+            if (store_h && gp && ok) gp[mo * ldg] = v;
           }
         }
       }
@@ -220,15 +220,28 @@ void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
       f32x16 acc[RTW];
       if (act) mma(acc, n);
       __syncthreads();
-      if (act) epi(acc, n, bufA);
+      if (act) epi(acc, n, bufA, false);
       __syncthreads();
+      // the activations kept for the backward leave from LDS as whole
+      // 16-byte row pieces (8 stores per thread instead of 16 scalar stores
+      // per row tile per lane); the next layer only reads bufA meanwhile
+      if (gout) {
+        const int n4 = N / 4;
+        for (int e = t; e < BM * n4; e += NT) {
+          const int rr = e / n4, c4 = (e - rr * n4) * 4;
+          const int64_t row = m0 + rr;
+          if (row >= h_from && row < rend)
+            *reinterpret_cast<float4*>(&gout[row * ldg + c4]) =
+                *reinterpret_cast<const float4*>(&bufA[rr * LDK + c4]);
+        }
+      }
       continue;
     }
     for (int ct = w / RG; ct < (N + 31) / 32; ct += NCW) {
       const int n = ct * 32 + li;
       f32x16 acc[RTW];
       mma(acc, n);
-      epi(acc, n, bufB);
+      epi(acc, n, bufB, true);
     }
     if (head) return;
     __syncthreads();
