@@ -50,6 +50,7 @@ struct Params {
   // next layer's weight-gradient epilogue (d3a_gemm_desc.wnext)
   const float* ew_x; int64_t ew_ldx, ew_sxb, ew_nin;
   float* ew_dW; float* ew_db;
+  int xcd_remap;
 };
 
 // Load a 4-vector of a tile at non-k coordinate x and reduction coordinate k.
@@ -158,15 +159,12 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
   const bool do_rowsum = p.rowsum != nullptr && bx == 0;
   double rs = 0.0;
 
-  // Global->register->LDS pipeline two K tiles deep: the loads of tile i+2
-  // are issued while tile i is multiplied and stored to LDS only at the end
-  // of tile i+1, so each load has two tiles' worth of MFMA work to land.
-  float4 ra0[AV], rb0[BV], ra1[AV], rb1[BV];
+  float4 ra0[AV], rb0[BV];
   // Generated A (the head backward, AGEN): gload keeps the raw loads (h and,
   // per K tile, w[j..j+3] (A k-contiguous) or g[r] and its scale (A
   // m-contiguous)) in registers and lstore forms g'[r] * w[j] * [h > 0], so
   // the loads stay in flight across the MFMA work like plain operands.
-  float4 rx0[AV], rx1[AV];
+  float4 rx0[AV];
   const float* hgH = AGEN ? p.hg_h + b * p.hg_shb : nullptr;
   const float* hgG = AGEN ? p.hg_g + b * p.hg_sgb : nullptr;
   const float* hgW = AGEN ? p.hg_w + b * p.hg_swb : nullptr;
@@ -253,24 +251,18 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
   auto compute = [&](int buf) {
     const float* Ac = As[buf];
     const float* Bc = Bs[buf];
-    // every operand of the K tile is read from LDS before the first MFMA, so
-    // the reads overlap each other instead of each MFMA waiting one LDS latency
-    float av[BK / 2][WM_T], bv[BK / 2][WN_T];
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
+      float av[WM_T], bv[WN_T];
 #pragma unroll
-      for (int i = 0; i < WM_T; ++i) av[kk / 2][i] = Ac[(kk + lk) * LDA + wm + 32 * i + li];
+      for (int i = 0; i < WM_T; ++i) av[i] = Ac[(kk + lk) * LDA + wm + 32 * i + li];
 #pragma unroll
-      for (int j = 0; j < WN_T; ++j) bv[kk / 2][j] = Bc[(kk + lk) * LDB + wn + 32 * j + li];
-    }
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
+      for (int j = 0; j < WN_T; ++j) bv[j] = Bc[(kk + lk) * LDB + wn + 32 * j + li];
 #pragma unroll
       for (int i = 0; i < WM_T; ++i)
 #pragma unroll
         for (int j = 0; j < WN_T; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk / 2][i], bv[kk / 2][j],
-                                                          acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
     if (do_rowsum && t < BM) {
 #pragma unroll
@@ -281,7 +273,6 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
   if (kbeg < kend) {
     gload(ra0, rx0, rb0, kbeg);
     lstore(ra0, rx0, rb0, 0);
-    if (kbeg + BK < kend) gload(ra1, rx1, rb1, kbeg + BK);
   }
   // one accumulator tile per wave: its ReLU-mask operand is loaded now and
   // stays in registers, so the epilogue does not wait a memory round trip
@@ -299,20 +290,16 @@ __device__ __forceinline__ void gemm_f32_tile(const Params& p, int64_t bx, int64
     }
   }
   __syncthreads();
-  // even tiles in LDS buffer 0 / registers 0, odd tiles in buffer 1 / registers 1
-  for (int64_t k0 = kbeg; k0 < kend;) {
-    if (k0 + 2 * BK < kend) gload(ra0, rx0, rb0, k0 + 2 * BK);
-    compute(0);
-    if (k0 + BK >= kend) break;
-    lstore(ra1, rx1, rb1, 1);
+  // the next K tile is loaded into registers while the current one is
+  // multiplied, then stored to the other LDS buffer (one barrier per tile)
+  int cur = 0;
+  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
+    const bool more = k0 + BK < kend;
+    if (more) gload(ra0, rx0, rb0, k0 + BK);
+    compute(cur);
+    if (more) lstore(ra0, rx0, rb0, cur ^ 1);
     __syncthreads();
-    k0 += BK;
-    if (k0 + 2 * BK < kend) gload(ra1, rx1, rb1, k0 + 2 * BK);
-    compute(1);
-    if (k0 + BK >= kend) break;
-    lstore(ra0, rx0, rb0, 0);
-    __syncthreads();
-    k0 += BK;
+    cur ^= 1;
   }
 
   if (do_rowsum && t < BM && m0 + t < p.M)
@@ -481,8 +468,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32_kernel(Params
   using LdsT = typename std::conditional<EW, TileLdsEW<WM_T, WN_T, WAVES_M, WAVES_N, BK>,
                                          TileLds<WM_T, WN_T, WAVES_M, WAVES_N, BK>>::type;
   __shared__ __attribute__((aligned(16))) LdsT lds;
-  int64_t bx, by, bz;
-  xcd_tile(bx, by, bz);
+  int64_t bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (p.xcd_remap) xcd_tile(bx, by, bz);
   gemm_f32_tile<AMODE, BMODE, WM_T, WN_T, WAVES_M, WAVES_N, BK, AGEN, EW, LdsT>(p, bx, by, bz,
                                                                               lds);
 }
@@ -805,6 +792,13 @@ int make_params(const d3a_gemm_desc* d, Params& p, int& variant, int& am, int& b
   // generated A: the LDS tiles launch_agen instantiates
   if (d->agen) variant = (d->M >= 128 && d->N >= 128) ? 14 : 0;  // as launch_agen
   p.ew_x = nullptr; p.ew_dW = nullptr; p.ew_db = nullptr;
+  {
+    static const int xr = [] {
+      const char* e = getenv("D3A_GEMM_XCD");
+      return e ? atoi(e) : 1;
+    }();
+    p.xcd_remap = xr;
+  }
   p.ew_ldx = p.ew_sxb = p.ew_nin = 0;
   if (d->wnext) {
     const d3a_gemm_wnext* w = d->wnext;
