@@ -51,6 +51,20 @@ class GemmWnext(C.Structure):
     ]
 
 
+class Head1MinDesc(C.Structure):
+    _fields_ = [
+        ("h", vp), ("shb", C.c_int64), ("ldh", C.c_int64),
+        ("w", vp), ("swb", C.c_int64),
+        ("b", vp), ("sbb", C.c_int64),
+        ("q", vp), ("sqb", C.c_int64),
+        ("scale", C.c_float),
+        ("g_out", vp), ("sgb", C.c_int64),
+        ("dz", vp), ("sdzb", C.c_int64), ("lddz", C.c_int64),
+        ("rows", C.c_int64), ("n", C.c_int64),
+        ("C", C.c_int32),
+    ]
+
+
 class Head1BwdDesc(C.Structure):
     _fields_ = [
         ("g", vp), ("sgb", C.c_int64),
@@ -387,6 +401,7 @@ _SIGNATURES = {
     "d3a_philox_fill": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_float, C.c_float, C.c_uint64,
                                   vp, vp, vp]),
     "d3a_head1_bwd": (C.c_int, [C.POINTER(Head1BwdDesc), vp]),
+    "d3a_head1_min": (C.c_int, [C.POINTER(Head1MinDesc), vp]),
     "d3a_cql_sample": (C.c_int, [C.POINTER(CqlSampleDesc), vp]),
     "d3a_cql_loss": (C.c_int, [C.POINTER(CqlLossDesc), vp]),
     "d3a_sac_actor_dq": (C.c_int, [vp, C.c_int64, C.c_int32, C.c_int32, vp, C.c_int64, vp]),

@@ -29,6 +29,7 @@ Row layout of the Q-input matrix x_q ([6NB+B][D+A], shared by the C critics):
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional, Sequence, Tuple
 
 import numpy as np
@@ -44,6 +45,9 @@ from .impl_base import DeviceBatch, ImplBase, as_device_batch
 METRIC_NAMES = ("temp_loss", "temp", "alpha_loss", "alpha", "critic_loss", "actor_loss",
                 "td_loss", "conservative_loss")
 
+
+# actor phase: Q head + min-over-critics backward in one launch (d3a_head1_min)
+_HEAD_MIN = os.environ.get("D3A_HEAD_MIN", "1") == "1"
 
 class CQLImpl(ImplBase):
     # conservative term + alpha (cql_impl.py); SACImpl (algos/sac.py) clears it
@@ -589,6 +593,32 @@ class _Workspace:
             self.eps_targ.copy_(g("eps_targ").view(-1))
 
     # ------------------------------------------------------------ roofline
+    def _head_min_desc(self):
+        """d3a_head1_min descriptor for the actor phase (Q head + its backward
+        through min over the critics, one launch), or None where the per-layer
+        shapes do not fit it (then rowdot + d3a_head1_bwd)."""
+        impl = self.impl
+        net = impl.critic
+        s = net.sizes
+        H, B = s[-2], self.B
+        if (s[-1] != 1 or net.n_layers < 2 or H % 4 or H > 256 or net.C > 8
+                or mlp.fused_ok(net, B) or self.abwd.fused or not _HEAD_MIN):
+            return None
+        d = getattr(self, "_hm_desc", None)
+        if d is None:
+            d = NAT.Head1MinDesc()
+            d.h, d.shb, d.ldh = self.aacts.h[-1].data_ptr(), self.aacts.R * H, H
+            d.w, d.swb = net.W(net.n_layers - 1, impl.store), H
+            d.b, d.sbb = net.b(net.n_layers - 1, impl.store), 1
+            d.q, d.sqb = self.aacts.out.data_ptr(), self.aacts.R
+            d.scale = -1.0 / B
+            d.g_out, d.sgb = self.adq.data_ptr(), B
+            dz = self.abwd.dz[0]
+            d.dz, d.sdzb, d.lddz = dz.data_ptr(), dz.shape[1] * dz.shape[2], dz.shape[2]
+            d.rows, d.n, d.C = B, H, net.C
+            self._hm_desc = d
+        return d
+
     def dominant_kernel(self):
         """(launch_fn, flops_per_launch, description) of the MFMA-bound hot
         kernel: the critic-ensemble forward over all R = 6NB+B Q rows of the
@@ -691,12 +721,21 @@ class _Workspace:
                 l.update_temp, l.update_alpha, l.update_critic = 0, 0, 0
                 ops.call_desc("d3a_cql_loss", l)
             # 6. actor: Q(s, tanh u) with the updated critic, dQ/da, policy backward
-            mlp.forward(impl.critic, impl.store, self.x_actor.data_ptr(), True, DA, self.aacts)
             # dL/dq = -1/B on the argmin critic (backward of min over the ensemble)
-            mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA, self.aacts,
-                         self.adq.data_ptr(), 1, B, 0, B, weight_grads=False, dx=self.adx,
-                         q_min=self.aacts.out.data_ptr(), sq_b=B, q_scale=-1.0 / B,
-                         g_out=self.adq.data_ptr())
+            hm = self._head_min_desc()
+            mlp.forward(impl.critic, impl.store, self.x_actor.data_ptr(), True, DA, self.aacts,
+                        skip_head=hm is not None)
+            if hm is not None:
+                # the Q head and its min-over-members backward in one launch
+                ops.call_desc("d3a_head1_min", hm)
+                mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA,
+                             self.aacts, self.adq.data_ptr(), 1, B, 0, B, weight_grads=False,
+                             dx=self.adx, head_ready=True)
+            else:
+                mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA,
+                             self.aacts, self.adq.data_ptr(), 1, B, 0, B, weight_grads=False,
+                             dx=self.adx, q_min=self.aacts.out.data_ptr(), sq_b=B,
+                             q_scale=-1.0 / B, g_out=self.adq.data_ptr())
             ops.call_desc("d3a_sac_actor_head", self.head_desc)
             mlp.backward(self.pbwd, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
                          self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B,

@@ -95,6 +95,61 @@ __global__ __launch_bounds__(1024) void head1_bwd_kernel(d3a_head1_bwd_desc d) {
   }
 }
 
+// d3a_head1_min: one wave per row; lane l holds columns 4l..4l+3 of every
+// member's activation row (loaded once, used for the dot and the mask).
+__global__ __launch_bounds__(256) void head1_min_kernel(d3a_head1_min_desc d) {
+  constexpr int MAXC = 8;
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= d.rows) return;
+  const int64_t k = (int64_t)lane * 4;
+  const bool on = k < d.n;
+  float4 hv[MAXC], wv[MAXC];
+  float q[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    if (c >= d.C) break;
+    hv[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    wv[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (on) {
+      hv[c] = *reinterpret_cast<const float4*>(d.h + c * d.shb + r * d.ldh + k);
+      wv[c] = *reinterpret_cast<const float4*>(d.w + c * d.swb + k);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    if (c >= d.C) break;
+    // the fmaf chain of d3a_rowdot_f32 (n <= 256: one float4 per lane)
+    const float a = fmaf(hv[c].w, wv[c].w,
+                         fmaf(hv[c].z, wv[c].z, fmaf(hv[c].y, wv[c].y, fmaf(hv[c].x, wv[c].x, 0.f))));
+    q[c] = wave_sum(a) + d.b[c * d.sbb];
+  }
+  int arg = 0;
+  float mn = q[0];
+#pragma unroll
+  for (int c = 1; c < MAXC; ++c) {
+    if (c >= d.C) break;
+    if (q[c] < mn) { mn = q[c]; arg = c; }
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    if (c >= d.C) break;
+    const float g = (arg == c) ? d.scale : 0.f;
+    if (lane == 0) {
+      d.q[c * d.sqb + r] = q[c];
+      if (d.g_out) d.g_out[c * d.sgb + r] = g;
+    }
+    if (on) {
+      float4 z;
+      z.x = hv[c].x > 0.f ? g * wv[c].x : 0.f;
+      z.y = hv[c].y > 0.f ? g * wv[c].y : 0.f;
+      z.z = hv[c].z > 0.f ? g * wv[c].z : 0.f;
+      z.w = hv[c].w > 0.f ? g * wv[c].w : 0.f;
+      *reinterpret_cast<float4*>(d.dz + c * d.sdzb + r * d.lddz + k) = z;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace d3a
 
@@ -111,5 +166,21 @@ extern "C" int d3a_head1_bwd(const d3a_head1_bwd_desc* d, void* stream) {
   dim3 grid((unsigned)((d->n + 63) / 64), (unsigned)d->splits, (unsigned)d->C);
   hipLaunchKernelGGL(head1_bwd_kernel, grid, dim3(1024), 0, (hipStream_t)stream, *d);
   D3A_LAUNCH_CHECK("d3a_head1_bwd");
+  return 0;
+}
+
+extern "C" int d3a_head1_min(const d3a_head1_min_desc* d, void* stream) {
+  D3A_CHECK_ARG(d && d->h && d->w && d->b && d->q && d->dz, "d3a_head1_min: null operand");
+  D3A_CHECK_ARG(d->C >= 1 && d->C <= 8 && d->rows >= 0, "d3a_head1_min: 1..8 members");
+  D3A_CHECK_ARG(d->n >= 4 && d->n <= 256 && d->n % 4 == 0, "d3a_head1_min: n must be 4..256, %4");
+  D3A_CHECK_ARG(d->ldh % 4 == 0 && d->lddz % 4 == 0 && d->shb % 4 == 0 && d->sdzb % 4 == 0 &&
+                    d->swb % 4 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(d->h) | reinterpret_cast<uintptr_t>(d->w) |
+                      reinterpret_cast<uintptr_t>(d->dz)) & 15) == 0,
+                "d3a_head1_min: 16-byte aligned rows");
+  if (d->rows == 0) return 0;
+  hipLaunchKernelGGL(head1_min_kernel, dim3((unsigned)((d->rows + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, *d);
+  D3A_LAUNCH_CHECK("d3a_head1_min");
   return 0;
 }

@@ -88,7 +88,8 @@ def fused_ok(net: EnsembleMLP, rows: Optional[int] = None, backward: bool = Fals
 def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: int, acts: Acts,
             r0: int = 0, r1: Optional[int] = None, sxb: Optional[int] = None,
             members: Optional[int] = None, keep_h: bool = True,
-            h_from: Optional[int] = None, aux: Optional[tuple] = None) -> None:
+            h_from: Optional[int] = None, aux: Optional[tuple] = None,
+            skip_head: bool = False) -> None:
     """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
     (through its first ``members`` members only, when given).  ``keep_h``:
     store the hidden activations in ``acts.h`` (needed by a backward pass),
@@ -162,6 +163,9 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     out_dim = sizes[-1]
     Hl = sizes[-2]
     dout = (aacts.out.data_ptr() - acts.out.data_ptr()) // 4 if pair else 0
+    if skip_head:  # the caller's kernel evaluates the head (head1_min)
+        assert not pair
+        return
     if out_dim <= 16:
         # narrow heads (Q values, policy mu|logstd): one wave per row beats a
         # 32-wide MFMA tile that is mostly padding
@@ -286,7 +290,7 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         agen.dW, agen.sWs = gW.data_ptr(), C * Hin
         agen.db, agen.sbs = gb.data_ptr(), C
         agen.rows, agen.n, agen.C, agen.splits = n, Hin, C, S
-    if agen is not None:
+    if agen is not None or head_ready:
         pass
     elif out_dim == 1:
         # fused: masked input gradient + head weight/bias gradients, h read once

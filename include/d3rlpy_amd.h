@@ -171,6 +171,28 @@ typedef struct d3a_head1_bwd_desc {
 } d3a_head1_bwd_desc;
 int d3a_head1_bwd(const d3a_head1_bwd_desc* desc, void* stream);
 
+/* The single-output Q head of an ensemble evaluated and differentiated
+ * through min over the members in one launch (the actor loss of
+ * SACImpl.compute_actor_loss, sac_impl.py:114-121: q = min_c Q_c(s, a)).
+ * One wave per row r:
+ *   q[c*sqb + r] = h[c][r] . w[c] + b[c]        (the order of d3a_rowdot_f32)
+ *   g_c = scale if c is the first argmin over c of q[.][r] else 0
+ *   dz[c][r][j] = g_c * w[c][j] * [h[c][r][j] > 0],  g_out[c*sgb + r] = g_c
+ * i.e. d3a_rowdot_f32 followed by d3a_head1_bwd in argmin mode; n <= 256,
+ * n % 4 == 0, C <= 8. */
+typedef struct d3a_head1_min_desc {
+  const float* h; int64_t shb, ldh;   /* [C][rows][ldh]                     */
+  const float* w; int64_t swb;        /* [C][n]                             */
+  const float* b; int64_t sbb;        /* [C]                                */
+  float* q; int64_t sqb;              /* [C] x rows (out)                   */
+  float scale;
+  float* g_out; int64_t sgb;          /* [C] x rows (out, may be NULL)      */
+  float* dz; int64_t sdzb, lddz;      /* [C][rows][lddz] (out)              */
+  int64_t rows, n;
+  int32_t C;
+} d3a_head1_min_desc;
+int d3a_head1_min(const d3a_head1_min_desc* desc, void* stream);
+
 /* Whole-MLP forward, one launch (replaces the per-layer nn.Linear + ReLU
  * chain of VectorEncoder / VectorEncoderWithAction, encoders.py:265-275,
  * 328-339, and the linear head: mean_q_function.py:255-256 `_fc`,

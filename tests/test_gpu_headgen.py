@@ -152,3 +152,50 @@ def test_first_layer_weight_gradient_epilogue(generated, n_in, ldx):
                           for t in range(P)])
     e = float((dW.double() - tile_w).abs().max()) / float(tile_w.abs().max())
     assert e <= 1e-6, e
+
+
+@pytest.mark.parametrize("C", [2, 5])
+def test_head1_min_matches_rowdot_and_argmin_backward(C):
+    """d3a_head1_min (the actor phase's Q head + min-over-critics backward in
+    one launch) is bit-identical to d3a_rowdot_f32 followed by d3a_head1_bwd
+    in argmin mode, ties included."""
+    g = torch.Generator(device="cuda").manual_seed(13)
+    rows, H = 300, 256
+    h = torch.relu(torch.randn(C, rows, H, device="cuda", generator=g))
+    w = torch.randn(C, H, device="cuda", generator=g) * 0.06
+    b = torch.randn(C, device="cuda", generator=g)
+    # ties: member 1 a copy of member 0 on some rows
+    h[1, :50] = h[0, :50]
+    w[1] = w[0]
+    b[1] = b[0]
+    q_ref = torch.zeros(C, rows, device="cuda")
+    ops.rowdot(h.data_ptr(), rows * H, H, w.data_ptr(), H, b.data_ptr(), 1, q_ref.data_ptr(),
+               rows, C, rows, H)
+    dz_ref = torch.zeros(C, rows, H, device="cuda")
+    gout_ref = torch.zeros(C, rows, device="cuda")
+    d = N.Head1BwdDesc()
+    d.q_min, d.sqb, d.scale = q_ref.data_ptr(), rows, -1.0 / 256
+    d.g_out, d.sgb = gout_ref.data_ptr(), rows
+    d.h, d.shb, d.ldh = h.data_ptr(), rows * H, H
+    d.w, d.swb = w.data_ptr(), H
+    d.dz, d.sdzb, d.lddz = dz_ref.data_ptr(), rows * H, H
+    d.rows, d.n, d.C, d.splits = rows, H, C, max(1, rows // 64)
+    ops.call_desc("d3a_head1_bwd", d)
+    q = torch.full((C, rows), float("nan"), device="cuda")
+    dz = torch.full((C, rows, H), float("nan"), device="cuda")
+    gout = torch.full((C, rows), float("nan"), device="cuda")
+    m = N.Head1MinDesc()
+    m.h, m.shb, m.ldh = h.data_ptr(), rows * H, H
+    m.w, m.swb = w.data_ptr(), H
+    m.b, m.sbb = b.data_ptr(), 1
+    m.q, m.sqb = q.data_ptr(), rows
+    m.scale = -1.0 / 256
+    m.g_out, m.sgb = gout.data_ptr(), rows
+    m.dz, m.sdzb, m.lddz = dz.data_ptr(), rows * H, H
+    m.rows, m.n, m.C = rows, H, C
+    ops.call_desc("d3a_head1_min", m)
+    torch.cuda.synchronize()
+    assert torch.equal(q, q_ref)
+    assert torch.equal(gout, gout_ref)
+    assert torch.equal(dz, dz_ref)
+    assert torch.equal(torch.signbit(dz), torch.signbit(dz_ref))
