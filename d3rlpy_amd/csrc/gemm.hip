@@ -708,7 +708,7 @@ void launch_modes(const Params& p, int variant, hipStream_t st) {
 // Tile choice, from per-call sweeps of every GEMM of a K2 CQL and a K1 TD3+BC
 // update (tools/gemm_pipeline_sweep.py, graph-captured timings,
 // profiles/r01_pipe_sweep_*.log):
-//  - few output tiles (< 128 64x64 workgroups, or a 32-wide output) with at
+//  - few output tiles (<= 256 64x64 workgroups, or a 32-wide output) with at
 //    least 32 k per split: the register-direct split-K kernel (9), 1.7-2.6x
 //    faster than any LDS tile on the 256-row policy / target / actor layers
 //    and the narrow first-layer input gradients;
@@ -725,7 +725,7 @@ int choose_variant(const Params& p) {
   const int64_t blocks128 =
       ((p.M + 127) / 128) * ((p.N + 127) / 128) * p.batch * p.batch2 * p.splits;
   const int64_t kslice = (p.K + p.splits - 1) / p.splits;
-  if (kslice >= 32 && (blocks64 < 128 || p.M <= 32 || p.N <= 32)) return 9;
+  if (kslice >= 32 && (blocks64 <= 256 || p.M <= 32 || p.N <= 32)) return 9;
   if (p.M >= 128 && p.N >= 128 && blocks128 >= 64 && kslice >= 192) return 14;
   if (blocks64 >= 128) return 0;
   return 6;
