@@ -35,17 +35,16 @@ constexpr int LDK = 260;
 
 // One 32-column output tile over all RT row tiles:
 //   acc[i] += A[i*32.., 0:Kin] (LDS, row stride LDK) x B[0:Kin][this column]
-// Kin is a multiple of 32 (the LDS operand is zero-padded up to it);
+// Kin is a multiple of 8U (the LDS operand is zero-padded up to it);
 // load(k) returns the lane's B operand B[k..k+3][column].  The B operand is
 // double-buffered in registers: the loads of the next 32-deep k slice are
 // issued before the MFMAs of the current one.  Loaders must be
 // unconditional (clamped addresses, no guarded loads) so the compiler can
 // keep them in flight across the MFMAs -- a guarded load makes it drain the
 // whole queue first.
-template <int RT, class LoadB>
+template <int RT, int U, class LoadB>
 __device__ __forceinline__ void tile_mfma(f32x16* acc, const float* A, int Kin, int li, int lg,
                                           LoadB load) {
-  constexpr int U = 4;
   // multiply one 32-deep slice at k0 with its weights b; every activation
   // operand of the slice is read before its MFMAs
   auto slice = [&](int k0, const float4* b) {
@@ -117,7 +116,9 @@ void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
   float* const outp = aux ? d.aux_out + c * d.aux_sout : d.out + c * d.sout;
   const int H = d.H;
   const int K0 = d.n_in;
-  const int K0p = (K0 + 31) / 32 * 32;  // zero-padded to whole 32-deep k slices
+  // zero-padded to whole k slices: 16-deep (U = 2) for the narrow first layer
+  // (K2: 14 inputs -> 16 instead of 32), 32-deep for the hidden layers
+  const int K0p = (K0 + 15) / 16 * 16;
   float* bufA = lds;
   float* bufB = INPLACE ? lds : lds + BM * LDK;
 
@@ -174,7 +175,7 @@ void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
       if (l == 0) {
         // k beyond the real inputs clamps to the last one; its product with
         // the zero padding of the LDS operand is an exact zero
-        tile_mfma<RTW>(acc, Ag, Kin, li, lg, [&](int k) {
+        tile_mfma<RTW, 2>(acc, Ag, Kin, li, lg, [&](int k) {
           float4 r;
           r.x = W[wo + min(k + 0, Kreal - 1)];
           r.y = W[wo + min(k + 1, Kreal - 1)];
@@ -183,7 +184,7 @@ void mlp_fwd_kernel(d3a_mlp_fwd_desc d) {
           return r;
         });
       } else {
-        tile_mfma<RTW>(acc, Ag, Kin, li, lg,
+        tile_mfma<RTW, 4>(acc, Ag, Kin, li, lg,
                        [&](int k) { return *reinterpret_cast<const float4*>(W + (wo + k)); });
       }
     };
@@ -436,7 +437,7 @@ __global__ __launch_bounds__(64 * NW) void mlp_bwd_kernel(d3a_mlp_bwd_desc d) {
       // B(n, k) = W[n][k]: four rows, one column per lane (coalesced over
       // lanes); columns >= Kout read a clamped column and are dropped
       const int kc = min(k, Kout - 1);
-      tile_mfma<RT>(acc, bufA, H, li, lg, [&](int n) {
+      tile_mfma<RT, 4>(acc, bufA, H, li, lg, [&](int n) {
         float4 r;
         r.x = W[kc + (n + 0) * ldw];
         r.y = W[kc + (n + 1) * ldw];
