@@ -141,23 +141,29 @@ __global__ __launch_bounds__(256) void outer_mask_kernel(const float* g, int64_t
 // bit-identical).  A segment with many partials (>= 64, e.g. one per batch
 // row) gives each element a group of L = 16 lanes: lane j sums partials
 // q = j, j + L, ... in order, then the group is summed by a fixed butterfly.
-// Loads are issued 8 at a time so a lane has 8 independent requests in flight.
+// A lane issues up to 32 loads before it adds (clamped addresses, so short
+// segments take one memory round trip too); the addition order is q ascending.
 __host__ __device__ __forceinline__ int seg_lanes(int64_t n_partials) {
   return n_partials >= 64 ? 16 : 1;
 }
 
 __device__ __forceinline__ double sum_partials(const float* g, int64_t n, int64_t stride,
                                                int64_t i, int j, int L) {
+  constexpr int U = 32;
   double gd = 0.0;
-  int64_t q = j;
-  for (; q + 7 * L < n; q += 8 * L) {
-    float v[8];
+  for (int64_t q = j; q < n; q += (int64_t)U * L) {
+    float v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = g[(q + u * L) * stride + i];
+    for (int u = 0; u < U; ++u) {
+      // a clamped (always valid) address: the loads stay unconditional, so
+      // none of them is fenced behind a branch and all are in flight at once
+      const int64_t qq = q + (int64_t)u * L;
+      v[u] = g[(qq < n ? qq : n - 1) * stride + i];
+    }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) gd += (double)v[u];
+    for (int u = 0; u < U; ++u)
+      if (q + (int64_t)u * L < n) gd += (double)v[u];
   }
-  for (; q < n; q += L) gd += (double)g[q * stride + i];
   for (int o = L >> 1; o > 0; o >>= 1) gd += __shfl_xor(gd, o, 64);
   return gd;
 }
@@ -165,18 +171,33 @@ __device__ __forceinline__ double sum_partials(const float* g, int64_t n, int64_
 // ---- Adam (torch.optim.adam._single_tensor_adam, weight_decay = 0) ---------
 // The grid is flat over the segments: segment s owns ceil(numel_s * L_s / 256)
 // consecutive blocks, in table order (no idle blocks for small segments).
+// Wave 0 finds the block's segment: lane s reads segment s's block count and a
+// wave prefix sum gives every segment's first block (one memory round trip for
+// up to 64 segments, instead of one per segment walked).
 __device__ __forceinline__ void locate_block(const d3a_adam_segment* segs, int n_seg, int* s_seg,
                                              int64_t* s_first) {
-  if (threadIdx.x == 0) {
-    int64_t first = 0;
-    int s = 0;
-    for (; s < n_seg - 1; ++s) {
-      const int64_t nb = (segs[s].numel * seg_lanes(segs[s].n_partials) + 255) / 256;
-      if ((int64_t)blockIdx.x < first + nb) break;
-      first += nb;
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  const long long b = blockIdx.x;
+  long long base = 0;
+  for (int c = 0; c < n_seg; c += 64) {
+    const int s = c + lane;
+    long long nb = 0;
+    if (s < n_seg) nb = (segs[s].numel * seg_lanes(segs[s].n_partials) + 255) / 256;
+    long long incl = nb;
+    for (int o = 1; o < 64; o <<= 1) {
+      const long long t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
     }
-    *s_seg = s;
-    *s_first = first;
+    const long long first = base + incl - nb;
+    // the last segment also owns any block past the end (as the serial walk did)
+    const bool own = s < n_seg && b >= first && (b < base + incl || s == n_seg - 1);
+    if (own) {
+      *s_seg = s;
+      *s_first = first;
+    }
+    if (__ballot(own)) break;
+    base += __shfl(incl, 63, 64);
   }
 }
 
@@ -186,9 +207,9 @@ __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
   __shared__ float s_step_size, s_bc2_sqrt;
   __shared__ int s_seg;
   __shared__ int64_t s_first;
-  locate_block(segs, n_seg, &s_seg, &s_first);
   const int64_t t = *step + 1;  // read by every block before the last one commits
-  if (threadIdx.x == 0) {
+  locate_block(segs, n_seg, &s_seg, &s_first);
+  if (threadIdx.x == 64) {  // wave 1, concurrently with wave 0's segment search
     // bias corrections in fp64 exactly as torch computes them in Python floats
     const double bc1 = 1.0 - pow(beta1, (double)t);
     const double bc2 = 1.0 - pow(beta2, (double)t);
@@ -201,8 +222,16 @@ __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
   const int64_t lt = ((int64_t)blockIdx.x - s_first) * 256 + threadIdx.x;
   const int64_t i = lt / L;
   if (i < sg.numel) {  // uniform over each lane group
+    // the state loads go out with the partial loads (one round trip for both)
+    const bool lead = (lt % L) == 0;
+    float m = 0.f, v = 0.f, p = 0.f;
+    if (lead) {
+      m = sg.exp_avg[i];
+      v = sg.exp_avg_sq[i];
+      p = sg.param[i];
+    }
     const double gd = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i, (int)(lt % L), L);
-    if (lt % L) return;
+    if (!lead) return;
     // grad_scale: 1, or 1/world after a data-parallel SUM all-reduce (exact
     // for power-of-two worlds)
     const float g = grad_scale == 1.f ? (float)gd : __fmul_rn((float)gd, grad_scale);
@@ -210,16 +239,15 @@ __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
     // exp_avg.lerp_(grad, 1 - beta1): weight < 0.5 -> self + w * (end - self)
     // (ATen's vectorised CPU lerp: fmadd(weight, end - self, self))
     const float w = (float)(1.0 - beta1);
-    float m = sg.exp_avg[i];
     m = fmaf(w, __fsub_rn(g, m), m);
     // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
-    float v = __fmul_rn(sg.exp_avg_sq[i], (float)beta2);
+    v = __fmul_rn(v, (float)beta2);
     const float omb2 = (float)(1.0 - beta2);
     v = __fadd_rn(v, __fmul_rn(__fmul_rn(omb2, g), g));
     const float step_size = s_step_size;
     const float bc2_sqrt = s_bc2_sqrt;
     const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), (float)eps);
-    const float pnew = __fadd_rn(sg.param[i], __fmul_rn(-step_size, __fdiv_rn(m, denom)));
+    const float pnew = __fadd_rn(p, __fmul_rn(-step_size, __fdiv_rn(m, denom)));
     sg.exp_avg[i] = m;
     sg.exp_avg_sq[i] = v;
     sg.param[i] = pnew;
@@ -300,17 +328,19 @@ __global__ __launch_bounds__(256) void step_end_kernel(const float* m, int n, fl
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (targ && i < ns) targ[i] = __fadd_rn(__fmul_rn(targ[i], omt), __fmul_rn(tau, src[i]));
   if (blockIdx.x != 0) return;
+  // counters: one lane each, in parallel with the ring push
+  if (threadIdx.x < 32 && (inc_mask >> threadIdx.x & 1u)) counters[threadIdx.x] += 1;
+  int64_t c0 = 0;
   if (ring) {
-    const int64_t slot = *ctr % cap;
-    for (int k = threadIdx.x; k < n; k += blockDim.x)
+    const float mk = threadIdx.x < n ? m[threadIdx.x] : 0.f;  // issued with the ctr load
+    c0 = *ctr;
+    const int64_t slot = c0 % cap;
+    if (threadIdx.x < n) ring[slot * n + threadIdx.x] = mscale == 1.f ? mk : mk * mscale;
+    for (int k = threadIdx.x + blockDim.x; k < n; k += blockDim.x)
       ring[slot * n + k] = mscale == 1.f ? m[k] : m[k] * mscale;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (ring) *ctr = *ctr + 1;
-    for (int k = 0; k < 32; ++k)
-      if (inc_mask & (1u << k)) counters[k] += 1;
-  }
+  __syncthreads();  // every thread has read *ctr before it moves
+  if (ring && threadIdx.x == 0) *ctr = c0 + 1;
 }
 
 }  // namespace
