@@ -167,8 +167,8 @@ def test_soft_update_bit_exact(dev):
 
 def test_adam_matches_torch(dev):
     """torch.optim.Adam single-tensor step (the oracle's CPU Adam), 3 steps;
-    11 split-K partials (one unrolled batch of 8 + a remainder) over a
-    multi-block segment followed by a one-block segment (flat grid)."""
+    11 split-K partials (one batch of 32 clamped loads) over a multi-block
+    segment followed by a one-block segment (flat grid)."""
     from d3rlpy_amd.nets import AdamGroup, GradSpace, ParamStore
     store = ParamStore()
     store.add("w", (300, 7))
@@ -242,6 +242,53 @@ def test_adam_many_partials_matches_torch(dev):
     torch.testing.assert_close(store.view("w").cpu(), pw.detach(), rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(store.view("b").cpu(), pb.detach(), rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(opt.grad("w").cpu(), pw.grad, rtol=1e-6, atol=1e-6)
+
+
+def test_adam_many_segments_matches_torch(dev):
+    """150 segments (the block -> segment search runs over three 64-lane
+    chunks of the table) of 1 .. 700 elements with 1, 11, 40 (two load
+    batches) or 70 (16-lane groups) split-K partials: 2 Adam steps vs
+    torch.optim.Adam on the fp64 sums of the partials."""
+    from d3rlpy_amd import ops
+    from d3rlpy_amd.nets import AdamGroup, GradSpace, OptimState, ParamStore
+    g = torch.Generator().manual_seed(21)
+    n_seg = 150
+    sizes = [int(x) for x in torch.randint(1, 700, (n_seg,), generator=g)]
+    sizes[3], sizes[77] = 1, 257  # a one-element segment, a block edge
+    parts_of = [(1, 11, 40, 70)[k % 4] for k in range(n_seg)]
+    store = ParamStore()
+    for k, n in enumerate(sizes):
+        store.add(f"p{k}", (n,))
+    store.allocate(dev)
+    gs = GradSpace(dev)
+    views, tparams = [], []
+    for k, n in enumerate(sizes):
+        x0 = torch.randn(n, generator=g)
+        store.view(f"p{k}").copy_(x0)
+        views.append(gs.add(f"p{k}", (n,), parts_of[k]))
+        tparams.append(torch.nn.Parameter(x0.clone()))
+    names = [f"p{k}" for k in range(n_seg)]
+    opt = AdamGroup(OptimState(store, names, lr=1e-3), gs)
+    topt = torch.optim.Adam(tparams, lr=1e-3)
+    for it in range(2):
+        for k, n in enumerate(sizes):
+            parts = torch.randn(parts_of[k], n, generator=g)
+            views[k].copy_(parts.view(views[k].shape))
+            tparams[k].grad = parts.double().sum(0).float()
+        opt.launch()
+        ops.step_end(opt.step, 1)
+        topt.step()
+    torch.cuda.synchronize()
+    for k in range(n_seg):
+        torch.testing.assert_close(store.view(f"p{k}").cpu(), tparams[k].detach(),
+                                   rtol=1e-6, atol=1e-7, msg=f"segment {k}")
+    # the data-parallel path's partial reduction walks the same segment table
+    opt.grad_store.data.zero_()
+    opt.reduce()
+    torch.cuda.synchronize()
+    for k in (0, 3, 64, 77, 128, 149):
+        torch.testing.assert_close(opt.grad(f"p{k}").cpu(), tparams[k].grad, rtol=2e-7, atol=1e-9,
+                                   msg=f"reduced segment {k}")
 
 
 def test_philox_statistics(dev):
