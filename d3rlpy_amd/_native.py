@@ -133,6 +133,8 @@ class SacActorHeadDesc(C.Structure):
         ("min_logstd", C.c_float), ("max_logstd", C.c_float),
         ("w_head", vp), ("h", vp), ("ldh", C.c_int64), ("dz", vp), ("lddz", C.c_int64),
         ("H", C.c_int32), ("dW_part", vp), ("db_part", vp),
+        ("dq_dz", vp), ("lddqz", C.c_int64), ("sdz_c", C.c_int64),
+        ("w0", vp), ("ldw0", C.c_int64), ("sw0_c", C.c_int64), ("H0", C.c_int32),
     ]
 
 

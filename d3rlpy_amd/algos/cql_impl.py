@@ -48,6 +48,10 @@ METRIC_NAMES = ("temp_loss", "temp", "alpha_loss", "alpha", "critic_loss", "acto
 
 # actor phase: Q head + min-over-critics backward in one launch (d3a_head1_min)
 _HEAD_MIN = os.environ.get("D3A_HEAD_MIN", "1") == "1"
+# actor phase: dQ/da formed in d3a_sac_actor_head from the critic's first-layer
+# pre-activation gradient (one input-gradient launch fewer)
+_DQ_IN_HEAD = os.environ.get("D3A_DQ_IN_HEAD", "1") == "1"
+_DQ_IN_HEAD_MAX_PAIRS = min(32, int(os.environ.get("D3A_DQ_IN_HEAD_MAX_PAIRS", "8")))
 
 class CQLImpl(ImplBase):
     # conservative term + alpha (cql_impl.py); SACImpl (algos/sac.py) clears it
@@ -725,18 +729,33 @@ class _Workspace:
             hm = self._head_min_desc()
             mlp.forward(impl.critic, impl.store, self.x_actor.data_ptr(), True, DA, self.aacts,
                         skip_head=hm is not None)
+            hd = self.head_desc
+            hd.dq_dz = None
             if hm is not None:
                 # the Q head and its min-over-members backward in one launch
                 ops.call_desc("d3a_head1_min", hm)
-                mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA,
-                             self.aacts, self.adq.data_ptr(), 1, B, 0, B, weight_grads=False,
-                             dx=self.adx, head_ready=True)
+                net = impl.critic
+                # measured: faster than the input-gradient launch for C * A <= 8
+                # (K2: 6 pairs), slower for K4's 16 pairs
+                fuse = (_DQ_IN_HEAD and net.n_layers >= 2 and net.C <= 4
+                        and net.C * A <= _DQ_IN_HEAD_MAX_PAIRS and net.sizes[1] <= 256)
+                dz0 = mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA,
+                                   self.aacts, self.adq.data_ptr(), 1, B, 0, B,
+                                   weight_grads=False, dx=None if fuse else self.adx,
+                                   head_ready=True)
+                if fuse:
+                    # dQ/da from the first layer's pre-activation gradient, in
+                    # the actor head (the last input-gradient launch is skipped)
+                    hd.dq_dz, hd.lddqz = dz0.data_ptr(), dz0.shape[2]
+                    hd.sdz_c = dz0.shape[1] * dz0.shape[2]
+                    hd.w0, hd.ldw0 = net.W(0, impl.store), net.sizes[0]
+                    hd.sw0_c, hd.H0 = net.sizes[1] * net.sizes[0], net.sizes[1]
             else:
                 mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA,
                              self.aacts, self.adq.data_ptr(), 1, B, 0, B, weight_grads=False,
                              dx=self.adx, q_min=self.aacts.out.data_ptr(), sq_b=B,
                              q_scale=-1.0 / B, g_out=self.adq.data_ptr())
-            ops.call_desc("d3a_sac_actor_head", self.head_desc)
+            ops.call_desc("d3a_sac_actor_head", hd)
             mlp.backward(self.pbwd, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
                          self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B,
                          head_ready=self.head_dz)

@@ -375,6 +375,8 @@ __global__ __launch_bounds__(256) void sac_actor_dq_kernel(const float* q, int64
 __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_desc d) {
   __shared__ float scratch[4];
   __shared__ float s_dh[32];
+  __shared__ float s_dq[4][64];  // per-wave dQ_c/da_j sums [wave][c * 16 + j]
+  __shared__ float s_w0[32 * 256];  // the first layer's action columns [c * A + j][k]
   const int tid = threadIdx.x;
   const int A = d.A, B = d.B, C = d.C;
   const int64_t b = blockIdx.x;
@@ -399,10 +401,45 @@ __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_
     hv = d.h[b * d.ldh + tid];
     for (int k = 0; k < 2 * A; ++k) wk[k] = d.w_head[(int64_t)k * d.H + tid];
   }
+  if (d.dq_dz) {
+    // dQ_c/da_j = sum_k dz0[c][b][k] w0[c][k][da_off + j].  The P = C*A weight
+    // columns go to LDS (every workgroup reads the same few KB from L2), then
+    // thread k's product of each pair (c, j) is summed per wave by a fixed
+    // butterfly and the four wave sums are added in order.
+    const int P = C * A, H0 = d.H0;
+    const int n_w = P * H0;
+#pragma unroll 8
+    for (int e = tid; e < n_w; e += 256) {
+      const int c = e / (H0 * A), r = e - c * (H0 * A), k = r / A, j = r - k * A;
+      s_w0[(c * A + j) * 256 + k] = d.w0[c * d.sw0_c + (int64_t)k * d.ldw0 + d.da_off + j];
+    }
+    const int k = tid < H0 ? tid : H0 - 1;
+    const float live = tid < H0 ? 1.f : 0.f;
+    float zv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) zv[c] = d.dq_dz[(c < C ? c : C - 1) * d.sdz_c + b * d.lddqz + k];
+    __syncthreads();
+    const int w = tid >> 6, lane = tid & 63;
+    for (int p = 0; p < P; ++p) {
+      const int c = p / A, j = p - c * A;
+      const float z = c == 0 ? zv[0] : c == 1 ? zv[1] : c == 2 ? zv[2] : zv[3];
+      float v = live * __fmul_rn(z, s_w0[p * 256 + k]);
+      for (int o = 32; o > 0; o >>= 1) v = __fadd_rn(v, __shfl_xor(v, o, 64));
+      if (lane == 0) s_dq[w][c * 16 + j] = v;
+    }
+    __syncthreads();
+  }
   if (tid < A) {
     const int j = tid;
     float da = 0.f;
-    for (int c = 0; c < C; ++c) da += d.dq_da[c * d.sda_c + b * d.ld_da + d.da_off + j];
+    if (d.dq_dz) {
+      for (int c = 0; c < C; ++c) {
+        const float* sc = &s_dq[0][c * 16 + j];
+        da += ((sc[0] + sc[64]) + sc[128]) + sc[192];
+      }
+    } else {
+      for (int c = 0; c < C; ++c) da += d.dq_da[c * d.sda_c + b * d.ld_da + d.da_off + j];
+    }
     const float mu = hrow[j], lsr = hrow[A + j];
     const float l = fminf(fmaxf(lsr, d.min_logstd), d.max_logstd);
     const float sd = expf(l);
@@ -497,6 +534,11 @@ extern "C" int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream
                 "d3a_sac_actor_head: bad args");
   D3A_CHECK_ARG(!d->dz || (d->h && d->w_head && d->H >= 1 && d->H <= 256),
                 "d3a_sac_actor_head: dz needs h, w_head and 1 <= H <= 256");
+  D3A_CHECK_ARG(d->dq_dz ? (d->w0 && d->C <= 4 && d->C * d->A <= 32 && d->H0 >= 1 &&
+                            d->H0 <= 256)
+                         : d->dq_da != nullptr,
+                "d3a_sac_actor_head: dq_dz needs w0, C <= 4, C * A <= 32, 1 <= H0 <= 256 "
+                "(else dq_da)");
   hipLaunchKernelGGL(sac_actor_head_kernel, dim3((unsigned)d->B + 1), dim3(256), 0,
                      (hipStream_t)stream, *d);
   D3A_LAUNCH_CHECK("d3a_sac_actor_head");

@@ -225,8 +225,10 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
              sxb: Optional[int] = None, q_min: Optional[int] = None, sq_b: int = 0,
              q_scale: float = 0.0, g_out: Optional[int] = None,
              g_scale: Optional[int] = None, n_scaled: int = 0,
-             members: Optional[int] = None, head_ready: bool = False) -> None:
+             members: Optional[int] = None, head_ready: bool = False) -> Optional[torch.Tensor]:
     """Backward of rows [r0, r0+n) given dL/d(output) (``dout`` points at row r0).
+    Returns (per-layer path) the dz buffer holding the first layer's
+    pre-activation gradient [C][rows][ld] once the trunk has run.
 
     dout layout: [C] x rows, member stride sdout_b, row stride ld_dout (1 for a
     single-output head).  ``dx`` (if given) receives dL/dx as [C][n][in].
@@ -355,6 +357,7 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         elif dx is not None:
             ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(0, store), dx.data_ptr(), Hin,
                              n * Hin, C, n, Hin, Hout, agen=ag)
+    return cur
 
 
 

@@ -465,6 +465,16 @@ typedef struct d3a_sac_actor_head_desc {
    * dhead[b][k] (summed over b, in row order, by d3a_adam_f32) */
   float* dW_part;
   float* db_part;
+  /* optional (dq_dz != NULL, C <= 4, C * A <= 32): dQ_c/da formed here from the critic's
+   * first-layer pre-activation gradient instead of read from dq_da (the
+   * critic backward's last input-gradient launch is skipped):
+   * dQ_c/da_j = sum_k dq_dz[c*sdz_c + b*lddqz + k] * w0[c*sw0_c + k*ldw0 + da_off + j],
+   * k < H0 <= 256 (w0: the critic's first layer, nn.Linear [H0][in] per member) */
+  const float* dq_dz;
+  int64_t lddqz, sdz_c;
+  const float* w0;
+  int64_t ldw0, sw0_c;
+  int32_t H0;
 } d3a_sac_actor_head_desc;
 int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream);
 
