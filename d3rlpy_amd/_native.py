@@ -382,6 +382,7 @@ _SIGNATURES = {
     "d3a_last_error": (C.c_char_p, []),
     "d3a_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "d3a_gemm_f32": (C.c_int, [C.POINTER(GemmDesc), vp]),
+    "d3a_gemm_f32_pair": (C.c_int, [C.POINTER(GemmDesc), C.POINTER(GemmDesc), vp]),
     "d3a_rowdot_f32": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,
                                  C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
     "d3a_rowdot2_f32": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp,

@@ -510,17 +510,17 @@ __device__ __forceinline__ float4 rd_load(const float* base, int64_t sx, int64_t
   return r;
 }
 
+// One register-direct tile: output tile (bx, by) of batch / split bz, computed
+// by the KW waves w = 0 .. KW-1 (t = 64 w + lane) of the caller; red / rsum are
+// the caller's LDS (KW * WN * 16 * 64 floats, KW * 32 doubles).  Every thread
+// of the workgroup passes the body's one __syncthreads.
 template <int AMODE, int BMODE, int KW, int WN, int U>
-__global__ __launch_bounds__(64 * KW) void gemm_rd_kernel(Params p) {
-  // every wave's partial tile: red[w][j*16 + r][lane]
-  __shared__ float red[(KW > 1 ? KW : 1) * WN * 16 * 64];
-  __shared__ double rsum[KW * 32];
-  const int t = threadIdx.x;
+__device__ __forceinline__ void gemm_rd_tile(const Params& p, int64_t bx, int64_t by, int64_t bz,
+                                             int t, float* red, double* rsum) {
   const int lane = t & 63, w = t >> 6;
   const int li = lane & 31, lg = lane >> 5;
-  const int64_t n0 = (int64_t)blockIdx.x * (32 * WN);
-  const int64_t m0 = (int64_t)blockIdx.y * 32;
-  const int64_t bz = blockIdx.z;
+  const int64_t n0 = bx * (32 * WN);
+  const int64_t m0 = by * 32;
   const int64_t bb = bz / p.splits, s = bz % p.splits;
   const int64_t b = bb % p.batch, t2 = bb / p.batch;
   const int64_t sbeg = s * p.kchunk;
@@ -533,7 +533,7 @@ __global__ __launch_bounds__(64 * KW) void gemm_rd_kernel(Params p) {
   const float* Ab = p.A + b * p.sAb + t2 * p.sAb2;
   const float* Bb = p.B + b * p.sBb + t2 * p.sBb2;
   const int64_t m = m0 + li;
-  const bool do_rowsum = p.rowsum != nullptr && blockIdx.x == 0;
+  const bool do_rowsum = p.rowsum != nullptr && bx == 0;
 
   f32x16 acc[WN];
 #pragma unroll
@@ -612,6 +612,42 @@ __global__ __launch_bounds__(64 * KW) void gemm_rd_kernel(Params p) {
     for (int j = 0; j < WN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) emit(j, r, acc[j][r]);
+  }
+}
+
+template <int AMODE, int BMODE, int KW, int WN, int U>
+__global__ __launch_bounds__(64 * KW) void gemm_rd_kernel(Params p) {
+  // every wave's partial tile: red[w][j*16 + r][lane]
+  __shared__ float red[(KW > 1 ? KW : 1) * WN * 16 * 64];
+  __shared__ double rsum[KW * 32];
+  gemm_rd_tile<AMODE, BMODE, KW, WN, U>(p, blockIdx.x, blockIdx.y, blockIdx.z, threadIdx.x, red,
+                                        rsum);
+}
+
+// Two independent register-direct problems in one launch of 512-thread
+// workgroups (the weight- and input-gradient GEMMs of one backward layer):
+// workgroups [0, nb1) run problem 1 as one-wave tiles, eight per workgroup
+// (wave w takes tile 8 * blockIdx.x + w), the rest run problem 2 as eight-wave
+// K-split tiles.  Each tile computes exactly what its own launch computes.
+template <int AM1, int BM1, int AM2, int BM2>
+__global__ __launch_bounds__(512) void gemm_rd_pair_kernel(Params p1, Params p2, int64_t nb1,
+                                                           int64_t n1) {
+  __shared__ float red[8 * 16 * 64];
+  __shared__ double rsum[8 * 32];
+  const int t = threadIdx.x, w = t >> 6;
+  if ((int64_t)blockIdx.x < nb1) {
+    const int64_t v = (int64_t)blockIdx.x * 8 + w;
+    if (v >= n1) {
+      __syncthreads();  // the tile body's barrier
+      return;
+    }
+    const int64_t gx = (p1.N + 31) / 32, gy = (p1.M + 31) / 32;
+    gemm_rd_tile<AM1, BM1, 1, 1, 4>(p1, v % gx, (v / gx) % gy, v / (gx * gy), t & 63, red,
+                                    rsum + w * 32);
+  } else {
+    const int64_t u = (int64_t)blockIdx.x - nb1;
+    const int64_t gx = (p2.N + 31) / 32, gy = (p2.M + 31) / 32;
+    gemm_rd_tile<AM2, BM2, 8, 1, 4>(p2, u % gx, (u / gx) % gy, u / (gx * gy), t, red, rsum);
   }
 }
 
@@ -875,8 +911,79 @@ void launch_params(const Params& p, int variant, int am, int bm, hipStream_t st)
   }
 }
 
+template <int AM1, int BM1, int AM2, int BM2>
+void launch_pair4(const Params& p1, const Params& p2, int64_t nb1, int64_t n1, int64_t n2,
+                  hipStream_t st) {
+  hipLaunchKernelGGL((gemm_rd_pair_kernel<AM1, BM1, AM2, BM2>), dim3((unsigned)(nb1 + n2)),
+                     dim3(512), 0, st, p1, p2, nb1, n1);
+}
+
+template <int AM1, int BM1>
+void launch_pair2(const Params& p1, const Params& p2, int am2, int bm2, int64_t nb1, int64_t n1,
+                  int64_t n2, hipStream_t st) {
+  if (am2 == MODE_KCONTIG) {
+    if (bm2 == MODE_KCONTIG) launch_pair4<AM1, BM1, MODE_KCONTIG, MODE_KCONTIG>(p1, p2, nb1, n1, n2, st);
+    else launch_pair4<AM1, BM1, MODE_KCONTIG, MODE_XCONTIG>(p1, p2, nb1, n1, n2, st);
+  } else {
+    if (bm2 == MODE_KCONTIG) launch_pair4<AM1, BM1, MODE_XCONTIG, MODE_KCONTIG>(p1, p2, nb1, n1, n2, st);
+    else launch_pair4<AM1, BM1, MODE_XCONTIG, MODE_XCONTIG>(p1, p2, nb1, n1, n2, st);
+  }
+}
+
+int64_t rd_tiles(const Params& p) {
+  return ((p.N + 31) / 32) * ((p.M + 31) / 32) * p.batch * p.batch2 * p.splits;
+}
+
+// p1 one-wave register-direct tiles, p2 eight-wave ones (as their own launches
+// would choose), both plain (no generated A / epilogue) with contiguous modes
+bool pairable(const Params& p1, int v1, int am1, int bm1, const Params& p2, int v2, int am2,
+              int bm2) {
+  auto plain = [](const Params& p, int v, int am, int bm) {
+    return v == 9 && !p.hg_h && !p.ew_x && am != MODE_GENERIC && bm != MODE_GENERIC;
+  };
+  return plain(p1, v1, am1, bm1) && plain(p2, v2, am2, bm2) && rd_waves(p1, 1) == 1 &&
+         rd_waves(p2, 1) == 8 && (rd_tiles(p1) + 7) / 8 + rd_tiles(p2) < (1ll << 31);
+}
+
 }  // namespace
 }  // namespace d3a
+
+extern "C" int d3a_gemm_f32_pair(const d3a_gemm_desc* d1, const d3a_gemm_desc* d2, void* stream) {
+  using namespace d3a;
+  Params p1, p2;
+  int v1, am1, bm1, v2, am2, bm2;
+  bool s1, s2;
+  if (make_params(d1, p1, v1, am1, bm1, s1) != 0) return -1;
+  if (make_params(d2, p2, v2, am2, bm2, s2) != 0) return -1;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const Params* q1 = &p1;
+  const Params* q2 = &p2;
+  int qa1 = am1, qb1 = bm1, qa2 = am2, qb2 = bm2;
+  bool pair = !s1 && !s2;
+  if (pair && !pairable(p1, v1, am1, bm1, p2, v2, am2, bm2)) {
+    pair = pairable(p2, v2, am2, bm2, p1, v1, am1, bm1);
+    if (pair) {
+      q1 = &p2; q2 = &p1;
+      qa1 = am2; qb1 = bm2; qa2 = am1; qb2 = bm1;
+    }
+  }
+  if (!pair) {  // two launches, exactly as d3a_gemm_f32 twice
+    if (!s1) launch_params(p1, v1, am1, bm1, st);
+    if (!s2) launch_params(p2, v2, am2, bm2, st);
+    D3A_LAUNCH_CHECK("d3a_gemm_f32_pair");
+    return 0;
+  }
+  const int64_t n1 = rd_tiles(*q1), n2 = rd_tiles(*q2), nb1 = (n1 + 7) / 8;
+  if (qa1 == MODE_KCONTIG) {
+    if (qb1 == MODE_KCONTIG) launch_pair2<MODE_KCONTIG, MODE_KCONTIG>(*q1, *q2, qa2, qb2, nb1, n1, n2, st);
+    else launch_pair2<MODE_KCONTIG, MODE_XCONTIG>(*q1, *q2, qa2, qb2, nb1, n1, n2, st);
+  } else {
+    if (qb1 == MODE_KCONTIG) launch_pair2<MODE_XCONTIG, MODE_KCONTIG>(*q1, *q2, qa2, qb2, nb1, n1, n2, st);
+    else launch_pair2<MODE_XCONTIG, MODE_XCONTIG>(*q1, *q2, qa2, qb2, nb1, n1, n2, st);
+  }
+  D3A_LAUNCH_CHECK("d3a_gemm_f32_pair");
+  return 0;
+}
 
 extern "C" int d3a_gemm_f32(const d3a_gemm_desc* d, void* stream) {
   using namespace d3a;

@@ -335,6 +335,20 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         ag = agen if l == L - 2 else None  # the head's dz, generated
         if l == 0 and ew:
             break  # written by the l == 1 launch
+        if weight_grads and l > 0 and not (l == 1 and ew):
+            # this layer's weight and input gradients are independent: one
+            # paired submission (a single launch on the register-direct kernel)
+            gW, gb = gs.get(net.wname(l)), gs.get(net.bname(l))
+            nxt = bs.dz[1] if cur is bs.dz[0] else bs.dz[0]
+            ops.gemm_pair(
+                lambda: ops.linear_bwd_w(dz.data_ptr(), ld_cur, scur, hin, ld_h, sh,
+                                         gW.data_ptr(), C, n, Hin, Hout, S, db=gb.data_ptr(),
+                                         agen=ag),
+                lambda: ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(l, store),
+                                         nxt.data_ptr(), ld_cur, scur, C, n, Hin, Hout,
+                                         mask=hin, ldm=ld_h, smb=sh, agen=ag))
+            cur = nxt
+            continue
         if weight_grads:
             gW, gb = gs.get(net.wname(l)), gs.get(net.bname(l))
             S_l = bs.l0_tiles if (l == 0 and bs.l0_tiles) else S

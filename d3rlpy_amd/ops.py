@@ -73,7 +73,39 @@ def gemm(A: int, B: int, Cp: int, M: int, Nn: int, K: int, *, batch: int = 1,
         print(f"gemm M={M} N={Nn} K={K} batch={batch} splits={splits} sA={tuple(sA)} "
               f"sB={tuple(sB)} sC={tuple(sC)} mask={mask is not None} relu={relu} "
               f"rowsum={rowsum is not None} variant={variant}", flush=True)
+    if _CAPTURE is not None:  # inside gemm_pair: submitted together
+        _CAPTURE.append((d, agen, wnext))
+        return
     N.check(N.lib().d3a_gemm_f32(C.byref(d), _stream()), "d3a_gemm_f32")
+
+
+_CAPTURE = None  # descriptors collected by gemm_pair
+PAIR = os.environ.get("D3A_GEMM_PAIR", "1") != "0"
+
+
+def gemm_pair(first, second) -> None:
+    """Enqueue two independent GEMM wrapper calls (``first()``, ``second()``,
+    e.g. one backward layer's weight- and input-gradient GEMMs): when each
+    enqueues one d3a_gemm_f32, both go to d3a_gemm_f32_pair (one launch where
+    both take the register-direct kernel, else two launches)."""
+    global _CAPTURE
+    if not PAIR:
+        first()
+        second()
+        return
+    _CAPTURE = []
+    try:
+        first()
+        second()
+        caps = _CAPTURE
+    finally:
+        _CAPTURE = None
+    if len(caps) == 2:
+        N.check(N.lib().d3a_gemm_f32_pair(C.byref(caps[0][0]), C.byref(caps[1][0]), _stream()),
+                "d3a_gemm_f32_pair")
+    else:
+        for d, _, _ in caps:
+            N.check(N.lib().d3a_gemm_f32(C.byref(d), _stream()), "d3a_gemm_f32")
 
 
 def rowdot(X: int, sXb: int, sXr: int, w: int, swb: int, bias: Optional[int], sbb: int,

@@ -107,6 +107,13 @@ typedef struct d3a_gemm_desc {
 } d3a_gemm_desc;
 int d3a_gemm_f32(const d3a_gemm_desc* desc, void* stream);
 
+/* Two independent GEMMs (no data dependence between them; the weight- and
+ * input-gradient GEMMs of one backward layer) enqueued as ONE launch when both
+ * resolve to the register-direct kernel, one with one-wave tiles and one with
+ * eight-wave K-split tiles (each tile then computes exactly what its own
+ * d3a_gemm_f32 launch computes); otherwise as two d3a_gemm_f32 launches. */
+int d3a_gemm_f32_pair(const d3a_gemm_desc* d1, const d3a_gemm_desc* d2, void* stream);
+
 /* The same GEMM (A k-contiguous; B k-contiguous, y = x W^T (+ bias, ReLU),
  * or n-contiguous, dx = (dy W) * mask) evaluated on the bf16 matrix cores with
  * each fp32 operand split into bf16 parts: terms = 3 (hi/lo, ~2^-16 relative

@@ -547,3 +547,43 @@ def test_mlp_input_gradient_member_subset(dev, C, R, K0, H, J, members):
                 h = h.clamp_min(0)
         h.backward(dout[c].double().cpu().view(R, J))
         assert _rel_err(dx[c], a.grad) < 5e-6, (c, _rel_err(dx[c], a.grad))
+
+
+@pytest.mark.parametrize("C_,R,n_in,n_out,S", [(1, 256, 256, 256, 8), (2, 256, 256, 256, 8),
+                                               (1, 100, 256, 256, 4), (2, 512, 64, 48, 8)])
+def test_gemm_pair_bit_identical(dev, C_, R, n_in, n_out, S):
+    """d3a_gemm_f32_pair (one backward layer's weight- and input-gradient GEMMs
+    submitted together: one launch on the register-direct kernel, or two
+    launches where the pair does not fit it) writes exactly what the two
+    separate d3a_gemm_f32 launches write."""
+    from d3rlpy_amd import ops
+    g = torch.Generator().manual_seed(C_ * 1000 + R + n_in)
+    dz = torch.randn(C_, R, n_out, generator=g).to(dev)
+    h = torch.randn(C_, R, n_in, generator=g).relu().to(dev)
+    W = torch.randn(C_, n_out, n_in, generator=g).to(dev)
+    outs = []
+    for paired in (False, True):
+        dW = torch.full((S, C_, n_out, n_in), 12345.0, device=dev)
+        db = torch.full((S, C_, n_out), 12345.0, device=dev)
+        dx = torch.full((C_, R, n_in), 12345.0, device=dev)
+
+        def w():
+            ops.linear_bwd_w(dz.data_ptr(), n_out, R * n_out, h.data_ptr(), n_in, R * n_in,
+                             dW.data_ptr(), C_, R, n_in, n_out, S, db=db.data_ptr())
+
+        def x():
+            ops.linear_bwd_x(dz.data_ptr(), n_out, R * n_out, W.data_ptr(), dx.data_ptr(), n_in,
+                             R * n_in, C_, R, n_in, n_out, mask=h.data_ptr(), ldm=n_in,
+                             smb=R * n_in)
+        if paired:
+            ops.gemm_pair(w, x)
+        else:
+            w()
+            x()
+        torch.cuda.synchronize()
+        outs.append((dW.cpu(), db.cpu(), dx.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    # and the pair is right: fp64 reference of dX
+    ref = ((dz.double() @ W.double()) * (h > 0)).cpu()
+    torch.testing.assert_close(outs[1][2].double(), ref, rtol=1e-5, atol=1e-4)
