@@ -90,6 +90,19 @@ class AdamSegment(C.Structure):
     ]
 
 
+class AdamDesc(C.Structure):
+    _fields_ = [
+        ("segs", vp), ("n_seg", C.c_int32), ("n_blocks", C.c_int64),
+        ("step", vp), ("step_add", C.c_int32),
+        ("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double),
+        ("grad_scale", C.c_double),
+        ("soft", C.c_int32), ("targ_delta", C.c_int64), ("tau", C.c_double),
+        ("counters", vp), ("inc_mask", C.c_uint32),
+        ("metrics", vp), ("n_metrics", C.c_int32),
+        ("ring", vp), ("ring_cap", C.c_int64), ("ring_ctr", vp), ("metric_scale", C.c_float),
+    ]
+
+
 class CqlSampleDesc(C.Structure):
     _fields_ = [
         ("head", vp), ("obs", vp), ("next_obs", vp), ("act", vp),
@@ -153,6 +166,7 @@ class GatherDesc(C.Structure):
         ("o_term", vp), ("o_n_steps", vp), ("row_offset", C.c_int64),
         ("t_term_value", vp),
         ("gamma_pow", C.c_float * 64),
+        ("ctr_value", C.c_int64),
     ]
 
     def set_gamma(self, gamma: float, n_steps: int) -> None:
@@ -248,6 +262,20 @@ class MlpBwdDesc(C.Structure):
         ("dz", vp * MLP_MAX_HIDDEN), ("sdz", C.c_int64),
         ("dx", vp), ("sdxb", C.c_int64), ("lddx", C.c_int64),
         ("rows", C.c_int64), ("block_rows", C.c_int32),
+    ]
+
+
+class Q2BwdDesc(C.Structure):
+    _fields_ = [
+        ("x", vp), ("ldx", C.c_int64), ("sxb", C.c_int64),
+        ("h1", vp), ("h2", vp), ("sh", C.c_int64), ("ldh", C.c_int64),
+        ("g", vp), ("sgb", C.c_int64),
+        ("gscale", vp), ("n_scaled", C.c_int64),
+        ("W2", vp), ("sW2", C.c_int64),
+        ("w3", vp), ("sw3", C.c_int64),
+        ("dW1", vp), ("db1", vp), ("dW2", vp), ("db2", vp), ("dW3", vp), ("db3", vp),
+        ("rows", C.c_int64),
+        ("n_in", C.c_int32), ("C", C.c_int32),
     ]
 
 
@@ -395,6 +423,22 @@ _SIGNATURES = {
                                      C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp]),
     "d3a_adam_f32": (C.c_int, [vp, C.c_int32, C.c_int64, vp, C.c_double, C.c_double,
                                C.c_double, C.c_double, C.c_double, vp]),
+    "d3a_adam_step": (C.c_int, [C.POINTER(AdamDesc), vp]),
+    "d3a_logsumexp_f32": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp]),
+    "d3a_logsumexp_bwd_f32": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp,
+                                        C.c_int64, vp]),
+    "d3a_td_mse_f32": (C.c_int, [vp, vp, vp, vp, vp, C.c_int64, C.c_int64, vp, vp, vp]),
+    "d3a_td_mse_bwd_f32": (C.c_int, [vp, vp, C.c_int64, C.c_int64, vp, vp]),
+    "d3a_quantile_huber_f32": (C.c_int, [vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, C.c_int64,
+                                         C.c_int64, C.c_int64, vp, vp]),
+    "d3a_quantile_huber_bwd_f32": (C.c_int, [vp, C.c_int64, vp, C.c_int64, vp, C.c_int64,
+                                             C.c_int64, C.c_int64, C.c_int64, vp, vp, C.c_int64,
+                                             vp]),
+    "d3a_squashed_gauss_f32": (C.c_int, [vp, vp, vp, C.c_int64, C.c_int32, C.c_float, C.c_float,
+                                         vp, vp, vp]),
+    "d3a_squashed_gauss_bwd_f32": (C.c_int, [vp, vp, vp, C.c_int64, C.c_int32, C.c_float,
+                                             C.c_float, vp, vp, vp, vp, vp]),
+    "d3a_relu_mask_f32": (C.c_int, [vp, vp, C.c_int64, vp, vp]),
     "d3a_grad_reduce_f32": (C.c_int, [vp, C.c_int32, C.c_int64, vp]),
     "d3a_soft_update_f32": (C.c_int, [vp, vp, C.c_int64, C.c_double, vp]),
     "d3a_standardize_f32": (C.c_int, [vp, vp, C.c_int64, C.c_int32, C.c_int64, vp, vp, C.c_float,
@@ -430,6 +474,7 @@ _SIGNATURES = {
     "d3a_bcq_qr_loss": (C.c_int, [C.POINTER(BcqQrDesc), vp]),
     "d3a_bcq_actor_head": (C.c_int, [C.POINTER(BcqActorDesc), vp]),
     "d3a_mlp_bwd": (C.c_int, [C.POINTER(MlpBwdDesc), vp]),
+    "d3a_q2_bwd": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
     "d3a_td3_prep": (C.c_int, [C.POINTER(Td3PrepDesc), vp]),
     "d3a_td3_target": (C.c_int, [C.POINTER(Td3TargetDesc), vp]),
     "d3a_td3_critic_loss": (C.c_int, [C.POINTER(Td3CriticLossDesc), vp]),

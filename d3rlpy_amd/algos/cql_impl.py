@@ -52,6 +52,9 @@ _HEAD_MIN = os.environ.get("D3A_HEAD_MIN", "1") == "1"
 # pre-activation gradient (one input-gradient launch fewer)
 _DQ_IN_HEAD = os.environ.get("D3A_DQ_IN_HEAD", "1") == "1"
 _DQ_IN_HEAD_MAX_PAIRS = min(32, int(os.environ.get("D3A_DQ_IN_HEAD_MAX_PAIRS", "8")))
+# full update_step: the soft target updates, counters and metric ring ride in
+# the two Adam launches (d3a_adam_step) instead of a d3a_step_end launch
+_ADAM_TAIL = os.environ.get("D3A_ADAM_TAIL", "1") == "1"
 
 class CQLImpl(ImplBase):
     # conservative term + alpha (cql_impl.py); SACImpl (algos/sac.py) clears it
@@ -709,6 +712,13 @@ class _Workspace:
                 l.dp_phase = 0
             else:
                 ops.call_desc("d3a_cql_loss", l)
+        rng = 16 if sampled and not self._external_noise else 0  # counters[4] += 1
+        # whole update: Adam launches carry the targets' soft update and the
+        # step bookkeeping (critic Adam: counters[1] += 1, so the actor Adam
+        # reads its step already advanced; actor Adam: counters[0] and the
+        # sampler counter, metric ring)
+        fused_tail = _ADAM_TAIL and critic and actor and targets
+        mscale = 1.0 if dp is None else dp.scale
         if critic:
             # 5. critic backward on rows [3NB, R) and Adam
             r0 = 3 * NB
@@ -717,7 +727,10 @@ class _Workspace:
             mlp.backward(self.cbwd, impl.store, self.x_q.data_ptr(), True, DA, self.qacts,
                          self.dq.data_ptr() + 4 * r0, 1, R, r0, self.Rc,
                          g_scale=self.scalars.data_ptr() + 8, n_scaled=3 * NB)
-            self._apply(self.critic_opt, dp)
+            tail = None
+            if fused_tail:
+                tail = dict(targ=impl.targ, tau=impl._tau, counters=impl.counters, inc_mask=2)
+            self._apply(self.critic_opt, dp, tail)
         if actor:
             if not (temp or alpha or critic):
                 # scalars[0] = exp(log_temp) is produced by the loss kernel
@@ -759,23 +772,31 @@ class _Workspace:
             mlp.backward(self.pbwd, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
                          self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B,
                          head_ready=self.head_dz)
-            self._apply(self.actor_opt, dp)
+            tail = None
+            if fused_tail:
+                if dp is not None:
+                    dp.all_reduce_sum(self.metrics)  # logged losses: mean over ranks
+                tail = dict(targ=impl.targ, tau=impl._tau, counters=impl.counters,
+                            inc_mask=1 | rng, step_add=0, metrics=self.metrics, ring=self.ring,
+                            ring_ctr=self.ring_ctr, metric_scale=mscale)
+            self._apply(self.actor_opt, dp, tail)
+        if fused_tail:
+            return
         # 7. soft update of both targets + metric ring + optimiser step counters
         if dp is not None:
             dp.all_reduce_sum(self.metrics)  # logged losses: mean over ranks
-        rng = 16 if sampled and not self._external_noise else 0  # counters[4] += 1
         ops.step_end(impl.counters, (1 if critic else 0) | (2 if actor else 0) | rng, self.metrics,
                      self.ring, self.ring_ctr, impl.targ.data if targets else None,
-                     impl.store.data if targets else None, impl._tau,
-                     metric_scale=1.0 if dp is None else dp.scale)
+                     impl.store.data if targets else None, impl._tau, metric_scale=mscale)
 
     @staticmethod
-    def _apply(opt: AdamGroup, dp) -> None:
+    def _apply(opt: AdamGroup, dp, tail: Optional[dict] = None) -> None:
         """Adam; with data parallelism: reduce the split-K partials, SUM
-        all-reduce the one gradient copy, Adam on it scaled by 1/world."""
+        all-reduce the one gradient copy, Adam on it scaled by 1/world.
+        ``tail``: the fused soft update / bookkeeping (AdamGroup.launch)."""
         if dp is None:
-            opt.launch()
+            opt.launch(tail=tail)
             return
         opt.reduce()
         dp.all_reduce_sum(opt.grad_span())
-        opt.launch(reduced=True, grad_scale=dp.scale)
+        opt.launch(reduced=True, grad_scale=dp.scale, tail=tail)

@@ -201,22 +201,40 @@ __device__ __forceinline__ void locate_block(const d3a_adam_segment* segs, int n
   }
 }
 
-__global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs, int n_seg,
-                                                   const int64_t* step, double lr, double beta1,
-                                                   double beta2, double eps, float grad_scale) {
+__global__ __launch_bounds__(256) void adam_kernel(d3a_adam_desc a) {
   __shared__ float s_step_size, s_bc2_sqrt;
   __shared__ int s_seg;
   __shared__ int64_t s_first;
-  const int64_t t = *step + 1;  // read by every block before the last one commits
+  const d3a_adam_segment* segs = a.segs;
+  const int n_seg = a.n_seg;
+  const double beta1 = a.beta1, beta2 = a.beta2;
+  const float grad_scale = (float)a.grad_scale;
+  // t: the optimiser's step for this update (*step completed steps + 1, or a
+  // counter another kernel of the update already advanced: step_add 0)
+  const int64_t t = *a.step + a.step_add;
+  // block 0 also does the update's bookkeeping (d3a_step_end's, for counters
+  // this launch does not read): the metric ring push and counter increments
+  const bool tail = blockIdx.x == 0;
+  int64_t rc0 = 0;
+  if (tail && a.ring && (int)threadIdx.x < a.n_metrics) {
+    const float mk = a.metrics[threadIdx.x];
+    rc0 = *a.ring_ctr;
+    a.ring[(rc0 % a.ring_cap) * a.n_metrics + threadIdx.x] =
+        a.metric_scale == 1.f ? mk : mk * a.metric_scale;
+  }
   locate_block(segs, n_seg, &s_seg, &s_first);
   if (threadIdx.x == 64) {  // wave 1, concurrently with wave 0's segment search
     // bias corrections in fp64 exactly as torch computes them in Python floats
     const double bc1 = 1.0 - pow(beta1, (double)t);
     const double bc2 = 1.0 - pow(beta2, (double)t);
-    s_step_size = (float)(lr / bc1);
+    s_step_size = (float)(a.lr / bc1);
     s_bc2_sqrt = (float)sqrt(bc2);
   }
-  __syncthreads();
+  __syncthreads();  // (block 0: every ring writer has read *ring_ctr)
+  if (tail) {
+    if (a.ring && threadIdx.x == 0) *a.ring_ctr = rc0 + 1;
+    if (threadIdx.x < 32 && (a.inc_mask >> threadIdx.x & 1u)) a.counters[threadIdx.x] += 1;
+  }
   const d3a_adam_segment sg = segs[s_seg];
   const int L = seg_lanes(sg.n_partials);
   const int64_t lt = ((int64_t)blockIdx.x - s_first) * 256 + threadIdx.x;
@@ -224,11 +242,13 @@ __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
   if (i < sg.numel) {  // uniform over each lane group
     // the state loads go out with the partial loads (one round trip for both)
     const bool lead = (lt % L) == 0;
-    float m = 0.f, v = 0.f, p = 0.f;
+    float m = 0.f, v = 0.f, p = 0.f, tv = 0.f;
+    float* tg = a.soft ? sg.param + a.targ_delta : nullptr;
     if (lead) {
       m = sg.exp_avg[i];
       v = sg.exp_avg_sq[i];
       p = sg.param[i];
+      if (tg) tv = tg[i];
     }
     const double gd = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i, (int)(lt % L), L);
     if (!lead) return;
@@ -246,13 +266,17 @@ __global__ __launch_bounds__(256) void adam_kernel(const d3a_adam_segment* segs,
     v = __fadd_rn(v, __fmul_rn(__fmul_rn(omb2, g), g));
     const float step_size = s_step_size;
     const float bc2_sqrt = s_bc2_sqrt;
-    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), (float)eps);
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), (float)a.eps);
     const float pnew = __fadd_rn(p, __fmul_rn(-step_size, __fdiv_rn(m, denom)));
     sg.exp_avg[i] = m;
     sg.exp_avg_sq[i] = v;
     sg.param[i] = pnew;
+    // soft_sync of the target copy from the updated parameter, the three
+    // separately rounded ops of d3a_soft_update_f32 (torch_utility.py:27-33)
+    if (tg) tg[i] = __fadd_rn(__fmul_rn(tv, (float)(1.0 - a.tau)), __fmul_rn((float)a.tau, pnew));
   }
-  // the step counter is committed by d3a_step_end after the update
+  // the step counter this launch reads is committed by another kernel
+  // (d3a_step_end, or a later d3a_adam_step's inc_mask)
 }
 
 // ---- split-K partials -> one gradient (the data-parallel path reduces
@@ -430,16 +454,51 @@ extern "C" int d3a_outer_mask_f32(const float* g, int64_t sgb, const float* w, i
   return 0;
 }
 
+extern "C" int d3a_adam_step(const d3a_adam_desc* a, void* stream) {
+  D3A_CHECK_ARG(a && a->segs && a->step, "d3a_adam_step: null pointer");
+  D3A_CHECK_ARG(a->n_seg > 0 && a->n_seg < 65536, "d3a_adam_step: bad segment count");
+  D3A_CHECK_ARG(a->n_blocks >= a->n_seg && a->n_blocks < (1ll << 31),
+                "d3a_adam_step: bad n_blocks");
+  D3A_CHECK_ARG(a->step_add == 0 || a->step_add == 1, "d3a_adam_step: step_add must be 0 or 1");
+  D3A_CHECK_ARG(!a->inc_mask || a->counters, "d3a_adam_step: counters required");
+  D3A_CHECK_ARG(!a->ring || (a->metrics && a->ring_ctr && a->n_metrics >= 1 &&
+                             a->n_metrics <= 256 && a->ring_cap > 0),
+                "d3a_adam_step: bad metric ring");
+  D3A_CHECK_ARG(!a->soft || a->targ_delta != 0, "d3a_adam_step: soft update needs targ_delta");
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)a->n_blocks), dim3(256), 0, (hipStream_t)stream,
+                     *a);
+  D3A_LAUNCH_CHECK("d3a_adam_step");
+  return 0;
+}
+
 extern "C" int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg, int64_t n_blocks,
                             const int64_t* step, double lr, double beta1, double beta2,
                             double eps, double grad_scale, void* stream) {
-  D3A_CHECK_ARG(segs && step, "d3a_adam_f32: null pointer");
-  D3A_CHECK_ARG(n_seg > 0 && n_seg < 65536, "d3a_adam_f32: bad segment count");
-  D3A_CHECK_ARG(n_blocks >= n_seg && n_blocks < (1ll << 31), "d3a_adam_f32: bad n_blocks");
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)n_blocks), dim3(256), 0, (hipStream_t)stream,
-                     segs, (int)n_seg, step, lr, beta1, beta2, eps, (float)grad_scale);
-  D3A_LAUNCH_CHECK("d3a_adam_f32");
-  return 0;
+  d3a_adam_desc a;
+  memset(&a, 0, sizeof(a));
+  a.segs = segs;
+  a.n_seg = n_seg;
+  a.n_blocks = n_blocks;
+  a.step = step;
+  a.step_add = 1;
+  a.lr = lr;
+  a.beta1 = beta1;
+  a.beta2 = beta2;
+  a.eps = eps;
+  a.grad_scale = grad_scale;
+  a.metric_scale = 1.f;
+  if (segs == nullptr || step == nullptr) {
+    set_error("d3a_adam_f32: null pointer");
+    return -1;
+  }
+  const int rc = d3a_adam_step(&a, stream);
+  if (rc != 0) {
+    // report under this entry point's name
+    char buf[512];
+    snprintf(buf, sizeof(buf), "%s", d3a_last_error());
+    set_error("d3a_adam_f32: %s", buf);
+  }
+  return rc;
 }
 
 extern "C" int d3a_grad_reduce_f32(const d3a_adam_segment* segs, int32_t n_seg,

@@ -141,6 +141,74 @@ __global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
   }
 }
 
+// Vector observations: one wave per batch row, four rows per workgroup.  The
+// index draw is lane-uniform (every lane computes the same Philox output), the
+// transition's table entries arrive in one round trip, and the observation,
+// action and reward loads that depend only on its row go out together in the
+// next one (the next observation too when n_steps == 1); longer n-step walks
+// follow the chain lane-uniformly as the generic kernel does.
+__global__ __launch_bounds__(256) void gather_vec_kernel(d3a_gather_desc d) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= d.B) return;
+  int64_t t;
+  if (d.idx) {
+    t = d.idx[b];
+  } else {
+    const uint64_t c = d.ctr ? (uint64_t)(*d.ctr) : (uint64_t)d.ctr_value;
+    uint32_t r[4];
+    Philox::gen(d.seed, c, (uint64_t)(d.row_offset + b), r);
+    const uint64_t x = ((uint64_t)r[0] << 32) | r[1];
+    t = (int64_t)(x % (uint64_t)d.n_trans);
+    if (lane == 0) d.idx_out[b] = t;
+  }
+  const int64_t row_t = d.t_row[t], last_t = d.t_ep_last[t];
+  const uint8_t term_t = d.t_terminal[t];
+  const int D = d.D, A = d.A;
+  // row-only loads first (they do not wait for the n-step walk)
+  const float rew_t = d.rew[row_t];
+  float ov = 0.f, av = 0.f;
+  if (lane < D) ov = d.obs[row_t * D + lane];
+  if (d.act && lane < A) av = d.act[row_t * A + lane];
+  int32_t ai = 0;
+  if (d.act_i && lane == 0) ai = d.act_i[row_t];
+  // n-step return (dataset.pyx:1323-1330), the generic kernel's arithmetic
+  float ret = __fmul_rn(rew_t, d.gamma_pow[0]);
+  ret = __fadd_rn(0.f, ret);
+  int64_t nt_i = t, row_i = row_t, last_i = last_t;
+  int k = 0;
+  for (k = 0; k < d.n_steps; ++k) {
+    if (k > 0) ret = __fadd_rn(ret, __fmul_rn(d.rew[row_i], d.gamma_pow[k]));
+    if (nt_i == last_i || k == d.n_steps - 1) break;
+    nt_i = nt_i + 1 == d.n_trans ? 0 : nt_i + 1;
+    row_i = d.t_row[nt_i];
+    last_i = d.t_ep_last[nt_i];
+  }
+  const bool term = (nt_i == t ? term_t : d.t_terminal[nt_i]) != 0;
+  const int64_t nrow = term ? -1 : row_i + 1;
+  float nv = 0.f;
+  if (nrow >= 0 && lane < D) nv = d.obs[nrow * D + lane];
+  if (lane < D) {
+    d.o_obs[b * D + lane] = ov;
+    d.o_next_obs[b * D + lane] = nv;
+  }
+  // observations wider than a wave (rare): the remaining columns
+  for (int j = lane + 64; j < D; j += 64) {
+    d.o_obs[b * D + j] = d.obs[row_t * D + j];
+    d.o_next_obs[b * D + j] = nrow >= 0 ? d.obs[nrow * D + j] : 0.f;
+  }
+  if (d.act) {
+    if (lane < A) d.o_act[b * A + lane] = av;
+    for (int j = lane + 64; j < A; j += 64) d.o_act[b * A + j] = d.act[row_t * A + j];
+  }
+  if (lane == 0) {
+    if (d.act_i) d.o_act_i[b] = ai;
+    d.o_rew[b] = ret;
+    d.o_term[b] = d.t_term_value ? d.t_term_value[nt_i] : (term ? 1.f : 0.f);
+    d.o_n_steps[b] = (float)(k + 1);
+  }
+}
+
 }  // namespace
 }  // namespace d3a
 
@@ -158,14 +226,26 @@ extern "C" int d3a_gather_batch(const d3a_gather_desc* d, void* stream) {
                 "d3a_gather_batch: exactly one of act / act_i");
   D3A_CHECK_ARG(d->n_steps >= 1 && d->n_frames >= 1, "d3a_gather_batch: n_steps, n_frames >= 1");
   D3A_CHECK_ARG(d->n_steps <= D3A_MAX_NSTEP, "d3a_gather_batch: n_steps > D3A_MAX_NSTEP");
-  D3A_CHECK_ARG(d->idx || (d->idx_out && d->ctr && d->ticket),
-                "d3a_gather_batch: indices must be given or drawn (idx_out, ctr, ticket)");
+  D3A_CHECK_ARG(d->idx || (d->idx_out && ((d->ctr && d->ticket) || (!d->ctr && d->ctr_value >= 0))),
+                "d3a_gather_batch: indices must be given or drawn (idx_out and ctr + ticket, "
+                "or ctr_value)");
+  D3A_CHECK_ARG(d->obs || d->ctr || d->idx, "d3a_gather_batch: ctr_value needs vector obs");
   D3A_CHECK_ARG(d->obs ? (d->o_obs && d->o_next_obs) : (d->o_frames && d->o_next_frames),
                 "d3a_gather_batch: missing observation outputs");
   D3A_CHECK_ARG(d->o_rew && d->o_term && d->o_n_steps && (d->act ? d->o_act != nullptr
                                                                  : d->o_act_i != nullptr),
                 "d3a_gather_batch: missing outputs");
-  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)d->B), dim3(256), 0, (hipStream_t)stream, *d);
+  if (d->obs && !d->idx && !d->ctr) {
+    // counter by value: the vector kernel (no ticket)
+    hipLaunchKernelGGL(gather_vec_kernel, dim3((unsigned)((d->B + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, *d);
+  } else if (d->obs && d->idx) {
+    hipLaunchKernelGGL(gather_vec_kernel, dim3((unsigned)((d->B + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, *d);
+  } else {
+    hipLaunchKernelGGL(gather_kernel, dim3((unsigned)d->B), dim3(256), 0, (hipStream_t)stream,
+                       *d);
+  }
   D3A_LAUNCH_CHECK("d3a_gather_batch");
   return 0;
 }

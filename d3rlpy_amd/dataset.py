@@ -412,6 +412,7 @@ class DeviceDataset:
         self.t_row, self.t_ep_start, self.t_ep_last, self.t_terminal = (up(t_row), up(t_s),
                                                                         up(t_l), up(t_t))
         self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._draws = 0  # host draw counter of the vector-observation sampler
         self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def __len__(self) -> int:
@@ -467,8 +468,14 @@ class DeviceDataset:
                 idx_out = torch.zeros(B, dtype=torch.int64, device=self.device)
             d.idx_out = ops.ptr(idx_out)
             d.seed = C.c_uint64(seed & 0xFFFFFFFFFFFFFFFF).value
-            d.ctr = ops.ptr(self.ctr)
-            d.ticket = ops.ptr(self.ticket)
+            if self.is_image:
+                d.ctr = ops.ptr(self.ctr)
+                d.ticket = ops.ptr(self.ticket)
+            else:
+                # the draw counter by value (this host call is the only
+                # consumer): the one-wave-per-row kernel, no device ticket
+                d.ctr_value = self._draws
+                self._draws += 1
             d.row_offset = row_offset
         d.B = B
         if self.is_image:

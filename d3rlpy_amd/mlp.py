@@ -75,6 +75,19 @@ _HEAD_GEN_MIN_ROWS = 4096
 _FIRST_LAYER_EPI = os.environ.get("D3A_W0_EPI", "1") == "1"
 # rows per fused workgroup (32 or 64; 0 = the library's choice)
 _FUSED_BM = int(os.environ.get("D3A_FUSED_BM", "0"))
+# the whole weight-gradient backward of a [n_in -> 256 -> 256 -> 1] Q ensemble
+# in one launch (d3a_q2_bwd) for large critic passes (the K2 / K4 CQL critic:
+# 7,936 rows x 2 members); D3A_Q2_BWD=0 keeps the per-layer GEMM path
+_Q2 = os.environ.get("D3A_Q2_BWD", "1") == "1"
+
+
+def q2_ok(net: EnsembleMLP, rows: int) -> bool:
+    """d3a_q2_bwd applies: two hidden layers of 256, one output, <= 48 inputs,
+    a large pass (per-layer GEMMs win on the 100-512-row passes)."""
+    s = net.sizes
+    return (_Q2 and not _FUSED_BWD and not ops.SBF16_TERMS and net.n_layers == 3
+            and s[1] == 256 and s[2] == 256 and s[3] == 1 and s[0] <= 48
+            and rows * net.C >= _HEAD_GEN_MIN_ROWS)
 
 
 def fused_ok(net: EnsembleMLP, rows: Optional[int] = None, backward: bool = False) -> bool:
@@ -204,17 +217,23 @@ class BackwardSpace:
         self.g_eff = torch.zeros(net.C, rows, device=device) if self.fused else None
         self.splits = n_splits(rows) if splits is None else splits
         self.grads = grads
+        # every weight gradient from d3a_q2_bwd: one partial per 256-row block
+        self.q2 = grads is not None and head_partials is None and q2_ok(net, rows)
         # first-layer weight gradients as one partial per 128-row tile, from
-        # the second layer's input-gradient GEMM (backward's wnext path)
+        # the second layer's input-gradient GEMM (backward's wnext path; it
+        # needs a layer above the first one, i.e. >= 2 hidden layers)
         self.l0_tiles = None
-        if (grads is not None and _FIRST_LAYER_EPI and not self.fused and net.n_layers >= 2
-                and net.sizes[0] <= 64 and rows * net.C >= _HEAD_GEN_MIN_ROWS):
+        if (grads is not None and _FIRST_LAYER_EPI and not self.fused and not self.q2
+                and net.n_layers >= 3 and net.sizes[0] <= 64
+                and rows * net.C >= _HEAD_GEN_MIN_ROWS):
             self.l0_tiles = (rows + 127) // 128
         if grads is not None:
             for l in range(net.n_layers):
                 o, i = net.sizes[l + 1], net.sizes[l]
                 parts = head_partials if (head_partials and l == net.n_layers - 1) \
                     else (self.l0_tiles if (l == 0 and self.l0_tiles) else self.splits)
+                if self.q2:
+                    parts = (rows + 255) // 256
                 grads.add(net.wname(l), (net.C, o, i), parts)
                 grads.add(net.bname(l), (net.C, o), parts)
 
@@ -252,6 +271,27 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         _backward_fused(bs, store, x, ldx, sxb_, acts, dout, ld_dout, sdout_b, r0, n,
                         weight_grads, dx, q_min, sq_b, q_scale, g_out, g_scale, n_scaled, C)
         return
+    if bs.q2 and weight_grads:
+        if (dx is not None or q_min is not None or head_ready or members is not None
+                or n != bs.rows or ld_dout != 1):
+            raise NotImplementedError("d3a_q2_bwd space: weight gradients of all rows only")
+        d = N.Q2BwdDesc()
+        H = sizes[1]
+        d.x, d.ldx, d.sxb = x + 4 * r0 * ldx, ldx, sxb_
+        d.h1 = acts.h[0].data_ptr() + 4 * r0 * H
+        d.h2 = acts.h[1].data_ptr() + 4 * r0 * H
+        d.sh, d.ldh = R * H, H
+        d.g, d.sgb = dout, sdout_b
+        if g_scale is not None:
+            d.gscale, d.n_scaled = g_scale, n_scaled
+        d.W2, d.sW2 = net.W(1, store), H * H
+        d.w3, d.sw3 = net.W(2, store), H
+        d.dW1, d.db1 = gs.get(net.wname(0)).data_ptr(), gs.get(net.bname(0)).data_ptr()
+        d.dW2, d.db2 = gs.get(net.wname(1)).data_ptr(), gs.get(net.bname(1)).data_ptr()
+        d.dW3, d.db3 = gs.get(net.wname(2)).data_ptr(), gs.get(net.bname(2)).data_ptr()
+        d.rows, d.n_in, d.C = n, sizes[0], C
+        ops.call_desc("d3a_q2_bwd", d)
+        return None
 
     def h_ptr(l):  # input activation of layer l at row r0
         if l == 0:

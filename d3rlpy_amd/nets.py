@@ -222,15 +222,29 @@ class AdamGroup:
             self.seg_table_reduced = torch.frombuffer(bytearray(bytes(red)),
                                                       dtype=torch.uint8).to(dev)
 
-    def launch(self, reduced: bool = False, grad_scale: float = 1.0) -> None:
+    def launch(self, reduced: bool = False, grad_scale: float = 1.0,
+               tail: Optional[dict] = None) -> None:
         """Adam over every segment; ``reduced``: from grad_store (after
-        ``reduce`` and an all-reduce) scaled by ``grad_scale``."""
+        ``reduce`` and an all-reduce) scaled by ``grad_scale``.  ``tail``:
+        keyword arguments of ops.adam_step (soft target update through
+        ``targ`` — a ParamStore of the same layout — and ``tau``, step_add,
+        counters / metric ring) for the fused end-of-update launch."""
         from . import ops
         table = self.seg_table_reduced if reduced else self.seg_table
         assert table is not None
-        ops.adam(table, len(self.names), self.n_blocks_reduced if reduced else self.n_blocks,
-                 self.step,
-                 self.lr, self.beta1, self.beta2, self.eps, grad_scale)
+        nb = self.n_blocks_reduced if reduced else self.n_blocks
+        if tail is None:
+            ops.adam(table, len(self.names), nb, self.step, self.lr, self.beta1, self.beta2,
+                     self.eps, grad_scale)
+            return
+        kw = dict(tail)
+        targ = kw.pop("targ", None)
+        if targ is not None:
+            assert targ.size == self.store.size and list(targ.specs) == list(self.store.specs)
+            kw["targ_delta"] = (targ.data.data_ptr() - self.store.data.data_ptr()) // 4
+            assert kw["targ_delta"] != 0
+        ops.adam_step(table, len(self.names), nb, self.step, self.lr, self.beta1, self.beta2,
+                      self.eps, grad_scale, **kw)
 
     def reduce(self) -> None:
         """grad_store <- sum of the split-K partials (no parameter update)."""

@@ -140,6 +140,28 @@ def adam(segs: torch.Tensor, n_seg: int, n_blocks: int, step: torch.Tensor, lr: 
                                  grad_scale, _stream()), "d3a_adam_f32")
 
 
+def adam_step(segs: torch.Tensor, n_seg: int, n_blocks: int, step: torch.Tensor, lr: float,
+              beta1: float, beta2: float, eps: float, grad_scale: float = 1.0,
+              step_add: int = 1, targ_delta: int = 0, tau: float = 0.0,
+              counters: Optional[torch.Tensor] = None, inc_mask: int = 0,
+              metrics: Optional[torch.Tensor] = None, ring: Optional[torch.Tensor] = None,
+              ring_ctr: Optional[torch.Tensor] = None, metric_scale: float = 1.0) -> None:
+    """d3a_adam_step: Adam with the soft target update (``targ_delta`` != 0:
+    the target copy ``targ_delta`` elements from each parameter) and the
+    step's counter / metric-ring bookkeeping in one launch."""
+    d = N.AdamDesc()
+    d.segs, d.n_seg, d.n_blocks = ptr(segs), n_seg, n_blocks
+    d.step, d.step_add = ptr(step), step_add
+    d.lr, d.beta1, d.beta2, d.eps, d.grad_scale = lr, beta1, beta2, eps, grad_scale
+    d.soft, d.targ_delta, d.tau = int(targ_delta != 0), targ_delta, tau
+    d.counters, d.inc_mask = ptr(counters), inc_mask
+    if ring is not None:
+        d.metrics, d.n_metrics = ptr(metrics), metrics.numel()
+        d.ring, d.ring_cap, d.ring_ctr = ptr(ring), ring.shape[0], ptr(ring_ctr)
+    d.metric_scale = metric_scale
+    N.check(N.lib().d3a_adam_step(C.byref(d), _stream()), "d3a_adam_step")
+
+
 def grad_reduce(segs: torch.Tensor, n_seg: int, n_blocks: int) -> None:
     N.check(N.lib().d3a_grad_reduce_f32(ptr(segs), n_seg, n_blocks, _stream()),
             "d3a_grad_reduce_f32")

@@ -268,6 +268,34 @@ typedef struct d3a_mlp_bwd_desc {
 } d3a_mlp_bwd_desc;
 int d3a_mlp_bwd(const d3a_mlp_bwd_desc* d, void* stream);
 
+/* Weight gradients of a single-output Q ensemble with two hidden layers of
+ * width 256 (VectorEncoderWithAction [n_in -> 256 -> 256], encoders.py:265-275,
+ * 328-339, + ContinuousMeanQFunction._fc, mean_q_function.py:255-256), one
+ * launch — the backward of update_critic's loss (ddpg_impl.py:119-133,
+ * cql_impl.py:110-125).  Per member c, rows r < rows (pointers at row 0):
+ *   g' = g[c*sgb + r] (* *gscale for r < n_scaled; gscale may be NULL)
+ *   dz2 = g' w3 * [h2 > 0],  dz1 = (dz2 W2) * [h1 > 0]
+ *   dW3 = g'^T h2, db3 = sum g', dW2 = dz2^T h1, db2 = sum dz2,
+ *   dW1 = dz1^T x, db1 = sum dz1
+ * as one partial per 256-row block p < P = ceil(rows / 256), laid out like
+ * the split-K partials d3a_adam_f32 sums: dW1 [P][C][256][n_in], db1
+ * [P][C][256], dW2 [P][C][256][256], db2 [P][C][256], dW3 [P][C][256], db3
+ * [P][C].  h1 / h2 [C][rows][ldh] (member stride sh), x [rows][ldx] (member
+ * stride sxb, 0 = shared), W2 [C][256][256] (stride sW2), w3 [C][256] (stride
+ * sw3); h1, h2, x, W2 16-byte aligned, ldx % 4 == 0, n_in <= 48. */
+typedef struct d3a_q2_bwd_desc {
+  const float* x; int64_t ldx, sxb;
+  const float* h1; const float* h2; int64_t sh, ldh;
+  const float* g; int64_t sgb;
+  const float* gscale; int64_t n_scaled;
+  const float* W2; int64_t sW2;
+  const float* w3; int64_t sw3;
+  float* dW1; float* db1; float* dW2; float* db2; float* dW3; float* db3;
+  int64_t rows;
+  int32_t n_in, C;
+} d3a_q2_bwd_desc;
+int d3a_q2_bwd(const d3a_q2_bwd_desc* d, void* stream);
+
 /* ---- optimiser and target networks ------------------------------------- */
 
 /* One parameter tensor inside a flat buffer, with its gradient given as
@@ -300,6 +328,31 @@ int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg,
                  double lr, double beta1, double beta2, double eps,
                  double grad_scale, void* stream);
 
+/* d3a_adam_f32 with the update's end-of-step bookkeeping folded in (one
+ * launch instead of Adam + d3a_step_end):
+ *   t = *step + step_add (1: *step counts completed steps; 0: an earlier
+ *       launch of the same update already advanced it);
+ *   soft != 0: after each element's step the target copy at
+ *       param + targ_delta (elements; a second buffer of the same layout) is
+ *       soft-synced from the new value, targ = targ*(1-tau) + tau*p, the three
+ *       rounded ops of d3a_soft_update_f32 (soft_sync, torch_utility.py:27-33:
+ *       DDPGBaseImpl.update_critic_target / update_actor_target run after the
+ *       parameter's last change of the step, so the fusion is exact);
+ *   block 0: counters[i] += 1 for each bit i of inc_mask, and with ring !=
+ *       NULL metrics[0:n_metrics] (* metric_scale) appended to
+ *       ring[*ring_ctr % ring_cap], *ring_ctr += 1 — as d3a_step_end; the
+ *       counters incremented must not include the one `step` points at. */
+typedef struct d3a_adam_desc {
+  const d3a_adam_segment* segs; int32_t n_seg; int64_t n_blocks;
+  const int64_t* step; int32_t step_add;
+  double lr, beta1, beta2, eps, grad_scale;
+  int32_t soft; int64_t targ_delta; double tau;
+  int64_t* counters; uint32_t inc_mask;
+  const float* metrics; int32_t n_metrics;
+  float* ring; int64_t ring_cap; int64_t* ring_ctr; float metric_scale;
+} d3a_adam_desc;
+int d3a_adam_step(const d3a_adam_desc* d, void* stream);
+
 /* grad_out = sum of the n_partials split-K partials of each segment (fp64
  * accumulation, same order and flat grid as d3a_adam_f32) — the data-parallel path's
  * reduction before the gradient all-reduce. */
@@ -331,6 +384,60 @@ int d3a_step_end(const float* metrics, int32_t n, float* ring, int64_t cap,
                  int64_t* ring_ctr, int64_t* counters, uint32_t inc_mask,
                  float* targ, const float* src, int64_t n_soft, double tau,
                  float metric_scale, void* stream);
+
+/* ---- stand-alone loss / sampling blocks (csrc/ops_generic.hip): the op set
+ *      behind the PyTorch custom ops of csrc/torch_ops.cpp; the update
+ *      pipelines run fused versions of the same arithmetic ------------------ */
+
+/* out[r] = logsumexp(x[r*ldx + 0:n]) (torch.logsumexp over the last dim; the
+ * CQL conservative term, d3rlpy/algos/torch/cql_impl.py:208-213), and its
+ * backward dx[r*lddx + j] = gout[r] * exp(x[r][j] - out[r]). */
+int d3a_logsumexp_f32(const float* x, int64_t rows, int64_t n, int64_t ldx, float* out,
+                      void* stream);
+int d3a_logsumexp_bwd_f32(const float* x, int64_t rows, int64_t n, int64_t ldx,
+                          const float* lse, const float* gout, float* dx, int64_t lddx,
+                          void* stream);
+
+/* TD error of ContinuousMeanQFunction.compute_error (q_functions/
+ * mean_q_function.py:74-87) per member c < C over n rows:
+ *   y = rew + gamma[r] * target[c][r] * (1 - term[r]),  diff[c][r] = q[c][r] - y
+ *   loss[c] = mean_r diff^2   (gamma[r] = gamma ** n_steps[r], ddpg_impl.py:123)
+ * and its backward dq[c][r] = 2 * diff[c][r] * gout[c] / n. */
+int d3a_td_mse_f32(const float* q, const float* rew, const float* target, const float* term,
+                   const float* gamma, int64_t C, int64_t n, float* diff, float* loss,
+                   void* stream);
+int d3a_td_mse_bwd_f32(const float* diff, const float* gout, int64_t C, int64_t n, float* dq,
+                       void* stream);
+
+/* compute_quantile_huber_loss (q_functions/utility.py:27-46) of quantiles
+ * q[b][0:N] against targets y[b][0:M] at fractions taus[b][0:N]:
+ *   loss[b] = (1/M) sum_j sum_i |taus_i - [y_j - q_i < 0]| * huber(y_j - q_i)
+ * (huber with beta 1; the QR / IQN losses of utility.py:49-64,
+ * iqn_q_function.py), and its backward dq[b][i] = gout[b] * d loss[b]/d q_i
+ * (the indicator is detached, as in the reference). */
+int d3a_quantile_huber_f32(const float* q, int64_t ldq, const float* y, int64_t ldy,
+                           const float* taus, int64_t ldt, int64_t B, int64_t N, int64_t M,
+                           float* loss, void* stream);
+int d3a_quantile_huber_bwd_f32(const float* q, int64_t ldq, const float* y, int64_t ldy,
+                               const float* taus, int64_t ldt, int64_t B, int64_t N, int64_t M,
+                               const float* gout, float* dq, int64_t lddq, void* stream);
+
+/* SquashedNormalPolicy.sample_with_log_prob (policies.py:196-216 +
+ * distributions.py:112-135) for rows b < B of A actions given the noise:
+ *   s = exp(clamp(logstd, min, max)), raw = mu + eps * s, action = tanh(raw),
+ *   logp[b] = sum_a Normal(mu, s).log_prob(raw) - 2 (log 2 - raw - softplus(-2 raw))
+ * and its backward (grad_action and / or grad_logp may be NULL = 0) to dmu and
+ * dlogstd (zero where the clamp is active). */
+int d3a_squashed_gauss_f32(const float* mu, const float* logstd, const float* eps, int64_t B,
+                           int32_t A, float min_logstd, float max_logstd, float* action,
+                           float* logp, void* stream);
+int d3a_squashed_gauss_bwd_f32(const float* mu, const float* logstd, const float* eps,
+                               int64_t B, int32_t A, float min_logstd, float max_logstd,
+                               const float* grad_action, const float* grad_logp, float* dmu,
+                               float* dlogstd, void* stream);
+
+/* ReLU backward: dz[i] = y[i] > 0 ? dy[i] : 0 (y the ReLU output). */
+int d3a_relu_mask_f32(const float* dy, const float* y, int64_t n, float* dz, void* stream);
 
 /* ---- random numbers ----------------------------------------------------- */
 
@@ -529,6 +636,9 @@ typedef struct d3a_gather_desc {
    * `acc = acc + reward * powf(gamma, (float)i)` — all fp32 — and powf is
    * not always the correctly rounded power, so the kernel reads the host's */
   float gamma_pow[D3A_MAX_NSTEP];
+  /* drawn indices with ctr == NULL: the step's counter value is ctr_value
+   * (the caller counts its draws; no device counter, no ticket) */
+  int64_t ctr_value;
 } d3a_gather_desc;
 int d3a_gather_batch(const d3a_gather_desc* d, void* stream);
 

@@ -46,14 +46,15 @@ def test_argument_errors_are_reported_without_a_gpu():
 
 
 STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_gemm_wnext", "GemmWnext"),
-           ("d3a_adam_segment", "AdamSegment"),
+           ("d3a_adam_segment", "AdamSegment"), ("d3a_adam_desc", "AdamDesc"),
            ("d3a_head1_bwd_desc", "Head1BwdDesc"), ("d3a_head1_min_desc", "Head1MinDesc"),
            ("d3a_cql_sample_desc", "CqlSampleDesc"), ("d3a_cql_loss_desc", "CqlLossDesc"),
            ("d3a_sac_actor_head_desc", "SacActorHeadDesc"), ("d3a_gather_desc", "GatherDesc"),
            ("d3a_td3_prep_desc", "Td3PrepDesc"), ("d3a_td3_target_desc", "Td3TargetDesc"),
            ("d3a_td3_critic_loss_desc", "Td3CriticLossDesc"),
            ("d3a_td3bc_actor_desc", "Td3bcActorDesc"), ("d3a_mlp_fwd_desc", "MlpFwdDesc"), ("d3a_dqn_loss_desc", "DqnLossDesc"),
-           ("d3a_mlp_bwd_desc", "MlpBwdDesc"), ("d3a_bcq_rows_desc", "BcqRowsDesc"),
+           ("d3a_mlp_bwd_desc", "MlpBwdDesc"), ("d3a_q2_bwd_desc", "Q2BwdDesc"),
+           ("d3a_bcq_rows_desc", "BcqRowsDesc"),
            ("d3a_bcq_vae_desc", "BcqVaeDesc"), ("d3a_bcq_target_desc", "BcqTargetDesc"),
            ("d3a_bcq_qr_desc", "BcqQrDesc"), ("d3a_bcq_actor_desc", "BcqActorDesc"),
            ("d3a_im2col_desc", "Im2colDesc"), ("d3a_col2im_desc", "Col2imDesc"),

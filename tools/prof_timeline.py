@@ -6,7 +6,7 @@ import sys
 
 path = sys.argv[1]
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "gather_kernel" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "gather_" in r["Kernel_Name"]]
 a, b = starts[-3], starts[-2]
 prev_end = None
 tot_k = tot_gap = 0
