@@ -11,7 +11,7 @@ from __future__ import annotations
 from typing import Any, Dict, Optional, Sequence
 
 from ..constants import ActionSpace
-from ..factories import AdamFactory, OptimizerFactory, check_encoder, check_q_func
+from ..factories import AdamFactory, OptimizerFactory, check_encoder, check_q_func, check_use_gpu
 from .base import AlgoBase
 from .bcq_impl import BCQImpl
 
@@ -42,7 +42,7 @@ class BCQ(AlgoBase):
         action_flexibility: float = 0.05,
         rl_start_step: int = 0,
         beta: float = 0.5,
-        use_gpu=False,
+        use_gpu=True,
         scaler=None,
         action_scaler=None,
         reward_scaler=None,
@@ -70,7 +70,7 @@ class BCQ(AlgoBase):
         self._action_flexibility = action_flexibility
         self._rl_start_step = rl_start_step
         self._beta = beta
-        self._use_gpu = use_gpu
+        self._use_gpu = check_use_gpu(use_gpu)
         self._impl = impl
 
     def _create_impl(self, observation_shape: Sequence[int], action_size: int) -> None:

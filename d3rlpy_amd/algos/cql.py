@@ -43,7 +43,7 @@ class CQL(AlgoBase):
         conservative_weight: float = 5.0,
         n_action_samples: int = 10,
         soft_q_backup: bool = False,
-        use_gpu=False,
+        use_gpu=True,
         scaler=None,
         action_scaler=None,
         reward_scaler=None,
@@ -72,7 +72,7 @@ class CQL(AlgoBase):
         self._conservative_weight = conservative_weight
         self._n_action_samples = n_action_samples
         self._soft_q_backup = soft_q_backup
-        self._use_gpu = use_gpu
+        self._use_gpu = check_use_gpu(use_gpu)
         self._impl = impl
 
     def _create_impl(self, observation_shape: Sequence[int], action_size: int) -> None:
@@ -145,7 +145,7 @@ class DiscreteCQL(AlgoBase):
         n_critics: int = 1,
         target_update_interval: int = 8000,
         alpha: float = 1.0,
-        use_gpu=False,
+        use_gpu=True,
         scaler=None,
         reward_scaler=None,
         impl: Optional[DiscreteCQLImpl] = None,
@@ -161,7 +161,7 @@ class DiscreteCQL(AlgoBase):
         self._n_critics = n_critics
         self._target_update_interval = target_update_interval
         self._alpha = alpha
-        self._use_gpu = use_gpu
+        self._use_gpu = check_use_gpu(use_gpu)
         self._impl = impl
 
     def _create_impl(self, observation_shape: Sequence[int], action_size: int) -> None:

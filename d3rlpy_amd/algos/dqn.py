@@ -15,7 +15,7 @@ from __future__ import annotations
 
 from typing import Any, Optional, Sequence
 
-from ..factories import AdamFactory, OptimizerFactory
+from ..factories import AdamFactory, OptimizerFactory, check_use_gpu
 from .cql import DiscreteCQL, _resolve
 from .discrete_cql_impl import DiscreteCQLImpl
 
@@ -57,7 +57,7 @@ class DQN(DiscreteCQL):
         gamma: float = 0.99,
         n_critics: int = 1,
         target_update_interval: int = 8000,
-        use_gpu=False,
+        use_gpu=True,
         scaler=None,
         reward_scaler=None,
         impl: Optional[DQNImpl] = None,

@@ -97,11 +97,15 @@ class ImplBase:
         self._scaler = scaler
         self._action_scaler = action_scaler
         self._reward_scaler = reward_scaler
+        device = check_use_gpu(use_gpu)
+        if device is None:
+            # the reference's use_gpu=False / None is its CPU path
+            raise NotImplementedError(
+                "use_gpu=False / None selects the reference's CPU path; the HIP engine has "
+                "no CPU compute path (pass use_gpu=True, a device id or a Device)")
         if not torch.cuda.is_available():
             raise RuntimeError("d3rlpy_amd requires a HIP GPU (no CPU fallback)")
-        dev_id = check_use_gpu(use_gpu) if use_gpu not in (None, False, True) \
-            else torch.cuda.current_device()
-        self._device = f"cuda:{dev_id}"
+        self._device = f"cuda:{device.get_id()}"
         self.torch_device = torch.device(self._device)
 
     # ---- inference (numpy in / numpy out) ---------------------------------

@@ -20,7 +20,7 @@ import torch
 
 from .. import checkpoint as ckpt
 from ..constants import ActionSpace
-from ..factories import AdamFactory, OptimizerFactory, check_encoder, check_q_func
+from ..factories import AdamFactory, OptimizerFactory, check_encoder, check_q_func, check_use_gpu
 from .base import AlgoBase
 from .cql import _resolve
 from .cql_impl import CQLImpl
@@ -105,7 +105,7 @@ class SAC(AlgoBase):
         tau: float = 0.005,
         n_critics: int = 2,
         initial_temperature: float = 1.0,
-        use_gpu=False,
+        use_gpu=True,
         scaler=None,
         action_scaler=None,
         reward_scaler=None,
@@ -127,7 +127,7 @@ class SAC(AlgoBase):
         self._tau = tau
         self._n_critics = n_critics
         self._initial_temperature = initial_temperature
-        self._use_gpu = use_gpu
+        self._use_gpu = check_use_gpu(use_gpu)
         self._impl = impl
 
     def _create_impl(self, observation_shape: Sequence[int], action_size: int) -> None:

@@ -16,7 +16,7 @@ from __future__ import annotations
 from typing import Any, Dict, Optional, Sequence
 
 from ..constants import ActionSpace
-from ..factories import AdamFactory, OptimizerFactory, check_encoder, check_q_func
+from ..factories import AdamFactory, OptimizerFactory, check_encoder, check_q_func, check_use_gpu
 from .base import AlgoBase
 from .td3_plus_bc_impl import TD3PlusBCImpl
 
@@ -81,7 +81,7 @@ class TD3(AlgoBase):
         target_smoothing_sigma: float = 0.2,
         target_smoothing_clip: float = 0.5,
         update_actor_interval: int = 2,
-        use_gpu=False,
+        use_gpu=True,
         scaler=None,
         action_scaler=None,
         reward_scaler=None,
@@ -103,7 +103,7 @@ class TD3(AlgoBase):
         self._target_smoothing_sigma = target_smoothing_sigma
         self._target_smoothing_clip = target_smoothing_clip
         self._update_actor_interval = update_actor_interval
-        self._use_gpu = use_gpu
+        self._use_gpu = check_use_gpu(use_gpu)
         self._impl = impl
 
     def _create_impl(self, observation_shape: Sequence[int], action_size: int) -> None:
@@ -165,7 +165,7 @@ class DDPG(AlgoBase):
         gamma: float = 0.99,
         tau: float = 0.005,
         n_critics: int = 1,
-        use_gpu=False,
+        use_gpu=True,
         scaler=None,
         action_scaler=None,
         reward_scaler=None,
@@ -184,7 +184,7 @@ class DDPG(AlgoBase):
         self._q_func_factory = check_q_func(q_func_factory)
         self._tau = tau
         self._n_critics = n_critics
-        self._use_gpu = use_gpu
+        self._use_gpu = check_use_gpu(use_gpu)
         self._impl = impl
 
     def _create_impl(self, observation_shape: Sequence[int], action_size: int) -> None:

@@ -11,7 +11,7 @@ from __future__ import annotations
 from typing import Any, Dict, Optional, Sequence
 
 from ..constants import ActionSpace
-from ..factories import AdamFactory, OptimizerFactory, check_encoder, check_q_func
+from ..factories import AdamFactory, OptimizerFactory, check_encoder, check_q_func, check_use_gpu
 from .base import AlgoBase
 from .td3_plus_bc_impl import TD3PlusBCImpl
 
@@ -37,7 +37,7 @@ class TD3PlusBC(AlgoBase):
         target_smoothing_clip: float = 0.5,
         alpha: float = 2.5,
         update_actor_interval: int = 2,
-        use_gpu=False,
+        use_gpu=True,
         scaler="standard",
         action_scaler=None,
         reward_scaler=None,
@@ -60,7 +60,7 @@ class TD3PlusBC(AlgoBase):
         self._target_smoothing_clip = target_smoothing_clip
         self._alpha = alpha
         self._update_actor_interval = update_actor_interval
-        self._use_gpu = use_gpu
+        self._use_gpu = check_use_gpu(use_gpu)
         self._impl = impl
 
     def _create_impl(self, observation_shape: Sequence[int], action_size: int) -> None:

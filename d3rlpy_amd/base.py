@@ -153,7 +153,8 @@ class LearnableBase:
             if k == "impl":
                 continue
             if k == "use_gpu":
-                v = None if v is None or v is False else (0 if v is True else int(v))
+                v = None if v is None or v is False else (
+                    0 if v is True else (v.get_id() if hasattr(v, "get_id") else int(v)))
             params[k] = _serialize(v)
         params["algorithm"] = self.__class__.__name__
         params["observation_shape"] = list(self._impl.observation_shape)
@@ -162,22 +163,23 @@ class LearnableBase:
             json.dump(params, f, indent=2, default=_json_default)
 
     @classmethod
-    def params_from_json(cls, fname: str, use_gpu=False):
+    def params_from_json(cls, fname: str, use_gpu=True):
         """(observation_shape, action_size, constructor kwargs) of a params.json
         written by the reference or by save_params (base.py:186-232)."""
         with open(fname) as f:
             params = json.load(f)
         observation_shape = tuple(params.pop("observation_shape"))
         action_size = params.pop("action_size")
-        algorithm = params.pop("algorithm", None)
-        if algorithm is not None and algorithm != cls.__name__:
-            raise ValueError(f"params.json is for {algorithm}, not {cls.__name__}")
+        # the reference passes every remaining key through **kwargs and its
+        # constructors ignore ``algorithm``: a params.json of a related class
+        # (DQN -> DoubleDQN, a subclass) loads too
+        params.pop("algorithm", None)
         params = {k: _deserialize(k, v) for k, v in params.items()}
         params["use_gpu"] = use_gpu
         return observation_shape, action_size, params
 
     @classmethod
-    def from_json(cls, fname: str, use_gpu=False) -> "LearnableBase":
+    def from_json(cls, fname: str, use_gpu=True) -> "LearnableBase":
         observation_shape, action_size, params = cls.params_from_json(fname, use_gpu)
         algo = cls(**params)
         algo.create_impl(observation_shape, action_size)
@@ -308,17 +310,17 @@ class LearnableBase:
             # loss); the reference logs such a metric only on the steps that
             # produce it, so the epoch mean skips those rows
             epoch_loss = {n: _mean_present(values[:, i]) for i, n in enumerate(names)}
-            logger.add_epoch(epoch, total_step, epoch_loss,
-                             {"time_step": elapsed / max(1, len(iterator))})
             self._loss_history["epoch"].append(epoch)
             self._loss_history["step"].append(total_step)
             for k, v in epoch_loss.items():
                 self._loss_history[k].append(v)
             if scorers and eval_episodes:
-                # base.py:806-821: scorer(algo, episodes) per named scorer
+                # base.py:806-821: scorer(algo, episodes) per named scorer, added
+                # to the same epoch record (add_metric before commit)
                 scores = self._evaluate(eval_episodes, scorers)
-                logger.add_epoch(epoch, total_step, scores, {})
                 epoch_loss.update(scores)
+            logger.add_epoch(epoch, total_step, epoch_loss,
+                             {"time_step": elapsed / max(1, len(iterator))})
             if save_metrics and epoch % save_interval == 0:
                 logger.save_model(total_step, self)
             yield epoch, dict(epoch_loss)

@@ -186,9 +186,12 @@ __global__ __launch_bounds__(256) void cql_lse_kernel(d3a_cql_loss_desc d) {
 // Latency-bound (one CU): every input is loaded up front — the per-row values
 // into registers (LOSS_MP slots per thread, the same p = tid + i * nt order
 // the sums use), the scalar optimiser states by thread 0 — so the stage pays
-// about one global round trip instead of one per phase.
+// about one global round trip instead of one per phase.  Ensembles x batches
+// beyond LOSS_MP * 1024 rows (REG = false) read the per-row values where they
+// are used, in the same p = tid + i * nt order (identical sums).
 constexpr int LOSS_MP = 8;
 
+template <bool REG>
 __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   __shared__ float scratch[16];
   __shared__ float sh[4];
@@ -222,11 +225,10 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   float s_temp = 0.f;
   if (temp_on && phase != 2)
     for (int64_t b = tid; b < B; b += nt) s_temp += d.logp_temp[b] - (float)d.A;
-#pragma unroll
-  for (int i = 0; i < LOSS_MP; ++i) {
-    const int64_t p = tid + (int64_t)i * nt;
+  // the per-row inputs of row p = c * B + b (slot i of REG's registers)
+  auto load_row = [&](int i, int64_t p) {
     r_lseA[i] = r_qd[i] = r_lseC[i] = r_tq[i] = r_rw[i] = r_tm[i] = r_ns[i] = 0.f;
-    if (p >= CB) continue;
+    if (p >= CB) return;
     const int64_t c = p / B, b = p % B;
     if ((alpha_on && phase != 2) || critic_on) r_qd[i] = d.q[c * d.R + 6 * NB + b];
     if (alpha_on && phase != 2) r_lseA[i] = d.lse[c * B + b];
@@ -239,7 +241,22 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
       r_ns[i] = d.n_steps[b];
       if (cons_on) r_lseC[i] = d.lse[(C + c) * B + b];
     }
+  };
+  // row slots per thread: LOSS_MP registers, or (REG false) one register
+  // reused for every p = tid + i * nt < CB
+  const int n_slot = REG ? LOSS_MP : (int)((CB + nt - 1) / nt);
+  if constexpr (REG) {
+#pragma unroll
+    for (int i = 0; i < LOSS_MP; ++i) load_row(i, tid + (int64_t)i * nt);
   }
+  auto slot = [&](int i) -> int {  // register index holding slot i's row
+    if constexpr (REG) {
+      return i;
+    } else {
+      load_row(0, tid + (int64_t)i * nt);
+      return 0;
+    }
+  };
   __syncthreads();  // s_bc
 
   // ---- update_temp (sac_impl.py:123-146) ----
@@ -273,9 +290,17 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
     if (phase != 2) {
       float sl = 0.f, sd = 0.f;
 #pragma unroll
-      for (int i = 0; i < LOSS_MP; ++i) {
-        sl += r_lseA[i];
-        sd += r_qd[i];
+      for (int i = 0; i < (REG ? LOSS_MP : 1); ++i) {
+        if (REG) {
+          sl += r_lseA[i];
+          sd += r_qd[i];
+        } else {
+          for (int k = 0; k < n_slot; ++k) {
+            const int j = slot(k);
+            sl += r_lseA[j];
+            sd += r_qd[j];
+          }
+        }
       }
       lsum = block_sum(sl, scratch);
       dsum = block_sum(sd, scratch);
@@ -321,9 +346,11 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   const float gcons = cons_on ? ca * d.conservative_weight / (float)CB : 0.f;
   float s_td = 0.f, s_l = 0.f, s_d = 0.f;
 #pragma unroll
-  for (int i = 0; i < LOSS_MP; ++i) {
-    const int64_t p = tid + (int64_t)i * nt;
+  for (int k = 0; k < (REG ? LOSS_MP : 1); ++k) for (int i0 = 0; i0 < (REG ? 1 : n_slot); ++i0) {
+    const int si = REG ? k : i0;
+    const int64_t p = tid + (int64_t)si * nt;
     if (p >= CB) continue;
+    const int i = slot(si);
     const int64_t c = p / B, b = p % B;
     float tq = r_tq[i];
     // soft backup: target - exp(log_temp) * log_prob (sac_impl.py:156-162)
@@ -507,15 +534,16 @@ extern "C" int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream) {
   D3A_CHECK_ARG(d->conservative || !d->update_alpha,
                 "d3a_cql_loss: update_alpha needs the conservative term");
   D3A_CHECK_ARG(!d->conservative || d->N >= 1, "d3a_cql_loss: the conservative term needs N >= 1");
-  D3A_CHECK_ARG((int64_t)d->C * d->B <= (int64_t)LOSS_MP * 1024,
-                "d3a_cql_loss: n_critics * batch must be <= 8192");
   // phase 2 reuses the logsumexp / softmax weights phase 1 wrote
   if (d->conservative && (d->update_alpha || d->update_critic) && d->dp_phase != 2) {
     const int64_t waves = 2LL * d->C * d->B;
     hipLaunchKernelGGL(cql_lse_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, *d);
   }
-  hipLaunchKernelGGL(cql_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, *d);
+  if ((int64_t)d->C * d->B <= (int64_t)LOSS_MP * 1024)
+    hipLaunchKernelGGL(cql_loss_kernel<true>, dim3(1), dim3(1024), 0, (hipStream_t)stream, *d);
+  else
+    hipLaunchKernelGGL(cql_loss_kernel<false>, dim3(1), dim3(1024), 0, (hipStream_t)stream, *d);
   D3A_LAUNCH_CHECK("d3a_cql_loss");
   return 0;
 }

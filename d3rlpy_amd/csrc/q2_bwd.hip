@@ -14,22 +14,28 @@
 // Why one kernel: the two large products of this backward, dz2 W2 (the input
 // gradient of layer 2) and dz2^T h1 (its weight gradient), read the same dz2
 // and h1 rows.  A workgroup owns 256 rows of one member and a quarter (64
-// units) of layer 1: it stages W2[:, quarter] in LDS once, then for each
-// 64-row sub-block generates dz2 (64 x 256) into LDS from h2 and stages the
-// h1 and x tiles beside it.  Four waves, one per SIMD (so each has the whole
-// 512-entry register file: accumulators, the next sub-block's loads and the
-// operand pipeline never spill); wave w computes, per sub-block,
-//   dh1 tile (rows 32 (w & 1).., units 32 (w >> 1)..) = dz2 W2[:, quarter]
-//       (K = 256), its ReLU mask, and the first layer's dW1 / db1 from the
-//       masked tile in registers
-//   dW2[64 w .. 64 w + 63][quarter] += dz2^T h1[:, quarter]  (K = 64 rows)
-// with the two independent MFMA chains interleaved (272 MFMAs per wave per
-// sub-block).  The next sub-block's loads are in flight during the MFMAs.  Gradients leave as one partial per 256-row block
+// units) of layer 1 and walks its rows in 32-row sub-blocks through LDS tiles
+// (dz2 32 x 256 generated from h2, double-buffered; h1[:, quarter] and x,
+// triple-buffered).  Eight waves, two per SIMD, split by role so each SIMD
+// holds one wave of each (waves w and w + 4 share a SIMD):
+//   waves 0-3  dh1 (32 rows x units 32 (w & 1)..) over half of K (o in
+//              128 (w >> 1)..), with their W2 slice held in registers; the
+//              half-K partials meet in LDS and the w < 2 waves apply the ReLU
+//              mask and form the first layer's dW1 / db1 from the masked tile
+//              (one sub-block later, overlapping the next sub-block's MFMAs)
+//   waves 4-7  dW2[64 (w - 4) .. + 63][quarter] += dz2^T h1[:, quarter]
+//              (K = 32 rows; four 32 x 32 accumulators)
+// 64 MFMAs per wave per sub-block.  While a sub-block is multiplied, every
+// wave also stages the next one into the other buffers (from registers loaded
+// one sub-block earlier) and issues the loads of the one after, spread over
+// the MFMA loop, so the matrix pipe is not idle while tiles are built; one
+// barrier per sub-block.  Gradients leave as one partial per 256-row block
 // (the optimiser sums them in order, like split-K partials); every other
 // reduction is in a fixed order, so the result is run-to-run bit-identical.
 // MFMA: v_mfma_f32_32x32x2_f32 (exact fp32), operands from LDS with
 // conflict-free strides (dz2 rows 257 floats apart: its rows and its columns
 // are both read as 32 consecutive banks).
+#include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
 
@@ -40,20 +46,19 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int Q2_H = 256;    // hidden width
 constexpr int Q2_RB = 256;   // rows per workgroup (one gradient partial)
-constexpr int Q2_SB = 64;    // rows per LDS sub-block
+constexpr int Q2_SB = 32;    // rows per LDS sub-block
 constexpr int Q2_NSB = Q2_RB / Q2_SB;
 constexpr int Q2_QW = 64;    // layer-1 units per workgroup
 constexpr int Q2_LDZ = 257;  // dz2 row stride
-constexpr int Q2_XMAX = 48;  // widest first-layer input staged in LDS
-constexpr int Q2_NT = 256;   // threads: four waves, one per SIMD
+constexpr int Q2_NT = 512;   // threads: eight waves, two per SIMD
 
+template <int XL>
 struct Q2Lds {
-  float w2[Q2_H * Q2_QW];    // W2[o][i0 + i]
-  float dz[Q2_SB * Q2_LDZ];  // dz2[r][o]
-  float h1[Q2_SB * Q2_QW];   // h1[r][i0 + i]
-  float x[Q2_SB * Q2_XMAX];  // x[r][d]
+  float dz[2][Q2_SB * Q2_LDZ];      // dz2[r][o]
+  float h1[3][Q2_SB * Q2_QW];       // h1[r][i0 + i]
+  float x[3][Q2_SB * XL];           // x[r][d]
+  float ex[2][2 * 16 * 64];         // dh1 half-K partials of waves 2, 3
 };
-static_assert(sizeof(Q2Lds) <= 163840, "LDS");
 
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
@@ -61,9 +66,12 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 
 // XL: the first layer's input width rounded up to 4 (16, 32 or 48), fixed at
 // compile time so the LDS addresses of the x operand are immediates
-template <int XL>
+// NOSTAGE (timing probe only, tools/bench_q2.py --probe): the sub-block
+// staging and loads are skipped, every sub-block reuses the first one's tiles
+template <int XL, bool NOSTAGE = false>
 __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
-  __shared__ __attribute__((aligned(16))) Q2Lds L;
+  __shared__ __attribute__((aligned(16))) Q2Lds<XL> L;
+  static_assert(sizeof(Q2Lds<XL>) <= 163840, "LDS");
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform
   const int li = lane & 31, lk = lane >> 5;
@@ -93,188 +101,243 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
   const int i0 = q * Q2_QW;
   const int nin = d.n_in, xr4 = (nin + 3) / 4;  // float4 pieces of an x row
   constexpr int x4 = XL / 4;
-  constexpr int XV = (Q2_SB * x4 + Q2_NT - 1) / Q2_NT;  // x pieces per thread
   const int64_t rlast = rows - 1;
+  const bool role_dx = w < 4;
+  const int ib = w & 1, kh = (w >> 1) & 1;  // dX waves: unit block, K half
+  const int ob0 = 64 * (w - 4);             // dW2 waves: o block
 
-  // ---- W2[:, quarter] -> LDS (once), w3 for this lane's columns
-#pragma unroll
-  for (int v = 0; v < 16; ++v) {
-    const int idx = t + Q2_NT * v, o = idx >> 4, c4 = (idx & 15) * 4;
-    const float4 wv = *reinterpret_cast<const float4*>(W2g + o * Q2_H + i0 + c4);
-    *reinterpret_cast<float4*>(&L.w2[o * Q2_QW + c4]) = wv;
-  }
   float w3v[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) w3v[j] = w3g[lane + 64 * j];
 
-  // ---- sub-block loads (unconditional, clamped rows; validity applied at staging)
-  // thread (w, lane): h2 rows w + 4s, columns lane + 64j; h1 / x as float4 pieces
-  float hv[16][4], gv[16];
-  float h1v[4][4], xv[XV][4];  // float4 pieces kept as scalars (registers)
-  auto prefetch = [&](int sb) {
+  // ---- staging registers of one sub-block (unconditional loads, clamped
+  // rows; validity applied when staged).  Thread (w, lane): h2 rows w + 8s
+  // (s < 4), columns lane + 64j; one float4 piece of h1 and of x
+  float hv[4][4], gv[4], h1v[4], xv[4];
+  auto load_row = [&](int sb, int s) {
+    int64_t r = rb0 + sb * Q2_SB + w + 8 * s;
+    r = r < rlast ? r : rlast;
+    gv[s] = gg[r];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hv[s][j] = h2g[(int)r * ldh + lane + 64 * j];
+  };
+  auto load_tiles = [&](int sb) {
     const int64_t base = rb0 + sb * Q2_SB;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      int64_t r = base + w + 4 * s;
+    {
+      int64_t r = base + (t >> 4);
       r = r < rlast ? r : rlast;
-      gv[s] = gg[r];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) hv[s][j] = h2g[(int)r * ldh + lane + 64 * j];
+      const float4 a = *reinterpret_cast<const float4*>(h1g + (int)r * ldh + i0 + (t & 15) * 4);
+      h1v[0] = a.x; h1v[1] = a.y; h1v[2] = a.z; h1v[3] = a.w;
     }
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int idx = t + Q2_NT * v;
-      int64_t r = base + (idx >> 4);
-      r = r < rlast ? r : rlast;
-      const float4 a = *reinterpret_cast<const float4*>(h1g + (int)r * ldh + i0 + (idx & 15) * 4);
-      h1v[v][0] = a.x; h1v[v][1] = a.y; h1v[v][2] = a.z; h1v[v][3] = a.w;
-    }
-#pragma unroll
-    for (int v = 0; v < XV; ++v) {
-      const int idx = t + Q2_NT * v;
-      const int ix = idx < Q2_SB * x4 ? idx : Q2_SB * x4 - 1;
+    {
+      const int ix = t < Q2_SB * x4 ? t : Q2_SB * x4 - 1;
       int64_t rx = base + ix / x4;
       rx = rx < rlast ? rx : rlast;
       const int cx = ix % x4 < xr4 ? ix % x4 : 0;  // pieces past n_in: staged as 0
       const float4 a = *reinterpret_cast<const float4*>(xg + (int)rx * ldx + cx * 4);
-      xv[v][0] = a.x; xv[v][1] = a.y; xv[v][2] = a.z; xv[v][3] = a.w;
+      xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
     }
   };
 
   // fp64 running sums: db2 / dW3 of column i0 + lane (every thread), db3
-  // (lane 0 of each wave), db1 of this wave's dh1 column
+  // (lane 0 of each wave), db1 of a w < 2 wave's column
   double acc_db2 = 0.0, acc_dw3 = 0.0, acc_db3 = 0.0, acc_db1 = 0.0;
-  const int rh = w & 1, ib = w >> 1;  // dh1 tile: row half, 32-unit block
-  // accumulators: A1 dh1 of the sub-block, W1[db] dW1 (input block db),
-  // W2t[ob][bb] dW2 tile (o block 64 w + 32 ob, unit block 32 bb)
-  f32x16 A1, W1[2], W2t[2][2];
+  auto stage_row = [&](int sb, int s) {
+    const int buf = sb & 1;
+    const int rl = w + 8 * s;
+    const int64_t r = rb0 + sb * Q2_SB + rl;
+    const bool ok = r < rows && sb < Q2_NSB;  // (the loop's one-past-the-end stage is all zero)
+    float gp = gv[s];
+    if (r < d.n_scaled) gp *= gs;  // as d3a_head1_bwd forms g'
+    if (!ok) gp = 0.f;
+    float hq = 0.f, dq = 0.f;  // this workgroup's quarter column (j == q)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    W1[0][r] = W1[1][r] = 0.f;
-    W2t[0][0][r] = W2t[0][1][r] = W2t[1][0][r] = W2t[1][1][r] = 0.f;
-  }
-  const int ndb = (nin + 31) / 32;  // 32-wide input blocks of dW1 (1 or 2)
-
-  auto stage = [&](int sb) {
+    for (int j = 0; j < 4; ++j) {
+      const float hval = ok ? hv[s][j] : 0.f;
+      const float dzv = hval > 0.f ? gp * w3v[j] : 0.f;
+      L.dz[buf][rl * Q2_LDZ + lane + 64 * j] = dzv;
+      hq = j == q ? hval : hq;
+      dq = j == q ? dzv : dq;
+    }
+    acc_db2 += (double)dq;
+    acc_dw3 += (double)(gp * hq);
+    if (lane == 0) acc_db3 += (double)gp;
+  };
+  auto stage_tiles = [&](int sb) {
+    const int buf = sb % 3;
     const int64_t base = rb0 + sb * Q2_SB;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int rl = w + 4 * s;
-      const int64_t r = base + rl;
-      const bool ok = r < rows;
-      float gp = gv[s];
-      if (r < d.n_scaled) gp *= gs;  // as d3a_head1_bwd forms g'
-      if (!ok) gp = 0.f;
-      float hq = 0.f, dq = 0.f;  // this workgroup's quarter column (j == q)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float hval = ok ? hv[s][j] : 0.f;
-        const float dzv = hval > 0.f ? gp * w3v[j] : 0.f;
-        L.dz[rl * Q2_LDZ + lane + 64 * j] = dzv;
-        hq = j == q ? hval : hq;
-        dq = j == q ? dzv : dq;
-      }
-      acc_db2 += (double)dq;
-      acc_dw3 += (double)(gp * hq);
-      if (lane == 0) acc_db3 += (double)gp;
-    }
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int idx = t + Q2_NT * v, rl = idx >> 4;
-      *reinterpret_cast<float4*>(&L.h1[rl * Q2_QW + (idx & 15) * 4]) =
-          base + rl < rows ? make_float4(h1v[v][0], h1v[v][1], h1v[v][2], h1v[v][3]) : z;
+    const int rl = t >> 4;
+    *reinterpret_cast<float4*>(&L.h1[buf][rl * Q2_QW + (t & 15) * 4]) =
+        (base + rl < rows && sb < Q2_NSB) ? make_float4(h1v[0], h1v[1], h1v[2], h1v[3]) : z;
+    if (t < Q2_SB * x4) {
+      const int rx = t / x4;
+      *reinterpret_cast<float4*>(&L.x[buf][rx * XL + (t % x4) * 4]) =
+          (base + rx < rows && sb < Q2_NSB && t % x4 < xr4) ? make_float4(xv[0], xv[1], xv[2], xv[3]) : z;
     }
-#pragma unroll
-    for (int v = 0; v < XV; ++v) {
-      const int idx = t + Q2_NT * v;
-      if (idx < Q2_SB * x4) {
-        const int rx = idx / x4;
-        *reinterpret_cast<float4*>(&L.x[rx * XL + (idx % x4) * 4]) =
-            (base + rx < rows && idx % x4 < xr4)
-                ? make_float4(xv[v][0], xv[v][1], xv[v][2], xv[v][3]) : z;
-      }
+  };
+  // pipelined staging step it < 8 of sub-block sb's MFMA loop: the next
+  // sub-block's rows / tiles staged from registers, the registers reloaded
+  // with the sub-block after it
+  // Branch-free, so the wait-count pass sees the same straight-line
+  // schedule every iteration: past the end a zero sub-block is staged into a
+  // free buffer and the last one is reloaded (both unused).
+  auto pipe = [&](int sb, int it) {
+    if constexpr (NOSTAGE) return;
+    const int ld = sb + 2 < Q2_NSB ? sb + 2 : Q2_NSB - 1;
+    if (it < 4) {
+      stage_row(sb + 1, it);
+      load_row(ld, it);
+    } else if (it == 4) {
+      stage_tiles(sb + 1);
+      load_tiles(ld);
     }
   };
 
-  prefetch(0);
-#pragma unroll 1
-  for (int sb = 0; sb < Q2_NSB; ++sb) {
-    stage(sb);
-    __syncthreads();
-    if (sb + 1 < Q2_NSB) prefetch(sb + 1);  // in flight during the MFMAs
+  constexpr int ndb = XL > 32 ? 2 : 1;  // 32-wide input blocks of dW1 (n_in <= XL)
+  const int64_t pc = p * d.C + c;   // this workgroup's partial index
+
+  // prologue: sub-block 0 staged, sub-block 1 in registers
 #pragma unroll
-    for (int r = 0; r < 16; ++r) A1[r] = 0.f;
-    // dh1: A = dz2[rows of half rh][o], B = W2[o][units of block ib]
-    const float* Ax = &L.dz[(32 * rh + li) * Q2_LDZ + lk];
-    const float* Bx = &L.w2[lk * Q2_QW + 32 * ib + li];
-    // dW2: A = dz2[r][o of this wave's block], B = h1[r][units]
-    const float* Aw = &L.dz[lk * Q2_LDZ + 64 * w + li];
-    const float* Bw = &L.h1[lk * Q2_QW + li];
-    // 32 steps, each: 4 k-steps of dh1 (8 o) + 1 k-step of dW2 (2 rows, 4 tiles)
-#pragma unroll 2
-    for (int it = 0; it < 32; ++it) {
-      float a[4], b[4], aw[2], bw[2];
+  for (int s = 0; s < 4; ++s) load_row(0, s);
+  load_tiles(0);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a[e] = Ax[8 * it + 2 * e];
-        b[e] = Bx[(8 * it + 2 * e) * Q2_QW];
+  for (int s = 0; s < 4; ++s) stage_row(0, s);
+  stage_tiles(0);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) load_row(1, s);
+  load_tiles(1);
+  __syncthreads();
+
+  // The two roles run separate loops (same barrier count: one per sub-block),
+  // so their register sets do not have to coexist.
+  f32x16 W1[2];  // dX waves: dW1 over the rows they finish (input blocks 0, 1)
+  if (role_dx) {
+    // W2 operand in registers, B[k = o][n = unit] of the 64 k-steps of this
+    // wave's K half (lane: o = 128 kh + 2 s + lk, unit 32 ib + li)
+    float wreg[64];
+#pragma unroll
+    for (int s = 0; s < 64; ++s)
+      wreg[s] = W2g[(128 * kh + 2 * s + lk) * Q2_H + i0 + 32 * ib + li];
+    // dh1 half-K partials of this and of the previous sub-block; dW1 over the
+    // rows this wave finishes (accumulator registers 8 kh .. 8 kh + 7 of
+    // every sub-block; the partner wave (kh ^ 1) finishes the others)
+    f32x16 acc, accp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) W1[0][r] = W1[1][r] = accp[r] = 0.f;
+    float z[8];
+#pragma unroll
+    for (int r2 = 0; r2 < 8; ++r2) z[r2] = 0.f;  // sub-block -1: nothing to add
+    // the masked dh1 of sub-block sb's rows this wave finishes: its own half-K
+    // partial (accp) and the partner's from LDS, o < 128 first (fixed order)
+    auto mask = [&](int sb) {
+      const int eb = sb & 1, tb = sb % 3;
+#pragma unroll
+      for (int r2 = 0; r2 < 8; ++r2) {
+        const int r = 8 * kh + r2;
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * lk;
+        const float o = L.ex[eb][((ib * 2 + (kh ^ 1)) * 8 + r2) * 64 + lane];
+        const float v = kh == 0 ? __fadd_rn(accp[r], o) : __fadd_rn(o, accp[r]);
+        z[r2] = L.h1[tb][rl * Q2_QW + 32 * ib + li] > 0.f ? v : 0.f;
+        acc_db1 += (double)z[r2];
       }
-      aw[0] = Aw[(2 * it) * Q2_LDZ];
-      aw[1] = Aw[(2 * it) * Q2_LDZ + 32];
-      bw[0] = Bw[(2 * it) * Q2_QW];
-      bw[1] = Bw[(2 * it) * Q2_QW + 32];
-      A1 = mfma(a[0], b[0], A1);
-      W2t[0][0] = mfma(aw[0], bw[0], W2t[0][0]);
-      A1 = mfma(a[1], b[1], A1);
-      W2t[0][1] = mfma(aw[0], bw[1], W2t[0][1]);
-      A1 = mfma(a[2], b[2], A1);
-      W2t[1][0] = mfma(aw[1], bw[0], W2t[1][0]);
-      A1 = mfma(a[3], b[3], A1);
-      W2t[1][1] = mfma(aw[1], bw[1], W2t[1][1]);
-    }
-    // ReLU mask -> dz1 (in registers), its column sum, and dW1 from it: MFMA
-    // k-step s pairs accumulator row (s, lk) with that row of x
-    float z[16];
+    };
+    // dW1 k-step r2 of sub-block sb: accumulator row (8 kh + r2, lk) x that row of x
+    auto w1step = [&](int sb, int r2) {
+      const int tb = sb % 3;
+      const int r = 8 * kh + r2;
+      const int rl = (r & 3) + 8 * (r >> 2) + 4 * lk;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rl = 32 * rh + (r & 3) + 8 * (r >> 2) + 4 * lk;
-      z[r] = L.h1[rl * Q2_QW + 32 * ib + li] > 0.f ? A1[r] : 0.f;
-      acc_db1 += (double)z[r];
-    }
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      if (db < ndb) {
-        const int dcol = 32 * db + li;
-        const bool okd = dcol < XL;
-        const int dc = okd ? dcol : 0;
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const int rl = 32 * rh + (s & 3) + 8 * (s >> 2) + 4 * lk;
-          const float xval = L.x[rl * XL + dc];
-          W1[db] = mfma(z[s], okd ? xval : 0.f, W1[db]);
+      for (int db = 0; db < 2; ++db) {
+        if (db < ndb) {
+          const int dcol = 32 * db + li;
+          const bool okd = dcol < XL;
+          const float xval = L.x[tb][rl * XL + (okd ? dcol : 0)];
+          W1[db] = mfma(z[r2], okd ? xval : 0.f, W1[db]);
         }
       }
+    };
+#pragma unroll 1
+    for (int sb = 0; sb < Q2_NSB; ++sb) {
+      const int cb = sb & 1;
+      if (sb > 0) mask(sb - 1);  // the previous sub-block's partials met at the barrier
+      // two independent accumulation chains (even / odd k-steps), summed at
+      // the end of the sub-block: more MFMA issue freedom beside the partner wave
+      f32x16 acc1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = acc1[r] = 0.f;
+      // dh1 half-K: A = dz2[row li][o = 128 kh + 2 s + lk], B = wreg[s]; the
+      // previous sub-block's dW1 k-steps ride along (independent accumulators)
+      const float* A = &L.dz[cb][li * Q2_LDZ + 128 * kh + lk];
+      // operand reads one step ahead of their MFMAs
+      float a[2][8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[0][e] = A[2 * e];
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        if (it + 1 < 8) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[(it + 1) & 1][e] = A[16 * (it + 1) + 2 * e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          acc = mfma(a[it & 1][e], wreg[8 * it + e], acc);
+          acc1 = mfma(a[it & 1][e + 1], wreg[8 * it + e + 1], acc1);
+        }
+        w1step(sb > 0 ? sb - 1 : 0, it);  // z = 0 at sb = 0: adds nothing
+        pipe(sb, it);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = __fadd_rn(acc[r], acc1[r]);
+      // the half of this partial the partner finishes, to LDS
+#pragma unroll
+      for (int r2 = 0; r2 < 8; ++r2)
+        L.ex[cb][((ib * 2 + kh) * 8 + r2) * 64 + lane] = acc[8 * (kh ^ 1) + r2];
+      accp = acc;
+      __syncthreads();  // sub-block sb + 1 staged; sb's half-K partials in LDS
     }
-    __syncthreads();  // the next stage overwrites dz2 / h1 / x
-  }
-
-  // ---- epilogue: partial of this 256-row block (index p)
-  const int64_t pc = p * d.C + c;
-  float* scr = L.dz;                                // dW1 of the rh = 1 waves
-  double* dscr = reinterpret_cast<double*>(L.w2);   // [4 waves][64] x {db2, dW3}
-  double* dscr1 = reinterpret_cast<double*>(L.h1);  // db1 of the rh = 1 waves
-  dscr[(w * 64 + lane) * 2 + 0] = acc_db2;
-  dscr[(w * 64 + lane) * 2 + 1] = acc_dw3;
-  if (lane == 0) dscr[512 + w] = acc_db3;
-  if (rh == 1) {
+    mask(Q2_NSB - 1);
 #pragma unroll
-    for (int db = 0; db < 2; ++db)
+    for (int it = 0; it < 8; ++it) w1step(Q2_NSB - 1, it);
+  } else {
+    f32x16 R[4];  // dW2 tiles R[2 ob + bb]: o block ob0 + 32 ob, unit block 32 bb
 #pragma unroll
-      for (int r = 0; r < 16; ++r) scr[((ib * 2 + db) * 16 + r) * 64 + lane] = W1[db][r];
-    dscr1[ib * 64 + lane] = acc_db1;
-  }
-  {
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) R[k][r] = 0.f;
+#pragma unroll 1
+    for (int sb = 0; sb < Q2_NSB; ++sb) {
+      const int cb = sb & 1;
+      // dW2[o block][quarter] += dz2[rows][o]^T h1[rows][quarter], K = 32 rows
+      const float* A = &L.dz[cb][lk * Q2_LDZ + ob0 + li];
+      const float* B = &L.h1[sb % 3][lk * Q2_QW + li];
+      // operand reads one step ahead of their MFMAs
+      float a[2][2][2], b[2][2][2];
+      auto rd = [&](int it, int buf) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          a[buf][e][0] = A[(4 * it + 2 * e) * Q2_LDZ];
+          a[buf][e][1] = A[(4 * it + 2 * e) * Q2_LDZ + 32];
+          b[buf][e][0] = B[(4 * it + 2 * e) * Q2_QW];
+          b[buf][e][1] = B[(4 * it + 2 * e) * Q2_QW + 32];
+        }
+      };
+      rd(0, 0);
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        if (it + 1 < 8) rd(it + 1, (it + 1) & 1);
+        const int u = it & 1;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          R[0] = mfma(a[u][e][0], b[u][e][0], R[0]);
+          R[1] = mfma(a[u][e][0], b[u][e][1], R[1]);
+          R[2] = mfma(a[u][e][1], b[u][e][0], R[2]);
+          R[3] = mfma(a[u][e][1], b[u][e][1], R[3]);
+        }
+        pipe(sb, it);
+      }
+      __syncthreads();  // sub-block sb + 1 staged
+    }
     float* dW2 = d.dW2 + pc * (Q2_H * Q2_H);
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob)
@@ -282,41 +345,59 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
       for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int o = 64 * w + 32 * ob + (r & 3) + 8 * (r >> 2) + 4 * lk;
-          dW2[o * Q2_H + i0 + 32 * bb + li] = W2t[ob][bb][r];
+          const int o = ob0 + 32 * ob + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          dW2[o * Q2_H + i0 + 32 * bb + li] = R[2 * ob + bb][r];
         }
   }
+
+  // ---- epilogue (after the loops' last barrier every LDS tile is free):
+  // dW1 / db1 halves of the two K-half waves summed kh 0 first; the head's and
+  // layer 2's bias / weight partials summed over the waves in order (fp64)
+  float* w1s = &L.dz[0][0];                                  // [ib][db][16][64]
+  double* db1s = reinterpret_cast<double*>(&L.dz[0][0] + 4096);  // [ib][64]
+  double* dscr = reinterpret_cast<double*>(&L.dz[1][0]);     // [8 waves][64] x 2
+  if (role_dx && kh == 1) {
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) w1s[((ib * 2 + db) * 16 + r) * 64 + lane] = W1[db][r];
+    db1s[ib * 64 + lane] = acc_db1;
+  }
+  dscr[(w * 64 + lane) * 2 + 0] = acc_db2;
+  dscr[(w * 64 + lane) * 2 + 1] = acc_dw3;
+  if (lane == 0) dscr[1024 + w] = acc_db3;
   __syncthreads();
-  if (rh == 0) {
+  if (role_dx && kh == 0) {
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
       if (db < ndb) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float v = W1[db][r] + scr[((ib * 2 + db) * 16 + r) * 64 + lane];
+          const float v = __fadd_rn(W1[db][r], w1s[((ib * 2 + db) * 16 + r) * 64 + lane]);
           const int i = 32 * ib + (r & 3) + 8 * (r >> 2) + 4 * lk;
           const int dcol = 32 * db + li;
           if (dcol < nin) d.dW1[(pc * Q2_H + i0 + i) * nin + dcol] = v;
         }
       }
     }
-    // column 32 ib + li: (rh 0 + rh 1) per row half, then the two halves
-    double s1 = acc_db1 + dscr1[ib * 64 + lane];
+    // column 32 ib + li: (kh 0 + kh 1) per row group, then the two row groups
+    double s1 = acc_db1 + db1s[ib * 64 + lane];
     s1 += __shfl_xor(s1, 32, 64);
     if (lk == 0) d.db1[pc * Q2_H + i0 + 32 * ib + li] = (float)s1;
   }
-  if (t < 64) {
+  if (t >= 256 && t < 320) {  // a dW2 wave: the column sums
+    const int tt = t - 256;
     double s2 = 0.0, s3 = 0.0;
-    for (int v = 0; v < 4; ++v) {
-      s2 += dscr[(v * 64 + t) * 2 + 0];
-      s3 += dscr[(v * 64 + t) * 2 + 1];
+    for (int v = 0; v < 8; ++v) {
+      s2 += dscr[(v * 64 + tt) * 2 + 0];
+      s3 += dscr[(v * 64 + tt) * 2 + 1];
     }
-    d.db2[pc * Q2_H + i0 + t] = (float)s2;
-    d.dW3[pc * Q2_H + i0 + t] = (float)s3;
-  } else if (t == 64 && q == 0) {
-    double s = 0.0;
-    for (int v = 0; v < 4; ++v) s += dscr[512 + v];
-    d.db3[pc] = (float)s;
+    d.db2[pc * Q2_H + i0 + tt] = (float)s2;
+    d.dW3[pc * Q2_H + i0 + tt] = (float)s3;
+  } else if (t == 320 && q == 0) {
+    double sg = 0.0;
+    for (int v = 0; v < 8; ++v) sg += dscr[1024 + v];
+    d.db3[pc] = (float)sg;
   }
 }
 
@@ -330,7 +411,7 @@ extern "C" int d3a_q2_bwd(const d3a_q2_bwd_desc* dp, void* stream) {
   const d3a_q2_bwd_desc& d = *dp;
   D3A_CHECK_ARG(d.x && d.h1 && d.h2 && d.g && d.W2 && d.w3, "d3a_q2_bwd: null input");
   D3A_CHECK_ARG(d.dW1 && d.db1 && d.dW2 && d.db2 && d.dW3 && d.db3, "d3a_q2_bwd: null output");
-  D3A_CHECK_ARG(d.n_in >= 1 && d.n_in <= Q2_XMAX, "d3a_q2_bwd: n_in must be 1..48");
+  D3A_CHECK_ARG(d.n_in >= 1 && d.n_in <= 48, "d3a_q2_bwd: n_in must be 1..48");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.n_scaled >= 0, "d3a_q2_bwd: bad sizes");
   // float4 loads of h1, x and W2 rows
   auto a16 = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; };
@@ -347,6 +428,15 @@ extern "C" int d3a_q2_bwd(const d3a_q2_bwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(blocks < (int64_t(1) << 31), "d3a_q2_bwd: too many rows");
   const int xl = (d.n_in + 3) & ~3;
   const dim3 grid((unsigned)blocks), block(Q2_NT);
+  static const bool probe = [] {
+    const char* e = getenv("D3A_Q2_PROBE");
+    return e && e[0] == '1';
+  }();
+  if (probe && xl <= 16) {
+    hipLaunchKernelGGL((q2_bwd_kernel<16, true>), grid, block, 0, (hipStream_t)stream, d);
+    D3A_LAUNCH_CHECK("d3a_q2_bwd");
+    return 0;
+  }
   if (xl <= 16)
     hipLaunchKernelGGL(q2_bwd_kernel<16>, grid, block, 0, (hipStream_t)stream, d);
   else if (xl <= 32)

@@ -265,18 +265,19 @@ def check_q_func(value: Union[QFunctionFactory, str]) -> QFunctionFactory:
     raise ValueError("This argument must be str or QFunctionFactory object.")
 
 
-def check_use_gpu(value) -> Optional[int]:
-    """argument_utility.py:103-114 — returns a device id or None.
-
-    The HIP engine runs on a GPU only; ``use_gpu=False`` is accepted for
-    API compatibility and maps to device 0 (there is no CPU compute path).
-    """
-    if isinstance(value, bool):
-        return 0
-    if isinstance(value, int):
+def check_use_gpu(value):
+    """argument_utility.py:96-114: True -> Device(0), int -> Device(int),
+    a Device as is, False / None -> None (the reference's CPU).  The HIP
+    engine has no CPU path: an Impl built with None raises
+    NotImplementedError (algos/impl_base.py)."""
+    from .gpu import Device
+    # isinstance cannot tell bool from int
+    if type(value) == bool:
+        return Device(0) if value else None
+    if type(value) == int:
+        return Device(value)
+    if isinstance(value, Device):
         return value
     if value is None:
-        return 0
-    if hasattr(value, "get_id"):
-        return int(value.get_id())
+        return None
     raise ValueError("This argument must be bool, int or Device.")

@@ -41,6 +41,16 @@ CASES = {
     # K4 shapes (antmaze obs 29 / act 8, 256 rows per GPU): Q-input rows of
     # 37 floats padded to 40, 8-wide tanh-Gaussian sample / log-prob
     "k4_antmaze": dict(D=29, A=8, hidden=[256, 256], N=10, B=256),
+    # one hidden layer at a large critic pass (7,936 rows x 2): the first
+    # layer's weight gradient must not depend on a second trunk layer
+    # (one step: on later steps of this seed a hidden unit's pre-activation
+    # sits within rounding of 0 and the two fp32 paths take different ReLU
+    # branches -- the tie the fp64 arbiters resolve)
+    "one_hidden": dict(D=11, A=3, hidden=[256], N=10, B=256, steps=1),
+    # n_critics x batch beyond the loss kernel's register slots (10 x 1,024 >
+    # 8,192): the strided-load instantiation of d3a_cql_loss (two steps: at the
+    # third, two of the ten critics tie in the actor's min over the ensemble)
+    "wide_ensemble": dict(D=5, A=2, hidden=[64, 64], N=2, B=1024, C=10, steps=2),
 }
 
 
@@ -109,11 +119,12 @@ def test_cql_update_parity(case):
     batch and noise."""
     cfg = CASES[case]
     D, A, H, N, B = cfg["D"], cfg["A"], cfg["hidden"], cfg["N"], cfg["B"]
-    orc = make_oracle(D, A, H, N, seed=11)
-    impl = make_impl(D, A, H, N)
+    C = cfg.get("C", 2)
+    orc = make_oracle(D, A, H, N, C=C, seed=11)
+    impl = make_impl(D, A, H, N, C=C)
     rs = np.random.RandomState(0)
     gen = torch.Generator().manual_seed(1)
-    for step in range(3):
+    for step in range(cfg.get("steps", 3)):
         impl.set_state_dict(oracle_state(orc))
         arrs = make_batch(rs, B, D, A)
         if cfg.get("nstep"):

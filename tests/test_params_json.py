@@ -84,9 +84,17 @@ def test_reference_params_json_configures_the_algo(tmp_path):
     np.testing.assert_array_equal(np.asarray(algo.scaler._std).reshape(-1), [1.0, 2.0, 0.25])
 
 
-def test_params_json_rejects_another_algorithm(tmp_path):
-    with pytest.raises(ValueError):
-        TD3PlusBC.params_from_json(_write(tmp_path, REFERENCE_CQL_PARAMS))
+def test_params_json_of_a_related_class_loads(tmp_path):
+    """The reference's from_json passes the remaining keys through **kwargs
+    without checking ``algorithm`` (base.py:216-232): a params.json written
+    for one class configures a subclass too."""
+    class MyCQL(CQL):
+        pass
+
+    shape, asize, kw = MyCQL.params_from_json(_write(tmp_path, REFERENCE_CQL_PARAMS))
+    assert "algorithm" not in kw and shape == (3,)
+    algo = MyCQL(**kw)
+    assert algo._conservative_weight == 10.0
 
 
 def test_save_params_writes_the_reference_schema(tmp_path):

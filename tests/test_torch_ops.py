@@ -22,12 +22,49 @@ SCHEMAS = {
 }
 
 
+# the §8(b) loss / sampling / backward ops (reference call sites in
+# csrc/torch_ops.cpp): every one has a HIP and a Meta kernel
+OPS_8B = ("linear_backward", "mlp_backward", "logsumexp", "logsumexp_backward", "td_mse_loss",
+          "td_mse_loss_backward", "quantile_huber_loss", "quantile_huber_loss_backward",
+          "iqn_cos_embed", "iqn_cos_embed_backward", "squashed_gaussian_sample",
+          "squashed_gaussian_sample_backward")
+
+
 def test_ops_registered_with_schemas():
     ops = torch_ops.load()
     for name, schema in SCHEMAS.items():
         assert str(getattr(ops, name).default._schema) == schema
-    for name in ("adam_step_", "gather_batch"):
-        assert hasattr(ops, name)
+    for name in ("adam_step_", "gather_batch") + OPS_8B:
+        assert hasattr(ops, name), name
+        assert torch._C._dispatch_has_kernel_for_dispatch_key(f"d3rlpy_amd::{name}", "CUDA")
+        assert torch._C._dispatch_has_kernel_for_dispatch_key(f"d3rlpy_amd::{name}", "Meta")
+
+
+def test_meta_shapes_of_loss_and_backward_ops():
+    ops = torch_ops.load()
+    m = lambda *s: torch.empty(*s, device="meta")  # noqa: E731
+    dx, dW, db = ops.linear_backward(m(2, 9, 256), m(9, 14), m(2, 256, 14), m(2, 9, 256))
+    assert (dx.shape, dW.shape, db.shape) == ((2, 9, 14), (2, 256, 14), (2, 256))
+    out = ops.mlp_backward(m(9, 1), m(9, 14), [m(256, 14), m(256, 256), m(1, 256)],
+                           [m(9, 256), m(9, 256)])
+    assert [tuple(t.shape) for t in out] == [(9, 14), (256, 14), (256, 256), (1, 256), (256,),
+                                             (256,), (1,)]
+    assert ops.logsumexp(m(2, 32, 30)).shape == (2, 32)
+    assert ops.logsumexp_backward(m(2, 32), m(2, 32, 30), m(2, 32)).shape == (2, 32, 30)
+    loss, diff = ops.td_mse_loss(m(2, 32), m(32), m(2, 32), m(32), m(32))
+    assert loss.shape == (2,) and diff.shape == (2, 32)
+    assert ops.td_mse_loss_backward(m(2), m(2, 32)).shape == (2, 32)
+    assert ops.quantile_huber_loss(m(8, 200), m(8, 200), m(8, 200)).shape == (8,)
+    assert ops.quantile_huber_loss_backward(m(8), m(8, 200), m(8, 200), m(8, 200)).shape == \
+        (8, 200)
+    assert ops.iqn_cos_embed(m(8, 64), m(3136, 64), m(3136)).shape == (512, 3136)
+    dW, db = ops.iqn_cos_embed_backward(m(512, 3136), m(8, 64), m(512, 3136), m(3136, 64))
+    assert dW.shape == (3136, 64) and db.shape == (3136,)
+    a, lp = ops.squashed_gaussian_sample(m(16, 3), m(16, 3), m(16, 3), -20.0, 2.0)
+    assert a.shape == (16, 3) and lp.shape == (16, 1)
+    dmu, dls = ops.squashed_gaussian_sample_backward(m(16, 3), m(16, 1), m(16, 3), m(16, 3),
+                                                     m(16, 3), -20.0, 2.0)
+    assert dmu.shape == dls.shape == (16, 3)
 
 
 def test_meta_shapes():

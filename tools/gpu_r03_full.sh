@@ -1,0 +1,12 @@
+# Full GPU suite + K2 bench line + K2 kernel trace (breakdown, timeline).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd $R && mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/full_tests.log 2>&1; rc=$?
+timeout -k 10 200 python bench.py --steps 2000 --no-cpu-baseline > gpurun_out/full_bench_cql.log 2>&1 || exit $?
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/full_prof -o k2 --output-format csv -- python3 bench.py --steps 300 --warmup 20 --no-cpu-baseline --transitions 200000 > gpurun_out/full_prof.log 2>&1 || exit $?
+f=$(find gpurun_out/full_prof -name '*kernel_trace.csv' -print -quit)
+python tools/prof_by_shape.py "$f" 320 > gpurun_out/full_breakdown.txt 2>&1 || true
+python tools/prof_timeline.py "$f" > gpurun_out/full_timeline.txt 2>&1 || true
+exit $rc
