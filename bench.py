@@ -89,21 +89,42 @@ def launch_ranks(n: int, argv, timeout: float = None) -> int:
     return rc
 
 
-def _dist_setup(backend: str = "nccl"):
+def _watchdog(seconds: float, what: str):
+    """Exit this process with status 75 unless the returned event is set
+    within ``seconds`` -- a rendezvous, RCCL initialisation or first graph
+    capture that hangs (a rank that never joins, a wedged communicator) ends
+    the job in bounded time with a non-zero status instead of at the driver's
+    limit.  (os._exit: no exec, no cleanup that could block on the hung call.)"""
+    import threading
+    ev = threading.Event()
+
+    def run():
+        if not ev.wait(seconds):
+            sys.stderr.write(f"bench: {what} did not finish within {seconds:.0f}s; exiting 75\n")
+            sys.stderr.flush()
+            os._exit(75)
+    if seconds and seconds > 0:
+        threading.Thread(target=run, daemon=True).start()
+    return ev
+
+
+def _dist_setup(backend: str = "nccl", timeout_s: float = 300.0):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import datetime
+    tmo = datetime.timedelta(seconds=max(1.0, timeout_s))
     if backend == "gloo":  # launcher self-test: CPU only
         import torch.distributed as dist
         if ws > 1:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
         return ws, rank, local
     import torch
     if ws > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), timeout=tmo)
     else:
         torch.cuda.set_device(0)
     return ws, rank, local
@@ -219,6 +240,58 @@ def measure_kernel(ws_obj, reps: int = 50):
     torch.cuda.synchronize()
     avg_s = e0.elapsed_time(e1) / 1e3 / reps
     return avg_s, flops, desc
+
+
+def _record_all_reduces(algo):
+    """For a data-parallel impl: a list that collects (numel, dtype, device)
+    of every all-reduce the update pipeline issues (recorded while the first
+    update runs eagerly, before the graph capture), else None."""
+    dp = getattr(algo.impl, "_dp", None)
+    if dp is None:
+        return None
+    log = {"calls": [], "armed": True}
+    inner = dp.all_reduce_sum
+
+    def rec(t):
+        if log["armed"]:
+            log["calls"].append((t.numel(), t.dtype, t.device))
+        inner(t)
+    dp.all_reduce_sum = rec
+    return log
+
+
+def measure_all_reduces(log, ws: int, reps: int = 200) -> dict:
+    """The exchange of one data-parallel step measured on its own: the same
+    all-reduces (sizes, dtypes, order) on scratch tensors of the recorded
+    shapes, ``reps`` steps bracketed by HIP events on the current stream
+    (RCCL runs on it), max over ranks.  Reported beside the step time as
+    "allreduce": calls and bytes per step, microseconds per step."""
+    import torch
+    import torch.distributed as dist
+    step = log["calls"]  # recorded over exactly one (eager) update
+    bufs = [torch.zeros(m, dtype=dt, device=dev) for m, dt, dev in step]
+    nbytes = sum(b.numel() * b.element_size() for b in bufs)
+    if ws == 1 or not step:
+        return {"calls_per_step": len(step), "bytes_per_step": nbytes, "us_per_step": 0.0}
+    for _ in range(5):
+        for b in bufs:
+            dist.all_reduce(b)
+    torch.cuda.synchronize()
+    dist.barrier()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        for b in bufs:
+            dist.all_reduce(b)
+    e1.record(s)
+    torch.cuda.synchronize()
+    us = _max_over_ranks(e0.elapsed_time(e1) * 1e3 / reps, ws)
+    return {"calls_per_step": len(step), "bytes_per_step": nbytes, "us_per_step": round(us, 2),
+            "busbw_GBps": round(2 * (ws - 1) / ws * nbytes / (us * 1e-6) / 1e9, 2),
+            "method": f"the step's {len(step)} RCCL SUM all-reduces replayed eagerly on "
+                      f"scratch buffers of the same sizes, {reps} steps, HIP events, max over "
+                      "ranks (in the update they are captured in its graph)"}
 
 
 def cpu_step_fn(name: str = "cql"):
@@ -342,7 +415,12 @@ def _selftest(args) -> None:
     the step (tests/test_bench_launcher.py): rendezvous, barrier-bracketed
     timing, max over ranks, rank-0 line with the whole-job value; for
     ``cqldp`` each rank also reports its shard of the global index stream."""
-    ws, rank, _ = _dist_setup("gloo")
+    wd = _watchdog(args.init_timeout, "rendezvous")
+    hang = os.environ.get("D3A_SELFTEST_HANG_RANK")
+    if hang is not None and int(hang) == int(os.environ.get("RANK", "0")):
+        time.sleep(3600)  # a rank that never joins the rendezvous
+    ws, rank, _ = _dist_setup("gloo", args.init_timeout)
+    wd.set()
     shape, batch, _ = WORKLOADS[args.algo]
     dp = args.algo == "cqldp"
     rs = np.random.RandomState(1000)
@@ -403,6 +481,9 @@ def main():
                          "process's CPU share)")
     ap.add_argument("--selftest-gloo", action="store_true",
                     help="launcher self-test without a GPU: gloo ranks, a host stand-in step")
+    ap.add_argument("--init-timeout", type=float, default=300.0,
+                    help="seconds allowed for the rendezvous, RCCL initialisation and the "
+                         "warm-up (first graph capture); past it the rank exits with status 75")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary of the dominant kernel (tools/pmc_pass.sh); default "
                          "profiles/r01_pmc_traffic_<algo>.json")
@@ -418,15 +499,21 @@ def main():
     if args.precision == "sbf16x6":
         from d3rlpy_amd import ops as _ops
         _ops.set_sbf16(6)
-    ws, rank, local = _dist_setup()
+    wd = _watchdog(args.init_timeout, "rendezvous / RCCL init / warm-up with graph capture")
+    ws, rank, local = _dist_setup("nccl", args.init_timeout)
     if ws != args.gpus:
         print(f"bench: WORLD_SIZE={ws} but --gpus {args.gpus}; reporting n_gpus={ws}",
               file=sys.stderr)
     algo, it = build_workload(rank, args.transitions, args.algo, ws)
+    ar_log = _record_all_reduces(algo)
 
-    gpu_steps(algo, it, args.warmup)
+    gpu_steps(algo, it, 1)  # eager first update: its all-reduces are recorded
+    if ar_log is not None:
+        ar_log["armed"] = False
+    gpu_steps(algo, it, max(0, args.warmup - 1))
     torch.cuda.synchronize()
     _barrier(ws)
+    wd.set()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     gpu_steps(algo, it, args.steps)
@@ -443,6 +530,7 @@ def main():
 
     wsp = next(iter(algo.impl._ws.values()))
     kern_s, kflops, kdesc = measure_kernel(wsp)
+    allreduce = measure_all_reduces(ar_log, ws) if ar_log is not None else None
     if rank != 0:
         if ws > 1:
             import torch.distributed as dist
@@ -539,6 +627,9 @@ def main():
                      "avg_launch_us": round(kern_s * 1e6, 3)},
         "cpu_baseline": cpu,
     }
+    if allreduce is not None:
+        allreduce["frac_of_step"] = round(allreduce["us_per_step"] / (1e3 * out["ms_per_step"]), 4)
+        out["allreduce"] = allreduce
     if cpu is not None:
         out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
     print(json.dumps(out))

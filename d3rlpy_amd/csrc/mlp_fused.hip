@@ -25,6 +25,9 @@
 #include "../../include/d3rlpy_amd.h"
 
 namespace d3a {
+// q2_fwd.hip: the register-resident instantiation for [n_in, 256, 256, 1]
+bool q2_fwd_launch(const d3a_mlp_fwd_desc& d, hipStream_t st);
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -327,6 +330,17 @@ extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
   // K2 critic pass, 2 x 15616 rows; 32 (two workgroups per CU) otherwise --
   // 164.9 us against 173.5 (128) / 194.9 (64) on the K3 200-quantile target
   // pass, 2 x 25600 rows, and more workgroups for the 100-2560-row passes
+  // [n_in <= 48, 256, 256, 1] over >= 8,192 member-rows: W1 in registers,
+  // sub-block pipelined (q2_fwd.hip); block_rows > 0 forces the generic kernel
+  static const bool q2_on = [] {
+    const char* e = getenv("D3A_FWD_Q2");
+    return !(e && e[0] == '0');
+  }();
+  if (q2_on && d.block_rows == 0 && (d.rows + d.aux_rows) * d.C >= 8192 &&
+      q2_fwd_launch(d, (hipStream_t)stream)) {
+    D3A_LAUNCH_CHECK("d3a_mlp_fwd");
+    return 0;
+  }
   const int bm = d.block_rows > 0
                      ? d.block_rows
                      : (d.n_out <= 64 && d.rows * d.C >= 16384 ? 128 : 32);

@@ -77,3 +77,16 @@ def test_dp_seeds_gloo():
     assert r0["own"] != r1["own"]
     assert r0["shared"] == r1["shared"] == r0["own"]
     assert r0["key"] != r1["key"]
+
+
+def test_bench_hung_rank_exits_in_bounded_time():
+    """A rank that never reaches the rendezvous: the others' watchdog ends the
+    job with a non-zero status (75) well before any driver limit."""
+    import time
+    t0 = time.monotonic()
+    r = _bench("--gpus", "2", "--selftest-gloo", "--steps", "5", "--warmup", "1",
+               "--init-timeout", "8", env={"D3A_SELFTEST_HANG_RANK": "1"})
+    el = time.monotonic() - t0
+    assert r.returncode != 0
+    assert el < 120, el
+    assert "did not finish within" in r.stderr

@@ -1,0 +1,95 @@
+"""Microbenchmark of d3a_mlp_fwd on the K2 CQL critic-forward shape: 2 members
+x (15,616 Q rows, activations kept for rows >= 7,680, + 256 target rows as the
+aux pass) x 14 -> 256 -> 256 -> 1.  Average launch time by HIP events on the
+launching stream and the fp32 MFMA fraction of the 4.41 GFLOP it performs.
+Used for A/B runs of the kernel and its rocprofv3 PMC passes."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from d3rlpy_amd import _native as N  # noqa: E402
+from d3rlpy_amd import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=15616)
+    ap.add_argument("--h-from", type=int, default=7680)
+    ap.add_argument("--aux", type=int, default=256)
+    ap.add_argument("--n-in", type=int, default=14)
+    ap.add_argument("--bm", type=int, default=0)
+    ap.add_argument("--reps", type=int, default=200)
+    a = ap.parse_args()
+    dev, C, H = "cuda", 2, 256
+    sizes = [a.n_in, H, H, 1]
+    ldx = (a.n_in + 3) // 4 * 4
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(a.rows, ldx, device=dev, generator=g)
+    xa = torch.randn(max(a.aux, 1), ldx, device=dev, generator=g)
+    # parameters: one buffer per store, [W0 b0 W1 b1 W2 b2] per member-major layer
+    n_par = sum(C * (sizes[l] * sizes[l + 1] + sizes[l + 1]) for l in range(3))
+    n_par = (n_par + 3) // 4 * 4
+    store = torch.randn(2 * n_par, device=dev, generator=g) * 0.06
+    offs, o = [], 0
+    for l in range(3):
+        w = o
+        o += C * sizes[l] * sizes[l + 1]
+        o = (o + 3) // 4 * 4
+        b = o
+        o += C * sizes[l + 1]
+        o = (o + 3) // 4 * 4
+        offs.append((w, b))
+    h = [torch.zeros(C, a.rows, H, device=dev) for _ in range(2)]
+    out = torch.zeros(C, a.rows, device=dev)
+    aout = torch.zeros(C, max(a.aux, 1), device=dev)
+    d = N.MlpFwdDesc()
+    d.block_rows = a.bm
+    d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
+    d.n_in, d.n_hidden, d.H, d.n_out = a.n_in, 2, H, 1
+    for l in range(3):
+        d.W[l] = store.data_ptr() + 4 * offs[l][0]
+        d.b[l] = store.data_ptr() + 4 * offs[l][1]
+        d.sW[l], d.sb[l] = sizes[l + 1] * sizes[l], sizes[l + 1]
+    for l in range(2):
+        d.h[l] = h[l].data_ptr()
+    d.sh = a.rows * H
+    d.out, d.sout, d.ldout = out.data_ptr(), a.rows, 1
+    d.r0, d.rows, d.C, d.h_from = 0, a.rows, C, a.h_from
+    if a.aux:
+        d.aux_x, d.aux_ldx, d.aux_sxb, d.aux_wdelta = xa.data_ptr(), ldx, 0, n_par
+        d.aux_out, d.aux_sout, d.aux_rows = aout.data_ptr(), a.aux, a.aux
+    for _ in range(5):
+        ops.call_desc("d3a_mlp_fwd", d)
+    torch.cuda.synchronize()
+    # check against torch fp32 on a row sample
+    W = [store[offs[l][0]:offs[l][0] + C * sizes[l] * sizes[l + 1]].view(C, sizes[l + 1], sizes[l])
+         for l in range(3)]
+    bb = [store[offs[l][1]:offs[l][1] + C * sizes[l + 1]].view(C, 1, sizes[l + 1]) for l in range(3)]
+    xs = x[:, :a.n_in]
+    r1 = torch.relu(xs @ W[0].transpose(1, 2) + bb[0])
+    r2 = torch.relu(r1 @ W[1].transpose(1, 2) + bb[1])
+    q = (r2 @ W[2].transpose(1, 2) + bb[2]).squeeze(-1)
+    err = ((q - out).abs().max() / q.abs().max()).item()
+    herr = ((r2[:, a.h_from:] - h[1][:, a.h_from:]).abs().max()).item()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(a.reps):
+        ops.call_desc("d3a_mlp_fwd", d)
+    e1.record(s)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / a.reps
+    flops = 2 * C * (a.rows + a.aux) * sum(sizes[l] * sizes[l + 1] for l in range(3))
+    print(json.dumps({"kernel": "d3a_mlp_fwd", "rows": a.rows, "aux": a.aux, "bm": a.bm,
+                      "variant": os.environ.get("D3A_FWD_PROBE", "") + ("generic" if os.environ.get("D3A_FWD_Q2") == "0" else ""),
+                      "avg_us": round(us, 2), "tflops": round(flops / us / 1e6, 2),
+                      "frac_fp32_peak": round(flops / us / 1e6 / 157.3, 4),
+                      "max_rel_err_q": err, "max_abs_err_h2": herr}))
+
+
+if __name__ == "__main__":
+    main()

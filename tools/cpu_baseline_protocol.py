@@ -13,6 +13,12 @@ then `--steps` (1000) timed with time.perf_counter, median of `--runs` (5):
     the protocol fits one bounded call).
 Writes one JSON file with both medians, every run and the host description;
 bench.py reports it next to its live bounded sample.
+
+``--threads N`` sets the all-cores leg's thread count (default: the host's
+physical core count, BASELINE.md:27-28 -- on the GPU box that is more threads
+than the 16-CPU share a one-GPU tenant is given, which the file records);
+``--sweep 1,16,64,128`` adds a bounded sample (``--sweep-seconds`` each) at
+every listed thread count.
 """
 import argparse
 import json
@@ -39,6 +45,36 @@ def timed_run(algo: str, threads: int, steps: int, warmup: int) -> float:
     return steps / (time.perf_counter() - t0)
 
 
+def physical_cores() -> int:
+    """Distinct (physical id, core id) pairs of /proc/cpuinfo (lscpu's
+    Core(s) per socket x Socket(s)); the logical count if unreadable."""
+    pairs, phys, core = set(), None, None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":", 1)[1].strip()
+                elif not line.strip():
+                    if phys is not None and core is not None:
+                        pairs.add((phys, core))
+                    phys = core = None
+    except OSError:
+        pass
+    return len(pairs) or os.cpu_count()
+
+
+def sweep(algo: str, threads, seconds: float) -> list:
+    import bench
+    out = []
+    for n in threads:
+        sps, k, el = bench.cpu_baseline(seconds, n, algo)
+        out.append({"threads": n, "steps_per_s": sps, "steps": k, "seconds": el})
+        print(f"sweep {n} threads: {sps:.3f} steps/s ({k} steps in {el:.1f}s)", flush=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--algo", default="cql")
@@ -46,6 +82,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--runs", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--threads", type=int, default=None,
+                    help="all-cores leg thread count (default: physical cores)")
+    ap.add_argument("--sweep", default="", help="comma-separated thread counts")
+    ap.add_argument("--sweep-seconds", type=float, default=10.0)
     ap.add_argument("--single-on-core", type=int, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.single_on_core is not None:
@@ -54,10 +94,13 @@ def main():
         return
     import bench
     host = bench.host_cpu()
-    print(f"host {host}", flush=True)
+    host["physical_cores"] = physical_cores()
+    n_all = args.threads or host["physical_cores"]
+    print(f"host {host}; all-cores leg {n_all} threads", flush=True)
+    sw = sweep(args.algo, [int(v) for v in args.sweep.split(",") if v], args.sweep_seconds)
     allc = []
     for r in range(args.runs):
-        allc.append(timed_run(args.algo, host["threads"], args.steps, args.warmup))
+        allc.append(timed_run(args.algo, n_all, args.steps, args.warmup))
         print(f"all cores run {r}: {allc[-1]:.3f} steps/s", flush=True)
     cores = sorted(os.sched_getaffinity(0))
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--algo", args.algo,
@@ -73,8 +116,11 @@ def main():
     print(f"1-thread runs: {[round(v, 3) for v in one]}", flush=True)
     res = {"algo": args.algo, "unit": "gradient-steps/s", "steps": args.steps,
            "warmup": args.warmup, "runs": args.runs,
-           "all_cores": {"threads": host["threads"], "median": statistics.median(allc),
-                         "runs": allc},
+           "all_cores": {"threads": n_all, "median": statistics.median(allc), "runs": allc,
+                         "note": ("physical cores of the host (BASELINE.md:27-28)"
+                                  if n_all == host["physical_cores"] else
+                                  f"{n_all} threads (--threads)")},
+           "thread_sweep": sw,
            "one_thread": {"threads": 1, "median": statistics.median(one), "runs": one,
                           "note": "runs concurrent, pinned to distinct cores"},
            "host": host}
