@@ -472,10 +472,12 @@ def main():
     ap.add_argument("--algo", choices=sorted(WORKLOADS), default="cql",
                     help="cql = the BASELINE.json headline (K2); td3bc = K1 shapes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", choices=["fp32", "sbf16x6"], default="fp32",
-                    help="sbf16x6: the large input-gradient GEMMs on the bf16 matrix cores "
-                         "with hi/mid/lo split operands (fp32-accurate; a separate line, "
-                         "never the headline)")
+    ap.add_argument("--precision", choices=["fp32", "bf16", "sbf16x6"], default="fp32",
+                    help="bf16: the critic-ensemble forward / backward (the 7,936 + 7,680-row "
+                         "critic pass) with bf16 operands and fp32 accumulation "
+                         "(d3a_q2_fwd_bf16 / d3a_q2_bwd_bf16), a throughput line, never the "
+                         "headline; sbf16x6: the large input-gradient GEMMs on the bf16 "
+                         "matrix cores with hi/mid/lo split operands (fp32-accurate)")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="host threads of the all-cores CPU baseline (default: this "
                          "process's CPU share)")
@@ -496,6 +498,9 @@ def main():
 
     import torch
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if args.precision == "bf16":
+        from d3rlpy_amd import ops as _ops
+        _ops.set_critic_precision("bf16")
     if args.precision == "sbf16x6":
         from d3rlpy_amd import ops as _ops
         _ops.set_sbf16(6)
@@ -537,7 +542,9 @@ def main():
             dist.destroy_process_group()
         return
 
-    peak_tflops = 157.3  # MI355X FP32 MFMA dense peak (MI355X_MICROARCH.md)
+    # MI355X dense MFMA peaks (MI355X_MICROARCH.md): fp32-input 157.3 TF; bf16
+    # 2.5 PF (the bf16 line's dominant kernel runs on the bf16 matrix cores)
+    peak_tflops = 2500.0 if args.precision == "bf16" else 157.3
     achieved = kflops / kern_s / 1e12
     traffic = None
     if args.traffic_json is None:
@@ -611,6 +618,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32" if args.precision == "fp32" else
+                 "bf16 (critic-ensemble GEMM operands; fp32 accumulation, losses, optimiser)"
+                 if args.precision == "bf16" else
                  "fp32 (input-gradient GEMMs: split-bf16 x6 on bf16 MFMA)",
         "data": (f"synthetic (D4RL {shape} shapes, {args.transitions} transitions, "
                  "HBM-resident)" if shape != "atari" else

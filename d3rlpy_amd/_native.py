@@ -475,6 +475,8 @@ _SIGNATURES = {
     "d3a_bcq_actor_head": (C.c_int, [C.POINTER(BcqActorDesc), vp]),
     "d3a_mlp_bwd": (C.c_int, [C.POINTER(MlpBwdDesc), vp]),
     "d3a_q2_bwd": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
+    "d3a_q2_fwd_bf16": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
+    "d3a_q2_bwd_bf16": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
     "d3a_td3_prep": (C.c_int, [C.POINTER(Td3PrepDesc), vp]),
     "d3a_td3_target": (C.c_int, [C.POINTER(Td3TargetDesc), vp]),
     "d3a_td3_critic_loss": (C.c_int, [C.POINTER(Td3CriticLossDesc), vp]),

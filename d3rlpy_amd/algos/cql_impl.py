@@ -451,7 +451,12 @@ class _Workspace:
         self.actor_logp = z(B)
         self.logp_targ = z(B)
         # critic / target / actor-critic activations
-        self.qacts = mlp.Acts.alloc(impl.critic, self.R, dev)
+        # bf16 throughput line (ops.CRITIC_PRECISION): the critic pass's kept
+        # activations in bf16 select the bf16 forward / backward kernels
+        bf16 = (ops.CRITIC_PRECISION == "bf16" and mlp.q2_shape(impl.critic)
+                and mlp.q2_ok(impl.critic, 3 * NB + B))
+        self.qacts = mlp.Acts.alloc(impl.critic, self.R, dev,
+                                    dtype=torch.bfloat16 if bf16 else torch.float32)
         self.tacts = mlp.Acts.alloc(impl.critic, B, dev)
         self.aacts = mlp.Acts.alloc(impl.critic, B, dev)
         self.dq = z(C, self.R)

@@ -27,6 +27,8 @@
 namespace d3a {
 // q2_fwd.hip: the register-resident instantiation for [n_in, 256, 256, 1]
 bool q2_fwd_launch(const d3a_mlp_fwd_desc& d, hipStream_t st);
+// mlp_small.hip: 16-row workgroups for small passes (block_rows == 16)
+bool mlp_small_launch(const d3a_mlp_fwd_desc& d, hipStream_t st);
 
 namespace {
 
@@ -341,11 +343,18 @@ extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
     D3A_LAUNCH_CHECK("d3a_mlp_fwd");
     return 0;
   }
+  if (d.block_rows == 16) {
+    D3A_CHECK_ARG(mlp_small_launch(d, (hipStream_t)stream),
+                  "d3a_mlp_fwd: block_rows 16 needs H == 256, n_in <= 256, n_out <= 64 and "
+                  "16-byte aligned W[1..], biases and activation rows");
+    D3A_LAUNCH_CHECK("d3a_mlp_fwd");
+    return 0;
+  }
   const int bm = d.block_rows > 0
                      ? d.block_rows
                      : (d.n_out <= 64 && d.rows * d.C >= 16384 ? 128 : 32);
   D3A_CHECK_ARG(bm == 32 || bm == 64 || bm == 128,
-                "d3a_mlp_fwd: block_rows must be 0, 32, 64 or 128");
+                "d3a_mlp_fwd: block_rows must be 0, 16, 32, 64 or 128");
   dim3 grid((unsigned)((d.rows + bm - 1) / bm + (d.aux_rows + bm - 1) / bm), 1, (unsigned)d.C);
   hipStream_t st = (hipStream_t)stream;
   if (bm == 128)

@@ -1,0 +1,264 @@
+// Whole-MLP forward for small row passes (hundreds of rows): 16-row
+// workgroups on v_mfma_f32_16x16x4_f32.
+//
+// The d3a_mlp_fwd instantiation selected with block_rows = 16 for the
+// latency-bound passes of the hot path -- the policy over [obs; next_obs]
+// (512 rows, VectorEncoder 256-256 + mu | logstd head: encoders.py:265-275,
+// policies.py:170-176), TD3+BC / BCQ policies and targets at 100-256 rows.
+// Those passes do ~35 MFLOP per 256x256 layer: as per-layer launches each pays
+// a dependent-kernel boundary, and the 32-row fused workgroup puts 4.2 MFLOP
+// per layer on one CU.  Here a workgroup owns 16 rows (the smallest MFMA
+// tile), so a 512-row pass spreads over 32 CUs and every layer's chain is
+// half as long, and the whole MLP is one launch.
+//
+// Eight waves, wave w owning hidden units 32 w .. 32 w + 31 (two 16-unit
+// tiles, two independent accumulation chains).  The MFMAs compute the
+// transposed tile C^T[unit][row] = W[unit] . act[row] (W the A operand, read
+// from global/L2 with every load of the layer issued up front; activation
+// rows the B operand, from LDS), so a lane holds one row and four consecutive
+// units: 16-byte stores to LDS and to the kept activations.  k order: group g
+// of 16 k, lane group q = lane >> 4 supplying k = 16 g + 4 q + i to MFMA i
+// (the same permutation on both operands: an exact fp32 chain, deterministic).
+// The head (n_out <= 64 columns) reads the last layer from LDS: four threads
+// per (row, column) dot, then a fixed butterfly.
+#include <cstdlib>
+#include "common.hpp"
+#include "../../include/d3rlpy_amd.h"
+
+namespace d3a {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int S_RB = 16;    // rows per workgroup
+constexpr int S_H = 256;    // hidden width
+constexpr int S_LDK = 260;  // activation row stride in LDS
+constexpr int S_JMAX = 64;
+
+struct SmallLds {
+  float x[S_RB * S_LDK];     // input rows (zero-padded to a multiple of 16)
+  float h[2][S_RB * S_LDK];  // hidden activations, ping-pong
+  float wh[S_JMAX * S_H];    // head weights
+};
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// NL: hidden layers (compile time: the layer loop unrolls, so the registers
+// of the prefetched weights are allocated statically)
+// PROBE (timing probes only, D3A_SMALL_PROBE): bit 0 skips the 256-wide
+// layers' MFMAs, bit 1 the head
+template <int NL, int PROBE = 0>
+__global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
+  __shared__ __attribute__((aligned(16))) SmallLds S;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lr = lane & 15, lq = lane >> 4;
+  const int c = blockIdx.z;
+  const int nb_main = (int)((d.rows + S_RB - 1) / S_RB);
+  const bool aux = (int)blockIdx.x >= nb_main;
+  const int m0 = aux ? ((int)blockIdx.x - nb_main) * S_RB : (int)d.r0 + (int)blockIdx.x * S_RB;
+  const int rend = aux ? (int)d.aux_rows : (int)(d.r0 + d.rows);
+  const int h_from = aux ? rend : (int)d.h_from;
+  const int64_t wdel = aux ? d.aux_wdelta : 0;
+  float* const outp = aux ? d.aux_out + c * d.aux_sout : d.out + c * d.sout;
+  const int K0 = d.n_in, K0p = (K0 + 15) / 16 * 16;
+  const int J = d.n_out;
+  constexpr int L = NL;
+
+  // ---- the small operands are loaded up front, in the order they are needed
+  // (the vector memory counter retires in order): the input rows, the head
+  // weights, the first layer's weights (narrow inputs), every bias.
+  const int u0 = 32 * w + lr;  // A-operand unit of tile 0 (tile 1: + 16)
+  const float* xb = aux ? d.aux_x + c * d.aux_sxb : d.x + c * d.sxb;
+  const int64_t ldx = aux ? d.aux_ldx : d.ldx;
+  constexpr int XS = (S_RB * S_H + 511) / 512;  // staged input elements per thread (<= 8)
+  float xs[XS];
+#pragma unroll
+  for (int i = 0; i < XS; ++i) {
+    const int e = t + 512 * i;
+    const int m = e / K0p, k = e - m * K0p;
+    const int r = m0 + m;
+    xs[i] = (e < S_RB * K0p && r < rend && k < K0) ? xb[(int64_t)r * ldx + k] : 0.f;
+  }
+  const float* Wh = d.W[L] + wdel + c * d.sW[L];
+  constexpr int WS = (S_JMAX * S_H) / 512;  // head weights per thread (<= 32)
+  float whs[WS];
+#pragma unroll
+  for (int i = 0; i < WS; ++i) {
+    const int e = t + 512 * i;
+    whs[i] = e < J * S_H ? Wh[e] : 0.f;
+  }
+  const float* W0 = d.W[0] + wdel + c * d.sW[0];
+  const bool w0_regs = K0p <= 32;  // first layer's operand in registers
+  float w0a[8], w0b[8];  // group g, element i: W0[unit][min(16 g + 4 lq + i, n_in - 1)]
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = min(16 * g + 4 * lq + i, K0 - 1);
+      w0a[4 * g + i] = (w0_regs && 16 * g < K0p) ? W0[u0 * K0 + k] : 0.f;
+      w0b[4 * g + i] = (w0_regs && 16 * g < K0p) ? W0[(u0 + 16) * K0 + k] : 0.f;
+    }
+  float4 bias[L][2];  // this lane's four units of each tile, every layer
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    const float* b = d.b[l] + wdel + c * d.sb[l];
+    bias[l][0] = *reinterpret_cast<const float4*>(b + 32 * w + 4 * lq);
+    bias[l][1] = *reinterpret_cast<const float4*>(b + 32 * w + 16 + 4 * lq);
+  }
+  const float* bh = d.b[L] + wdel + c * d.sb[L];
+  const float bh0 = bh[((t >> 2) % J)];  // the head bias of this thread's first pair
+  float4 wa[16], wb[16];
+  auto load_w = [&](int l) {
+    const float* W = d.W[l] + wdel + c * d.sW[l];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      wa[g] = *reinterpret_cast<const float4*>(W + u0 * S_H + 16 * g + 4 * lq);
+      wb[g] = *reinterpret_cast<const float4*>(W + (u0 + 16) * S_H + 16 * g + 4 * lq);
+    }
+  };
+  // stage the input rows and the head weights
+#pragma unroll
+  for (int i = 0; i < XS; ++i) {
+    const int e = t + 512 * i;
+    if (e < S_RB * K0p) {
+      const int m = e / K0p, k = e - m * K0p;
+      S.x[m * S_LDK + k] = xs[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < WS; ++i) S.wh[t + 512 * i] = whs[i];
+  __syncthreads();
+
+  // ---- hidden layers
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    const float* src = l == 0 ? S.x : S.h[(l - 1) & 1];
+    float* dst = S.h[l & 1];
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    if (l > 0 && (PROBE & 1)) {
+      acc0[0] += wa[l].x + wb[l].y;
+    } else if (l > 0) {
+      // the layer's weights stream through this CU's L1 (256 KB per
+      // workgroup: with the MFMA chain, what bounds a 16-row pass); issued
+      // here rather than at kernel start, where they would queue ahead of
+      // the input rows the first layer waits on (measured 15.2 vs 17.2 us on
+      // the 512-row policy pass)
+      load_w(l);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const float4 a = *reinterpret_cast<const float4*>(&src[lr * S_LDK + 16 * g + 4 * lq]);
+        acc0 = mfma4(wa[g].x, a.x, acc0); acc1 = mfma4(wb[g].x, a.x, acc1);
+        acc0 = mfma4(wa[g].y, a.y, acc0); acc1 = mfma4(wb[g].y, a.y, acc1);
+        acc0 = mfma4(wa[g].z, a.z, acc0); acc1 = mfma4(wb[g].z, a.z, acc1);
+        acc0 = mfma4(wa[g].w, a.w, acc0); acc1 = mfma4(wb[g].w, a.w, acc1);
+      }
+    } else if (w0_regs) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        if (16 * g < K0p) {
+          const float4 a = *reinterpret_cast<const float4*>(&src[lr * S_LDK + 16 * g + 4 * lq]);
+          acc0 = mfma4(w0a[4 * g + 0], a.x, acc0); acc1 = mfma4(w0b[4 * g + 0], a.x, acc1);
+          acc0 = mfma4(w0a[4 * g + 1], a.y, acc0); acc1 = mfma4(w0b[4 * g + 1], a.y, acc1);
+          acc0 = mfma4(w0a[4 * g + 2], a.z, acc0); acc1 = mfma4(w0b[4 * g + 2], a.z, acc1);
+          acc0 = mfma4(w0a[4 * g + 3], a.w, acc0); acc1 = mfma4(w0b[4 * g + 3], a.w, acc1);
+        }
+      }
+    } else {
+      // wide first layer (K0p > 32): W rows of n_in floats read per group (k
+      // past n_in reads a clamped column times the zero padding of x: an exact 0)
+      for (int g = 0; g < K0p / 16; ++g) {
+        const float4 a = *reinterpret_cast<const float4*>(&src[lr * S_LDK + 16 * g + 4 * lq]);
+        float va[4], vb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = min(16 * g + 4 * lq + i, K0 - 1);
+          va[i] = W0[u0 * K0 + k];
+          vb[i] = W0[(u0 + 16) * K0 + k];
+        }
+        acc0 = mfma4(va[0], a.x, acc0); acc1 = mfma4(vb[0], a.x, acc1);
+        acc0 = mfma4(va[1], a.y, acc0); acc1 = mfma4(vb[1], a.y, acc1);
+        acc0 = mfma4(va[2], a.z, acc0); acc1 = mfma4(vb[2], a.z, acc1);
+        acc0 = mfma4(va[3], a.w, acc0); acc1 = mfma4(vb[3], a.w, acc1);
+      }
+    }
+    // epilogue: lane holds row lr, units 32 w + 16 tile + 4 lq + i
+    float* hg = (!aux && d.h[l]) ? d.h[l] + c * d.sh : nullptr;
+    const int row = m0 + lr;
+    const bool keep = hg != nullptr && row >= h_from && row < rend;
+#pragma unroll
+    for (int tl = 0; tl < 2; ++tl) {
+      const f32x4& a = tl ? acc1 : acc0;
+      const int u = 32 * w + 16 * tl + 4 * lq;
+      const float4 bv = bias[l][tl];
+      const float4 v = make_float4(fmaxf(a[0] + bv.x, 0.f), fmaxf(a[1] + bv.y, 0.f),
+                                   fmaxf(a[2] + bv.z, 0.f), fmaxf(a[3] + bv.w, 0.f));
+      *reinterpret_cast<float4*>(&dst[lr * S_LDK + u]) = v;
+      if (keep) *reinterpret_cast<float4*>(hg + (int64_t)row * S_H + u) = v;
+    }
+    __syncthreads();
+  }
+
+  // ---- head: out[row][j] = h[row] . Wh[j] + bh[j]; four threads per pair
+  const float* hl = S.h[(L - 1) & 1];
+  if (PROBE & 2) return;
+  for (int p = t >> 2; p < S_RB * J; p += 128) {
+    const int m = p / J, j = p - m * J, q = t & 3;
+    float s = 0.f;
+#pragma unroll 4
+    for (int n = 4 * q; n < S_H; n += 16) {
+      const float4 hv = *reinterpret_cast<const float4*>(&hl[m * S_LDK + n]);
+      const float4 wv = *reinterpret_cast<const float4*>(&S.wh[j * S_H + n]);
+      s = fmaf(hv.x, wv.x, s);
+      s = fmaf(hv.y, wv.y, s);
+      s = fmaf(hv.z, wv.z, s);
+      s = fmaf(hv.w, wv.w, s);
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    const int r = m0 + m;
+    const float bj = p == (t >> 2) ? bh0 : bh[j];
+    if (q == 0 && r < rend) outp[(int64_t)r * d.ldout + j] = s + bj;
+  }
+}
+
+}  // namespace
+
+// d3a_mlp_fwd's block_rows == 16 path; false when the shape does not fit
+bool mlp_small_launch(const d3a_mlp_fwd_desc& d, hipStream_t st) {
+  if (d.H != S_H || d.n_out > S_JMAX || d.n_in > S_H || d.n_hidden < 1 || d.n_hidden > 4)
+    return false;
+  auto a16 = [](const void* p, int64_t stride) {
+    return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && stride % 4 == 0;
+  };
+  for (int l = 1; l < d.n_hidden; ++l)
+    if (!a16(d.W[l], d.sW[l])) return false;
+  for (int l = 0; l < d.n_hidden; ++l)
+    if (!a16(d.b[l], d.sb[l])) return false;
+  for (int l = 0; l < d.n_hidden; ++l)
+    if (d.h[l] && !a16(d.h[l], d.sh)) return false;
+  if (d.aux_rows > 0 && d.aux_wdelta % 4) return false;
+  const int64_t nb = (d.rows + S_RB - 1) / S_RB + (d.aux_rows + S_RB - 1) / S_RB;
+  const dim3 grid((unsigned)nb, 1, (unsigned)d.C);
+  static const int probe = [] {
+    const char* e = getenv("D3A_SMALL_PROBE");
+    return e ? atoi(e) : 0;
+  }();
+  if (probe && d.n_hidden == 2) {
+    if (probe == 1) hipLaunchKernelGGL((mlp_small_kernel<2, 1>), grid, dim3(512), 0, st, d);
+    else if (probe == 2) hipLaunchKernelGGL((mlp_small_kernel<2, 2>), grid, dim3(512), 0, st, d);
+    else hipLaunchKernelGGL((mlp_small_kernel<2, 3>), grid, dim3(512), 0, st, d);
+    return true;
+  }
+  switch (d.n_hidden) {
+    case 1: hipLaunchKernelGGL(mlp_small_kernel<1>, grid, dim3(512), 0, st, d); break;
+    case 2: hipLaunchKernelGGL(mlp_small_kernel<2>, grid, dim3(512), 0, st, d); break;
+    case 3: hipLaunchKernelGGL(mlp_small_kernel<3>, grid, dim3(512), 0, st, d); break;
+    default: hipLaunchKernelGGL(mlp_small_kernel<4>, grid, dim3(512), 0, st, d); break;
+  }
+  return true;
+}
+
+}  // namespace d3a

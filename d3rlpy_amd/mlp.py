@@ -43,8 +43,11 @@ class Acts:
     R: int
 
     @staticmethod
-    def alloc(net: EnsembleMLP, R: int, device) -> "Acts":
-        hs = [torch.zeros(net.C, R, net.sizes[l + 1], device=device)
+    def alloc(net: EnsembleMLP, R: int, device, dtype=torch.float32) -> "Acts":
+        """``dtype`` bfloat16: kept activations for the bf16 critic kernels
+        (d3a_q2_fwd_bf16 / d3a_q2_bwd_bf16 are then selected by forward /
+        backward); outputs stay fp32."""
+        hs = [torch.zeros(net.C, R, net.sizes[l + 1], device=device, dtype=dtype)
               for l in range(net.n_layers - 1)]
         out_dim = net.sizes[-1]
         out = torch.zeros((net.C, R) if out_dim == 1 else (net.C, R, out_dim), device=device)
@@ -81,6 +84,12 @@ _FUSED_BM = int(os.environ.get("D3A_FUSED_BM", "0"))
 _Q2 = os.environ.get("D3A_Q2_BWD", "1") == "1"
 
 
+def q2_shape(net: EnsembleMLP) -> bool:
+    """[n_in <= 48, 256, 256, 1]: the shape of the q2 critic kernels."""
+    s = net.sizes
+    return net.n_layers == 3 and s[1] == 256 and s[2] == 256 and s[3] == 1 and s[0] <= 48
+
+
 def q2_ok(net: EnsembleMLP, rows: int) -> bool:
     """d3a_q2_bwd applies: two hidden layers of 256, one output, <= 48 inputs,
     a large pass (per-layer GEMMs win on the 100-512-row passes)."""
@@ -88,6 +97,19 @@ def q2_ok(net: EnsembleMLP, rows: int) -> bool:
     return (_Q2 and not _FUSED_BWD and not ops.SBF16_TERMS and net.n_layers == 3
             and s[1] == 256 and s[2] == 256 and s[3] == 1 and s[0] <= 48
             and rows * net.C >= _HEAD_GEN_MIN_ROWS)
+
+
+# small passes (policy over [obs; next_obs], actor / target passes of a few
+# hundred rows): 16-row workgroups, the whole MLP in one launch
+# (d3a_mlp_fwd block_rows 16, csrc/mlp_small.hip)
+_SMALL = os.environ.get("D3A_MLP_SMALL", "1") == "1"
+SMALL_MAX_ROWS = 2048
+
+
+def small_ok(net: EnsembleMLP, rows: int) -> bool:
+    hidden = net.sizes[1:-1]
+    return (_SMALL and 1 <= len(hidden) <= N.MLP_MAX_HIDDEN and set(hidden) == {256}
+            and net.sizes[0] <= 256 and net.sizes[-1] <= 64 and rows * net.C <= SMALL_MAX_ROWS)
 
 
 def fused_ok(net: EnsembleMLP, rows: Optional[int] = None, backward: bool = False) -> bool:
@@ -124,9 +146,14 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         return
     C = net.C if members is None else members
     sizes = net.sizes
-    if fused_ok(net, n * C // net.C):
+    bf16 = bool(acts.h) and acts.h[0].dtype == torch.bfloat16
+    if bf16 and not (q2_shape(net) and keep_h and members is None and not skip_head):
+        raise NotImplementedError("bf16 activations: [n_in <= 48, 256, 256, 1] critics, "
+                                  "all members, activations kept")
+    small = not bf16 and not skip_head and small_ok(net, n * C // net.C)
+    if bf16 or small or fused_ok(net, n * C // net.C):
         d = N.MlpFwdDesc()
-        d.block_rows = _FUSED_BM
+        d.block_rows = 16 if small else _FUSED_BM
         d.x, d.ldx = x, ldx
         d.sxb = (0 if x_shared else R * ldx) if sxb is None else sxb
         L = net.n_layers
@@ -148,7 +175,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             d.aux_wdelta = (ast.data.data_ptr() - store.data.data_ptr()) // 4
             d.aux_out, d.aux_sout, d.aux_rows = aacts.out.data_ptr(), aacts.R * sizes[-1], aacts.R
             aux = None
-        ops.call_desc("d3a_mlp_fwd", d)
+        ops.call_desc("d3a_q2_fwd_bf16" if bf16 else "d3a_mlp_fwd", d)
         if aux is not None:
             forward(net, aux[0], aux[1], True, aux[2], aux[3], keep_h=False)
         return
@@ -277,9 +304,10 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
             raise NotImplementedError("d3a_q2_bwd space: weight gradients of all rows only")
         d = N.Q2BwdDesc()
         H = sizes[1]
+        esz = acts.h[0].element_size()  # 2: bf16 activations (d3a_q2_bwd_bf16)
         d.x, d.ldx, d.sxb = x + 4 * r0 * ldx, ldx, sxb_
-        d.h1 = acts.h[0].data_ptr() + 4 * r0 * H
-        d.h2 = acts.h[1].data_ptr() + 4 * r0 * H
+        d.h1 = acts.h[0].data_ptr() + esz * r0 * H
+        d.h2 = acts.h[1].data_ptr() + esz * r0 * H
         d.sh, d.ldh = R * H, H
         d.g, d.sgb = dout, sdout_b
         if g_scale is not None:
@@ -290,7 +318,7 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         d.dW2, d.db2 = gs.get(net.wname(1)).data_ptr(), gs.get(net.bname(1)).data_ptr()
         d.dW3, d.db3 = gs.get(net.wname(2)).data_ptr(), gs.get(net.bname(2)).data_ptr()
         d.rows, d.n_in, d.C = n, sizes[0], C
-        ops.call_desc("d3a_q2_bwd", d)
+        ops.call_desc("d3a_q2_bwd_bf16" if esz == 2 else "d3a_q2_bwd", d)
         return None
 
     def h_ptr(l):  # input activation of layer l at row r0

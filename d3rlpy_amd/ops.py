@@ -261,6 +261,20 @@ SBF16_MIN_ROWS = 4096
 SBF16_W = os.environ.get("D3A_SBF16_W", "1") == "1"  # also the weight-gradient GEMMs
 
 
+# critic-ensemble precision of the large CQL critic passes: "fp32" (the
+# reference's; parity path) or "bf16" (throughput line: d3a_q2_fwd_bf16 /
+# d3a_q2_bwd_bf16, bf16 operands with fp32 accumulation, bf16 kept
+# activations).  Read when an Impl builds its pipeline workspace.
+CRITIC_PRECISION = os.environ.get("D3A_CRITIC_PRECISION", "fp32")
+
+
+def set_critic_precision(p: str) -> None:
+    global CRITIC_PRECISION
+    if p not in ("fp32", "bf16"):
+        raise ValueError(f"critic precision must be fp32 or bf16, got {p!r}")
+    CRITIC_PRECISION = p
+
+
 def set_sbf16(terms: int) -> None:
     global SBF16_TERMS
     assert terms in (0, 3, 6)

@@ -212,8 +212,11 @@ int d3a_head1_min(const d3a_head1_min_desc* desc, void* stream);
  * receives a_{l+1} as [C][R][H] (member stride sh, absolute row index) for
  * the backward pass, for rows r >= h_from only (rows no backward reads are
  * not stored).  Activations stay in LDS between layers; block_rows (0 =
- * automatic, 32, 64 or 128) rows per workgroup.  Heads wider than 64
- * (quantile heads) run on MFMA as well. */
+ * automatic, 16, 32, 64 or 128) rows per workgroup.  Heads wider than 64
+ * (quantile heads) run on MFMA as well.  block_rows 16: the small-pass
+ * kernel (hundreds of rows; H == 256, n_out <= 64, 16-byte aligned W[1..],
+ * biases and h rows).  Automatic on [n_in <= 48, 256, 256, 1] over >= 8,192
+ * member-rows: the register-resident critic kernel (csrc/q2_fwd.hip). */
 #define D3A_MLP_MAX_HIDDEN 4
 typedef struct d3a_mlp_fwd_desc {
   const float* x; int64_t ldx, sxb;
@@ -295,6 +298,15 @@ typedef struct d3a_q2_bwd_desc {
   int32_t n_in, C;
 } d3a_q2_bwd_desc;
 int d3a_q2_bwd(const d3a_q2_bwd_desc* d, void* stream);
+
+/* bf16 throughput instantiation of the critic forward / backward (the
+ * `--precision bf16` bench line, never the parity path): the same contracts
+ * as d3a_mlp_fwd on [n_in <= 48, 256, 256, 1] and d3a_q2_bwd, with every GEMM
+ * operand rounded to bf16 and fp32 accumulation (v_mfma_f32_32x32x16_bf16);
+ * the kept activations h[0] / h[1] (forward) and h1 / h2 (backward) are bf16
+ * rows ([C][rows][256] __bf16, 16-byte aligned), everything else fp32. */
+int d3a_q2_fwd_bf16(const d3a_mlp_fwd_desc* d, void* stream);
+int d3a_q2_bwd_bf16(const d3a_q2_bwd_desc* d, void* stream);
 
 /* ---- optimiser and target networks ------------------------------------- */
 

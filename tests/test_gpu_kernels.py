@@ -357,6 +357,49 @@ def test_fused_mlp_forward(dev, C, R, r0, n, K0, H, L, J, x_shared, bm, monkeypa
         assert _rel_err(out.reshape(n, J), a) < 2e-6, c
 
 
+@pytest.mark.parametrize("C,R,r0,n,K0,L,J,x_shared", [
+    (1, 512, 0, 512, 11, 2, 6, True),      # CQL policy on [obs; next_obs] (mu | logstd)
+    (2, 256, 0, 256, 14, 2, 1, True),      # actor-phase critic pass
+    (1, 100, 0, 100, 3, 2, 1, True),       # K1 TD3+BC policy, odd rows
+    (3, 77, 5, 60, 37, 1, 5, False),       # per-member inputs, one hidden layer, r0 > 0
+    (2, 300, 0, 300, 256, 3, 64, True),    # widest first layer and head, 3 hidden layers
+])
+def test_small_mlp_forward(dev, C, R, r0, n, K0, L, J, x_shared, monkeypatch):
+    """d3a_mlp_fwd block_rows 16 (csrc/mlp_small.hip: 16-row workgroups on
+    v_mfma_f32_16x16x4_f32, the small-pass instantiation) against an fp64
+    torch MLP, activations kept for rows >= h_from only (2e-6 relative)."""
+    from d3rlpy_amd import mlp
+    from d3rlpy_amd.nets import EnsembleMLP, ParamStore
+    g = torch.Generator().manual_seed(R + K0 + J)
+    st = ParamStore()
+    net = EnsembleMLP(st, "m", C, [K0] + [256] * L + [J])
+    st.allocate(dev)
+    with torch.no_grad():
+        st.data.copy_(torch.randn(st.data.numel(), generator=g) * 0.1)
+    assert mlp.small_ok(net, n)
+    ldx = (K0 + 3) // 4 * 4 + 4
+    x = torch.randn((1 if x_shared else C), R, ldx, generator=g).to(dev)
+    acts = mlp.Acts.alloc(net, R, dev)
+    for h in acts.h:
+        h.fill_(float("nan"))
+    acts.out.fill_(float("nan"))
+    h_from = r0 + n // 3
+    mlp.forward(net, st, x.data_ptr(), x_shared, ldx, acts, r0, r0 + n, h_from=h_from)
+    torch.cuda.synchronize()
+    k = h_from - r0
+    for c in range(C):
+        a = x[0 if x_shared else c, r0:r0 + n, :K0].double()
+        for l in range(L + 1):
+            W, b = net.export_linear(l, c, st)
+            a = a @ W.double().T + b.double()
+            if l < L:
+                a = a.clamp_min(0)
+                assert _rel_err(acts.h[l][c, h_from:r0 + n], a[k:]) < 2e-6, (c, l)
+                assert torch.isnan(acts.h[l][c, r0:h_from]).all(), (c, l)
+        assert _rel_err(acts.out[c, r0:r0 + n].reshape(n, J), a) < 2e-6, c
+        assert torch.isnan(acts.out[c, :r0]).all() and torch.isnan(acts.out[c, r0 + n:]).all()
+
+
 @pytest.mark.parametrize("bm", [0, 32, 128])
 @pytest.mark.parametrize("R,n_aux", [(15616, 256), (4096, 100), (300, 1000)])
 def test_fused_mlp_forward_aux_pass(dev, R, n_aux, bm, monkeypatch):

@@ -23,9 +23,12 @@ def main():
     ap.add_argument("--n-in", type=int, default=14)
     ap.add_argument("--bm", type=int, default=0)
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--C", type=int, default=2)
+    ap.add_argument("--J", type=int, default=1)
+    ap.add_argument("--bf16", action="store_true", help="d3a_q2_fwd_bf16 (bf16 kept activations)")
     a = ap.parse_args()
-    dev, C, H = "cuda", 2, 256
-    sizes = [a.n_in, H, H, 1]
+    dev, C, H = "cuda", a.C, 256
+    sizes = [a.n_in, H, H, a.J]
     ldx = (a.n_in + 3) // 4 * 4
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(a.rows, ldx, device=dev, generator=g)
@@ -43,9 +46,11 @@ def main():
         o += C * sizes[l + 1]
         o = (o + 3) // 4 * 4
         offs.append((w, b))
-    h = [torch.zeros(C, a.rows, H, device=dev) for _ in range(2)]
-    out = torch.zeros(C, a.rows, device=dev)
-    aout = torch.zeros(C, max(a.aux, 1), device=dev)
+    h = [torch.zeros(C, a.rows, H, device=dev,
+                     dtype=torch.bfloat16 if a.bf16 else torch.float32) for _ in range(2)]
+    entry = "d3a_q2_fwd_bf16" if a.bf16 else "d3a_mlp_fwd"
+    out = torch.zeros(C, a.rows, a.J, device=dev)
+    aout = torch.zeros(C, max(a.aux, 1), a.J, device=dev)
     d = N.MlpFwdDesc()
     d.block_rows = a.bm
     d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
@@ -57,13 +62,13 @@ def main():
     for l in range(2):
         d.h[l] = h[l].data_ptr()
     d.sh = a.rows * H
-    d.out, d.sout, d.ldout = out.data_ptr(), a.rows, 1
+    d.out, d.sout, d.ldout = out.data_ptr(), a.rows * a.J, a.J
     d.r0, d.rows, d.C, d.h_from = 0, a.rows, C, a.h_from
     if a.aux:
         d.aux_x, d.aux_ldx, d.aux_sxb, d.aux_wdelta = xa.data_ptr(), ldx, 0, n_par
-        d.aux_out, d.aux_sout, d.aux_rows = aout.data_ptr(), a.aux, a.aux
+        d.aux_out, d.aux_sout, d.aux_rows = aout.data_ptr(), a.aux * a.J, a.aux
     for _ in range(5):
-        ops.call_desc("d3a_mlp_fwd", d)
+        ops.call_desc(entry, d)
     torch.cuda.synchronize()
     # check against torch fp32 on a row sample
     W = [store[offs[l][0]:offs[l][0] + C * sizes[l] * sizes[l + 1]].view(C, sizes[l + 1], sizes[l])
@@ -72,19 +77,19 @@ def main():
     xs = x[:, :a.n_in]
     r1 = torch.relu(xs @ W[0].transpose(1, 2) + bb[0])
     r2 = torch.relu(r1 @ W[1].transpose(1, 2) + bb[1])
-    q = (r2 @ W[2].transpose(1, 2) + bb[2]).squeeze(-1)
+    q = r2 @ W[2].transpose(1, 2) + bb[2]
     err = ((q - out).abs().max() / q.abs().max()).item()
-    herr = ((r2[:, a.h_from:] - h[1][:, a.h_from:]).abs().max()).item()
+    herr = ((r2[:, a.h_from:] - h[1][:, a.h_from:].float()).abs().max()).item()
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(a.reps):
-        ops.call_desc("d3a_mlp_fwd", d)
+        ops.call_desc(entry, d)
     e1.record(s)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / a.reps
     flops = 2 * C * (a.rows + a.aux) * sum(sizes[l] * sizes[l + 1] for l in range(3))
-    print(json.dumps({"kernel": "d3a_mlp_fwd", "rows": a.rows, "aux": a.aux, "bm": a.bm,
+    print(json.dumps({"kernel": entry, "rows": a.rows, "aux": a.aux, "bm": a.bm, "C": C, "J": a.J,
                       "variant": os.environ.get("D3A_FWD_PROBE", "") + ("generic" if os.environ.get("D3A_FWD_Q2") == "0" else ""),
                       "avg_us": round(us, 2), "tflops": round(flops / us / 1e6, 2),
                       "frac_fp32_peak": round(flops / us / 1e6 / 157.3, 4),
