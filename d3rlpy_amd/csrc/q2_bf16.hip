@@ -326,29 +326,39 @@ __global__ __launch_bounds__(512) void q2_bwd_bf16_kernel(d3a_q2_bwd_desc d) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) gv[j] = gg[gr0 + j < rows ? gr0 + j : rows - 1];
     __builtin_amdgcn_sched_barrier(0);
+    // per element: ~8 VALU (the staging was VALU-bound at ~30): fp32 sums
+    // over the sub-block's 16 rows, one fp64 accumulation per sub-block
     float dz[16];
+    float f_db2 = 0.f, f_dw3 = 0.f, f_db3 = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const int r = gr0 + j;
-      const bool ok = r < rows;
+      const int r = gr0 + j;  // uniform
       float gp = gv[j];
       if (r < d.n_scaled) gp *= gs;
-      if (!ok) gp = 0.f;
-      const unsigned bits = (S.h2[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-      const float h2v = ok ? __builtin_bit_cast(float, bits << 16) : 0.f;
-      dz[j] = h2v > 0.f ? gp * w3o : 0.f;
-      if (own_o) {
-        s_db2 += (double)dz[j];
-        s_dw3 += (double)(gp * h2v);
-      }
-      if (so == 0) s_db3 += (double)gp;
-      L.dzr[b2][(sr + j) * BB_LDR + so] = (__bf16)dz[j];
+      if (r >= rows) gp = 0.f;
+      const unsigned pk = S.h2[j >> 1];
+      const unsigned bits = (j & 1) ? (pk & 0xffff0000u) : (pk << 16);
+      const float h2v = r < rows ? __builtin_bit_cast(float, bits) : 0.f;
+      dz[j] = (int)bits > 0 && r < rows ? gp * w3o : 0.f;  // h2 > 0 (bf16 sign, nonzero)
+      f_db2 += dz[j];
+      f_dw3 = fmaf(gp, h2v, f_dw3);
+      f_db3 += gp;
     }
+    if (own_o) {
+      s_db2 += (double)f_db2;
+      s_dw3 += (double)f_dw3;
+    }
+    if (so == 0) s_db3 += (double)f_db3;
     bf16x8 v0, v1;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       v0[j] = (__bf16)dz[j];
       v1[j] = (__bf16)dz[8 + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      L.dzr[b2][(sr + j) * BB_LDR + so] = v0[j];
+      L.dzr[b2][(sr + 8 + j) * BB_LDR + so] = v1[j];
     }
     *reinterpret_cast<bf16x8*>(&L.dzt[b2][so * BB_LDT + sr]) = v0;
     *reinterpret_cast<bf16x8*>(&L.dzt[b2][so * BB_LDT + sr + 8]) = v1;
