@@ -10,14 +10,16 @@ gathered by the oracle's TransitionMiniBatch, and each step's device draws
 reproduced with d3a_philox_fill at that step's Philox counter (the sampler
 kernels draw bit-identically to it: test_cql_sample_draws_equal_philox_fill).
 
-Bars (a 12-step trajectory without re-synchronisation): every logged loss
-within 1e-4 relative; parameters and targets: at least 99.9 % of the entries of
-every network within 1e-5 and all within 1e-3.  The two fp32 trajectories
-separate only where Adam's first steps amplify a near-zero gradient entry
-(lr * g / (|g| + eps): a rounding-level difference in g can move such an entry
-by up to 2 * lr; proven entry by entry for single steps in
-tests/test_gpu_arbiters.py) — isolated entries that then stay apart.  The index
-stream and the reproduced draws themselves are exact.
+Two tests.  test_cql_fit_production_path_per_step_proof: every one of the
+12 production steps against the oracle started from HIP's pre-step state --
+metrics 1e-5, gradients 2e-5, and every parameter entry within 1e-5 or proven
+entry by entry to be Adam applied to HIP's own checked gradient (the per-entry
+proof).  The trajectory tests (no re-synchronisation for 12 steps): every
+logged loss within 1e-4 relative; parameters and targets: at least 99.9 % of
+the entries of every network within 1e-5 and all within 1e-3 -- the two fp32
+trajectories separate only where Adam amplifies a near-zero gradient entry
+(lr * g / (|g| + eps)), which the per-step test proves entry by entry.  The
+index stream and the reproduced draws themselves are exact.
 """
 import numpy as np
 import pytest
@@ -29,6 +31,13 @@ from oracle.cql import Batch
 pytestmark = pytest.mark.gpu
 
 STEPS = 12
+# HIP gradients vs an fp64 evaluation of each production step (max-normalised
+# per tensor).  Measured worst 1.2e-4 (step 9, critic 1 layer 1, where the fp32
+# oracle is at 1.5e-6: a pre-activation within rounding of zero that HIP's
+# fp32 sum puts on the other side of the ReLU; the conservative loss's
+# importance-sampled and data rows cancel across the 7,936-row critic pass, so
+# one row's decision shows at this size).  Bar 1e-3.
+GRAD_BAR_FP64 = 1e-3
 
 
 def _transitions(ds):
@@ -71,6 +80,134 @@ def _compare_state(sd, ref, keys):
     frac = n_off / n_all
     assert worst <= 1e-3 and frac <= 1e-3, (worst, frac)
     return worst, frac
+
+
+def _cql_noise(ws, s, B, A, N):
+    """The device draws of production step ``s`` (Philox counter s), as the
+    oracle's CQLNoise."""
+    from oracle.cql import CQLNoise
+    tmpl = CQLNoise.draw(torch.Generator(), B, A, N)
+    NB = N * B
+    buf = _philox(ws.n_normal, ws.n_uniform, ws.seed, s)
+    o = 0
+    eps_temp = buf[o:o + B * A]; o += B * A
+    ep = buf[o:o + 4 * NB * A].view(2, 2, N, B, A); o += 4 * NB * A
+    eps_actor = buf[o:o + B * A]; o += B * A
+    ur = buf[ws.n_normal:ws.n_normal + 2 * NB * A].view(2, NB, A)
+    f = dict(eps_temp=eps_temp, alpha_pi_t=ep[0, 0], alpha_pi_tp1=ep[0, 1],
+             critic_pi_t=ep[1, 0], critic_pi_tp1=ep[1, 1], alpha_rand=ur[0],
+             critic_rand=ur[1], eps_actor=eps_actor)
+    return CQLNoise(**{k: v.reshape(getattr(tmpl, k).shape).clone() for k, v in f.items()},
+                    **{k: getattr(tmpl, k) for k in tmpl.__dataclass_fields__ if k not in f})
+
+
+def test_cql_fit_production_path_per_step_proof():
+    """Twelve production steps -- Algo.fit, one step per call: the first
+    eager, the rest replays of the captured graph, device-drawn noise, the
+    numpy index stream -- each replayed on the oracle started from HIP's exact
+    state before that step, on the same batch and the reproduced draws.  Per
+    step: every logged metric within 1e-5, every critic / policy gradient
+    within GRAD_BAR_FP64 of an fp64 evaluation, targets and log_alpha / log_temp within
+    1e-5 / 1e-6, and every parameter entry within 1e-5 of the oracle or --
+    entry by entry -- equal (1e-7) to Adam from HIP's pre-step optimiser state
+    applied to HIP's own checked gradient (arbiter_helpers.check_params_adam).
+    This is the per-entry proof behind the 12-step trajectory bar below."""
+    from arbiter_helpers import adam_state_by_key, check_params_adam, hip_grads
+    from cql_helpers import make_oracle, max_rel, oracle_state
+    from d3rlpy_amd.algos.cql import CQL
+    from d3rlpy_amd.datasets import get_synthetic_d4rl
+    from test_gpu_cql_parity import _oracle_step
+    D, A, N, B = 11, 3, 10, 256
+    ds = get_synthetic_d4rl("hopper-medium-v0", n=5000, seed=2)
+    torch.manual_seed(67280421310721)
+    algo = CQL(batch_size=B)
+    algo.build_with_dataset(ds)
+    impl = algo.impl
+    orc = make_oracle(D, A, [256, 256], N, seed=0)
+    batches = _oracle_batches(_transitions(ds), B, 42)
+    np.random.seed(42)
+    cref, pref = impl._critic_refs(), impl._policy_refs()
+    n_amp, worst_g = 0, 0.0
+    for s in range(STEPS):
+        sd0 = impl.get_state_dict()
+        algo.fit(ds, n_steps=1, n_steps_per_epoch=1, save_metrics=False, verbose=False,
+                 show_progress=False, index_source="numpy")
+        ws = impl._last_ws()
+        sd1 = impl.get_state_dict()
+        names, ring = impl.read_metrics_ring(None)  # this fit call's rows: its one step
+        assert ring.shape[0] >= 1
+        nz = _cql_noise(ws, s, B, A, N)
+        for k, v in sd0.items():
+            getattr(orc, k).load_state_dict(v)
+        m, cgrads, pgrads = _oracle_step(orc, batches[s], nz, A)
+        for j, name in enumerate(names):
+            assert abs(ring[-1, j] - m[name]) <= 1e-5 * max(1.0, abs(m[name])), (s, name)
+        # the gradients against an fp64 evaluation of the same step (the fp32
+        # oracle's own rounding on the cancelling conservative gradient is of
+        # the same order as HIP's: test_gpu_cql_parity.test_cql_grad_accuracy_vs_fp64)
+        o64 = make_oracle(D, A, [256, 256], N, seed=0)
+        for k, v in sd0.items():
+            getattr(o64, k).load_state_dict(v)
+        for mod in (o64._q_func, o64._policy, o64._targ_q_func, o64._targ_policy,
+                    o64._log_temp, o64._log_alpha):
+            mod.double()
+        for opt in (o64._critic_optim, o64._actor_optim, o64._temp_optim, o64._alpha_optim):
+            for st in opt.state.values():  # HIP's moments, in fp64 like the parameters
+                for k_, v_ in st.items():
+                    if torch.is_tensor(v_) and k_ != "step":
+                        st[k_] = v_.double()
+        tb = batches[s]
+        tb64 = type(tb)(*(getattr(tb, f).double() for f in tb.__dataclass_fields__))
+        nz64 = type(nz)(**{k: (None if getattr(nz, k) is None else getattr(nz, k).double())
+                           for k in nz.__dataclass_fields__})
+        o64.update_temp(tb64, nz64.eps_temp)
+        o64.update_alpha(tb64, nz64)
+        o64.update_critic(tb64, nz64)
+        g64 = {}
+        for key_, _s, c, _sl in cref:
+            qf = o64._q_func.q_funcs[c]
+            l = int(key_.split("_fcs.")[1].split(".")[0]) if "_fcs." in key_ else 2
+            fc = (list(qf._encoder._fcs) + [qf._fc])[l]
+            g64[key_] = (fc.weight if key_.endswith("weight") else fc.bias).grad.detach().clone()
+        # the actor stage on HIP's own updated critic (and temperature): the
+        # critic step's Adam amplification of near-zero gradient entries (proven
+        # below) moves a few critic weights by up to 2 lr, enough to flip the
+        # min over the two critics on a row -- the actor-gradient check then
+        # compares the same function, not a tie
+        o64._q_func.load_state_dict({k: v.double() for k, v in sd1["_q_func"].items()})
+        o64._log_temp.load_state_dict({k: v.double() for k, v in sd1["_log_temp"].items()})
+        o64.update_actor(tb64, nz64.eps_actor)
+        g64.update({k: p.grad.detach().clone() for k, p in o64._policy.named_parameters()})
+        g_hip = {**hip_grads(cref, impl.critic_grad), **hip_grads(pref, impl.policy_grad)}
+        g32 = {}
+        for key_, _s, c, _sl in cref:
+            l = int(key_.split("_fcs.")[1].split(".")[0]) if "_fcs." in key_ else 2
+            g32[key_] = cgrads[c][l][0 if key_.endswith("weight") else 1]
+        for k in g64:
+            eh = max_rel(g_hip[k], g64[k])
+            eo = max_rel(g32[k], g64[k]) if k in g32 else float("nan")
+            if eh > 1e-5:
+                print(f"  step {s} grad {k}: hip-vs-fp64 {eh:.1e} oracle32-vs-fp64 {eo:.1e}")
+        e = max(max_rel(g_hip[k], g64[k]) for k in g64)
+        worst_g = max(worst_g, e)
+        assert e <= GRAD_BAR_FP64, (s, e)
+        ref = oracle_state(orc)
+        for key, refs, opt, lr in (("_q_func", cref, "_critic_optim", 3e-4),
+                                   ("_policy", pref, "_actor_optim", 1e-4)):
+            states = adam_state_by_key(sd0[opt], [r[0] for r in refs])
+            getter = impl.critic_grad if key == "_q_func" else impl.policy_grad
+            _, n = check_params_adam(f"step {s} {key}", sd0[key], sd1[key], ref[key],
+                                     hip_grads(refs, getter), lr=lr, states=states or None)
+            n_amp += n
+        for key in ("_targ_q_func", "_targ_policy"):
+            for n_, t in ref[key].items():
+                assert float((sd1[key][n_] - t).abs().max()) <= 1e-5, (s, key, n_)
+        assert abs(float(impl.log_alpha.item()) - float(orc._log_alpha().item())) <= 1e-6
+        assert abs(float(impl.log_temp.item()) - float(orc._log_temp().item())) <= 1e-6
+    assert len(impl._last_ws()._graphs) == 1  # steps 2..12 replayed the captured graph
+    print(f"CQL production path, per-step proof: {STEPS} steps, gradients within {worst_g:.1e} "
+          f"of fp64, {n_amp} parameter entries beyond 1e-5, each equal to Adam of HIP's own "
+          "checked gradient")
 
 
 def test_cql_fit_production_path_vs_oracle():
