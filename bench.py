@@ -585,14 +585,18 @@ def main():
                "host": host}
         # BASELINE.md's full protocol (>= 1000 steps after 50 warm-up, median
         # of 5, all cores and 1 thread), run by tools/cpu_baseline_protocol.py
-        proto = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                             f"r02_cpu_baseline_{args.algo}.json")
+        proto = next((p for p in (os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                               "profiles", f"r0{r}_cpu_baseline_{args.algo}.json")
+                                  for r in (3, 2)) if os.path.exists(p)), "")
         if os.path.exists(proto):
             with open(proto) as f:
                 pr = json.load(f)
             cpu["protocol"] = {"file": os.path.relpath(proto, os.path.dirname(
                 os.path.abspath(__file__))), "all_cores_median": round(pr["all_cores"]["median"], 3),
                 "all_cores_threads": pr["all_cores"]["threads"],
+                "all_cores_note": pr["all_cores"].get("note", ""),
+                "thread_sweep": [(w["threads"], round(w["steps_per_s"], 3))
+                                 for w in pr.get("thread_sweep", [])],
                 "one_thread_median": round(pr["one_thread"]["median"], 3),
                 "steps": pr["steps"], "warmup": pr["warmup"], "runs": pr["runs"],
                 "host_model": pr["host"]["model"]}

@@ -399,11 +399,14 @@ __global__ __launch_bounds__(256) void sac_actor_dq_kernel(const float* q, int64
 // 170-176; thread n, H <= 256, operands loaded before the head math).
 // Workgroup B: the actor loss mean(exp(log_temp) * logp - min_c Q) into
 // metrics[5] (rows summed in a fixed order).
+// DQZ: dQ/da formed here from dq_dz (the first layer's action columns staged
+// in 32 KB of LDS); otherwise read from dq_da and no LDS is reserved for it
+template <bool DQZ>
 __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_desc d) {
   __shared__ float scratch[4];
   __shared__ float s_dh[32];
-  __shared__ float s_dq[4][64];  // per-wave dQ_c/da_j sums [wave][c * 16 + j]
-  __shared__ float s_w0[32 * 256];  // the first layer's action columns [c * A + j][k]
+  __shared__ float s_dq[DQZ ? 4 : 1][64];  // per-wave dQ_c/da_j sums [wave][c * 16 + j]
+  __shared__ float s_w0[DQZ ? 32 * 256 : 1];  // the first layer's action columns [c * A + j][k]
   const int tid = threadIdx.x;
   const int A = d.A, B = d.B, C = d.C;
   const int64_t b = blockIdx.x;
@@ -428,7 +431,7 @@ __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_
     hv = d.h[b * d.ldh + tid];
     for (int k = 0; k < 2 * A; ++k) wk[k] = d.w_head[(int64_t)k * d.H + tid];
   }
-  if (d.dq_dz) {
+  if constexpr (DQZ) {
     // dQ_c/da_j = sum_k dz0[c][b][k] w0[c][k][da_off + j].  The P = C*A weight
     // columns go to LDS (every workgroup reads the same few KB from L2), then
     // thread k's product of each pair (c, j) is summed per wave by a fixed
@@ -459,7 +462,7 @@ __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_
   if (tid < A) {
     const int j = tid;
     float da = 0.f;
-    if (d.dq_dz) {
+    if constexpr (DQZ) {
       for (int c = 0; c < C; ++c) {
         const float* sc = &s_dq[0][c * 16 + j];
         da += ((sc[0] + sc[64]) + sc[128]) + sc[192];
@@ -567,8 +570,12 @@ extern "C" int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream
                          : d->dq_da != nullptr,
                 "d3a_sac_actor_head: dq_dz needs w0, C <= 4, C * A <= 32, 1 <= H0 <= 256 "
                 "(else dq_da)");
-  hipLaunchKernelGGL(sac_actor_head_kernel, dim3((unsigned)d->B + 1), dim3(256), 0,
-                     (hipStream_t)stream, *d);
+  if (d->dq_dz)
+    hipLaunchKernelGGL(sac_actor_head_kernel<true>, dim3((unsigned)d->B + 1), dim3(256), 0,
+                       (hipStream_t)stream, *d);
+  else
+    hipLaunchKernelGGL(sac_actor_head_kernel<false>, dim3((unsigned)d->B + 1), dim3(256), 0,
+                       (hipStream_t)stream, *d);
   D3A_LAUNCH_CHECK("d3a_sac_actor_head");
   return 0;
 }

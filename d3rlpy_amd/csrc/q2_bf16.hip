@@ -270,7 +270,8 @@ __global__ __launch_bounds__(512) void q2_bwd_bf16_kernel(d3a_q2_bwd_desc d) {
   const float* gg = d.g + c * d.sgb;
   const float* xg = d.x + c * d.sxb;
   const float* W2g = d.W2 + c * d.sW2;
-  const float gs = d.gscale ? *d.gscale : 1.f;
+  const float gs = __builtin_bit_cast(
+      float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, d.gscale ? *d.gscale : 1.f)));
   const int64_t pc = p * d.C + c;
 
   // x images: columns past n_in stay zero
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(512) void q2_bwd_bf16_kernel(d3a_q2_bwd_desc d) {
   // h1 unit i = t & 63, rows 4 (t >> 6) .. + 3; x element(s) t, t + 512, ..).
   // The g rows are wave-uniform (scalar loads); h2 / h1 values stay packed.
   const int so = t & 255, sr = 16 * (w >> 2);
-  const int hi = t & 63, hr = 4 * (t >> 6);
+  const int hi = t & 63, hr = 4 * w;  // (t >> 6 == w: wave-uniform rows)
   const float w3o = (d.w3 + c * d.sw3)[so];
   constexpr int XE = (BB_SB * (XB < 48 ? XB : 48) + 511) / 512;  // x elements per thread
   struct Stage {
@@ -291,19 +292,22 @@ __global__ __launch_bounds__(512) void q2_bwd_bf16_kernel(d3a_q2_bwd_desc d) {
   const unsigned short* h2u = reinterpret_cast<const unsigned short*>(h2g);
   const unsigned short* h1u = reinterpret_cast<const unsigned short*>(h1g);
   auto clamp_row = [&](int r) { return r < rows ? r : rows - 1; };
+  // row indices are wave-uniform (sr, hr from the wave index), so each load is
+  // a scalar row base plus the lane's 32-bit column offset (no per-lane 64-bit
+  // address arithmetic: the staging is VALU-bound)
   auto load_stage = [&](Stage& S, int sb) {
-    const int base = rb0 + sb * BB_SB;
+    const int base = __builtin_amdgcn_readfirstlane(rb0 + sb * BB_SB);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const unsigned a = h2u[clamp_row(base + sr + 2 * j) * B_H + so];
-      const unsigned b = h2u[clamp_row(base + sr + 2 * j + 1) * B_H + so];
-      S.h2[j] = a | (b << 16);
+      const unsigned short* ra = h2u + (size_t)clamp_row(base + sr + 2 * j) * B_H;
+      const unsigned short* rb = h2u + (size_t)clamp_row(base + sr + 2 * j + 1) * B_H;
+      S.h2[j] = (unsigned)ra[so] | ((unsigned)rb[so] << 16);
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const unsigned a = h1u[clamp_row(base + hr + 2 * j) * B_H + i0 + hi];
-      const unsigned b = h1u[clamp_row(base + hr + 2 * j + 1) * B_H + i0 + hi];
-      S.h1[j] = a | (b << 16);
+      const unsigned short* ra = h1u + (size_t)clamp_row(base + hr + 2 * j) * B_H + i0;
+      const unsigned short* rb = h1u + (size_t)clamp_row(base + hr + 2 * j + 1) * B_H + i0;
+      S.h1[j] = (unsigned)ra[hi] | ((unsigned)rb[hi] << 16);
     }
 #pragma unroll
     for (int k = 0; k < XE; ++k) {
@@ -315,6 +319,7 @@ __global__ __launch_bounds__(512) void q2_bwd_bf16_kernel(d3a_q2_bwd_desc d) {
   // column sums of the quarter's o (db2, dW3), db3 (thread so == 0 of each half)
   double s_db2 = 0.0, s_dw3 = 0.0, s_db3 = 0.0;
   const bool own_o = (so >> 6) == q;
+  const int n_scaled32 = d.n_scaled < (int64_t)rows ? (int)d.n_scaled : rows;
   auto write_stage = [&](const Stage& S, int sb) {
     const int b2 = sb & 1;
     const int base = rb0 + sb * BB_SB;
@@ -326,23 +331,31 @@ __global__ __launch_bounds__(512) void q2_bwd_bf16_kernel(d3a_q2_bwd_desc d) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) gv[j] = gg[gr0 + j < rows ? gr0 + j : rows - 1];
     __builtin_amdgcn_sched_barrier(0);
-    // per element: ~8 VALU (the staging was VALU-bound at ~30): fp32 sums
-    // over the sub-block's 16 rows, one fp64 accumulation per sub-block
+    // row factors: 0 past the last row, gscale on the scaled rows (uniform
+    // selects on scalar registers, one multiply per row)
+    // per element ~6 VALU (the staging is VALU-bound: 4 cycles per wave-wide
+    // VALU instruction, two waves per SIMD): the row factors g' w3[o] formed
+    // once per row (row index and bounds are wave-uniform, so their tests are
+    // scalar), fp32 sums over the sub-block's 16 rows, one fp64 accumulation
+    // per sub-block
     float dz[16];
     float f_db2 = 0.f, f_dw3 = 0.f, f_db3 = 0.f;
+    const int nsc = n_scaled32, gl = rows - gr0;  // rows gr0 + j valid for j < gl
+    float gp[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const int r = gr0 + j;  // uniform
-      float gp = gv[j];
-      if (r < d.n_scaled) gp *= gs;
-      if (r >= rows) gp = 0.f;
+      const float mult = j < gl ? (gr0 + j < nsc ? gs : 1.f) : 0.f;
+      gp[j] = gv[j] * mult;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
       const unsigned pk = S.h2[j >> 1];
       const unsigned bits = (j & 1) ? (pk & 0xffff0000u) : (pk << 16);
-      const float h2v = r < rows ? __builtin_bit_cast(float, bits) : 0.f;
-      dz[j] = (int)bits > 0 && r < rows ? gp * w3o : 0.f;  // h2 > 0 (bf16 sign, nonzero)
+      const float h2v = __builtin_bit_cast(float, bits);  // (rows past the end: gp = 0)
+      dz[j] = (int)bits > 0 ? gp[j] * w3o : 0.f;  // h2 > 0 (bf16 sign, nonzero)
       f_db2 += dz[j];
-      f_dw3 = fmaf(gp, h2v, f_dw3);
-      f_db3 += gp;
+      f_dw3 = fmaf(gp[j], h2v, f_dw3);
+      f_db3 += gp[j];
     }
     if (own_o) {
       s_db2 += (double)f_db2;
@@ -355,13 +368,21 @@ __global__ __launch_bounds__(512) void q2_bwd_bf16_kernel(d3a_q2_bwd_desc d) {
       v0[j] = (__bf16)dz[j];
       v1[j] = (__bf16)dz[8 + j];
     }
+    if constexpr (!(PROBE & 8)) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      L.dzr[b2][(sr + j) * BB_LDR + so] = v0[j];
-      L.dzr[b2][(sr + 8 + j) * BB_LDR + so] = v1[j];
+      for (int j = 0; j < 8; ++j) {
+        L.dzr[b2][(sr + j) * BB_LDR + so] = v0[j];
+        L.dzr[b2][(sr + 8 + j) * BB_LDR + so] = v1[j];
+      }
+    } else {
+      s_db3 += (double)(float)v0[0] + (double)(float)v1[7];
     }
-    *reinterpret_cast<bf16x8*>(&L.dzt[b2][so * BB_LDT + sr]) = v0;
-    *reinterpret_cast<bf16x8*>(&L.dzt[b2][so * BB_LDT + sr + 8]) = v1;
+    if constexpr (!(PROBE & 16)) {
+      *reinterpret_cast<bf16x8*>(&L.dzt[b2][so * BB_LDT + sr]) = v0;
+      *reinterpret_cast<bf16x8*>(&L.dzt[b2][so * BB_LDT + sr + 8]) = v1;
+    } else {
+      s_db3 += (double)(float)v0[3] + (double)(float)v1[4];
+    }
     unsigned hv[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -590,6 +611,9 @@ extern "C" int d3a_q2_bwd_bf16(const d3a_q2_bwd_desc* dp, void* stream) {
       case 2: hipLaunchKernelGGL((q2_bwd_bf16_kernel<32, 2>), grid, block, 0, st, d); break;
       case 3: hipLaunchKernelGGL((q2_bwd_bf16_kernel<32, 3>), grid, block, 0, st, d); break;
       case 4: hipLaunchKernelGGL((q2_bwd_bf16_kernel<32, 4>), grid, block, 0, st, d); break;
+      case 8: hipLaunchKernelGGL((q2_bwd_bf16_kernel<32, 8>), grid, block, 0, st, d); break;
+      case 16: hipLaunchKernelGGL((q2_bwd_bf16_kernel<32, 16>), grid, block, 0, st, d); break;
+      case 24: hipLaunchKernelGGL((q2_bwd_bf16_kernel<32, 24>), grid, block, 0, st, d); break;
       default: hipLaunchKernelGGL((q2_bwd_bf16_kernel<32, 7>), grid, block, 0, st, d); break;
     }
     D3A_LAUNCH_CHECK("d3a_q2_bwd_bf16");

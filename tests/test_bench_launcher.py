@@ -90,3 +90,26 @@ def test_bench_hung_rank_exits_in_bounded_time():
     assert r.returncode != 0
     assert el < 120, el
     assert "did not finish within" in r.stderr
+
+
+def test_bench_all_reduce_accounting():
+    """bench.py's data-parallel line: the all-reduces one eager update issues
+    are recorded (calls, dtype, bytes) and then disarmed, so the graph capture
+    and the timed replays are not counted."""
+    import types
+    import torch
+    sys.path.insert(0, ROOT)
+    import bench
+    seen = []
+    dp = types.SimpleNamespace(all_reduce_sum=lambda t: seen.append(t.numel()))
+    algo = types.SimpleNamespace(impl=types.SimpleNamespace(_dp=dp))
+    log = bench._record_all_reduces(algo)
+    for n in (2, 151_000, 77_000, 8):  # scalar grads, critic, actor, metrics
+        algo.impl._dp.all_reduce_sum(torch.zeros(n))
+    log["armed"] = False
+    algo.impl._dp.all_reduce_sum(torch.zeros(5))  # a later (captured) call
+    assert seen == [2, 151_000, 77_000, 8, 5]  # every call still reaches the backend
+    out = bench.measure_all_reduces(log, ws=1)
+    assert out["calls_per_step"] == 4
+    assert out["bytes_per_step"] == 4 * (2 + 151_000 + 77_000 + 8)
+    assert bench._record_all_reduces(types.SimpleNamespace(impl=types.SimpleNamespace(_dp=None))) is None

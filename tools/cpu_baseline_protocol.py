@@ -40,8 +40,13 @@ def timed_run(algo: str, threads: int, steps: int, warmup: int) -> float:
     for _ in range(warmup):
         step()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    last = t0
+    for i in range(steps):
         step()
+        now = time.perf_counter()
+        if now - last > 30:  # progress (a silent GPU-box command is taken for hung)
+            print(f"  {threads} threads: {i + 1}/{steps} steps, {now - t0:.0f}s", flush=True)
+            last = now
     return steps / (time.perf_counter() - t0)
 
 
