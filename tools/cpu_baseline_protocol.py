@@ -88,7 +88,11 @@ def main():
     ap.add_argument("--runs", type=int, default=5)
     ap.add_argument("--out", default=None)
     ap.add_argument("--threads", type=int, default=None,
-                    help="all-cores leg thread count (default: physical cores)")
+                    help="physical-cores leg thread count (default: physical cores)")
+    ap.add_argument("--phys-steps", type=int, default=None,
+                    help="steps per physical-cores run (default --steps; the leg can run "
+                         "far slower than the best thread count on a shared host)")
+    ap.add_argument("--phys-runs", type=int, default=None)
     ap.add_argument("--sweep", default="", help="comma-separated thread counts")
     ap.add_argument("--sweep-seconds", type=float, default=10.0)
     ap.add_argument("--single-on-core", type=int, default=None, help=argparse.SUPPRESS)
@@ -100,13 +104,30 @@ def main():
     import bench
     host = bench.host_cpu()
     host["physical_cores"] = physical_cores()
-    n_all = args.threads or host["physical_cores"]
-    print(f"host {host}; all-cores leg {n_all} threads", flush=True)
+    n_phys = args.threads or host["physical_cores"]
+    print(f"host {host}; physical-cores leg {n_phys} threads", flush=True)
     sw = sweep(args.algo, [int(v) for v in args.sweep.split(",") if v], args.sweep_seconds)
-    allc = []
-    for r in range(args.runs):
-        allc.append(timed_run(args.algo, n_all, args.steps, args.warmup))
-        print(f"all cores run {r}: {allc[-1]:.3f} steps/s", flush=True)
+    # legs: the host's physical core count (BASELINE.md:27-28), the fastest
+    # thread count of the sweep (when it differs), one thread
+    legs = {}
+    phys_steps, phys_runs = args.phys_steps or args.steps, args.phys_runs or args.runs
+    runs = []
+    for r in range(phys_runs):
+        runs.append(timed_run(args.algo, n_phys, phys_steps, min(args.warmup, phys_steps)))
+        print(f"physical-cores run {r}: {runs[-1]:.3f} steps/s", flush=True)
+    legs["physical_cores"] = {"threads": n_phys, "median": statistics.median(runs), "runs": runs,
+                              "steps": phys_steps, "warmup": min(args.warmup, phys_steps),
+                              "note": "torch.set_num_threads(physical cores of the host)"}
+    if sw:
+        best = max(sw, key=lambda w: w["steps_per_s"])["threads"]
+        if best != n_phys and best != 1:
+            runs = []
+            for r in range(args.runs):
+                runs.append(timed_run(args.algo, best, args.steps, args.warmup))
+                print(f"best-threads ({best}) run {r}: {runs[-1]:.3f} steps/s", flush=True)
+            legs["best_threads"] = {"threads": best, "median": statistics.median(runs),
+                                    "runs": runs, "steps": args.steps, "warmup": args.warmup,
+                                    "note": "the fastest thread count of the sweep"}
     cores = sorted(os.sched_getaffinity(0))
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--algo", args.algo,
                                "--steps", str(args.steps), "--warmup", str(args.warmup),
@@ -119,16 +140,16 @@ def main():
         assert p.returncode == 0, out
         one.append(json.loads(out.strip().splitlines()[-1])["sps"])
     print(f"1-thread runs: {[round(v, 3) for v in one]}", flush=True)
+    legs["one_thread"] = {"threads": 1, "median": statistics.median(one), "runs": one,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "note": "runs concurrent, pinned to distinct cores"}
+    # "all_cores": the multi-thread leg bench.py quotes -- the faster of the
+    # physical-cores and best-threads legs, labelled with its thread count
+    allc = max((v for k, v in legs.items() if k != "one_thread"), key=lambda v: v["median"])
     res = {"algo": args.algo, "unit": "gradient-steps/s", "steps": args.steps,
-           "warmup": args.warmup, "runs": args.runs,
-           "all_cores": {"threads": n_all, "median": statistics.median(allc), "runs": allc,
-                         "note": ("physical cores of the host (BASELINE.md:27-28)"
-                                  if n_all == host["physical_cores"] else
-                                  f"{n_all} threads (--threads)")},
-           "thread_sweep": sw,
-           "one_thread": {"threads": 1, "median": statistics.median(one), "runs": one,
-                          "note": "runs concurrent, pinned to distinct cores"},
-           "host": host}
+           "warmup": args.warmup, "runs": args.runs, "legs": legs,
+           "all_cores": dict(allc, note=allc["note"] + " (the faster multi-thread leg)"),
+           "thread_sweep": sw, "one_thread": legs["one_thread"], "host": host}
     print(json.dumps(res))
     if args.out:
         with open(args.out, "w") as f:
