@@ -60,7 +60,10 @@ struct FwdLdsB {
 // both hidden layers and computes the transposed tiles C^T[unit][row] (W as
 // the A operand from registers, activation rows as B from LDS), so a lane
 // holds one row and four runs of four consecutive units.
-template <int XL>
+// PROBE (timing probes only, D3A_FWDB_PROBE): bit 0 skips the kept-activation
+// stores, bit 1 loads one W1 fragment pair and replicates it, bit 2 skips the
+// layer-2 MFMAs.
+template <int XL, int PROBE = 0>
 __global__ __launch_bounds__(512) void q2_fwd_bf16_kernel(d3a_mlp_fwd_desc d) {
   constexpr int LDX = XL + 8;
   constexpr int NS0 = XL / 16;  // layer-1 MFMA steps
@@ -82,13 +85,23 @@ __global__ __launch_bounds__(512) void q2_fwd_bf16_kernel(d3a_mlp_fwd_desc d) {
   __bf16* const h0g = (!aux && d.h[0]) ? reinterpret_cast<__bf16*>(d.h[0]) + c * d.sh : nullptr;
   __bf16* const h1g = (!aux && d.h[1]) ? reinterpret_cast<__bf16*>(d.h[1]) + c * d.sh : nullptr;
 
-  // ---- prologue: W1 / W0 fragments to registers (bf16), x rows to LDS (bf16)
-  const float* W1 = d.W[1] + wdel + c * d.sW[1];
-  bf16x8 w1f[16];  // step s: W1[col][16 s + 8 lh + j]
+  // ---- prologue, loads in the order they are needed (the vector memory
+  // counter retires in order): the input rows, W0, then W1 as raw fp32 -- W1 is
+  // converted to bf16 fragments only after layer 1, so its 256 KB per workgroup
+  // streams in behind the input staging and the first layer
+  const float* xb = aux ? d.aux_x + c * d.aux_sxb : d.x + c * d.sxb;
+  const int64_t ldx = aux ? d.aux_ldx : d.ldx;
+  constexpr int X4 = XL / 4;
+  constexpr int XS = (B_RB * X4 + 511) / 512;  // float4 pieces of x per thread
+  float xv[XS][4];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const float* p = W1 + col * B_H + 16 * s + 8 * lh;
-    w1f[s] = cvt8(*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 4));
+  for (int i = 0; i < XS; ++i) {
+    const int e = t + 512 * i;
+    const int m = e / X4, k4 = (e - m * X4) * 4;
+    const int r = m0 + m;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      xv[i][j] = (e < B_RB * X4 && r < rend && k4 + j < nin) ? xb[r * ldx + k4 + j] : 0.f;
   }
   const float* W0 = d.W[0] + wdel + c * d.sW[0];
   bf16x8 w0f[NS0];
@@ -100,23 +113,23 @@ __global__ __launch_bounds__(512) void q2_fwd_bf16_kernel(d3a_mlp_fwd_desc d) {
       w0f[s][j] = (__bf16)(k < nin ? W0[col * nin + k] : 0.f);
     }
   }
-  const float b2v = (d.b[2] + wdel + c * d.sb[2])[0];
-  {
-    const float* xb = aux ? d.aux_x + c * d.aux_sxb : d.x + c * d.sxb;
-    const int64_t ldx = aux ? d.aux_ldx : d.ldx;
-    constexpr int X4 = XL / 4;
-    for (int e = t; e < B_RB * X4; e += 512) {
-      const int m = e / X4, k4 = (e - m * X4) * 4;
-      const int r = m0 + m;
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (r < rend) {
-        const float* p = xb + r * ldx + k4;
+  const float* W1 = d.W[1] + wdel + c * d.sW[1];
+  float4 w1raw[32];  // step s: W1[col][16 s + 8 lh + 0..7] as two float4
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = k4 + j < nin ? p[j] : 0.f;
-      }
+  for (int s = 0; s < 16; ++s) {
+    const float* p = W1 + col * B_H + 16 * ((PROBE & 2) ? 0 : s) + 8 * lh;
+    w1raw[2 * s] = *reinterpret_cast<const float4*>(p);
+    w1raw[2 * s + 1] = *reinterpret_cast<const float4*>(p + 4);
+  }
+  const float b2v = (d.b[2] + wdel + c * d.sb[2])[0];
+#pragma unroll
+  for (int i = 0; i < XS; ++i) {
+    const int e = t + 512 * i;
+    if (e < B_RB * X4) {
+      const int m = e / X4, k4 = (e - m * X4) * 4;
       bf16x4 b;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = (__bf16)v[j];
+      for (int j = 0; j < 4; ++j) b[j] = (__bf16)xv[i][j];
       *reinterpret_cast<bf16x4*>(&L.u.x[m * LDX + k4]) = b;
     }
   }
@@ -161,11 +174,14 @@ __global__ __launch_bounds__(512) void q2_fwd_bf16_kernel(d3a_mlp_fwd_desc d) {
   }
   load_units(d.b[1] + wdel + c * d.sb[1], bb);
   load_units(d.W[2] + wdel + c * d.sW[2], ww);
+  bf16x8 w1f[16];  // step s: W1[col][16 s + 8 lh + j]
+#pragma unroll
+  for (int s = 0; s < 16; ++s) w1f[s] = cvt8(w1raw[2 * s], w1raw[2 * s + 1]);
   __syncthreads();  // layer-1 rows in LDS; x dead (hp aliases it)
 
   // h[0] leaves from LDS: wave w copies rows 16 w .. 16 w + 15 (two rows of
   // 512 B per instruction)
-  if (h0g) {
+  if (h0g && !(PROBE & 1)) {
 #pragma unroll
     for (int j = 0; j < 16; j += 2) {
       const int rl = 16 * w + j + lh;
@@ -183,13 +199,24 @@ __global__ __launch_bounds__(512) void q2_fwd_bf16_kernel(d3a_mlp_fwd_desc d) {
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    // the tile's 16 B fragments read ahead of its MFMA chain (LDS latency paid
+    // once per tile, not per MFMA)
+    bf16x8 bf[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) acc = mfma16(w1f[k], *reinterpret_cast<const bf16x8*>(Bp + 16 * k), acc);
+    for (int k = 0; k < 16; ++k) bf[k] = *reinterpret_cast<const bf16x8*>(Bp + 16 * k);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (PROBE & 4) {
+        acc[k] += (float)bf[k][0] * (float)w1f[k][1];
+      } else {
+        acc = mfma16(w1f[k], bf[k], acc);
+      }
+    }
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = fmaxf(acc[r] + bb[r], 0.f);
     const int rb = m0 + s * B_SB;
-    if (kept(h1g, rb)) {
+    if (kept(h1g, rb) && !(PROBE & 1)) {
 #pragma unroll
       for (int R = 0; R < 4; ++R) put4(h1g + (rb + li) * B_H + unit_of(R), v + 4 * R);
     }
@@ -575,7 +602,19 @@ extern "C" int d3a_q2_fwd_bf16(const d3a_mlp_fwd_desc* dp, void* stream) {
   const dim3 grid((unsigned)nb, 1, (unsigned)d.C);
   const int xl = (d.n_in + 15) / 16 * 16;
   hipStream_t st = (hipStream_t)stream;
-  if (xl == 16)
+  static const int probe = [] {
+    const char* e = getenv("D3A_FWDB_PROBE");
+    return e ? atoi(e) : 0;
+  }();
+  if (probe && xl == 16) {
+    switch (probe) {
+      case 1: hipLaunchKernelGGL((q2_fwd_bf16_kernel<16, 1>), grid, dim3(512), 0, st, d); break;
+      case 2: hipLaunchKernelGGL((q2_fwd_bf16_kernel<16, 2>), grid, dim3(512), 0, st, d); break;
+      case 3: hipLaunchKernelGGL((q2_fwd_bf16_kernel<16, 3>), grid, dim3(512), 0, st, d); break;
+      case 4: hipLaunchKernelGGL((q2_fwd_bf16_kernel<16, 4>), grid, dim3(512), 0, st, d); break;
+      default: hipLaunchKernelGGL((q2_fwd_bf16_kernel<16, 7>), grid, dim3(512), 0, st, d); break;
+    }
+  } else if (xl == 16)
     hipLaunchKernelGGL(q2_fwd_bf16_kernel<16>, grid, dim3(512), 0, st, d);
   else if (xl == 32)
     hipLaunchKernelGGL(q2_fwd_bf16_kernel<32>, grid, dim3(512), 0, st, d);
