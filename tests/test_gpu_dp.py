@@ -139,38 +139,55 @@ def test_dp_two_ranks_match_global_batch(tmp_path, case):
         # itself not reproducible to better than ~1e-2 on its cancelling hidden
         # layers (threaded reductions + ReLU ties, measured 3e-4 .. 1.2e-2
         # between runs), so the fp64 evaluation is the arbiter, as in
-        # test_gpu_cql_parity.test_cql_grad_accuracy_vs_fp64.  Bar 1e-3
-        # (max-normalised): the importance-sampled rows' softmax weights cancel
+        # test_gpu_cql_parity.test_cql_grad_accuracy_vs_fp64.  Bar, per tensor
+        # (max-normalised): HIP within max(1e-3, 2 x the fp32 oracle's own
+        # error) of fp64 — the importance-sampled rows' softmax weights cancel
         # the data rows' term across 15,872 rows, which amplifies fp32 rounding
-        # on the hidden layers' gradients (measured 1.8e-4 on c0 layer 1;
-        # 1e-5 holds at the 7,936-row B = 256 shapes of the parity tests)
+        # on the hidden layers' gradients (measured 1.8e-4 .. 1.1e-3 across
+        # tensors and draws; 1e-5 holds at the 7,936-row B = 256 shapes of the
+        # parity tests), so the reference's own fp32 arithmetic on the same
+        # state and draws sets the envelope
         from cql_helpers import make_oracle
         from oracle.cql import Batch
-        o64 = make_oracle(D, A, [H] * L, N, seed=0)
-        for k, v in sd0.items():
-            getattr(o64, k).load_state_dict(v)
-        for mod in (o64._q_func, o64._policy, o64._targ_q_func, o64._targ_policy, o64._log_temp,
-                    o64._log_alpha):
-            mod.double()
+        from arbiter_helpers import max_rel
         arrs, nz, _ = batches[0]
         tb = Batch.from_numpy(*arrs)
-        tb64 = Batch(*(getattr(tb, f).double() for f in tb.__dataclass_fields__))
-        nz64 = CQLNoise(**{k: v.double() for k, v in nz.items()})
-        o64.update_temp(tb64, nz64.eps_temp)
-        o64.update_alpha(tb64, nz64)
-        o64.update_critic(tb64, nz64)
-        g64 = {"_q_func": {}}
-        for key_, seg_, c, sl_ in ref._critic_refs():
-            qf = o64._q_func.q_funcs[c]
-            l = int(key_.split("_fcs.")[1].split(".")[0]) if "_fcs." in key_ else L
-            fc = (list(qf._encoder._fcs) + [qf._fc])[l]
-            g64["_q_func"][key_] = (fc.weight if key_.endswith("weight") else fc.bias).grad.detach().clone()
-        o64.update_actor(tb64, nz64.eps_actor)
-        g64["_policy"] = {k: p.grad.detach().clone() for k, p in o64._policy.named_parameters()}
+
+        def oracle_grads(dtype):
+            o = make_oracle(D, A, [H] * L, N, seed=0)
+            for k, v in sd0.items():
+                getattr(o, k).load_state_dict(v)
+            for mod in (o._q_func, o._policy, o._targ_q_func, o._targ_policy, o._log_temp,
+                        o._log_alpha):
+                mod.to(dtype)
+            tbd = Batch(*(getattr(tb, f).to(dtype) for f in tb.__dataclass_fields__))
+            nzd = CQLNoise(**{k: v.to(dtype) for k, v in nz.items()})
+            o.update_temp(tbd, nzd.eps_temp)
+            o.update_alpha(tbd, nzd)
+            o.update_critic(tbd, nzd)
+            g = {"_q_func": {}}
+            for key_, seg_, c, sl_ in ref._critic_refs():
+                qf = o._q_func.q_funcs[c]
+                l = int(key_.split("_fcs.")[1].split(".")[0]) if "_fcs." in key_ else L
+                fc = (list(qf._encoder._fcs) + [qf._fc])[l]
+                g["_q_func"][key_] = (fc.weight if key_.endswith("weight")
+                                      else fc.bias).grad.detach().double().clone()
+            o.update_actor(tbd, nzd.eps_actor)
+            g["_policy"] = {k: p.grad.detach().double().clone()
+                            for k, p in o._policy.named_parameters()}
+            return o, g
+
+        o64, g64 = oracle_grads(torch.float64)
+        _, g32 = oracle_grads(torch.float32)
         for key, refs, lr in (("_q_func", ref._critic_refs(), 3e-4),
                               ("_policy", ref._policy_refs(), 1e-4)):
             g_dp = {k: gd[f"{key}/{k}"].double() for k, *_ in refs}
-            check_grads(f"dp vs fp64 oracle {key}", g_dp, g64[key], tol=1e-3)
+            for k, r64 in g64[key].items():
+                e_hip, e32 = max_rel(g_dp[k], r64), max_rel(g32[key][k], r64)
+                bar = max(1e-3, 2.0 * e32)
+                print(f"  dp vs fp64 oracle {key} {k}: hip {e_hip:.1e} oracle32 {e32:.1e} "
+                      f"bar {bar:.1e}")
+                assert e_hip <= bar, (key, k, e_hip, e32)
             p64 = {k: v.detach() for k, v in getattr(o64, key).named_parameters()}
             pw, namp = check_params_adam1(f"dp vs fp64 oracle {key}", sd0[key], sd[key], p64,
                                           g_dp, lr=lr)
