@@ -148,6 +148,18 @@ class SacActorHeadDesc(C.Structure):
         ("H", C.c_int32), ("dW_part", vp), ("db_part", vp),
         ("dq_dz", vp), ("lddqz", C.c_int64), ("sdz_c", C.c_int64),
         ("w0", vp), ("ldw0", C.c_int64), ("sw0_c", C.c_int64), ("H0", C.c_int32),
+        ("dq_min", C.c_int32), ("dq_scale", C.c_float),
+    ]
+
+
+class SacActorQDesc(C.Structure):
+    _fields_ = [
+        ("x", vp), ("ldx", C.c_int64),
+        ("W0", vp), ("b0", vp), ("W1", vp), ("b1", vp), ("wh", vp), ("bh", vp),
+        ("q", vp), ("sqc", C.c_int64),
+        ("dq_da", vp), ("ld_da", C.c_int64), ("sda_c", C.c_int64),
+        ("B", C.c_int32), ("C", C.c_int32), ("n_in", C.c_int32), ("A", C.c_int32),
+        ("da_off", C.c_int32),
     ]
 
 
@@ -453,6 +465,7 @@ _SIGNATURES = {
     "d3a_cql_loss": (C.c_int, [C.POINTER(CqlLossDesc), vp]),
     "d3a_sac_actor_dq": (C.c_int, [vp, C.c_int64, C.c_int32, C.c_int32, vp, C.c_int64, vp]),
     "d3a_sac_actor_head": (C.c_int, [C.POINTER(SacActorHeadDesc), vp]),
+    "d3a_sac_actor_q": (C.c_int, [C.POINTER(SacActorQDesc), vp]),
     "d3a_gather_batch": (C.c_int, [C.POINTER(GatherDesc), vp]),
     "d3a_mlp_fwd": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_gemm_sbf16": (C.c_int, [C.POINTER(GemmDesc), C.c_int32, vp]),

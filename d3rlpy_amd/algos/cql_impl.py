@@ -51,6 +51,9 @@ _HEAD_MIN = os.environ.get("D3A_HEAD_MIN", "1") == "1"
 # actor phase: dQ/da formed in d3a_sac_actor_head from the critic's first-layer
 # pre-activation gradient (one input-gradient launch fewer)
 _DQ_IN_HEAD = os.environ.get("D3A_DQ_IN_HEAD", "1") == "1"
+# actor phase: the critic pass at (s, tanh u) and its backward to the action
+# in one launch (d3a_sac_actor_q) for [n_in <= 64, 256, 256, 1] critics
+_ACTOR_Q = os.environ.get("D3A_ACTOR_Q", "1") == "1"
 _DQ_IN_HEAD_MAX_PAIRS = min(32, int(os.environ.get("D3A_DQ_IN_HEAD_MAX_PAIRS", "8")))
 # full update_step: the soft target updates, counters and metric ring ride in
 # the two Adam launches (d3a_adam_step) instead of a d3a_step_end launch
@@ -744,35 +747,16 @@ class _Workspace:
                 ops.call_desc("d3a_cql_loss", l)
             # 6. actor: Q(s, tanh u) with the updated critic, dQ/da, policy backward
             # dL/dq = -1/B on the argmin critic (backward of min over the ensemble)
-            hm = self._head_min_desc()
-            mlp.forward(impl.critic, impl.store, self.x_actor.data_ptr(), True, DA, self.aacts,
-                        skip_head=hm is not None)
+            aq = self._actor_q_desc()
             hd = self.head_desc
-            hd.dq_dz = None
-            if hm is not None:
-                # the Q head and its min-over-members backward in one launch
-                ops.call_desc("d3a_head1_min", hm)
-                net = impl.critic
-                # measured: faster than the input-gradient launch for C * A <= 8
-                # (K2: 6 pairs), slower for K4's 16 pairs
-                fuse = (_DQ_IN_HEAD and net.n_layers >= 2 and net.C <= 4
-                        and net.C * A <= _DQ_IN_HEAD_MAX_PAIRS and net.sizes[1] <= 256)
-                dz0 = mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA,
-                                   self.aacts, self.adq.data_ptr(), 1, B, 0, B,
-                                   weight_grads=False, dx=None if fuse else self.adx,
-                                   head_ready=True)
-                if fuse:
-                    # dQ/da from the first layer's pre-activation gradient, in
-                    # the actor head (the last input-gradient launch is skipped)
-                    hd.dq_dz, hd.lddqz = dz0.data_ptr(), dz0.shape[2]
-                    hd.sdz_c = dz0.shape[1] * dz0.shape[2]
-                    hd.w0, hd.ldw0 = net.W(0, impl.store), net.sizes[0]
-                    hd.sw0_c, hd.H0 = net.sizes[1] * net.sizes[0], net.sizes[1]
+            if aq is not None:
+                # every member's q and unscaled dQ_c/da in one launch; the
+                # actor head applies the min's backward (dq_min)
+                ops.call_desc("d3a_sac_actor_q", aq)
+                hd.dq_dz, hd.dq_min, hd.dq_scale = None, 1, -1.0 / B
             else:
-                mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA,
-                             self.aacts, self.adq.data_ptr(), 1, B, 0, B, weight_grads=False,
-                             dx=self.adx, q_min=self.aacts.out.data_ptr(), sq_b=B,
-                             q_scale=-1.0 / B, g_out=self.adq.data_ptr())
+                hd.dq_min = 0
+                self._actor_critic_layers(B, A, DA)
             ops.call_desc("d3a_sac_actor_head", hd)
             mlp.backward(self.pbwd, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
                          self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B,
@@ -793,6 +777,66 @@ class _Workspace:
         ops.step_end(impl.counters, (1 if critic else 0) | (2 if actor else 0) | rng, self.metrics,
                      self.ring, self.ring_ctr, impl.targ.data if targets else None,
                      impl.store.data if targets else None, impl._tau, metric_scale=mscale)
+
+    def _actor_q_desc(self):
+        """d3a_sac_actor_q descriptor (the actor phase's critic pass, forward
+        and backward to the action, one launch), or None where the critic's
+        shape does not fit it (then the per-layer path)."""
+        impl = self.impl
+        net = impl.critic
+        s = net.sizes
+        if (not _ACTOR_Q or len(s) != 4 or s[1] != 256 or s[2] != 256 or s[3] != 1
+                or s[0] > 64 or self.A > 16):
+            return None
+        d = getattr(self, "_aq_desc", None)
+        if d is None:
+            st = impl.store
+            d = NAT.SacActorQDesc()
+            d.x, d.ldx = self.x_actor.data_ptr(), self.LDX
+            d.W0, d.b0 = net.W(0, st), net.b(0, st)
+            d.W1, d.b1 = net.W(1, st), net.b(1, st)
+            d.wh, d.bh = net.W(2, st), net.b(2, st)
+            d.q, d.sqc = self.aacts.out.data_ptr(), self.B
+            d.dq_da, d.ld_da, d.sda_c = (self.adx.data_ptr(), self.D + self.A,
+                                         self.B * (self.D + self.A))
+            d.B, d.C, d.n_in, d.A, d.da_off = self.B, net.C, s[0], self.A, self.D
+            self._aq_desc = d
+        return d
+
+    def _actor_critic_layers(self, B: int, A: int, DA: int) -> None:
+        """The actor phase's critic pass on the per-layer path: forward, the
+        Q head and min-over-members backward, input gradients (dQ/da into
+        self.adx, or formed by the actor head from the first layer's dz)."""
+        impl = self.impl
+        hm = self._head_min_desc()
+        mlp.forward(impl.critic, impl.store, self.x_actor.data_ptr(), True, DA, self.aacts,
+                    skip_head=hm is not None)
+        hd = self.head_desc
+        hd.dq_dz = None
+        if hm is not None:
+            # the Q head and its min-over-members backward in one launch
+            ops.call_desc("d3a_head1_min", hm)
+            net = impl.critic
+            # measured: faster than the input-gradient launch for C * A <= 8
+            # (K2: 6 pairs), slower for K4's 16 pairs
+            fuse = (_DQ_IN_HEAD and net.n_layers >= 2 and net.C <= 4
+                    and net.C * A <= _DQ_IN_HEAD_MAX_PAIRS and net.sizes[1] <= 256)
+            dz0 = mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA,
+                               self.aacts, self.adq.data_ptr(), 1, B, 0, B,
+                               weight_grads=False, dx=None if fuse else self.adx,
+                               head_ready=True)
+            if fuse:
+                # dQ/da from the first layer's pre-activation gradient, in
+                # the actor head (the last input-gradient launch is skipped)
+                hd.dq_dz, hd.lddqz = dz0.data_ptr(), dz0.shape[2]
+                hd.sdz_c = dz0.shape[1] * dz0.shape[2]
+                hd.w0, hd.ldw0 = net.W(0, impl.store), net.sizes[0]
+                hd.sw0_c, hd.H0 = net.sizes[1] * net.sizes[0], net.sizes[1]
+        else:
+            mlp.backward(self.abwd, impl.store, self.x_actor.data_ptr(), True, DA,
+                         self.aacts, self.adq.data_ptr(), 1, B, 0, B, weight_grads=False,
+                         dx=self.adx, q_min=self.aacts.out.data_ptr(), sq_b=B,
+                         q_scale=-1.0 / B, g_out=self.adq.data_ptr())
 
     @staticmethod
     def _apply(opt: AdamGroup, dp, tail: Optional[dict] = None) -> None:

@@ -467,6 +467,16 @@ __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_
         const float* sc = &s_dq[0][c * 16 + j];
         da += ((sc[0] + sc[64]) + sc[128]) + sc[192];
       }
+    } else if (d.dq_min) {
+      // backward of min over the members: the first member of least q
+      // (head1_min's rule) carries dq_scale, the others nothing
+      int arg = 0;
+      float mn = d.q[b];
+      for (int c = 1; c < C; ++c) {
+        const float v = d.q[c * d.sqc + b];
+        if (v < mn) { mn = v; arg = c; }
+      }
+      da = d.dq_scale * d.dq_da[arg * d.sda_c + b * d.ld_da + d.da_off + j];
     } else {
       for (int c = 0; c < C; ++c) da += d.dq_da[c * d.sda_c + b * d.ld_da + d.da_off + j];
     }
@@ -570,6 +580,8 @@ extern "C" int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream
                          : d->dq_da != nullptr,
                 "d3a_sac_actor_head: dq_dz needs w0, C <= 4, C * A <= 32, 1 <= H0 <= 256 "
                 "(else dq_da)");
+  D3A_CHECK_ARG(!d->dq_min || (!d->dq_dz && d->dq_da && d->q),
+                "d3a_sac_actor_head: dq_min reads dq_da and q (not dq_dz)");
   if (d->dq_dz)
     hipLaunchKernelGGL(sac_actor_head_kernel<true>, dim3((unsigned)d->B + 1), dim3(256), 0,
                        (hipStream_t)stream, *d);

@@ -50,6 +50,7 @@ STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_gemm_wnext", "GemmWnext"),
            ("d3a_head1_bwd_desc", "Head1BwdDesc"), ("d3a_head1_min_desc", "Head1MinDesc"),
            ("d3a_cql_sample_desc", "CqlSampleDesc"), ("d3a_cql_loss_desc", "CqlLossDesc"),
            ("d3a_sac_actor_head_desc", "SacActorHeadDesc"), ("d3a_gather_desc", "GatherDesc"),
+           ("d3a_sac_actor_q_desc", "SacActorQDesc"),
            ("d3a_td3_prep_desc", "Td3PrepDesc"), ("d3a_td3_target_desc", "Td3TargetDesc"),
            ("d3a_td3_critic_loss_desc", "Td3CriticLossDesc"),
            ("d3a_td3bc_actor_desc", "Td3bcActorDesc"), ("d3a_mlp_fwd_desc", "MlpFwdDesc"), ("d3a_dqn_loss_desc", "DqnLossDesc"),
