@@ -148,7 +148,8 @@ class SacActorHeadDesc(C.Structure):
         ("H", C.c_int32), ("dW_part", vp), ("db_part", vp),
         ("dq_dz", vp), ("lddqz", C.c_int64), ("sdz_c", C.c_int64),
         ("w0", vp), ("ldw0", C.c_int64), ("sw0_c", C.c_int64), ("H0", C.c_int32),
-        ("dq_min", C.c_int32), ("dq_scale", C.c_float),
+        ("dq_min", C.c_int32), ("dq_scale", C.c_float), ("n_part", C.c_int32),
+        ("sq_part", C.c_int64), ("sda_part", C.c_int64),
     ]
 
 
@@ -156,11 +157,13 @@ class SacActorQDesc(C.Structure):
     _fields_ = [
         ("x", vp), ("ldx", C.c_int64),
         ("W0", vp), ("b0", vp), ("W1", vp), ("b1", vp), ("wh", vp), ("bh", vp),
-        ("q", vp), ("sqc", C.c_int64),
-        ("dq_da", vp), ("ld_da", C.c_int64), ("sda_c", C.c_int64),
+        ("q", vp), ("dq_da", vp),
         ("B", C.c_int32), ("C", C.c_int32), ("n_in", C.c_int32), ("A", C.c_int32),
         ("da_off", C.c_int32),
     ]
+
+
+ACTOR_Q_PARTS = 4  # D3A_ACTOR_Q_PARTS
 
 
 class GatherDesc(C.Structure):

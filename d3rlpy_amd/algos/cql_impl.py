@@ -573,6 +573,13 @@ class _Workspace:
             h.H = pol.sizes[Lp - 1]
             h.dW_part = self.pgrads.get(pol.wname(Lp - 1)).data_ptr()
             h.db_part = self.pgrads.get(pol.bname(Lp - 1)).data_ptr()
+        if self._actor_q_desc() is not None:
+            # d3a_sac_actor_q's parts of every member's q and unscaled dQ/da
+            B, C, A = self.B, impl.critic.C, self.A
+            h.q, h.sqc, h.sq_part = self.aq_q.data_ptr(), B, C * B
+            h.dq_da, h.ld_da, h.da_off, h.sda_c = self.aq_j.data_ptr(), A, 0, B * A
+            h.sda_part, h.n_part = C * B * A, NAT.ACTOR_Q_PARTS
+            h.dq_min, h.dq_scale = 1, -1.0 / B
         self.head_desc = h
 
     # ---------------------------------------------------------------- inputs
@@ -750,12 +757,11 @@ class _Workspace:
             aq = self._actor_q_desc()
             hd = self.head_desc
             if aq is not None:
-                # every member's q and unscaled dQ_c/da in one launch; the
-                # actor head applies the min's backward (dq_min)
+                # every member's q and unscaled dQ_c/da (four parts) in one
+                # launch; the actor head sums the parts and applies the min's
+                # backward (dq_min, set in _build_descs)
                 ops.call_desc("d3a_sac_actor_q", aq)
-                hd.dq_dz, hd.dq_min, hd.dq_scale = None, 1, -1.0 / B
             else:
-                hd.dq_min = 0
                 self._actor_critic_layers(B, A, DA)
             ops.call_desc("d3a_sac_actor_head", hd)
             mlp.backward(self.pbwd, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
@@ -791,15 +797,17 @@ class _Workspace:
         d = getattr(self, "_aq_desc", None)
         if d is None:
             st = impl.store
+            P, B, C, A = NAT.ACTOR_Q_PARTS, self.B, net.C, self.A
+            dev = self.x_actor.device
+            self.aq_q = torch.zeros(P, C, B, dtype=torch.float32, device=dev)
+            self.aq_j = torch.zeros(P, C, B, A, dtype=torch.float32, device=dev)
             d = NAT.SacActorQDesc()
             d.x, d.ldx = self.x_actor.data_ptr(), self.LDX
             d.W0, d.b0 = net.W(0, st), net.b(0, st)
             d.W1, d.b1 = net.W(1, st), net.b(1, st)
             d.wh, d.bh = net.W(2, st), net.b(2, st)
-            d.q, d.sqc = self.aacts.out.data_ptr(), self.B
-            d.dq_da, d.ld_da, d.sda_c = (self.adx.data_ptr(), self.D + self.A,
-                                         self.B * (self.D + self.A))
-            d.B, d.C, d.n_in, d.A, d.da_off = self.B, net.C, s[0], self.A, self.D
+            d.q, d.dq_da = self.aq_q.data_ptr(), self.aq_j.data_ptr()
+            d.B, d.C, d.n_in, d.A, d.da_off = B, C, s[0], A, self.D
             self._aq_desc = d
         return d
 

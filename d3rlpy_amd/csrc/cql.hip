@@ -411,11 +411,18 @@ __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_
   const int A = d.A, B = d.B, C = d.C;
   const int64_t b = blockIdx.x;
   const float et = d.scalars[0];
+  // Q_c(r): the parts of d3a_sac_actor_q summed in order (dq_min), else one value
+  const int np = d.dq_min ? d.n_part : 1;
+  auto qv = [&](int c, int64_t r) {
+    float v = d.q[c * d.sqc + r];
+    for (int p = 1; p < np; ++p) v += d.q[p * d.sq_part + c * d.sqc + r];
+    return v;
+  };
   if (b == B) {
     float lsum = 0.f;
     for (int r = tid; r < B; r += blockDim.x) {
-      float qmin = d.q[r];
-      for (int c = 1; c < C; ++c) qmin = fminf(qmin, d.q[c * d.sqc + r]);
+      float qmin = qv(0, r);
+      for (int c = 1; c < C; ++c) qmin = fminf(qmin, qv(c, r));
       lsum += et * d.logp[r] - qmin;
     }
     const float tot = block_sum(lsum, scratch);
@@ -471,12 +478,15 @@ __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_
       // backward of min over the members: the first member of least q
       // (head1_min's rule) carries dq_scale, the others nothing
       int arg = 0;
-      float mn = d.q[b];
+      float mn = qv(0, b);
       for (int c = 1; c < C; ++c) {
-        const float v = d.q[c * d.sqc + b];
+        const float v = qv(c, b);
         if (v < mn) { mn = v; arg = c; }
       }
-      da = d.dq_scale * d.dq_da[arg * d.sda_c + b * d.ld_da + d.da_off + j];
+      const float* jp = d.dq_da + arg * d.sda_c + b * d.ld_da + d.da_off + j;
+      float jv = jp[0];
+      for (int p = 1; p < np; ++p) jv += jp[p * d.sda_part];
+      da = d.dq_scale * jv;
     } else {
       for (int c = 0; c < C; ++c) da += d.dq_da[c * d.sda_c + b * d.ld_da + d.da_off + j];
     }
@@ -580,8 +590,8 @@ extern "C" int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream
                          : d->dq_da != nullptr,
                 "d3a_sac_actor_head: dq_dz needs w0, C <= 4, C * A <= 32, 1 <= H0 <= 256 "
                 "(else dq_da)");
-  D3A_CHECK_ARG(!d->dq_min || (!d->dq_dz && d->dq_da && d->q),
-                "d3a_sac_actor_head: dq_min reads dq_da and q (not dq_dz)");
+  D3A_CHECK_ARG(!d->dq_min || (!d->dq_dz && d->dq_da && d->q && d->n_part >= 1),
+                "d3a_sac_actor_head: dq_min reads dq_da and q in n_part >= 1 parts (not dq_dz)");
   if (d->dq_dz)
     hipLaunchKernelGGL(sac_actor_head_kernel<true>, dim3((unsigned)d->B + 1), dim3(256), 0,
                        (hipStream_t)stream, *d);

@@ -602,37 +602,44 @@ typedef struct d3a_sac_actor_head_desc {
   int64_t ldw0, sw0_c;
   int32_t H0;
   /* dq_min != 0 (with dq_da, not dq_dz): dq_da holds each critic's UNSCALED
-   * dQ_c/da (d3a_sac_actor_q); the backward of min over the ensemble is
-   * applied here: dQ/da = dq_scale * dq_da[c*] with c* the first member of
-   * least q (`y.min(dim=0).values`, d3rlpy/models/torch/q_functions/
+   * dQ_c/da as n_part partial sums (d3a_sac_actor_q), q likewise:
+   *   Q_c(b)      = sum_{p < n_part} q[p*sq_part + c*sqc + b]
+   *   dQ_c/da_j   = sum_{p < n_part} dq_da[p*sda_part + c*sda_c + b*ld_da + da_off + j]
+   * (parts summed in order); the backward of min over the ensemble is
+   * applied here: dQ/da = dq_scale * dQ_m/da with m the first member of
+   * least Q (`y.min(dim=0).values`, d3rlpy/models/torch/q_functions/
    * ensemble_q_function.py:12-13) and dq_scale = -1/B the actor loss's d/dq
    * ((entropy - q_t).mean(), d3rlpy/algos/torch/sac_impl.py:114-121)      */
   int32_t dq_min;
   float dq_scale;
+  int32_t n_part;
+  int64_t sq_part, sda_part;
 } d3a_sac_actor_head_desc;
 int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream);
 
 /* ---- the actor phase's critic pass in one launch (CQL / SAC actor update,
  *      d3rlpy/algos/torch/sac_impl.py:120 `self._q_func(obs, action, "min")`
  *      and its autograd back to the action input):
- * for an ensemble [n_in, 256, 256, 1] of C members and B rows x[b] = (s, a):
- *   q[c*sqc + b]                        = Q_c(x[b])   (forward, every member)
- *   dq_da[c*sda_c + b*ld_da + da_off + j] = dQ_c/dx_(da_off+j) at x[b], j < A,
- * UNSCALED (dL/dQ_c = 1); d3a_sac_actor_head (dq_min = 1) selects the argmin
- * member and scales.  Replaces the per-layer forward, d3a_head1_min and the
- * input-gradient launches of the actor phase.  One workgroup per 16 rows and
- * member; exact-fp32 MFMA chains.  Requires n_in <= 64, A <= 16,
- * da_off + A <= n_in, W1 / b rows 16-byte aligned.                         */
+ * for an ensemble [n_in, 256, 256, 1] of C members and B rows x[b] = (s, a),
+ * with the second hidden layer's units split into D3A_ACTOR_Q_PARTS parts p
+ * of 64 (Q and dQ/da are linear in the parts' contributions):
+ *   q[(p*C + c)*B + b]               = part p of Q_c(x[b]) (+ the head bias in p = 0)
+ *   dq_da[((p*C + c)*B + b)*A + j]   = part p of dQ_c/dx_(da_off+j) at x[b], j < A,
+ * UNSCALED (dL/dQ_c = 1); d3a_sac_actor_head (dq_min = 1, n_part =
+ * D3A_ACTOR_Q_PARTS) sums the parts, selects the argmin member and scales.
+ * Replaces the per-layer forward, d3a_head1_min and the input-gradient
+ * launches of the actor phase.  One workgroup per 16 rows, member and part;
+ * exact-fp32 MFMA chains.  Requires n_in <= 64, A <= 16, da_off + A <= n_in,
+ * W1 / b rows 16-byte aligned.                                             */
+#define D3A_ACTOR_Q_PARTS 4
 typedef struct d3a_sac_actor_q_desc {
   const float* x;         /* [B][ldx] critic input rows (obs | action | pad) */
   int64_t ldx;
   const float* W0; const float* b0;   /* [C][256][n_in], [C][256] */
   const float* W1; const float* b1;   /* [C][256][256],  [C][256] */
   const float* wh; const float* bh;   /* [C][1][256],    [C][1]   */
-  float* q;               /* [C] x [B], member stride sqc                  */
-  int64_t sqc;
-  float* dq_da;           /* [C] x [B][ld_da], member stride sda_c         */
-  int64_t ld_da, sda_c;
+  float* q;               /* [D3A_ACTOR_Q_PARTS][C][B]                      */
+  float* dq_da;           /* [D3A_ACTOR_Q_PARTS][C][B][A]                   */
   int32_t B, C, n_in, A, da_off;
 } d3a_sac_actor_q_desc;
 int d3a_sac_actor_q(const d3a_sac_actor_q_desc* d, void* stream);

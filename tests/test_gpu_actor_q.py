@@ -55,26 +55,29 @@ def test_sac_actor_q_vs_fp64(B, D, A, C):
     x = torch.zeros(B, ldx, device="cuda")
     x[:, :D] = torch.randn(B, D, device="cuda", generator=g)
     x[:, D:n_in] = torch.tanh(torch.randn(B, A, device="cuda", generator=g))
-    q = torch.full((C, B), float("nan"), device="cuda")
-    dq = torch.full((C, B, n_in), float("nan"), device="cuda")
+    P = N.ACTOR_Q_PARTS
+    qp = torch.full((P, C, B), float("nan"), device="cuda")
+    jp = torch.full((P, C, B, A), float("nan"), device="cuda")
     d = N.SacActorQDesc()
     d.x, d.ldx = x.data_ptr(), ldx
     (W0, b0), (W1, b1), (Wh, bh) = ws
     d.W0, d.b0, d.W1, d.b1 = W0.data_ptr(), b0.data_ptr(), W1.data_ptr(), b1.data_ptr()
     d.wh, d.bh = Wh.data_ptr(), bh.data_ptr()
-    d.q, d.sqc = q.data_ptr(), B
-    d.dq_da, d.ld_da, d.sda_c = dq.data_ptr(), n_in, B * n_in
+    d.q, d.dq_da = qp.data_ptr(), jp.data_ptr()
     d.B, d.C, d.n_in, d.A, d.da_off = B, C, n_in, A, D
     ops.call_desc("d3a_sac_actor_q", d)
     torch.cuda.synchronize()
+    assert not torch.isnan(qp).any() and not torch.isnan(jp).any()
+    # the parts summed in order, as d3a_sac_actor_head does
+    q, dq = qp[0].clone(), jp[0].clone()
+    for p in range(1, P):
+        q, dq = q + qp[p], dq + jp[p]
     q64, j64 = _fp64(ws, x[:, :n_in], D, A)
     eq = float((q.double() - q64).abs().max()) / float(q64.abs().max())
     assert eq <= 1e-5, eq
     for c in range(C):
-        ej = float((dq[c, :, D:].double() - j64[c]).abs().max()) / float(j64[c].abs().max())
+        ej = float((dq[c].double() - j64[c]).abs().max()) / float(j64[c].abs().max())
         assert ej <= 1e-5, (c, ej)
-    # only the action columns are written
-    assert torch.isnan(dq[:, :, :D]).all()
 
 
 def test_sac_actor_q_rejects_bad_shapes():
@@ -84,7 +87,7 @@ def test_sac_actor_q_rejects_bad_shapes():
     t = torch.zeros(16, device="cuda")
     p = t.data_ptr()
     d.x = d.W0 = d.b0 = d.W1 = d.b1 = d.wh = d.bh = d.q = d.dq_da = p
-    d.B, d.C, d.n_in, d.A, d.da_off, d.ldx, d.ld_da = 4, 2, 65, 1, 0, 65, 65
+    d.B, d.C, d.n_in, d.A, d.da_off, d.ldx = 4, 2, 65, 1, 0, 65
     with pytest.raises(RuntimeError, match="n_in <= 64"):
         ops.call_desc("d3a_sac_actor_q", d)
     d.n_in, d.A, d.da_off = 8, 3, 6
@@ -92,18 +95,22 @@ def test_sac_actor_q_rejects_bad_shapes():
         ops.call_desc("d3a_sac_actor_q", d)
 
 
-@pytest.mark.parametrize("C", [2, 3])
-def test_actor_head_dq_min_matches_summed_path(C):
-    """dq_min mode (dQ/da = -1/B * the argmin member's unscaled dQ_c/da) is
-    bit-identical to the summed path fed with the min's backward already
-    applied (zeros on the other members), ties included (first member wins,
-    as y.min(dim=0) of the reference)."""
-    g = torch.Generator(device="cuda").manual_seed(5 + C)
+@pytest.mark.parametrize("C,P", [(2, 1), (3, 1), (2, 4)])
+def test_actor_head_dq_min_matches_summed_path(C, P):
+    """dq_min mode (dQ/da = -1/B * the argmin member's unscaled dQ_c/da, q and
+    dQ/da given as P parts summed in order) is bit-identical to the summed
+    path fed with the parts' sums and the min's backward already applied
+    (zeros on the other members), ties included (first member wins, as
+    y.min(dim=0) of the reference)."""
+    g = torch.Generator(device="cuda").manual_seed(5 + C + P)
     B, A, D = 200, 3, 11
     H = 256
-    q = torch.randn(C, B, device="cuda", generator=g)
-    q[1, :40] = q[0, :40]  # ties
-    jac = torch.randn(C, B, D + A, device="cuda", generator=g)
+    qparts = torch.randn(P, C, B, device="cuda", generator=g)
+    qparts[:, 1, :40] = qparts[:, 0, :40]  # ties
+    jparts = torch.randn(P, C, B, D + A, device="cuda", generator=g)
+    q, jac = qparts[0].clone(), jparts[0].clone()
+    for p in range(1, P):
+        q, jac = q + qparts[p], jac + jparts[p]
     # the first member of least q (strict <, as y.min(dim=0) on ties)
     arg = torch.zeros(B, dtype=torch.long, device="cuda")
     mn = q[0].clone()
@@ -123,14 +130,14 @@ def test_actor_head_dq_min_matches_summed_path(C):
     hp = torch.relu(torch.randn(B, H, device="cuda", generator=g))
     wh = torch.randn(2 * A, H, device="cuda", generator=g) * 0.05
 
-    def run(dq_buf, dq_min):
+    def run(dq_buf, q_buf, dq_min):
         out = {k: torch.zeros(*s, device="cuda") for k, s in
                (("dhead", (B, 2 * A)), ("metrics", (16,)), ("dz", (B, H)),
                 ("dW", (B, 2 * A, H)), ("db", (B, 2 * A)))}
         h = N.SacActorHeadDesc()
         h.head, h.eps, h.u, h.logp = head.data_ptr(), eps.data_ptr(), u.data_ptr(), logp.data_ptr()
         h.dq_da, h.ld_da, h.da_off, h.sda_c = dq_buf.data_ptr(), D + A, D, B * (D + A)
-        h.q, h.sqc, h.scalars = q.data_ptr(), B, scalars.data_ptr()
+        h.q, h.sqc, h.scalars = q_buf.data_ptr(), B, scalars.data_ptr()
         h.dhead, h.metrics = out["dhead"].data_ptr(), out["metrics"].data_ptr()
         h.B, h.A, h.C = B, A, C
         h.min_logstd, h.max_logstd = -20.0, 2.0
@@ -138,11 +145,12 @@ def test_actor_head_dq_min_matches_summed_path(C):
         h.dz, h.lddz = out["dz"].data_ptr(), H
         h.dW_part, h.db_part = out["dW"].data_ptr(), out["db"].data_ptr()
         h.dq_min, h.dq_scale = dq_min, -1.0 / B
+        h.n_part, h.sq_part, h.sda_part = P, C * B, C * B * (D + A)
         ops.call_desc("d3a_sac_actor_head", h)
         torch.cuda.synchronize()
         return out
 
-    a = run(jac, 1)
-    b = run(scaled, 0)
+    a = run(jparts, qparts, 1)
+    b = run(scaled, q, 0)
     for k in a:
         assert torch.equal(a[k], b[k]), k
