@@ -115,6 +115,7 @@ class CqlSampleDesc(C.Structure):
         ("eps_targ", vp), ("logp_targ", vp), ("soft_target", C.c_int32),
         ("noise_base", vp), ("rng_ctr", vp), ("eps_actor_out", vp), ("seed", C.c_uint64),
         ("n_normal", C.c_int64), ("gen_noise", C.c_int32),
+        ("head_parts", C.c_int32), ("s_head_part", C.c_int64),
     ]
 
 
@@ -150,6 +151,7 @@ class SacActorHeadDesc(C.Structure):
         ("w0", vp), ("ldw0", C.c_int64), ("sw0_c", C.c_int64), ("H0", C.c_int32),
         ("dq_min", C.c_int32), ("dq_scale", C.c_float), ("n_part", C.c_int32),
         ("sq_part", C.c_int64), ("sda_part", C.c_int64),
+        ("head_parts", C.c_int32), ("s_head_part", C.c_int64),
     ]
 
 
@@ -261,7 +263,11 @@ class MlpFwdDesc(C.Structure):
         ("aux_x", vp), ("aux_ldx", C.c_int64), ("aux_sxb", C.c_int64),
         ("aux_wdelta", C.c_int64), ("aux_out", vp), ("aux_sout", C.c_int64),
         ("aux_rows", C.c_int64),
+        ("parts", C.c_int32), ("s_part", C.c_int64),
     ]
+
+
+MLP_PARTS = 4  # D3A_MLP_PARTS
 
 
 class MlpBwdDesc(C.Structure):

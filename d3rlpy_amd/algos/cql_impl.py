@@ -444,6 +444,10 @@ class _Workspace:
             self.seed = impl._dp.rank_seed(self.seed)
         # policy forward on 2B rows
         self.pacts = mlp.Acts.alloc(impl.policy, 2 * B, dev)
+        # the policy head as unit-part partial sums (d3a_mlp_fwd parts), summed
+        # by the sampler and the actor head
+        self.phead = (torch.zeros(NAT.MLP_PARTS, 1, 2 * B, 2 * A, dtype=torch.float32, device=dev)
+                      if mlp.parts_ok(impl.policy) and impl.policy.C == 1 else None)
         # sample outputs
         self.x_q = z(self.R, LDX)
         self.x_targ = z(B, LDX)
@@ -499,6 +503,9 @@ class _Workspace:
         impl = self.impl
         s = NAT.CqlSampleDesc()
         s.head = self.pacts.out.data_ptr()
+        if self.phead is not None:
+            s.head, s.head_parts, s.s_head_part = (self.phead.data_ptr(), NAT.MLP_PARTS,
+                                                   2 * self.B * 2 * self.A)
         s.obs = self.xobs2.data_ptr()
         s.next_obs = self.xobs2.data_ptr() + 4 * self.B * self.D
         s.act = self.act.data_ptr()
@@ -552,6 +559,9 @@ class _Workspace:
 
         h = NAT.SacActorHeadDesc()
         h.head = self.pacts.out.data_ptr()
+        if self.phead is not None:
+            h.head, h.head_parts, h.s_head_part = (self.phead.data_ptr(), NAT.MLP_PARTS,
+                                                   2 * self.B * 2 * self.A)
         h.eps = self.eps_actor.data_ptr()
         h.u = self.actor_u.data_ptr()
         h.logp = self.actor_logp.data_ptr()
@@ -701,7 +711,8 @@ class _Workspace:
             ops.standardize(self.obs2, self.xobs2, self.sc_mean, self.sc_std, self.sc_eps)
         if sampled:
             # 1. policy on [obs; next_obs]
-            mlp.forward(impl.policy, impl.store, self.xobs2.data_ptr(), True, D, self.pacts)
+            mlp.forward(impl.policy, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
+                        out_parts=self.phead)
             # 2. samples and Q inputs
             ops.call_desc("d3a_cql_sample", self.sample_desc)
         if alpha or critic:

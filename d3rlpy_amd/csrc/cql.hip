@@ -22,15 +22,28 @@ constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
 // SquashedGaussianDistribution sample + log-prob for one row:
 //   std = exp(clamp(ls, lo, hi)); u = mu + eps * std; a = tanh(u)
 //   logp = sum_j [Normal(mu, std).log_prob(u) - 2 (log 2 - u - softplus(-2u))]
-__device__ __forceinline__ float squashed_sample(const float* mu, const float* ls, const float* eps,
-                                                 int A, float lo, float hi, float* act,
-                                                 float* u_out) {
+// A head value: np partial sums at h + p * sp, summed in order (np = 1: one)
+__device__ __forceinline__ float head_val(const float* h, int64_t sp, int np, int64_t j) {
+  if (np == D3A_MLP_PARTS) {
+    const float a = h[j], b = h[sp + j], c = h[2 * sp + j], e = h[3 * sp + j];
+    return ((a + b) + c) + e;
+  }
+  float v = h[j];
+  for (int p = 1; p < np; ++p) v += h[p * sp + j];
+  return v;
+}
+
+// the head row hrow = (mu | logstd) of A + A values, given as np parts
+__device__ __forceinline__ float squashed_sample(const float* hrow, int64_t sp, int np,
+                                                 const float* eps, int A, float lo, float hi,
+                                                 float* act, float* u_out) {
   float logp = 0.f;
   for (int j = 0; j < A; ++j) {
-    const float l = fminf(fmaxf(ls[j], lo), hi);
+    const float muj = head_val(hrow, sp, np, j);
+    const float l = fminf(fmaxf(head_val(hrow, sp, np, A + j), lo), hi);
     const float sd = expf(l);
-    const float u = mu[j] + eps[j] * sd;
-    const float d = u - mu[j];
+    const float u = muj + eps[j] * sd;
+    const float d = u - muj;
     const float var = sd * sd;
     const float lp = -(d * d) / (2.f * var) - logf(sd) - kLogSqrt2Pi;
     const float jac = 2.f * (kLn2 - u - softplus_t(-2.f * u));
@@ -51,6 +64,10 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
   if (i >= total) return;
   const int64_t H = 2 * A;                 // head row width
   float act[16], ev[16];
+  // policy head rows (mu | logstd); with head_parts, the parts summed in order
+  const int np = d.head_parts > 1 ? d.head_parts : 1;
+  const int64_t sp = d.s_head_part;
+  auto head_row = [&](int64_t row) { return d.head + row * H; };
   // the step's noise: drawn here from the Philox stream (gen_noise) or read
   // from the buffers the caller filled (parity mode)
   const uint64_t ctr = d.gen_noise ? (uint64_t)*d.rng_ctr : 0;
@@ -71,9 +88,9 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
     for (int64_t j = 0; j < D; ++j) x[j] = o[j];
     if (blk < 2) {
       // policy rows: head row b (obs) or B + b (next_obs); noise [s][blk][n][b]
-      const float* hrow = d.head + (blk * B + b) * H;
+      const float* hrow = head_row(blk * B + b);
       noise(d.eps_pi + (((s * 2 + blk) * N + n) * B + b) * A, (int)A, ev);
-      const float lp = squashed_sample(hrow, hrow + A, ev, (int)A, d.min_logstd, d.max_logstd,
+      const float lp = squashed_sample(hrow, sp, np, ev, (int)A, d.min_logstd, d.max_logstd,
                                        act, nullptr);
       d.logp_is[(s * 2 + blk) * NB + r] = lp;
       for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
@@ -90,36 +107,36 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
   } else if (i < R + B) {
     // update_temp sample: log-prob only
     const int64_t b = i - R;
-    const float* hrow = d.head + b * H;
+    const float* hrow = head_row(b);
     noise(d.eps_temp + b * A, (int)A, ev);
-    d.logp_temp[b] = squashed_sample(hrow, hrow + A, ev, (int)A, d.min_logstd, d.max_logstd,
+    d.logp_temp[b] = squashed_sample(hrow, sp, np, ev, (int)A, d.min_logstd, d.max_logstd,
                                      nullptr, nullptr);
   } else if (i < R + 2 * B) {
     const int64_t b = i - R - B;
-    const float* hrow = d.head + (B + b) * H;
+    const float* hrow = head_row(B + b);
     float* x = d.x_targ + b * DA;
     for (int64_t j = 0; j < D; ++j) x[j] = d.next_obs[b * D + j];
     if (d.soft_target) {
       // SACImpl.compute_target: policy.sample_with_log_prob(next_obs)
       noise(d.eps_targ + b * A, (int)A, ev);
-      d.logp_targ[b] = squashed_sample(hrow, hrow + A, ev, (int)A, d.min_logstd, d.max_logstd,
+      d.logp_targ[b] = squashed_sample(hrow, sp, np, ev, (int)A, d.min_logstd, d.max_logstd,
                                        act, nullptr);
       for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
     } else {
       // deterministic target action tanh(mu(s_t+1)) (NormalPolicy.best_action)
-      for (int64_t j = 0; j < A; ++j) x[D + j] = tanhf(hrow[j]);
+      for (int64_t j = 0; j < A; ++j) x[D + j] = tanhf(head_val(hrow, sp, np, j));
     }
   } else {
     // actor sample (rsample, with gradient later)
     const int64_t b = i - R - 2 * B;
-    const float* hrow = d.head + b * H;
+    const float* hrow = head_row(b);
     float* x = d.x_actor + b * DA;
     for (int64_t j = 0; j < D; ++j) x[j] = d.obs[b * D + j];
     noise(d.eps_actor + b * A, (int)A, ev);
     // the actor head (d3a_sac_actor_head) reads these draws again
     if (d.gen_noise)
       for (int64_t j = 0; j < A; ++j) d.eps_actor_out[b * A + j] = ev[j];
-    d.actor_logp[b] = squashed_sample(hrow, hrow + A, ev, (int)A, d.min_logstd, d.max_logstd,
+    d.actor_logp[b] = squashed_sample(hrow, sp, np, ev, (int)A, d.min_logstd, d.max_logstd,
                                       act, d.actor_u + b * A);
     for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
   }
@@ -431,6 +448,7 @@ __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_
   }
   const float dlogp = et / (float)B;
   const float* hrow = d.head + b * 2 * A;
+  const int hp = d.head_parts > 1 ? d.head_parts : 1;
   // input-gradient operands of this thread's column
   const bool col = d.dz != nullptr && tid < d.H;
   float hv = 0.f, wk[32];
@@ -490,7 +508,8 @@ __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_
     } else {
       for (int c = 0; c < C; ++c) da += d.dq_da[c * d.sda_c + b * d.ld_da + d.da_off + j];
     }
-    const float mu = hrow[j], lsr = hrow[A + j];
+    const float mu = head_val(hrow, d.s_head_part, hp, j);
+    const float lsr = head_val(hrow, d.s_head_part, hp, A + j);
     const float l = fminf(fmaxf(lsr, d.min_logstd), d.max_logstd);
     const float sd = expf(l);
     const float u = d.u[b * A + j];

@@ -224,7 +224,163 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
   }
 }
 
+
+// ---- parts variant (d3a_mlp_fwd_desc.parts): two hidden layers of 256, the
+// second layer's units split into D3A_MLP_PARTS parts of 64.  A workgroup owns
+// 16 rows, one member and one part: the narrow first layer for all 256 units
+// (W0 in registers), its 64 units of the second layer (its W1 rows straight
+// into registers), and its part of the head, out[p][row][j] = sum over its
+// units of h2 Wh[j] (+ bias in part 0).  Four waves: wave w owns first-layer
+// units 64 w .. 64 w + 63 (four tiles) and second-layer units U0 + 16 w ..
+// U0 + 16 w + 15 (one tile, full k chain).  The head is summed over lane
+// groups by a fixed butterfly and over waves in wave order.
+constexpr int P_LDX = 68;  // input row stride in LDS (n_in <= 64)
+
+struct PartsLds {
+  float x[S_RB * P_LDX];
+  float h1[S_RB * S_LDK];
+  float op[4][S_RB][16];  // per-wave head partials
+};
+
+__global__ __launch_bounds__(256) void mlp_parts_kernel(d3a_mlp_fwd_desc d) {
+  __shared__ __attribute__((aligned(16))) PartsLds S;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lr = lane & 15, lq = lane >> 4;
+  const int c = blockIdx.y, p = blockIdx.z;
+  const int U0 = 64 * p;
+  const int m0 = (int)d.r0 + (int)blockIdx.x * S_RB;
+  const int rend = (int)(d.r0 + d.rows);
+  const int K0 = d.n_in, K0p = (K0 + 15) / 16 * 16, J = d.n_out;
+  const float* xb = d.x + c * d.sxb;
+  for (int e = t; e < S_RB * P_LDX; e += 256) {
+    const int m = e / P_LDX, k = e - m * P_LDX;
+    const int r = m0 + m;
+    S.x[e] = (k < K0 && r < rend) ? xb[(int64_t)r * d.ldx + k] : 0.f;
+  }
+  const float* W0 = d.W[0] + c * d.sW[0];
+  float w0r[4][16];  // tile tt, group g, element i: W0[unit][min(16 g + 4 lq + i, n_in - 1)]
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = min(16 * g + 4 * lq + i, K0 - 1);
+        w0r[tt][4 * g + i] = 16 * g < K0p ? W0[(64 * w + 16 * tt + lr) * K0 + k] : 0.f;
+      }
+  const float* W1 = d.W[1] + c * d.sW[1] + (int64_t)(U0 + 16 * w + lr) * S_H;
+  float4 w1r[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) w1r[g] = *reinterpret_cast<const float4*>(W1 + 16 * g + 4 * lq);
+  const float* b0 = d.b[0] + c * d.sb[0];
+  float4 bias0[4];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt)
+    bias0[tt] = *reinterpret_cast<const float4*>(b0 + 64 * w + 16 * tt + 4 * lq);
+  const float4 bias1 =
+      *reinterpret_cast<const float4*>(d.b[1] + c * d.sb[1] + U0 + 16 * w + 4 * lq);
+  const float* Wh = d.W[2] + c * d.sW[2] + U0 + 16 * w + 4 * lq;
+  float4 whv[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    whv[j] = j < J ? *reinterpret_cast<const float4*>(Wh + j * S_H) : make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+
+  // ---- first layer, all 256 units
+  {
+    f32x4 acc[4];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (16 * g < K0p) {
+        const float4 a = *reinterpret_cast<const float4*>(&S.x[lr * P_LDX + 16 * g + 4 * lq]);
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          acc[tt] = mfma4(w0r[tt][4 * g + 0], a.x, acc[tt]);
+          acc[tt] = mfma4(w0r[tt][4 * g + 1], a.y, acc[tt]);
+          acc[tt] = mfma4(w0r[tt][4 * g + 2], a.z, acc[tt]);
+          acc[tt] = mfma4(w0r[tt][4 * g + 3], a.w, acc[tt]);
+        }
+      }
+    }
+    const int row = m0 + lr;
+    float* hg = (p == 0 && d.h[0]) ? d.h[0] + c * d.sh : nullptr;
+    const bool keep = hg != nullptr && row >= d.h_from && row < rend;
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const float4 bv = bias0[tt];
+      const int u = 64 * w + 16 * tt + 4 * lq;
+      const float4 v = make_float4(fmaxf(acc[tt][0] + bv.x, 0.f), fmaxf(acc[tt][1] + bv.y, 0.f),
+                                   fmaxf(acc[tt][2] + bv.z, 0.f), fmaxf(acc[tt][3] + bv.w, 0.f));
+      *reinterpret_cast<float4*>(&S.h1[lr * S_LDK + u]) = v;
+      if (keep) *reinterpret_cast<float4*>(hg + (int64_t)row * S_H + u) = v;
+    }
+  }
+  __syncthreads();
+
+  // ---- the part's second-layer tile and its head terms
+  {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const float4 a = *reinterpret_cast<const float4*>(&S.h1[lr * S_LDK + 16 * g + 4 * lq]);
+      acc = mfma4(w1r[g].x, a.x, acc);
+      acc = mfma4(w1r[g].y, a.y, acc);
+      acc = mfma4(w1r[g].z, a.z, acc);
+      acc = mfma4(w1r[g].w, a.w, acc);
+    }
+    // lane: row lr, units U0 + 16 w + 4 lq + i
+    const float4 v = make_float4(fmaxf(acc[0] + bias1.x, 0.f), fmaxf(acc[1] + bias1.y, 0.f),
+                                 fmaxf(acc[2] + bias1.z, 0.f), fmaxf(acc[3] + bias1.w, 0.f));
+    const int row = m0 + lr;
+    if (d.h[1] && row >= d.h_from && row < rend)
+      *reinterpret_cast<float4*>(d.h[1] + c * d.sh + (int64_t)row * S_H + U0 + 16 * w + 4 * lq) = v;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < J) {
+        float s = 0.f;
+        s = fmaf(v.x, whv[j].x, s);
+        s = fmaf(v.y, whv[j].y, s);
+        s = fmaf(v.z, whv[j].z, s);
+        s = fmaf(v.w, whv[j].w, s);
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if (lq == 0) S.op[w][lr][j] = s;
+      }
+    }
+  }
+  __syncthreads();
+  if (t < S_RB * J) {
+    const int m = t / J, j = t - m * J;
+    const int r = m0 + m;
+    if (r < rend) {
+      float v = ((S.op[0][m][j] + S.op[1][m][j]) + S.op[2][m][j]) + S.op[3][m][j];
+      if (p == 0) v += d.b[2][c * d.sb[2] + j];
+      d.out[p * d.s_part + c * d.sout + (int64_t)r * d.ldout + j] = v;
+    }
+  }
+}
+
 }  // namespace
+
+// d3a_mlp_fwd's parts path (the caller checked the shape); false when an
+// alignment does not hold
+bool mlp_parts_launch(const d3a_mlp_fwd_desc& d, hipStream_t st) {
+  auto a16 = [](const void* p, int64_t stride) {
+    return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && stride % 4 == 0;
+  };
+  if (!a16(d.W[1], d.sW[1]) || !a16(d.W[2], d.sW[2]) || !a16(d.b[0], d.sb[0]) ||
+      !a16(d.b[1], d.sb[1]))
+    return false;
+  for (int l = 0; l < 2; ++l)
+    if (d.h[l] && !a16(d.h[l], d.sh)) return false;
+  if (d.rows == 0) return true;
+  const dim3 grid((unsigned)((d.rows + S_RB - 1) / S_RB), (unsigned)d.C, (unsigned)D3A_MLP_PARTS);
+  hipLaunchKernelGGL(mlp_parts_kernel, grid, dim3(256), 0, st, d);
+  return true;
+}
 
 // d3a_mlp_fwd's block_rows == 16 path; false when the shape does not fit
 bool mlp_small_launch(const d3a_mlp_fwd_desc& d, hipStream_t st) {

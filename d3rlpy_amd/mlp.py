@@ -104,12 +104,23 @@ def q2_ok(net: EnsembleMLP, rows: int) -> bool:
 # (d3a_mlp_fwd block_rows 16, csrc/mlp_small.hip)
 _SMALL = os.environ.get("D3A_MLP_SMALL", "1") == "1"
 SMALL_MAX_ROWS = 2048
+# few-hundred-row passes of [n_in, 256, 256, n_out <= 16] MLPs whose consumer
+# sums head parts (the CQL / SAC policy over [obs; next_obs]): the second
+# hidden layer split over four times the workgroups (d3a_mlp_fwd parts)
+_PARTS = os.environ.get("D3A_MLP_PARTS", "1") == "1"
 
 
 def small_ok(net: EnsembleMLP, rows: int) -> bool:
     hidden = net.sizes[1:-1]
     return (_SMALL and 1 <= len(hidden) <= N.MLP_MAX_HIDDEN and set(hidden) == {256}
             and net.sizes[0] <= 256 and net.sizes[-1] <= 64 and rows * net.C <= SMALL_MAX_ROWS)
+
+
+def parts_ok(net: EnsembleMLP) -> bool:
+    """Shape of d3a_mlp_fwd's parts path (two hidden layers of 256, the
+    second split into D3A_MLP_PARTS unit parts; n_in <= 64, n_out <= 16)."""
+    return (_PARTS and list(net.sizes[1:-1]) == [256, 256] and net.sizes[0] <= 64
+            and net.sizes[-1] <= 16)
 
 
 def fused_ok(net: EnsembleMLP, rows: Optional[int] = None, backward: bool = False) -> bool:
@@ -124,7 +135,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             r0: int = 0, r1: Optional[int] = None, sxb: Optional[int] = None,
             members: Optional[int] = None, keep_h: bool = True,
             h_from: Optional[int] = None, aux: Optional[tuple] = None,
-            skip_head: bool = False) -> None:
+            skip_head: bool = False, out_parts: Optional[torch.Tensor] = None) -> None:
     """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
     (through its first ``members`` members only, when given).  ``keep_h``:
     store the hidden activations in ``acts.h`` (needed by a backward pass),
@@ -138,7 +149,12 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     workgroups use the CUs the main pass leaves idle); on the per-layer path
     each layer's launch carries it as a second batch dimension when its shape
     equals the main pass's (acts2.R == acts.R rows, same ldx); otherwise it is
-    a separate forward."""
+    a separate forward.
+
+    ``out_parts`` ([D3A_MLP_PARTS][C][R][n_out], ``parts_ok`` shapes): the
+    head is written there as partial sums over the second hidden layer's unit
+    parts (d3a_mlp_fwd_desc.parts; consumers sum them in order), not to
+    acts.out."""
     R = acts.R
     r1 = R if r1 is None else r1
     n = r1 - r0
@@ -151,6 +167,10 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         raise NotImplementedError("bf16 activations: [n_in <= 48, 256, 256, 1] critics, "
                                   "all members, activations kept")
     small = not bf16 and not skip_head and small_ok(net, n * C // net.C)
+    if out_parts is not None:
+        assert parts_ok(net) and not bf16 and not skip_head and aux is None
+        assert tuple(out_parts.shape) == (N.MLP_PARTS, C, R, sizes[-1])
+        small = True
     if bf16 or small or fused_ok(net, n * C // net.C):
         d = N.MlpFwdDesc()
         d.block_rows = 16 if small else _FUSED_BM
@@ -166,6 +186,8 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         d.sh = R * sizes[1]
         d.out = acts.out.data_ptr()
         d.sout, d.ldout = R * sizes[-1], sizes[-1]
+        if out_parts is not None:
+            d.out, d.parts, d.s_part = out_parts.data_ptr(), N.MLP_PARTS, C * R * sizes[-1]
         d.r0, d.rows, d.C = r0, n, C
         d.h_from = r0 if h_from is None else max(r0, h_from)
         if aux is not None and members is None:

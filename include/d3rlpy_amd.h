@@ -238,7 +238,17 @@ typedef struct d3a_mlp_fwd_desc {
    * run on the CUs the main pass leaves idle. */
   const float* aux_x; int64_t aux_ldx, aux_sxb, aux_wdelta;
   float* aux_out; int64_t aux_sout, aux_rows;
+  /* Optional (parts = D3A_MLP_PARTS, block_rows 16, two hidden layers of 256,
+   * n_in <= 64, n_out <= 16, no aux pass): the second hidden layer's units
+   * are split into parts of 64, one workgroup per 16 rows, member and part,
+   * so a few-hundred-row pass spreads over four times the CUs.  The head is
+   * linear in the parts: out + p*s_part holds part p's sum over its units
+   * (the head bias in part 0); a consumer sums the parts in order.  h[0] is
+   * written by part 0, h[1] unit-slice by slice.  parts 0 / 1: off.       */
+  int32_t parts;
+  int64_t s_part;
 } d3a_mlp_fwd_desc;
+#define D3A_MLP_PARTS 4
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);
 
 /* Backward-data of the same MLP, one launch (the autograd backward of the
@@ -510,6 +520,10 @@ typedef struct d3a_cql_sample_desc {
   uint64_t seed;
   int64_t n_normal;
   int32_t gen_noise;
+  /* head_parts >= 2: the policy head rows are head_parts partial sums at
+   * head + p*s_head_part (d3a_mlp_fwd parts), summed in order here */
+  int32_t head_parts;
+  int64_t s_head_part;
 } d3a_cql_sample_desc;
 int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream);
 
@@ -614,6 +628,10 @@ typedef struct d3a_sac_actor_head_desc {
   float dq_scale;
   int32_t n_part;
   int64_t sq_part, sda_part;
+  /* head_parts >= 2: the policy head rows as partial sums, as in
+   * d3a_cql_sample_desc */
+  int32_t head_parts;
+  int64_t s_head_part;
 } d3a_sac_actor_head_desc;
 int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream);
 

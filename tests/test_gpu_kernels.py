@@ -630,3 +630,50 @@ def test_gemm_pair_bit_identical(dev, C_, R, n_in, n_out, S):
     # and the pair is right: fp64 reference of dX
     ref = ((dz.double() @ W.double()) * (h > 0)).cpu()
     torch.testing.assert_close(outs[1][2].double(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("C,R,r0,n,K0,J,x_shared", [
+    (1, 512, 0, 512, 11, 6, True),       # CQL policy on [obs; next_obs] (mu | logstd)
+    (1, 512, 0, 512, 29, 16, True),      # K4 policy (antmaze 29 -> 2 x 8)
+    (2, 300, 7, 200, 64, 5, False),      # widest input, per-member inputs, r0 > 0, ragged
+])
+def test_mlp_forward_parts(dev, C, R, r0, n, K0, J, x_shared):
+    """d3a_mlp_fwd parts (the second hidden layer's units split into
+    D3A_MLP_PARTS parts, one workgroup per 16 rows, member and part): the head
+    parts summed in order against an fp64 torch MLP, kept activations for rows
+    >= h_from only (2e-6 relative); rows outside [r0, r0 + n) untouched."""
+    from d3rlpy_amd import _native as N
+    from d3rlpy_amd import mlp
+    from d3rlpy_amd.nets import EnsembleMLP, ParamStore
+    g = torch.Generator().manual_seed(R + K0 + J + 1)
+    st = ParamStore()
+    net = EnsembleMLP(st, "m", C, [K0, 256, 256, J])
+    st.allocate(dev)
+    with torch.no_grad():
+        st.data.copy_(torch.randn(st.data.numel(), generator=g) * 0.1)
+    assert mlp.parts_ok(net)
+    ldx = (K0 + 3) // 4 * 4 + 4
+    x = torch.randn((1 if x_shared else C), R, ldx, generator=g).to(dev)
+    acts = mlp.Acts.alloc(net, R, dev)
+    for h in acts.h:
+        h.fill_(float("nan"))
+    parts = torch.full((N.MLP_PARTS, C, R, J), float("nan"), device=dev)
+    h_from = r0 + n // 3
+    mlp.forward(net, st, x.data_ptr(), x_shared, ldx, acts, r0, r0 + n, h_from=h_from,
+                out_parts=parts)
+    torch.cuda.synchronize()
+    out = parts[0]
+    for p in range(1, N.MLP_PARTS):
+        out = out + parts[p]
+    k = h_from - r0
+    for c in range(C):
+        a = x[0 if x_shared else c, r0:r0 + n, :K0].double()
+        for l in range(3):
+            W, b = net.export_linear(l, c, st)
+            a = a @ W.double().T + b.double()
+            if l < 2:
+                a = a.clamp_min(0)
+                assert _rel_err(acts.h[l][c, h_from:r0 + n], a[k:]) < 2e-6, (c, l)
+                assert torch.isnan(acts.h[l][c, r0:h_from]).all(), (c, l)
+        assert _rel_err(out[c, r0:r0 + n], a) < 2e-6, c
+        assert torch.isnan(parts[:, c, :r0]).all() and torch.isnan(parts[:, c, r0 + n:]).all()

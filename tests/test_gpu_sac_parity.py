@@ -7,6 +7,8 @@ each step starts HIP from the oracle's exact state loaded through the
 reference checkpoint layout; same batch, same injected noise (eps_targ is the
 soft target's policy-sample noise).
 """
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -47,7 +49,8 @@ def test_sac_update_parity(case):
     rs = np.random.RandomState(3)
     gen = torch.Generator().manual_seed(3)
     for step in range(3):
-        impl.set_state_dict(oracle_state(orc))
+        sd0 = copy.deepcopy(oracle_state(orc))
+        impl.set_state_dict(sd0)
         arrs = make_batch(rs, B, D, A)
         nz = CQLNoise.draw(gen, B, A, 0, soft_target=True)
         m_orc, cgrads, pgrads = _sac_oracle_step(orc, Batch.from_numpy(*arrs), nz, A)
@@ -55,7 +58,7 @@ def test_sac_update_parity(case):
         torch.cuda.synchronize()
         assert set(impl.active_metric_names()) == set(m_orc)
         _compare_step("sac-" + case, step, impl, orc, m_hip, m_orc, cgrads, pgrads, A,
-                      grad_tol=2e-5)
+                      grad_tol=2e-5, sd0=sd0)
 
 
 @pytest.mark.parametrize("case", list(CASES))
@@ -67,14 +70,15 @@ def test_cql_soft_q_backup_parity(case):
     rs = np.random.RandomState(4)
     gen = torch.Generator().manual_seed(4)
     for step in range(3):
-        impl.set_state_dict(oracle_state(orc))
+        sd0 = copy.deepcopy(oracle_state(orc))
+        impl.set_state_dict(sd0)
         arrs = make_batch(rs, B, D, A)
         nz = CQLNoise.draw(gen, B, A, N, soft_target=True)
         m_orc, cgrads, pgrads = _oracle_step(orc, Batch.from_numpy(*arrs), nz, A)
         m_hip = impl.update_step(HostBatch(*arrs), noise=noise_dict(nz))
         torch.cuda.synchronize()
         _compare_step("cql-soft-" + case, step, impl, orc, m_hip, m_orc, cgrads, pgrads, A,
-                      grad_tol=2e-5)
+                      grad_tol=2e-5, sd0=sd0)
 
 
 def test_cql_standard_scaler_parity():
