@@ -550,7 +550,7 @@ def main():
     if args.traffic_json is None:
         prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
         args.traffic_json = next((p for p in (os.path.join(prof, f"r0{r}_pmc_traffic_{args.algo}.json")
-                                              for r in (2, 1)) if os.path.exists(p)), "")
+                                              for r in (3, 2, 1)) if os.path.exists(p)), "")
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:

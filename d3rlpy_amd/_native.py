@@ -100,7 +100,12 @@ class AdamDesc(C.Structure):
         ("counters", vp), ("inc_mask", C.c_uint32),
         ("metrics", vp), ("n_metrics", C.c_int32),
         ("ring", vp), ("ring_cap", C.c_int64), ("ring_ctr", vp), ("metric_scale", C.c_float),
+        ("blocks", vp),
     ]
+
+
+class AdamBlock(C.Structure):
+    _fields_ = [("seg", AdamSegment), ("first", C.c_int64)]
 
 
 class CqlSampleDesc(C.Structure):
@@ -297,6 +302,8 @@ class Q2BwdDesc(C.Structure):
         ("dW1", vp), ("db1", vp), ("dW2", vp), ("db2", vp), ("dW3", vp), ("db3", vp),
         ("rows", C.c_int64),
         ("n_in", C.c_int32), ("C", C.c_int32),
+        ("dz2", vp), ("sdz", C.c_int64),
+        ("block_rows", C.c_int32),
     ]
 
 

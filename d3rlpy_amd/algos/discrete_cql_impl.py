@@ -537,7 +537,7 @@ class _Workspace:
                 return
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize()
-            with torch.cuda.graph(g):
+            with ops.graph_capture(g):
                 self._enqueue(*flags)
             self._graphs[key] = g
         g.replay()

@@ -54,16 +54,39 @@ __device__ __forceinline__ float squashed_sample(const float* hrow, int64_t sp, 
   return logp;
 }
 
-__global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) {
-  const int64_t B = d.B, N = d.N, A = d.A, D = d.D;
+// One output row per four lanes, 64-row workgroups (the 15,872 rows of K2
+// spread over ~250 CUs, four waves each).  Lane k of a row's quad takes the
+// action components j = k, k + 4, .. (the Philox draw, the squashed-Gaussian
+// term, tanh), so a row's serial transcendental chain is a quarter as long;
+// the log-prob terms meet at lane 0 in j order (the sequential sum of
+// squashed_sample, bitwise).  Rows are assembled in LDS (zero-padded to ldx)
+// and leave as whole 16-byte pieces: a workgroup's rows of one destination
+// matrix are contiguous, so the copy-out is fully coalesced.
+constexpr int SMP_R = 64;       // rows per workgroup
+constexpr int SMP_T = 4 * SMP_R;
+constexpr int SMP_MAXLDX = 64;  // ldx handled by the LDS copy-out
+__global__ __launch_bounds__(SMP_T) void cql_sample_kernel(d3a_cql_sample_desc d) {
+  __shared__ float xs[SMP_R * (SMP_MAXLDX + 1)];
+  const int64_t B = d.B, N = d.N, D = d.D;
+  const int A = d.A;
   const int64_t NB = N * B;
   const int64_t DA = d.ldx;  // row stride of the Q-input matrices (>= D + A, padded)
   const int64_t R = 6 * NB + B;           // x_q rows
   const int64_t total = R + 3 * B;         // + temp, target, actor rows
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
+  const int rl = threadIdx.x >> 2, k = threadIdx.x & 3;
+  const int64_t i0 = (int64_t)blockIdx.x * SMP_R;
+  const int64_t i = i0 + rl;
+  constexpr int LS = SMP_MAXLDX + 1;  // LDS row stride
+  float* const xl = xs + rl * LS;
+  // the destination row of output row q (nullptr: no Q-input row)
+  auto dest = [&](int64_t q) -> float* {
+    if (q < R) return d.x_q + q * DA;
+    if (q < R + B) return nullptr;
+    if (q < R + 2 * B) return d.x_targ + (q - R - B) * DA;
+    if (q < total) return d.x_actor + (q - R - 2 * B) * DA;
+    return nullptr;
+  };
   const int64_t H = 2 * A;                 // head row width
-  float act[16], ev[16];
   // policy head rows (mu | logstd); with head_parts, the parts summed in order
   const int np = d.head_parts > 1 ? d.head_parts : 1;
   const int64_t sp = d.s_head_part;
@@ -71,74 +94,140 @@ __global__ __launch_bounds__(256) void cql_sample_kernel(d3a_cql_sample_desc d) 
   // the step's noise: drawn here from the Philox stream (gen_noise) or read
   // from the buffers the caller filled (parity mode)
   const uint64_t ctr = d.gen_noise ? (uint64_t)*d.rng_ctr : 0;
-  auto noise = [&](const float* p, int n, float* out) {
-    for (int j = 0; j < n; ++j)
-      out[j] = d.gen_noise ? philox_elem(d.seed, ctr, (p + j) - d.noise_base, d.n_normal, -1.f, 1.f)
-                           : p[j];
+  auto noise1 = [&](const float* p) {
+    return d.gen_noise ? philox_elem(d.seed, ctr, p - d.noise_base, d.n_normal, -1.f, 1.f) : *p;
   };
+  // component j of a squashed-Gaussian sample (squashed_sample's loop body):
+  // returns its log-prob term, writes tanh(u) and u
+  auto comp = [&](const float* hrow, int j, float e, float& a, float& u) {
+    const float muj = head_val(hrow, sp, np, j);
+    const float l = fminf(fmaxf(head_val(hrow, sp, np, A + j), d.min_logstd), d.max_logstd);
+    const float sd = expf(l);
+    u = muj + e * sd;
+    const float dd = u - muj;
+    const float var = sd * sd;
+    const float lp = -(dd * dd) / (2.f * var) - logf(sd) - kLogSqrt2Pi;
+    const float jac = 2.f * (kLn2 - u - softplus_t(-2.f * u));
+    a = tanhf(u);
+    return lp - jac;
+  };
+  // the row's log-prob at lane 0 of the quad: terms t[j / 4] of lane j % 4,
+  // summed in j order
+  auto logp_sum = [&](const float* t) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float v = __shfl(t[j >> 2], (threadIdx.x & ~3) + (j & 3), 64);
+      if (j < A) s = j == 0 ? v : s + v;
+    }
+    return s;
+  };
+  // copy D floats of an observation row into the LDS row (quad-strided)
+  auto put_obs = [&](const float* o) {
+    for (int64_t jj = k; jj < D; jj += 4) xl[jj] = o[jj];
+  };
+  float t[4] = {0.f, 0.f, 0.f, 0.f};
 
-  if (i < 6 * NB) {
+  if (i >= total) {
+    // past the last row: nothing (the copy-out skips it)
+  } else if (i < 6 * NB) {
     const int64_t s = i / (3 * NB);        // 0 = alpha set, 1 = critic set
     const int64_t w = i % (3 * NB);
     const int64_t blk = w / NB;            // 0 pi(.|s_t), 1 pi(.|s_t+1), 2 uniform
     const int64_t r = w % NB;              // = b * N + n
     const int64_t b = r / N, n = r % N;
-    float* x = d.x_q + i * DA;
-    const float* o = d.obs + b * D;
-    for (int64_t j = 0; j < D; ++j) x[j] = o[j];
+    put_obs(d.obs + b * D);
     if (blk < 2) {
       // policy rows: head row b (obs) or B + b (next_obs); noise [s][blk][n][b]
       const float* hrow = head_row(blk * B + b);
-      noise(d.eps_pi + (((s * 2 + blk) * N + n) * B + b) * A, (int)A, ev);
-      const float lp = squashed_sample(hrow, sp, np, ev, (int)A, d.min_logstd, d.max_logstd,
-                                       act, nullptr);
-      d.logp_is[(s * 2 + blk) * NB + r] = lp;
-      for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
+      const float* ep = d.eps_pi + (((s * 2 + blk) * N + n) * B + b) * A;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = k + 4 * q;
+        if (j < A) {
+          float a, u;
+          t[q] = comp(hrow, j, noise1(ep + j), a, u);
+          xl[D + j] = a;
+        }
+      }
+      const float lp = logp_sum(t);
+      if (k == 0) d.logp_is[(s * 2 + blk) * NB + r] = lp;
     } else {
-      noise(d.u_rand + (s * NB + r) * A, (int)A, ev);
-      for (int64_t j = 0; j < A; ++j) x[D + j] = ev[j];
+      const float* up = d.u_rand + (s * NB + r) * A;
+      for (int j = k; j < A; j += 4) xl[D + j] = noise1(up + j);
     }
   } else if (i < R) {
     // data rows (obs_t, a_t)
     const int64_t b = i - 6 * NB;
-    float* x = d.x_q + i * DA;
-    for (int64_t j = 0; j < D; ++j) x[j] = d.obs[b * D + j];
-    for (int64_t j = 0; j < A; ++j) x[D + j] = d.act[b * A + j];
+    put_obs(d.obs + b * D);
+    for (int j = k; j < A; j += 4) xl[D + j] = d.act[b * A + j];
   } else if (i < R + B) {
     // update_temp sample: log-prob only
     const int64_t b = i - R;
     const float* hrow = head_row(b);
-    noise(d.eps_temp + b * A, (int)A, ev);
-    d.logp_temp[b] = squashed_sample(hrow, sp, np, ev, (int)A, d.min_logstd, d.max_logstd,
-                                     nullptr, nullptr);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = k + 4 * q;
+      if (j < A) {
+        float a, u;
+        t[q] = comp(hrow, j, noise1(d.eps_temp + b * A + j), a, u);
+      }
+    }
+    const float lp = logp_sum(t);
+    if (k == 0) d.logp_temp[b] = lp;
   } else if (i < R + 2 * B) {
     const int64_t b = i - R - B;
     const float* hrow = head_row(B + b);
-    float* x = d.x_targ + b * DA;
-    for (int64_t j = 0; j < D; ++j) x[j] = d.next_obs[b * D + j];
+    put_obs(d.next_obs + b * D);
     if (d.soft_target) {
       // SACImpl.compute_target: policy.sample_with_log_prob(next_obs)
-      noise(d.eps_targ + b * A, (int)A, ev);
-      d.logp_targ[b] = squashed_sample(hrow, sp, np, ev, (int)A, d.min_logstd, d.max_logstd,
-                                       act, nullptr);
-      for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = k + 4 * q;
+        if (j < A) {
+          float a, u;
+          t[q] = comp(hrow, j, noise1(d.eps_targ + b * A + j), a, u);
+          xl[D + j] = a;
+        }
+      }
+      const float lp = logp_sum(t);
+      if (k == 0) d.logp_targ[b] = lp;
     } else {
       // deterministic target action tanh(mu(s_t+1)) (NormalPolicy.best_action)
-      for (int64_t j = 0; j < A; ++j) x[D + j] = tanhf(head_val(hrow, sp, np, j));
+      for (int j = k; j < A; j += 4) xl[D + j] = tanhf(head_val(hrow, sp, np, j));
     }
   } else {
     // actor sample (rsample, with gradient later)
     const int64_t b = i - R - 2 * B;
     const float* hrow = head_row(b);
-    float* x = d.x_actor + b * DA;
-    for (int64_t j = 0; j < D; ++j) x[j] = d.obs[b * D + j];
-    noise(d.eps_actor + b * A, (int)A, ev);
-    // the actor head (d3a_sac_actor_head) reads these draws again
-    if (d.gen_noise)
-      for (int64_t j = 0; j < A; ++j) d.eps_actor_out[b * A + j] = ev[j];
-    d.actor_logp[b] = squashed_sample(hrow, sp, np, ev, (int)A, d.min_logstd, d.max_logstd,
-                                      act, d.actor_u + b * A);
-    for (int64_t j = 0; j < A; ++j) x[D + j] = act[j];
+    put_obs(d.obs + b * D);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = k + 4 * q;
+      if (j < A) {
+        const float e = noise1(d.eps_actor + b * A + j);
+        // the actor head (d3a_sac_actor_head) reads these draws again
+        if (d.gen_noise) d.eps_actor_out[b * A + j] = e;
+        float a, u;
+        t[q] = comp(hrow, j, e, a, u);
+        d.actor_u[b * A + j] = u;
+        xl[D + j] = a;
+      }
+    }
+    const float lp = logp_sum(t);
+    if (k == 0) d.actor_logp[b] = lp;
+  }
+  // zero padding of the row (columns D + A .. ldx)
+  for (int64_t jj = D + A + k; jj < DA; jj += 4) xl[jj] = 0.f;
+  __syncthreads();
+  // copy-out: 16-byte pieces, consecutive threads on consecutive pieces
+  const int q4 = (int)(DA / 4);
+  for (int e = threadIdx.x; e < SMP_R * q4; e += SMP_T) {
+    const int r2 = e / q4, c4 = (e - r2 * q4) * 4;
+    float* dst = dest(i0 + r2);
+    if (dst == nullptr) continue;
+    const float* sr = xs + r2 * LS + c4;
+    *reinterpret_cast<float4*>(dst + c4) = make_float4(sr[0], sr[1], sr[2], sr[3]);
   }
 }
 
@@ -558,8 +647,14 @@ extern "C" int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream) {
   D3A_CHECK_ARG(d->ldx >= d->D + d->A, "d3a_cql_sample: ldx < D + A");
   D3A_CHECK_ARG(!d->gen_noise || (d->noise_base && d->rng_ctr && d->eps_actor_out),
                 "d3a_cql_sample: gen_noise needs noise_base, rng_ctr and eps_actor_out");
+  D3A_CHECK_ARG(d->ldx % 4 == 0 && d->ldx <= SMP_MAXLDX,
+                "d3a_cql_sample: ldx must be a multiple of 4 and <= 64");
+  D3A_CHECK_ARG((reinterpret_cast<uintptr_t>(d->x_q) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(d->x_targ) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(d->x_actor) & 15) == 0,
+                "d3a_cql_sample: x_q / x_targ / x_actor must be 16-byte aligned");
   const int64_t total = 6LL * d->N * d->B + 4LL * d->B;
-  hipLaunchKernelGGL(cql_sample_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(cql_sample_kernel, dim3((unsigned)((total + SMP_R - 1) / SMP_R)), dim3(SMP_T), 0,
                      (hipStream_t)stream, *d);
   D3A_LAUNCH_CHECK("d3a_cql_sample");
   return 0;

@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void adam_kernel(d3a_adam_desc a) {
     a.ring[(rc0 % a.ring_cap) * a.n_metrics + threadIdx.x] =
         a.metric_scale == 1.f ? mk : mk * a.metric_scale;
   }
-  locate_block(segs, n_seg, &s_seg, &s_first);
+  if (a.blocks == nullptr) locate_block(segs, n_seg, &s_seg, &s_first);
   if (threadIdx.x == 64) {  // wave 1, concurrently with wave 0's segment search
     // bias corrections in fp64 exactly as torch computes them in Python floats
     const double bc1 = 1.0 - pow(beta1, (double)t);
@@ -230,27 +230,37 @@ __global__ __launch_bounds__(256) void adam_kernel(d3a_adam_desc a) {
     s_step_size = (float)(a.lr / bc1);
     s_bc2_sqrt = (float)sqrt(bc2);
   }
-  __syncthreads();  // (block 0: every ring writer has read *ring_ctr)
-  if (tail) {
-    if (a.ring && threadIdx.x == 0) *a.ring_ctr = rc0 + 1;
-    if (threadIdx.x < 32 && (a.inc_mask >> threadIdx.x & 1u)) a.counters[threadIdx.x] += 1;
-  }
-  const d3a_adam_segment sg = segs[s_seg];
+  // per-block table: the segment is one (scalar) load, and the state and
+  // partial loads go out before the barrier (the bias-correction pows of wave
+  // 1 run under them); else the search's result after the barrier
+  const bool tab = a.blocks != nullptr;
+  if (!tab) __syncthreads();  // (block 0: every ring writer has read *ring_ctr)
+  const d3a_adam_segment sg = tab ? a.blocks[blockIdx.x].seg : segs[s_seg];
+  const int64_t first = tab ? a.blocks[blockIdx.x].first : s_first;
   const int L = seg_lanes(sg.n_partials);
-  const int64_t lt = ((int64_t)blockIdx.x - s_first) * 256 + threadIdx.x;
+  const int64_t lt = ((int64_t)blockIdx.x - first) * 256 + threadIdx.x;
   const int64_t i = lt / L;
-  if (i < sg.numel) {  // uniform over each lane group
+  const bool act = i < sg.numel;
+  float m = 0.f, v = 0.f, p = 0.f, tv = 0.f;
+  float* tg = a.soft ? sg.param + a.targ_delta : nullptr;
+  const bool lead = (lt % L) == 0;
+  double gd = 0.0;
+  if (act) {
     // the state loads go out with the partial loads (one round trip for both)
-    const bool lead = (lt % L) == 0;
-    float m = 0.f, v = 0.f, p = 0.f, tv = 0.f;
-    float* tg = a.soft ? sg.param + a.targ_delta : nullptr;
     if (lead) {
       m = sg.exp_avg[i];
       v = sg.exp_avg_sq[i];
       p = sg.param[i];
       if (tg) tv = tg[i];
     }
-    const double gd = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i, (int)(lt % L), L);
+    gd = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i, (int)(lt % L), L);
+  }
+  if (tab) __syncthreads();  // s_step_size; block 0: every ring writer has read *ring_ctr
+  if (tail) {
+    if (a.ring && threadIdx.x == 0) *a.ring_ctr = rc0 + 1;
+    if (threadIdx.x < 32 && (a.inc_mask >> threadIdx.x & 1u)) a.counters[threadIdx.x] += 1;
+  }
+  if (act) {  // uniform over each lane group
     if (!lead) return;
     // grad_scale: 1, or 1/world after a data-parallel SUM all-reduce (exact
     // for power-of-two worlds)

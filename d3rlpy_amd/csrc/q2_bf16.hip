@@ -630,6 +630,8 @@ extern "C" int d3a_q2_bwd_bf16(const d3a_q2_bwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(d.x && d.h1 && d.h2 && d.g && d.W2 && d.w3, "d3a_q2_bwd_bf16: null input");
   D3A_CHECK_ARG(d.dW1 && d.db1 && d.dW2 && d.db2 && d.dW3 && d.db3, "d3a_q2_bwd_bf16: null output");
   D3A_CHECK_ARG(d.n_in >= 1 && d.n_in <= 48, "d3a_q2_bwd_bf16: n_in must be 1..48");
+  D3A_CHECK_ARG(d.dz2 == nullptr && (d.block_rows == 0 || d.block_rows == 256),
+                "d3a_q2_bwd_bf16: dz2 / block_rows are fp32-only (d3a_q2_bwd)");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.n_scaled >= 0, "d3a_q2_bwd_bf16: bad sizes");
   D3A_CHECK_ARG(d.ldh == B_H, "d3a_q2_bwd_bf16: h1 / h2 must be rows of 256 bf16");
   D3A_CHECK_ARG(d.rows * (d.ldx > B_H ? d.ldx : B_H) < (int64_t(1) << 31),

@@ -45,9 +45,8 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int Q2_H = 256;    // hidden width
-constexpr int Q2_RB = 256;   // rows per workgroup (one gradient partial)
 constexpr int Q2_SB = 32;    // rows per LDS sub-block
-constexpr int Q2_NSB = Q2_RB / Q2_SB;
+constexpr int Q2_NSB8 = 8;   // sub-blocks per workgroup: 256 rows (one gradient partial)
 constexpr int Q2_QW = 64;    // layer-1 units per workgroup
 constexpr int Q2_LDZ = 257;  // dz2 row stride
 constexpr int Q2_NT = 512;   // threads: eight waves, two per SIMD
@@ -68,8 +67,14 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 // compile time so the LDS addresses of the x operand are immediates
 // NOSTAGE (timing probe only, tools/bench_q2.py --probe): the sub-block
 // staging and loads are skipped, every sub-block reuses the first one's tiles
-template <int XL, bool NOSTAGE = false>
+// NSB: 32-row sub-blocks per workgroup (8: 256-row partials; 1: 32-row
+// partials for passes of a few hundred rows, e.g. the K2 policy's 256)
+// DZIN: dz2 is given (d.dz2, already masked: a caller's head kernel formed
+// it, e.g. d3a_sac_actor_head for the policy) instead of generated from g, w3
+// and h2; no head gradients
+template <int XL, bool NOSTAGE = false, int Q2_NSB = Q2_NSB8, bool DZIN = false>
 __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
+  constexpr int Q2_RB = Q2_NSB * Q2_SB;
   __shared__ __attribute__((aligned(16))) Q2Lds<XL> L;
   static_assert(sizeof(Q2Lds<XL>) <= 163840, "LDS");
   const int t = threadIdx.x, lane = t & 63;
@@ -92,14 +97,19 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
   const int ldx = (int)d.ldx;
   constexpr int ldh = Q2_H;  // h1 / h2 rows are [C][rows][256] (checked)
   const float* h1g = d.h1 + c * d.sh;
-  const float* h2g = d.h2 + c * d.sh;
-  const float* gg = d.g + c * d.sgb;
+  // DZIN: h2g walks dz2 (same [rows][256] row layout), gg unused
+  const float* h2g = DZIN ? d.dz2 + c * d.sdz : d.h2 + c * d.sh;
+  const float* gg = DZIN ? nullptr : d.g + c * d.sgb;
   const float* xg = d.x + c * d.sxb;
   const float* W2g = d.W2 + c * d.sW2;
-  const float* w3g = d.w3 + c * d.sw3;
+  const float* w3g = DZIN ? nullptr : d.w3 + c * d.sw3;
   const float gs = d.gscale ? *d.gscale : 1.f;
   const int i0 = q * Q2_QW;
   const int nin = d.n_in, xr4 = (nin + 3) / 4;  // float4 pieces of an x row
+  // x rows as 16-byte pieces, or (ldx % 4 != 0) element by element
+  // (the 256-row critic instantiation is always handed padded rows: checked)
+  const bool xal = !DZIN || ((reinterpret_cast<uintptr_t>(d.x) | (uintptr_t)(d.ldx * 4) |
+                              (uintptr_t)(d.sxb * 4)) & 15) == 0;
   constexpr int x4 = XL / 4;
   const int64_t rlast = rows - 1;
   const bool role_dx = w < 4;
@@ -108,7 +118,7 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
 
   float w3v[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) w3v[j] = w3g[lane + 64 * j];
+  for (int j = 0; j < 4; ++j) w3v[j] = DZIN ? 0.f : w3g[lane + 64 * j];
 
   // ---- staging registers of one sub-block (unconditional loads, clamped
   // rows; validity applied when staged).  Thread (w, lane): h2 rows w + 8s
@@ -117,7 +127,7 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
   auto load_row = [&](int sb, int s) {
     int64_t r = rb0 + sb * Q2_SB + w + 8 * s;
     r = r < rlast ? r : rlast;
-    gv[s] = gg[r];
+    gv[s] = DZIN ? 0.f : gg[r];
 #pragma unroll
     for (int j = 0; j < 4; ++j) hv[s][j] = h2g[(int)r * ldh + lane + 64 * j];
   };
@@ -134,8 +144,14 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
       int64_t rx = base + ix / x4;
       rx = rx < rlast ? rx : rlast;
       const int cx = ix % x4 < xr4 ? ix % x4 : 0;  // pieces past n_in: staged as 0
-      const float4 a = *reinterpret_cast<const float4*>(xg + (int)rx * ldx + cx * 4);
-      xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
+      const float* px = xg + (int)rx * ldx + cx * 4;
+      if (xal) {
+        const float4 a = *reinterpret_cast<const float4*>(px);
+        xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
+      } else {  // unpadded rows (e.g. the policy's [obs; next_obs], ldx = n_in)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[e] = cx * 4 + e < nin ? px[e] : 0.f;
+      }
     }
   };
 
@@ -154,14 +170,16 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float hval = ok ? hv[s][j] : 0.f;
-      const float dzv = hval > 0.f ? gp * w3v[j] : 0.f;
+      const float dzv = DZIN ? hval : (hval > 0.f ? gp * w3v[j] : 0.f);
       L.dz[buf][rl * Q2_LDZ + lane + 64 * j] = dzv;
       hq = j == q ? hval : hq;
       dq = j == q ? dzv : dq;
     }
     acc_db2 += (double)dq;
-    acc_dw3 += (double)(gp * hq);
-    if (lane == 0) acc_db3 += (double)gp;
+    if (!DZIN) {
+      acc_dw3 += (double)(gp * hq);
+      if (lane == 0) acc_db3 += (double)gp;
+    }
   };
   auto stage_tiles = [&](int sb) {
     const int buf = sb % 3;
@@ -393,8 +411,8 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
       s3 += dscr[(v * 64 + tt) * 2 + 1];
     }
     d.db2[pc * Q2_H + i0 + tt] = (float)s2;
-    d.dW3[pc * Q2_H + i0 + tt] = (float)s3;
-  } else if (t == 320 && q == 0) {
+    if (!DZIN) d.dW3[pc * Q2_H + i0 + tt] = (float)s3;
+  } else if (!DZIN && t == 320 && q == 0) {
     double sg = 0.0;
     for (int v = 0; v < 8; ++v) sg += dscr[1024 + v];
     d.db3[pc] = (float)sg;
@@ -409,21 +427,30 @@ using namespace d3a;
 extern "C" int d3a_q2_bwd(const d3a_q2_bwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_bwd: null desc");
   const d3a_q2_bwd_desc& d = *dp;
-  D3A_CHECK_ARG(d.x && d.h1 && d.h2 && d.g && d.W2 && d.w3, "d3a_q2_bwd: null input");
-  D3A_CHECK_ARG(d.dW1 && d.db1 && d.dW2 && d.db2 && d.dW3 && d.db3, "d3a_q2_bwd: null output");
+  const bool dzin = d.dz2 != nullptr;
+  D3A_CHECK_ARG(d.x && d.h1 && d.W2 && (dzin || (d.h2 && d.g && d.w3)), "d3a_q2_bwd: null input");
+  D3A_CHECK_ARG(d.dW1 && d.db1 && d.dW2 && d.db2 && (dzin || (d.dW3 && d.db3)),
+                "d3a_q2_bwd: null output");
+  D3A_CHECK_ARG(d.block_rows == 0 || d.block_rows == 256 || (d.block_rows == 32 && dzin),
+                "d3a_q2_bwd: block_rows must be 0 / 256, or 32 with dz2");
+  D3A_CHECK_ARG(!dzin || (d.block_rows == 32), "d3a_q2_bwd: dz2 needs block_rows 32");
   D3A_CHECK_ARG(d.n_in >= 1 && d.n_in <= 48, "d3a_q2_bwd: n_in must be 1..48");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.n_scaled >= 0, "d3a_q2_bwd: bad sizes");
   // float4 loads of h1, x and W2 rows
   auto a16 = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; };
-  D3A_CHECK_ARG(a16(d.h1) && a16(d.h2) && d.ldh == Q2_H && d.sh % 4 == 0,
+  D3A_CHECK_ARG(a16(d.h1) && (dzin || a16(d.h2)) && d.ldh == Q2_H && d.sh % 4 == 0,
                 "d3a_q2_bwd: h1 / h2 must be 16-byte aligned rows of 256 floats");
-  D3A_CHECK_ARG(a16(d.x) && d.ldx % 4 == 0 && d.ldx >= ((d.n_in + 3) & ~3) && d.sxb % 4 == 0,
-                "d3a_q2_bwd: x rows must be 16-byte aligned with ldx >= n_in rounded to 4");
+  D3A_CHECK_ARG(!dzin || (a16(d.dz2) && d.sdz % 4 == 0),
+                "d3a_q2_bwd: dz2 must be 16-byte aligned rows of 256 floats");
+  D3A_CHECK_ARG(d.ldx >= d.n_in, "d3a_q2_bwd: ldx < n_in");
+  D3A_CHECK_ARG(dzin || (a16(d.x) && d.ldx % 4 == 0 && d.sxb % 4 == 0),
+                "d3a_q2_bwd: x rows must be 16-byte aligned with ldx % 4 == 0 (without dz2)");
   D3A_CHECK_ARG(a16(d.W2) && d.sW2 % 4 == 0, "d3a_q2_bwd: W2 must be 16-byte aligned");
   D3A_CHECK_ARG(d.rows * (d.ldh > d.ldx ? d.ldh : d.ldx) < (int64_t(1) << 31),
                 "d3a_q2_bwd: rows x row stride exceeds 2^31");
   if (d.rows == 0) return 0;
-  const int64_t units = ((d.rows + Q2_RB - 1) / Q2_RB) * d.C;
+  const int64_t rb = dzin ? 32 : 256;
+  const int64_t units = ((d.rows + rb - 1) / rb) * d.C;
   const int64_t blocks = (units + 7) / 8 * 32;
   D3A_CHECK_ARG(blocks < (int64_t(1) << 31), "d3a_q2_bwd: too many rows");
   const int xl = (d.n_in + 3) & ~3;
@@ -434,6 +461,16 @@ extern "C" int d3a_q2_bwd(const d3a_q2_bwd_desc* dp, void* stream) {
   }();
   if (probe && xl <= 16) {
     hipLaunchKernelGGL((q2_bwd_kernel<16, true>), grid, block, 0, (hipStream_t)stream, d);
+    D3A_LAUNCH_CHECK("d3a_q2_bwd");
+    return 0;
+  }
+  if (dzin) {
+    if (xl <= 16)
+      hipLaunchKernelGGL((q2_bwd_kernel<16, false, 1, true>), grid, block, 0, (hipStream_t)stream, d);
+    else if (xl <= 32)
+      hipLaunchKernelGGL((q2_bwd_kernel<32, false, 1, true>), grid, block, 0, (hipStream_t)stream, d);
+    else
+      hipLaunchKernelGGL((q2_bwd_kernel<48, false, 1, true>), grid, block, 0, (hipStream_t)stream, d);
     D3A_LAUNCH_CHECK("d3a_q2_bwd");
     return 0;
   }

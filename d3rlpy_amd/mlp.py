@@ -99,6 +99,20 @@ def q2_ok(net: EnsembleMLP, rows: int) -> bool:
             and rows * net.C >= _HEAD_GEN_MIN_ROWS)
 
 
+# trunk backward of a [n_in <= 48, 256, 256, J] net whose head a caller's
+# kernel differentiated (the SAC / CQL actor phase's policy, d3a_sac_actor_head
+# writes dz2 and the head partials): d3a_q2_bwd with dz2 given and 32-row
+# partials -- one launch instead of the paired layer-2 launch + the layer-1
+# weight-gradient launch
+_Q2P = os.environ.get("D3A_Q2P", "1") == "1"
+
+
+def q2p_ok(net: EnsembleMLP, rows: int) -> bool:
+    s = net.sizes
+    return (_Q2P and not _FUSED_BWD and not ops.SBF16_TERMS and net.n_layers == 3
+            and s[1] == 256 and s[2] == 256 and s[0] <= 48 and 0 < rows <= 4096)
+
+
 # small passes (policy over [obs; next_obs], actor / target passes of a few
 # hundred rows): 16-row workgroups, the whole MLP in one launch
 # (d3a_mlp_fwd block_rows 16, csrc/mlp_small.hip)
@@ -268,6 +282,9 @@ class BackwardSpace:
         self.grads = grads
         # every weight gradient from d3a_q2_bwd: one partial per 256-row block
         self.q2 = grads is not None and head_partials is None and q2_ok(net, rows)
+        # the trunk from a caller-formed dz2 (head_ready), 32-row partials
+        self.q2p = (grads is not None and head_partials is not None and not self.fused
+                    and q2p_ok(net, rows))
         # first-layer weight gradients as one partial per 128-row tile, from
         # the second layer's input-gradient GEMM (backward's wnext path; it
         # needs a layer above the first one, i.e. >= 2 hidden layers)
@@ -283,6 +300,8 @@ class BackwardSpace:
                     else (self.l0_tiles if (l == 0 and self.l0_tiles) else self.splits)
                 if self.q2:
                     parts = (rows + 255) // 256
+                elif self.q2p and l < net.n_layers - 1:
+                    parts = (rows + 31) // 32
                 grads.add(net.wname(l), (net.C, o, i), parts)
                 grads.add(net.bname(l), (net.C, o), parts)
 
@@ -341,6 +360,24 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         d.dW3, d.db3 = gs.get(net.wname(2)).data_ptr(), gs.get(net.bname(2)).data_ptr()
         d.rows, d.n_in, d.C = n, sizes[0], C
         ops.call_desc("d3a_q2_bwd_bf16" if esz == 2 else "d3a_q2_bwd", d)
+        return None
+
+    if (bs.q2p and weight_grads and head_ready and dx is None and members is None
+            and n == bs.rows):
+        # trunk backward in one launch from the head kernel's dz2 (bs.dz[0])
+        d = N.Q2BwdDesc()
+        H = sizes[1]
+        d.x, d.ldx, d.sxb = x + 4 * r0 * ldx, ldx, sxb_
+        d.h1 = acts.h[0].data_ptr() + 4 * r0 * H
+        d.sh, d.ldh = R * H, H
+        d.dz2, d.sdz = bs.dz[0].data_ptr(), bs.rows * bs.dz[0].shape[2]
+        assert bs.dz[0].shape[2] == H
+        d.block_rows = 32
+        d.W2, d.sW2 = net.W(1, store), H * H
+        d.dW1, d.db1 = gs.get(net.wname(0)).data_ptr(), gs.get(net.bname(0)).data_ptr()
+        d.dW2, d.db2 = gs.get(net.wname(1)).data_ptr(), gs.get(net.bname(1)).data_ptr()
+        d.rows, d.n_in, d.C = n, sizes[0], C
+        ops.call_desc("d3a_q2_bwd", d)
         return None
 
     def h_ptr(l):  # input activation of layer l at row r0

@@ -207,7 +207,9 @@ class AdamGroup:
         raw = bytes(segs)
         self.seg_table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
         self._segs = segs
+        self.block_table = self._block_table(segs, True)
         self.seg_table_reduced = None
+        self.block_table_reduced = None
         if self.grad_store is not None:
             # the same segments reading the already-reduced gradient (one
             # partial) from grad_store: the data-parallel path's Adam
@@ -221,6 +223,24 @@ class AdamGroup:
                 red[i].grad_out = None
             self.seg_table_reduced = torch.frombuffer(bytearray(bytes(red)),
                                                       dtype=torch.uint8).to(dev)
+            self.block_table_reduced = self._block_table(red, False)
+
+    def _block_table(self, segs, partials: bool) -> torch.Tensor:
+        """d3a_adam_block per flat block (the segment search done once here,
+        in the kernel's block order: segment s owns ceil(numel_s * L_s / 256)
+        blocks, L_s = 16 lanes per element for >= 64 partials, else 1)."""
+        rows = []
+        first = 0
+        for sg in segs:
+            lanes = 16 if (partials and sg.n_partials >= 64) else 1
+            nb = (sg.numel * lanes + 255) // 256
+            for _ in range(nb):
+                blk = N.AdamBlock()
+                blk.seg, blk.first = sg, first
+                rows.append(bytes(blk))
+            first += nb
+        raw = b"".join(rows)
+        return torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.store.data.device)
 
     def launch(self, reduced: bool = False, grad_scale: float = 1.0,
                tail: Optional[dict] = None) -> None:
@@ -243,8 +263,9 @@ class AdamGroup:
             assert targ.size == self.store.size and list(targ.specs) == list(self.store.specs)
             kw["targ_delta"] = (targ.data.data_ptr() - self.store.data.data_ptr()) // 4
             assert kw["targ_delta"] != 0
+        blocks = self.block_table_reduced if reduced else self.block_table
         ops.adam_step(table, len(self.names), nb, self.step, self.lr, self.beta1, self.beta2,
-                      self.eps, grad_scale, **kw)
+                      self.eps, grad_scale, blocks=blocks, **kw)
 
     def reduce(self) -> None:
         """grad_store <- sum of the split-K partials (no parameter update)."""

@@ -7,7 +7,9 @@ and contiguous where a row-major layout is implied.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
+import gc
 import os
 from typing import Optional, Sequence
 
@@ -145,7 +147,8 @@ def adam_step(segs: torch.Tensor, n_seg: int, n_blocks: int, step: torch.Tensor,
               step_add: int = 1, targ_delta: int = 0, tau: float = 0.0,
               counters: Optional[torch.Tensor] = None, inc_mask: int = 0,
               metrics: Optional[torch.Tensor] = None, ring: Optional[torch.Tensor] = None,
-              ring_ctr: Optional[torch.Tensor] = None, metric_scale: float = 1.0) -> None:
+              ring_ctr: Optional[torch.Tensor] = None, metric_scale: float = 1.0,
+              blocks: Optional[torch.Tensor] = None) -> None:
     """d3a_adam_step: Adam with the soft target update (``targ_delta`` != 0:
     the target copy ``targ_delta`` elements from each parameter) and the
     step's counter / metric-ring bookkeeping in one launch."""
@@ -159,6 +162,7 @@ def adam_step(segs: torch.Tensor, n_seg: int, n_blocks: int, step: torch.Tensor,
         d.metrics, d.n_metrics = ptr(metrics), metrics.numel()
         d.ring, d.ring_cap, d.ring_ctr = ptr(ring), ring.shape[0], ptr(ring_ctr)
     d.metric_scale = metric_scale
+    d.blocks = ptr(blocks)  # per-block segment table (AdamGroup), or None
     N.check(N.lib().d3a_adam_step(C.byref(d), _stream()), "d3a_adam_step")
 
 
@@ -352,3 +356,21 @@ def linear_bwd_w(dy: int, ldy: int, sdyb: int, x: int, ldx: int, sxb: int, dW: i
     gemm(dy, x, dW, n_out, n_in, R, batch=C_, sA=(sdyb, 1, ldy), sB=(sxb, ldx, 1),
          sC=(n_out * n_in, n_in, 1), splits=splits, sCs=C_ * n_out * n_in,
          rowsum=db, sR=(n_out, C_ * n_out), variant=variant)
+
+
+@contextlib.contextmanager
+def graph_capture(g):
+    """``torch.cuda.graph(g)`` with Python's cyclic garbage collector paused for
+    the capture: a collection triggered by an allocation inside the capture runs
+    the finalizers of unreachable objects from earlier work (freeing device
+    memory, destroying another HIP graph), which is not legal while the stream
+    is capturing -- measured as an abort in the GPU suite.  (torch.cuda.graph
+    already collects once before the capture starts.)"""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g):
+            yield
+    finally:
+        if was:
+            gc.enable()

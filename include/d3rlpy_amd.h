@@ -290,12 +290,13 @@ int d3a_mlp_bwd(const d3a_mlp_bwd_desc* d, void* stream);
  *   dz2 = g' w3 * [h2 > 0],  dz1 = (dz2 W2) * [h1 > 0]
  *   dW3 = g'^T h2, db3 = sum g', dW2 = dz2^T h1, db2 = sum dz2,
  *   dW1 = dz1^T x, db1 = sum dz1
- * as one partial per 256-row block p < P = ceil(rows / 256), laid out like
+ * as one partial per 256-row block p < P = ceil(rows / 256) (block_rows), laid out like
  * the split-K partials d3a_adam_f32 sums: dW1 [P][C][256][n_in], db1
  * [P][C][256], dW2 [P][C][256][256], db2 [P][C][256], dW3 [P][C][256], db3
  * [P][C].  h1 / h2 [C][rows][ldh] (member stride sh), x [rows][ldx] (member
  * stride sxb, 0 = shared), W2 [C][256][256] (stride sW2), w3 [C][256] (stride
- * sw3); h1, h2, x, W2 16-byte aligned, ldx % 4 == 0, n_in <= 48. */
+ * sw3); h1, h2, W2 16-byte aligned, ldx >= n_in (16-byte x pieces when x is
+ * aligned and ldx % 4 == 0, else element loads), n_in <= 48. */
 typedef struct d3a_q2_bwd_desc {
   const float* x; int64_t ldx, sxb;
   const float* h1; const float* h2; int64_t sh, ldh;
@@ -306,6 +307,15 @@ typedef struct d3a_q2_bwd_desc {
   float* dW1; float* db1; float* dW2; float* db2; float* dW3; float* db3;
   int64_t rows;
   int32_t n_in, C;
+  /* dz2 != NULL (fp32 only): the trunk backward of a two-hidden-layer net
+   * whose head a caller already differentiated -- dz2 [C][rows][256] (member
+   * stride sdz) is the masked pre-activation gradient of the second hidden
+   * layer (e.g. d3a_sac_actor_head's dz for the policy, sac_impl.py:164-176);
+   * g, w3, h2 are unused and dW3 / db3 not written.  block_rows: rows per
+   * partial, 0 or 256 (default), or 32 (required with dz2: the few-hundred-row
+   * actor pass spread over ceil(rows / 32) * 4 workgroups). */
+  const float* dz2; int64_t sdz;
+  int32_t block_rows;
 } d3a_q2_bwd_desc;
 int d3a_q2_bwd(const d3a_q2_bwd_desc* d, void* stream);
 
@@ -364,6 +374,14 @@ int d3a_adam_f32(const d3a_adam_segment* segs, int32_t n_seg,
  *       NULL metrics[0:n_metrics] (* metric_scale) appended to
  *       ring[*ring_ctr % ring_cap], *ring_ctr += 1 — as d3a_step_end; the
  *       counters incremented must not include the one `step` points at. */
+/* One workgroup's share of a flat Adam launch: its segment and the
+ * segment's first block (a table of n_blocks of these, built once per
+ * optimiser, saves the in-kernel segment search: one memory round trip). */
+typedef struct d3a_adam_block {
+  d3a_adam_segment seg;
+  int64_t first;
+} d3a_adam_block;
+
 typedef struct d3a_adam_desc {
   const d3a_adam_segment* segs; int32_t n_seg; int64_t n_blocks;
   const int64_t* step; int32_t step_add;
@@ -372,6 +390,10 @@ typedef struct d3a_adam_desc {
   int64_t* counters; uint32_t inc_mask;
   const float* metrics; int32_t n_metrics;
   float* ring; int64_t ring_cap; int64_t* ring_ctr; float metric_scale;
+  /* optional (may be NULL): DEVICE table of n_blocks d3a_adam_block, block b
+   * = the segment owning flat block b in the layout above and its first
+   * block; segs is then not read */
+  const d3a_adam_block* blocks;
 } d3a_adam_desc;
 int d3a_adam_step(const d3a_adam_desc* d, void* stream);
 

@@ -291,6 +291,51 @@ def test_adam_many_segments_matches_torch(dev):
                                    msg=f"reduced segment {k}")
 
 
+def test_adam_block_table_bit_identical(dev):
+    """d3a_adam_step with the per-block segment table (AdamGroup.block_table,
+    the production launch) against the in-kernel segment search on the same
+    150-segment layout (1 / 11 / 40 / 70 partials): bit-identical parameters,
+    moments and target copies (soft update fused)."""
+    from d3rlpy_amd import ops
+    from d3rlpy_amd.nets import AdamGroup, GradSpace, OptimState, ParamStore
+    g = torch.Generator().manual_seed(5)
+    n_seg = 150
+    sizes = [int(x) for x in torch.randint(1, 700, (n_seg,), generator=g)]
+    parts_of = [(1, 11, 40, 70)[k % 4] for k in range(n_seg)]
+    runs = []
+    for use_table in (True, False):
+        store = ParamStore()
+        for k, n in enumerate(sizes):
+            store.add(f"p{k}", (n,))
+        store.allocate(dev)
+        targ = store.like()
+        gs = GradSpace(dev)
+        gk = torch.Generator().manual_seed(9)
+        views = []
+        for k, n in enumerate(sizes):
+            x0 = torch.randn(n, generator=gk)
+            store.view(f"p{k}").copy_(x0)
+            targ.view(f"p{k}").copy_(x0 * 0.5)
+            views.append(gs.add(f"p{k}", (n,), parts_of[k]))
+        names = [f"p{k}" for k in range(n_seg)]
+        opt = AdamGroup(OptimState(store, names, lr=1e-3), gs)
+        ctr = torch.zeros(8, dtype=torch.int64, device=dev)
+        for it in range(3):
+            for k, n in enumerate(sizes):
+                views[k].copy_(torch.randn(parts_of[k], n, generator=gk).view(views[k].shape))
+            ops.adam_step(opt.seg_table, n_seg, opt.n_blocks, opt.step, opt.lr, opt.beta1,
+                          opt.beta2, opt.eps, 1.0, targ_delta=(targ.data.data_ptr()
+                                                               - store.data.data_ptr()) // 4,
+                          tau=0.005, counters=ctr, inc_mask=1,
+                          blocks=opt.block_table if use_table else None)
+            ops.step_end(opt.step, 1)
+        torch.cuda.synchronize()
+        runs.append((store.data.clone(), targ.data.clone(), opt.exp_avg.data.clone(),
+                     opt.exp_avg_sq.data.clone(), ctr.clone()))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+
+
 def test_philox_statistics(dev):
     from d3rlpy_amd import ops
     out = torch.zeros(1 << 20, device=dev)

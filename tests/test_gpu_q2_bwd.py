@@ -113,3 +113,63 @@ def test_q2_bwd_rejects_bad_shapes():
     d = N.Q2BwdDesc()
     rc = N.lib().d3a_q2_bwd(C.byref(d), None)
     assert rc < 0 and b"null input" in N.lib().d3a_last_error()
+
+
+def _run_dz(x, ldx, h1, dz2, W2, n_in, rows, Cm):
+    P = (rows + 31) // 32
+    dev = x.device
+    out = {
+        "dW1": torch.full((P, Cm, H, n_in), float("nan"), device=dev),
+        "db1": torch.full((P, Cm, H), float("nan"), device=dev),
+        "dW2": torch.full((P, Cm, H, H), float("nan"), device=dev),
+        "db2": torch.full((P, Cm, H), float("nan"), device=dev),
+    }
+    d = N.Q2BwdDesc()
+    d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
+    d.h1, d.sh, d.ldh = h1.data_ptr(), rows * H, H
+    d.dz2, d.sdz, d.block_rows = dz2.data_ptr(), rows * H, 32
+    d.W2, d.sW2 = W2.data_ptr(), H * H
+    for k, v in out.items():
+        setattr(d, k, v.data_ptr())
+    d.rows, d.n_in, d.C = rows, n_in, Cm
+    ops.call_desc("d3a_q2_bwd", d)
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("rows,n_in,ldx,Cm", [
+    (256, 11, 11, 1),   # K2 policy trunk: [obs; next_obs] rows unpadded (ldx = n_in)
+    (256, 29, 29, 1),   # K4 antmaze policy
+    (100, 3, 3, 1),     # ragged last 32-row block
+    (300, 16, 16, 2),   # aligned rows, two members
+    (64, 48, 52, 1),
+])
+def test_q2_bwd_dz2_trunk_matches_fp64(rows, n_in, ldx, Cm):
+    """dz2 given (d3a_sac_actor_head's masked head input gradient): the trunk
+    of the policy backward (encoders.py:265-275 under sac_impl.py:164-176), as
+    one partial per 32-row block, against fp64."""
+    gen = torch.Generator(device="cuda").manual_seed(rows * 7 + n_in)
+    dev = "cuda"
+    # x as a flat buffer of rows ldx apart, with one row of slack
+    xb = torch.randn((rows + 1) * ldx, device=dev, generator=gen)
+    x = xb[: rows * ldx].view(rows, ldx)
+    h1 = torch.relu(torch.randn(Cm, rows, H, device=dev, generator=gen))
+    h2 = torch.randn(Cm, rows, H, device=dev, generator=gen)
+    dz2 = torch.randn(Cm, rows, H, device=dev, generator=gen) * 1e-2 * (h2 > 0)
+    W2 = torch.randn(Cm, H, H, device=dev, generator=gen) * 0.06
+    out = _run_dz(x, ldx, h1, dz2, W2, n_in, rows, Cm)
+    xd = x[:, :n_in].double()
+    for p in range((rows + 31) // 32):
+        sl = slice(32 * p, min(rows, 32 * p + 32))
+        for c in range(Cm):
+            a1, dz = h1[c, sl].double(), dz2[c, sl].double()
+            dz1 = (dz @ W2[c].double()) * (a1 > 0)
+            exp = {"dW1": dz1.T @ xd[sl], "db1": dz1.sum(0), "dW2": dz.T @ a1, "db2": dz.sum(0)}
+            for k, e in exp.items():
+                got = out[k][p, c].double()
+                assert torch.isfinite(got).all(), (k, p, c)
+                err = ((got - e).abs().max() / e.abs().max().clamp_min(1e-30)).item()
+                assert err < 1e-5, (k, p, c, err)
+    again = _run_dz(x, ldx, h1, dz2, W2, n_in, rows, Cm)
+    for k in out:
+        assert torch.equal(out[k], again[k]), k
