@@ -60,6 +60,27 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   return s;
 }
 
+// block_sum of K values at once (one pair of barriers; each sum in the same
+// order as block_sum, so bitwise equal).  `scratch` holds K * blockDim.x / 64.
+template <int K>
+__device__ __forceinline__ void block_sum_k(float (&v)[K], float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = wave_sum(v[k]);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) scratch[k * nw + wid] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float s = 0.f;
+    for (int i = 0; i < nw; ++i) s += scratch[k * nw + i];
+    v[k] = s;
+  }
+}
+
 // torch.nn.functional.softplus(x, beta=1, threshold=20)
 __device__ __forceinline__ float softplus_t(float x) {
   return x > 20.f ? x : log1pf(expf(x));

@@ -299,7 +299,7 @@ constexpr int LOSS_MP = 8;
 
 template <bool REG>
 __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
-  __shared__ float scratch[16];
+  __shared__ float scratch[48];  // block_sum_k<3> over 16 waves
   __shared__ float sh[4];
   __shared__ double s_bc[4];
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -322,11 +322,14 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   float r_lseA[LOSS_MP], r_qd[LOSS_MP], r_lseC[LOSS_MP], r_tq[LOSS_MP], r_rw[LOSS_MP],
       r_tm[LOSS_MP], r_ns[LOSS_MP];
   float ltemp = 0.f, tm_ = 0.f, tv_ = 0.f, lalpha = 0.f, am_ = 0.f, av_ = 0.f;
+  int64_t tstep = 0, astep = 0;  // the optimisers' step counts (thread 0)
   if (tid == 0) {
     ltemp = *d.log_temp;
     lalpha = *d.log_alpha;
-    if (temp_on) { tm_ = *d.temp_m; tv_ = *d.temp_v; }
-    if (alpha_on) { am_ = *d.alpha_m; av_ = *d.alpha_v; }
+    // (read here with the other scalars: the increments below would otherwise
+    // reload them behind the state stores, a dependent round trip each)
+    if (temp_on) { tm_ = *d.temp_m; tv_ = *d.temp_v; tstep = *d.temp_step; }
+    if (alpha_on) { am_ = *d.alpha_m; av_ = *d.alpha_v; astep = *d.alpha_step; }
   }
   float s_temp = 0.f;
   if (temp_on && phase != 2)
@@ -383,7 +386,7 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
         float* pm = d.temp_m; float* pv = d.temp_v;
         const float ln = adam_scalar_r(ltemp, tm_, tv_, g, d.temp_lr, d.beta1, d.beta2,
                                        d.adam_eps, s_bc);
-        *pm = tm_; *pv = tv_; *d.log_temp = ln; *d.temp_step = *d.temp_step + 1;
+        *pm = tm_; *pv = tv_; *d.log_temp = ln; *d.temp_step = tstep + 1;
         ltemp = ln;
         d.metrics[1] = expf(ln);
       }
@@ -408,8 +411,10 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
           }
         }
       }
-      lsum = block_sum(sl, scratch);
-      dsum = block_sum(sd, scratch);
+      float v2[2] = {sl, sd};
+      block_sum_k<2>(v2, scratch);
+      lsum = v2[0];
+      dsum = v2[1];
     }
     if (tid == 0) {
       float g = 0.f;
@@ -430,7 +435,7 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
         float* pm = d.alpha_m; float* pv = d.alpha_v;
         const float ln = adam_scalar_r(lalpha, am_, av_, g, d.alpha_lr, d.beta1, d.beta2,
                                        d.adam_eps, s_bc + 2);
-        *pm = am_; *pv = av_; *d.log_alpha = ln; *d.alpha_step = *d.alpha_step + 1;
+        *pm = am_; *pv = av_; *d.log_alpha = ln; *d.alpha_step = astep + 1;
         lalpha = ln;
         d.metrics[3] = expf(ln);
       }
@@ -473,9 +478,11 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   // critic-set IS rows keep the unscaled softmax weights of stage A; the
   // backward (d3a_head1_bwd) multiplies them by scalars[2] = gcons on read.
   if (tid == 0) d.scalars[2] = gcons;
-  const float td = block_sum(s_td, scratch) / (float)B;
-  const float lsum = block_sum(s_l, scratch);
-  const float dsum = block_sum(s_d, scratch);
+  float v3[3] = {s_td, s_l, s_d};
+  block_sum_k<3>(v3, scratch);
+  const float td = v3[0] / (float)B;
+  const float lsum = v3[1];
+  const float dsum = v3[2];
   if (tid == 0) {
     const float loss = lsum / (float)CB - dsum / (float)CB;
     const float cons = cons_on ? ca * (d.conservative_weight * loss - d.alpha_threshold) : 0.f;
