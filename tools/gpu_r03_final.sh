@@ -25,3 +25,4 @@ for a in td3bc bcq dcql cqldp; do
   timeout -k 10 300 python bench.py --algo $a --cpu-seconds 10 > gpurun_out/fin_bench_$a.log 2>&1 || exit $?
 done
 timeout -k 10 200 python bench.py --precision bf16 --steps 2000 --no-cpu-baseline > gpurun_out/fin_bench_bf16.log 2>&1 || exit $?
+timeout -k 10 60 ./tools/probes/pow_latency > gpurun_out/pow_latency.jsonl 2>&1 || true
