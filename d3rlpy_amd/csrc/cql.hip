@@ -368,9 +368,35 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
   };
   __syncthreads();  // s_bc
 
+  // the temperature's and alpha's block sums in one barrier pair (each in
+  // block_sum's order)
+  float tsum = 0.f, alsum = 0.f, adsum = 0.f;
+  if (phase != 2 && (temp_on || alpha_on)) {
+    float sl = 0.f, sd = 0.f;
+    if (alpha_on) {
+#pragma unroll
+      for (int i = 0; i < (REG ? LOSS_MP : 1); ++i) {
+        if (REG) {
+          sl += r_lseA[i];
+          sd += r_qd[i];
+        } else {
+          for (int k = 0; k < n_slot; ++k) {
+            const int j = slot(k);
+            sl += r_lseA[j];
+            sd += r_qd[j];
+          }
+        }
+      }
+    }
+    float v3[3] = {s_temp, sl, sd};
+    block_sum_k<3>(v3, scratch);
+    tsum = v3[0];
+    alsum = v3[1];
+    adsum = v3[2];
+  }
+
   // ---- update_temp (sac_impl.py:123-146) ----
   if (temp_on) {
-    const float tsum = phase != 2 ? block_sum(s_temp, scratch) : 0.f;
     if (tid == 0) {
       float g = 0.f;
       if (phase != 2) {
@@ -395,31 +421,10 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
 
   // ---- update_alpha (cql_impl.py:119-141) on sample set 0 ----
   if (alpha_on) {
-    float lsum = 0.f, dsum = 0.f;
-    if (phase != 2) {
-      float sl = 0.f, sd = 0.f;
-#pragma unroll
-      for (int i = 0; i < (REG ? LOSS_MP : 1); ++i) {
-        if (REG) {
-          sl += r_lseA[i];
-          sd += r_qd[i];
-        } else {
-          for (int k = 0; k < n_slot; ++k) {
-            const int j = slot(k);
-            sl += r_lseA[j];
-            sd += r_qd[j];
-          }
-        }
-      }
-      float v2[2] = {sl, sd};
-      block_sum_k<2>(v2, scratch);
-      lsum = v2[0];
-      dsum = v2[1];
-    }
     if (tid == 0) {
       float g = 0.f;
       if (phase != 2) {
-        const float loss = lsum / (float)CB - dsum / (float)CB;
+        const float loss = alsum / (float)CB - adsum / (float)CB;
         const float scaled = d.conservative_weight * loss;
         const float e = expf(lalpha);
         const float ca = fminf(fmaxf(e, 0.f), 1e6f);
