@@ -133,20 +133,53 @@ __global__ __launch_bounds__(256) void bcq_vae_enc_grad_kernel(d3a_bcq_vae_desc 
 
 // ---- BCQ target: compute_max_with_n_actions over N sampled actions ---------
 // q: [C][B*N][K] target-critic quantiles (row b*N + n); one workgroup per b
-__global__ __launch_bounds__(256) void bcq_target_kernel(d3a_bcq_target_desc d) {
+// (the waves keep eight quantile rows each in flight)
+constexpr int TG_T = 256;
+__global__ __launch_bounds__(TG_T) void bcq_target_kernel(d3a_bcq_target_desc d) {
   extern __shared__ float sm[];  // [C][N] quantile means
   __shared__ int s_arg, s_cmax, s_cmin;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int64_t b = blockIdx.x;
   const int C = d.C, N = d.N, K = d.K;
   const int64_t BN = (int64_t)d.B * N;
-  for (int p = wid; p < C * N; p += 4) {
-    const int c = p / N, n = p - c * N;
-    const float* q = d.q + ((int64_t)c * BN + b * N + n) * K;
-    float s = 0.f;
-    for (int k = lane; k < K; k += 64) s += q[k];
-    s = wave_sum(s);
-    if (lane == 0) sm[c * N + n] = s / (float)K;  // values.mean(dim=3)
+  const int CN = C * N;
+  if (K <= 256) {
+    // eight (c, n) rows per wave in flight (their loads issued before any
+    // sum), each row summed exactly as below: lane l adds q[l], q[l + 64], ..
+    // in order, then the wave butterfly -- bitwise the same means
+    constexpr int PB = 8;
+    for (int p0 = wid * PB; p0 < CN; p0 += (TG_T / 64) * PB) {
+      float v[PB][4];
+#pragma unroll
+      for (int i = 0; i < PB; ++i) {
+        const int p = p0 + i < CN ? p0 + i : CN - 1;
+        const int c = p / N, n = p - c * N;
+        const float* q = d.q + ((int64_t)c * BN + b * N + n) * K;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = lane + 64 * u;
+          v[i][u] = k < K ? q[k] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < PB; ++i) {
+        float s = 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (lane + 64 * u < K) s += v[i][u];
+        s = wave_sum(s);
+        if (lane == 0 && p0 + i < CN) sm[p0 + i] = s / (float)K;  // values.mean(dim=3)
+      }
+    }
+  } else {
+    for (int p = wid; p < CN; p += TG_T / 64) {
+      const int c = p / N, n = p - c * N;
+      const float* q = d.q + ((int64_t)c * BN + b * N + n) * K;
+      float s = 0.f;
+      for (int k = lane; k < K; k += 64) s += q[k];
+      s = wave_sum(s);
+      if (lane == 0) sm[c * N + n] = s / (float)K;  // values.mean(dim=3)
+    }
   }
   __syncthreads();
   if (t == 0) {
@@ -169,7 +202,7 @@ __global__ __launch_bounds__(256) void bcq_target_kernel(d3a_bcq_target_desc d) 
   __syncthreads();
   const float* qmax = d.q + ((int64_t)s_cmax * BN + b * N + s_arg) * K;
   const float* qmin = d.q + ((int64_t)s_cmin * BN + b * N + s_arg) * K;
-  for (int k = t; k < K; k += 256)
+  for (int k = t; k < K; k += TG_T)
     d.target[b * K + k] = __fadd_rn(__fmul_rn(1.f - d.lam, qmax[k]), __fmul_rn(d.lam, qmin[k]));
 }
 
@@ -300,7 +333,7 @@ extern "C" int d3a_bcq_target(const d3a_bcq_target_desc* d, void* stream) {
   D3A_CHECK_ARG(d && d->q && d->target, "d3a_bcq_target: null pointer");
   D3A_CHECK_ARG(d->B >= 1 && d->N >= 1 && d->K >= 1 && d->C >= 1 && d->C * d->N <= 8192,
                 "d3a_bcq_target: bad sizes");
-  hipLaunchKernelGGL(bcq_target_kernel, dim3((unsigned)d->B), dim3(256),
+  hipLaunchKernelGGL(bcq_target_kernel, dim3((unsigned)d->B), dim3(TG_T),
                      (size_t)d->C * d->N * sizeof(float), (hipStream_t)stream, *d);
   D3A_LAUNCH_CHECK("d3a_bcq_target");
   return 0;
