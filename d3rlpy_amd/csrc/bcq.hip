@@ -132,9 +132,9 @@ __global__ __launch_bounds__(256) void bcq_vae_enc_grad_kernel(d3a_bcq_vae_desc 
 }
 
 // ---- BCQ target: compute_max_with_n_actions over N sampled actions ---------
-// q: [C][B*N][K] target-critic quantiles (row b*N + n); one workgroup per b
-// (the waves keep eight quantile rows each in flight)
-constexpr int TG_T = 256;
+// q: [C][B*N][K] target-critic quantiles (row b*N + n); one workgroup of
+// sixteen waves per b (the waves keep eight quantile rows each in flight)
+constexpr int TG_T = 1024;
 __global__ __launch_bounds__(TG_T) void bcq_target_kernel(d3a_bcq_target_desc d) {
   extern __shared__ float sm[];  // [C][N] quantile means
   __shared__ int s_arg, s_cmax, s_cmin;
@@ -182,10 +182,14 @@ __global__ __launch_bounds__(TG_T) void bcq_target_kernel(d3a_bcq_target_desc d)
     }
   }
   __syncthreads();
-  if (t == 0) {
+  if (wid == 0) {
+    // argmax over n of the mix (the first n of the largest value, as a
+    // sequential strict-greater scan picks it; NaN never wins): each lane
+    // scans n = lane, lane + 64, .. in order, then the wave reduces
+    // (largest value, then smallest n)
     float best = -INFINITY;
-    int arg = 0, bmax = 0, bmin = 0;
-    for (int n = 0; n < N; ++n) {
+    int arg = -1, bmax = 0, bmin = 0;
+    for (int n = lane; n < N; n += 64) {
       float mx = sm[n], mn = sm[n];
       int cmx = 0, cmn = 0;
       for (int c = 1; c < C; ++c) {
@@ -197,7 +201,14 @@ __global__ __launch_bounds__(TG_T) void bcq_target_kernel(d3a_bcq_target_desc d)
       const float mix = __fadd_rn(__fmul_rn(1.f - d.lam, mx), __fmul_rn(d.lam, mn));
       if (mix > best) { best = mix; arg = n; bmax = cmx; bmin = cmn; }
     }
-    s_arg = arg; s_cmax = bmax; s_cmin = bmin;
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oa = __shfl_xor(arg, o, 64);
+      const int ox = __shfl_xor(bmax, o, 64), on = __shfl_xor(bmin, o, 64);
+      const bool take = oa >= 0 && (arg < 0 || ob > best || (ob == best && oa < arg));
+      if (take) { best = ob; arg = oa; bmax = ox; bmin = on; }
+    }
+    if (lane == 0) { s_arg = arg < 0 ? 0 : arg; s_cmax = bmax; s_cmin = bmin; }
   }
   __syncthreads();
   const float* qmax = d.q + ((int64_t)s_cmax * BN + b * N + s_arg) * K;
