@@ -170,22 +170,26 @@ WORKLOADS = {
 }
 
 
-def _make_algo(name: str, batch: int):
+def _make_algo(name: str, batch: int, gpu: int = 0):
+    """The workload's algorithm on GPU ``gpu`` (this rank's LOCAL_RANK)."""
     if name in ("cql", "cqldp"):
         from d3rlpy_amd.algos.cql import CQL
-        return CQL(batch_size=batch, n_critics=2, n_action_samples=10)
+        return CQL(batch_size=batch, n_critics=2, n_action_samples=10, use_gpu=gpu)
     if name == "dcql":
         from d3rlpy_amd.algos.cql import DiscreteCQL
-        return DiscreteCQL(batch_size=batch, n_frames=4, q_func_factory="iqn", scaler="pixel")
+        return DiscreteCQL(batch_size=batch, n_frames=4, q_func_factory="iqn", scaler="pixel",
+                           use_gpu=gpu)
     if name == "bcq":
         from d3rlpy_amd.algos.bcq import BCQ
         from d3rlpy_amd.factories import QRQFunctionFactory
-        return BCQ(batch_size=batch, q_func_factory=QRQFunctionFactory(n_quantiles=200))
+        return BCQ(batch_size=batch, q_func_factory=QRQFunctionFactory(n_quantiles=200),
+                   use_gpu=gpu)
     from d3rlpy_amd.algos.td3_plus_bc import TD3PlusBC
-    return TD3PlusBC(batch_size=batch)
+    return TD3PlusBC(batch_size=batch, use_gpu=gpu)
 
 
-def build_workload(rank: int, n_transitions: int, name: str = "cql", world: int = 1):
+def build_workload(rank: int, n_transitions: int, name: str = "cql", world: int = 1,
+                   local: int = 0):
     from d3rlpy_amd.dataset import DeviceDataset
     from d3rlpy_amd.datasets import get_synthetic_d4rl
     from d3rlpy_amd.iterators import RandomIterator
@@ -197,11 +201,12 @@ def build_workload(rank: int, n_transitions: int, name: str = "cql", world: int 
         ds = get_synthetic_d4rl(shape, n=n_transitions, seed=0)
     import torch
     torch.manual_seed(rank)
-    algo = _make_algo(name, batch)
+    algo = _make_algo(name, batch, local)
     if algo.scaler is not None:
         algo.scaler.fit_dataset(ds)  # as fit() does before building the impl
     algo.build_with_dataset(ds)
-    ddata = DeviceDataset(ds)
+    ddata = DeviceDataset(ds, device=f"cuda:{local}")
+    assert algo.impl.device == f"cuda:{local}", (algo.impl.device, local)
     shard = (0, 1)
     seed = 1000 + rank
     if name == "cqldp" and world > 1:
@@ -509,7 +514,7 @@ def main():
     if ws != args.gpus:
         print(f"bench: WORLD_SIZE={ws} but --gpus {args.gpus}; reporting n_gpus={ws}",
               file=sys.stderr)
-    algo, it = build_workload(rank, args.transitions, args.algo, ws)
+    algo, it = build_workload(rank, args.transitions, args.algo, ws, local)
     ar_log = _record_all_reduces(algo)
 
     gpu_steps(algo, it, 1)  # eager first update: its all-reduces are recorded

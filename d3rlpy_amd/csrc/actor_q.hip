@@ -233,8 +233,11 @@ __global__ __launch_bounds__(256) void sac_actor_q_kernel(d3a_sac_actor_q_desc d
     const int r = m0 + t;
     if (r < d.B)
       d.q[pc * d.B + r] = (((S.qp[0][t] + S.qp[1][t]) + S.qp[2][t]) + S.qp[3][t]) + bh;
-  } else if (t >= 64 && t < 64 + AQ_RB * A) {
-    const int e = t - 64, m = e / A, j = e - m * A;
+  }
+  // AQ_RB * A <= 256 entries: threads 0..255 cover every (row, action) pair
+  // (waves 1..3 first, so wave 0's q stores issue alongside)
+  for (int e = (t + 64) & 255; e < AQ_RB * A; e += 256) {
+    const int m = e / A, j = e - m * A;
     const int r = m0 + m;
     if (r < d.B)
       d.dq_da[(pc * d.B + r) * A + j] =

@@ -260,8 +260,8 @@ __device__ __forceinline__ float is_value(const d3a_cql_loss_desc& d, int64_t c,
 // Stage A (many waves): one wave per (sample set s, critic c, batch row b):
 // lse[s][c][b] = logsumexp_j v_j over the 3N IS values (torch.logsumexp:
 // amax shift, |max| == inf -> 0), and for the critic set the softmax
-// weights exp(v_j - lse) into dq (scaled by the alpha-dependent factor in
-// stage B).
+// weights exp(v_j - lse) = exp(v_j - max) / sum_j exp(v_j - max) into dq
+// (scaled by the alpha-dependent factor in stage B).
 __global__ __launch_bounds__(256) void cql_lse_kernel(d3a_cql_loss_desc d) {
   const int lane = threadIdx.x & 63;
   const int64_t B = d.B, C = d.C, N = d.N, NB = N * B, M = 3 * N;
@@ -280,9 +280,14 @@ __global__ __launch_bounds__(256) void cql_lse_kernel(d3a_cql_loss_desc d) {
   const float l = logf(se) + mx;
   if (lane == 0) d.lse[(s * C + c) * B + b] = l;
   if (s == 1) {
+    // softmax weight exp(v_j - lse) formed as exp(v_j - max) / sum: the same
+    // value without lse's absolute rounding (eps |lse|, shared by every j)
+    // scaling all 3N weights -- that shared error survives the cancellation of
+    // the sampled and data rows in the head-bias / hidden-layer gradients
     for (int64_t j = lane; j < M; j += 64) {
       const int64_t blk = j / N, n = j % N;
-      d.dq[c * d.R + 3 * NB + blk * NB + b * N + n] = expf(is_value(d, c, 1, b, j, rand_logp) - l);
+      d.dq[c * d.R + 3 * NB + blk * NB + b * N + n] =
+          __fdiv_rn(expf(is_value(d, c, 1, b, j, rand_logp) - mx), se);
     }
   }
 }

@@ -1,0 +1,291 @@
+// fp32 critic ensemble on the bf16 matrix cores: the forward of the
+// [n_in <= 48 -> 256 -> 256 -> 1] Q ensemble (q2_fwd.hip's contract, d3a_mlp_fwd
+// descriptor) with every GEMM evaluated as a three-way split-bf16 product.
+//
+// Reference: VectorEncoderWithAction [n_in -> 256 -> 256] (encoders.py:265-275,
+// 328-339) + ContinuousMeanQFunction._fc [256 -> 1] (q_functions/
+// mean_q_function.py:255-256), over the CQL critic pass (15,616 Q rows + 256
+// target rows per member at K2) -- fp32 in the reference, fp32-accurate here.
+//
+// Split products.  An fp32 value x is split exactly into three bf16 parts,
+//   x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1),  x = x0 + x1 + x2
+// (each subtraction exact in fp32; 8 + 8 + 8 significant bits), and a product
+// x * y is formed as the six part products above fp32's resolution,
+//   x2 y0 + x1 y1 + x0 y2 + x1 y0 + x0 y1 + x0 y0   (dropped: x1 y2, x2 y1,
+//   x2 y2, each below 2^-24 |x y|),
+// on v_mfma_f32_32x32x16_bf16 with fp32 accumulation: six 32-cycle MFMAs per
+// 16 k against eight 64-cycle v_mfma_f32_32x32x2_f32 -- 2.67x the fp32 MFMA
+// rate on the same work.  The split GEMM is within 6e-7 (max-normalised) of
+// fp64 where fp32 MFMA is within 5e-7 (profiles/r02_sbf16_accuracy.txt); the
+// CQL parity suite holds at its fp32 bars on it (tests/test_gpu_x6.py).
+//
+// Forward structure.  A workgroup owns 128 rows of one member; eight waves,
+// wave w owning hidden units 32 w .. 32 w + 31 of layer 2 over all 128 rows
+// (four transposed tiles C^T[unit][row]: W1 the A operand, activation rows the
+// B operand, so a lane holds one row and four runs of four consecutive units:
+// 16-byte stores and a register head dot, as in q2_fwd.hip).  Layer 2's K (the
+// 256 layer-1 units) is walked in eight chunks of 32.  Layer 1 produces chunk
+// j + 1 (its 32 units for the 128 rows: four 32x32 tiles, one per wave of the
+// half (j + 1) & 1, so each SIMD carries one producing wave per chunk) while
+// layer 2 consumes chunk j; the chunk is written to a two-slot LDS ring as its
+// three bf16 parts ([row][k], 80-byte rows: conflict-free 16-byte fragment
+// reads), and as fp32 to h[0] for kept rows.  Each wave loads its W1 slice of
+// the next chunk from global memory as fp32 one chunk ahead and splits it in
+// registers.  One barrier per chunk.
+#include <cstdlib>
+#include "common.hpp"
+#include "../../include/d3rlpy_amd.h"
+#include "x6.hpp"
+
+namespace d3a {
+namespace {
+
+using namespace x6;
+
+constexpr int X_H = 256;    // hidden width
+constexpr int X_RB = 128;   // rows per workgroup
+constexpr int X_CK = 32;    // layer-2 k per chunk (= layer-1 units per chunk)
+constexpr int X_NCK = X_H / X_CK;
+constexpr int X_LDB = 40;   // bf16 row stride of a ring slot (80 B)
+
+template <int XL>
+struct X6FwdLds {
+  __bf16 h[2][3][X_RB * X_LDB];     // layer-1 chunk ring: slot, part, [row][k]
+  __bf16 x[3][X_RB * (XL + 8)];     // input rows, parts, zero-padded to XL
+  float hp[8][X_RB];                // head partials [wave][row]
+};
+
+template <int XL>
+__global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
+  constexpr int XLD = XL + 8;
+  constexpr int NS0 = XL / 16;  // layer-1 k steps
+  __shared__ __attribute__((aligned(16))) X6FwdLds<XL> L;
+  static_assert(sizeof(X6FwdLds<XL>) <= 163840, "LDS");
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  const int c = blockIdx.z;
+  const int nb_main = (int)((d.rows + X_RB - 1) / X_RB);
+  const bool aux = (int)blockIdx.x >= nb_main;
+  // row indices fit 32 bits (checked on the host)
+  const int m0 = aux ? ((int)blockIdx.x - nb_main) * X_RB : (int)d.r0 + (int)blockIdx.x * X_RB;
+  const int rend = aux ? (int)d.aux_rows : (int)(d.r0 + d.rows);
+  const int h_from = aux ? rend : (int)d.h_from;
+  const int64_t wdel = aux ? d.aux_wdelta : 0;
+  float* const outp = aux ? d.aux_out + c * d.aux_sout : d.out + c * d.sout;
+  const int nin = d.n_in;
+  float* const h0g = (!aux && d.h[0]) ? d.h[0] + c * d.sh : nullptr;
+  float* const h1g = (!aux && d.h[1]) ? d.h[1] + c * d.sh : nullptr;
+  const float* W0 = d.W[0] + wdel + c * d.sW[0];
+  const float* b0 = d.b[0] + wdel + c * d.sb[0];
+  // this lane's W1 row (unit 32 w + li) at k offset 8 lh
+  const float* W1 = d.W[1] + wdel + c * d.sW[1] + (32 * w + li) * X_H + 8 * lh;
+
+  // ---- prologue: the first W1 chunk in flight, input rows split into LDS
+  float4 wr[2][2];  // raw fp32 W1 of the chunk in flight: [k step][half]
+  auto load_w1 = [&](int j) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      wr[s][0] = *reinterpret_cast<const float4*>(W1 + X_CK * j + 16 * s);
+      wr[s][1] = *reinterpret_cast<const float4*>(W1 + X_CK * j + 16 * s + 4);
+    }
+  };
+  load_w1(0);
+  {
+    const float* xb = aux ? d.aux_x + c * d.aux_sxb : d.x + c * d.sxb;
+    const int64_t ldx = aux ? d.aux_ldx : d.ldx;
+    constexpr int X4 = XL / 4;
+    for (int e = t; e < X_RB * X4; e += 512) {
+      const int m = e / X4, k4 = (e - m * X4) * 4;
+      const int r = m0 + m;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? xb[r * ldx + k4 + j] : 0.f;
+      bf16x4 p[3];
+      split4(v, p);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&L.x[q][m * XLD + k4]) = p[q];
+    }
+  }
+  __syncthreads();  // x parts staged
+
+  // ---- layer 1, chunk j: units 32 j .. + 31 of rows 32 (w & 3) .. + 31 (a wave
+  // of the half j & 1): bias, ReLU, fp32 kept rows to h[0], parts to ring slot
+  // j & 1.  The wave's W0 rows and bias of its next chunk are loaded one
+  // production ahead (a production is on the chunk's critical path).
+  float w0n[NS0][8];
+  float4 b0n[4];
+  auto load_w0 = [&](int j) {
+    const int u = X_CK * j + li;
+#pragma unroll
+    for (int s = 0; s < NS0; ++s)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = 16 * s + 8 * lh + i;
+        w0n[s][i] = k < nin ? W0[u * nin + k] : 0.f;
+      }
+#pragma unroll
+    for (int R = 0; R < 4; ++R) b0n[R] = *reinterpret_cast<const float4*>(b0 + X_CK * j + 8 * R + 4 * lh);
+  };
+  load_w0(w >> 2);
+  auto produce = [&](int j) {
+    const int tt = w & 3;
+    f32x16 a;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS0; ++s) {
+      bf16x8 wp[3], xp[3];
+      split8(w0n[s], wp);
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        xp[q] = *reinterpret_cast<const bf16x8*>(&L.x[q][(32 * tt + li) * XLD + 16 * s + 8 * lh]);
+      a = prod6(wp, xp, a);
+    }
+    float4 bv4[4];
+#pragma unroll
+    for (int R = 0; R < 4; ++R) bv4[R] = b0n[R];
+    if (j + 2 < X_NCK) load_w0(j + 2);
+    // lane: row 32 tt + li, units 32 j + 8 R + 4 lh + i (accumulator 4 R + i)
+    const int row = m0 + 32 * tt + li;
+    const bool keep = h0g != nullptr && row >= h_from && row < rend;
+#pragma unroll
+    for (int R = 0; R < 4; ++R) {
+      const int k = 8 * R + 4 * lh;  // local k of the chunk
+      const float4 bv = bv4[R];
+      float v[4] = {fmaxf(a[4 * R + 0] + bv.x, 0.f), fmaxf(a[4 * R + 1] + bv.y, 0.f),
+                    fmaxf(a[4 * R + 2] + bv.z, 0.f), fmaxf(a[4 * R + 3] + bv.w, 0.f)};
+      if (keep)
+        *reinterpret_cast<float4*>(h0g + row * X_H + X_CK * j + k) = make_float4(v[0], v[1], v[2], v[3]);
+      bf16x4 p[3];
+      split4(v, p);
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        *reinterpret_cast<bf16x4*>(&L.h[j & 1][q][(32 * tt + li) * X_LDB + k]) = p[q];
+    }
+  };
+  if ((w >> 2) == 0) produce(0);
+  __syncthreads();  // chunk 0 in slot 0
+
+  // ---- layer 2: acc[tt] = C^T[units 32 w ..][rows 32 tt ..]
+  f32x16 acc[4];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[tt][r] = 0.f;
+#pragma unroll 1
+  for (int j = 0; j < X_NCK; ++j) {
+    bf16x8 wa[2][3];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const float v[8] = {wr[s][0].x, wr[s][0].y, wr[s][0].z, wr[s][0].w,
+                          wr[s][1].x, wr[s][1].y, wr[s][1].z, wr[s][1].w};
+      split8(v, wa[s]);
+    }
+    if (j + 1 < X_NCK) {
+      load_w1(j + 1);
+      if ((w >> 2) == ((j + 1) & 1)) produce(j + 1);
+    }
+    const int slot = j & 1;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        bf16x8 bp[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          bp[q] = *reinterpret_cast<const bf16x8*>(&L.h[slot][q][(32 * tt + li) * X_LDB + 16 * s + 8 * lh]);
+        acc[tt] = prod6(wa[s], bp, acc[tt]);
+      }
+    }
+    __syncthreads();  // slot j & 1 free; chunk j + 1 in slot (j + 1) & 1
+  }
+
+  // ---- epilogue: bias, ReLU, kept rows to h[1], the head dot of the lane's
+  // 16 units in order, then the two lane halves and the eight waves in order
+  float bb[16], ww[16];
+  {
+    const float* b1 = d.b[1] + wdel + c * d.sb[1];
+    const float* wh = d.W[2] + wdel + c * d.sW[2];
+#pragma unroll
+    for (int R = 0; R < 4; ++R) {
+      const int u = 32 * w + 8 * R + 4 * lh;
+      const float4 bv = *reinterpret_cast<const float4*>(b1 + u);
+      const float4 hv = *reinterpret_cast<const float4*>(wh + u);
+      bb[4 * R] = bv.x; bb[4 * R + 1] = bv.y; bb[4 * R + 2] = bv.z; bb[4 * R + 3] = bv.w;
+      ww[4 * R] = hv.x; ww[4 * R + 1] = hv.y; ww[4 * R + 2] = hv.z; ww[4 * R + 3] = hv.w;
+    }
+  }
+  const float b2v = (d.b[2] + wdel + c * d.sb[2])[0];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) {
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = fmaxf(acc[tt][r] + bb[r], 0.f);
+    const int row = m0 + 32 * tt + li;
+    if (h1g != nullptr && row >= h_from && row < rend) {
+#pragma unroll
+      for (int R = 0; R < 4; ++R)
+        *reinterpret_cast<float4*>(h1g + row * X_H + 32 * w + 8 * R + 4 * lh) =
+            make_float4(v[4 * R], v[4 * R + 1], v[4 * R + 2], v[4 * R + 3]);
+    }
+    float hs = v[0] * ww[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) hs = fmaf(v[r], ww[r], hs);
+    const float o = __shfl_xor(hs, 32, 64);
+    if (lh == 0) L.hp[w][32 * tt + li] = hs + o;
+  }
+  __syncthreads();
+  if (t < X_RB) {
+    float q = L.hp[0][t];
+#pragma unroll
+    for (int v = 1; v < 8; ++v) q += L.hp[v][t];
+    const int row = m0 + t;
+    if (row < rend) outp[(int64_t)row * d.ldout] = q + b2v;
+  }
+}
+
+}  // namespace
+}  // namespace d3a
+
+using namespace d3a;
+
+extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
+  D3A_CHECK_ARG(dp, "d3a_q2_fwd_x6: null desc");
+  const d3a_mlp_fwd_desc& d = *dp;
+  D3A_CHECK_ARG(d.n_hidden == 2 && d.H == X_H && d.n_out == 1 && d.n_in >= 1 && d.n_in <= 48,
+                "d3a_q2_fwd_x6: needs [n_in <= 48, 256, 256, 1]");
+  D3A_CHECK_ARG(d.x && d.out && d.W[0] && d.W[1] && d.W[2] && d.b[0] && d.b[1] && d.b[2],
+                "d3a_q2_fwd_x6: null operand");
+  D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.r0 >= 0 && d.h_from >= 0 && d.aux_rows >= 0,
+                "d3a_q2_fwd_x6: bad sizes");
+  auto a16 = [](const void* p, int64_t stride) {
+    return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && stride % 4 == 0;
+  };
+  D3A_CHECK_ARG(a16(d.W[1], d.sW[1]) && a16(d.b[0], d.sb[0]) && a16(d.b[1], d.sb[1]) &&
+                    a16(d.W[2], d.sW[2]),
+                "d3a_q2_fwd_x6: W1, b0, b1 and the head row must be 16-byte aligned");
+  D3A_CHECK_ARG((d.h[0] == nullptr || (reinterpret_cast<uintptr_t>(d.h[0]) & 15) == 0) &&
+                    (d.h[1] == nullptr || (reinterpret_cast<uintptr_t>(d.h[1]) & 15) == 0) &&
+                    d.sh % 4 == 0,
+                "d3a_q2_fwd_x6: kept activations must be 16-byte aligned rows of 256");
+  D3A_CHECK_ARG(d.aux_rows == 0 || (d.aux_x && d.aux_out && d.aux_wdelta % 4 == 0),
+                "d3a_q2_fwd_x6: aux pass needs aux_x, aux_out and a 16-byte aligned aux_wdelta");
+  D3A_CHECK_ARG((d.r0 + d.rows) * (int64_t)(d.ldout > X_H ? d.ldout : X_H) < (int64_t(1) << 31) &&
+                    (d.r0 + d.rows) * d.ldx < (int64_t(1) << 31) &&
+                    d.aux_rows * (int64_t)(d.aux_ldx > X_H ? d.aux_ldx : X_H) < (int64_t(1) << 31),
+                "d3a_q2_fwd_x6: rows x row stride exceeds 2^31");
+  if (d.rows == 0 && d.aux_rows == 0) return 0;
+  const int64_t nb = (d.rows + X_RB - 1) / X_RB + (d.aux_rows + X_RB - 1) / X_RB;
+  const dim3 grid((unsigned)nb, 1, (unsigned)d.C);
+  const hipStream_t st = (hipStream_t)stream;
+  const int xl = (d.n_in + 15) / 16 * 16;
+  if (xl == 16)
+    hipLaunchKernelGGL(q2x6_fwd_kernel<16>, grid, dim3(512), 0, st, d);
+  else if (xl == 32)
+    hipLaunchKernelGGL(q2x6_fwd_kernel<32>, grid, dim3(512), 0, st, d);
+  else
+    hipLaunchKernelGGL(q2x6_fwd_kernel<48>, grid, dim3(512), 0, st, d);
+  D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
+  return 0;
+}

@@ -1,0 +1,436 @@
+// fp32 critic backward on the bf16 matrix cores: d3a_q2_bwd's contract
+// (every weight / bias gradient of [n_in <= 48 -> 256 -> 256 -> 1], one
+// partial per 256-row block) with the two large products factored so that one
+// operand of each is the ReLU mask -- exactly 0 or 1, one bf16 part:
+//
+//   dz2[r][o] = g'[r] w3[o] m[r][o],  m = [h2 > 0]
+//   dh1[r][i] = sum_o dz2[r][o] W2[o][i] = g'[r] * sum_o m[r][o] (w3[o] W2[o][i])
+//   dW2[o][i] = sum_r dz2[r][o] h1[r][i] = w3[o] * sum_r m[r][o] (g'[r] h1[r][i])
+//
+// so each of them is three MFMAs per 16 k (the mask times the three bf16 parts
+// of the fp32 operand, every product exact, fp32 accumulation) against eight
+// 64-cycle v_mfma_f32_32x32x2_f32 -- 5.3x the fp32 MFMA rate.  The rounding is
+// fp32's: w3 W2 and g' h1 are rounded once each (as the reference's g' w3 is),
+// the sums are fp32, and the outer factor is one more rounding.  The first
+// layer's weight gradient dW1 = dz1^T x takes the six-product split of both
+// operands (x6.hpp).  Reference: the autograd backward of update_critic's loss
+// (ddpg_impl.py:119-133 via cql_impl.py:110-125) through
+// VectorEncoderWithAction (encoders.py:265-275, 328-339) and
+// ContinuousMeanQFunction._fc (mean_q_function.py:255-256).
+//
+// Geometry as q2_bwd.hip: a workgroup owns 256 rows of one member and a quarter
+// (64 units) of layer 1, walking its rows in 32-row sub-blocks.  Eight waves:
+//   waves 0-3 (ib = w & 1, kh = w >> 1 & 1): dh1[32 rows][units 32 ib ..] over
+//     the o half 128 kh .. (A = mask rows [r][o] from LDS, B = w3 W2 parts in
+//     registers, split once in the prologue); the two o halves meet in LDS one
+//     sub-block later, where wave kh finishes the rows of its accumulator
+//     registers 8 kh .. 8 kh + 7: dz1 = g' * dh1 * [h1 > 0] (g', h1 and x of
+//     those rows prefetched from global memory one sub-block ahead), db1, and
+//     dW1 += dz1^T x with the dz1 accumulator as the MFMA's A operand (its
+//     rows are the K of that product: no LDS round trip)
+//   waves 4-7: dW2[o block 64 (w - 4) ..][quarter] += m^T (g' h1) over the
+//     sub-block's 32 rows (A = mask [o][r], B = g' h1 parts [i][r], both LDS)
+// Every thread stages the next sub-block (mask images from h2, the g' h1
+// parts) while the current one is multiplied; one barrier per sub-block.
+// The head's gradients (dW3 = g'^T h2, db3 = sum g') and db2 = sum dz2 are
+// accumulated in fp64 at staging, exactly as q2_bwd.hip forms them.
+#include <cstdlib>
+#include "common.hpp"
+#include "../../include/d3rlpy_amd.h"
+#include "x6.hpp"
+
+namespace d3a {
+namespace {
+
+using namespace x6;
+
+constexpr int B6_H = 256;
+constexpr int B6_SB = 32;     // rows per sub-block
+constexpr int B6_NSB = 8;     // sub-blocks per workgroup (one 256-row partial)
+constexpr int B6_RB = B6_SB * B6_NSB;
+constexpr int B6_QW = 64;     // layer-1 units per workgroup
+constexpr int B6_LRO = 264;   // bf16 stride of the [r][o] mask rows (528 B)
+constexpr int B6_LR = 40;     // bf16 stride of the [.][r] images (80 B)
+constexpr int B6_NT = 512;
+
+struct B6Buf {
+  __bf16 mro[B6_SB * B6_LRO];      // m[r][o]
+  __bf16 mor[B6_H * B6_LR];        // m[o][r]
+  __bf16 hg[3][B6_QW * B6_LR];     // parts of g'[r] h1[r][i0 + i], [i][r]
+};
+
+struct B6Lds {
+  B6Buf b[2];
+  float ex[2][2 * 2 * 16 * 64];    // dh1 o-half partials [buf][ib][kh][reg][lane]
+};
+
+template <int NDB>  // 32-wide input blocks of dW1 (n_in <= 32 NDB)
+__global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
+  __shared__ __attribute__((aligned(16))) B6Lds L;
+  static_assert(sizeof(B6Lds) <= 163840, "LDS");
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  // XCD-aware decode (as q2_bwd.hip): the four quarters of one (row block,
+  // member) unit get block ids 8 apart -- one XCD under round-robin dispatch
+  const int64_t P = (d.rows + B6_RB - 1) / B6_RB;
+  const int64_t nunits = P * d.C;
+  const int bid = blockIdx.x;
+  const int kx = bid >> 3;
+  const int q = kx & 3;
+  const int64_t u = (int64_t)(kx >> 2) * 8 + (bid & 7);
+  if (u >= nunits) return;  // whole workgroup, before any barrier
+  const int64_t p = u / d.C;
+  const int c = (int)(u - p * d.C);
+  const int rows = (int)d.rows;
+  const int rb0 = (int)(p * B6_RB);
+  const int rlast = rows - 1;
+  const int ldx = (int)d.ldx;
+  const int nin = d.n_in;
+  const float* h1g = d.h1 + c * d.sh;
+  const float* h2g = d.h2 + c * d.sh;
+  const float* gg = d.g + c * d.sgb;
+  const float* xg = d.x + c * d.sxb;
+  const float* W2g = d.W2 + c * d.sW2;
+  const float* w3g = d.w3 + c * d.sw3;
+  const float gs = d.gscale ? *d.gscale : 1.f;
+  const int i0 = q * B6_QW;
+  const bool role_dx = w < 4;
+  const int ib = w & 1, kh = (w >> 1) & 1;
+  const int ob0 = 64 * (w - 4);
+  auto gprime = [&](int r) {  // g' of row r (r clamped to a valid row)
+    float v = gg[r];
+    if (r < d.n_scaled) v *= gs;
+    return v;
+  };
+
+  // ---- staging.  dW2 waves (t2 = t - 256): two 4 x 4 blocks of h2 (rows
+  // 4 (t2 & 7) + k, o = 4 (t2 >> 3) + e and + 128) -> the two mask images and
+  // the fp64 head / bias sums; dX waves: h1 of rows 8 (t >> 6) + k at unit
+  // i0 + (t & 63) -> the parts of g' h1
+  const int t2 = t - 256;
+  const int ra = 4 * (t2 & 7), oa = 4 * (t2 >> 3);
+  const int ih = t & 63, rh = 8 * (t >> 6);
+
+  f32x16 W1acc[NDB];  // dX waves: dW1 over the rows they finish
+  double s_db1 = 0.0;
+  // fp64 running sums (dW2 waves) of q2_bwd.hip's definitions: db2 += fp32(g'
+  // w3) over unmasked entries, dW3 += fp32(g' h2), db3 += g'
+  double s_db2[2][4], s_dw3[2][4], s_db3 = 0.0;
+#pragma unroll
+  for (int bo = 0; bo < 2; ++bo)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s_db2[bo][e] = s_dw3[bo][e] = 0.0;
+  if (role_dx) {
+    float h1v[8], gh[8];
+    auto load_sb = [&](int sb) {
+      const int base = rb0 + sb * B6_SB;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = min(base + rh + k, rlast);
+        h1v[k] = h1g[r * B6_H + i0 + ih];
+        gh[k] = gprime(r);
+      }
+    };
+    auto stage_sb = [&](int sb) {
+      B6Buf& B = L.b[sb & 1];
+      const int base = rb0 + sb * B6_SB;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        float hgv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool ok = base + rh + 4 * hh + k < rows && sb < B6_NSB;
+          hgv[k] = ok ? gh[4 * hh + k] * h1v[4 * hh + k] : 0.f;
+        }
+        bf16x4 pp[3];
+        split4(hgv, pp);
+#pragma unroll
+        for (int qq = 0; qq < 3; ++qq)
+          *reinterpret_cast<bf16x4*>(&B.hg[qq][ih * B6_LR + rh + 4 * hh]) = pp[qq];
+      }
+    };
+    // ---- B operand: (w3 W2)[o][i] for o = 128 kh + 16 s + 8 lh + j, unit
+    // i0 + 32 ib + li, as three bf16 parts per k step
+    bf16x8 wb[8][3];
+    {
+      const int ii = i0 + 32 * ib + li;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int o = 128 * kh + 16 * s + 8 * lh + j;
+          v[j] = w3g[o] * W2g[o * B6_H + ii];
+        }
+        split8(v, wb[s]);
+      }
+    }
+    load_sb(0);
+    stage_sb(0);
+    load_sb(1);
+    // the rows this wave finishes of a sub-block: accumulator registers
+    // 8 kh + r2, rows 16 kh + 8 (r2 >> 2) + 4 lh + (r2 & 3)
+    auto frow = [&](int r2) { return 16 * kh + 8 * (r2 >> 2) + 4 * lh + (r2 & 3); };
+    // finishing operands of one sub-block, prefetched from global memory
+    float fg[8], fh[8], fx[NDB][8];
+    auto load_fin = [&](int sb) {
+      const int base = rb0 + sb * B6_SB;
+#pragma unroll
+      for (int r2 = 0; r2 < 8; ++r2) {
+        const int r = min(base + frow(r2), rlast);
+        fg[r2] = gprime(r);
+        fh[r2] = h1g[r * B6_H + i0 + 32 * ib + li];
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) {
+          const int dc = 32 * db + li;
+          fx[db][r2] = dc < nin ? xg[r * ldx + dc] : 0.f;
+        }
+      }
+    };
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) W1acc[db][r] = 0.f;
+    // rows of sub-block sb this wave finishes: both o halves from LDS (its own
+    // and the partner's, o half 0 first), dz1 = g' dh1 [h1 > 0], db1, dW1
+    auto finish = [&](int sb) {
+      const int eb = sb & 1;
+      const int base = rb0 + sb * B6_SB;
+      float z[8];
+#pragma unroll
+      for (int r2 = 0; r2 < 8; ++r2) {
+        const float o0 = L.ex[eb][((ib * 2 + 0) * 16 + 8 * kh + r2) * 64 + lane];
+        const float o1 = L.ex[eb][((ib * 2 + 1) * 16 + 8 * kh + r2) * 64 + lane];
+        const float v = __fadd_rn(o0, o1);
+        const bool ok = base + frow(r2) < rows;
+        z[r2] = (ok && fh[r2] > 0.f) ? fg[r2] * v : 0.f;
+        s_db1 += (double)z[r2];
+      }
+      // dW1[i][d] += sum_r dz1[r][i] x[r][d]: A = the dz1 rows (k step kh of the
+      // accumulator-as-operand order), B = x of the same rows
+      bf16x8 za[3];
+      split8(z, za);
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        bf16x8 xb[3];
+        split8(fx[db], xb);
+        W1acc[db] = prod6(za, xb, W1acc[db]);
+      }
+    };
+    load_fin(0);
+    __syncthreads();  // sub-block 0 staged
+#pragma unroll 1
+    for (int sb = 0; sb < B6_NSB; ++sb) {
+      const B6Buf& B = L.b[sb & 1];
+      if (sb > 0) {
+        finish(sb - 1);
+        load_fin(sb);
+      }
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const __bf16* A = &B.mro[li * B6_LRO + 128 * kh + 8 * lh];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + 16 * s);
+        acc = x3m(a, wb[s], acc);
+        if (s == 2) stage_sb(sb + 1);
+        if (s == 5) load_sb(sb + 2 < B6_NSB ? sb + 2 : B6_NSB - 1);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) L.ex[sb & 1][((ib * 2 + kh) * 16 + r) * 64 + lane] = acc[r];
+      __syncthreads();  // sub-block sb + 1 staged; sb's o-half partials in LDS
+    }
+    finish(B6_NSB - 1);
+  } else {
+    float4 h2v[2][4];
+    float ga[4];
+    float w3a[2][4];
+#pragma unroll
+    for (int bo = 0; bo < 2; ++bo) {
+      const float4 v = *reinterpret_cast<const float4*>(w3g + oa + 128 * bo);
+      w3a[bo][0] = v.x; w3a[bo][1] = v.y; w3a[bo][2] = v.z; w3a[bo][3] = v.w;
+    }
+    auto load_sb = [&](int sb) {
+      const int base = rb0 + sb * B6_SB;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = min(base + ra + k, rlast);
+#pragma unroll
+        for (int bo = 0; bo < 2; ++bo)
+          h2v[bo][k] = *reinterpret_cast<const float4*>(h2g + r * B6_H + oa + 128 * bo);
+        ga[k] = gprime(r);
+      }
+    };
+    auto stage_sb = [&](int sb) {
+      B6Buf& B = L.b[sb & 1];
+      const int base = rb0 + sb * B6_SB;
+#pragma unroll
+      for (int bo = 0; bo < 2; ++bo) {
+        __bf16 m[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool ok = base + ra + k < rows && sb < B6_NSB;
+          const float g = ok ? ga[k] : 0.f;
+          const float hv[4] = {h2v[bo][k].x, h2v[bo][k].y, h2v[bo][k].z, h2v[bo][k].w};
+          bf16x4 mv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool on = ok && hv[e] > 0.f;
+            m[k][e] = on ? (__bf16)1.f : (__bf16)0.f;
+            mv[e] = m[k][e];
+            s_db2[bo][e] += (double)(on ? g * w3a[bo][e] : 0.f);
+            s_dw3[bo][e] += (double)(g * (ok ? hv[e] : 0.f));
+          }
+          if (bo == 0 && t2 < 8) s_db3 += (double)g;
+          *reinterpret_cast<bf16x4*>(&B.mro[(ra + k) * B6_LRO + oa + 128 * bo]) = mv;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bf16x4 mv;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) mv[k] = m[k][e];
+          *reinterpret_cast<bf16x4*>(&B.mor[(oa + 128 * bo + e) * B6_LR + ra]) = mv;
+        }
+      }
+    };
+    load_sb(0);
+    stage_sb(0);
+    load_sb(1);
+    f32x16 R[4];  // R[2 ob + bi]: o block ob0 + 32 ob, unit block 32 bi
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) R[k][r] = 0.f;
+    __syncthreads();  // sub-block 0 staged
+#pragma unroll 1
+    for (int sb = 0; sb < B6_NSB; ++sb) {
+      const B6Buf& B = L.b[sb & 1];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 a[2], hb[2][3];
+#pragma unroll
+        for (int ob = 0; ob < 2; ++ob)
+          a[ob] = *reinterpret_cast<const bf16x8*>(&B.mor[(ob0 + 32 * ob + li) * B6_LR + 16 * s + 8 * lh]);
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int qq = 0; qq < 3; ++qq)
+            hb[bi][qq] = *reinterpret_cast<const bf16x8*>(&B.hg[qq][(32 * bi + li) * B6_LR + 16 * s + 8 * lh]);
+#pragma unroll
+        for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi) R[2 * ob + bi] = x3m(a[ob], hb[bi], R[2 * ob + bi]);
+        if (s == 0) stage_sb(sb + 1);
+        else load_sb(sb + 2 < B6_NSB ? sb + 2 : B6_NSB - 1);
+      }
+      __syncthreads();  // sub-block sb + 1 staged
+    }
+    // dW2[o][i] = w3[o] * R: lane column = unit 32 bi + li, rows o
+    const int64_t pc = p * d.C + c;
+    float* dW2 = d.dW2 + pc * (B6_H * B6_H);
+#pragma unroll
+    for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = ob0 + 32 * ob + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float wo = w3g[o];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi) dW2[o * B6_H + i0 + 32 * bi + li] = wo * R[2 * ob + bi][r];
+      }
+  }
+
+  // ---- epilogue (after the loops' last barrier every buffer is free)
+  __syncthreads();
+  const int64_t pc = p * d.C + c;
+  float* w1s = reinterpret_cast<float*>(&L.b[0].mro[0]);             // [ib][db][16][64]
+  double* db1s = reinterpret_cast<double*>(&L.b[0].mor[0]);          // [ib][64]
+  double* hs = reinterpret_cast<double*>(&L.b[1].mro[0]);            // [256][2][2][4], over mro + mor
+  double* db3s = reinterpret_cast<double*>(&L.b[1].hg[0][0]);        // [8]
+  if (role_dx && kh == 1) {
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) w1s[((ib * 2 + db) * 16 + r) * 64 + lane] = W1acc[db][r];
+    db1s[ib * 64 + lane] = s_db1;
+  }
+  if (!role_dx) {
+#pragma unroll
+    for (int bo = 0; bo < 2; ++bo)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hs[((t2 * 2 + bo) * 2 + 0) * 4 + e] = s_db2[bo][e];
+        hs[((t2 * 2 + bo) * 2 + 1) * 4 + e] = s_dw3[bo][e];
+      }
+    if (t2 < 8) db3s[t2] = s_db3;
+  }
+  __syncthreads();
+  if (role_dx && kh == 0) {
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = __fadd_rn(W1acc[db][r], w1s[((ib * 2 + db) * 16 + r) * 64 + lane]);
+        const int i = 32 * ib + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int dc = 32 * db + li;
+        if (dc < nin) d.dW1[(pc * B6_H + i0 + i) * nin + dc] = v;
+      }
+    }
+    double s1 = s_db1 + db1s[ib * 64 + lane];
+    s1 += __shfl_xor(s1, 32, 64);
+    if (lh == 0) d.db1[pc * B6_H + i0 + 32 * ib + li] = (float)s1;
+  }
+  // db2 / dW3 of o = i0 + tt (this workgroup's quarter): the eight threads
+  // holding o's column (rows 4 v .. 4 v + 3), in order
+  if (t >= 256 && t < 320) {
+    const int tt = t - 256, o = i0 + tt;
+    const int bo = o >> 7, oo = o & 127;
+    const int tb = (oo >> 2) << 3, e = oo & 3;
+    double s2 = 0.0, s3 = 0.0;
+    for (int v = 0; v < 8; ++v) {
+      s2 += hs[(((tb + v) * 2 + bo) * 2 + 0) * 4 + e];
+      s3 += hs[(((tb + v) * 2 + bo) * 2 + 1) * 4 + e];
+    }
+    d.db2[pc * B6_H + o] = (float)s2;
+    d.dW3[pc * B6_H + o] = (float)s3;
+  } else if (t == 320 && q == 0) {
+    double sg = 0.0;
+    for (int v = 0; v < 8; ++v) sg += db3s[v];
+    d.db3[pc] = (float)sg;
+  }
+}
+
+}  // namespace
+}  // namespace d3a
+
+using namespace d3a;
+
+extern "C" int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* dp, void* stream) {
+  D3A_CHECK_ARG(dp, "d3a_q2_bwd_x6: null desc");
+  const d3a_q2_bwd_desc& d = *dp;
+  D3A_CHECK_ARG(d.dz2 == nullptr, "d3a_q2_bwd_x6: dz2 input is not supported (use d3a_q2_bwd)");
+  D3A_CHECK_ARG(d.block_rows == 0 || d.block_rows == 256, "d3a_q2_bwd_x6: block_rows must be 0 / 256");
+  D3A_CHECK_ARG(d.x && d.h1 && d.h2 && d.g && d.W2 && d.w3, "d3a_q2_bwd_x6: null input");
+  D3A_CHECK_ARG(d.dW1 && d.db1 && d.dW2 && d.db2 && d.dW3 && d.db3, "d3a_q2_bwd_x6: null output");
+  D3A_CHECK_ARG(d.n_in >= 1 && d.n_in <= 48, "d3a_q2_bwd_x6: n_in must be 1..48");
+  D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.n_scaled >= 0, "d3a_q2_bwd_x6: bad sizes");
+  auto a16 = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; };
+  D3A_CHECK_ARG(a16(d.h1) && a16(d.h2) && d.ldh == B6_H && d.sh % 4 == 0,
+                "d3a_q2_bwd_x6: h1 / h2 must be 16-byte aligned rows of 256 floats");
+  D3A_CHECK_ARG(a16(d.w3) && d.sw3 % 4 == 0, "d3a_q2_bwd_x6: w3 must be 16-byte aligned");
+  D3A_CHECK_ARG(d.ldx >= d.n_in, "d3a_q2_bwd_x6: ldx < n_in");
+  D3A_CHECK_ARG(d.rows * (d.ldh > d.ldx ? d.ldh : d.ldx) < (int64_t(1) << 31),
+                "d3a_q2_bwd_x6: rows x row stride exceeds 2^31");
+  if (d.rows == 0) return 0;
+  const int64_t units = ((d.rows + B6_RB - 1) / B6_RB) * d.C;
+  const int64_t blocks = (units + 7) / 8 * 32;
+  D3A_CHECK_ARG(blocks < (int64_t(1) << 31), "d3a_q2_bwd_x6: too many rows");
+  const dim3 grid((unsigned)blocks), block(B6_NT);
+  if (d.n_in <= 32)
+    hipLaunchKernelGGL(q2x6_bwd_kernel<1>, grid, block, 0, (hipStream_t)stream, d);
+  else
+    hipLaunchKernelGGL(q2x6_bwd_kernel<2>, grid, block, 0, (hipStream_t)stream, d);
+  D3A_LAUNCH_CHECK("d3a_q2_bwd_x6");
+  return 0;
+}

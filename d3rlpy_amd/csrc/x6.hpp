@@ -1,0 +1,71 @@
+// Split-bf16 helpers of the fp32-accurate critic kernels (q2_x6.hip,
+// q2_x6_bwd.hip): the exact three-way split of an fp32 value into bf16 parts
+// and the part products on v_mfma_f32_32x32x16_bf16.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace d3a {
+namespace x6 {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+
+__device__ __forceinline__ f32x16 mfma16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// exact three-way split of one fp32 value
+__device__ __forceinline__ void split1(float x, __bf16& p0, __bf16& p1, __bf16& p2) {
+  p0 = (__bf16)x;
+  const float r1 = x - (float)p0;
+  p1 = (__bf16)r1;
+  p2 = (__bf16)(r1 - (float)p1);
+}
+
+__device__ __forceinline__ void split8(const float* x, bf16x8* p) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    __bf16 a, b, c;
+    split1(x[i], a, b, c);
+    p[0][i] = a;
+    p[1][i] = b;
+    p[2][i] = c;
+  }
+}
+
+__device__ __forceinline__ void split4(const float* x, bf16x4* p) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    __bf16 a, b, c;
+    split1(x[i], a, b, c);
+    p[0][i] = a;
+    p[1][i] = b;
+    p[2][i] = c;
+  }
+}
+
+// the six part products, smallest first
+__device__ __forceinline__ f32x16 prod6(const bf16x8* a, const bf16x8* b, f32x16 c) {
+  c = mfma16(a[2], b[0], c);
+  c = mfma16(a[1], b[1], c);
+  c = mfma16(a[0], b[2], c);
+  c = mfma16(a[1], b[0], c);
+  c = mfma16(a[0], b[1], c);
+  c = mfma16(a[0], b[0], c);
+  return c;
+}
+
+// the three products of a 0/1 operand a (exact in one bf16 part) with the
+// parts of b, smallest first
+__device__ __forceinline__ f32x16 x3m(bf16x8 a, const bf16x8* b, f32x16 c) {
+  c = mfma16(a, b[2], c);
+  c = mfma16(a, b[1], c);
+  c = mfma16(a, b[0], c);
+  return c;
+}
+
+}  // namespace x6
+}  // namespace d3a

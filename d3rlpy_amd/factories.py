@@ -266,14 +266,24 @@ def check_q_func(value: Union[QFunctionFactory, str]) -> QFunctionFactory:
 
 
 def check_use_gpu(value):
-    """argument_utility.py:96-114: True -> Device(0), int -> Device(int),
+    """argument_utility.py:96-114: True -> Device(0) (Device(LOCAL_RANK) in a
+    multi-process launch, WORLD_SIZE > 1), int -> Device(int),
     a Device as is, False / None -> None (the reference's CPU).  The HIP
     engine has no CPU path: an Impl built with None raises
     NotImplementedError (algos/impl_base.py)."""
     from .gpu import Device
     # isinstance cannot tell bool from int
     if type(value) == bool:
-        return Device(0) if value else None
+        if not value:
+            return None
+        # one process per GPU (torchrun / bench.launch_ranks): a bare True is
+        # this rank's GPU, LOCAL_RANK, not GPU 0 -- otherwise every rank's
+        # parameters would land on cuda:0 beside a dataset and communicator
+        # on cuda:LOCAL_RANK.  Single-process runs keep the reference's 0.
+        import os
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "LOCAL_RANK" in os.environ:
+            return Device(int(os.environ["LOCAL_RANK"]))
+        return Device(0)
     if type(value) == int:
         return Device(value)
     if isinstance(value, Device):

@@ -211,7 +211,11 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             d.aux_wdelta = (ast.data.data_ptr() - store.data.data_ptr()) // 4
             d.aux_out, d.aux_sout, d.aux_rows = aacts.out.data_ptr(), aacts.R * sizes[-1], aacts.R
             aux = None
-        ops.call_desc("d3a_q2_fwd_bf16" if bf16 else "d3a_mlp_fwd", d)
+        entry = "d3a_q2_fwd_bf16" if bf16 else "d3a_mlp_fwd"
+        if (not bf16 and not small and ops.CRITIC_GEMM == "x6" and q2_shape(net)
+                and (n + (d.aux_rows if d.aux_rows else 0)) * C >= 8192):
+            entry = "d3a_q2_fwd_x6"  # the q2_fwd pass, fp32-accurate split-bf16
+        ops.call_desc(entry, d)
         if aux is not None:
             forward(net, aux[0], aux[1], True, aux[2], aux[3], keep_h=False)
         return
@@ -359,7 +363,10 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         d.dW2, d.db2 = gs.get(net.wname(1)).data_ptr(), gs.get(net.bname(1)).data_ptr()
         d.dW3, d.db3 = gs.get(net.wname(2)).data_ptr(), gs.get(net.bname(2)).data_ptr()
         d.rows, d.n_in, d.C = n, sizes[0], C
-        ops.call_desc("d3a_q2_bwd_bf16" if esz == 2 else "d3a_q2_bwd", d)
+        entry = "d3a_q2_bwd_bf16" if esz == 2 else "d3a_q2_bwd"
+        if esz == 4 and ops.CRITIC_GEMM == "x6":
+            entry = "d3a_q2_bwd_x6"  # fp32-accurate split-bf16 (mask-factored)
+        ops.call_desc(entry, d)
         return None
 
     if (bs.q2p and weight_grads and head_ready and dx is None and members is None

@@ -279,6 +279,21 @@ def set_critic_precision(p: str) -> None:
     CRITIC_PRECISION = p
 
 
+# GEMM arithmetic of the [n_in <= 48, 256, 256, 1] critic passes at fp32
+# precision: "fp32" (v_mfma_f32_32x32x2_f32, exact fp32 fma chains: q2_fwd /
+# q2_bwd) or "x6" (exact three-way split-bf16 operands on the bf16 matrix
+# cores, fp32-accurate: d3a_q2_fwd_x6 / d3a_q2_bwd_x6, csrc/q2_x6*.hip).  Read
+# at each launch, so set it before an update graph is captured.
+CRITIC_GEMM = os.environ.get("D3A_CRITIC_GEMM", "fp32")
+
+
+def set_critic_gemm(mode: str) -> None:
+    global CRITIC_GEMM
+    if mode not in ("fp32", "x6"):
+        raise ValueError(f"critic GEMM mode must be fp32 or x6, got {mode!r}")
+    CRITIC_GEMM = mode
+
+
 def set_sbf16(terms: int) -> None:
     global SBF16_TERMS
     assert terms in (0, 3, 6)

@@ -328,6 +328,18 @@ int d3a_q2_bwd(const d3a_q2_bwd_desc* d, void* stream);
 int d3a_q2_fwd_bf16(const d3a_mlp_fwd_desc* d, void* stream);
 int d3a_q2_bwd_bf16(const d3a_q2_bwd_desc* d, void* stream);
 
+/* fp32-accurate critic forward / backward on the bf16 matrix cores (csrc/
+ * q2_x6.hip): the contracts of d3a_mlp_fwd on [n_in <= 48, 256, 256, 1]
+ * (fp32 kept activations) and d3a_q2_bwd (block_rows 0 / 256), every GEMM
+ * product x*y formed from an exact three-way bf16 split of both operands as
+ * the six part products above fp32 resolution, accumulated in fp32
+ * (v_mfma_f32_32x32x16_bf16): within fp32 rounding of the exact product, not
+ * a reduced-precision path.  Replaces, like d3a_mlp_fwd / d3a_q2_bwd, the
+ * critic passes of cql_impl.py:110-223 / ddpg_impl.py:119-133 through
+ * encoders.py:265-275, 328-339 and mean_q_function.py:255-256. */
+int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* d, void* stream);
+int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* d, void* stream);
+
 /* ---- optimiser and target networks ------------------------------------- */
 
 /* One parameter tensor inside a flat buffer, with its gradient given as

@@ -55,6 +55,11 @@ def main():
     torch.cuda.synchronize()
     # the Philox key this rank's workspace draws its own noise with
     np.save(os.path.join(work, f"seed{rank}.npy"), np.array(impl._workspace(sl.stop - sl.start).seed))
+    # this rank's ReLU decisions of the critic stage (the last step's kept
+    # critic activations), for the decision-aware fp64 arbiter
+    from relu_arbiter import hip_critic_masks
+    torch.save(hip_critic_masks(impl._workspace(sl.stop - sl.start)),
+               os.path.join(work, f"masks{rank}.pt"))
     if rank == 0:
         torch.save(impl.get_state_dict(), os.path.join(work, "dp_state.pt"))
         # the gradients the last Adam steps consumed: all-reduced SUM x 1/world

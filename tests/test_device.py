@@ -67,3 +67,20 @@ def test_cpu_selection_raises_not_implemented():
     with pytest.raises(NotImplementedError, match="no CPU compute path"):
         algo.create_impl((11,), 3)
     assert CQL()._use_gpu == Device(0)  # the default: the GPU (documented deviation)
+
+
+def test_bare_true_is_this_ranks_gpu_in_a_multi_process_launch(monkeypatch):
+    """One process per GPU (torchrun / bench.launch_ranks): use_gpu=True is
+    GPU LOCAL_RANK, so a rank's parameters sit beside its dataset and RCCL
+    communicator; a single process (or WORLD_SIZE 1) keeps Device(0)."""
+    from d3rlpy_amd.algos.cql import CQL
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    assert check_use_gpu(True) == Device(3)
+    assert CQL()._use_gpu == Device(3)
+    assert check_use_gpu(1) == Device(1)  # an explicit id still wins
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert check_use_gpu(True) == Device(0)
+    monkeypatch.delenv("LOCAL_RANK")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert check_use_gpu(True) == Device(0)

@@ -46,7 +46,9 @@ def _fp64(ws, x, da_off, A):
                                      (256, 29, 8, 2),    # K4 antmaze
                                      (100, 3, 1, 2),     # K1 pendulum shapes, ragged B
                                      (37, 17, 6, 3),     # ragged, three members
-                                     (64, 58, 6, 10)])   # n_in = 64, ten members
+                                     (64, 58, 6, 10),    # n_in = 64, ten members
+                                     (50, 20, 13, 2),    # A = 13: 208 (row, action) pairs
+                                     (40, 17, 16, 2)])   # A = 16: all 256 threads write
 def test_sac_actor_q_vs_fp64(B, D, A, C):
     g = torch.Generator(device="cuda").manual_seed(B + 7 * D + C)
     n_in = D + A

@@ -31,13 +31,6 @@ from oracle.cql import Batch
 pytestmark = pytest.mark.gpu
 
 STEPS = 12
-# HIP gradients vs an fp64 evaluation of each production step (max-normalised
-# per tensor).  Measured worst 1.2e-4 (step 9, critic 1 layer 1, where the fp32
-# oracle is at 1.5e-6: a pre-activation within rounding of zero that HIP's
-# fp32 sum puts on the other side of the ReLU; the conservative loss's
-# importance-sampled and data rows cancel across the 7,936-row critic pass, so
-# one row's decision shows at this size).  Bar 1e-3.
-GRAD_BAR_FP64 = 1e-3
 
 
 def _transitions(ds):
@@ -106,14 +99,17 @@ def test_cql_fit_production_path_per_step_proof():
     eager, the rest replays of the captured graph, device-drawn noise, the
     numpy index stream -- each replayed on the oracle started from HIP's exact
     state before that step, on the same batch and the reproduced draws.  Per
-    step: every logged metric within 1e-5, every critic / policy gradient
-    within GRAD_BAR_FP64 of an fp64 evaluation, targets and log_alpha / log_temp within
-    1e-5 / 1e-6, and every parameter entry within 1e-5 of the oracle or --
+    step: every logged metric within 1e-5, every critic gradient within
+    max(1e-5, 2 x the fp32 oracle's own rounding error) of an fp64 evaluation
+    with HIP's ReLU decisions (every decision HIP takes differently from the
+    exact sign proven a tie, tests/relu_arbiter.py), every policy gradient
+    within 1e-5 of fp64, targets and log_alpha / log_temp within 1e-5 / 1e-6, and every parameter entry within 1e-5 of the oracle or --
     entry by entry -- equal (1e-7) to Adam from HIP's pre-step optimiser state
     applied to HIP's own checked gradient (arbiter_helpers.check_params_adam).
     This is the per-entry proof behind the 12-step trajectory bar below."""
-    from arbiter_helpers import adam_state_by_key, check_params_adam, hip_grads
-    from cql_helpers import make_oracle, max_rel, oracle_state
+    from arbiter_helpers import adam_state_by_key, check_grads, check_params_adam, hip_grads
+    from cql_helpers import make_oracle, oracle_state
+    from relu_arbiter import cql_critic_arbiter, hip_critic_masks, to64
     from d3rlpy_amd.algos.cql import CQL
     from d3rlpy_amd.datasets import get_synthetic_d4rl
     from test_gpu_cql_parity import _oracle_step
@@ -127,7 +123,7 @@ def test_cql_fit_production_path_per_step_proof():
     batches = _oracle_batches(_transitions(ds), B, 42)
     np.random.seed(42)
     cref, pref = impl._critic_refs(), impl._policy_refs()
-    n_amp, worst_g = 0, 0.0
+    n_amp, worst_g, flips = 0, 0.0, 0
     for s in range(STEPS):
         sd0 = impl.get_state_dict()
         algo.fit(ds, n_steps=1, n_steps_per_epoch=1, save_metrics=False, verbose=False,
@@ -142,33 +138,16 @@ def test_cql_fit_production_path_per_step_proof():
         m, cgrads, pgrads = _oracle_step(orc, batches[s], nz, A)
         for j, name in enumerate(names):
             assert abs(ring[-1, j] - m[name]) <= 1e-5 * max(1.0, abs(m[name])), (s, name)
-        # the gradients against an fp64 evaluation of the same step (the fp32
-        # oracle's own rounding on the cancelling conservative gradient is of
-        # the same order as HIP's: test_gpu_cql_parity.test_cql_grad_accuracy_vs_fp64)
-        o64 = make_oracle(D, A, [256, 256], N, seed=0)
-        for k, v in sd0.items():
-            getattr(o64, k).load_state_dict(v)
-        for mod in (o64._q_func, o64._policy, o64._targ_q_func, o64._targ_policy,
-                    o64._log_temp, o64._log_alpha):
-            mod.double()
-        for opt in (o64._critic_optim, o64._actor_optim, o64._temp_optim, o64._alpha_optim):
-            for st in opt.state.values():  # HIP's moments, in fp64 like the parameters
-                for k_, v_ in st.items():
-                    if torch.is_tensor(v_) and k_ != "step":
-                        st[k_] = v_.double()
-        tb = batches[s]
-        tb64 = type(tb)(*(getattr(tb, f).double() for f in tb.__dataclass_fields__))
-        nz64 = type(nz)(**{k: (None if getattr(nz, k) is None else getattr(nz, k).double())
-                           for k in nz.__dataclass_fields__})
-        o64.update_temp(tb64, nz64.eps_temp)
-        o64.update_alpha(tb64, nz64)
-        o64.update_critic(tb64, nz64)
-        g64 = {}
-        for key_, _s, c, _sl in cref:
-            qf = o64._q_func.q_funcs[c]
-            l = int(key_.split("_fcs.")[1].split(".")[0]) if "_fcs." in key_ else 2
-            fc = (list(qf._encoder._fcs) + [qf._fc])[l]
-            g64[key_] = (fc.weight if key_.endswith("weight") else fc.bias).grad.detach().clone()
+        # the critic gradients against fp64 evaluated with HIP's own ReLU
+        # decisions (relu_arbiter.py: HIP within max(1e-5, 2 x the fp32
+        # oracle's own rounding error), every decision HIP takes differently
+        # from the exact sign a tie); the policy gradients within 1e-5 of fp64
+        g_hip = {**hip_grads(cref, impl.critic_grad), **hip_grads(pref, impl.policy_grad)}
+        o64, info = cql_critic_arbiter(
+            f"step {s}", lambda: make_oracle(D, A, [256, 256], N, seed=0), sd0, batches[s], nz,
+            {k: g_hip[k] for k, *_ in cref}, hip_critic_masks(ws), B, N)
+        worst_g = max(worst_g, info["worst"])
+        flips += info["hip_flips"]
         # the actor stage on HIP's own updated critic (and temperature): the
         # critic step's Adam amplification of near-zero gradient entries (proven
         # below) moves a few critic weights by up to 2 lr, enough to flip the
@@ -176,21 +155,9 @@ def test_cql_fit_production_path_per_step_proof():
         # compares the same function, not a tie
         o64._q_func.load_state_dict({k: v.double() for k, v in sd1["_q_func"].items()})
         o64._log_temp.load_state_dict({k: v.double() for k, v in sd1["_log_temp"].items()})
-        o64.update_actor(tb64, nz64.eps_actor)
-        g64.update({k: p.grad.detach().clone() for k, p in o64._policy.named_parameters()})
-        g_hip = {**hip_grads(cref, impl.critic_grad), **hip_grads(pref, impl.policy_grad)}
-        g32 = {}
-        for key_, _s, c, _sl in cref:
-            l = int(key_.split("_fcs.")[1].split(".")[0]) if "_fcs." in key_ else 2
-            g32[key_] = cgrads[c][l][0 if key_.endswith("weight") else 1]
-        for k in g64:
-            eh = max_rel(g_hip[k], g64[k])
-            eo = max_rel(g32[k], g64[k]) if k in g32 else float("nan")
-            if eh > 1e-5:
-                print(f"  step {s} grad {k}: hip-vs-fp64 {eh:.1e} oracle32-vs-fp64 {eo:.1e}")
-        e = max(max_rel(g_hip[k], g64[k]) for k in g64)
-        worst_g = max(worst_g, e)
-        assert e <= GRAD_BAR_FP64, (s, e)
+        o64.update_actor(to64(batches[s]), to64(nz).eps_actor)
+        g64p = {k: p.grad.detach().clone() for k, p in o64._policy.named_parameters()}
+        check_grads(f"step {s} policy", {k: g_hip[k] for k, *_ in pref}, g64p)
         ref = oracle_state(orc)
         for key, refs, opt, lr in (("_q_func", cref, "_critic_optim", 3e-4),
                                    ("_policy", pref, "_actor_optim", 1e-4)):
@@ -205,9 +172,10 @@ def test_cql_fit_production_path_per_step_proof():
         assert abs(float(impl.log_alpha.item()) - float(orc._log_alpha().item())) <= 1e-6
         assert abs(float(impl.log_temp.item()) - float(orc._log_temp().item())) <= 1e-6
     assert len(impl._last_ws()._graphs) == 1  # steps 2..12 replayed the captured graph
-    print(f"CQL production path, per-step proof: {STEPS} steps, gradients within {worst_g:.1e} "
-          f"of fp64, {n_amp} parameter entries beyond 1e-5, each equal to Adam of HIP's own "
-          "checked gradient")
+    print(f"CQL production path, per-step proof: {STEPS} steps, critic gradients within "
+          f"{worst_g:.1e} of fp64 with HIP's ReLU decisions ({flips} tie decisions), "
+          f"{n_amp} parameter entries beyond 1e-5, each equal to Adam of HIP's own checked "
+          "gradient")
 
 
 def test_cql_fit_production_path_vs_oracle():

@@ -1,0 +1,243 @@
+"""fp32-accurate critic kernels on the bf16 matrix cores (csrc/q2_x6.hip:
+d3a_q2_fwd_x6 / d3a_q2_bwd_x6, three-way split-bf16 operands, six part
+products, fp32 accumulation) against fp64 -- at the fp32 kernels' own bars.
+
+The split is exact (x = x0 + x1 + x2) and the three dropped part products are
+each below 2^-24 |x y|, so a product carries fp32-level error: bars are
+relative to the rounding scale sum_k |a_k b_k| (what an fp32 dot product is
+accurate to), 2e-6 -- the fp32 MFMA kernels measure ~1e-7 .. 5e-7 there, and
+a single bf16-rounded operand would show at ~4e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+from d3rlpy_amd import _native as N
+from d3rlpy_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+SCALE_BAR = 2e-6
+
+
+def _net(C, n_in, gen, dev):
+    sizes = [n_in, 256, 256, 1]
+    Ws = [torch.randn(C, sizes[l + 1], sizes[l], generator=gen) * (1.0 / np.sqrt(sizes[l]))
+          for l in range(3)]
+    bs = [torch.randn(C, sizes[l + 1], generator=gen) * 0.1 for l in range(3)]
+    return [w.to(dev) for w in Ws], [b.to(dev) for b in bs]
+
+
+def _fwd64(x, Ws, bs):
+    """fp64 forward; per layer the value and its rounding scale sum |w x| + |b|."""
+    a, sa = x.double(), x.double().abs()
+    hs, scales = [], []
+    for l in range(3):
+        W, b = Ws[l].double(), bs[l].double().unsqueeze(1)
+        z = a @ W.transpose(-1, -2) + b
+        sz = a.abs() @ W.abs().transpose(-1, -2) + b.abs()
+        if l < 2:
+            z = z.clamp_min(0)
+        hs.append(z)
+        scales.append(sz)
+        a = z
+    return hs, scales
+
+
+def _fwd_desc(x, ldx, n_in, Ws, bs, Wt, bt, h, out, aout, xa, rows, h_from, aux, C, dev):
+    flat = [torch.cat([W[l].reshape(-1) for l in range(3)] + [b[l].reshape(-1) for l in range(3)])
+            for W, b in ((Ws, bs), (Wt, bt))]
+    pad = (-flat[0].numel()) % 4
+    buf = torch.cat([flat[0], torch.zeros(pad, device=dev), flat[1]])
+    n1 = flat[0].numel() + pad
+    offs, o = [], 0
+    for l in range(3):
+        offs.append(o)
+        o += Ws[l].numel()
+    boffs = []
+    for l in range(3):
+        boffs.append(o)
+        o += bs[l].numel()
+    d = N.MlpFwdDesc()
+    d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
+    d.n_in, d.n_hidden, d.H, d.n_out = n_in, 2, 256, 1
+    for l in range(3):
+        d.W[l] = buf.data_ptr() + 4 * offs[l]
+        d.b[l] = buf.data_ptr() + 4 * boffs[l]
+        d.sW[l], d.sb[l] = Ws[l].shape[1] * Ws[l].shape[2], bs[l].shape[1]
+    for l in range(2):
+        d.h[l] = h[l].data_ptr()
+    d.sh = rows * 256
+    d.out, d.sout, d.ldout = out.data_ptr(), rows, 1
+    d.r0, d.rows, d.C, d.h_from = 0, rows, C, h_from
+    if aux:
+        d.aux_x, d.aux_ldx, d.aux_sxb, d.aux_wdelta = xa.data_ptr(), ldx, 0, n1
+        d.aux_out, d.aux_sout, d.aux_rows = aout.data_ptr(), aux, aux
+    return d, buf
+
+
+@pytest.mark.parametrize("rows,h_from,aux,n_in", [(15616, 7680, 256, 14), (1000, 0, 0, 48),
+                                                   (300, 100, 77, 23), (129, 0, 5, 37)])
+def test_q2_fwd_x6_vs_fp64(rows, h_from, aux, n_in):
+    dev = torch.device("cuda")
+    C = 2
+    gen = torch.Generator().manual_seed(rows + n_in)
+    Ws, bs = _net(C, n_in, gen, dev)
+    Wt, bt = _net(C, n_in, gen, dev)
+    ldx = (n_in + 3) // 4 * 4
+    x = torch.randn(rows, ldx, generator=gen).to(dev)
+    xa = torch.randn(max(aux, 1), ldx, generator=gen).to(dev)
+    h = [torch.full((C, rows, 256), float("nan"), device=dev) for _ in range(2)]
+    out = torch.full((C, rows), float("nan"), device=dev)
+    aout = torch.full((C, max(aux, 1)), float("nan"), device=dev)
+    d, _buf = _fwd_desc(x, ldx, n_in, Ws, bs, Wt, bt, h, out, aout, xa, rows, h_from, aux, C, dev)
+    ops.call_desc("d3a_q2_fwd_x6", d)
+    torch.cuda.synchronize()
+    hs, sc = _fwd64(x[:, :n_in], Ws, bs)
+    # each layer against fp64 evaluated on the kernel's own (fp32) input
+    # activations: relative to that layer's rounding scale
+    h0, h1 = h[0][:, h_from:].double(), h[1][:, h_from:].double()
+    e0 = float(((h0 - hs[0][:, h_from:]).abs() / sc[0][:, h_from:]).max())
+    z1 = (h0 @ Ws[1].double().transpose(1, 2) + bs[1].double().unsqueeze(1)).clamp_min(0)
+    s1 = h0.abs() @ Ws[1].double().abs().transpose(1, 2) + bs[1].double().abs().unsqueeze(1)
+    e1 = float(((h1 - z1).abs() / s1).max())
+    q = (h1 @ Ws[2].double().transpose(1, 2) + bs[2].double().unsqueeze(1)).squeeze(-1)
+    sq = (h1.abs() @ Ws[2].double().abs().transpose(1, 2)).squeeze(-1) + bs[2].double().abs()
+    eq = float(((out[:, h_from:].double() - q).abs() / sq).max())
+    print(f"x6 forward vs fp64 (per rounding scale): h0 {e0:.1e} h1 {e1:.1e} q {eq:.1e}")
+    assert e0 < SCALE_BAR and e1 < SCALE_BAR and eq < SCALE_BAR, (e0, e1, eq)
+    # every row's Q (kept or not) against end-to-end fp64
+    qf = hs[2].squeeze(-1)
+    rel = float((out.double() - qf).abs().max() / qf.abs().max())
+    assert rel < 1e-5, rel
+    assert torch.isnan(h[0][:, :h_from]).all() and torch.isnan(h[1][:, :h_from]).all()
+    if aux:
+        ha, _ = _fwd64(xa[:aux, :n_in], Wt, bt)
+        qa = ha[2].squeeze(-1)
+        assert float((aout[:, :aux].double() - qa).abs().max() / qa.abs().max()) < 1e-5
+    # deterministic
+    o1 = out.clone()
+    ops.call_desc("d3a_q2_fwd_x6", d)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, out)
+
+
+def test_q2_fwd_x6_matches_fp32_kernel():
+    """The x6 forward and the exact-fp32 MFMA forward (q2_fwd) agree to fp32
+    rounding on the K2 critic pass."""
+    dev = torch.device("cuda")
+    C, rows, n_in, h_from, aux = 2, 15616, 14, 7680, 256
+    gen = torch.Generator().manual_seed(7)
+    Ws, bs = _net(C, n_in, gen, dev)
+    Wt, bt = _net(C, n_in, gen, dev)
+    x = torch.randn(rows, 16, generator=gen).to(dev)
+    xa = torch.randn(aux, 16, generator=gen).to(dev)
+    res = []
+    for entry in ("d3a_q2_fwd_x6", "d3a_mlp_fwd"):
+        h = [torch.zeros(C, rows, 256, device=dev) for _ in range(2)]
+        out, aout = torch.zeros(C, rows, device=dev), torch.zeros(C, aux, device=dev)
+        d, _b = _fwd_desc(x, 16, n_in, Ws, bs, Wt, bt, h, out, aout, xa, rows, h_from, aux, C, dev)
+        ops.call_desc(entry, d)
+        torch.cuda.synchronize()
+        res.append((out, aout, h))
+    for a, b in ((res[0][0], res[1][0]), (res[0][1], res[1][1]), (res[0][2][1], res[1][2][1])):
+        assert float((a - b).abs().max() / b.abs().max()) < 2e-6
+
+
+def _bwd_case(rows, n_in, n_scaled, C, gen, dev):
+    Ws, bs = _net(C, n_in, gen, dev)
+    ldx = (n_in + 3) // 4 * 4
+    x = torch.randn(rows, ldx, generator=gen).to(dev)
+    hs, _ = _fwd64(x[:, :n_in], Ws, bs)
+    h1 = hs[0].float().contiguous()
+    h2 = hs[1].float().contiguous()
+    g = (torch.randn(C, rows, generator=gen) * 1e-2).to(dev)
+    gscale = torch.tensor([0.7], device=dev)
+    P = (rows + 255) // 256
+    W2 = Ws[1].contiguous()
+    w3 = Ws[2].reshape(C, 256).contiguous()
+
+    def run(entry):
+        outs = [torch.full((P, C, 256, n_in), float("nan"), device=dev),
+                torch.full((P, C, 256), float("nan"), device=dev),
+                torch.full((P, C, 256, 256), float("nan"), device=dev),
+                torch.full((P, C, 256), float("nan"), device=dev),
+                torch.full((P, C, 256), float("nan"), device=dev),
+                torch.full((P, C), float("nan"), device=dev)]
+        d = N.Q2BwdDesc()
+        d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
+        d.h1, d.h2, d.sh, d.ldh = h1.data_ptr(), h2.data_ptr(), rows * 256, 256
+        d.g, d.sgb, d.gscale, d.n_scaled = g.data_ptr(), rows, gscale.data_ptr(), n_scaled
+        d.W2, d.sW2, d.w3, d.sw3 = W2.data_ptr(), 256 * 256, w3.data_ptr(), 256
+        d.dW1, d.db1, d.dW2, d.db2, d.dW3, d.db3 = [t.data_ptr() for t in outs]
+        d.rows, d.n_in, d.C = rows, n_in, C
+        ops.call_desc(entry, d)
+        torch.cuda.synchronize()
+        return outs, d
+    # fp64 reference on the kernel's fp32 inputs, and each product's rounding scale
+    gp = g.double().clone()
+    gp[:, :n_scaled] *= 0.7
+    a1, a2 = h1.double(), h2.double()
+    dz2 = gp.unsqueeze(-1) * w3.double().unsqueeze(1) * (a2 > 0)
+    dh1 = dz2 @ W2.double()
+    sdh1 = dz2.abs() @ W2.double().abs()
+    dz1 = dh1 * (a1 > 0)
+    xd = x[:, :n_in].double()
+    ref = {"dW1": (dz1.transpose(1, 2) @ xd, (sdh1 * (a1 > 0)).transpose(1, 2) @ xd.abs()),
+           "db1": (dz1.sum(1), (sdh1 * (a1 > 0)).sum(1)),
+           "dW2": (dz2.transpose(1, 2) @ a1, dz2.abs().transpose(1, 2) @ a1),
+           "db2": (dz2.sum(1), dz2.abs().sum(1)),
+           "dW3": ((gp.unsqueeze(-1) * a2).sum(1), (gp.abs().unsqueeze(-1) * a2).sum(1)),
+           "db3": (gp.sum(1), gp.abs().sum(1))}
+    return run, ref
+
+
+NAMES = ["dW1", "db1", "dW2", "db2", "dW3", "db3"]
+
+
+@pytest.mark.parametrize("rows,n_in,n_scaled", [(7936, 14, 7680), (1000, 48, 999), (300, 23, 0),
+                                                (257, 37, 100)])
+def test_q2_bwd_x6_vs_fp64(rows, n_in, n_scaled):
+    dev = torch.device("cuda")
+    C = 2
+    gen = torch.Generator().manual_seed(rows * 3 + n_in)
+    run, ref = _bwd_case(rows, n_in, n_scaled, C, gen, dev)
+    outs, d = run("d3a_q2_bwd_x6")
+    worst = {}
+    for name, o in zip(NAMES, outs):
+        assert not torch.isnan(o).any(), name
+        got = o.double().sum(0).cpu()
+        r, sc = (v.cpu() for v in ref[name])
+        e_sc = float(((got - r).abs() / sc.clamp_min(1e-30)).max())
+        e_max = float((got - r).abs().max() / r.abs().max())
+        worst[name] = (e_sc, e_max)
+        assert e_sc < SCALE_BAR and e_max < 1e-6, (name, e_sc, e_max)
+    print("x6 backward vs fp64 (rounding scale, max-normalised): " +
+          " ".join(f"{k} {a:.1e}/{b:.1e}" for k, (a, b) in worst.items()))
+    # run-to-run bit-identical (fixed reduction orders)
+    first = [o.clone() for o in outs]
+    ops.call_desc("d3a_q2_bwd_x6", d)
+    torch.cuda.synchronize()
+    for a, b in zip(first, outs):
+        assert torch.equal(a, b)
+
+
+def test_q2_bwd_x6_matches_fp32_kernel():
+    dev = torch.device("cuda")
+    gen = torch.Generator().manual_seed(11)
+    run, _ = _bwd_case(7936, 14, 7680, 2, gen, dev)
+    a, _ = run("d3a_q2_bwd_x6")
+    b, _ = run("d3a_q2_bwd")
+    for name, x, y in zip(NAMES, a, b):
+        xs, ys = x.double().sum(0), y.double().sum(0)
+        assert float((xs - ys).abs().max() / ys.abs().max()) < 2e-6, name
+
+
+def test_q2_x6_rejects_bad_shapes():
+    d = N.Q2BwdDesc()
+    with pytest.raises(RuntimeError, match="null"):
+        ops.call_desc("d3a_q2_bwd_x6", d)
+    f = N.MlpFwdDesc()
+    f.n_in, f.n_hidden, f.H, f.n_out = 64, 2, 256, 1
+    with pytest.raises(RuntimeError, match="n_in <= 48"):
+        ops.call_desc("d3a_q2_fwd_x6", f)
