@@ -163,6 +163,10 @@ WORKLOADS = {
               "256 x n_gpus), n_critics 2, n_action_samples 10, hidden [256,256], reference "
               "defaults; per step three RCCL SUM all-reduces (scalar, critic, actor gradients) "
               "captured in the update graph"),
+    "cqlrepro": ("hopper-medium-v0", 256,
+                 "CQL reproduction (reproductions/offline/cql.py:21-37, hopper-medium-v0): obs 11, "
+                 "act 3, batch 256, n_critics 2, n_action_samples 10, hidden [256,256,256], "
+                 "alpha_learning_rate 0 (no update_alpha), conservative_weight 10"),
     "dcql": ("atari", 512,
              "DiscreteCQL K5 (configs[4]): 4x84x84 uint8 frame stacks (n_frames 4), IQN "
              "(64 quantiles, embed 64), batch 512, 4 actions, pixel scaler, Nature-DQN "
@@ -175,6 +179,14 @@ def _make_algo(name: str, batch: int, gpu: int = 0):
     if name in ("cql", "cqldp"):
         from d3rlpy_amd.algos.cql import CQL
         return CQL(batch_size=batch, n_critics=2, n_action_samples=10, use_gpu=gpu)
+    if name == "cqlrepro":
+        from d3rlpy_amd.algos.cql import CQL
+        from d3rlpy_amd.factories import VectorEncoderFactory
+        enc = VectorEncoderFactory([256, 256, 256])
+        return CQL(actor_learning_rate=1e-4, critic_learning_rate=3e-4, temp_learning_rate=1e-4,
+                   actor_encoder_factory=enc, critic_encoder_factory=enc, batch_size=batch,
+                   n_action_samples=10, alpha_learning_rate=0.0, conservative_weight=10.0,
+                   use_gpu=gpu)
     if name == "dcql":
         from d3rlpy_amd.algos.cql import DiscreteCQL
         return DiscreteCQL(batch_size=batch, n_frames=4, q_func_factory="iqn", scaler="pixel",
@@ -311,14 +323,17 @@ def cpu_step_fn(name: str = "cql"):
     if name == "dcql":
         return _cpu_step_dcql(B, gen)
     n = 100_000
-    D, A = {"cql": (11, 3), "cqldp": (29, 8), "td3bc": (3, 1), "bcq": (17, 6)}[name]
+    D, A = {"cql": (11, 3), "cqlrepro": (11, 3), "cqldp": (29, 8), "td3bc": (3, 1),
+            "bcq": (17, 6)}[name]
     obs, act, rew, term = synthetic_dataset(n, D, A, episode_len=1000, seed=0)
     trans = []
     for o, a, r, t in to_episodes(obs, act, rew, term):
         trans += to_transitions(o, a, r, t)
     np.random.seed(0)
-    if name in ("cql", "cqldp"):
-        orc = CQLOracle(D, A, n_critics=2, n_action_samples=10, seed=0)
+    if name in ("cql", "cqldp", "cqlrepro"):
+        kw = (dict(hidden_units=(256, 256, 256), alpha_learning_rate=0.0, conservative_weight=10.0)
+              if name == "cqlrepro" else {})
+        orc = CQLOracle(D, A, n_critics=2, n_action_samples=10, seed=0, **kw)
 
         def update(batch, k):
             orc.update(batch, CQLNoise.draw(gen, B, A, 10))
@@ -483,6 +498,11 @@ def main():
                          "(d3a_q2_fwd_bf16 / d3a_q2_bwd_bf16), a throughput line, never the "
                          "headline; sbf16x6: the large input-gradient GEMMs on the bf16 "
                          "matrix cores with hi/mid/lo split operands (fp32-accurate)")
+    ap.add_argument("--critic-gemm", choices=["fp32", "x6"], default=None,
+                    help="GEMM arithmetic of the [n_in, 256, 256, 1] critic passes at fp32 "
+                         "accuracy: fp32 = v_mfma_f32_32x32x2_f32; x6 = exact three-way split-bf16 "
+                         "operands on the bf16 matrix cores (csrc/q2_x6*.hip); default: "
+                         "d3rlpy_amd.ops.CRITIC_GEMM")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="host threads of the all-cores CPU baseline (default: this "
                          "process's CPU share)")
@@ -509,6 +529,9 @@ def main():
     if args.precision == "sbf16x6":
         from d3rlpy_amd import ops as _ops
         _ops.set_sbf16(6)
+    from d3rlpy_amd import ops as _ops
+    if args.critic_gemm is not None:
+        _ops.set_critic_gemm(args.critic_gemm)
     wd = _watchdog(args.init_timeout, "rendezvous / RCCL init / warm-up with graph capture")
     ws, rank, local = _dist_setup("nccl", args.init_timeout)
     if ws != args.gpus:
@@ -527,10 +550,26 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     gpu_steps(algo, it, args.steps)
+    t_enq = time.perf_counter()  # host: every step enqueued (no sync inside the loop)
     torch.cuda.synchronize()
     _barrier(ws)
     t1 = time.perf_counter()
     elapsed = _max_over_ranks(t1 - t0, ws)
+    # host cost of one step on its own: a burst enqueued onto an idle device
+    # right after a sync (the gather launch + graph replay through ctypes /
+    # torch), before the device can push back
+    nb = min(20, max(1, args.steps))
+    torch.cuda.synchronize()
+    th0 = time.perf_counter()
+    gpu_steps(algo, it, nb)
+    th1 = time.perf_counter()
+    torch.cuda.synchronize()
+    host = {"host_us_per_step": round(1e6 * (th1 - th0) / nb, 2),
+            "host_loop_us_per_step": round(1e6 * (t_enq - t0) / max(1, args.steps), 2),
+            "method": f"perf_counter around next(it) + _update_async with no sync: a burst of "
+                      f"{nb} steps enqueued onto an idle device (host_us_per_step), and the timed "
+                      "loop's enqueue time over its steps (host_loop_us_per_step: equals "
+                      "ms_per_step when the device pushes back)"}
     # sanity: the losses are finite
     names, vals = algo.impl.read_metrics_ring(None)
     # NaN in a column marks "not computed at this step" (TD3+BC's delayed
@@ -549,13 +588,21 @@ def main():
 
     # MI355X dense MFMA peaks (MI355X_MICROARCH.md): fp32-input 157.3 TF; bf16
     # 2.5 PF (the bf16 line's dominant kernel runs on the bf16 matrix cores)
-    peak_tflops = 2500.0 if args.precision == "bf16" else 157.3
+    # the fp32-accurate split-bf16 critic kernels (CRITIC_GEMM "x6") run six bf16
+    # MFMA products per fp32 product: their ceiling is the bf16 peak / 6
+    x6 = _ops.CRITIC_GEMM == "x6" and args.precision == "fp32" and "x6" in kdesc
+    peak_tflops = 2500.0 if args.precision == "bf16" else (2500.0 / 6 if x6 else 157.3)
     achieved = kflops / kern_s / 1e12
     traffic = None
     if args.traffic_json is None:
         prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
-        args.traffic_json = next((p for p in (os.path.join(prof, f"r0{r}_pmc_traffic_{args.algo}.json")
-                                              for r in (3, 2, 1)) if os.path.exists(p)), "")
+        # the PMC summary of THIS line's dominant kernel: the bf16 and x6 lines
+        # have their own kernels and files (r04_pmc_traffic_<algo>_<suffix>.json)
+        suffix = "_bf16" if args.precision == "bf16" else "_x6" if x6 else ""
+        rounds = (4, 3, 2, 1) if not suffix else (4,)
+        args.traffic_json = next((p for p in (os.path.join(prof, f"r0{r}_pmc_traffic_{args.algo}"
+                                                           f"{suffix}.json")
+                                              for r in rounds) if os.path.exists(p)), "")
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
@@ -573,6 +620,9 @@ def main():
                        "sac_impl.py/ddpg_impl.py)",
                 "cqldp": "CQL update at antmaze shapes, batch 256 (torch CPU, op-for-op "
                          "restatement of cql_impl.py/sac_impl.py/ddpg_impl.py)",
+                "cqlrepro": "CQL reproduction update (hidden [256,256,256], no update_alpha, "
+                            "conservative_weight 10; torch CPU, op-for-op restatement of "
+                            "cql_impl.py/sac_impl.py/ddpg_impl.py)",
                 "td3bc": "TD3+BC update (torch CPU, op-for-op restatement of "
                          "td3_plus_bc_impl.py/td3_impl.py/ddpg_impl.py, standard scaler)",
                 "bcq": "BCQ update (torch CPU, op-for-op restatement of bcq_impl.py/"
@@ -612,6 +662,8 @@ def main():
     shape, batch, wdesc = WORKLOADS[args.algo]
     metric = {"cql": "gradient-steps/sec (CQL, batch=256, obs=11 act=3) at 1/2/4/8 GPU",
               "cqldp": "gradient-steps/sec (CQL data-parallel, 256 rows per GPU, obs=29 act=8)",
+              "cqlrepro": "gradient-steps/sec (CQL reproduction config, batch=256, obs=11 act=3, "
+                          "hidden 3x256, alpha fixed)",
               "td3bc": "gradient-steps/sec (TD3+BC, batch=100, obs=3 act=1)",
               "bcq": "gradient-steps/sec (BCQ QR-200, batch=256, obs=17 act=6)",
               "dcql": "gradient-steps/sec (DiscreteCQL-IQN, batch=512, 4x84x84 pixels)"}[args.algo]
@@ -626,7 +678,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32" if args.precision == "fp32" else
+        "dtype": ("fp32 (critic GEMMs fp32-accurate: exact three-way split-bf16 operands, "
+                  "fp32 accumulation on the bf16 matrix cores)" if x6 else "fp32")
+                 if args.precision == "fp32" else
                  "bf16 (critic-ensemble GEMM operands; fp32 accumulation, losses, optimiser)"
                  if args.precision == "bf16" else
                  "fp32 (input-gradient GEMMs: split-bf16 x6 on bf16 MFMA)",
@@ -642,9 +696,12 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak_tflops,
                      "unit": "TFLOP/s", "frac": round(achieved / peak_tflops, 4),
                      "traffic": traffic, "kernel": kdesc,
+                     **({"bf16_mfma_frac": round(6 * achieved / 2500.0, 4),
+                         "peak_note": "bf16 dense MFMA peak 2500 TF / 6 products"} if x6 else {}),
                      "avg_launch_us": round(kern_s * 1e6, 3)},
         "cpu_baseline": cpu,
     }
+    out["host"] = host
     if allreduce is not None:
         allreduce["frac_of_step"] = round(allreduce["us_per_step"] / (1e3 * out["ms_per_step"]), 4)
         out["allreduce"] = allreduce

@@ -653,23 +653,26 @@ class _Workspace:
 
     def dominant_kernel(self):
         """(launch_fn, flops_per_launch, description) of the MFMA-bound hot
-        kernel: the critic-ensemble forward over all R = 6NB+B Q rows of the
-        step (update_alpha on) with the target ensemble over the B next-state
-        rows as its aux pass — the pipeline's d3a_mlp_fwd launch exactly
-        (activations kept for rows >= 3NB) — or its hidden-layer GEMM when the
+        kernel: the critic-ensemble forward over the step's Q rows -- all R =
+        6NB+B with update_alpha on, the critic set's 3NB+B otherwise
+        (cql.py:244-247) -- with the target ensemble over the B next-state rows
+        as its aux pass: the pipeline's d3a_mlp_fwd launch exactly
+        (activations kept for rows >= 3NB) -- or its hidden-layer GEMM when the
         per-layer path is in use."""
         impl = self.impl
         net, st = impl.critic, impl.store
         s = net.sizes
         R, C, DA, B = self.R, self.C, self.LDX, self.B
-        if mlp.fused_ok(net, R):
+        r0 = 0 if impl._alpha_learning_rate > 0 else 3 * self.NB
+        if mlp.fused_ok(net, R - r0):
             def launch():
-                mlp.forward(net, st, self.x_q.data_ptr(), True, DA, self.qacts, 0, R,
+                mlp.forward(net, st, self.x_q.data_ptr(), True, DA, self.qacts, r0, R,
                             h_from=3 * self.NB,
                             aux=(impl.targ, self.x_targ.data_ptr(), DA, self.tacts))
-            flops = 2 * C * (R + B) * sum(s[l] * s[l + 1] for l in range(len(s) - 1))
-            return launch, flops, (f"d3a_mlp_fwd critic ensemble: C={C} x ({R} + {B} target) "
-                                   f"rows x {'-'.join(map(str, s))}")
+            flops = 2 * C * (R - r0 + B) * sum(s[l] * s[l + 1] for l in range(len(s) - 1))
+            gemm = "split-bf16 x6" if (ops.CRITIC_GEMM == "x6" and mlp.q2_shape(net)) else "fp32"
+            return launch, flops, (f"d3a_mlp_fwd critic ensemble ({gemm} MFMA): C={C} x "
+                                   f"({R - r0} + {B} target) rows x {'-'.join(map(str, s))}")
         H, Hin = s[2], s[1]
         h0, h1 = self.qacts.h[0], self.qacts.h[1]
 

@@ -55,7 +55,10 @@ struct X6FwdLds {
   float hp[8][X_RB];                // head partials [wave][row]
 };
 
-template <int XL>
+// PROBE (timing probes only, D3A_X6_PROBE; results are wrong): bit 0 skips
+// the layer-1 productions after the first, bit 1 the per-chunk W1 split (the
+// first chunk's parts reused), bit 2 the kept-activation stores
+template <int XL, int PROBE = 0>
 __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   constexpr int XLD = XL + 8;
   constexpr int NS0 = XL / 16;  // layer-1 k steps
@@ -155,7 +158,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       const float4 bv = bv4[R];
       float v[4] = {fmaxf(a[4 * R + 0] + bv.x, 0.f), fmaxf(a[4 * R + 1] + bv.y, 0.f),
                     fmaxf(a[4 * R + 2] + bv.z, 0.f), fmaxf(a[4 * R + 3] + bv.w, 0.f)};
-      if (keep)
+      if (keep && !(PROBE & 4))
         *reinterpret_cast<float4*>(h0g + row * X_H + X_CK * j + k) = make_float4(v[0], v[1], v[2], v[3]);
       bf16x4 p[3];
       split4(v, p);
@@ -180,11 +183,11 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     for (int s = 0; s < 2; ++s) {
       const float v[8] = {wr[s][0].x, wr[s][0].y, wr[s][0].z, wr[s][0].w,
                           wr[s][1].x, wr[s][1].y, wr[s][1].z, wr[s][1].w};
-      split8(v, wa[s]);
+      if (!(PROBE & 2) || j == 0) split8(v, wa[s]);
     }
     if (j + 1 < X_NCK) {
       load_w1(j + 1);
-      if ((w >> 2) == ((j + 1) & 1)) produce(j + 1);
+      if (!(PROBE & 1) && (w >> 2) == ((j + 1) & 1)) produce(j + 1);
     }
     const int slot = j & 1;
 #pragma unroll
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = fmaxf(acc[tt][r] + bb[r], 0.f);
     const int row = m0 + 32 * tt + li;
-    if (h1g != nullptr && row >= h_from && row < rend) {
+    if (!(PROBE & 4) && h1g != nullptr && row >= h_from && row < rend) {
 #pragma unroll
       for (int R = 0; R < 4; ++R)
         *reinterpret_cast<float4*>(h1g + row * X_H + 32 * w + 8 * R + 4 * lh) =
@@ -280,6 +283,21 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
   const dim3 grid((unsigned)nb, 1, (unsigned)d.C);
   const hipStream_t st = (hipStream_t)stream;
   const int xl = (d.n_in + 15) / 16 * 16;
+  static const int probe = [] {
+    const char* e = getenv("D3A_X6_PROBE");
+    return e ? atoi(e) : 0;
+  }();
+  if (probe && xl == 16) {
+    switch (probe & 7) {
+      case 1: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 1>), grid, dim3(512), 0, st, d); break;
+      case 2: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 2>), grid, dim3(512), 0, st, d); break;
+      case 3: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 3>), grid, dim3(512), 0, st, d); break;
+      case 4: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 4>), grid, dim3(512), 0, st, d); break;
+      default: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 7>), grid, dim3(512), 0, st, d); break;
+    }
+    D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
+    return 0;
+  }
   if (xl == 16)
     hipLaunchKernelGGL(q2x6_fwd_kernel<16>, grid, dim3(512), 0, st, d);
   else if (xl == 32)

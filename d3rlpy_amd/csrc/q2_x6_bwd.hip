@@ -64,7 +64,10 @@ struct B6Lds {
   float ex[2][2 * 2 * 16 * 64];    // dh1 o-half partials [buf][ib][kh][reg][lane]
 };
 
-template <int NDB>  // 32-wide input blocks of dW1 (n_in <= 32 NDB)
+// NDB: 32-wide input blocks of dW1 (n_in <= 32 NDB).  PROBE (timing probes
+// only, D3A_X6_PROBE >> 3; results are wrong): bit 0 skips the staging after
+// the first sub-block, bit 1 the dX waves' finishing work, bit 2 the fp64 sums
+template <int NDB, int PROBE = 0>
 __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
   __shared__ __attribute__((aligned(16))) B6Lds L;
   static_assert(sizeof(B6Lds) <= 163840, "LDS");
@@ -224,7 +227,7 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
     for (int sb = 0; sb < B6_NSB; ++sb) {
       const B6Buf& B = L.b[sb & 1];
       if (sb > 0) {
-        finish(sb - 1);
+        if (!(PROBE & 2)) finish(sb - 1);
         load_fin(sb);
       }
       f32x16 acc;
@@ -235,8 +238,8 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
       for (int s = 0; s < 8; ++s) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + 16 * s);
         acc = x3m(a, wb[s], acc);
-        if (s == 2) stage_sb(sb + 1);
-        if (s == 5) load_sb(sb + 2 < B6_NSB ? sb + 2 : B6_NSB - 1);
+        if (!(PROBE & 1) && s == 2) stage_sb(sb + 1);
+        if (!(PROBE & 1) && s == 5) load_sb(sb + 2 < B6_NSB ? sb + 2 : B6_NSB - 1);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) L.ex[sb & 1][((ib * 2 + kh) * 16 + r) * 64 + lane] = acc[r];
@@ -280,8 +283,10 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
             const bool on = ok && hv[e] > 0.f;
             m[k][e] = on ? (__bf16)1.f : (__bf16)0.f;
             mv[e] = m[k][e];
-            s_db2[bo][e] += (double)(on ? g * w3a[bo][e] : 0.f);
-            s_dw3[bo][e] += (double)(g * (ok ? hv[e] : 0.f));
+            if (!(PROBE & 4)) {
+              s_db2[bo][e] += (double)(on ? g * w3a[bo][e] : 0.f);
+              s_dw3[bo][e] += (double)(g * (ok ? hv[e] : 0.f));
+            }
           }
           if (bo == 0 && t2 < 8) s_db3 += (double)g;
           *reinterpret_cast<bf16x4*>(&B.mro[(ra + k) * B6_LRO + oa + 128 * bo]) = mv;
@@ -322,8 +327,10 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
         for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
           for (int bi = 0; bi < 2; ++bi) R[2 * ob + bi] = x3m(a[ob], hb[bi], R[2 * ob + bi]);
-        if (s == 0) stage_sb(sb + 1);
-        else load_sb(sb + 2 < B6_NSB ? sb + 2 : B6_NSB - 1);
+        if (!(PROBE & 1)) {
+          if (s == 0) stage_sb(sb + 1);
+          else load_sb(sb + 2 < B6_NSB ? sb + 2 : B6_NSB - 1);
+        }
       }
       __syncthreads();  // sub-block sb + 1 staged
     }
@@ -427,6 +434,22 @@ extern "C" int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* dp, void* stream) {
   const int64_t blocks = (units + 7) / 8 * 32;
   D3A_CHECK_ARG(blocks < (int64_t(1) << 31), "d3a_q2_bwd_x6: too many rows");
   const dim3 grid((unsigned)blocks), block(B6_NT);
+  static const int probe = [] {
+    const char* e = getenv("D3A_X6_PROBE");
+    return e ? atoi(e) >> 3 : 0;
+  }();
+  if (probe && d.n_in <= 32) {
+    const hipStream_t st = (hipStream_t)stream;
+    switch (probe & 7) {
+      case 1: hipLaunchKernelGGL((q2x6_bwd_kernel<1, 1>), grid, block, 0, st, d); break;
+      case 2: hipLaunchKernelGGL((q2x6_bwd_kernel<1, 2>), grid, block, 0, st, d); break;
+      case 3: hipLaunchKernelGGL((q2x6_bwd_kernel<1, 3>), grid, block, 0, st, d); break;
+      case 4: hipLaunchKernelGGL((q2x6_bwd_kernel<1, 4>), grid, block, 0, st, d); break;
+      default: hipLaunchKernelGGL((q2x6_bwd_kernel<1, 7>), grid, block, 0, st, d); break;
+    }
+    D3A_LAUNCH_CHECK("d3a_q2_bwd_x6");
+    return 0;
+  }
   if (d.n_in <= 32)
     hipLaunchKernelGGL(q2x6_bwd_kernel<1>, grid, block, 0, (hipStream_t)stream, d);
   else

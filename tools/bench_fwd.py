@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--C", type=int, default=2)
     ap.add_argument("--J", type=int, default=1)
     ap.add_argument("--bf16", action="store_true", help="d3a_q2_fwd_bf16 (bf16 kept activations)")
+    ap.add_argument("--x6", action="store_true", help="d3a_q2_fwd_x6 (split-bf16 x6, fp32-accurate)")
     a = ap.parse_args()
     dev, C, H = "cuda", a.C, 256
     sizes = [a.n_in, H, H, a.J]
@@ -48,7 +49,7 @@ def main():
         offs.append((w, b))
     h = [torch.zeros(C, a.rows, H, device=dev,
                      dtype=torch.bfloat16 if a.bf16 else torch.float32) for _ in range(2)]
-    entry = "d3a_q2_fwd_bf16" if a.bf16 else "d3a_mlp_fwd"
+    entry = "d3a_q2_fwd_bf16" if a.bf16 else "d3a_q2_fwd_x6" if a.x6 else "d3a_mlp_fwd"
     out = torch.zeros(C, a.rows, a.J, device=dev)
     aout = torch.zeros(C, max(a.aux, 1), a.J, device=dev)
     d = N.MlpFwdDesc()

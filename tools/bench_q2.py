@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--rows", type=int, default=7936)
     ap.add_argument("--n-in", type=int, default=14)
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--x6", action="store_true", help="d3a_q2_bwd_x6 (split-bf16, fp32-accurate)")
     a = ap.parse_args()
     rows, n_in, Cm, dev = a.rows, a.n_in, 2, "cuda"
     ldx = (n_in + 3) // 4 * 4
@@ -37,6 +38,7 @@ def main():
     outs = [torch.zeros(P, Cm, H, n_in, device=dev), torch.zeros(P, Cm, H, device=dev),
             torch.zeros(P, Cm, H, H, device=dev), torch.zeros(P, Cm, H, device=dev),
             torch.zeros(P, Cm, H, device=dev), torch.zeros(P, Cm, device=dev)]
+    entry = "d3a_q2_bwd_x6" if a.x6 else "d3a_q2_bwd"
     d = N.Q2BwdDesc()
     d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
     d.h1, d.h2, d.sh, d.ldh = h1.data_ptr(), h2.data_ptr(), rows * H, H
@@ -45,18 +47,18 @@ def main():
     d.dW1, d.db1, d.dW2, d.db2, d.dW3, d.db3 = [t.data_ptr() for t in outs]
     d.rows, d.n_in, d.C = rows, n_in, Cm
     for _ in range(5):
-        ops.call_desc("d3a_q2_bwd", d)
+        ops.call_desc(entry, d)
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(a.reps):
-        ops.call_desc("d3a_q2_bwd", d)
+        ops.call_desc(entry, d)
     e1.record(s)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / a.reps
     flops = 2 * Cm * rows * (2 * H * H + H * 32)
-    print(json.dumps({"kernel": "d3a_q2_bwd", "rows": rows, "n_in": n_in, "avg_us": round(us, 2),
+    print(json.dumps({"kernel": entry, "rows": rows, "n_in": n_in, "avg_us": round(us, 2),
                       "tflops": round(flops / us / 1e6, 2),
                       "frac_fp32_peak": round(flops / us / 1e6 / 157.3, 4)}))
 

@@ -8,7 +8,7 @@ timeout -k 10 300 python bench.py > gpurun_out/final_bench_cql.log 2>&1 || exit 
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/final_prof -o run --output-format csv -- python3 $R/bench.py --steps 500 --warmup 20 --no-cpu-baseline --transitions 200000 > $R/gpurun_out/final_prof.log 2>&1 || exit $?
 cd $R && python tools/prof_by_shape.py gpurun_out/final_prof/run_kernel_trace.csv 520 > gpurun_out/final_prof_breakdown.txt && rm -f gpurun_out/final_prof/run_kernel_trace.csv
-bash tools/pmc_pass.sh cql mlp_fwd_kernel || exit $?
+bash tools/profiling/pmc_pass.sh cql mlp_fwd_kernel || exit $?
 cd $R
 for a in td3bc bcq dcql cqldp; do
   timeout -k 10 300 python bench.py --algo $a --cpu-seconds 10 > gpurun_out/final_bench_$a.log 2>&1 || exit $?

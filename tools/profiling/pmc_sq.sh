@@ -1,6 +1,6 @@
 #!/bin/bash
 # One rocprofv3 pass of SQ stall counters over the dominant kernel:
-#   bash tools/pmc_sq.sh ALGO KERNEL_SUBSTRING TAG
+#   bash tools/profiling/pmc_sq.sh ALGO KERNEL_SUBSTRING TAG
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 ALGO=${1:-cql}
 SUB=${2:-mlp_fwd_kernel}
