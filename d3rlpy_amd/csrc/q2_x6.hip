@@ -44,9 +44,10 @@ using namespace x6;
 
 constexpr int X_H = 256;    // hidden width
 constexpr int X_RB = 128;   // rows per workgroup
-constexpr int X_CK = 32;    // layer-2 k per chunk (= layer-1 units per chunk)
+constexpr int X_CK = 64;    // layer-2 k per chunk (= layer-1 units per chunk)
 constexpr int X_NCK = X_H / X_CK;
-constexpr int X_LDB = 40;   // bf16 row stride of a ring slot (80 B)
+constexpr int X_KS = X_CK / 16;  // MFMA k steps per chunk
+constexpr int X_LDB = 72;   // bf16 row stride of a ring slot (144 B: conflict-free 16-B reads)
 
 template <int XL>
 struct X6FwdLds {
@@ -56,8 +57,11 @@ struct X6FwdLds {
 };
 
 // PROBE (timing probes only, D3A_X6_PROBE; results are wrong): bit 0 skips
-// the layer-1 productions after the first, bit 1 the per-chunk W1 split (the
-// first chunk's parts reused), bit 2 the kept-activation stores
+// the layer-1 productions after the first, bit 2 the kept-activation stores,
+// bit 3 the W1 reloads (chunk 0's registers reused); bit 4 (diagnostic build,
+// results right) records s_memtime stamps of wave 0 at the phase boundaries
+// into x6_stamps (read with d3a_x6_stamps)
+__device__ unsigned long long x6_stamps[2048 * 10];
 template <int XL, int PROBE = 0>
 __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   constexpr int XLD = XL + 8;
@@ -81,14 +85,24 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   float* const h1g = (!aux && d.h[1]) ? d.h[1] + c * d.sh : nullptr;
   const float* W0 = d.W[0] + wdel + c * d.sW[0];
   const float* b0 = d.b[0] + wdel + c * d.sb[0];
+  const int wg = blockIdx.x + blockIdx.z * gridDim.x;
+  auto stamp = [&](int k) {
+    if constexpr ((PROBE & 16) != 0) {
+      if (t == 0 && wg < 2048) x6_stamps[wg * 10 + k] = __builtin_amdgcn_s_memtime();
+    }
+  };
+  if constexpr ((PROBE & 16) != 0) {
+    if (t == 0 && wg < 2048) x6_stamps[wg * 10 + 9] = __builtin_amdgcn_s_memrealtime();
+  }
+  stamp(0);
   // this lane's W1 row (unit 32 w + li) at k offset 8 lh
   const float* W1 = d.W[1] + wdel + c * d.sW[1] + (32 * w + li) * X_H + 8 * lh;
 
   // ---- prologue: the first W1 chunk in flight, input rows split into LDS
-  float4 wr[2][2];  // raw fp32 W1 of the chunk in flight: [k step][half]
+  float4 wr[X_KS][2];  // raw fp32 W1 of the chunk in flight: [k step][half]
   auto load_w1 = [&](int j) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < X_KS; ++s) {
       wr[s][0] = *reinterpret_cast<const float4*>(W1 + X_CK * j + 16 * s);
       wr[s][1] = *reinterpret_cast<const float4*>(W1 + X_CK * j + 16 * s + 4);
     }
@@ -111,15 +125,17 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     }
   }
   __syncthreads();  // x parts staged
+  stamp(1);
 
-  // ---- layer 1, chunk j: units 32 j .. + 31 of rows 32 (w & 3) .. + 31 (a wave
-  // of the half j & 1): bias, ReLU, fp32 kept rows to h[0], parts to ring slot
-  // j & 1.  The wave's W0 rows and bias of its next chunk are loaded one
-  // production ahead (a production is on the chunk's critical path).
+  // ---- layer 1, chunk j: every wave produces one 32 x 32 tile of it -- units
+  // 64 j + 32 (w >> 2) .. + 31 of rows 32 (w & 3) .. + 31: bias, ReLU, fp32 kept
+  // rows to h[0], parts to ring slot j & 1.  The wave's W0 rows and bias of
+  // its next chunk are loaded one production ahead.
   float w0n[NS0][8];
   float4 b0n[4];
+  const int ut = 32 * (w >> 2);  // this wave's unit tile inside a chunk
   auto load_w0 = [&](int j) {
-    const int u = X_CK * j + li;
+    const int u = X_CK * j + ut + li;
 #pragma unroll
     for (int s = 0; s < NS0; ++s)
 #pragma unroll
@@ -128,9 +144,9 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
         w0n[s][i] = k < nin ? W0[u * nin + k] : 0.f;
       }
 #pragma unroll
-    for (int R = 0; R < 4; ++R) b0n[R] = *reinterpret_cast<const float4*>(b0 + X_CK * j + 8 * R + 4 * lh);
+    for (int R = 0; R < 4; ++R) b0n[R] = *reinterpret_cast<const float4*>(b0 + X_CK * j + ut + 8 * R + 4 * lh);
   };
-  load_w0(w >> 2);
+  load_w0(0);
   auto produce = [&](int j) {
     const int tt = w & 3;
     f32x16 a;
@@ -148,13 +164,13 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     float4 bv4[4];
 #pragma unroll
     for (int R = 0; R < 4; ++R) bv4[R] = b0n[R];
-    if (j + 2 < X_NCK) load_w0(j + 2);
-    // lane: row 32 tt + li, units 32 j + 8 R + 4 lh + i (accumulator 4 R + i)
+    if (j + 1 < X_NCK) load_w0(j + 1);
+    // lane: row 32 tt + li, units 64 j + ut + 8 R + 4 lh + i (accumulator 4 R + i)
     const int row = m0 + 32 * tt + li;
     const bool keep = h0g != nullptr && row >= h_from && row < rend;
 #pragma unroll
     for (int R = 0; R < 4; ++R) {
-      const int k = 8 * R + 4 * lh;  // local k of the chunk
+      const int k = ut + 8 * R + 4 * lh;  // local k of the chunk
       const float4 bv = bv4[R];
       float v[4] = {fmaxf(a[4 * R + 0] + bv.x, 0.f), fmaxf(a[4 * R + 1] + bv.y, 0.f),
                     fmaxf(a[4 * R + 2] + bv.z, 0.f), fmaxf(a[4 * R + 3] + bv.w, 0.f)};
@@ -167,8 +183,9 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
         *reinterpret_cast<bf16x4*>(&L.h[j & 1][q][(32 * tt + li) * X_LDB + k]) = p[q];
     }
   };
-  if ((w >> 2) == 0) produce(0);
+  produce(0);
   __syncthreads();  // chunk 0 in slot 0
+  stamp(2);
 
   // ---- layer 2: acc[tt] = C^T[units 32 w ..][rows 32 tt ..]
   f32x16 acc[4];
@@ -178,30 +195,33 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     for (int r = 0; r < 16; ++r) acc[tt][r] = 0.f;
 #pragma unroll 1
   for (int j = 0; j < X_NCK; ++j) {
-    bf16x8 wa[2][3];
+    float4 wc[X_KS][2];  // this chunk's raw W1 (the next chunk's loads reuse wr)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const float v[8] = {wr[s][0].x, wr[s][0].y, wr[s][0].z, wr[s][0].w,
-                          wr[s][1].x, wr[s][1].y, wr[s][1].z, wr[s][1].w};
-      if (!(PROBE & 2) || j == 0) split8(v, wa[s]);
+    for (int s = 0; s < X_KS; ++s) {
+      wc[s][0] = wr[s][0];
+      wc[s][1] = wr[s][1];
     }
-    if (j + 1 < X_NCK) {
-      load_w1(j + 1);
-      if (!(PROBE & 1) && (w >> 2) == ((j + 1) & 1)) produce(j + 1);
-    }
+    if (j + 1 < X_NCK && !((PROBE & 8) && j > 0)) load_w1(j + 1);
     const int slot = j & 1;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < X_KS; ++s) {
+      bf16x8 wa[3];
+      const float v[8] = {wc[s][0].x, wc[s][0].y, wc[s][0].z, wc[s][0].w,
+                          wc[s][1].x, wc[s][1].y, wc[s][1].z, wc[s][1].w};
+      split8(v, wa);
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
         bf16x8 bp[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q)
           bp[q] = *reinterpret_cast<const bf16x8*>(&L.h[slot][q][(32 * tt + li) * X_LDB + 16 * s + 8 * lh]);
-        acc[tt] = prod6(wa[s], bp, acc[tt]);
+        acc[tt] = prod6(wa, bp, acc[tt]);
       }
+      // the next chunk's layer-1 tile, issued behind this chunk's first half
+      if (s == 1 && j + 1 < X_NCK && !(PROBE & 1)) produce(j + 1);
     }
     __syncthreads();  // slot j & 1 free; chunk j + 1 in slot (j + 1) & 1
+    stamp(3 + j);
   }
 
   // ---- epilogue: bias, ReLU, kept rows to h[1], the head dot of the lane's
@@ -238,6 +258,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     const float o = __shfl_xor(hs, 32, 64);
     if (lh == 0) L.hp[w][32 * tt + li] = hs + o;
   }
+  stamp(7);
   __syncthreads();
   if (t < X_RB) {
     float q = L.hp[0][t];
@@ -246,6 +267,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     const int row = m0 + t;
     if (row < rend) outp[(int64_t)row * d.ldout] = q + b2v;
   }
+  stamp(8);
 }
 
 }  // namespace
@@ -288,12 +310,13 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
     return e ? atoi(e) : 0;
   }();
   if (probe && xl == 16) {
-    switch (probe & 7) {
+    switch (probe & 31) {
       case 1: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 1>), grid, dim3(512), 0, st, d); break;
-      case 2: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 2>), grid, dim3(512), 0, st, d); break;
-      case 3: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 3>), grid, dim3(512), 0, st, d); break;
       case 4: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 4>), grid, dim3(512), 0, st, d); break;
-      default: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 7>), grid, dim3(512), 0, st, d); break;
+      case 5: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
+      case 13: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 13>), grid, dim3(512), 0, st, d); break;
+      case 16: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 16>), grid, dim3(512), 0, st, d); break;
+      default: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
     }
     D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
     return 0;
@@ -305,5 +328,16 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
   else
     hipLaunchKernelGGL(q2x6_fwd_kernel<48>, grid, dim3(512), 0, st, d);
   D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
+  return 0;
+}
+
+// diagnostic: copy the stamp buffer of the last D3A_X6_PROBE & 16 launch
+extern "C" int d3a_x6_stamps(unsigned long long* dst, int n) {
+  D3A_CHECK_ARG(dst && n >= 0 && n <= 2048 * 10, "d3a_x6_stamps: bad arguments");
+  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(x6_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) !=
+      hipSuccess) {
+    set_error("d3a_x6_stamps: copy failed");
+    return -2;
+  }
   return 0;
 }

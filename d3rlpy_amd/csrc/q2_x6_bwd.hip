@@ -62,6 +62,10 @@ struct B6Buf {
 struct B6Lds {
   B6Buf b[2];
   float ex[2][2 * 2 * 16 * 64];    // dh1 o-half partials [buf][ib][kh][reg][lane]
+  // what the dX waves' finish of a sub-block reads one sub-block later (a
+  // three-slot ring: the slot being finished, staged and read)
+  __bf16 h1m[3][B6_QW * B6_LR];    // [h1 > 0] [i][r]
+  float gp[3][B6_SB];              // g' of the rows
 };
 
 // NDB: 32-wide input blocks of dW1 (n_in <= 32 NDB).  PROBE (timing probes
@@ -109,50 +113,115 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
 
   // ---- staging.  dW2 waves (t2 = t - 256): two 4 x 4 blocks of h2 (rows
   // 4 (t2 & 7) + k, o = 4 (t2 >> 3) + e and + 128) -> the two mask images and
-  // the fp64 head / bias sums; dX waves: h1 of rows 8 (t >> 6) + k at unit
-  // i0 + (t & 63) -> the parts of g' h1
+  // the head / bias sums; dX waves: h1 of rows 8 (t >> 6) + k at unit
+  // i0 + (t & 63) -> the parts of g' h1.  (The dX waves carry the w3 W2
+  // operand in registers: the heavier staging goes to the dW2 waves.)
   const int t2 = t - 256;
   const int ra = 4 * (t2 & 7), oa = 4 * (t2 >> 3);
   const int ih = t & 63, rh = 8 * (t >> 6);
-
-  f32x16 W1acc[NDB];  // dX waves: dW1 over the rows they finish
-  double s_db1 = 0.0;
-  // fp64 running sums (dW2 waves) of q2_bwd.hip's definitions: db2 += fp32(g'
-  // w3) over unmasked entries, dW3 += fp32(g' h2), db3 += g'
-  double s_db2[2][4], s_dw3[2][4], s_db3 = 0.0;
+  // running sums (dW2 waves) of q2_bwd.hip's definitions (db2 over unmasked
+  // fp32(g' w3), dW3 over fp32(g' h2), db3 over g'): each thread's 32 rows of
+  // the block in fp32, in row order (the register budget of this role has no
+  // room for 16 fp64 accumulators), the eight threads of a column in fp64
+  float s_db2[2][4], s_dw3[2][4];
+  double s_db3 = 0.0;
 #pragma unroll
   for (int bo = 0; bo < 2; ++bo)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) s_db2[bo][e] = s_dw3[bo][e] = 0.0;
-  if (role_dx) {
-    float h1v[8], gh[8];
-    auto load_sb = [&](int sb) {
-      const int base = rb0 + sb * B6_SB;
+    for (int e = 0; e < 4; ++e) s_db2[bo][e] = s_dw3[bo][e] = 0.f;
+  float4 h2v[2][4];
+  float ga[4];
+  float h1v[8], gh[8];
+  auto load_sb = [&](int sb) {
+    const int base = rb0 + sb * B6_SB;
+    if (role_dx) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int r = min(base + rh + k, rlast);
         h1v[k] = h1g[r * B6_H + i0 + ih];
         gh[k] = gprime(r);
       }
-    };
-    auto stage_sb = [&](int sb) {
-      B6Buf& B = L.b[sb & 1];
-      const int base = rb0 + sb * B6_SB;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = min(base + ra + k, rlast);
+#pragma unroll
+        for (int bo = 0; bo < 2; ++bo)
+          h2v[bo][k] = *reinterpret_cast<const float4*>(h2g + r * B6_H + oa + 128 * bo);
+        ga[k] = gprime(r);
+      }
+    }
+  };
+  auto stage_sb = [&](int sb) {
+    B6Buf& B = L.b[sb & 1];
+    const int base = rb0 + sb * B6_SB;
+    if (role_dx) {
+      const int slot = sb % 3;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         float hgv[4];
+        bf16x4 mk;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const bool ok = base + rh + 4 * hh + k < rows && sb < B6_NSB;
           hgv[k] = ok ? gh[4 * hh + k] * h1v[4 * hh + k] : 0.f;
+          mk[k] = (ok && h1v[4 * hh + k] > 0.f) ? (__bf16)1.f : (__bf16)0.f;
         }
         bf16x4 pp[3];
         split4(hgv, pp);
 #pragma unroll
         for (int qq = 0; qq < 3; ++qq)
           *reinterpret_cast<bf16x4*>(&B.hg[qq][ih * B6_LR + rh + 4 * hh]) = pp[qq];
+        *reinterpret_cast<bf16x4*>(&L.h1m[slot][ih * B6_LR + rh + 4 * hh]) = mk;
       }
-    };
+      if (ih == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) L.gp[slot][rh + k] = gh[k];
+      }
+      return;
+    }
+    float pg = 0.f;
+#pragma unroll
+    for (int bo = 0; bo < 2; ++bo) {
+      const float4 w4 = *reinterpret_cast<const float4*>(w3g + oa + 128 * bo);
+      const float w3a[4] = {w4.x, w4.y, w4.z, w4.w};
+      __bf16 m[4][4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool ok = base + ra + k < rows && sb < B6_NSB;
+        const float g = ok ? ga[k] : 0.f;
+        const float hv[4] = {h2v[bo][k].x, h2v[bo][k].y, h2v[bo][k].z, h2v[bo][k].w};
+        bf16x4 mv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool on = ok && hv[e] > 0.f;
+          m[k][e] = on ? (__bf16)1.f : (__bf16)0.f;
+          mv[e] = m[k][e];
+          if (!(PROBE & 4)) {
+            s_db2[bo][e] += on ? g * w3a[e] : 0.f;
+            s_dw3[bo][e] += g * (ok ? hv[e] : 0.f);
+          }
+        }
+        if (bo == 0) pg += g;
+        *reinterpret_cast<bf16x4*>(&B.mro[(ra + k) * B6_LRO + oa + 128 * bo]) = mv;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bf16x4 mv;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) mv[k] = m[k][e];
+        *reinterpret_cast<bf16x4*>(&B.mor[(oa + 128 * bo + e) * B6_LR + ra]) = mv;
+      }
+    }
+    if (t2 < 8) s_db3 += (double)pg;
+  };
+
+  f32x16 W1acc[NDB];  // dX waves: dW1 over the rows they finish
+  double s_db1 = 0.0;
+  load_sb(0);
+  stage_sb(0);
+  load_sb(1);
+  if (role_dx) {
     // ---- B operand: (w3 W2)[o][i] for o = 128 kh + 16 s + 8 lh + j, unit
     // i0 + 32 ib + li, as three bf16 parts per k step
     bf16x8 wb[8][3];
@@ -169,21 +238,17 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
         split8(v, wb[s]);
       }
     }
-    load_sb(0);
-    stage_sb(0);
-    load_sb(1);
     // the rows this wave finishes of a sub-block: accumulator registers
     // 8 kh + r2, rows 16 kh + 8 (r2 >> 2) + 4 lh + (r2 & 3)
     auto frow = [&](int r2) { return 16 * kh + 8 * (r2 >> 2) + 4 * lh + (r2 & 3); };
-    // finishing operands of one sub-block, prefetched from global memory
-    float fg[8], fh[8], fx[NDB][8];
+    // x of the rows this wave finishes, prefetched from global memory; their
+    // g' and [h1 > 0] come from the ring the staging wrote
+    float fx[NDB][8];
     auto load_fin = [&](int sb) {
       const int base = rb0 + sb * B6_SB;
 #pragma unroll
       for (int r2 = 0; r2 < 8; ++r2) {
         const int r = min(base + frow(r2), rlast);
-        fg[r2] = gprime(r);
-        fh[r2] = h1g[r * B6_H + i0 + 32 * ib + li];
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
           const int dc = 32 * db + li;
@@ -195,19 +260,25 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
     for (int db = 0; db < NDB; ++db)
 #pragma unroll
       for (int r = 0; r < 16; ++r) W1acc[db][r] = 0.f;
-    // rows of sub-block sb this wave finishes: both o halves from LDS (its own
-    // and the partner's, o half 0 first), dz1 = g' dh1 [h1 > 0], db1, dW1
+    // rows of sub-block sb this wave finishes: both o halves from LDS (o half
+    // 0 first), dz1 = g' dh1 [h1 > 0], db1, dW1
     auto finish = [&](int sb) {
-      const int eb = sb & 1;
-      const int base = rb0 + sb * B6_SB;
+      const int eb = sb & 1, slot = sb % 3;
+      // rows frow(0..3) and frow(4..7) are two runs of four
+      const bf16x4 m0 = *reinterpret_cast<const bf16x4*>(&L.h1m[slot][(32 * ib + li) * B6_LR + frow(0)]);
+      const bf16x4 m1 = *reinterpret_cast<const bf16x4*>(&L.h1m[slot][(32 * ib + li) * B6_LR + frow(4)]);
+      const float4 g0 = *reinterpret_cast<const float4*>(&L.gp[slot][frow(0)]);
+      const float4 g1 = *reinterpret_cast<const float4*>(&L.gp[slot][frow(4)]);
+      const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
       float z[8];
 #pragma unroll
       for (int r2 = 0; r2 < 8; ++r2) {
         const float o0 = L.ex[eb][((ib * 2 + 0) * 16 + 8 * kh + r2) * 64 + lane];
         const float o1 = L.ex[eb][((ib * 2 + 1) * 16 + 8 * kh + r2) * 64 + lane];
         const float v = __fadd_rn(o0, o1);
-        const bool ok = base + frow(r2) < rows;
-        z[r2] = (ok && fh[r2] > 0.f) ? fg[r2] * v : 0.f;
+        const __bf16 mk = r2 < 4 ? m0[r2 & 3] : m1[r2 & 3];
+        // rows past the end were staged with mask 0
+        z[r2] = (float)mk != 0.f ? gv[r2] * v : 0.f;
         s_db1 += (double)z[r2];
       }
       // dW1[i][d] += sum_r dz1[r][i] x[r][d]: A = the dz1 rows (k step kh of the
@@ -226,10 +297,6 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
 #pragma unroll 1
     for (int sb = 0; sb < B6_NSB; ++sb) {
       const B6Buf& B = L.b[sb & 1];
-      if (sb > 0) {
-        if (!(PROBE & 2)) finish(sb - 1);
-        load_fin(sb);
-      }
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -238,8 +305,10 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
       for (int s = 0; s < 8; ++s) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + 16 * s);
         acc = x3m(a, wb[s], acc);
-        if (!(PROBE & 1) && s == 2) stage_sb(sb + 1);
-        if (!(PROBE & 1) && s == 5) load_sb(sb + 2 < B6_NSB ? sb + 2 : B6_NSB - 1);
+        if (s == 1 && sb > 0 && !(PROBE & 2)) finish(sb - 1);
+        if (s == 3 && sb > 0) load_fin(sb);
+        if (!(PROBE & 1) && s == 5) stage_sb(sb + 1);
+        if (!(PROBE & 1) && s == 7) load_sb(sb + 2 < B6_NSB ? sb + 2 : B6_NSB - 1);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) L.ex[sb & 1][((ib * 2 + kh) * 16 + r) * 64 + lane] = acc[r];
@@ -247,62 +316,6 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
     }
     finish(B6_NSB - 1);
   } else {
-    float4 h2v[2][4];
-    float ga[4];
-    float w3a[2][4];
-#pragma unroll
-    for (int bo = 0; bo < 2; ++bo) {
-      const float4 v = *reinterpret_cast<const float4*>(w3g + oa + 128 * bo);
-      w3a[bo][0] = v.x; w3a[bo][1] = v.y; w3a[bo][2] = v.z; w3a[bo][3] = v.w;
-    }
-    auto load_sb = [&](int sb) {
-      const int base = rb0 + sb * B6_SB;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int r = min(base + ra + k, rlast);
-#pragma unroll
-        for (int bo = 0; bo < 2; ++bo)
-          h2v[bo][k] = *reinterpret_cast<const float4*>(h2g + r * B6_H + oa + 128 * bo);
-        ga[k] = gprime(r);
-      }
-    };
-    auto stage_sb = [&](int sb) {
-      B6Buf& B = L.b[sb & 1];
-      const int base = rb0 + sb * B6_SB;
-#pragma unroll
-      for (int bo = 0; bo < 2; ++bo) {
-        __bf16 m[4][4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const bool ok = base + ra + k < rows && sb < B6_NSB;
-          const float g = ok ? ga[k] : 0.f;
-          const float hv[4] = {h2v[bo][k].x, h2v[bo][k].y, h2v[bo][k].z, h2v[bo][k].w};
-          bf16x4 mv;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bool on = ok && hv[e] > 0.f;
-            m[k][e] = on ? (__bf16)1.f : (__bf16)0.f;
-            mv[e] = m[k][e];
-            if (!(PROBE & 4)) {
-              s_db2[bo][e] += (double)(on ? g * w3a[bo][e] : 0.f);
-              s_dw3[bo][e] += (double)(g * (ok ? hv[e] : 0.f));
-            }
-          }
-          if (bo == 0 && t2 < 8) s_db3 += (double)g;
-          *reinterpret_cast<bf16x4*>(&B.mro[(ra + k) * B6_LRO + oa + 128 * bo]) = mv;
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          bf16x4 mv;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) mv[k] = m[k][e];
-          *reinterpret_cast<bf16x4*>(&B.mor[(oa + 128 * bo + e) * B6_LR + ra]) = mv;
-        }
-      }
-    };
-    load_sb(0);
-    stage_sb(0);
-    load_sb(1);
     f32x16 R[4];  // R[2 ob + bi]: o block ob0 + 32 ob, unit block 32 bi
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -367,8 +380,8 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
     for (int bo = 0; bo < 2; ++bo)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        hs[((t2 * 2 + bo) * 2 + 0) * 4 + e] = s_db2[bo][e];
-        hs[((t2 * 2 + bo) * 2 + 1) * 4 + e] = s_dw3[bo][e];
+        hs[((t2 * 2 + bo) * 2 + 0) * 4 + e] = (double)s_db2[bo][e];
+        hs[((t2 * 2 + bo) * 2 + 1) * 4 + e] = (double)s_dw3[bo][e];
       }
     if (t2 < 8) db3s[t2] = s_db3;
   }
@@ -388,8 +401,8 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
     s1 += __shfl_xor(s1, 32, 64);
     if (lh == 0) d.db1[pc * B6_H + i0 + 32 * ib + li] = (float)s1;
   }
-  // db2 / dW3 of o = i0 + tt (this workgroup's quarter): the eight threads
-  // holding o's column (rows 4 v .. 4 v + 3), in order
+  // db2 / dW3 of o = i0 + tt (this workgroup's quarter): the eight dW2-wave
+  // threads holding o's column (rows 4 v .. 4 v + 3 of each sub-block), in order
   if (t >= 256 && t < 320) {
     const int tt = t - 256, o = i0 + tt;
     const int bo = o >> 7, oo = o & 127;

@@ -90,6 +90,13 @@ def q2_shape(net: EnsembleMLP) -> bool:
     return net.n_layers == 3 and s[1] == 256 and s[2] == 256 and s[3] == 1 and s[0] <= 48
 
 
+def x6_wide_shape(net: EnsembleMLP) -> bool:
+    """[n_in <= 64, 256, 256, 1 < n_out <= 256]: d3a_mlp_fwd_x6's shape."""
+    s = net.sizes
+    return (net.n_layers == 3 and s[1] == 256 and s[2] == 256 and 1 < s[3] <= 256
+            and s[0] <= 64)
+
+
 def q2_ok(net: EnsembleMLP, rows: int) -> bool:
     """d3a_q2_bwd applies: two hidden layers of 256, one output, <= 48 inputs,
     a large pass (per-layer GEMMs win on the 100-512-row passes)."""
@@ -215,6 +222,9 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         if (not bf16 and not small and ops.CRITIC_GEMM == "x6" and q2_shape(net)
                 and (n + (d.aux_rows if d.aux_rows else 0)) * C >= 8192):
             entry = "d3a_q2_fwd_x6"  # the q2_fwd pass, fp32-accurate split-bf16
+        elif (not bf16 and not small and ops.CRITIC_GEMM == "x6" and x6_wide_shape(net)
+              and out_parts is None and not d.aux_rows and n * C >= 8192):
+            entry = "d3a_mlp_fwd_x6"  # wide head (e.g. BCQ's target QR critics)
         ops.call_desc(entry, d)
         if aux is not None:
             forward(net, aux[0], aux[1], True, aux[2], aux[3], keep_h=False)

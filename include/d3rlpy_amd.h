@@ -339,6 +339,14 @@ int d3a_q2_bwd_bf16(const d3a_q2_bwd_desc* d, void* stream);
  * encoders.py:265-275, 328-339 and mean_q_function.py:255-256. */
 int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* d, void* stream);
 int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* d, void* stream);
+/* The same split-bf16 forward for a wide head, [n_in <= 64, 256, 256,
+ * n_out <= 256] (csrc/mlp_x6.hip): d3a_mlp_fwd's contract without the aux pass
+ * and parts; e.g. BCQ's target QR critics over B*N sampled actions
+ * (bcq_impl.py:215-226, qr_q_function.py:97-161). */
+int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* d, void* stream);
+/* Diagnostic (synchronous, not for graphs): the phase-boundary s_memtime
+ * stamps of the last d3a_q2_fwd_x6 launch built with D3A_X6_PROBE bit 4. */
+int d3a_x6_stamps(unsigned long long* dst, int n);
 
 /* ---- optimiser and target networks ------------------------------------- */
 

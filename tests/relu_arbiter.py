@@ -213,6 +213,13 @@ def cql_critic_arbiter(label: str, make_oracle, sd0, tb, nz, g_hip: Dict[str, to
     g64 = critic_stage(o64, tb64, nz64, fh)
     flips, worst_tie = fh.tie_report()
     oflips, oworst = fa.tie_report()
+    # do HIP and the fp32 oracle take the same decisions everywhere?
+    orec = f32.recorded_masks()
+    same = all(torch.equal(hip_masks[c][kind][l] if kind == "data" else hip_masks[c][kind][k][l],
+                           orec[c][kind][l] if kind == "data" else orec[c][kind][k][l])
+               for c in range(len(orec)) for kind in ("data", "blocks")
+               for k in (range(1) if kind == "data" else range(3))
+               for l in range(len(orec[c]["data"])))
     assert worst_tie <= TIE_TOL, (label, flips, worst_tie)
     worst, worst_ratio = 0.0, 0.0
     for k, r64 in g64.items():
@@ -225,8 +232,8 @@ def cql_critic_arbiter(label: str, make_oracle, sd0, tb, nz, g_hip: Dict[str, to
         worst = max(worst, e_hip)
         worst_ratio = max(worst_ratio, e_hip / bar)
     info = dict(worst=worst, worst_ratio=worst_ratio, hip_flips=flips, hip_tie=worst_tie,
-                oracle_flips=oflips, oracle_tie=oworst)
+                oracle_flips=oflips, oracle_tie=oworst, same_decisions=same)
     print(f"  {label}: critic grads within {worst:.1e} of fp64 with HIP's ReLU decisions "
           f"({flips} decisions differ from the exact sign, max |z|/scale {worst_tie:.1e}; the "
-          f"fp32 oracle: {oflips}, {oworst:.1e})")
+          f"fp32 oracle: {oflips}, {oworst:.1e}; HIP and the oracle decide alike: {same})")
     return o64, info

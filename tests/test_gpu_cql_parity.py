@@ -57,12 +57,11 @@ CASES = {
     # hopper-medium-v0): hidden [256, 256, 256], alpha_learning_rate 0 (no
     # update_alpha: cql.py:244-247, so the critic pass starts at the critic
     # set's rows), conservative_weight 10, batch 256, N 10
-    # The 23.8 M critic ReLU decisions of a step here include near-ties the two
-    # fp32 implementations put on different sides (step 0 of this seed: one
-    # layer-1 unit of critic 0, 5.5e-4 on its weight gradient), so the critic
-    # gradients are decided by the ReLU-decision-aware fp64 arbiter
-    # (relu_arbiter.py) instead of the HIP-vs-oracle bar
-    "repro_hopper": dict(D=11, A=3, hidden=[256, 256, 256], N=10, B=256, arbiter=True,
+    # (the 23.8 M critic ReLU decisions of a step here include near-ties the two
+    # fp32 implementations put on different sides -- step 0 of this seed: one
+    # layer-1 unit of critic 0, 5.5e-4 on its weight gradient -- decided by the
+    # ReLU-decision-aware fp64 arbiter every case goes through)
+    "repro_hopper": dict(D=11, A=3, hidden=[256, 256, 256], N=10, B=256,
                          kw=dict(alpha_learning_rate=0.0, conservative_weight=10.0)),
 }
 
@@ -79,7 +78,7 @@ def _check_metrics(m_hip, m_orc):
 
 
 def _compare_step(case, step, impl, orc, m_hip, m_orc, cgrads, pgrads, A, grad_tol, sd0=None,
-                  critic_arbitrated=False):
+                  critic_arbitrated=False, same_decisions=True):
     """Metrics within 1e-5, gradients within ``grad_tol`` of the oracle, targets
     and log_temp / log_alpha within 1e-5 / 1e-6, and every online parameter
     entry within 1e-5 of the oracle or -- entry by entry -- Adam from the
@@ -115,8 +114,10 @@ def _compare_step(case, step, impl, orc, m_hip, m_orc, cgrads, pgrads, A, grad_t
     assert abs(float(impl.log_alpha.item()) - float(orc._log_alpha().item())) <= 1e-6
     assert perr <= grad_tol, perr
     # (critic_arbitrated: the caller checked the critic gradients against fp64
-    # with HIP's ReLU decisions, tests/relu_arbiter.py)
-    assert critic_arbitrated or gerr <= grad_tol, gerr
+    # with HIP's ReLU decisions, tests/relu_arbiter.py; where HIP and the fp32
+    # oracle take the same decisions everywhere the two fp32 evaluations must
+    # also agree directly)
+    assert (critic_arbitrated and not same_decisions) or gerr <= grad_tol, gerr
     assert targ_abs <= 1e-5, targ_abs
     if sd0 is None:
         assert perr_abs <= 1e-5, perr_abs
@@ -177,16 +178,17 @@ def test_cql_update_parity(case):
         m_orc, cgrads, pgrads = _oracle_step(orc, Batch.from_numpy(*arrs), nz, A)
         m_hip = impl.update_step(HostBatch(*arrs), noise=noise_dict(nz))
         torch.cuda.synchronize()
-        if cfg.get("arbiter"):
-            from arbiter_helpers import hip_grads
-            from relu_arbiter import cql_critic_arbiter, hip_critic_masks
-            cql_critic_arbiter(f"[{case}] step {step}",
-                               lambda: make_oracle(D, A, H, N, C=C, seed=0, **kw), sd0,
-                               Batch.from_numpy(*arrs), nz,
-                               hip_grads(impl._critic_refs(), impl.critic_grad),
-                               hip_critic_masks(impl._last_ws()), B, N)
+        # every case through the ReLU-decision-aware fp64 arbiter; the direct
+        # HIP-vs-oracle bar applies where both take the same ReLU decisions
+        from arbiter_helpers import hip_grads
+        from relu_arbiter import cql_critic_arbiter, hip_critic_masks
+        _, info = cql_critic_arbiter(f"[{case}] step {step}",
+                                     lambda: make_oracle(D, A, H, N, C=C, seed=0, **kw), sd0,
+                                     Batch.from_numpy(*arrs), nz,
+                                     hip_grads(impl._critic_refs(), impl.critic_grad),
+                                     hip_critic_masks(impl._last_ws()), B, N)
         _compare_step(case, step, impl, orc, m_hip, m_orc, cgrads, pgrads, A, grad_tol=2e-5,
-                      sd0=sd0, critic_arbitrated=bool(cfg.get("arbiter")))
+                      sd0=sd0, critic_arbitrated=True, same_decisions=info["same_decisions"])
 
 
 def test_cql_trajectory_drift():

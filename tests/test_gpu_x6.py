@@ -241,3 +241,66 @@ def test_q2_x6_rejects_bad_shapes():
     f.n_in, f.n_hidden, f.H, f.n_out = 64, 2, 256, 1
     with pytest.raises(RuntimeError, match="n_in <= 48"):
         ops.call_desc("d3a_q2_fwd_x6", f)
+
+
+@pytest.mark.parametrize("rows,n_in,n_out,keep", [(25600, 23, 200, False), (1000, 23, 6, True),
+                                                  (257, 64, 256, True), (77, 33, 1 + 32, False)])
+def test_mlp_fwd_x6_wide_head_vs_fp64(rows, n_in, n_out, keep):
+    """d3a_mlp_fwd_x6 ([n_in <= 64, 256, 256, n_out <= 256]; the K3 target QR
+    critics are the first case) against fp64, per layer relative to the
+    layer's rounding scale, on the kernel's own fp32 inputs to each layer."""
+    dev = torch.device("cuda")
+    C = 2
+    gen = torch.Generator().manual_seed(rows + n_out)
+    sizes = [n_in, 256, 256, n_out]
+    Ws = [(torch.randn(C, sizes[l + 1], sizes[l], generator=gen) / np.sqrt(sizes[l])).to(dev)
+          for l in range(3)]
+    bs = [(torch.randn(C, sizes[l + 1], generator=gen) * 0.1).to(dev) for l in range(3)]
+    ldx = (n_in + 3) // 4 * 4
+    x = torch.randn(rows, ldx, generator=gen).to(dev)
+    flat = torch.cat([W.reshape(-1) for W in Ws] + [b.reshape(-1) for b in bs])
+    offs, o = [], 0
+    for W in Ws:
+        offs.append(o)
+        o += W.numel()
+    boffs = []
+    for b in bs:
+        o = (o + 3) // 4 * 4
+        boffs.append(o)
+        o += b.numel()
+    buf = torch.zeros(o + 4, device=dev)
+    for W, of in zip(Ws, offs):
+        buf[of:of + W.numel()] = W.reshape(-1)
+    for b, of in zip(bs, boffs):
+        buf[of:of + b.numel()] = b.reshape(-1)
+    h = [torch.full((C, rows, 256), float("nan"), device=dev) for _ in range(2)]
+    out = torch.full((C, rows, n_out), float("nan"), device=dev)
+    d = N.MlpFwdDesc()
+    d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
+    d.n_in, d.n_hidden, d.H, d.n_out = n_in, 2, 256, n_out
+    for l in range(3):
+        d.W[l], d.b[l] = buf.data_ptr() + 4 * offs[l], buf.data_ptr() + 4 * boffs[l]
+        d.sW[l], d.sb[l] = sizes[l + 1] * sizes[l], sizes[l + 1]
+    for l in range(2):
+        d.h[l] = h[l].data_ptr() if keep else None
+    d.sh = rows * 256
+    d.out, d.sout, d.ldout = out.data_ptr(), rows * n_out, n_out
+    d.r0, d.rows, d.C, d.h_from = 0, rows, C, 0
+    ops.call_desc("d3a_mlp_fwd_x6", d)
+    torch.cuda.synchronize()
+    assert not torch.isnan(out).any()
+    hs, sc = _fwd64(x[:, :n_in], Ws, bs)
+    if keep:
+        h0, h1 = h[0].double(), h[1].double()
+        e0 = float(((h0 - hs[0]).abs() / sc[0]).max())
+        z1 = (h0 @ Ws[1].double().transpose(1, 2) + bs[1].double().unsqueeze(1)).clamp_min(0)
+        s1 = h0.abs() @ Ws[1].double().abs().transpose(1, 2) + bs[1].double().abs().unsqueeze(1)
+        e1 = float(((h1 - z1).abs() / s1).max())
+        zq = h1 @ Ws[2].double().transpose(1, 2) + bs[2].double().unsqueeze(1)
+        sq = h1.abs() @ Ws[2].double().abs().transpose(1, 2) + bs[2].double().abs().unsqueeze(1)
+        eq = float(((out.double() - zq).abs() / sq).max())
+        print(f"x6 wide forward vs fp64 (rounding scale): h0 {e0:.1e} h1 {e1:.1e} out {eq:.1e}")
+        assert e0 < SCALE_BAR and e1 < SCALE_BAR and eq < SCALE_BAR, (e0, e1, eq)
+    rel = float((out.double() - hs[2]).abs().max() / hs[2].abs().max())
+    print(f"x6 wide forward vs fp64 end to end: {rel:.1e}")
+    assert rel < 1e-5, rel
