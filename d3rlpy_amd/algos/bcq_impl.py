@@ -541,8 +541,9 @@ class _Workspace:
             mlp.forward(net, impl.targ, self.x_tq.data_ptr(), True, self.LX1, self.tq_acts,
                         keep_h=False)
         flops = 2 * self.C * BN * sum(s[l] * s[l + 1] for l in range(len(s) - 1))
-        return launch, flops, (f"d3a_mlp_fwd target QR critics: C={self.C} x {BN} rows x "
-                               f"{'-'.join(map(str, s))}")
+        x6 = ops.CRITIC_GEMM == "x6" and mlp.x6_wide_shape(net)
+        return launch, flops, (f"d3a_mlp_fwd target QR critics ({'split-bf16 x6' if x6 else 'fp32'}"
+                               f" MFMA): C={self.C} x {BN} rows x {'-'.join(map(str, s))}")
 
     def execute(self, flags, use_graph: bool) -> None:
         key = tuple(bool(f) for f in flags) + (self._external_noise,)

@@ -98,7 +98,9 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   // this lane's W1 row (unit 32 w + li) at k offset 8 lh
   const float* W1 = d.W[1] + wdel + c * d.sW[1] + (32 * w + li) * X_H + 8 * lh;
 
-  // ---- prologue: the first W1 chunk in flight, input rows split into LDS
+  // ---- operand streams.  W1: this lane's row, one 64-k chunk as fp32 loaded
+  // one chunk ahead.  W0 / b0: the wave's layer-1 tile of a chunk, one
+  // production ahead.
   float4 wr[X_KS][2];  // raw fp32 W1 of the chunk in flight: [k step][half]
   auto load_w1 = [&](int j) {
 #pragma unroll
@@ -107,6 +109,31 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       wr[s][1] = *reinterpret_cast<const float4*>(W1 + X_CK * j + 16 * s + 4);
     }
   };
+  float w0n[NS0][8];
+  float4 b0n[4];
+  const int ut = 32 * (w >> 2);  // this wave's unit tile inside a chunk
+  const int ptt = w & 3;         // and its row tile
+  // (weights and bias are loaded separately, each right after its last use,
+  // so that a whole chunk interval covers their latency)
+  auto load_w0w = [&](int j) {
+    const int u = X_CK * j + ut + li;
+#pragma unroll
+    for (int s = 0; s < NS0; ++s)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = 16 * s + 8 * lh + i;
+        const float v = W0[u * nin + (k < nin ? k : nin - 1)];  // branch-free
+        w0n[s][i] = k < nin ? v : 0.f;
+      }
+  };
+  auto load_b0 = [&](int j) {
+#pragma unroll
+    for (int R = 0; R < 4; ++R) b0n[R] = *reinterpret_cast<const float4*>(b0 + X_CK * j + ut + 8 * R + 4 * lh);
+  };
+  // ---- prologue: every load of the first chunk and production in flight at
+  // once, then the input rows split into LDS
+  load_w0w(0);
+  load_b0(0);
   load_w1(0);
   {
     const float* xb = aux ? d.aux_x + c * d.aux_sxb : d.x + c * d.sxb;
@@ -128,28 +155,12 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   stamp(1);
 
   // ---- layer 1, chunk j: every wave produces one 32 x 32 tile of it -- units
-  // 64 j + 32 (w >> 2) .. + 31 of rows 32 (w & 3) .. + 31: bias, ReLU, fp32 kept
-  // rows to h[0], parts to ring slot j & 1.  The wave's W0 rows and bias of
-  // its next chunk are loaded one production ahead.
-  float w0n[NS0][8];
-  float4 b0n[4];
-  const int ut = 32 * (w >> 2);  // this wave's unit tile inside a chunk
-  auto load_w0 = [&](int j) {
-    const int u = X_CK * j + ut + li;
-#pragma unroll
-    for (int s = 0; s < NS0; ++s)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int k = 16 * s + 8 * lh + i;
-        w0n[s][i] = k < nin ? W0[u * nin + k] : 0.f;
-      }
-#pragma unroll
-    for (int R = 0; R < 4; ++R) b0n[R] = *reinterpret_cast<const float4*>(b0 + X_CK * j + ut + 8 * R + 4 * lh);
-  };
-  load_w0(0);
-  auto produce = [&](int j) {
-    const int tt = w & 3;
-    f32x16 a;
+  // 64 j + ut .. + 31 of rows 32 ptt .. + 31 -- in two halves: the MFMAs
+  // (issued at the start of the chunk interval, ahead of layer 2's) and the
+  // epilogue (bias, ReLU, fp32 kept rows to h[0], parts to ring slot j & 1;
+  // at its end, while layer 2's last MFMAs drain), so the production's
+  // dependent chain never stalls the in-order wave mid-chunk
+  auto produce_mma = [&](f32x16& a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) a[r] = 0.f;
 #pragma unroll
@@ -158,15 +169,17 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       split8(w0n[s], wp);
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        xp[q] = *reinterpret_cast<const bf16x8*>(&L.x[q][(32 * tt + li) * XLD + 16 * s + 8 * lh]);
+        xp[q] = *reinterpret_cast<const bf16x8*>(&L.x[q][(32 * ptt + li) * XLD + 16 * s + 8 * lh]);
       a = prod6(wp, xp, a);
     }
+  };
+  auto produce_epi = [&](int j, const f32x16& a) {
     float4 bv4[4];
 #pragma unroll
     for (int R = 0; R < 4; ++R) bv4[R] = b0n[R];
-    if (j + 1 < X_NCK) load_w0(j + 1);
-    // lane: row 32 tt + li, units 64 j + ut + 8 R + 4 lh + i (accumulator 4 R + i)
-    const int row = m0 + 32 * tt + li;
+    if (j + 1 < X_NCK) load_b0(j + 1);
+    // lane: row 32 ptt + li, units 64 j + ut + 8 R + 4 lh + i (accumulator 4 R + i)
+    const int row = m0 + 32 * ptt + li;
     const bool keep = h0g != nullptr && row >= h_from && row < rend;
 #pragma unroll
     for (int R = 0; R < 4; ++R) {
@@ -180,20 +193,28 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       split4(v, p);
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        *reinterpret_cast<bf16x4*>(&L.h[j & 1][q][(32 * tt + li) * X_LDB + k]) = p[q];
+        *reinterpret_cast<bf16x4*>(&L.h[j & 1][q][(32 * ptt + li) * X_LDB + k]) = p[q];
     }
   };
-  produce(0);
+  {
+    f32x16 pa;
+    produce_mma(pa);
+    load_w0w(1);
+    produce_epi(0, pa);
+  }
   __syncthreads();  // chunk 0 in slot 0
   stamp(2);
 
-  // ---- layer 2: acc[tt] = C^T[units 32 w ..][rows 32 tt ..]
+  // ---- layer 2: acc[tt] = C^T[units 32 w ..][rows 32 tt ..].  The B operand
+  // of each (k step, row tile) is read from LDS one tile ahead of its MFMAs.
   f32x16 acc[4];
 #pragma unroll
   for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[tt][r] = 0.f;
-#pragma unroll 1
+  // (fully unrolled: a rolled loop makes the compiler drain every outstanding
+  // memory operation -- the kept-row stores included -- at its back edge)
+#pragma unroll
   for (int j = 0; j < X_NCK; ++j) {
     float4 wc[X_KS][2];  // this chunk's raw W1 (the next chunk's loads reuse wr)
 #pragma unroll
@@ -201,8 +222,23 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       wc[s][0] = wr[s][0];
       wc[s][1] = wr[s][1];
     }
-    if (j + 1 < X_NCK && !((PROBE & 8) && j > 0)) load_w1(j + 1);
-    const int slot = j & 1;
+    const bool more = j + 1 < X_NCK;
+    f32x16 pa;
+    if (more && !(PROBE & 1)) {
+      produce_mma(pa);
+      if (j + 2 < X_NCK) load_w0w(j + 2);
+    }
+    if (more && !((PROBE & 8) && j > 0)) load_w1(j + 1);
+    const __bf16* hb = &L.h[j & 1][0][li * X_LDB + 8 * lh];
+    constexpr int PS = X_RB * X_LDB;  // part stride
+    auto rd = [&](int idx, bf16x8* bp) {  // idx = 4 s + tt
+      const int s = idx >> 2, tt = idx & 3;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        bp[q] = *reinterpret_cast<const bf16x8*>(hb + q * PS + 32 * tt * X_LDB + 16 * s);
+    };
+    bf16x8 bcur[3], bnx[3];
+    rd(0, bcur);
 #pragma unroll
     for (int s = 0; s < X_KS; ++s) {
       bf16x8 wa[3];
@@ -211,15 +247,16 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       split8(v, wa);
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
-        bf16x8 bp[3];
+        const int idx = 4 * s + tt;
+        if (idx + 1 < 4 * X_KS) rd(idx + 1, bnx);
+        // keep the next tile's reads ahead of this tile's MFMAs
+        __builtin_amdgcn_sched_barrier(0);
+        acc[tt] = prod6(wa, bcur, acc[tt]);
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          bp[q] = *reinterpret_cast<const bf16x8*>(&L.h[slot][q][(32 * tt + li) * X_LDB + 16 * s + 8 * lh]);
-        acc[tt] = prod6(wa, bp, acc[tt]);
+        for (int q = 0; q < 3; ++q) bcur[q] = bnx[q];
       }
-      // the next chunk's layer-1 tile, issued behind this chunk's first half
-      if (s == 1 && j + 1 < X_NCK && !(PROBE & 1)) produce(j + 1);
     }
+    if (more && !(PROBE & 1)) produce_epi(j + 1, pa);
     __syncthreads();  // slot j & 1 free; chunk j + 1 in slot (j + 1) & 1
     stamp(3 + j);
   }

@@ -114,10 +114,10 @@ def _compare_step(case, step, impl, orc, m_hip, m_orc, cgrads, pgrads, A, grad_t
     assert abs(float(impl.log_alpha.item()) - float(orc._log_alpha().item())) <= 1e-6
     assert perr <= grad_tol, perr
     # (critic_arbitrated: the caller checked the critic gradients against fp64
-    # with HIP's ReLU decisions, tests/relu_arbiter.py; where HIP and the fp32
-    # oracle take the same decisions everywhere the two fp32 evaluations must
-    # also agree directly)
-    assert (critic_arbitrated and not same_decisions) or gerr <= grad_tol, gerr
+    # with HIP's ReLU decisions, tests/relu_arbiter.py -- the criterion, since
+    # the HIP-vs-oracle distance printed above also carries the fp32 oracle's
+    # own error: 3.7e-5 of fp64 on a head weight of the reproduction config)
+    assert critic_arbitrated or gerr <= grad_tol, gerr
     assert targ_abs <= 1e-5, targ_abs
     if sd0 is None:
         assert perr_abs <= 1e-5, perr_abs
@@ -292,6 +292,7 @@ def test_cql_grad_accuracy_vs_fp64(shape):
     impl = make_impl(D, A, H, N, **kw)
     copy_oracle_to_impl(orc, impl)
     sd0 = impl.get_state_dict()
+    sdo = copy.deepcopy(oracle_state(orc))
     rs = np.random.RandomState(0)
     gen = torch.Generator().manual_seed(1)
     arrs = make_batch(rs, B, D, A)
@@ -321,11 +322,27 @@ def test_cql_grad_accuracy_vs_fp64(shape):
     for c in range(2):
         for l in range(impl.critic.n_layers):
             for k, nm in enumerate((impl.critic.wname(l), impl.critic.bname(l))):
-                g_hip = impl.critic_grad(nm)[c]
-                e_hip = max_rel(g_hip, grads[1][c][l][k])
                 e_orc = max_rel(grads[0][c][l][k], grads[1][c][l][k])
-                print(f"critic {c} {nm}: hip-vs-fp64 {e_hip:.1e}  oracle32-vs-fp64 {e_orc:.1e}")
-                worst_hip, worst_orc = max(worst_hip, e_hip), max(worst_orc, e_orc)
+                print(f"critic {c} {nm}: oracle32-vs-fp64 {e_orc:.1e}")
+                worst_orc = max(worst_orc, e_orc)
+    # HIP's critic gradients against fp64 evaluated with HIP's own ReLU
+    # decisions (tests/relu_arbiter.py): a decision within fp32 rounding of
+    # zero may fall either way -- every one that differs from the exact sign
+    # must be such a tie -- and the rest of the difference is rounding
+    from relu_arbiter import (TIE_TOL, CriticReluForcer, critic_stage, hip_critic_masks,
+                              oracle_from_state)
+    o64h = oracle_from_state(lambda: make_oracle(D, A, H, N, seed=0, **kw), sdo, torch.float64)
+    fh = CriticReluForcer(o64h._q_func, B, N, masks=hip_critic_masks(impl._last_ws()))
+    g64h = critic_stage(o64h, tb64, nz64, fh)
+    flips, tie = fh.tie_report()
+    print(f"HIP critic ReLU decisions differing from the exact sign: {flips} (max |z|/scale "
+          f"{tie:.1e})")
+    assert tie <= TIE_TOL, (flips, tie)
+    g_hip = hip_grads(impl._critic_refs(), impl.critic_grad)
+    for k, r64 in g64h.items():
+        e_hip = max_rel(g_hip[k], r64)
+        print(f"critic {k}: hip-vs-fp64(HIP decisions) {e_hip:.1e}")
+        worst_hip = max(worst_hip, e_hip)
     assert worst_hip <= 1e-5, (worst_hip, worst_orc)
     sd1 = impl.get_state_dict()
     for key, refs, getter, lr in (("_q_func", impl._critic_refs(), impl.critic_grad, 3e-4),
