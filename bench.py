@@ -492,12 +492,15 @@ def main():
     ap.add_argument("--algo", choices=sorted(WORKLOADS), default="cql",
                     help="cql = the BASELINE.json headline (K2); td3bc = K1 shapes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", choices=["fp32", "bf16", "sbf16x6"], default="fp32",
-                    help="bf16: the critic-ensemble forward / backward (the 7,936 + 7,680-row "
-                         "critic pass) with bf16 operands and fp32 accumulation "
-                         "(d3a_q2_fwd_bf16 / d3a_q2_bwd_bf16), a throughput line, never the "
-                         "headline; sbf16x6: the large input-gradient GEMMs on the bf16 "
-                         "matrix cores with hi/mid/lo split operands (fp32-accurate)")
+    ap.add_argument("--precision", choices=["fp32", "bf16", "bf16h", "sbf16x6"], default="fp32",
+                    help="bf16: the critic-ensemble forward (the 15,616 + 256-row critic pass) "
+                         "with one bf16 part per operand and fp32 accumulation (d3a_q2_fwd_x1), "
+                         "its backward the mask-factored split-bf16 d3a_q2_bwd_x6 -- a "
+                         "throughput line, never the headline; bf16h: round 3's line (every "
+                         "operand of forward and backward one bf16 part, bf16 kept activations: "
+                         "d3a_q2_fwd_bf16 / d3a_q2_bwd_bf16); sbf16x6: the large input-gradient "
+                         "GEMMs on the bf16 matrix cores with hi/mid/lo split operands "
+                         "(fp32-accurate)")
     ap.add_argument("--critic-gemm", choices=["fp32", "x6"], default=None,
                     help="GEMM arithmetic of the [n_in, 256, 256, 1] critic passes at fp32 "
                          "accuracy: fp32 = v_mfma_f32_32x32x2_f32; x6 = exact three-way split-bf16 "
@@ -523,9 +526,9 @@ def main():
 
     import torch
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    if args.precision == "bf16":
+    if args.precision in ("bf16", "bf16h"):
         from d3rlpy_amd import ops as _ops
-        _ops.set_critic_precision("bf16")
+        _ops.set_critic_precision(args.precision)
     if args.precision == "sbf16x6":
         from d3rlpy_amd import ops as _ops
         _ops.set_sbf16(6)
@@ -591,14 +594,15 @@ def main():
     # the fp32-accurate split-bf16 critic kernels (CRITIC_GEMM "x6") run six bf16
     # MFMA products per fp32 product: their ceiling is the bf16 peak / 6
     x6 = _ops.CRITIC_GEMM == "x6" and args.precision == "fp32" and "x6" in kdesc
-    peak_tflops = 2500.0 if args.precision == "bf16" else (2500.0 / 6 if x6 else 157.3)
+    bf16 = args.precision in ("bf16", "bf16h")
+    peak_tflops = 2500.0 if bf16 else (2500.0 / 6 if x6 else 157.3)
     achieved = kflops / kern_s / 1e12
     traffic = None
     if args.traffic_json is None:
         prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
         # the PMC summary of THIS line's dominant kernel: the bf16 and x6 lines
         # have their own kernels and files (r04_pmc_traffic_<algo>_<suffix>.json)
-        suffix = "_bf16" if args.precision == "bf16" else "_x6" if x6 else ""
+        suffix = f"_{args.precision}" if bf16 else "_x6" if x6 else ""
         rounds = (4, 3, 2, 1) if not suffix else (4,)
         args.traffic_json = next((p for p in (os.path.join(prof, f"r0{r}_pmc_traffic_{args.algo}"
                                                            f"{suffix}.json")
@@ -681,8 +685,12 @@ def main():
         "dtype": ("fp32 (critic GEMMs fp32-accurate: exact three-way split-bf16 operands, "
                   "fp32 accumulation on the bf16 matrix cores)" if x6 else "fp32")
                  if args.precision == "fp32" else
-                 "bf16 (critic-ensemble GEMM operands; fp32 accumulation, losses, optimiser)"
+                 "bf16 (critic-ensemble forward operands one bf16 part; backward split-bf16 "
+                 "mask-factored; fp32 accumulation, losses, optimiser)"
                  if args.precision == "bf16" else
+                 "bf16 (critic-ensemble GEMM operands and kept activations; fp32 accumulation, "
+                 "losses, optimiser)"
+                 if args.precision == "bf16h" else
                  "fp32 (input-gradient GEMMs: split-bf16 x6 on bf16 MFMA)",
         "data": (f"synthetic (D4RL {shape} shapes, {args.transitions} transitions, "
                  "HBM-resident)" if shape != "atari" else

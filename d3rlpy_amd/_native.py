@@ -508,6 +508,7 @@ _SIGNATURES = {
     "d3a_q2_bwd_bf16": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
     "d3a_q2_fwd_x6": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_q2_bwd_x6": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
+    "d3a_q2_fwd_x1": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_mlp_fwd_x6": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_x6_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_td3_prep": (C.c_int, [C.POINTER(Td3PrepDesc), vp]),

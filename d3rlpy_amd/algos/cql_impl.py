@@ -460,7 +460,7 @@ class _Workspace:
         # critic / target / actor-critic activations
         # bf16 throughput line (ops.CRITIC_PRECISION): the critic pass's kept
         # activations in bf16 select the bf16 forward / backward kernels
-        bf16 = (ops.CRITIC_PRECISION == "bf16" and mlp.q2_shape(impl.critic)
+        bf16 = (ops.CRITIC_PRECISION == "bf16h" and mlp.q2_shape(impl.critic)
                 and mlp.q2_ok(impl.critic, 3 * NB + B))
         self.qacts = mlp.Acts.alloc(impl.critic, self.R, dev,
                                     dtype=torch.bfloat16 if bf16 else torch.float32)
@@ -670,7 +670,14 @@ class _Workspace:
                             h_from=3 * self.NB,
                             aux=(impl.targ, self.x_targ.data_ptr(), DA, self.tacts))
             flops = 2 * C * (R - r0 + B) * sum(s[l] * s[l + 1] for l in range(len(s) - 1))
-            gemm = "split-bf16 x6" if (ops.CRITIC_GEMM == "x6" and mlp.q2_shape(net)) else "fp32"
+            gemm = "fp32"
+            if mlp.q2_shape(net):
+                if self.qacts.h[0].dtype == torch.bfloat16:
+                    gemm = "bf16, bf16 kept activations"
+                elif ops.CRITIC_PRECISION == "bf16":
+                    gemm = "bf16 x1"
+                elif ops.CRITIC_GEMM == "x6":
+                    gemm = "split-bf16 x6"
             return launch, flops, (f"d3a_mlp_fwd critic ensemble ({gemm} MFMA): C={C} x "
                                    f"({R - r0} + {B} target) rows x {'-'.join(map(str, s))}")
         H, Hin = s[2], s[1]

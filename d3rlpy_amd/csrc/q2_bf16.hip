@@ -22,6 +22,7 @@
 #include "../../include/d3rlpy_amd.h"
 
 namespace d3a {
+void launch_q2x1_fwd(const d3a_mlp_fwd_desc& d, hipStream_t st);  // q2_x6.hip
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -595,7 +596,9 @@ extern "C" int d3a_q2_fwd_bf16(const d3a_mlp_fwd_desc* dp, void* stream) {
                     d.sh % 8 == 0,
                 "d3a_q2_fwd_bf16: bf16 activation buffers must be 16-byte aligned");
   const int64_t rmax = (d.r0 + d.rows) > d.aux_rows ? (d.r0 + d.rows) : d.aux_rows;
-  D3A_CHECK_ARG(rmax * B_H < (int64_t(1) << 31) && rmax * d.ldout < (int64_t(1) << 31),
+  D3A_CHECK_ARG(rmax * B_H < (int64_t(1) << 31) && rmax * d.ldout < (int64_t(1) << 31) &&
+                    (d.r0 + d.rows) * d.ldx < (int64_t(1) << 31) &&
+                    d.aux_rows * d.aux_ldx < (int64_t(1) << 31),
                 "d3a_q2_fwd_bf16: rows x row stride exceeds 2^31");
   if (d.rows == 0 && d.aux_rows == 0) return 0;
   const int64_t nb = (d.rows + B_RB - 1) / B_RB + (d.aux_rows + B_RB - 1) / B_RB;
@@ -606,7 +609,15 @@ extern "C" int d3a_q2_fwd_bf16(const d3a_mlp_fwd_desc* dp, void* stream) {
     const char* e = getenv("D3A_FWDB_PROBE");
     return e ? atoi(e) : 0;
   }();
-  if (probe && xl == 16) {
+  // default: the split-bf16 kernel's structure with one part (q2_x6.hip);
+  // D3A_FWDB_OLD=1 selects this file's round-3 kernel (A/B timing)
+  static const bool old = [] {
+    const char* e = getenv("D3A_FWDB_OLD");
+    return e && atoi(e) != 0;
+  }();
+  if (!old && !probe) {
+    launch_q2x1_fwd(d, st);
+  } else if (probe && xl == 16) {
     switch (probe) {
       case 1: hipLaunchKernelGGL((q2_fwd_bf16_kernel<16, 1>), grid, dim3(512), 0, st, d); break;
       case 2: hipLaunchKernelGGL((q2_fwd_bf16_kernel<16, 2>), grid, dim3(512), 0, st, d); break;

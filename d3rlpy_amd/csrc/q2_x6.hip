@@ -49,10 +49,10 @@ constexpr int X_NCK = X_H / X_CK;
 constexpr int X_KS = X_CK / 16;  // MFMA k steps per chunk
 constexpr int X_LDB = 72;   // bf16 row stride of a ring slot (144 B: conflict-free 16-B reads)
 
-template <int XL>
+template <int XL, int NP>
 struct X6FwdLds {
-  __bf16 h[2][3][X_RB * X_LDB];     // layer-1 chunk ring: slot, part, [row][k]
-  __bf16 x[3][X_RB * (XL + 8)];     // input rows, parts, zero-padded to XL
+  __bf16 h[2][NP][X_RB * X_LDB];    // layer-1 chunk ring: slot, part, [row][k]
+  __bf16 x[NP][X_RB * (XL + 8)];    // input rows, parts, zero-padded to XL
   float hp[8][X_RB];                // head partials [wave][row]
 };
 
@@ -61,13 +61,17 @@ struct X6FwdLds {
 // bit 3 the W1 reloads (chunk 0's registers reused); bit 4 (diagnostic build,
 // results right) records s_memtime stamps of wave 0 at the phase boundaries
 // into x6_stamps (read with d3a_x6_stamps)
+//
+// NP / HT: NP = 3 the exact split (fp32-accurate, kept activations fp32);
+// NP = 1, HT = __bf16 the bf16 throughput line's forward (d3a_q2_fwd_bf16's
+// contract: one bf16 rounding per operand, kept activations stored as bf16)
 __device__ unsigned long long x6_stamps[2048 * 10];
-template <int XL, int PROBE = 0>
+template <int XL, int PROBE = 0, int NP = 3, typename HT = float>
 __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   constexpr int XLD = XL + 8;
   constexpr int NS0 = XL / 16;  // layer-1 k steps
-  __shared__ __attribute__((aligned(16))) X6FwdLds<XL> L;
-  static_assert(sizeof(X6FwdLds<XL>) <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) X6FwdLds<XL, NP> L;
+  static_assert(sizeof(X6FwdLds<XL, NP>) <= 163840, "LDS");
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int li = lane & 31, lh = lane >> 5;
@@ -81,8 +85,19 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   const int64_t wdel = aux ? d.aux_wdelta : 0;
   float* const outp = aux ? d.aux_out + c * d.aux_sout : d.out + c * d.sout;
   const int nin = d.n_in;
-  float* const h0g = (!aux && d.h[0]) ? d.h[0] + c * d.sh : nullptr;
-  float* const h1g = (!aux && d.h[1]) ? d.h[1] + c * d.sh : nullptr;
+  HT* const h0g = (!aux && d.h[0]) ? reinterpret_cast<HT*>(d.h[0]) + c * d.sh : nullptr;
+  HT* const h1g = (!aux && d.h[1]) ? reinterpret_cast<HT*>(d.h[1]) + c * d.sh : nullptr;
+  // a kept run of four activations (16 bytes fp32, 8 bytes bf16)
+  auto put4 = [](HT* p, const float* v) {
+    if constexpr (sizeof(HT) == 4) {
+      *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      bf16x4 b;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[i] = (__bf16)v[i];
+      *reinterpret_cast<bf16x4*>(p) = b;
+    }
+  };
   const float* W0 = d.W[0] + wdel + c * d.sW[0];
   const float* b0 = d.b[0] + wdel + c * d.sb[0];
   const int wg = blockIdx.x + blockIdx.z * gridDim.x;
@@ -145,10 +160,10 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? xb[r * ldx + k4 + j] : 0.f;
-      bf16x4 p[3];
-      split4(v, p);
+      bf16x4 p[NP];
+      splitn4<NP>(v, p);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&L.x[q][m * XLD + k4]) = p[q];
+      for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x4*>(&L.x[q][m * XLD + k4]) = p[q];
     }
   }
   __syncthreads();  // x parts staged
@@ -165,12 +180,12 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     for (int r = 0; r < 16; ++r) a[r] = 0.f;
 #pragma unroll
     for (int s = 0; s < NS0; ++s) {
-      bf16x8 wp[3], xp[3];
-      split8(w0n[s], wp);
+      bf16x8 wp[NP], xp[NP];
+      splitn8<NP>(w0n[s], wp);
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < NP; ++q)
         xp[q] = *reinterpret_cast<const bf16x8*>(&L.x[q][(32 * ptt + li) * XLD + 16 * s + 8 * lh]);
-      a = prod6(wp, xp, a);
+      a = prodn<NP>(wp, xp, a);
     }
   };
   auto produce_epi = [&](int j, const f32x16& a) {
@@ -187,12 +202,11 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       const float4 bv = bv4[R];
       float v[4] = {fmaxf(a[4 * R + 0] + bv.x, 0.f), fmaxf(a[4 * R + 1] + bv.y, 0.f),
                     fmaxf(a[4 * R + 2] + bv.z, 0.f), fmaxf(a[4 * R + 3] + bv.w, 0.f)};
-      if (keep && !(PROBE & 4))
-        *reinterpret_cast<float4*>(h0g + row * X_H + X_CK * j + k) = make_float4(v[0], v[1], v[2], v[3]);
-      bf16x4 p[3];
-      split4(v, p);
+      if (keep && !(PROBE & 4)) put4(h0g + row * X_H + X_CK * j + k, v);
+      bf16x4 p[NP];
+      splitn4<NP>(v, p);
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < NP; ++q)
         *reinterpret_cast<bf16x4*>(&L.h[j & 1][q][(32 * ptt + li) * X_LDB + k]) = p[q];
     }
   };
@@ -234,26 +248,26 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     auto rd = [&](int idx, bf16x8* bp) {  // idx = 4 s + tt
       const int s = idx >> 2, tt = idx & 3;
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < NP; ++q)
         bp[q] = *reinterpret_cast<const bf16x8*>(hb + q * PS + 32 * tt * X_LDB + 16 * s);
     };
-    bf16x8 bcur[3], bnx[3];
+    bf16x8 bcur[NP], bnx[NP];
     rd(0, bcur);
 #pragma unroll
     for (int s = 0; s < X_KS; ++s) {
-      bf16x8 wa[3];
+      bf16x8 wa[NP];
       const float v[8] = {wc[s][0].x, wc[s][0].y, wc[s][0].z, wc[s][0].w,
                           wc[s][1].x, wc[s][1].y, wc[s][1].z, wc[s][1].w};
-      split8(v, wa);
+      splitn8<NP>(v, wa);
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
         const int idx = 4 * s + tt;
         if (idx + 1 < 4 * X_KS) rd(idx + 1, bnx);
         // keep the next tile's reads ahead of this tile's MFMAs
         __builtin_amdgcn_sched_barrier(0);
-        acc[tt] = prod6(wa, bcur, acc[tt]);
+        acc[tt] = prodn<NP>(wa, bcur, acc[tt]);
 #pragma unroll
-        for (int q = 0; q < 3; ++q) bcur[q] = bnx[q];
+        for (int q = 0; q < NP; ++q) bcur[q] = bnx[q];
       }
     }
     if (more && !(PROBE & 1)) produce_epi(j + 1, pa);
@@ -285,9 +299,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     const int row = m0 + 32 * tt + li;
     if (!(PROBE & 4) && h1g != nullptr && row >= h_from && row < rend) {
 #pragma unroll
-      for (int R = 0; R < 4; ++R)
-        *reinterpret_cast<float4*>(h1g + row * X_H + 32 * w + 8 * R + 4 * lh) =
-            make_float4(v[4 * R], v[4 * R + 1], v[4 * R + 2], v[4 * R + 3]);
+      for (int R = 0; R < 4; ++R) put4(h1g + row * X_H + 32 * w + 8 * R + 4 * lh, v + 4 * R);
     }
     float hs = v[0] * ww[0];
 #pragma unroll
@@ -365,6 +377,66 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
   else
     hipLaunchKernelGGL(q2x6_fwd_kernel<48>, grid, dim3(512), 0, st, d);
   D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
+  return 0;
+}
+
+// the bf16 throughput line's forward (d3a_q2_fwd_bf16, q2_bf16.hip): this
+// kernel with one bf16 part per operand and bf16 kept activations; the caller
+// has checked the descriptor
+namespace d3a {
+void launch_q2x1_fwd(const d3a_mlp_fwd_desc& d, hipStream_t st) {
+  const int64_t nb = (d.rows + X_RB - 1) / X_RB + (d.aux_rows + X_RB - 1) / X_RB;
+  const dim3 grid((unsigned)nb, 1, (unsigned)d.C);
+  const int xl = (d.n_in + 15) / 16 * 16;
+  if (xl == 16)
+    hipLaunchKernelGGL((q2x6_fwd_kernel<16, 0, 1, __bf16>), grid, dim3(512), 0, st, d);
+  else if (xl == 32)
+    hipLaunchKernelGGL((q2x6_fwd_kernel<32, 0, 1, __bf16>), grid, dim3(512), 0, st, d);
+  else
+    hipLaunchKernelGGL((q2x6_fwd_kernel<48, 0, 1, __bf16>), grid, dim3(512), 0, st, d);
+}
+}  // namespace d3a
+
+// the bf16 line's forward with fp32 kept activations (the backward that reads
+// them is the mask-factored split-bf16 d3a_q2_bwd_x6): one bf16 part per
+// operand, fp32 accumulation
+extern "C" int d3a_q2_fwd_x1(const d3a_mlp_fwd_desc* dp, void* stream) {
+  D3A_CHECK_ARG(dp, "d3a_q2_fwd_x1: null desc");
+  const d3a_mlp_fwd_desc& e = *dp;  // d3a_q2_fwd_x6's contract
+  D3A_CHECK_ARG(e.n_hidden == 2 && e.H == X_H && e.n_out == 1 && e.n_in >= 1 && e.n_in <= 48,
+                "d3a_q2_fwd_x1: needs [n_in <= 48, 256, 256, 1]");
+  D3A_CHECK_ARG(e.x && e.out && e.W[0] && e.W[1] && e.W[2] && e.b[0] && e.b[1] && e.b[2],
+                "d3a_q2_fwd_x1: null operand");
+  D3A_CHECK_ARG(e.C >= 1 && e.rows >= 0 && e.r0 >= 0 && e.h_from >= 0 && e.aux_rows >= 0,
+                "d3a_q2_fwd_x1: bad sizes");
+  auto a16 = [](const void* p, int64_t stride) {
+    return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && stride % 4 == 0;
+  };
+  D3A_CHECK_ARG(a16(e.W[1], e.sW[1]) && a16(e.b[0], e.sb[0]) && a16(e.b[1], e.sb[1]) &&
+                    a16(e.W[2], e.sW[2]),
+                "d3a_q2_fwd_x1: W1, b0, b1 and the head row must be 16-byte aligned");
+  D3A_CHECK_ARG((e.h[0] == nullptr || (reinterpret_cast<uintptr_t>(e.h[0]) & 15) == 0) &&
+                    (e.h[1] == nullptr || (reinterpret_cast<uintptr_t>(e.h[1]) & 15) == 0) &&
+                    e.sh % 4 == 0,
+                "d3a_q2_fwd_x1: kept activations must be 16-byte aligned rows of 256");
+  D3A_CHECK_ARG(e.aux_rows == 0 || (e.aux_x && e.aux_out && e.aux_wdelta % 4 == 0),
+                "d3a_q2_fwd_x1: aux pass needs aux_x, aux_out and a 16-byte aligned aux_wdelta");
+  D3A_CHECK_ARG((e.r0 + e.rows) * (int64_t)(e.ldout > X_H ? e.ldout : X_H) < (int64_t(1) << 31) &&
+                    (e.r0 + e.rows) * e.ldx < (int64_t(1) << 31) &&
+                    e.aux_rows * (int64_t)(e.aux_ldx > X_H ? e.aux_ldx : X_H) < (int64_t(1) << 31),
+                "d3a_q2_fwd_x1: rows x row stride exceeds 2^31");
+  if (e.rows == 0 && e.aux_rows == 0) return 0;
+  const int64_t nb = (e.rows + X_RB - 1) / X_RB + (e.aux_rows + X_RB - 1) / X_RB;
+  const dim3 grid((unsigned)nb, 1, (unsigned)e.C);
+  const hipStream_t st = (hipStream_t)stream;
+  const int xl = (e.n_in + 15) / 16 * 16;
+  if (xl == 16)
+    hipLaunchKernelGGL((q2x6_fwd_kernel<16, 0, 1, float>), grid, dim3(512), 0, st, e);
+  else if (xl == 32)
+    hipLaunchKernelGGL((q2x6_fwd_kernel<32, 0, 1, float>), grid, dim3(512), 0, st, e);
+  else
+    hipLaunchKernelGGL((q2x6_fwd_kernel<48, 0, 1, float>), grid, dim3(512), 0, st, e);
+  D3A_LAUNCH_CHECK("d3a_q2_fwd_x1");
   return 0;
 }
 

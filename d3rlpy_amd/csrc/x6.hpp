@@ -67,5 +67,33 @@ __device__ __forceinline__ f32x16 x3m(bf16x8 a, const bf16x8* b, f32x16 c) {
   return c;
 }
 
+// NP-part generalisations: NP = 3 is the exact split above (six products),
+// NP = 1 a single bf16 rounding per operand (one product: the bf16 line)
+template <int NP>
+__device__ __forceinline__ void splitn8(const float* x, bf16x8* p) {
+  if constexpr (NP == 3) {
+    split8(x, p);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p[0][i] = (__bf16)x[i];
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void splitn4(const float* x, bf16x4* p) {
+  if constexpr (NP == 3) {
+    split4(x, p);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p[0][i] = (__bf16)x[i];
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ f32x16 prodn(const bf16x8* a, const bf16x8* b, f32x16 c) {
+  if constexpr (NP == 3) return prod6(a, b, c);
+  else return mfma16(a[0], b[0], c);
+}
+
 }  // namespace x6
 }  // namespace d3a

@@ -219,8 +219,11 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             d.aux_out, d.aux_sout, d.aux_rows = aacts.out.data_ptr(), aacts.R * sizes[-1], aacts.R
             aux = None
         entry = "d3a_q2_fwd_bf16" if bf16 else "d3a_mlp_fwd"
-        if (not bf16 and not small and ops.CRITIC_GEMM == "x6" and q2_shape(net)
-                and (n + (d.aux_rows if d.aux_rows else 0)) * C >= 8192):
+        big_q2 = (not bf16 and not small and q2_shape(net)
+                  and (n + (d.aux_rows if d.aux_rows else 0)) * C >= 8192)
+        if big_q2 and ops.CRITIC_PRECISION == "bf16":
+            entry = "d3a_q2_fwd_x1"  # the bf16 line: one bf16 part per operand
+        elif big_q2 and ops.CRITIC_GEMM == "x6":
             entry = "d3a_q2_fwd_x6"  # the q2_fwd pass, fp32-accurate split-bf16
         elif (not bf16 and not small and ops.CRITIC_GEMM == "x6" and x6_wide_shape(net)
               and out_parts is None and not d.aux_rows and n * C >= 8192):
@@ -374,7 +377,7 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         d.dW3, d.db3 = gs.get(net.wname(2)).data_ptr(), gs.get(net.bname(2)).data_ptr()
         d.rows, d.n_in, d.C = n, sizes[0], C
         entry = "d3a_q2_bwd_bf16" if esz == 2 else "d3a_q2_bwd"
-        if esz == 4 and ops.CRITIC_GEMM == "x6":
+        if esz == 4 and (ops.CRITIC_GEMM == "x6" or ops.CRITIC_PRECISION == "bf16"):
             entry = "d3a_q2_bwd_x6"  # fp32-accurate split-bf16 (mask-factored)
         ops.call_desc(entry, d)
         return None

@@ -266,16 +266,19 @@ SBF16_W = os.environ.get("D3A_SBF16_W", "1") == "1"  # also the weight-gradient 
 
 
 # critic-ensemble precision of the large CQL critic passes: "fp32" (the
-# reference's; parity path) or "bf16" (throughput line: d3a_q2_fwd_bf16 /
-# d3a_q2_bwd_bf16, bf16 operands with fp32 accumulation, bf16 kept
-# activations).  Read when an Impl builds its pipeline workspace.
+# reference's; parity path), "bf16" (throughput line: the forward's operands
+# rounded to one bf16 part, d3a_q2_fwd_x1, fp32 kept activations; the backward
+# the mask-factored split-bf16 d3a_q2_bwd_x6, whose non-mask operands keep
+# three parts) or "bf16h" (round 3's line: d3a_q2_fwd_bf16 / d3a_q2_bwd_bf16,
+# every operand one bf16 part, bf16 kept activations).  Read when an Impl
+# builds its pipeline workspace and at each launch.
 CRITIC_PRECISION = os.environ.get("D3A_CRITIC_PRECISION", "fp32")
 
 
 def set_critic_precision(p: str) -> None:
     global CRITIC_PRECISION
-    if p not in ("fp32", "bf16"):
-        raise ValueError(f"critic precision must be fp32 or bf16, got {p!r}")
+    if p not in ("fp32", "bf16", "bf16h"):
+        raise ValueError(f"critic precision must be fp32, bf16 or bf16h, got {p!r}")
     CRITIC_PRECISION = p
 
 

@@ -339,6 +339,11 @@ int d3a_q2_bwd_bf16(const d3a_q2_bwd_desc* d, void* stream);
  * encoders.py:265-275, 328-339 and mean_q_function.py:255-256. */
 int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* d, void* stream);
 int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* d, void* stream);
+/* The bf16 throughput line's critic forward: d3a_q2_fwd_x6's contract (fp32
+ * kept activations) with one bf16 rounding per operand (fp32 accumulation);
+ * its backward is d3a_q2_bwd_x6 (ReLU-mask operands exact, the other operand
+ * split in three parts). */
+int d3a_q2_fwd_x1(const d3a_mlp_fwd_desc* d, void* stream);
 /* The same split-bf16 forward for a wide head, [n_in <= 64, 256, 256,
  * n_out <= 256] (csrc/mlp_x6.hip): d3a_mlp_fwd's contract without the aux pass
  * and parts; e.g. BCQ's target QR critics over B*N sampled actions
