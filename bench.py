@@ -547,6 +547,13 @@ def main():
     if ar_log is not None:
         ar_log["armed"] = False
     gpu_steps(algo, it, max(0, args.warmup - 1))
+    # the dominant kernel's average launch time (HIP events on its stream),
+    # taken here, right before the timed region: its ~200 back-to-back
+    # launches also hold the device at its loaded clock, so a short timed
+    # window (the driver's --steps 20 --warmup 5) does not start on a device
+    # still ramping from idle (profiles/r04_bench_window.jsonl)
+    wsp = next(iter(algo.impl._ws.values()))
+    kern_s, kflops, kdesc = measure_kernel(wsp, reps=200)
     torch.cuda.synchronize()
     _barrier(ws)
     wd.set()
@@ -580,8 +587,6 @@ def main():
     ci = names.index("critic_loss") if "critic_loss" in names else names.index("loss")
     finite = bool(np.isfinite(vals[:, ci]).all() and np.isfinite(vals[~np.isnan(vals)]).all())
 
-    wsp = next(iter(algo.impl._ws.values()))
-    kern_s, kflops, kdesc = measure_kernel(wsp)
     allreduce = measure_all_reduces(ar_log, ws) if ar_log is not None else None
     if rank != 0:
         if ws > 1:

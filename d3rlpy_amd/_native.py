@@ -269,6 +269,7 @@ class MlpFwdDesc(C.Structure):
         ("aux_wdelta", C.c_int64), ("aux_out", vp), ("aux_sout", C.c_int64),
         ("aux_rows", C.c_int64),
         ("parts", C.c_int32), ("s_part", C.c_int64),
+        ("row_mean", vp), ("s_mean", C.c_int64),
     ]
 
 
@@ -332,7 +333,7 @@ class BcqTargetDesc(C.Structure):
     _fields_ = [
         ("q", vp), ("target", vp),
         ("B", C.c_int32), ("N", C.c_int32), ("K", C.c_int32), ("C", C.c_int32),
-        ("lam", C.c_float),
+        ("lam", C.c_float), ("means", vp),
     ]
 
 

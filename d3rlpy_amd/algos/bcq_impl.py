@@ -495,6 +495,8 @@ class _Workspace:
 
         t = NAT.BcqTargetDesc()
         t.q, t.target = self.tq_acts.out.data_ptr(), self.target.data_ptr()
+        # the quantile means, when the target pass's epilogue forms them
+        self.tq_means = torch.zeros(C, BN, dtype=torch.float32, device=self.target.device)
         t.B, t.N, t.K, t.C, t.lam = B, N, K, C, impl._lam
         self.target_desc = t
 
@@ -594,8 +596,9 @@ class _Workspace:
             mlp.forward(impl.policy, tg, self.x_tp.data_ptr(), True, self.LX1, self.tp_acts,
                         keep_h=False)
             ops.call_desc("d3a_bcq_rows", self.r_tq)
-            mlp.forward(impl.critic, tg, self.x_tq.data_ptr(), True, self.LX1, self.tq_acts,
-                        keep_h=False)
+            means = mlp.forward(impl.critic, tg, self.x_tq.data_ptr(), True, self.LX1,
+                                self.tq_acts, keep_h=False, row_mean=self.tq_means)
+            self.target_desc.means = self.tq_means.data_ptr() if means else None
             ops.call_desc("d3a_bcq_target", self.target_desc)
             # update_critic (ddpg_impl.py:138-165) with the quantile Huber loss
             mlp.forward(impl.critic, st, self.x_q.data_ptr(), True, self.LX1, self.q_acts)

@@ -143,7 +143,13 @@ __global__ __launch_bounds__(TG_T) void bcq_target_kernel(d3a_bcq_target_desc d)
   const int C = d.C, N = d.N, K = d.K;
   const int64_t BN = (int64_t)d.B * N;
   const int CN = C * N;
-  if (K <= 256) {
+  if (d.means != nullptr) {
+    // the target pass's epilogue formed the means (d3a_mlp_fwd_x6 row_mean)
+    for (int p = t; p < CN; p += TG_T) {
+      const int c = p / N, n = p - c * N;
+      sm[p] = d.means[(int64_t)c * BN + b * N + n];
+    }
+  } else if (K <= 256) {
     // eight (c, n) rows per wave in flight (their loads issued before any
     // sum), each row summed exactly as below: lane l adds q[l], q[l + 64], ..
     // in order, then the wave butterfly -- bitwise the same means

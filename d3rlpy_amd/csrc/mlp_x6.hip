@@ -68,6 +68,7 @@ struct WideLds {
     } a;
     __bf16 h2[3][W_RB * W_LDH];  // after layer 2
   } u;
+  float rs[8][W_RB];  // row_mean: per-wave output sums [wave][row]
 };
 
 // XL: n_in rounded up to 32 (32 or 64)
@@ -278,6 +279,7 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
     }
     // lane: row 32 rt + li, outputs 32 w + 8 R + 4 lh + i
     const int64_t ldo = d.ldout;
+    float rsum[2] = {0.f, 0.f};  // row_mean: this lane's outputs, in output order
     const bool vec = ((reinterpret_cast<uintptr_t>(outp) & 15) == 0) && (ldo & 3) == 0;
 #pragma unroll
     for (int R = 0; R < 4; ++R) {
@@ -292,6 +294,10 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
         float* op = outp + (int64_t)row * ldo + k0;
         const float v0 = o[rt][4 * R] + bv[0], v1 = o[rt][4 * R + 1] + bv[1];
         const float v2 = o[rt][4 * R + 2] + bv[2], v3 = o[rt][4 * R + 3] + bv[3];
+        if (k0 + 0 < nout) rsum[rt] += v0;
+        if (k0 + 1 < nout) rsum[rt] += v1;
+        if (k0 + 2 < nout) rsum[rt] += v2;
+        if (k0 + 3 < nout) rsum[rt] += v3;
         if (k0 + 3 < nout && vec) {
           *reinterpret_cast<float4*>(op) = make_float4(v0, v1, v2, v3);
         } else {
@@ -301,6 +307,24 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
           if (k0 + 3 < nout) op[3] = v3;
         }
       }
+    }
+    if (d.row_mean != nullptr) {
+      // the two lane halves hold interleaved runs of four outputs: the wave's
+      // 32 outputs of a row as (lane half 0's 16) + (lane half 1's 16)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const float other = __shfl_xor(rsum[rt], 32, 64);
+        if (lh == 0) L.rs[w][32 * rt + li] = rsum[rt] + other;
+      }
+    }
+  }
+  if (d.row_mean != nullptr) {
+    __syncthreads();  // uniform: row_mean is a kernel argument
+    if (t < W_RB) {
+      float s = L.rs[0][t];
+      for (int v = 1; v < nkt; ++v) s += L.rs[v][t];
+      const int row = m0 + t;
+      if (row < rend) d.row_mean[c * d.s_mean + row] = s / (float)nout;
     }
   }
 }
@@ -334,6 +358,9 @@ extern "C" int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
                     (d.r0 + d.rows) * d.ldx < (int64_t(1) << 31),
                 "d3a_mlp_fwd_x6: rows x row stride exceeds 2^31");
   D3A_CHECK_ARG(d.ldout >= d.n_out, "d3a_mlp_fwd_x6: ldout < n_out");
+  D3A_CHECK_ARG(d.row_mean == nullptr || (d.s_mean >= d.r0 + d.rows &&
+                                          d.s_mean * (int64_t)d.C < (int64_t(1) << 31)),
+                "d3a_mlp_fwd_x6: row_mean member stride must cover the rows");
   if (d.rows == 0) return 0;
   const dim3 grid((unsigned)((d.rows + W_RB - 1) / W_RB), 1, (unsigned)d.C);
   const hipStream_t st = (hipStream_t)stream;

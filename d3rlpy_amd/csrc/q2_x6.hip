@@ -49,11 +49,13 @@ constexpr int X_NCK = X_H / X_CK;
 constexpr int X_KS = X_CK / 16;  // MFMA k steps per chunk
 constexpr int X_LDB = 72;   // bf16 row stride of a ring slot (144 B: conflict-free 16-B reads)
 
-template <int XL, int NP>
+constexpr int X_NOMAX = 8;  // widest narrow head (NO = 8 instantiation)
+
+template <int XL, int NP, int NO>
 struct X6FwdLds {
   __bf16 h[2][NP][X_RB * X_LDB];    // layer-1 chunk ring: slot, part, [row][k]
   __bf16 x[NP][X_RB * (XL + 8)];    // input rows, parts, zero-padded to XL
-  float hp[8][X_RB];                // head partials [wave][row]
+  float hp[NO > 1 ? 1 : 8][X_RB];   // head partials [wave][row] (NO == 1)
 };
 
 // PROBE (timing probes only, D3A_X6_PROBE; results are wrong): bit 0 skips
@@ -65,13 +67,20 @@ struct X6FwdLds {
 // NP / HT: NP = 3 the exact split (fp32-accurate, kept activations fp32);
 // NP = 1, HT = __bf16 the bf16 throughput line's forward (d3a_q2_fwd_bf16's
 // contract: one bf16 rounding per operand, kept activations stored as bf16)
+//
+// NO: the head width; 1 (the Q head: a register dot) or X_NOMAX for a narrow
+// head of 2 .. 8 outputs (e.g. BCQ's VAE decoder and residual policy over the
+// B*N target rows, bcq_impl.py:215-226): head rows staged in LDS, one dot per
+// output, the per-wave partials over the freed chunk ring
 __device__ unsigned long long x6_stamps[2048 * 10];
-template <int XL, int PROBE = 0, int NP = 3, typename HT = float>
+template <int XL, int PROBE = 0, int NP = 3, typename HT = float, int NO = 1>
 __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   constexpr int XLD = XL + 8;
   constexpr int NS0 = XL / 16;  // layer-1 k steps
-  __shared__ __attribute__((aligned(16))) X6FwdLds<XL, NP> L;
-  static_assert(sizeof(X6FwdLds<XL, NP>) <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) X6FwdLds<XL, NP, NO> L;
+  static_assert(sizeof(X6FwdLds<XL, NP, NO>) <= 163840, "LDS");
+  static_assert(NO == 1 || 8 * NO * X_RB * 4 <= (int)sizeof(L.h), "head partials fit the ring");
+  static_assert(NO == 1 || NO * X_H * 4 <= (int)sizeof(L.x), "head rows fit the input image");
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int li = lane & 31, lh = lane >> 5;
@@ -277,6 +286,67 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 
   // ---- epilogue: bias, ReLU, kept rows to h[1], the head dot of the lane's
   // 16 units in order, then the two lane halves and the eight waves in order
+  if constexpr (NO > 1) {
+    // head rows over the input image (free after the last production; every
+    // wave passed the chunk loop's last barrier)
+    float* whl = reinterpret_cast<float*>(&L.x[0][0]);  // [output][256]
+    {
+      const float* whg = d.W[2] + wdel + c * d.sW[2];
+      for (int e = t; e < NO * X_H; e += 512) {
+        const int j = e / X_H;
+        whl[e] = j < d.n_out ? whg[e] : 0.f;
+      }
+    }
+    __syncthreads();
+    float bb[16];
+    {
+      const float* b1 = d.b[1] + wdel + c * d.sb[1];
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const float4 bv = *reinterpret_cast<const float4*>(b1 + 32 * w + 8 * R + 4 * lh);
+        bb[4 * R] = bv.x; bb[4 * R + 1] = bv.y; bb[4 * R + 2] = bv.z; bb[4 * R + 3] = bv.w;
+      }
+    }
+    float* hpn = reinterpret_cast<float*>(&L.h[0][0][0]);  // [wave][output][row]
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = fmaxf(acc[tt][r] + bb[r], 0.f);
+      const int row = m0 + 32 * tt + li;
+      if (!(PROBE & 4) && h1g != nullptr && row >= h_from && row < rend) {
+#pragma unroll
+        for (int R = 0; R < 4; ++R) put4(h1g + row * X_H + 32 * w + 8 * R + 4 * lh, v + 4 * R);
+      }
+#pragma unroll
+      for (int j = 0; j < NO; ++j) {
+        float hs = 0.f;
+#pragma unroll
+        for (int R = 0; R < 4; ++R) {
+          const float4 wv = *reinterpret_cast<const float4*>(&whl[j * X_H + 32 * w + 8 * R + 4 * lh]);
+          if (R == 0) hs = v[0] * wv.x;
+          else hs = fmaf(v[4 * R], wv.x, hs);
+          hs = fmaf(v[4 * R + 1], wv.y, hs);
+          hs = fmaf(v[4 * R + 2], wv.z, hs);
+          hs = fmaf(v[4 * R + 3], wv.w, hs);
+        }
+        const float o = __shfl_xor(hs, 32, 64);
+        if (lh == 0) hpn[(w * NO + j) * X_RB + 32 * tt + li] = hs + o;
+      }
+    }
+    __syncthreads();
+    const float* b2 = d.b[2] + wdel + c * d.sb[2];
+    for (int e = t; e < NO * X_RB; e += 512) {
+      const int m = e / NO, j = e - m * NO;
+      const int row = m0 + m;
+      if (j >= d.n_out || row >= rend) continue;
+      float q = hpn[j * X_RB + m];
+#pragma unroll
+      for (int v = 1; v < 8; ++v) q += hpn[(v * NO + j) * X_RB + m];
+      outp[(int64_t)row * d.ldout + j] = q + b2[j];
+    }
+    return;
+  }
   float bb[16], ww[16];
   {
     const float* b1 = d.b[1] + wdel + c * d.sb[1];
@@ -326,9 +396,12 @@ using namespace d3a;
 
 extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_fwd_x6: null desc");
+  D3A_CHECK_ARG(dp->row_mean == nullptr, "d3a_q2_fwd_x6: row_mean is d3a_mlp_fwd_x6 only");
   const d3a_mlp_fwd_desc& d = *dp;
-  D3A_CHECK_ARG(d.n_hidden == 2 && d.H == X_H && d.n_out == 1 && d.n_in >= 1 && d.n_in <= 48,
-                "d3a_q2_fwd_x6: needs [n_in <= 48, 256, 256, 1]");
+  D3A_CHECK_ARG(d.n_hidden == 2 && d.H == X_H && d.n_out >= 1 && d.n_out <= X_NOMAX &&
+                    d.n_in >= 1 && d.n_in <= 48,
+                "d3a_q2_fwd_x6: needs [n_in <= 48, 256, 256, n_out <= 8]");
+  D3A_CHECK_ARG(d.ldout >= d.n_out, "d3a_q2_fwd_x6: ldout < n_out");
   D3A_CHECK_ARG(d.x && d.out && d.W[0] && d.W[1] && d.W[2] && d.b[0] && d.b[1] && d.b[2],
                 "d3a_q2_fwd_x6: null operand");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.r0 >= 0 && d.h_from >= 0 && d.aux_rows >= 0,
@@ -358,7 +431,7 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
     const char* e = getenv("D3A_X6_PROBE");
     return e ? atoi(e) : 0;
   }();
-  if (probe && xl == 16) {
+  if (probe && xl == 16 && d.n_out == 1) {
     switch (probe & 31) {
       case 1: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 1>), grid, dim3(512), 0, st, d); break;
       case 4: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 4>), grid, dim3(512), 0, st, d); break;
@@ -370,7 +443,14 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
     D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
     return 0;
   }
-  if (xl == 16)
+  if (d.n_out > 1) {
+    if (xl == 16)
+      hipLaunchKernelGGL((q2x6_fwd_kernel<16, 0, 3, float, X_NOMAX>), grid, dim3(512), 0, st, d);
+    else if (xl == 32)
+      hipLaunchKernelGGL((q2x6_fwd_kernel<32, 0, 3, float, X_NOMAX>), grid, dim3(512), 0, st, d);
+    else
+      hipLaunchKernelGGL((q2x6_fwd_kernel<48, 0, 3, float, X_NOMAX>), grid, dim3(512), 0, st, d);
+  } else if (xl == 16)
     hipLaunchKernelGGL(q2x6_fwd_kernel<16>, grid, dim3(512), 0, st, d);
   else if (xl == 32)
     hipLaunchKernelGGL(q2x6_fwd_kernel<32>, grid, dim3(512), 0, st, d);
@@ -402,6 +482,7 @@ void launch_q2x1_fwd(const d3a_mlp_fwd_desc& d, hipStream_t st) {
 // operand, fp32 accumulation
 extern "C" int d3a_q2_fwd_x1(const d3a_mlp_fwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_fwd_x1: null desc");
+  D3A_CHECK_ARG(dp->row_mean == nullptr, "d3a_q2_fwd_x1: row_mean is d3a_mlp_fwd_x6 only");
   const d3a_mlp_fwd_desc& e = *dp;  // d3a_q2_fwd_x6's contract
   D3A_CHECK_ARG(e.n_hidden == 2 && e.H == X_H && e.n_out == 1 && e.n_in >= 1 && e.n_in <= 48,
                 "d3a_q2_fwd_x1: needs [n_in <= 48, 256, 256, 1]");

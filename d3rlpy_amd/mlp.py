@@ -90,11 +90,20 @@ def q2_shape(net: EnsembleMLP) -> bool:
     return net.n_layers == 3 and s[1] == 256 and s[2] == 256 and s[3] == 1 and s[0] <= 48
 
 
+def x6_narrow_shape(net: EnsembleMLP) -> bool:
+    """[n_in <= 48, 256, 256, 1 < n_out <= 8]: d3a_q2_fwd_x6's narrow-head
+    instantiation (BCQ's VAE decoder / residual policy over the target rows)."""
+    s = net.sizes
+    return (net.n_layers == 3 and s[1] == 256 and s[2] == 256 and 1 < s[3] <= 8
+            and s[0] <= 48)
+
+
 def x6_wide_shape(net: EnsembleMLP) -> bool:
-    """[n_in <= 64, 256, 256, 1 < n_out <= 256]: d3a_mlp_fwd_x6's shape."""
+    """[n_in <= 64, 256, 256, 1 < n_out <= 256] (not a narrow shape):
+    d3a_mlp_fwd_x6's shape."""
     s = net.sizes
     return (net.n_layers == 3 and s[1] == 256 and s[2] == 256 and 1 < s[3] <= 256
-            and s[0] <= 64)
+            and s[0] <= 64 and not x6_narrow_shape(net))
 
 
 def q2_ok(net: EnsembleMLP, rows: int) -> bool:
@@ -156,7 +165,8 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             r0: int = 0, r1: Optional[int] = None, sxb: Optional[int] = None,
             members: Optional[int] = None, keep_h: bool = True,
             h_from: Optional[int] = None, aux: Optional[tuple] = None,
-            skip_head: bool = False, out_parts: Optional[torch.Tensor] = None) -> None:
+            skip_head: bool = False, out_parts: Optional[torch.Tensor] = None,
+            row_mean: Optional[torch.Tensor] = None) -> bool:
     """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
     (through its first ``members`` members only, when given).  ``keep_h``:
     store the hidden activations in ``acts.h`` (needed by a backward pass),
@@ -172,6 +182,10 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     equals the main pass's (acts2.R == acts.R rows, same ldx); otherwise it is
     a separate forward.
 
+    ``row_mean`` ([C][R] fp32): also the mean of each row's outputs, where the
+    launch is d3a_mlp_fwd_x6 (its epilogue forms it); returns whether it was
+    written (False: the caller forms it).
+
     ``out_parts`` ([D3A_MLP_PARTS][C][R][n_out], ``parts_ok`` shapes): the
     head is written there as partial sums over the second hidden layer's unit
     parts (d3a_mlp_fwd_desc.parts; consumers sum them in order), not to
@@ -180,7 +194,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     r1 = R if r1 is None else r1
     n = r1 - r0
     if n <= 0:
-        return
+        return False
     C = net.C if members is None else members
     sizes = net.sizes
     bf16 = bool(acts.h) and acts.h[0].dtype == torch.bfloat16
@@ -219,19 +233,23 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             d.aux_out, d.aux_sout, d.aux_rows = aacts.out.data_ptr(), aacts.R * sizes[-1], aacts.R
             aux = None
         entry = "d3a_q2_fwd_bf16" if bf16 else "d3a_mlp_fwd"
-        big_q2 = (not bf16 and not small and q2_shape(net)
-                  and (n + (d.aux_rows if d.aux_rows else 0)) * C >= 8192)
-        if big_q2 and ops.CRITIC_PRECISION == "bf16":
+        big = (not bf16 and not small and out_parts is None
+               and (n + (d.aux_rows if d.aux_rows else 0)) * C >= 8192)
+        if big and q2_shape(net) and ops.CRITIC_PRECISION == "bf16":
             entry = "d3a_q2_fwd_x1"  # the bf16 line: one bf16 part per operand
-        elif big_q2 and ops.CRITIC_GEMM == "x6":
-            entry = "d3a_q2_fwd_x6"  # the q2_fwd pass, fp32-accurate split-bf16
+        elif big and (q2_shape(net) or x6_narrow_shape(net)) and ops.CRITIC_GEMM == "x6":
+            entry = "d3a_q2_fwd_x6"  # fp32-accurate split-bf16 (Q head or <= 8 outputs)
         elif (not bf16 and not small and ops.CRITIC_GEMM == "x6" and x6_wide_shape(net)
               and out_parts is None and not d.aux_rows and n * C >= 8192):
             entry = "d3a_mlp_fwd_x6"  # wide head (e.g. BCQ's target QR critics)
+        means = row_mean is not None and entry == "d3a_mlp_fwd_x6"
+        if means:
+            assert tuple(row_mean.shape) == (C, R) and row_mean.dtype == torch.float32
+            d.row_mean, d.s_mean = row_mean.data_ptr(), R
         ops.call_desc(entry, d)
         if aux is not None:
             forward(net, aux[0], aux[1], True, aux[2], aux[3], keep_h=False)
-        return
+        return means
     L = net.n_layers
     inp, ld_in = x + 4 * r0 * ldx, ldx
     sxb_ = (0 if x_shared else R * ldx) if sxb is None else sxb
@@ -258,7 +276,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     dout = (aacts.out.data_ptr() - acts.out.data_ptr()) // 4 if pair else 0
     if skip_head:  # the caller's kernel evaluates the head (head1_min)
         assert not pair
-        return
+        return False
     if out_dim <= 16:
         # narrow heads (Q values, policy mu|logstd): one wave per row beats a
         # 32-wide MFMA tile that is mostly padding
@@ -272,6 +290,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
                        pair=(dx, dW, dout) if pair else None)
     if aux is not None and not pair:
         forward(net, aux[0], aux[1], True, aux[2], aux[3], keep_h=False)
+    return False
 
 
 class BackwardSpace:

@@ -285,9 +285,11 @@ def set_critic_precision(p: str) -> None:
 # GEMM arithmetic of the [n_in <= 48, 256, 256, 1] critic passes at fp32
 # precision: "fp32" (v_mfma_f32_32x32x2_f32, exact fp32 fma chains: q2_fwd /
 # q2_bwd) or "x6" (exact three-way split-bf16 operands on the bf16 matrix
-# cores, fp32-accurate: d3a_q2_fwd_x6 / d3a_q2_bwd_x6, csrc/q2_x6*.hip).  Read
-# at each launch, so set it before an update graph is captured.
-CRITIC_GEMM = os.environ.get("D3A_CRITIC_GEMM", "fp32")
+# cores, fp32-accurate: d3a_q2_fwd_x6 / d3a_q2_bwd_x6, csrc/q2_x6*.hip; the
+# default since round 4: it holds the same parity bars, tests/test_gpu_x6.py,
+# test_gpu_cql_parity.py, and runs the K2 critic forward in 31.6 us against
+# 46.8).  Read at each launch, so set it before an update graph is captured.
+CRITIC_GEMM = os.environ.get("D3A_CRITIC_GEMM", "x6")
 
 
 def set_critic_gemm(mode: str) -> None:

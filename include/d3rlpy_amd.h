@@ -247,6 +247,12 @@ typedef struct d3a_mlp_fwd_desc {
    * written by part 0, h[1] unit-slice by slice.  parts 0 / 1: off.       */
   int32_t parts;
   int64_t s_part;
+  /* Optional (d3a_mlp_fwd_x6 only; null elsewhere): row_mean[c * s_mean + r]
+   * = the mean of row r's n_out outputs (a fixed summation order), written
+   * beside out -- e.g. the per-(critic, sampled action) quantile mean of
+   * compute_max_with_n_actions (q_functions/__init__.py:37-39), so that
+   * d3a_bcq_target does not re-read every quantile row.                  */
+  float* row_mean; int64_t s_mean;
 } d3a_mlp_fwd_desc;
 #define D3A_MLP_PARTS 4
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);
@@ -866,6 +872,9 @@ int d3a_bcq_vae_enc_grad(const d3a_bcq_vae_desc* d, void* stream);
 typedef struct d3a_bcq_target_desc {
   const float* q; float* target;
   int32_t B, N, K, C; float lam;
+  /* optional: the quantile means [C][B*N] (d3a_mlp_fwd_x6's row_mean); when
+   * null the kernel forms them from q */
+  const float* means;
 } d3a_bcq_target_desc;
 int d3a_bcq_target(const d3a_bcq_target_desc* d, void* stream);
 

@@ -186,19 +186,32 @@ def test_q2_fwd_x1(dev, rows, h_from, aux, n_in):
         sq = (a2.abs() @ W_[2].double().abs().transpose(1, 2)).squeeze(-1) + s2.max()
         return a1, s1, a2, s2, q, sq
     a1, s1, a2, s2, qe, sq = emu(x[:, :n_in], Ws, bs)
-    # the kept activations: h[0] exact up to the fp32 accumulation; h[1]'s
-    # bf16 operand r16(h[0]) may round a tie the other way -- 1e-4 of its terms
-    for l, (a, sc) in enumerate(((a1, s1), (a2, s2))):
-        got = h[l][:, h_from:].double().cpu()
-        err = float(((got - a[:, h_from:].cpu()).abs() / sc[:, h_from:].cpu().clamp_min(1e-30)).max())
-        assert err < 1e-4, (l, err)
+    # kept rows, layer by layer from the kernel's own previous layer (its fp32
+    # h[0] differs from the fp64 one by accumulation rounding, which can move
+    # r16(h[0]) across a bf16 rounding tie -- one bf16 ulp of one term): each
+    # layer within 1e-4 of the sum of |terms| of its products
+    k = slice(h_from, rows)
+    err0 = float(((h[0][:, k].double() - a1[:, k]).abs() / s1[:, k].clamp_min(1e-30)).max())
+    assert err0 < 1e-4, err0
+    hk0 = h[0][:, k].double()
+    z2 = r16(hk0) @ r16(Ws[1]).transpose(1, 2) + bs[1].double().unsqueeze(1)
+    s2k = r16(hk0).abs() @ r16(Ws[1]).abs().transpose(1, 2) + bs[1].double().abs().unsqueeze(1)
+    err1 = float(((h[1][:, k].double() - z2.clamp_min(0)).abs() / s2k.clamp_min(1e-30)).max())
+    assert err1 < 1e-4, err1
+    hk1 = h[1][:, k].double()
+    qk = (hk1 @ Ws[2].double().transpose(1, 2) + bs[2].double().unsqueeze(1)).squeeze(-1)
+    sqk = (hk1.abs() @ Ws[2].double().abs().transpose(1, 2)).squeeze(-1) + bs[2].double().abs()
+    assert float(((out[:, k].double() - qk).abs() / sqk.clamp_min(1e-30)).max()) < 1e-5
+    for l in range(2):
         assert torch.isnan(h[l][:, :h_from]).all(), l
-    assert float(((out.double() - qe).abs() / sq.clamp_min(1e-30)).max()) < 1e-4
+    # every row against the fp64 emulation: a bf16 tie moved by the layer-1
+    # accumulation shifts one of 256 terms by one bf16 ulp (2^-8 of it)
+    assert float(((out.double() - qe).abs() / sq.clamp_min(1e-30)).max()) < 4e-3
     hs, q = _fwd64(x[:, :n_in], Ws, bs)
     assert _rel(out, q) < 2e-2
     if aux:
         _, _, _, _, qa, sqa = emu(xa[:aux, :n_in], Wt, bt)
-        assert float(((aout[:, :aux].double() - qa).abs() / sqa.clamp_min(1e-30)).max()) < 1e-4
+        assert float(((aout[:, :aux].double() - qa).abs() / sqa.clamp_min(1e-30)).max()) < 4e-3
 
 
 @pytest.mark.parametrize("rows,n_in,n_scaled", [(7936, 14, 7680), (1000, 48, 999), (300, 23, 0)])

@@ -63,6 +63,10 @@ CASES = {
     # ReLU-decision-aware fp64 arbiter every case goes through)
     "repro_hopper": dict(D=11, A=3, hidden=[256, 256, 256], N=10, B=256,
                          kw=dict(alpha_learning_rate=0.0, conservative_weight=10.0)),
+    # the critic passes on the exact-fp32 MFMA kernels (q2_fwd / q2_bwd) rather
+    # than the default split-bf16 x6 kernels (ops.CRITIC_GEMM)
+    "hopper_fp32mfma": dict(D=11, A=3, hidden=[256, 256], N=10, B=256, gemm="fp32"),
+    "k4_antmaze_fp32mfma": dict(D=29, A=8, hidden=[256, 256], N=10, B=256, gemm="fp32"),
 }
 
 
@@ -161,6 +165,16 @@ def test_cql_update_parity(case):
     reference checkpoint layout, then both run one CQL._update on the same
     batch and noise."""
     cfg = CASES[case]
+    from d3rlpy_amd import ops
+    prev = ops.CRITIC_GEMM
+    ops.set_critic_gemm(cfg.get("gemm", prev))
+    try:
+        _update_parity(case, cfg)
+    finally:
+        ops.set_critic_gemm(prev)
+
+
+def _update_parity(case, cfg):
     D, A, H, N, B = cfg["D"], cfg["A"], cfg["hidden"], cfg["N"], cfg["B"]
     C = cfg.get("C", 2)
     kw = cfg.get("kw", {})

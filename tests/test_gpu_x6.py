@@ -243,12 +243,19 @@ def test_q2_x6_rejects_bad_shapes():
         ops.call_desc("d3a_q2_fwd_x6", f)
 
 
-@pytest.mark.parametrize("rows,n_in,n_out,keep", [(25600, 23, 200, False), (1000, 23, 6, True),
-                                                  (257, 64, 256, True), (77, 33, 1 + 32, False)])
-def test_mlp_fwd_x6_wide_head_vs_fp64(rows, n_in, n_out, keep):
+@pytest.mark.parametrize("entry,rows,n_in,n_out,keep", [
+    ("d3a_mlp_fwd_x6", 25600, 23, 200, False), ("d3a_mlp_fwd_x6", 1000, 23, 6, True),
+    ("d3a_mlp_fwd_x6", 257, 64, 256, True), ("d3a_mlp_fwd_x6", 77, 33, 1 + 32, False),
+    # the narrow-head instantiation of the Q-head kernel (K3's VAE decoder over
+    # B*N target rows: obs 17 + latent 12 -> 256 -> 256 -> act 6; the residual
+    # policy 23 -> .. -> 6; ragged rows, 8 outputs, 48 inputs)
+    ("d3a_q2_fwd_x6", 25600, 29, 6, False), ("d3a_q2_fwd_x6", 1000, 23, 6, True),
+    ("d3a_q2_fwd_x6", 333, 48, 8, True), ("d3a_q2_fwd_x6", 200, 5, 2, False)])
+def test_mlp_fwd_x6_wide_head_vs_fp64(entry, rows, n_in, n_out, keep):
     """d3a_mlp_fwd_x6 ([n_in <= 64, 256, 256, n_out <= 256]; the K3 target QR
-    critics are the first case) against fp64, per layer relative to the
-    layer's rounding scale, on the kernel's own fp32 inputs to each layer."""
+    critics are the first case) and d3a_q2_fwd_x6's narrow head ([n_in <= 48,
+    256, 256, n_out <= 8]) against fp64, per layer relative to the layer's
+    rounding scale, on the kernel's own fp32 inputs to each layer."""
     dev = torch.device("cuda")
     C = 2
     gen = torch.Generator().manual_seed(rows + n_out)
@@ -286,9 +293,29 @@ def test_mlp_fwd_x6_wide_head_vs_fp64(rows, n_in, n_out, keep):
     d.sh = rows * 256
     d.out, d.sout, d.ldout = out.data_ptr(), rows * n_out, n_out
     d.r0, d.rows, d.C, d.h_from = 0, rows, C, 0
-    ops.call_desc("d3a_mlp_fwd_x6", d)
+    # row_mean (the per-row output mean of compute_max_with_n_actions,
+    # q_functions/__init__.py:37-39) on the keep=False cases
+    means = torch.full((C, rows), float("nan"), device=dev)
+    wide = entry == "d3a_mlp_fwd_x6"
+    if not keep and wide:
+        d.row_mean, d.s_mean = means.data_ptr(), rows
+    ops.call_desc(entry, d)
     torch.cuda.synchronize()
     assert not torch.isnan(out).any()
+    if not keep and wide:
+        # the mean of the kernel's own outputs: fp32 summation of n_out terms
+        m64 = out.double().mean(-1)
+        sm = out.double().abs().mean(-1)
+        em = float(((means.double() - m64).abs() / sm.clamp_min(1e-30)).max())
+        print(f"x6 wide forward row_mean vs fp64 mean of its outputs: {em:.1e}")
+        assert em < 1e-6 * n_out, em
+        # run to run bit-identical (fixed summation order)
+        m1 = means.clone()
+        ops.call_desc(entry, d)
+        torch.cuda.synchronize()
+        assert torch.equal(m1, means)
+    else:
+        assert torch.isnan(means).all()
     hs, sc = _fwd64(x[:, :n_in], Ws, bs)
     if keep:
         h0, h1 = h[0].double(), h[1].double()

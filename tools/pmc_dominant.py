@@ -21,12 +21,12 @@ def main():
     ap.add_argument("--algo", default="cql")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--transitions", type=int, default=200_000)
-    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--precision", choices=["fp32", "bf16", "bf16h"], default="fp32")
     ap.add_argument("--critic-gemm", choices=["fp32", "x6"], default=None)
     a = ap.parse_args()
     from d3rlpy_amd import ops
-    if a.precision == "bf16":
-        ops.set_critic_precision("bf16")
+    if a.precision != "fp32":
+        ops.set_critic_precision(a.precision)
     if a.critic_gemm:
         ops.set_critic_gemm(a.critic_gemm)
     torch.cuda.set_device(0)
