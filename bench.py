@@ -241,11 +241,12 @@ def gpu_steps(algo, it, n):
         algo._grad_step += 1  # as fit() does (drives TD3+BC's delayed actor)
 
 
-def measure_kernel(ws_obj, reps: int = 50):
-    """Average duration of the dominant kernel via HIP events on its stream."""
+def measure_kernel(ws_obj, reps: int = 50, settle: int = 3):
+    """Average duration of the dominant kernel via HIP events on its stream,
+    over ``reps`` launches after ``settle`` untimed ones."""
     import torch
     launch, flops, desc = ws_obj.dominant_kernel()
-    for _ in range(3):
+    for _ in range(settle):
         launch()
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
@@ -548,12 +549,15 @@ def main():
         ar_log["armed"] = False
     gpu_steps(algo, it, max(0, args.warmup - 1))
     # the dominant kernel's average launch time (HIP events on its stream),
-    # taken here, right before the timed region: its ~200 back-to-back
-    # launches also hold the device at its loaded clock, so a short timed
-    # window (the driver's --steps 20 --warmup 5) does not start on a device
-    # still ramping from idle (profiles/r04_bench_window.jsonl)
+    # taken here, right before the timed region, over its last 500 of 1,000
+    # back-to-back launches: the MI355X takes >10 ms of load to reach its
+    # loaded clock (the same kernel measured 37.5 us after 5 warm-up steps,
+    # 34.2 after 50, 31.4 in a 300-step profile), so the measurement waits for
+    # the clock and leaves the device at it -- a short timed window (the
+    # driver's --steps 20 --warmup 5) then starts where a long one runs
+    # (profiles/r04_bench_window.jsonl)
     wsp = next(iter(algo.impl._ws.values()))
-    kern_s, kflops, kdesc = measure_kernel(wsp, reps=200)
+    kern_s, kflops, kdesc = measure_kernel(wsp, reps=500, settle=500)
     torch.cuda.synchronize()
     _barrier(ws)
     wd.set()
@@ -711,7 +715,9 @@ def main():
                      "traffic": traffic, "kernel": kdesc,
                      **({"bf16_mfma_frac": round(6 * achieved / 2500.0, 4),
                          "peak_note": "bf16 dense MFMA peak 2500 TF / 6 products"} if x6 else {}),
-                     "avg_launch_us": round(kern_s * 1e6, 3)},
+                     "avg_launch_us": round(kern_s * 1e6, 3),
+                     "launch_timing": "HIP events on the kernel's stream, 500 launches after 500 "
+                                      "settling launches, right before the timed region"},
         "cpu_baseline": cpu,
     }
     out["host"] = host

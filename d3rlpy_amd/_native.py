@@ -270,6 +270,9 @@ class MlpFwdDesc(C.Structure):
         ("aux_rows", C.c_int64),
         ("parts", C.c_int32), ("s_part", C.c_int64),
         ("row_mean", vp), ("s_mean", C.c_int64),
+        ("xg_mode", C.c_int32), ("xg_D", C.c_int32), ("xg_rep", C.c_int32), ("xg_E", C.c_int32),
+        ("xg_obs", vp), ("xg_a", vp), ("xg_lda", C.c_int64),
+        ("xg_base", vp), ("xg_clip", C.c_float), ("xg_scale", C.c_float),
     ]
 
 

@@ -411,7 +411,6 @@ class _Workspace:
         # critic target over B*N sampled actions
         self.x_td = z(BN, self.LX2)
         self.td_acts = mlp.Acts.alloc(impl.vae_dec, BN, dev)
-        self.a_dec_t = z(BN, A)
         self.x_tp = z(BN, self.LX1)
         self.tp_acts = mlp.Acts.alloc(impl.policy, BN, dev)
         self.x_tq = z(BN, self.LX1)
@@ -470,10 +469,13 @@ class _Workspace:
         # target: (s', clamp(z)) -> (s', tanh(dec)) -> (s', clamp(a_dec + flex tanh(pi)))
         self.r_td = self._rows(self.next_obs, N, self.z_target.data_ptr(), L, L, 1, self.x_td,
                                self.LX2, BN, clip=0.5)
+        # (the x6 target passes build these rows while staging them: mlp.forward
+        # xgen; the critic rows take the decoder's raw output as their base,
+        # mode 4, so the policy pass need not store tanh of it)
         self.r_tp = self._rows(self.next_obs, N, self.td_acts.out.data_ptr(), A, A, 2, self.x_tp,
-                               self.LX1, BN, e_out=self.a_dec_t)
-        self.r_tq = self._rows(self.next_obs, N, self.tp_acts.out.data_ptr(), A, A, 3, self.x_tq,
-                               self.LX1, BN, base=self.a_dec_t, scale=flex)
+                               self.LX1, BN)
+        self.r_tq = self._rows(self.next_obs, N, self.tp_acts.out.data_ptr(), A, A, 4, self.x_tq,
+                               self.LX1, BN, base=self.td_acts.out, scale=flex)
         # actor: the same chain on (s, z_actor) with the online policy
         self.r_ad = self._rows(self.obs, 1, self.z_actor.data_ptr(), L, L, 1, self.x_ad,
                                self.LX2, B, clip=0.5)
@@ -541,7 +543,7 @@ class _Workspace:
 
         def launch():
             mlp.forward(net, impl.targ, self.x_tq.data_ptr(), True, self.LX1, self.tq_acts,
-                        keep_h=False)
+                        keep_h=False, row_mean=self.tq_means, xgen=self.r_tq)
         flops = 2 * self.C * BN * sum(s[l] * s[l + 1] for l in range(len(s) - 1))
         x6 = ops.CRITIC_GEMM == "x6" and mlp.x6_wide_shape(net)
         return launch, flops, (f"d3a_mlp_fwd target QR critics ({'split-bf16 x6' if x6 else 'fp32'}"
@@ -589,15 +591,13 @@ class _Workspace:
             self.imitator_opt.launch()
         if critic:
             # compute_target (bcq_impl.py:215-226) over B*N sampled actions
-            ops.call_desc("d3a_bcq_rows", self.r_td)
             mlp.forward(impl.vae_dec, st, self.x_td.data_ptr(), True, self.LX2, self.td_acts,
-                        keep_h=False)
-            ops.call_desc("d3a_bcq_rows", self.r_tp)
+                        keep_h=False, xgen=self.r_td)
             mlp.forward(impl.policy, tg, self.x_tp.data_ptr(), True, self.LX1, self.tp_acts,
-                        keep_h=False)
-            ops.call_desc("d3a_bcq_rows", self.r_tq)
+                        keep_h=False, xgen=self.r_tp)
             means = mlp.forward(impl.critic, tg, self.x_tq.data_ptr(), True, self.LX1,
-                                self.tq_acts, keep_h=False, row_mean=self.tq_means)
+                                self.tq_acts, keep_h=False, row_mean=self.tq_means,
+                                xgen=self.r_tq)
             self.target_desc.means = self.tq_means.data_ptr() if means else None
             ops.call_desc("d3a_bcq_target", self.target_desc)
             # update_critic (ddpg_impl.py:138-165) with the quantile Huber loss

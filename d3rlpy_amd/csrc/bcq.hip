@@ -38,6 +38,11 @@ __global__ __launch_bounds__(256) void bcq_rows_kernel(d3a_bcq_rows_desc d) {
       v = fminf(fmaxf(__fadd_rn(d.base[r * d.E + e], res), -1.f), 1.f);
       break;
     }
+    case 4: {                                    // residual policy on the raw decoder output
+      const float res = __fmul_rn(d.scale, tanhf(a));
+      v = fminf(fmaxf(__fadd_rn(tanhf(d.base[r * d.E + e]), res), -1.f), 1.f);
+      break;
+    }
     default: v = a;
   }
   d.x[r * d.ldx + j] = v;
@@ -313,7 +318,8 @@ extern "C" int d3a_bcq_rows(const d3a_bcq_rows_desc* d, void* stream) {
   D3A_CHECK_ARG(d && d->obs && d->a && d->x, "d3a_bcq_rows: null pointer");
   D3A_CHECK_ARG(d->rep >= 1 && d->D >= 1 && d->E >= 1 && d->ldx >= d->D + d->E,
                 "d3a_bcq_rows: bad sizes");
-  D3A_CHECK_ARG(d->mode != 3 || d->base, "d3a_bcq_rows: mode 3 needs base");
+  D3A_CHECK_ARG(d->mode >= 0 && d->mode <= 4 && (d->mode < 3 || d->base),
+                "d3a_bcq_rows: mode 0..4; modes 3 / 4 need base");
   if (d->rows <= 0) return 0;
   hipLaunchKernelGGL(bcq_rows_kernel, dim3(blocks256(d->rows * (d->D + d->E))), dim3(256), 0,
                      (hipStream_t)stream, *d);

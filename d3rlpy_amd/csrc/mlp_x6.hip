@@ -115,7 +115,7 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
       const int r = m0 + m;
       float v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? xb[r * ldx + k4 + j] : 0.f;
+      for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? input_at(d, xb, ldx, r, k4 + j) : 0.f;
       bf16x4 p[3];
       split4(v, p);
 #pragma unroll
@@ -340,8 +340,10 @@ extern "C" int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(d.n_hidden == 2 && d.H == W_H && d.n_out >= 1 && d.n_out <= 256 && d.n_in >= 1 &&
                     d.n_in <= 64,
                 "d3a_mlp_fwd_x6: needs [n_in <= 64, 256, 256, n_out <= 256]");
-  D3A_CHECK_ARG(d.x && d.out && d.W[0] && d.W[1] && d.W[2] && d.b[0] && d.b[1] && d.b[2],
+  D3A_CHECK_ARG((d.x || d.xg_mode) && d.out && d.W[0] && d.W[1] && d.W[2] && d.b[0] && d.b[1] &&
+                    d.b[2],
                 "d3a_mlp_fwd_x6: null operand");
+  D3A_CHECK_ARG(xgen_ok(d), "d3a_mlp_fwd_x6: bad input-row builder (xg_*)");
   D3A_CHECK_ARG(d.aux_rows == 0 && d.parts <= 1, "d3a_mlp_fwd_x6: no aux pass / parts");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.r0 >= 0 && d.h_from >= 0, "d3a_mlp_fwd_x6: bad sizes");
   auto a16 = [](const void* p, int64_t stride) {

@@ -577,6 +577,7 @@ using namespace d3a;
 extern "C" int d3a_q2_fwd_bf16(const d3a_mlp_fwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_fwd_bf16: null desc");
   D3A_CHECK_ARG(dp->row_mean == nullptr, "d3a_q2_fwd_bf16: row_mean is d3a_mlp_fwd_x6 only");
+  D3A_CHECK_ARG(dp->xg_mode == 0, "d3a_q2_fwd_bf16: no input-row builder (xg_mode)");
   const d3a_mlp_fwd_desc& d = *dp;
   D3A_CHECK_ARG(d.x && d.out, "d3a_q2_fwd_bf16: null input / output");
   D3A_CHECK_ARG(d.n_hidden == 2 && d.H == B_H && d.n_out == 1,

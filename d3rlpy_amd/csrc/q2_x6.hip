@@ -168,7 +168,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       const int r = m0 + m;
       float v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? xb[r * ldx + k4 + j] : 0.f;
+      for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? input_at(d, xb, ldx, r, k4 + j) : 0.f;
       bf16x4 p[NP];
       splitn4<NP>(v, p);
 #pragma unroll
@@ -402,8 +402,10 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
                     d.n_in >= 1 && d.n_in <= 48,
                 "d3a_q2_fwd_x6: needs [n_in <= 48, 256, 256, n_out <= 8]");
   D3A_CHECK_ARG(d.ldout >= d.n_out, "d3a_q2_fwd_x6: ldout < n_out");
-  D3A_CHECK_ARG(d.x && d.out && d.W[0] && d.W[1] && d.W[2] && d.b[0] && d.b[1] && d.b[2],
+  D3A_CHECK_ARG((d.x || d.xg_mode) && d.out && d.W[0] && d.W[1] && d.W[2] && d.b[0] && d.b[1] &&
+                    d.b[2],
                 "d3a_q2_fwd_x6: null operand");
+  D3A_CHECK_ARG(xgen_ok(d), "d3a_q2_fwd_x6: bad input-row builder (xg_*)");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.r0 >= 0 && d.h_from >= 0 && d.aux_rows >= 0,
                 "d3a_q2_fwd_x6: bad sizes");
   auto a16 = [](const void* p, int64_t stride) {
@@ -483,6 +485,7 @@ void launch_q2x1_fwd(const d3a_mlp_fwd_desc& d, hipStream_t st) {
 extern "C" int d3a_q2_fwd_x1(const d3a_mlp_fwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_fwd_x1: null desc");
   D3A_CHECK_ARG(dp->row_mean == nullptr, "d3a_q2_fwd_x1: row_mean is d3a_mlp_fwd_x6 only");
+  D3A_CHECK_ARG(dp->xg_mode == 0, "d3a_q2_fwd_x1: no input-row builder");
   const d3a_mlp_fwd_desc& e = *dp;  // d3a_q2_fwd_x6's contract
   D3A_CHECK_ARG(e.n_hidden == 2 && e.H == X_H && e.n_out == 1 && e.n_in >= 1 && e.n_in <= 48,
                 "d3a_q2_fwd_x1: needs [n_in <= 48, 256, 256, 1]");

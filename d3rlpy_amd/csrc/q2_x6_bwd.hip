@@ -181,8 +181,13 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
       return;
     }
     float pg = 0.f;
+    // db2 / dW3 are written for this workgroup's quarter of o only
+    // (o = i0 .. i0 + 63: half bo = q >> 1, oa >> 6 = q & 1 -- wave-uniform,
+    // oa >> 6 = (w - 4) >> 1): only those threads keep the sums
+    const bool sums = ((oa >> 6) == (q & 1));
 #pragma unroll
     for (int bo = 0; bo < 2; ++bo) {
+      const bool sum_bo = sums && bo == (q >> 1);
       const float4 w4 = *reinterpret_cast<const float4*>(w3g + oa + 128 * bo);
       const float w3a[4] = {w4.x, w4.y, w4.z, w4.w};
       __bf16 m[4][4];
@@ -197,7 +202,7 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
           const bool on = ok && hv[e] > 0.f;
           m[k][e] = on ? (__bf16)1.f : (__bf16)0.f;
           mv[e] = m[k][e];
-          if (!(PROBE & 4)) {
+          if (!(PROBE & 4) && sum_bo) {
             s_db2[bo][e] += on ? g * w3a[e] : 0.f;
             s_dw3[bo][e] += g * (ok ? hv[e] : 0.f);
           }

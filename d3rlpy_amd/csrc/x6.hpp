@@ -97,3 +97,43 @@ __device__ __forceinline__ f32x16 prodn(const bf16x8* a, const bf16x8* b, f32x16
 
 }  // namespace x6
 }  // namespace d3a
+
+#include "../../include/d3rlpy_amd.h"
+
+namespace d3a {
+namespace x6 {
+
+// host: the input-row builder's fields are consistent (or it is off)
+inline bool xgen_ok(const d3a_mlp_fwd_desc& d) {
+  if (d.xg_mode == 0) return true;
+  return d.xg_mode >= 1 && d.xg_mode <= 4 && d.xg_obs && d.xg_a && d.xg_D >= 1 && d.xg_rep >= 1 &&
+         d.xg_E >= 1 && d.xg_D + d.xg_E == d.n_in && d.aux_rows == 0 && d.xg_lda >= d.xg_E &&
+         (d.xg_mode < 3 || d.xg_base != nullptr);
+}
+
+// element k of input row r of a forward pass: x itself, or the row the
+// descriptor's builder defines (d3a_mlp_fwd_desc.xg_mode; d3a_bcq_rows's
+// arithmetic, bcq.hip)
+__device__ __forceinline__ float input_at(const d3a_mlp_fwd_desc& d, const float* xb, int64_t ldx,
+                                          int r, int k) {
+  if (d.xg_mode == 0) return xb[(int64_t)r * ldx + k];
+  if (k < d.xg_D) return d.xg_obs[(int64_t)(r / d.xg_rep) * d.xg_D + k];
+  const int e = k - d.xg_D;
+  const float a = d.xg_a[(int64_t)r * d.xg_lda + e];
+  switch (d.xg_mode) {
+    case 1: return fminf(fmaxf(a, -d.xg_clip), d.xg_clip);
+    case 2: return tanhf(a);
+    case 3: {
+      const float res = __fmul_rn(d.xg_scale, tanhf(a));
+      return fminf(fmaxf(__fadd_rn(d.xg_base[(int64_t)r * d.xg_E + e], res), -1.f), 1.f);
+    }
+    default: {
+      const float res = __fmul_rn(d.xg_scale, tanhf(a));
+      const float base = tanhf(d.xg_base[(int64_t)r * d.xg_E + e]);
+      return fminf(fmaxf(__fadd_rn(base, res), -1.f), 1.f);
+    }
+  }
+}
+
+}  // namespace x6
+}  // namespace d3a

@@ -82,6 +82,9 @@ _FUSED_BM = int(os.environ.get("D3A_FUSED_BM", "0"))
 # in one launch (d3a_q2_bwd) for large critic passes (the K2 / K4 CQL critic:
 # 7,936 rows x 2 members); D3A_Q2_BWD=0 keeps the per-layer GEMM path
 _Q2 = os.environ.get("D3A_Q2_BWD", "1") == "1"
+# input rows built inside the x6 forwards (mlp.forward xgen); D3A_XGEN=0 keeps
+# the separate d3a_bcq_rows launch (A/B)
+_XGEN = os.environ.get("D3A_XGEN", "1") == "1"
 
 
 def q2_shape(net: EnsembleMLP) -> bool:
@@ -166,7 +169,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             members: Optional[int] = None, keep_h: bool = True,
             h_from: Optional[int] = None, aux: Optional[tuple] = None,
             skip_head: bool = False, out_parts: Optional[torch.Tensor] = None,
-            row_mean: Optional[torch.Tensor] = None) -> bool:
+            row_mean: Optional[torch.Tensor] = None, xgen=None) -> bool:
     """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
     (through its first ``members`` members only, when given).  ``keep_h``:
     store the hidden activations in ``acts.h`` (needed by a backward pass),
@@ -181,6 +184,10 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     each layer's launch carries it as a second batch dimension when its shape
     equals the main pass's (acts2.R == acts.R rows, same ldx); otherwise it is
     a separate forward.
+
+    ``xgen`` (a d3a_bcq_rows descriptor whose x is this pass's input ``x``):
+    the input rows are that builder's; the x6 kernels form them while staging
+    (d3a_mlp_fwd_desc.xg_*), any other path launches d3a_bcq_rows first.
 
     ``row_mean`` ([C][R] fp32): also the mean of each row's outputs, where the
     launch is d3a_mlp_fwd_x6 (its epilogue forms it); returns whether it was
@@ -242,6 +249,15 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         elif (not bf16 and not small and ops.CRITIC_GEMM == "x6" and x6_wide_shape(net)
               and out_parts is None and not d.aux_rows and n * C >= 8192):
             entry = "d3a_mlp_fwd_x6"  # wide head (e.g. BCQ's target QR critics)
+        if xgen is not None:
+            if (_XGEN and entry in ("d3a_q2_fwd_x6", "d3a_mlp_fwd_x6") and not d.aux_rows
+                    and r0 == 0):
+                d.xg_mode, d.xg_D, d.xg_rep, d.xg_E = xgen.mode, xgen.D, xgen.rep, xgen.E
+                d.xg_obs, d.xg_a, d.xg_lda = xgen.obs, xgen.a, xgen.lda
+                d.xg_base, d.xg_clip, d.xg_scale = xgen.base, xgen.clip, xgen.scale
+            else:
+                ops.call_desc("d3a_bcq_rows", xgen)
+            xgen = None
         means = row_mean is not None and entry == "d3a_mlp_fwd_x6"
         if means:
             assert tuple(row_mean.shape) == (C, R) and row_mean.dtype == torch.float32
@@ -250,6 +266,8 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         if aux is not None:
             forward(net, aux[0], aux[1], True, aux[2], aux[3], keep_h=False)
         return means
+    if xgen is not None:
+        ops.call_desc("d3a_bcq_rows", xgen)  # the per-layer path reads built rows
     L = net.n_layers
     inp, ld_in = x + 4 * r0 * ldx, ldx
     sxb_ = (0 if x_shared else R * ldx) if sxb is None else sxb

@@ -253,6 +253,16 @@ typedef struct d3a_mlp_fwd_desc {
    * compute_max_with_n_actions (q_functions/__init__.py:37-39), so that
    * d3a_bcq_target does not re-read every quantile row.                  */
   float* row_mean; int64_t s_mean;
+  /* Optional input-row builder (d3a_q2_fwd_x6 / d3a_mlp_fwd_x6 only, no aux
+   * pass; xg_mode 0: off, read x): the kernel forms input row r itself as
+   * d3a_bcq_rows would have written it -- (xg_obs[r / xg_rep][0..xg_D),
+   * f(xg_a[r][0..xg_E))), f by xg_mode: 1 clamp(a, -clip, clip), 2 tanh(a),
+   * 3 clamp(base + scale tanh(a), -1, 1), 4 as 3 with base = tanh(xg_base)
+   * (the raw decoder output; xg_base rows of xg_E) -- so BCQ's target chain
+   * (bcq_impl.py:215-226) needs no row-building launches.                */
+  int32_t xg_mode, xg_D, xg_rep, xg_E;
+  const float* xg_obs; const float* xg_a; int64_t xg_lda;
+  const float* xg_base; float xg_clip, xg_scale;
 } d3a_mlp_fwd_desc;
 #define D3A_MLP_PARTS 4
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);
@@ -832,7 +842,8 @@ int d3a_td3bc_actor_head(const d3a_td3bc_actor_desc* d, void* stream);
 /* x[r] = (obs[r / rep], f(a[r])), r < rows; f by mode: 0 copy, 1 clamp(a,
  * -clip, clip) (the clipped latent of bcq_impl.py:139,180), 2 tanh(a)
  * (ConditionalVAE.decode, imitators.py:70-72), 3 clamp(base + scale *
- * tanh(a), -1, 1) (DeterministicResidualPolicy.forward, policies.py:94-97);
+ * tanh(a), -1, 1) (DeterministicResidualPolicy.forward, policies.py:94-97),
+ * 4 as 3 with base = tanh(base) (the raw decoder output);
  * e_out (optional) also receives f(a).  Replaces _repeat_observation +
  * torch.cat of VectorEncoderWithAction (bcq_impl.py:163-187). */
 typedef struct d3a_bcq_rows_desc {

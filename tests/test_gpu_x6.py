@@ -331,3 +331,71 @@ def test_mlp_fwd_x6_wide_head_vs_fp64(entry, rows, n_in, n_out, keep):
     rel = float((out.double() - hs[2]).abs().max() / hs[2].abs().max())
     print(f"x6 wide forward vs fp64 end to end: {rel:.1e}")
     assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("entry,mode,n_out", [("d3a_q2_fwd_x6", 1, 6), ("d3a_q2_fwd_x6", 2, 6),
+                                              ("d3a_mlp_fwd_x6", 4, 200), ("d3a_q2_fwd_x6", 3, 1)])
+def test_x6_input_row_builder_matches_bcq_rows(entry, mode, n_out):
+    """The x6 forwards' in-kernel input rows (d3a_mlp_fwd_desc.xg_*: BCQ's target
+    chain, bcq_impl.py:215-226) give bitwise the outputs of the same kernel on
+    the rows d3a_bcq_rows writes (modes 1 clamp / 2 tanh / 3, 4 residual)."""
+    dev = torch.device("cuda")
+    C, D, E, rep, Bn = 2, 17, 6 if mode != 1 else 12, 10, 2048
+    rows = Bn * rep
+    n_in = D + E
+    gen = torch.Generator().manual_seed(mode * 7 + n_out)
+    sizes = [n_in, 256, 256, n_out]
+    Ws = [(torch.randn(C, sizes[l + 1], sizes[l], generator=gen) / np.sqrt(sizes[l])).to(dev)
+          for l in range(3)]
+    bs = [(torch.randn(C, sizes[l + 1], generator=gen) * 0.1).to(dev) for l in range(3)]
+    flat = torch.cat([W.reshape(-1) for W in Ws] + [b.reshape(-1) for b in bs])
+    offs, o = [], 0
+    for W in Ws:
+        offs.append(o)
+        o += W.numel()
+    boffs = []
+    for b in bs:
+        o = (o + 3) // 4 * 4
+        boffs.append(o)
+        o += b.numel()
+    buf = torch.zeros(o + 4, device=dev)
+    for W, of in zip(Ws, offs):
+        buf[of:of + W.numel()] = W.reshape(-1)
+    for b, of in zip(bs, boffs):
+        buf[of:of + b.numel()] = b.reshape(-1)
+    obs = torch.randn(Bn, D, generator=gen).to(dev)
+    a = (torch.randn(rows, E, generator=gen) * 1.5).to(dev)
+    base = torch.randn(rows, E, generator=gen).to(dev)
+    if mode == 3:
+        base = base.clamp(-1, 1)
+    ldx = (n_in + 3) // 4 * 4
+    x = torch.zeros(rows, ldx, device=dev)
+    r = N.BcqRowsDesc()
+    r.obs, r.D, r.rep, r.a, r.E, r.lda = obs.data_ptr(), D, rep, a.data_ptr(), E, E
+    r.base = base.data_ptr() if mode >= 3 else None
+    r.mode, r.clip, r.scale = mode, 0.5, 0.05
+    r.x, r.ldx, r.e_out, r.rows = x.data_ptr(), ldx, None, rows
+    outs = []
+    for fused in (False, True):
+        out = torch.full((C, rows, n_out), float("nan"), device=dev)
+        d = N.MlpFwdDesc()
+        d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
+        d.n_in, d.n_hidden, d.H, d.n_out = n_in, 2, 256, n_out
+        for l in range(3):
+            d.W[l], d.b[l] = buf.data_ptr() + 4 * offs[l], buf.data_ptr() + 4 * boffs[l]
+            d.sW[l], d.sb[l] = sizes[l + 1] * sizes[l], sizes[l + 1]
+        d.sh = rows * 256
+        d.out, d.sout, d.ldout = out.data_ptr(), rows * n_out, n_out
+        d.r0, d.rows, d.C, d.h_from = 0, rows, C, 0
+        if fused:
+            x.fill_(float("nan"))  # the kernel must not read x
+            d.xg_mode, d.xg_D, d.xg_rep, d.xg_E = mode, D, rep, E
+            d.xg_obs, d.xg_a, d.xg_lda = obs.data_ptr(), a.data_ptr(), E
+            d.xg_base, d.xg_clip, d.xg_scale = r.base, 0.5, 0.05
+        else:
+            ops.call_desc("d3a_bcq_rows", r)
+        ops.call_desc(entry, d)
+        torch.cuda.synchronize()
+        outs.append(out)
+    assert not torch.isnan(outs[0]).any()
+    assert torch.equal(outs[0], outs[1])
