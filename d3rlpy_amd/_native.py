@@ -273,6 +273,7 @@ class MlpFwdDesc(C.Structure):
         ("xg_mode", C.c_int32), ("xg_D", C.c_int32), ("xg_rep", C.c_int32), ("xg_E", C.c_int32),
         ("xg_obs", vp), ("xg_a", vp), ("xg_lda", C.c_int64),
         ("xg_base", vp), ("xg_clip", C.c_float), ("xg_scale", C.c_float),
+        ("hmask", vp), ("s_hmask", C.c_int64),
     ]
 
 
@@ -308,6 +309,7 @@ class Q2BwdDesc(C.Structure):
         ("n_in", C.c_int32), ("C", C.c_int32),
         ("dz2", vp), ("sdz", C.c_int64),
         ("block_rows", C.c_int32),
+        ("m2", vp), ("sm2", C.c_int64),
     ]
 
 
@@ -436,6 +438,15 @@ class IqnHeadBwdDesc(C.Structure):
     ]
 
 
+class IqnEmbedHeadDesc(C.Structure):
+    _fields_ = [
+        ("taus", vp), ("We", vp), ("be", vp), ("h", vp * IQN_MAX_GROUPS),
+        ("Wf", vp), ("bf", vp), ("q", vp), ("prior_out", vp), ("phi_out", vp),
+        ("rows", C.c_int64), ("group_rows", C.c_int64), ("n_keep", C.c_int64),
+        ("K", C.c_int32), ("E", C.c_int32), ("F", C.c_int32), ("A", C.c_int32),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "d3a_abi_version": (C.c_int, []),
@@ -513,6 +524,7 @@ _SIGNATURES = {
     "d3a_q2_fwd_x6": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_q2_bwd_x6": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
     "d3a_q2_fwd_x1": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
+    "d3a_iqn_embed_head": (C.c_int, [C.POINTER(IqnEmbedHeadDesc), vp]),
     "d3a_mlp_fwd_x6": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_x6_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_td3_prep": (C.c_int, [C.POINTER(Td3PrepDesc), vp]),

@@ -463,7 +463,8 @@ class _Workspace:
         bf16 = (ops.CRITIC_PRECISION == "bf16h" and mlp.q2_shape(impl.critic)
                 and mlp.q2_ok(impl.critic, 3 * NB + B))
         self.qacts = mlp.Acts.alloc(impl.critic, self.R, dev,
-                                    dtype=torch.bfloat16 if bf16 else torch.float32)
+                                    dtype=torch.bfloat16 if bf16 else torch.float32,
+                                    with_mask=not bf16 and mlp.q2_shape(impl.critic))
         self.tacts = mlp.Acts.alloc(impl.critic, B, dev)
         self.aacts = mlp.Acts.alloc(impl.critic, B, dev)
         self.dq = z(C, self.R)

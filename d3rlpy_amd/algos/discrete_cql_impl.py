@@ -26,6 +26,7 @@ online evaluations of obs share one encoder pass and its one backward.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -351,6 +352,11 @@ class _EncoderPass:
                        relu=True, variant=10 if n > 512 else -1)
 
 
+# the IQN head forward as one launch (d3a_iqn_embed_head); D3A_IQN_FUSED=0
+# keeps d3a_iqn_prior + the embed GEMM + d3a_iqn_head_fwd (A/B)
+_IQN_FUSED = os.environ.get("D3A_IQN_FUSED", "1") == "1"
+
+
 class _HeadPass:
     """IQN head forward buffers over `rows` quantile rows."""
 
@@ -363,8 +369,26 @@ class _HeadPass:
         self.rows = rows
 
     def launch(self, taus_ptr: int, h_groups: List[int], group_rows: int, K: int,
-               store: ParamStore) -> None:
+               store: ParamStore, n_keep: Optional[int] = None) -> None:
+        """q of every row; prior / phi of rows [0, n_keep) (all rows when
+        None) are left in self.prior / self.phi for a backward."""
         impl = self.impl
+        if (_IQN_FUSED and impl._E == 64 and impl._F % 64 == 0 and impl._F <= 512
+                and impl._action_size <= 8 and K % 32 == 0 and group_rows % K == 0):
+            # prior, embed + ReLU, product and head in one launch
+            # (d3a_iqn_embed_head; phi never round-trips HBM)
+            d = NAT.IqnEmbedHeadDesc()
+            d.taus, d.We, d.be = taus_ptr, store.ptr("q.embed.W"), store.ptr("q.embed.b")
+            for g, hp in enumerate(h_groups):
+                d.h[g] = hp
+            d.Wf, d.bf, d.q = store.ptr("q.fc.W"), store.ptr("q.fc.b"), self.q.data_ptr()
+            keep = self.rows if n_keep is None else n_keep
+            d.prior_out = self.prior.data_ptr() if keep else None
+            d.phi_out = self.phi.data_ptr() if keep else None
+            d.rows, d.group_rows, d.n_keep = self.rows, group_rows, keep
+            d.K, d.E, d.F, d.A = K, impl._E, impl._F, impl._action_size
+            ops.call_desc("d3a_iqn_embed_head", d)
+            return
         p = NAT.IqnPriorDesc()
         p.taus, p.prior, p.rows, p.E = taus_ptr, self.prior.data_ptr(), self.rows, impl._E
         ops.call_desc("d3a_iqn_prior", p)
@@ -571,9 +595,11 @@ class _Workspace:
                              F, B * F, 1, B, F, A, mask=h_obs, ldm=F, smb=B * F)
         else:
             # IQN heads: online rows [loss | lse | data | next], target rows
-            self.head.launch(self.taus.data_ptr(), [h_obs, h_obs, h_obs, h_next], BK, K, st)
+            # (the backward reads prior / phi of the three gradient passes only)
+            self.head.launch(self.taus.data_ptr(), [h_obs, h_obs, h_obs, h_next], BK, K, st,
+                             n_keep=3 * BK)
             self.head_t.launch(self.taus.data_ptr() + 4 * 4 * BK, [self.enc_t.h.data_ptr()], BK,
-                               K, tg)
+                               K, tg, n_keep=0)
             ops.call_desc("d3a_iqn_loss", self.loss_desc)
             # backward: head, embed, encoder (obs samples)
             ops.call_desc("d3a_iqn_head_bwd", self.head_bwd_desc)

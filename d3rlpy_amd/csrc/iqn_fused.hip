@@ -1,0 +1,200 @@
+// The IQN head's forward in one launch: the cosine prior, the embedding
+// Linear + ReLU and the head's product and Linear, per quantile row,
+//
+//   prior[r][e] = cos(pi (e + 1) tau[r])                      e < E
+//   phi[r][u]   = relu(sum_e prior[r][e] We[u][e] + be[u])    u < F
+//   q[r][a]     = sum_u (h[b(r)][u] * phi[r][u]) Wf[a][u] + bf[a]
+//
+// (compute_iqn_feature, iqn_q_function.py:33-47, and DiscreteIQNQFunction.
+// _compute_quantiles, iqn_q_function.py:82-88).  d3a_iqn_prior + the embed
+// GEMM + d3a_iqn_head_fwd wrote prior and phi ([rows][512] fp32: 268 MB for
+// K5's 131,072 online rows) and read them back; here phi stays in registers
+// and prior / phi are written only for the rows a backward needs (n_keep).
+//
+// The embedding product runs on the bf16 matrix cores with exact three-way
+// split-bf16 operands (x6.hpp: fp32-accurate).  A workgroup of F / 64 waves
+// walks row tiles of 32 rows; wave w owns units 64 w .. 64 w + 63 (two 32-unit
+// chunks) with its We rows split once into registers, and computes the
+// transposed tiles C^T[unit][row] (We the A operand, the tile's prior the B
+// operand from LDS), so a lane holds one row and 16 units per chunk: the
+// ReLU, the product with h (one b per tile: K % 32 == 0) and the dot with Wf
+// are register work, the per-row sums meet across waves in LDS (in wave order).
+#include "common.hpp"
+#include "../../include/d3rlpy_amd.h"
+#include "x6.hpp"
+
+namespace d3a {
+namespace {
+
+using namespace x6;
+
+constexpr int IF_RB = 32;       // rows per tile
+constexpr int IF_E = 64;        // embedding size (the factory default)
+constexpr int IF_LDP = IF_E + 8;  // bf16 row stride of the prior image
+constexpr int IF_AMAX = 8;      // actions handled here
+constexpr int IF_FMAX = 512;
+
+struct IfLds {
+  __bf16 pr[2][3][IF_RB * IF_LDP];         // prior parts [buf][part][row][e]
+  float qp[IF_FMAX / 64][IF_AMAX][IF_RB];  // per-wave head sums [wave][a][row]
+  float be[IF_FMAX], wf[IF_AMAX][IF_FMAX];
+};
+
+__global__ __launch_bounds__(512) void iqn_embed_head_kernel(d3a_iqn_embed_head_desc d) {
+  __shared__ __attribute__((aligned(16))) IfLds L;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nw = blockDim.x >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int F = d.F, A = d.A;
+  const int64_t ntiles = (d.rows + IF_RB - 1) / IF_RB;
+
+  // ---- prologue: bias / head rows to LDS; this wave's We rows split in registers
+  for (int i = t; i < F; i += blockDim.x) L.be[i] = d.be[i];
+  for (int i = t; i < IF_AMAX * F; i += blockDim.x) {
+    const int a = i / F;
+    L.wf[a][i - a * F] = a < A ? d.Wf[i] : 0.f;
+  }
+  bf16x8 wa[2][IF_E / 16][3];
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch) {
+    const float* wr = d.We + (int64_t)(64 * w + 32 * ch + li) * IF_E + 8 * lh;
+#pragma unroll
+    for (int s = 0; s < IF_E / 16; ++s) {
+      const float4 x0 = *reinterpret_cast<const float4*>(wr + 16 * s);
+      const float4 x1 = *reinterpret_cast<const float4*>(wr + 16 * s + 4);
+      const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      split8(v, wa[ch][s]);
+    }
+  }
+  const float pi_f = 3.14159265358979323846f;
+
+  // the prior of a tile: 32 rows x 64 values, four per thread (row t >> 4,
+  // e = 4 (t & 15) ..), as three bf16 parts; kept rows also to prior_out
+  auto stage_prior = [&](int64_t tile, int buf) {
+    for (int i = t; i < IF_RB * (IF_E / 4); i += blockDim.x) {
+      const int m = i >> 4, e4 = 4 * (i & 15);
+      const int64_t r = tile * IF_RB + m;
+      float v[4];
+      if (r < d.rows) {
+        const float tau = d.taus[r];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // torch: arange(1, E + 1) * pi, then * tau, cos (iqn_q_function.py:37-41)
+          const float ps = __fmul_rn(pi_f, (float)(e4 + j + 1));
+          v[j] = cosf(__fmul_rn(ps, tau));
+        }
+        if (d.prior_out && r < d.n_keep)
+          *reinterpret_cast<float4*>(d.prior_out + r * IF_E + e4) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = 0.f;
+      }
+      bf16x4 p[3];
+      split4(v, p);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&L.pr[buf][q][m * IF_LDP + e4]) = p[q];
+    }
+  };
+
+  int64_t tile = blockIdx.x;
+  if (tile < ntiles) stage_prior(tile, 0);
+  __syncthreads();  // be / wf / first prior staged
+  int buf = 0;
+  for (; tile < ntiles; tile += gridDim.x, buf ^= 1) {
+    const int64_t r0 = tile * IF_RB;
+    const int64_t row = r0 + li;
+    // b of the tile (K % 32 == 0: one b per 32-row tile)
+    const int g = (int)(r0 / d.group_rows);
+    const int64_t b = (r0 - (int64_t)g * d.group_rows) / d.K;
+    const float* hb = d.h[g] + b * F;
+    const bool keep = d.phi_out != nullptr && row < d.n_keep;
+    float qa[IF_AMAX];
+#pragma unroll
+    for (int a = 0; a < IF_AMAX; ++a) qa[a] = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < IF_E / 16; ++s) {
+        bf16x8 bp[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          bp[q] = *reinterpret_cast<const bf16x8*>(&L.pr[buf][q][li * IF_LDP + 16 * s + 8 * lh]);
+        acc = prod6(wa[ch][s], bp, acc);
+      }
+      // lane: row li, units 64 w + 32 ch + 8 R + 4 lh + i (register 4 R + i)
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const int u = 64 * w + 32 * ch + 8 * R + 4 * lh;
+        const float4 bv = *reinterpret_cast<const float4*>(&L.be[u]);
+        const float4 hv = *reinterpret_cast<const float4*>(hb + u);
+        const float bb[4] = {bv.x, bv.y, bv.z, bv.w}, hh[4] = {hv.x, hv.y, hv.z, hv.w};
+        float ph[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ph[i] = fmaxf(acc[4 * R + i] + bb[i], 0.f);
+        if (keep)
+          *reinterpret_cast<float4*>(d.phi_out + row * F + u) = make_float4(ph[0], ph[1], ph[2], ph[3]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = __fmul_rn(hh[i], ph[i]);  // prod = h * phi
+#pragma unroll
+          for (int a = 0; a < IF_AMAX; ++a)
+            if (a < A) qa[a] = fmaf(p, L.wf[a][u + i], qa[a]);
+        }
+      }
+    }
+    // the next tile's prior (other buffer) while the sums meet
+    if (tile + gridDim.x < ntiles) stage_prior(tile + gridDim.x, buf ^ 1);
+#pragma unroll
+    for (int a = 0; a < IF_AMAX; ++a) {
+      if (a >= A) break;
+      const float o = __shfl_xor(qa[a], 32, 64);
+      if (lh == 0) L.qp[w][a][li] = qa[a] + o;
+    }
+    __syncthreads();  // wave sums in LDS; next prior staged
+    for (int i = t; i < IF_RB * A; i += blockDim.x) {
+      const int m = i / A, a = i - m * A;
+      const int64_t r = r0 + m;
+      if (r >= d.rows) continue;
+      float s = L.qp[0][a][m];
+      for (int v = 1; v < nw; ++v) s += L.qp[v][a][m];
+      d.q[r * A + a] = s + d.bf[a];
+    }
+    __syncthreads();  // qp read before the next tile's sums
+  }
+}
+
+}  // namespace
+}  // namespace d3a
+
+using namespace d3a;
+
+extern "C" int d3a_iqn_embed_head(const d3a_iqn_embed_head_desc* dp, void* stream) {
+  D3A_CHECK_ARG(dp, "d3a_iqn_embed_head: null desc");
+  const d3a_iqn_embed_head_desc& d = *dp;
+  D3A_CHECK_ARG(d.taus && d.We && d.be && d.Wf && d.bf && d.q, "d3a_iqn_embed_head: null pointer");
+  D3A_CHECK_ARG(d.E == IF_E, "d3a_iqn_embed_head: embed size must be 64");
+  D3A_CHECK_ARG(d.F >= 64 && d.F <= IF_FMAX && d.F % 64 == 0, "d3a_iqn_embed_head: F must be 64..512, %64");
+  D3A_CHECK_ARG(d.A >= 1 && d.A <= IF_AMAX, "d3a_iqn_embed_head: 1..8 actions");
+  D3A_CHECK_ARG(d.K >= 32 && d.K % 32 == 0 && d.rows >= 0 && d.group_rows > 0 &&
+                    d.group_rows % d.K == 0 && d.n_keep >= 0 && d.n_keep <= d.rows,
+                "d3a_iqn_embed_head: K must be a multiple of 32 dividing group_rows");
+  const int64_t G = (d.rows + d.group_rows - 1) / d.group_rows;
+  D3A_CHECK_ARG(G <= D3A_IQN_MAX_GROUPS, "d3a_iqn_embed_head: too many row groups");
+  for (int64_t g = 0; g < G; ++g) D3A_CHECK_ARG(d.h[g], "d3a_iqn_embed_head: null feature group");
+  auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  for (int64_t g = 0; g < G; ++g) D3A_CHECK_ARG(a16(d.h[g]), "d3a_iqn_embed_head: h must be 16-byte aligned");
+  D3A_CHECK_ARG(a16(d.We) && (d.prior_out == nullptr || a16(d.prior_out)) &&
+                    (d.phi_out == nullptr || a16(d.phi_out)),
+                "d3a_iqn_embed_head: We, prior_out and phi_out must be 16-byte aligned");
+  if (d.rows == 0) return 0;
+  const int64_t ntiles = (d.rows + IF_RB - 1) / IF_RB;
+  const int64_t grid = ntiles < 256 ? ntiles : 256;  // one workgroup per CU, tiles strided
+  hipLaunchKernelGGL(iqn_embed_head_kernel, dim3((unsigned)grid), dim3(64 * (d.F / 64)), 0,
+                     (hipStream_t)stream, d);
+  D3A_LAUNCH_CHECK("d3a_iqn_embed_head");
+  return 0;
+}

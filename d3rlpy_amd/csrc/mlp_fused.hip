@@ -303,6 +303,7 @@ extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
   D3A_CHECK_ARG(d_in, "d3a_mlp_fwd: null desc");
   D3A_CHECK_ARG(d_in->row_mean == nullptr, "d3a_mlp_fwd: row_mean is d3a_mlp_fwd_x6 only");
   D3A_CHECK_ARG(d_in->xg_mode == 0, "d3a_mlp_fwd: no input-row builder (xg_mode)");
+  D3A_CHECK_ARG(d_in->hmask == nullptr, "d3a_mlp_fwd: hmask is d3a_q2_fwd_x6 only");
   d3a_mlp_fwd_desc d = *d_in;
   D3A_CHECK_ARG(d.x && d.out, "d3a_mlp_fwd: null input / output");
   D3A_CHECK_ARG(d.n_hidden >= 1 && d.n_hidden <= D3A_MLP_MAX_HIDDEN,

@@ -344,6 +344,7 @@ extern "C" int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
                     d.b[2],
                 "d3a_mlp_fwd_x6: null operand");
   D3A_CHECK_ARG(xgen_ok(d), "d3a_mlp_fwd_x6: bad input-row builder (xg_*)");
+  D3A_CHECK_ARG(d.hmask == nullptr, "d3a_mlp_fwd_x6: hmask is d3a_q2_fwd_x6 only");
   D3A_CHECK_ARG(d.aux_rows == 0 && d.parts <= 1, "d3a_mlp_fwd_x6: no aux pass / parts");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.r0 >= 0 && d.h_from >= 0, "d3a_mlp_fwd_x6: bad sizes");
   auto a16 = [](const void* p, int64_t stride) {

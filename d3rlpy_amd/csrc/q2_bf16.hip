@@ -578,6 +578,7 @@ extern "C" int d3a_q2_fwd_bf16(const d3a_mlp_fwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_fwd_bf16: null desc");
   D3A_CHECK_ARG(dp->row_mean == nullptr, "d3a_q2_fwd_bf16: row_mean is d3a_mlp_fwd_x6 only");
   D3A_CHECK_ARG(dp->xg_mode == 0, "d3a_q2_fwd_bf16: no input-row builder (xg_mode)");
+  D3A_CHECK_ARG(dp->hmask == nullptr, "d3a_q2_fwd_bf16: hmask is d3a_q2_fwd_x6 only");
   const d3a_mlp_fwd_desc& d = *dp;
   D3A_CHECK_ARG(d.x && d.out, "d3a_q2_fwd_bf16: null input / output");
   D3A_CHECK_ARG(d.n_hidden == 2 && d.H == B_H && d.n_out == 1,
@@ -641,6 +642,7 @@ extern "C" int d3a_q2_bwd_bf16(const d3a_q2_bwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_bwd_bf16: null desc");
   const d3a_q2_bwd_desc& d = *dp;
   D3A_CHECK_ARG(d.x && d.h1 && d.h2 && d.g && d.W2 && d.w3, "d3a_q2_bwd_bf16: null input");
+  D3A_CHECK_ARG(d.m2 == nullptr, "d3a_q2_bwd_bf16: the mask image is d3a_q2_bwd_x6 only");
   D3A_CHECK_ARG(d.dW1 && d.db1 && d.dW2 && d.db2 && d.dW3 && d.db3, "d3a_q2_bwd_bf16: null output");
   D3A_CHECK_ARG(d.n_in >= 1 && d.n_in <= 48, "d3a_q2_bwd_bf16: n_in must be 1..48");
   D3A_CHECK_ARG(d.dz2 == nullptr && (d.block_rows == 0 || d.block_rows == 256),

@@ -427,6 +427,7 @@ using namespace d3a;
 extern "C" int d3a_q2_bwd(const d3a_q2_bwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_bwd: null desc");
   const d3a_q2_bwd_desc& d = *dp;
+  D3A_CHECK_ARG(d.m2 == nullptr, "d3a_q2_bwd: the mask image is d3a_q2_bwd_x6 only");
   const bool dzin = d.dz2 != nullptr;
   D3A_CHECK_ARG(d.x && d.h1 && d.W2 && (dzin || (d.h2 && d.g && d.w3)), "d3a_q2_bwd: null input");
   D3A_CHECK_ARG(d.dW1 && d.db1 && d.dW2 && d.db2 && (dzin || (d.dW3 && d.db3)),

@@ -96,6 +96,9 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   const int nin = d.n_in;
   HT* const h0g = (!aux && d.h[0]) ? reinterpret_cast<HT*>(d.h[0]) + c * d.sh : nullptr;
   HT* const h1g = (!aux && d.h[1]) ? reinterpret_cast<HT*>(d.h[1]) + c * d.sh : nullptr;
+  // the ReLU mask image of the last hidden layer (kept rows; NO == 1)
+  __bf16* const hmg = (!aux && NO == 1 && d.hmask) ? reinterpret_cast<__bf16*>(d.hmask) + c * d.s_hmask
+                                                   : nullptr;
   // a kept run of four activations (16 bytes fp32, 8 bytes bf16)
   auto put4 = [](HT* p, const float* v) {
     if constexpr (sizeof(HT) == 4) {
@@ -371,6 +374,15 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
       for (int R = 0; R < 4; ++R) put4(h1g + row * X_H + 32 * w + 8 * R + 4 * lh, v + 4 * R);
     }
+    if (hmg != nullptr && row >= h_from && row < rend) {
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        bf16x4 mk;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mk[i] = v[4 * R + i] > 0.f ? (__bf16)1.f : (__bf16)0.f;
+        *reinterpret_cast<bf16x4*>(hmg + (int64_t)row * X_H + 32 * w + 8 * R + 4 * lh) = mk;
+      }
+    }
     float hs = v[0] * ww[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) hs = fmaf(v[r], ww[r], hs);
@@ -406,6 +418,10 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
                     d.b[2],
                 "d3a_q2_fwd_x6: null operand");
   D3A_CHECK_ARG(xgen_ok(d), "d3a_q2_fwd_x6: bad input-row builder (xg_*)");
+  D3A_CHECK_ARG(d.hmask == nullptr ||
+                    (d.n_out == 1 && (reinterpret_cast<uintptr_t>(d.hmask) & 15) == 0 &&
+                     d.s_hmask % 8 == 0 && d.s_hmask >= (d.r0 + d.rows) * X_H),
+                "d3a_q2_fwd_x6: hmask needs one output and 16-byte aligned rows of 256 bf16");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.r0 >= 0 && d.h_from >= 0 && d.aux_rows >= 0,
                 "d3a_q2_fwd_x6: bad sizes");
   auto a16 = [](const void* p, int64_t stride) {
@@ -486,6 +502,7 @@ extern "C" int d3a_q2_fwd_x1(const d3a_mlp_fwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_fwd_x1: null desc");
   D3A_CHECK_ARG(dp->row_mean == nullptr, "d3a_q2_fwd_x1: row_mean is d3a_mlp_fwd_x6 only");
   D3A_CHECK_ARG(dp->xg_mode == 0, "d3a_q2_fwd_x1: no input-row builder");
+  D3A_CHECK_ARG(dp->hmask == nullptr, "d3a_q2_fwd_x1: hmask is d3a_q2_fwd_x6 only");
   const d3a_mlp_fwd_desc& e = *dp;  // d3a_q2_fwd_x6's contract
   D3A_CHECK_ARG(e.n_hidden == 2 && e.H == X_H && e.n_out == 1 && e.n_in >= 1 && e.n_in <= 48,
                 "d3a_q2_fwd_x1: needs [n_in <= 48, 256, 256, 1]");

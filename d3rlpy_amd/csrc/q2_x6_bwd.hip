@@ -35,6 +35,7 @@
 // The head's gradients (dW3 = g'^T h2, db3 = sum g') and db2 = sum dz2 are
 // accumulated in fp64 at staging, exactly as q2_bwd.hip forms them.
 #include <cstdlib>
+#include <type_traits>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
 #include "x6.hpp"
@@ -68,13 +69,41 @@ struct B6Lds {
   float gp[3][B6_SB];              // g' of the rows
 };
 
+// MI (mask image; d.m2 given): the forward wrote the ReLU mask of h2 as bf16
+// 0 / 1 rows [r][o] (d3a_mlp_fwd_desc.hmask), so the dW2 waves' staging is a
+// copy: one [r][o] image per sub-block, 16-byte chunks XOR-swizzled by row
+// (mchunk), read by rows (ds_read_b128) as the dh1 product's A operand and
+// transposed (ds_read_b64_tr_b16) as the dW2 product's -- both conflict-free
+// -- instead of two mask images built from h2 by VALU.  The quarter's db2 /
+// dW3 sums read h2 for their 64 o only.
+struct B7Buf {
+  __bf16 mro[B6_SB * B6_H];        // m[r][o], chunk-swizzled rows of 512 B
+  __bf16 hg[3][B6_QW * B6_LR];     // parts of g'[r] h1[r][i0 + i], [i][r]
+};
+
+struct B7Lds {
+  B7Buf b[2];
+  float ex[2][2 * 2 * 16 * 64];
+  __bf16 h1m[3][B6_QW * B6_LR];
+  float gp[3][B6_SB];
+};
+
+// element offset of 16-byte chunk c (o = 8 c .. 8 c + 7) of row r in a B7 mask image
+__device__ __forceinline__ int mchunk(int r, int c) {
+  return r * B6_H + 8 * (c ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+}
+
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+
 // NDB: 32-wide input blocks of dW1 (n_in <= 32 NDB).  PROBE (timing probes
 // only, D3A_X6_PROBE >> 3; results are wrong): bit 0 skips the staging after
 // the first sub-block, bit 1 the dX waves' finishing work, bit 2 the fp64 sums
-template <int NDB, int PROBE = 0>
+template <int NDB, int PROBE = 0, bool MI = false>
 __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
-  __shared__ __attribute__((aligned(16))) B6Lds L;
-  static_assert(sizeof(B6Lds) <= 163840, "LDS");
+  using Lds = typename std::conditional<MI, B7Lds, B6Lds>::type;
+  __shared__ __attribute__((aligned(16))) Lds L;
+  static_assert(sizeof(Lds) <= 163840, "LDS");
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int li = lane & 31, lh = lane >> 5;
@@ -132,6 +161,15 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
   float4 h2v[2][4];
   float ga[4];
   float h1v[8], gh[8];
+  // MI: the dW2 waves copy mask chunk mc of rows mr + 8 k, and sum db2 / dW3
+  // of o = i0 + (t2 & 63) over rows (t2 >> 6) + 4 k
+  const __bf16* m2g = MI ? reinterpret_cast<const __bf16*>(d.m2) + c * d.sm2 : nullptr;
+  const int mc = t2 & 31, mr = t2 >> 5;
+  const int so = t2 & 63, sr = t2 >> 6;
+  uint4 mk4[4];
+  // (the dW2 waves' h2 / g' of the sums reuse the dX waves' h1v / gh: one
+  // pair of arrays for both roles keeps them in registers)
+  float s_db2m = 0.f, s_dw3m = 0.f;
   auto load_sb = [&](int sb) {
     const int base = rb0 + sb * B6_SB;
     if (role_dx) {
@@ -139,6 +177,18 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
       for (int k = 0; k < 8; ++k) {
         const int r = min(base + rh + k, rlast);
         h1v[k] = h1g[r * B6_H + i0 + ih];
+        gh[k] = gprime(r);
+      }
+    } else if constexpr (MI) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = min(base + mr + 8 * k, rlast);
+        mk4[k] = *reinterpret_cast<const uint4*>(m2g + r * B6_H + 8 * mc);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = min(base + sr + 4 * k, rlast);
+        h1v[k] = h2g[r * B6_H + i0 + so];
         gh[k] = gprime(r);
       }
     } else {
@@ -153,7 +203,7 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
     }
   };
   auto stage_sb = [&](int sb) {
-    B6Buf& B = L.b[sb & 1];
+    auto& B = L.b[sb & 1];
     const int base = rb0 + sb * B6_SB;
     if (role_dx) {
       const int slot = sb % 3;
@@ -180,6 +230,32 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
       }
       return;
     }
+    if constexpr (MI) {
+      // the mask rows (rows past the end: zero, as the float path stages them)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int rr = mr + 8 * k;
+        const bool ok = base + rr < rows && sb < B6_NSB;
+        *reinterpret_cast<uint4*>(&B.mro[mchunk(rr, mc)]) = ok ? mk4[k] : make_uint4(0u, 0u, 0u, 0u);
+      }
+      // the quarter's db2 / dW3 / db3 terms, in row order per thread
+      const float w3o = w3g[i0 + so];
+      float pg = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool ok = base + sr + 4 * k < rows && sb < B6_NSB;
+        const float g = ok ? gh[k] : 0.f;
+        const float hv = h1v[k];
+        const bool on = ok && hv > 0.f;
+        if (!(PROBE & 4)) {
+          s_db2m += on ? g * w3o : 0.f;
+          s_dw3m += g * (ok ? hv : 0.f);
+        }
+        pg += g;
+      }
+      if (so == 0) s_db3 += (double)pg;
+      return;
+    } else {
     float pg = 0.f;
     // db2 / dW3 are written for this workgroup's quarter of o only
     // (o = i0 .. i0 + 63: half bo = q >> 1, oa >> 6 = q & 1 -- wave-uniform,
@@ -219,6 +295,7 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
       }
     }
     if (t2 < 8) s_db3 += (double)pg;
+    }
   };
 
   f32x16 W1acc[NDB];  // dX waves: dW1 over the rows they finish
@@ -301,14 +378,19 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
     __syncthreads();  // sub-block 0 staged
 #pragma unroll 1
     for (int sb = 0; sb < B6_NSB; ++sb) {
-      const B6Buf& B = L.b[sb & 1];
+      const auto& B = L.b[sb & 1];
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const __bf16* A = &B.mro[li * B6_LRO + 128 * kh + 8 * lh];
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + 16 * s);
+        bf16x8 a;
+        if constexpr (MI) {
+          // mask row li, o = 128 kh + 16 s + 8 lh .. + 7: chunk 16 kh + 2 s + lh
+          a = *reinterpret_cast<const bf16x8*>(&B.mro[mchunk(li, 16 * kh + 2 * s + lh)]);
+        } else {
+          a = *reinterpret_cast<const bf16x8*>(&B.mro[li * B6_LRO + 128 * kh + 8 * lh + 16 * s]);
+        }
         acc = x3m(a, wb[s], acc);
         if (s == 1 && sb > 0 && !(PROBE & 2)) finish(sb - 1);
         if (s == 3 && sb > 0) load_fin(sb);
@@ -329,13 +411,33 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
     __syncthreads();  // sub-block 0 staged
 #pragma unroll 1
     for (int sb = 0; sb < B6_NSB; ++sb) {
-      const B6Buf& B = L.b[sb & 1];
+      const auto& B = L.b[sb & 1];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 a[2], hb[2][3];
 #pragma unroll
-        for (int ob = 0; ob < 2; ++ob)
-          a[ob] = *reinterpret_cast<const bf16x8*>(&B.mor[(ob0 + 32 * ob + li) * B6_LR + 16 * s + 8 * lh]);
+        for (int ob = 0; ob < 2; ++ob) {
+          if constexpr (MI) {
+            // A[o = ob0 + 32 ob + (lane & 31)][r = 16 s + 8 lh + j] from the
+            // [r][o] image by two transposed reads: 16-lane group G takes the
+            // 4 x 16 block at rows 16 s + 8 (G >> 1) (+ 4), columns
+            // ob0 + 32 ob + 16 (G & 1); lane 4 qq + p of the group addresses
+            // row qq, columns 4 p .. 4 p + 3
+            const int G = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
+            const int cb = (ob0 + 32 * ob) / 8 + 2 * (G & 1) + (p >> 1);
+            const int r0 = 16 * s + 8 * (G >> 1) + qq;
+            const __bf16* m0 = &B.mro[mchunk(r0, cb) + 4 * (p & 1)];
+            const __bf16* m1 = &B.mro[mchunk(r0 + 4, cb) + 4 * (p & 1)];
+            const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) i16x4*)(m0));
+            const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) i16x4*)(m1));
+            const i16x8 v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            a[ob] = __builtin_bit_cast(bf16x8, v8);
+          } else {
+            a[ob] = *reinterpret_cast<const bf16x8*>(&B.mor[(ob0 + 32 * ob + li) * B6_LR + 16 * s + 8 * lh]);
+          }
+        }
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -370,8 +472,12 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
   __syncthreads();
   const int64_t pc = p * d.C + c;
   float* w1s = reinterpret_cast<float*>(&L.b[0].mro[0]);             // [ib][db][16][64]
-  double* db1s = reinterpret_cast<double*>(&L.b[0].mor[0]);          // [ib][64]
-  double* hs = reinterpret_cast<double*>(&L.b[1].mro[0]);            // [256][2][2][4], over mro + mor
+  // [ib][64]
+  double* db1s;
+  if constexpr (MI) db1s = reinterpret_cast<double*>(&L.b[0].hg[0][0]);
+  else db1s = reinterpret_cast<double*>(&L.b[0].mor[0]);
+  // [256][2][2][4] over mro + mor (MI: [4][64][2] over mro)
+  double* hs = reinterpret_cast<double*>(&L.b[1].mro[0]);
   double* db3s = reinterpret_cast<double*>(&L.b[1].hg[0][0]);        // [8]
   if (role_dx && kh == 1) {
 #pragma unroll
@@ -381,14 +487,20 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
     db1s[ib * 64 + lane] = s_db1;
   }
   if (!role_dx) {
+    if constexpr (MI) {
+      hs[(sr * 64 + so) * 2 + 0] = (double)s_db2m;
+      hs[(sr * 64 + so) * 2 + 1] = (double)s_dw3m;
+      if (so == 0) db3s[sr] = s_db3;
+    } else {
 #pragma unroll
-    for (int bo = 0; bo < 2; ++bo)
+      for (int bo = 0; bo < 2; ++bo)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        hs[((t2 * 2 + bo) * 2 + 0) * 4 + e] = (double)s_db2[bo][e];
-        hs[((t2 * 2 + bo) * 2 + 1) * 4 + e] = (double)s_dw3[bo][e];
-      }
-    if (t2 < 8) db3s[t2] = s_db3;
+        for (int e = 0; e < 4; ++e) {
+          hs[((t2 * 2 + bo) * 2 + 0) * 4 + e] = (double)s_db2[bo][e];
+          hs[((t2 * 2 + bo) * 2 + 1) * 4 + e] = (double)s_dw3[bo][e];
+        }
+      if (t2 < 8) db3s[t2] = s_db3;
+    }
   }
   __syncthreads();
   if (role_dx && kh == 0) {
@@ -410,18 +522,26 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
   // threads holding o's column (rows 4 v .. 4 v + 3 of each sub-block), in order
   if (t >= 256 && t < 320) {
     const int tt = t - 256, o = i0 + tt;
-    const int bo = o >> 7, oo = o & 127;
-    const int tb = (oo >> 2) << 3, e = oo & 3;
     double s2 = 0.0, s3 = 0.0;
-    for (int v = 0; v < 8; ++v) {
-      s2 += hs[(((tb + v) * 2 + bo) * 2 + 0) * 4 + e];
-      s3 += hs[(((tb + v) * 2 + bo) * 2 + 1) * 4 + e];
+    if constexpr (MI) {
+      // the four threads of o (rows sr + 4 k of each sub-block), in order
+      for (int v = 0; v < 4; ++v) {
+        s2 += hs[(v * 64 + tt) * 2 + 0];
+        s3 += hs[(v * 64 + tt) * 2 + 1];
+      }
+    } else {
+      const int bo = o >> 7, oo = o & 127;
+      const int tb = (oo >> 2) << 3, e = oo & 3;
+      for (int v = 0; v < 8; ++v) {
+        s2 += hs[(((tb + v) * 2 + bo) * 2 + 0) * 4 + e];
+        s3 += hs[(((tb + v) * 2 + bo) * 2 + 1) * 4 + e];
+      }
     }
     d.db2[pc * B6_H + o] = (float)s2;
     d.dW3[pc * B6_H + o] = (float)s3;
   } else if (t == 320 && q == 0) {
     double sg = 0.0;
-    for (int v = 0; v < 8; ++v) sg += db3s[v];
+    for (int v = 0; v < (MI ? 4 : 8); ++v) sg += db3s[v];
     d.db3[pc] = (float)sg;
   }
 }
@@ -447,6 +567,9 @@ extern "C" int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(d.ldx >= d.n_in, "d3a_q2_bwd_x6: ldx < n_in");
   D3A_CHECK_ARG(d.rows * (d.ldh > d.ldx ? d.ldh : d.ldx) < (int64_t(1) << 31),
                 "d3a_q2_bwd_x6: rows x row stride exceeds 2^31");
+  D3A_CHECK_ARG(d.m2 == nullptr || ((reinterpret_cast<uintptr_t>(d.m2) & 15) == 0 && d.sm2 % 8 == 0 &&
+                                    d.sm2 >= d.rows * B6_H),
+                "d3a_q2_bwd_x6: the mask image must be 16-byte aligned rows of 256 bf16");
   if (d.rows == 0) return 0;
   const int64_t units = ((d.rows + B6_RB - 1) / B6_RB) * d.C;
   const int64_t blocks = (units + 7) / 8 * 32;
@@ -456,7 +579,7 @@ extern "C" int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* dp, void* stream) {
     const char* e = getenv("D3A_X6_PROBE");
     return e ? atoi(e) >> 3 : 0;
   }();
-  if (probe && d.n_in <= 32) {
+  if (probe && d.n_in <= 32 && d.m2 == nullptr) {
     const hipStream_t st = (hipStream_t)stream;
     switch (probe & 7) {
       case 1: hipLaunchKernelGGL((q2x6_bwd_kernel<1, 1>), grid, block, 0, st, d); break;
@@ -468,7 +591,12 @@ extern "C" int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* dp, void* stream) {
     D3A_LAUNCH_CHECK("d3a_q2_bwd_x6");
     return 0;
   }
-  if (d.n_in <= 32)
+  const bool mi = d.m2 != nullptr;
+  if (d.n_in <= 32 && mi)
+    hipLaunchKernelGGL((q2x6_bwd_kernel<1, 0, true>), grid, block, 0, (hipStream_t)stream, d);
+  else if (mi)
+    hipLaunchKernelGGL((q2x6_bwd_kernel<2, 0, true>), grid, block, 0, (hipStream_t)stream, d);
+  else if (d.n_in <= 32)
     hipLaunchKernelGGL(q2x6_bwd_kernel<1>, grid, block, 0, (hipStream_t)stream, d);
   else
     hipLaunchKernelGGL(q2x6_bwd_kernel<2>, grid, block, 0, (hipStream_t)stream, d);

@@ -36,14 +36,23 @@ def n_splits(rows: int, min_rows: int = 32, max_splits: int = 32) -> int:
 
 @dataclass
 class Acts:
-    """Activation buffers of one forward pass: h[l] is [C][R][H_l] (trunk)."""
+    """Activation buffers of one forward pass: h[l] is [C][R][H_l] (trunk);
+    ``hmask`` (optional, ``with_mask``): the last hidden layer's ReLU mask as
+    bf16 0 / 1 rows [C][R][H], written by the split-bf16 x6 Q forward for the
+    kept rows and read by its backward (d3a_mlp_fwd_desc.hmask / d3a_q2_bwd_
+    desc.m2)."""
 
     h: List[torch.Tensor]
     out: torch.Tensor  # [C][R] (single output) or [C][R][out]
     R: int
+    hmask: Optional[torch.Tensor] = None
+    # first row of the mask image the last forward wrote (None: not written;
+    # the backward then builds the mask from h2)
+    hmask_from: Optional[int] = None
 
     @staticmethod
-    def alloc(net: EnsembleMLP, R: int, device, dtype=torch.float32) -> "Acts":
+    def alloc(net: EnsembleMLP, R: int, device, dtype=torch.float32,
+              with_mask: bool = False) -> "Acts":
         """``dtype`` bfloat16: kept activations for the bf16 critic kernels
         (d3a_q2_fwd_bf16 / d3a_q2_bwd_bf16 are then selected by forward /
         backward); outputs stay fp32."""
@@ -51,7 +60,10 @@ class Acts:
               for l in range(net.n_layers - 1)]
         out_dim = net.sizes[-1]
         out = torch.zeros((net.C, R) if out_dim == 1 else (net.C, R, out_dim), device=device)
-        return Acts(hs, out, R)
+        hm = None
+        if with_mask and net.n_layers >= 2:
+            hm = torch.zeros(net.C, R, net.sizes[-2], device=device, dtype=torch.bfloat16)
+        return Acts(hs, out, R, hm)
 
 
 # one-launch forward (d3a_mlp_fwd) unless D3A_FUSED_MLP=0 (per-layer GEMMs,
@@ -85,6 +97,9 @@ _Q2 = os.environ.get("D3A_Q2_BWD", "1") == "1"
 # input rows built inside the x6 forwards (mlp.forward xgen); D3A_XGEN=0 keeps
 # the separate d3a_bcq_rows launch (A/B)
 _XGEN = os.environ.get("D3A_XGEN", "1") == "1"
+# the x6 critic backward reads the forward's bf16 mask image of h2 instead of
+# building it from h2 (D3A_MASK_IMAGE=0: build it, A/B)
+_MASK_IMAGE = os.environ.get("D3A_MASK_IMAGE", "1") == "1"
 
 
 def q2_shape(net: EnsembleMLP) -> bool:
@@ -200,6 +215,8 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     R = acts.R
     r1 = R if r1 is None else r1
     n = r1 - r0
+    if acts.hmask is not None:
+        acts.hmask_from = None  # set below where this forward writes the mask image
     if n <= 0:
         return False
     C = net.C if members is None else members
@@ -258,6 +275,10 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             else:
                 ops.call_desc("d3a_bcq_rows", xgen)
             xgen = None
+        if acts.hmask is not None:
+            if (entry == "d3a_q2_fwd_x6" and keep_h and members is None and sizes[-1] == 1):
+                d.hmask, d.s_hmask = acts.hmask.data_ptr(), R * sizes[-2]
+                acts.hmask_from = d.h_from
         means = row_mean is not None and entry == "d3a_mlp_fwd_x6"
         if means:
             assert tuple(row_mean.shape) == (C, R) and row_mean.dtype == torch.float32
@@ -416,6 +437,10 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         entry = "d3a_q2_bwd_bf16" if esz == 2 else "d3a_q2_bwd"
         if esz == 4 and (ops.CRITIC_GEMM == "x6" or ops.CRITIC_PRECISION == "bf16"):
             entry = "d3a_q2_bwd_x6"  # fp32-accurate split-bf16 (mask-factored)
+            if (acts.hmask is not None and acts.hmask_from is not None
+                    and acts.hmask_from <= r0 and _MASK_IMAGE):
+                # the forward's mask image of h2 (same rows as h1 / h2)
+                d.m2, d.sm2 = acts.hmask.data_ptr() + 2 * r0 * H, R * H
         ops.call_desc(entry, d)
         return None
 

@@ -263,6 +263,11 @@ typedef struct d3a_mlp_fwd_desc {
   int32_t xg_mode, xg_D, xg_rep, xg_E;
   const float* xg_obs; const float* xg_a; int64_t xg_lda;
   const float* xg_base; float xg_clip, xg_scale;
+  /* Optional (d3a_q2_fwd_x6 with one output only): the ReLU mask of the last
+   * hidden layer of the kept rows (>= h_from) as bf16 0 / 1, [C][rows][256]
+   * (member stride s_hmask elements, 16-byte aligned rows) -- the operand
+   * image d3a_q2_bwd_x6 reads (d3a_q2_bwd_desc.m2).                       */
+  void* hmask; int64_t s_hmask;
 } d3a_mlp_fwd_desc;
 #define D3A_MLP_PARTS 4
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);
@@ -332,6 +337,10 @@ typedef struct d3a_q2_bwd_desc {
    * actor pass spread over ceil(rows / 32) * 4 workgroups). */
   const float* dz2; int64_t sdz;
   int32_t block_rows;
+  /* Optional (d3a_q2_bwd_x6 only): the forward's bf16 0 / 1 mask image of h2
+   * (d3a_mlp_fwd_desc.hmask; rows at the same base as h1 / h2, member stride
+   * sm2) -- the ReLU-mask operand is then copied, not built from h2.       */
+  const void* m2; int64_t sm2;
 } d3a_q2_bwd_desc;
 int d3a_q2_bwd(const d3a_q2_bwd_desc* d, void* stream);
 
@@ -1043,6 +1052,26 @@ typedef struct d3a_iqn_head_bwd_desc {
   int32_t B, K, F, A, G;
 } d3a_iqn_head_bwd_desc;
 int d3a_iqn_head_bwd(const d3a_iqn_head_bwd_desc* d, void* stream);
+
+/* The IQN head forward in one launch (d3a_iqn_prior + the embed Linear + ReLU
+ * + d3a_iqn_head_fwd): prior[r][e] = cos(pi (e + 1) taus[r]), phi[r] =
+ * relu(prior[r] We^T + be), q[r][a] = (h[g][b] * phi[r]) . Wf[a] + bf[a] with
+ * the row groups of d3a_iqn_head_desc (compute_iqn_feature + _compute_
+ * quantiles, iqn_q_function.py:33-47, 82-88).  The embed product on the bf16
+ * matrix cores with exact split-bf16 operands (fp32-accurate).  prior_out /
+ * phi_out (optional) receive rows [0, n_keep) for a backward.  E == 64,
+ * F <= 512 (multiple of 64), A <= 8, K a multiple of 32. */
+typedef struct d3a_iqn_embed_head_desc {
+  const float* taus;
+  const float* We; const float* be;
+  const float* h[D3A_IQN_MAX_GROUPS];
+  const float* Wf; const float* bf;
+  float* q;
+  float* prior_out; float* phi_out;
+  int64_t rows, group_rows, n_keep;
+  int32_t K, E, F, A;
+} d3a_iqn_embed_head_desc;
+int d3a_iqn_embed_head(const d3a_iqn_embed_head_desc* d, void* stream);
 
 #ifdef __cplusplus
 }

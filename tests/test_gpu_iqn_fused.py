@@ -1,0 +1,95 @@
+"""d3a_iqn_embed_head (the IQN head forward in one launch: cosine prior, embed
+Linear + ReLU on split-bf16 MFMA, h * phi product and the head Linear) against
+the three-launch path it replaces (d3a_iqn_prior + the embed GEMM +
+d3a_iqn_head_fwd, fp32 MFMA) and against fp64.
+
+Reference: compute_iqn_feature (iqn_q_function.py:33-47) and
+DiscreteIQNQFunction._compute_quantiles (iqn_q_function.py:82-88).  Bars: the
+prior is bitwise the standalone kernel's (same fp32 ops); phi within 2e-6 of
+fp64 relative to its rounding scale sum_e |prior We| + |be| (fp32-accurate
+split products); q within 1e-5 (max-normalised) of fp64."""
+import numpy as np
+import pytest
+import torch
+
+from d3rlpy_amd import _native as N
+from d3rlpy_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(B, K, G, F, A, seed, dev):
+    gen = torch.Generator().manual_seed(seed)
+    E = 64
+    rows = G * B * K
+    taus = torch.rand(rows, generator=gen).to(dev)
+    We = (torch.randn(F, E, generator=gen) / np.sqrt(E)).to(dev)
+    be = (torch.randn(F, generator=gen) * 0.1).to(dev)
+    Wf = (torch.randn(A, F, generator=gen) / np.sqrt(F)).to(dev)
+    bf = (torch.randn(A, generator=gen) * 0.1).to(dev)
+    hs = [torch.relu(torch.randn(B, F, generator=gen)).to(dev) for _ in range(G)]
+    return rows, E, taus, We, be, Wf, bf, hs
+
+
+@pytest.mark.parametrize("B,K,G,F,A,keep_groups", [(512, 64, 4, 512, 4, 3), (512, 64, 1, 512, 4, 0),
+                                                   (37, 32, 2, 256, 7, 1), (16, 96, 3, 128, 1, 2)])
+def test_iqn_embed_head_matches_three_launches(B, K, G, F, A, keep_groups):
+    dev = torch.device("cuda")
+    rows, E, taus, We, be, Wf, bf, hs = _case(B, K, G, F, A, B * K + F + A, dev)
+    n_keep = keep_groups * B * K
+    # the three-launch path
+    prior = torch.zeros(rows, E, device=dev)
+    p = N.IqnPriorDesc()
+    p.taus, p.prior, p.rows, p.E = taus.data_ptr(), prior.data_ptr(), rows, E
+    ops.call_desc("d3a_iqn_prior", p)
+    phi = torch.zeros(rows, F, device=dev)
+    ops.linear_fwd(prior.data_ptr(), True, E, We.data_ptr(), be.data_ptr(), phi.data_ptr(), 1,
+                   rows, E, F, relu=True)
+    q3 = torch.zeros(rows, A, device=dev)
+    hd = N.IqnHeadDesc()
+    for g in range(G):
+        hd.h[g] = hs[g].data_ptr()
+    hd.phi, hd.Wf, hd.bf, hd.q = phi.data_ptr(), Wf.data_ptr(), bf.data_ptr(), q3.data_ptr()
+    hd.rows, hd.group_rows, hd.K, hd.F, hd.A = rows, B * K, K, F, A
+    ops.call_desc("d3a_iqn_head_fwd", hd)
+    # the fused launch
+    q1 = torch.full((rows, A), float("nan"), device=dev)
+    pr1 = torch.full((max(n_keep, 1), E), float("nan"), device=dev)
+    ph1 = torch.full((max(n_keep, 1), F), float("nan"), device=dev)
+    d = N.IqnEmbedHeadDesc()
+    d.taus, d.We, d.be = taus.data_ptr(), We.data_ptr(), be.data_ptr()
+    for g in range(G):
+        d.h[g] = hs[g].data_ptr()
+    d.Wf, d.bf, d.q = Wf.data_ptr(), bf.data_ptr(), q1.data_ptr()
+    d.prior_out = pr1.data_ptr() if n_keep else None
+    d.phi_out = ph1.data_ptr() if n_keep else None
+    d.rows, d.group_rows, d.n_keep = rows, B * K, n_keep
+    d.K, d.E, d.F, d.A = K, E, F, A
+    ops.call_desc("d3a_iqn_embed_head", d)
+    torch.cuda.synchronize()
+    assert not torch.isnan(q1).any()
+    if n_keep:
+        assert torch.equal(pr1, prior[:n_keep])
+        z64 = prior[:n_keep].double() @ We.double().t() + be.double()
+        sc = prior[:n_keep].double().abs() @ We.double().abs().t() + be.double().abs()
+        e_phi = float(((ph1.double() - z64.clamp_min(0)).abs() / sc).max())
+        assert e_phi < 2e-6, e_phi
+    # fp64 of the whole head
+    z = (prior.double() @ We.double().t() + be.double()).clamp_min(0)
+    hrow = torch.cat([hs[g].double().repeat_interleave(K, 0) for g in range(G)])
+    q64 = (hrow * z) @ Wf.double().t() + bf.double()
+    e1 = float((q1.double() - q64).abs().max() / q64.abs().max())
+    e3 = float((q3.double() - q64).abs().max() / q64.abs().max())
+    print(f"iqn head vs fp64: fused {e1:.1e}, three launches {e3:.1e}")
+    assert e1 < 1e-5 and e3 < 1e-5, (e1, e3)
+    # run to run bit-identical
+    qa = q1.clone()
+    ops.call_desc("d3a_iqn_embed_head", d)
+    torch.cuda.synchronize()
+    assert torch.equal(qa, q1)
+
+
+def test_iqn_embed_head_rejects_bad_shapes():
+    d = N.IqnEmbedHeadDesc()
+    with pytest.raises(RuntimeError, match="null"):
+        ops.call_desc("d3a_iqn_embed_head", d)

@@ -157,7 +157,10 @@ def _bwd_case(rows, n_in, n_scaled, C, gen, dev):
     W2 = Ws[1].contiguous()
     w3 = Ws[2].reshape(C, 256).contiguous()
 
-    def run(entry):
+    # the forward's bf16 0 / 1 mask image of h2 (d3a_mlp_fwd_desc.hmask)
+    m2 = (h2 > 0).to(torch.bfloat16).contiguous()
+
+    def run(entry, mask_image=False):
         outs = [torch.full((P, C, 256, n_in), float("nan"), device=dev),
                 torch.full((P, C, 256), float("nan"), device=dev),
                 torch.full((P, C, 256, 256), float("nan"), device=dev),
@@ -171,6 +174,8 @@ def _bwd_case(rows, n_in, n_scaled, C, gen, dev):
         d.W2, d.sW2, d.w3, d.sw3 = W2.data_ptr(), 256 * 256, w3.data_ptr(), 256
         d.dW1, d.db1, d.dW2, d.db2, d.dW3, d.db3 = [t.data_ptr() for t in outs]
         d.rows, d.n_in, d.C = rows, n_in, C
+        if mask_image:
+            d.m2, d.sm2 = m2.data_ptr(), rows * 256
         ops.call_desc(entry, d)
         torch.cuda.synchronize()
         return outs, d
@@ -195,14 +200,18 @@ def _bwd_case(rows, n_in, n_scaled, C, gen, dev):
 NAMES = ["dW1", "db1", "dW2", "db2", "dW3", "db3"]
 
 
+@pytest.mark.parametrize("mask_image", [False, True])
 @pytest.mark.parametrize("rows,n_in,n_scaled", [(7936, 14, 7680), (1000, 48, 999), (300, 23, 0),
                                                 (257, 37, 100)])
-def test_q2_bwd_x6_vs_fp64(rows, n_in, n_scaled):
+def test_q2_bwd_x6_vs_fp64(rows, n_in, n_scaled, mask_image):
+    """mask_image: the ReLU-mask operand copied from the forward's bf16 mask
+    image (d3a_q2_bwd_desc.m2; swizzled LDS rows, transposed reads) rather
+    than built from h2."""
     dev = torch.device("cuda")
     C = 2
     gen = torch.Generator().manual_seed(rows * 3 + n_in)
     run, ref = _bwd_case(rows, n_in, n_scaled, C, gen, dev)
-    outs, d = run("d3a_q2_bwd_x6")
+    outs, d = run("d3a_q2_bwd_x6", mask_image)
     worst = {}
     for name, o in zip(NAMES, outs):
         assert not torch.isnan(o).any(), name
@@ -220,6 +229,23 @@ def test_q2_bwd_x6_vs_fp64(rows, n_in, n_scaled):
     torch.cuda.synchronize()
     for a, b in zip(first, outs):
         assert torch.equal(a, b)
+
+
+def test_q2_bwd_x6_mask_image_matches_built_mask():
+    """The mask-image path gives the built-mask path's dW1 / db1 / dW2 bitwise
+    (same operands, same MFMA order) and its db2 / dW3 / db3 to fp32
+    summation order (rows grouped differently per thread)."""
+    dev = torch.device("cuda")
+    gen = torch.Generator().manual_seed(5)
+    run, _ = _bwd_case(7936, 14, 7680, 2, gen, dev)
+    a, _ = run("d3a_q2_bwd_x6", False)
+    b, _ = run("d3a_q2_bwd_x6", True)
+    for name, x, y in zip(NAMES, a, b):
+        if name in ("dW1", "db1", "dW2"):
+            assert torch.equal(x, y), name
+        else:
+            xs, ys = x.double().sum(0), y.double().sum(0)
+            assert float((xs - ys).abs().max() / ys.abs().max()) < 1e-6, name
 
 
 def test_q2_bwd_x6_matches_fp32_kernel():

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--J", type=int, default=1)
     ap.add_argument("--bf16", action="store_true", help="d3a_q2_fwd_bf16 (bf16 kept activations)")
     ap.add_argument("--x6", action="store_true", help="d3a_q2_fwd_x6 (split-bf16 x6, fp32-accurate)")
+    ap.add_argument("--hmask", action="store_true", help="x6: also write the bf16 mask image of h2")
     a = ap.parse_args()
     dev, C, H = "cuda", a.C, 256
     sizes = [a.n_in, H, H, a.J]
@@ -65,6 +66,9 @@ def main():
     d.sh = a.rows * H
     d.out, d.sout, d.ldout = out.data_ptr(), a.rows * a.J, a.J
     d.r0, d.rows, d.C, d.h_from = 0, a.rows, C, a.h_from
+    if a.hmask:
+        hm = torch.zeros(C, a.rows, H, device=dev, dtype=torch.bfloat16)
+        d.hmask, d.s_hmask = hm.data_ptr(), a.rows * H
     if a.aux:
         d.aux_x, d.aux_ldx, d.aux_sxb, d.aux_wdelta = xa.data_ptr(), ldx, 0, n_par
         d.aux_out, d.aux_sout, d.aux_rows = aout.data_ptr(), a.aux * a.J, a.aux
@@ -90,7 +94,7 @@ def main():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / a.reps
     flops = 2 * C * (a.rows + a.aux) * sum(sizes[l] * sizes[l + 1] for l in range(3))
-    print(json.dumps({"kernel": entry, "rows": a.rows, "aux": a.aux, "bm": a.bm, "C": C, "J": a.J,
+    print(json.dumps({"kernel": entry, "hmask": a.hmask, "rows": a.rows, "aux": a.aux, "bm": a.bm, "C": C, "J": a.J,
                       "variant": os.environ.get("D3A_FWD_PROBE", "") + ("generic" if os.environ.get("D3A_FWD_Q2") == "0" else ""),
                       "avg_us": round(us, 2), "tflops": round(flops / us / 1e6, 2),
                       "frac_fp32_peak": round(flops / us / 1e6 / 157.3, 4),
