@@ -10,3 +10,4 @@ for m in 1 0; do D3A_IQN_FUSED=$m timeout -k 10 300 python bench.py --algo dcql 
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/tl_dcql13 -o run --output-format csv -- python3 $R/bench.py --algo dcql --steps 60 --warmup 10 --no-cpu-baseline --transitions 100000 > $R/gpurun_out/tl_dcql13.log 2>&1 || exit $?
 python tools/prof_timeline.py gpurun_out/tl_dcql13/run_kernel_trace.csv > gpurun_out/tl_dcql13.txt; rm -f gpurun_out/tl_dcql13/run_kernel_trace.csv
+bash tools/profiling/gpu_r04_measure.sh
