@@ -447,6 +447,15 @@ class IqnEmbedHeadDesc(C.Structure):
     ]
 
 
+class IqnHeadBwdFusedDesc(C.Structure):
+    _fields_ = [
+        ("h", vp), ("phi", vp), ("prior", vp), ("dq", vp), ("Wf", vp),
+        ("dh", vp), ("dWf_part", vp), ("dbf_part", vp), ("dWe_part", vp), ("dbe_part", vp),
+        ("B", C.c_int32), ("K", C.c_int32), ("F", C.c_int32), ("E", C.c_int32),
+        ("A", C.c_int32), ("G", C.c_int32), ("NB", C.c_int32),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "d3a_abi_version": (C.c_int, []),
@@ -525,6 +534,7 @@ _SIGNATURES = {
     "d3a_q2_bwd_x6": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
     "d3a_q2_fwd_x1": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_iqn_embed_head": (C.c_int, [C.POINTER(IqnEmbedHeadDesc), vp]),
+    "d3a_iqn_head_bwd_fused": (C.c_int, [C.POINTER(IqnHeadBwdFusedDesc), vp]),
     "d3a_mlp_fwd_x6": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_x6_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_td3_prep": (C.c_int, [C.POINTER(Td3PrepDesc), vp]),

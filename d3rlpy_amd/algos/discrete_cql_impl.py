@@ -430,6 +430,7 @@ class _Workspace:
         self.enc = _EncoderPass(impl, 2 * B, dev)      # online: [obs; next_obs]
         self.enc_t = _EncoderPass(impl, B, dev)        # target: next_obs
         self.mean = impl._q_type == "mean"
+        self.fused_bwd = False
         if self.mean:
             # linear head: online Q over [obs; next_obs], target Q over next_obs
             self.q_on, self.q_t = z(2 * B, A), z(B, A)
@@ -469,9 +470,14 @@ class _Workspace:
             self.grads.add("q.fc.W", (1, A, F), self.S_head)
             self.grads.add("q.fc.b", (1, A), self.S_head)
         else:
-            self.grads.add("q.fc.W", (1, A, F), B)
-            self.grads.add("q.fc.b", (1, A), B)
-            self.S_emb = mlp.n_splits(3 * BK)
+            # the head backward + embed weight gradient as one launch
+            # (d3a_iqn_head_bwd_fused): one partial per workgroup of NB rows b
+            self.fused_bwd = (_IQN_FUSED and F == 512 and E == 64 and A <= 8 and K % 32 == 0)
+            self.NB = 2
+            P = (B + self.NB - 1) // self.NB
+            self.grads.add("q.fc.W", (1, A, F), P if self.fused_bwd else B)
+            self.grads.add("q.fc.b", (1, A), P if self.fused_bwd else B)
+            self.S_emb = P if self.fused_bwd else mlp.n_splits(3 * BK)
             self.grads.add("q.embed.W", (1, F, E), self.S_emb)
             self.grads.add("q.embed.b", (1, F), self.S_emb)
         self.opt = AdamGroup(impl.optim_state, self.grads)
@@ -515,6 +521,18 @@ class _Workspace:
         hb.dbf_part = self.grads.get("q.fc.b").data_ptr()
         hb.B, hb.K, hb.F, hb.A, hb.G = B, K, F, A, 3
         self.head_bwd_desc = hb
+        if self.fused_bwd:
+            fb = NAT.IqnHeadBwdFusedDesc()
+            fb.h, fb.phi, fb.prior = (self.enc.h.data_ptr(), self.head.phi.data_ptr(),
+                                      self.head.prior.data_ptr())
+            fb.dq, fb.Wf = self.dq.data_ptr(), impl.store.ptr("q.fc.W")
+            fb.dh = self.dzfc.data_ptr()
+            fb.dWf_part = self.grads.get("q.fc.W").data_ptr()
+            fb.dbf_part = self.grads.get("q.fc.b").data_ptr()
+            fb.dWe_part = self.grads.get("q.embed.W").data_ptr()
+            fb.dbe_part = self.grads.get("q.embed.b").data_ptr()
+            fb.B, fb.K, fb.F, fb.E, fb.A, fb.G, fb.NB = B, K, F, impl._E, A, 3, self.NB
+            self.head_bwd_fused_desc = fb
 
     def stage(self, db: DeviceBatch, taus) -> None:
         B = self.B
@@ -602,10 +620,13 @@ class _Workspace:
                                K, tg, n_keep=0)
             ops.call_desc("d3a_iqn_loss", self.loss_desc)
             # backward: head, embed, encoder (obs samples)
-            ops.call_desc("d3a_iqn_head_bwd", self.head_bwd_desc)
-            ops.linear_bwd_w(self.dphi.data_ptr(), F, 3 * BK * F, self.head.prior.data_ptr(), E,
-                             3 * BK * E, g.get("q.embed.W").data_ptr(), 1, 3 * BK, E, F,
-                             self.S_emb, db=g.get("q.embed.b").data_ptr(), variant=10)
+            if self.fused_bwd:
+                ops.call_desc("d3a_iqn_head_bwd_fused", self.head_bwd_fused_desc)
+            else:
+                ops.call_desc("d3a_iqn_head_bwd", self.head_bwd_desc)
+                ops.linear_bwd_w(self.dphi.data_ptr(), F, 3 * BK * F, self.head.prior.data_ptr(),
+                                 E, 3 * BK * E, g.get("q.embed.W").data_ptr(), 1, 3 * BK, E, F,
+                                 self.S_emb, db=g.get("q.embed.b").data_ptr(), variant=10)
         ops.linear_bwd_w(self.dzfc.data_ptr(), F, B * F, self.enc.yt.data_ptr(), impl.flat,
                          B * impl.flat, g.get("enc.fc.W").data_ptr(), 1, B, impl.flat, F,
                          self.S_fc, db=g.get("enc.fc.b").data_ptr())

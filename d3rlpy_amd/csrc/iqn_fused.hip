@@ -19,6 +19,7 @@
 // operand from LDS), so a lane holds one row and 16 units per chunk: the
 // ReLU, the product with h (one b per tile: K % 32 == 0) and the dot with Wf
 // are register work, the per-row sums meet across waves in LDS (in wave order).
+#include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
 #include "x6.hpp"
@@ -137,12 +138,18 @@ __global__ __launch_bounds__(512) void iqn_embed_head_kernel(d3a_iqn_embed_head_
         for (int i = 0; i < 4; ++i) ph[i] = fmaxf(acc[4 * R + i] + bb[i], 0.f);
         if (keep)
           *reinterpret_cast<float4*>(d.phi_out + row * F + u) = make_float4(ph[0], ph[1], ph[2], ph[3]);
+        float pr4[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = __fmul_rn(hh[i], ph[i]);  // prod = h * phi
+        for (int i = 0; i < 4; ++i) pr4[i] = __fmul_rn(hh[i], ph[i]);  // prod = h * phi
 #pragma unroll
-          for (int a = 0; a < IF_AMAX; ++a)
-            if (a < A) qa[a] = fmaf(p, L.wf[a][u + i], qa[a]);
+        for (int a = 0; a < IF_AMAX; ++a) {
+          if (a < A) {
+            const float4 wv = *reinterpret_cast<const float4*>(&L.wf[a][u]);
+            qa[a] = fmaf(pr4[0], wv.x, qa[a]);
+            qa[a] = fmaf(pr4[1], wv.y, qa[a]);
+            qa[a] = fmaf(pr4[2], wv.z, qa[a]);
+            qa[a] = fmaf(pr4[3], wv.w, qa[a]);
+          }
         }
       }
     }
@@ -192,9 +199,201 @@ extern "C" int d3a_iqn_embed_head(const d3a_iqn_embed_head_desc* dp, void* strea
                 "d3a_iqn_embed_head: We, prior_out and phi_out must be 16-byte aligned");
   if (d.rows == 0) return 0;
   const int64_t ntiles = (d.rows + IF_RB - 1) / IF_RB;
-  const int64_t grid = ntiles < 256 ? ntiles : 256;  // one workgroup per CU, tiles strided
-  hipLaunchKernelGGL(iqn_embed_head_kernel, dim3((unsigned)grid), dim3(64 * (d.F / 64)), 0,
+  // persistent workgroups, tiles strided; two per CU (54 KB of LDS, 167 VGPRs:
+  // four waves per SIMD) unless D3A_IQN_GRID says otherwise
+  static const int64_t gmax = [] {
+    const char* e = getenv("D3A_IQN_GRID");
+    return e ? (int64_t)atoll(e) : (int64_t)512;
+  }();
+  const int64_t grid = ntiles < gmax ? ntiles : gmax;
+  hipLaunchKernelGGL(d3a::iqn_embed_head_kernel, dim3((unsigned)grid), dim3(64 * (d.F / 64)), 0,
                      (hipStream_t)stream, d);
   D3A_LAUNCH_CHECK("d3a_iqn_embed_head");
+  return 0;
+}
+
+namespace d3a {
+namespace {
+
+using namespace x6;
+
+// ---------------------------------------------------------------------------
+// The IQN head's backward over the G gradient passes in one launch: what
+// d3a_iqn_head_bwd (dphi, dh, dWf / dbf) and the embed weight-gradient GEMM
+// (dWe = dphi^T prior, dbe) computed through a 200 MB dphi round trip.  A
+// workgroup owns NB batch rows b (thread n = feature unit n, F = 512) and
+// walks their G * K rows in 32-row tiles:
+//   per row (thread n, phi read from global, exactly d3a_iqn_head_bwd's ops)
+//     dprod = sum_a dq[r][a] Wf[a][n];  dphi = phi > 0 ? dprod * h : 0
+//     dh[b][n] += dprod * phi;  dWf[a][n] += dq[r][a] * (h * phi)
+//   per tile: dphi as three bf16 parts [n][r] in LDS, the tile's prior as
+//   three parts [e][r] (transposed while staged), and dWe[n][e] += dphi^T
+//   prior on the bf16 matrix cores (six part products, fp32 accumulation):
+//   wave w owns n = 64 w .. + 63 and all 64 e (four 32 x 32 accumulators).
+// Outputs per workgroup p (partials summed in order by the Adam kernel):
+// dWf_part[p][A][F], dbf_part[p][A], dWe_part[p][F][E], dbe_part[p][F]; dh
+// [B][F] (times [h > 0], the encoder fc's ReLU) is whole per b.
+constexpr int IB_F = 512;
+constexpr int IB_RT = 32;           // rows per tile
+constexpr int IB_LDR = IB_RT + 8;   // bf16 row stride of the [.][r] images
+
+struct IbLds {
+  __bf16 dT[3][IB_F * IB_LDR];      // dphi parts [n][r]
+  __bf16 pT[3][IF_E * IB_LDR];      // prior parts [e][r]
+  float dq[IB_RT][IF_AMAX];
+};
+
+__global__ __launch_bounds__(512) void iqn_head_bwd_fused_kernel(d3a_iqn_head_bwd_fused_desc d) {
+  __shared__ __attribute__((aligned(16))) IbLds L;
+  const int n = threadIdx.x, lane = n & 63;
+  const int w = __builtin_amdgcn_readfirstlane(n >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  const int A = d.A, K = d.K;
+  const int64_t BK = (int64_t)d.B * K;
+  const int64_t p = blockIdx.x;
+  float wv[IF_AMAX];
+#pragma unroll
+  for (int a = 0; a < IF_AMAX; ++a) wv[a] = a < A ? d.Wf[a * IB_F + n] : 0.f;
+  float dw[IF_AMAX];
+#pragma unroll
+  for (int a = 0; a < IF_AMAX; ++a) dw[a] = 0.f;
+  double dbe = 0.0;
+  f32x16 acc[2][2];  // dWe tiles [n block][e block]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int64_t b0 = p * d.NB;
+  for (int bi = 0; bi < d.NB; ++bi) {
+    const int64_t b = b0 + bi;
+    if (b >= d.B) break;  // workgroup-uniform
+    const float hv = d.h[b * IB_F + n];
+    float dh = 0.f;
+    for (int g = 0; g < d.G; ++g) {
+      for (int k0 = 0; k0 < K; k0 += IB_RT) {
+        const int64_t rbase = g * BK + b * K + k0;
+        // stage: the tile's dq rows and its prior, transposed, as bf16 parts
+        for (int i = n; i < IB_RT * IF_AMAX; i += 512) {
+          const int m = i / IF_AMAX, a = i - m * IF_AMAX;
+          L.dq[m][a] = a < A ? d.dq[(rbase + m) * A + a] : 0.f;
+        }
+        {
+          // thread: row m = n >> 4, e = 4 (n & 15) .. + 3
+          const int m = n >> 4, e4 = 4 * (n & 15);
+          const float4 pv = *reinterpret_cast<const float4*>(d.prior + (rbase + m) * IF_E + e4);
+          const float v[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            __bf16 q0, q1, q2;
+            split1(v[j], q0, q1, q2);
+            L.pT[0][(e4 + j) * IB_LDR + m] = q0;
+            L.pT[1][(e4 + j) * IB_LDR + m] = q1;
+            L.pT[2][(e4 + j) * IB_LDR + m] = q2;
+          }
+        }
+        // phi of the tile's rows for this unit, loaded before the barrier
+        float ph[IB_RT];
+#pragma unroll
+        for (int m = 0; m < IB_RT; ++m) ph[m] = d.phi[(rbase + m) * IB_F + n];
+        __syncthreads();  // dq / prior staged
+        // (dphi replaces phi in ph[] once used)
+#pragma unroll
+        for (int m = 0; m < IB_RT; ++m) {
+          float dp = 0.f;
+#pragma unroll
+          for (int a = 0; a < IF_AMAX; ++a) {
+            if (a >= A) break;
+            const float q = L.dq[m][a];
+            dp = fmaf(q, wv[a], dp);
+            dw[a] = fmaf(q, __fmul_rn(hv, ph[m]), dw[a]);
+          }
+          const float dv = ph[m] > 0.f ? __fmul_rn(dp, hv) : 0.f;
+          dh = fmaf(dp, ph[m], dh);
+          dbe += (double)dv;
+          ph[m] = dv;
+        }
+#pragma unroll
+        for (int m8 = 0; m8 < IB_RT; m8 += 8) {
+          bf16x8 pp[3];
+          split8(ph + m8, pp);
+#pragma unroll
+          for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(&L.dT[q][n * IB_LDR + m8]) = pp[q];
+        }
+        __syncthreads();  // dphi parts staged
+        // dWe[n][e] += sum_r dphi[r][n] prior[r][e]: A = dT rows (n), B = pT rows (e)
+#pragma unroll
+        for (int s = 0; s < IB_RT / 16; ++s) {
+          bf16x8 bp[2][3];
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+              bp[j][q] = *reinterpret_cast<const bf16x8*>(&L.pT[q][(32 * j + li) * IB_LDR + 16 * s + 8 * lh]);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            bf16x8 ap[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+              ap[q] = *reinterpret_cast<const bf16x8*>(&L.dT[q][(64 * w + 32 * i + li) * IB_LDR + 16 * s + 8 * lh]);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = prod6(ap, bp[j], acc[i][j]);
+          }
+        }
+        __syncthreads();  // images free for the next tile
+      }
+    }
+    d.dh[b * IB_F + n] = hv > 0.f ? dh : 0.f;
+  }
+  // partials of this workgroup
+#pragma unroll
+  for (int a = 0; a < IF_AMAX; ++a)
+    if (a < A) d.dWf_part[(p * A + a) * IB_F + n] = dw[a];
+  d.dbe_part[p * IB_F + n] = (float)dbe;
+  // dWe tile (i, j): lane column e = 32 j + li, rows n = 64 w + 32 i + (r & 3) + 8 (r >> 2) + 4 lh
+  float* dWe = d.dWe_part + p * IB_F * IF_E;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int nn = 64 * w + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        dWe[nn * IF_E + 32 * j + li] = acc[i][j][r];
+      }
+  if (n < A) {
+    double s = 0.0;
+    for (int bi = 0; bi < d.NB; ++bi) {
+      const int64_t b = b0 + bi;
+      if (b >= d.B) break;
+      for (int g = 0; g < d.G; ++g)
+        for (int k = 0; k < K; ++k) s += (double)d.dq[(g * BK + b * K + k) * A + n];
+    }
+    d.dbf_part[p * A + n] = (float)s;
+  }
+}
+
+}  // namespace
+}  // namespace d3a
+
+using namespace d3a;
+
+extern "C" int d3a_iqn_head_bwd_fused(const d3a_iqn_head_bwd_fused_desc* dp, void* stream) {
+  D3A_CHECK_ARG(dp, "d3a_iqn_head_bwd_fused: null desc");
+  const d3a_iqn_head_bwd_fused_desc& d = *dp;
+  D3A_CHECK_ARG(d.h && d.phi && d.prior && d.dq && d.Wf && d.dh && d.dWf_part && d.dbf_part &&
+                    d.dWe_part && d.dbe_part,
+                "d3a_iqn_head_bwd_fused: null pointer");
+  D3A_CHECK_ARG(d.F == IB_F && d.E == IF_E, "d3a_iqn_head_bwd_fused: needs F == 512, E == 64");
+  D3A_CHECK_ARG(d.A >= 1 && d.A <= IF_AMAX && d.G >= 1 && d.B >= 1 && d.NB >= 1 && d.K >= 32 &&
+                    d.K % 32 == 0,
+                "d3a_iqn_head_bwd_fused: bad sizes (A <= 8, K a multiple of 32)");
+  auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  D3A_CHECK_ARG(a16(d.prior), "d3a_iqn_head_bwd_fused: prior must be 16-byte aligned");
+  const int64_t grid = (d.B + d.NB - 1) / d.NB;
+  hipLaunchKernelGGL(d3a::iqn_head_bwd_fused_kernel, dim3((unsigned)grid), dim3(512), 0,
+                     (hipStream_t)stream, d);
+  D3A_LAUNCH_CHECK("d3a_iqn_head_bwd_fused");
   return 0;
 }

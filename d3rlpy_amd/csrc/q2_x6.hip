@@ -97,8 +97,8 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   HT* const h0g = (!aux && d.h[0]) ? reinterpret_cast<HT*>(d.h[0]) + c * d.sh : nullptr;
   HT* const h1g = (!aux && d.h[1]) ? reinterpret_cast<HT*>(d.h[1]) + c * d.sh : nullptr;
   // the ReLU mask image of the last hidden layer (kept rows; NO == 1)
-  __bf16* const hmg = (!aux && NO == 1 && d.hmask) ? reinterpret_cast<__bf16*>(d.hmask) + c * d.s_hmask
-                                                   : nullptr;
+  uint32_t* const hmg = (!aux && NO == 1 && d.hmask) ? reinterpret_cast<uint32_t*>(d.hmask) + c * d.s_hmask
+                                                     : nullptr;
   // a kept run of four activations (16 bytes fp32, 8 bytes bf16)
   auto put4 = [](HT* p, const float* v) {
     if constexpr (sizeof(HT) == 4) {
@@ -374,14 +374,16 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
       for (int R = 0; R < 4; ++R) put4(h1g + row * X_H + 32 * w + 8 * R + 4 * lh, v + 4 * R);
     }
-    if (hmg != nullptr && row >= h_from && row < rend) {
+    if (hmg != nullptr) {
+      // the ReLU mask of the lane's 16 units as bits of the wave's 32-unit
+      // word (bit = unit - 32 w), the two lane halves or-ed together
+      uint32_t bm = 0u;
 #pragma unroll
-      for (int R = 0; R < 4; ++R) {
-        bf16x4 mk;
+      for (int R = 0; R < 4; ++R)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) mk[i] = v[4 * R + i] > 0.f ? (__bf16)1.f : (__bf16)0.f;
-        *reinterpret_cast<bf16x4*>(hmg + (int64_t)row * X_H + 32 * w + 8 * R + 4 * lh) = mk;
-      }
+        for (int i = 0; i < 4; ++i) bm |= (v[4 * R + i] > 0.f ? 1u : 0u) << (8 * R + 4 * lh + i);
+      bm |= (uint32_t)__shfl_xor((int)bm, 32, 64);
+      if (lh == 0 && row >= h_from && row < rend) hmg[(int64_t)row * (X_H / 32) + w] = bm;
     }
     float hs = v[0] * ww[0];
 #pragma unroll
@@ -419,9 +421,9 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
                 "d3a_q2_fwd_x6: null operand");
   D3A_CHECK_ARG(xgen_ok(d), "d3a_q2_fwd_x6: bad input-row builder (xg_*)");
   D3A_CHECK_ARG(d.hmask == nullptr ||
-                    (d.n_out == 1 && (reinterpret_cast<uintptr_t>(d.hmask) & 15) == 0 &&
-                     d.s_hmask % 8 == 0 && d.s_hmask >= (d.r0 + d.rows) * X_H),
-                "d3a_q2_fwd_x6: hmask needs one output and 16-byte aligned rows of 256 bf16");
+                    (d.n_out == 1 && (reinterpret_cast<uintptr_t>(d.hmask) & 3) == 0 &&
+                     d.s_hmask >= (d.r0 + d.rows) * (X_H / 32)),
+                "d3a_q2_fwd_x6: hmask needs one output and rows of 8 32-bit words");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.r0 >= 0 && d.h_from >= 0 && d.aux_rows >= 0,
                 "d3a_q2_fwd_x6: bad sizes");
   auto a16 = [](const void* p, int64_t stride) {

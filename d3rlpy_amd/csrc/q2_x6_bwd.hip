@@ -69,9 +69,9 @@ struct B6Lds {
   float gp[3][B6_SB];              // g' of the rows
 };
 
-// MI (mask image; d.m2 given): the forward wrote the ReLU mask of h2 as bf16
-// 0 / 1 rows [r][o] (d3a_mlp_fwd_desc.hmask), so the dW2 waves' staging is a
-// copy: one [r][o] image per sub-block, 16-byte chunks XOR-swizzled by row
+// MI (mask image; d.m2 given): the forward wrote the ReLU mask of h2 as bits
+// (d3a_mlp_fwd_desc.hmask, 32 bytes a row), so the dW2 waves' staging expands
+// bits: one bf16 0 / 1 [r][o] image per sub-block, 16-byte chunks XOR-swizzled by row
 // (mchunk), read by rows (ds_read_b128) as the dh1 product's A operand and
 // transposed (ds_read_b64_tr_b16) as the dW2 product's -- both conflict-free
 // -- instead of two mask images built from h2 by VALU.  The quarter's db2 /
@@ -163,10 +163,11 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
   float h1v[8], gh[8];
   // MI: the dW2 waves copy mask chunk mc of rows mr + 8 k, and sum db2 / dW3
   // of o = i0 + (t2 & 63) over rows (t2 >> 6) + 4 k
-  const __bf16* m2g = MI ? reinterpret_cast<const __bf16*>(d.m2) + c * d.sm2 : nullptr;
-  const int mc = t2 & 31, mr = t2 >> 5;
+  // the forward's mask bits: row r, word wd = o >> 5, bit o & 31
+  const uint32_t* m2g = MI ? reinterpret_cast<const uint32_t*>(d.m2) + c * d.sm2 : nullptr;
+  const int mwd = t2 & 7, mrr = t2 >> 3;
   const int so = t2 & 63, sr = t2 >> 6;
-  uint4 mk4[4];
+  uint32_t mword = 0u;
   // (the dW2 waves' h2 / g' of the sums reuse the dX waves' h1v / gh: one
   // pair of arrays for both roles keeps them in registers)
   float s_db2m = 0.f, s_dw3m = 0.f;
@@ -180,11 +181,7 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
         gh[k] = gprime(r);
       }
     } else if constexpr (MI) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int r = min(base + mr + 8 * k, rlast);
-        mk4[k] = *reinterpret_cast<const uint4*>(m2g + r * B6_H + 8 * mc);
-      }
+      mword = m2g[min(base + mrr, rlast) * (B6_H / 32) + mwd];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int r = min(base + sr + 4 * k, rlast);
@@ -231,12 +228,22 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
       return;
     }
     if constexpr (MI) {
-      // the mask rows (rows past the end: zero, as the float path stages them)
+      // the mask row mrr, o = 32 mwd .. + 31, expanded to bf16 0 / 1 (rows
+      // past the end: zero, as the float path stages them)
+      {
+        const bool ok = base + mrr < rows && sb < B6_NSB;
+        const uint32_t mw = ok ? mword : 0u;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int rr = mr + 8 * k;
-        const bool ok = base + rr < rows && sb < B6_NSB;
-        *reinterpret_cast<uint4*>(&B.mro[mchunk(rr, mc)]) = ok ? mk4[k] : make_uint4(0u, 0u, 0u, 0u);
+        for (int cc = 0; cc < 4; ++cc) {
+          uint4 v;
+          uint32_t* vp = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+          for (int j2 = 0; j2 < 4; ++j2) {
+            const uint32_t lo = (mw >> (8 * cc + 2 * j2)) & 1u, hi = (mw >> (8 * cc + 2 * j2 + 1)) & 1u;
+            vp[j2] = (lo * 0x3F80u) | (hi * 0x3F800000u);
+          }
+          *reinterpret_cast<uint4*>(&B.mro[mchunk(mrr, 4 * mwd + cc)]) = v;
+        }
       }
       // the quarter's db2 / dW3 / db3 terms, in row order per thread
       const float w3o = w3g[i0 + so];
@@ -567,9 +574,9 @@ extern "C" int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(d.ldx >= d.n_in, "d3a_q2_bwd_x6: ldx < n_in");
   D3A_CHECK_ARG(d.rows * (d.ldh > d.ldx ? d.ldh : d.ldx) < (int64_t(1) << 31),
                 "d3a_q2_bwd_x6: rows x row stride exceeds 2^31");
-  D3A_CHECK_ARG(d.m2 == nullptr || ((reinterpret_cast<uintptr_t>(d.m2) & 15) == 0 && d.sm2 % 8 == 0 &&
-                                    d.sm2 >= d.rows * B6_H),
-                "d3a_q2_bwd_x6: the mask image must be 16-byte aligned rows of 256 bf16");
+  D3A_CHECK_ARG(d.m2 == nullptr || ((reinterpret_cast<uintptr_t>(d.m2) & 3) == 0 &&
+                                    d.sm2 >= d.rows * (B6_H / 32)),
+                "d3a_q2_bwd_x6: the mask must be rows of 8 32-bit words");
   if (d.rows == 0) return 0;
   const int64_t units = ((d.rows + B6_RB - 1) / B6_RB) * d.C;
   const int64_t blocks = (units + 7) / 8 * 32;

@@ -38,7 +38,7 @@ def n_splits(rows: int, min_rows: int = 32, max_splits: int = 32) -> int:
 class Acts:
     """Activation buffers of one forward pass: h[l] is [C][R][H_l] (trunk);
     ``hmask`` (optional, ``with_mask``): the last hidden layer's ReLU mask as
-    bf16 0 / 1 rows [C][R][H], written by the split-bf16 x6 Q forward for the
+    bits, int32 [C][R][H / 32], written by the split-bf16 x6 Q forward for the
     kept rows and read by its backward (d3a_mlp_fwd_desc.hmask / d3a_q2_bwd_
     desc.m2)."""
 
@@ -61,8 +61,8 @@ class Acts:
         out_dim = net.sizes[-1]
         out = torch.zeros((net.C, R) if out_dim == 1 else (net.C, R, out_dim), device=device)
         hm = None
-        if with_mask and net.n_layers >= 2:
-            hm = torch.zeros(net.C, R, net.sizes[-2], device=device, dtype=torch.bfloat16)
+        if with_mask and net.n_layers >= 2 and net.sizes[-2] % 32 == 0:
+            hm = torch.zeros(net.C, R, net.sizes[-2] // 32, device=device, dtype=torch.int32)
         return Acts(hs, out, R, hm)
 
 
@@ -277,7 +277,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             xgen = None
         if acts.hmask is not None:
             if (entry == "d3a_q2_fwd_x6" and keep_h and members is None and sizes[-1] == 1):
-                d.hmask, d.s_hmask = acts.hmask.data_ptr(), R * sizes[-2]
+                d.hmask, d.s_hmask = acts.hmask.data_ptr(), R * (sizes[-2] // 32)
                 acts.hmask_from = d.h_from
         means = row_mean is not None and entry == "d3a_mlp_fwd_x6"
         if means:
@@ -440,7 +440,7 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
             if (acts.hmask is not None and acts.hmask_from is not None
                     and acts.hmask_from <= r0 and _MASK_IMAGE):
                 # the forward's mask image of h2 (same rows as h1 / h2)
-                d.m2, d.sm2 = acts.hmask.data_ptr() + 2 * r0 * H, R * H
+                d.m2, d.sm2 = acts.hmask.data_ptr() + 4 * r0 * (H // 32), R * (H // 32)
         ops.call_desc(entry, d)
         return None
 

@@ -264,9 +264,9 @@ typedef struct d3a_mlp_fwd_desc {
   const float* xg_obs; const float* xg_a; int64_t xg_lda;
   const float* xg_base; float xg_clip, xg_scale;
   /* Optional (d3a_q2_fwd_x6 with one output only): the ReLU mask of the last
-   * hidden layer of the kept rows (>= h_from) as bf16 0 / 1, [C][rows][256]
-   * (member stride s_hmask elements, 16-byte aligned rows) -- the operand
-   * image d3a_q2_bwd_x6 reads (d3a_q2_bwd_desc.m2).                       */
+   * hidden layer of the kept rows (>= h_from) as bits, [C][rows][256 / 32]
+   * uint32 (bit o & 31 of word o >> 5; member stride s_hmask words) -- what
+   * d3a_q2_bwd_x6 builds its mask operand from (d3a_q2_bwd_desc.m2).       */
   void* hmask; int64_t s_hmask;
 } d3a_mlp_fwd_desc;
 #define D3A_MLP_PARTS 4
@@ -337,9 +337,10 @@ typedef struct d3a_q2_bwd_desc {
    * actor pass spread over ceil(rows / 32) * 4 workgroups). */
   const float* dz2; int64_t sdz;
   int32_t block_rows;
-  /* Optional (d3a_q2_bwd_x6 only): the forward's bf16 0 / 1 mask image of h2
+  /* Optional (d3a_q2_bwd_x6 only): the forward's mask bits of h2
    * (d3a_mlp_fwd_desc.hmask; rows at the same base as h1 / h2, member stride
-   * sm2) -- the ReLU-mask operand is then copied, not built from h2.       */
+   * sm2 words) -- the ReLU-mask operand is expanded from them, not built
+   * from h2.                                                              */
   const void* m2; int64_t sm2;
 } d3a_q2_bwd_desc;
 int d3a_q2_bwd(const d3a_q2_bwd_desc* d, void* stream);
@@ -1072,6 +1073,23 @@ typedef struct d3a_iqn_embed_head_desc {
   int32_t K, E, F, A;
 } d3a_iqn_embed_head_desc;
 int d3a_iqn_embed_head(const d3a_iqn_embed_head_desc* d, void* stream);
+
+/* The IQN head backward and the embed weight gradient in one launch (d3a_iqn_
+ * head_bwd + the dWe = dphi^T prior GEMM, without the dphi round trip): over
+ * the G gradient passes (rows g*B*K + b*K + k; phi / prior as the forward kept
+ * them), NB batch rows per workgroup p = b / NB:
+ *   dh[b] = (sum_r dprod * phi) * [h > 0], dprod = sum_a dq[r][a] Wf[a],
+ *   dWf_part[p][a] / dbf_part[p][a], dWe_part[p][F][E] = sum_r dphi^T prior,
+ *   dbe_part[p][F] = sum_r dphi, dphi = dprod * h * [phi > 0]
+ * (the backward of compute_iqn_feature + _compute_quantiles, iqn_q_function.py:
+ * 33-47, 82-88).  F == 512, E == 64, A <= 8, K a multiple of 32; the dWe
+ * product on the bf16 matrix cores with exact split-bf16 operands. */
+typedef struct d3a_iqn_head_bwd_fused_desc {
+  const float* h; const float* phi; const float* prior; const float* dq; const float* Wf;
+  float* dh; float* dWf_part; float* dbf_part; float* dWe_part; float* dbe_part;
+  int32_t B, K, F, E, A, G, NB;
+} d3a_iqn_head_bwd_fused_desc;
+int d3a_iqn_head_bwd_fused(const d3a_iqn_head_bwd_fused_desc* d, void* stream);
 
 #ifdef __cplusplus
 }

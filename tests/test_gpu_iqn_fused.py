@@ -93,3 +93,53 @@ def test_iqn_embed_head_rejects_bad_shapes():
     d = N.IqnEmbedHeadDesc()
     with pytest.raises(RuntimeError, match="null"):
         ops.call_desc("d3a_iqn_embed_head", d)
+
+
+@pytest.mark.parametrize("B,K,NB", [(512, 64, 2), (37, 32, 3), (16, 96, 1)])
+def test_iqn_head_bwd_fused_matches_two_launches(B, K, NB):
+    """d3a_iqn_head_bwd_fused against d3a_iqn_head_bwd + the embed weight-
+    gradient GEMM (dWe = dphi^T prior) it replaces, and against fp64: dh
+    bitwise (the same per-b fma chain), dWf / dbf / dbe summed partials within
+    fp32 summation-order noise, dWe within 1e-5 of fp64 (split-bf16 product)."""
+    dev = torch.device("cuda")
+    G, F, E, A = 3, 512, 64, 4
+    gen = torch.Generator().manual_seed(B * 7 + K)
+    rows = G * B * K
+    h = torch.relu(torch.randn(B, F, generator=gen)).to(dev)
+    phi = torch.relu(torch.randn(rows, F, generator=gen)).to(dev)
+    prior = torch.cos(torch.rand(rows, E, generator=gen) * 9).to(dev)
+    dq = (torch.randn(rows, A, generator=gen) * 1e-3).to(dev)
+    Wf = (torch.randn(A, F, generator=gen) / np.sqrt(F)).to(dev)
+    # reference: the two launches
+    dphi = torch.zeros(rows, F, device=dev)
+    dh2 = torch.zeros(B, F, device=dev)
+    dWf2, dbf2 = torch.zeros(B, A, F, device=dev), torch.zeros(B, A, device=dev)
+    hb = N.IqnHeadBwdDesc()
+    hb.h, hb.phi, hb.dq, hb.Wf = h.data_ptr(), phi.data_ptr(), dq.data_ptr(), Wf.data_ptr()
+    hb.dphi, hb.dh, hb.dWf_part, hb.dbf_part = dphi.data_ptr(), dh2.data_ptr(), dWf2.data_ptr(), dbf2.data_ptr()
+    hb.B, hb.K, hb.F, hb.A, hb.G = B, K, F, A, G
+    ops.call_desc("d3a_iqn_head_bwd", hb)
+    # fused
+    P = (B + NB - 1) // NB
+    dh1 = torch.full((B, F), float("nan"), device=dev)
+    dWf1, dbf1 = torch.full((P, A, F), float("nan"), device=dev), torch.full((P, A), float("nan"), device=dev)
+    dWe1, dbe1 = torch.full((P, F, E), float("nan"), device=dev), torch.full((P, F), float("nan"), device=dev)
+    fb = N.IqnHeadBwdFusedDesc()
+    fb.h, fb.phi, fb.prior, fb.dq, fb.Wf = (h.data_ptr(), phi.data_ptr(), prior.data_ptr(),
+                                            dq.data_ptr(), Wf.data_ptr())
+    fb.dh, fb.dWf_part, fb.dbf_part = dh1.data_ptr(), dWf1.data_ptr(), dbf1.data_ptr()
+    fb.dWe_part, fb.dbe_part = dWe1.data_ptr(), dbe1.data_ptr()
+    fb.B, fb.K, fb.F, fb.E, fb.A, fb.G, fb.NB = B, K, F, E, A, G, NB
+    ops.call_desc("d3a_iqn_head_bwd_fused", fb)
+    torch.cuda.synchronize()
+    assert torch.equal(dh1, dh2)
+    rel = lambda a, b: float((a.double() - b.double()).abs().max() / b.double().abs().max())  # noqa: E731
+    assert rel(dWf1.sum(0), dWf2.sum(0)) < 1e-6
+    assert rel(dbf1.sum(0), dbf2.sum(0)) < 1e-6
+    # fp64 of the embed gradients from the reference dphi (exact ops of the kernel)
+    dWe64 = dphi.double().t() @ prior.double()
+    dbe64 = dphi.double().sum(0)
+    e_w = rel(dWe1.double().sum(0), dWe64)
+    e_b = rel(dbe1.double().sum(0), dbe64)
+    print(f"fused IQN head backward: dWe {e_w:.1e} dbe {e_b:.1e} vs fp64")
+    assert e_w < 1e-5 and e_b < 1e-6, (e_w, e_b)

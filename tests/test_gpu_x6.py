@@ -157,8 +157,11 @@ def _bwd_case(rows, n_in, n_scaled, C, gen, dev):
     W2 = Ws[1].contiguous()
     w3 = Ws[2].reshape(C, 256).contiguous()
 
-    # the forward's bf16 0 / 1 mask image of h2 (d3a_mlp_fwd_desc.hmask)
-    m2 = (h2 > 0).to(torch.bfloat16).contiguous()
+    # the forward's mask bits of h2 (d3a_mlp_fwd_desc.hmask: bit o & 31 of
+    # word o >> 5)
+    bits = (h2 > 0).view(C, rows, 8, 32).to(torch.int64)
+    m2 = (bits << torch.arange(32, device=dev)).sum(-1)
+    m2 = torch.where(m2 >= 2 ** 31, m2 - 2 ** 32, m2).to(torch.int32).contiguous()
 
     def run(entry, mask_image=False):
         outs = [torch.full((P, C, 256, n_in), float("nan"), device=dev),
@@ -175,7 +178,7 @@ def _bwd_case(rows, n_in, n_scaled, C, gen, dev):
         d.dW1, d.db1, d.dW2, d.db2, d.dW3, d.db3 = [t.data_ptr() for t in outs]
         d.rows, d.n_in, d.C = rows, n_in, C
         if mask_image:
-            d.m2, d.sm2 = m2.data_ptr(), rows * 256
+            d.m2, d.sm2 = m2.data_ptr(), rows * 8
         ops.call_desc(entry, d)
         torch.cuda.synchronize()
         return outs, d

@@ -62,7 +62,8 @@ STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_gemm_wnext", "GemmWnext"),
            ("d3a_transpose_desc", "TransposeDesc"), ("d3a_iqn_prior_desc", "IqnPriorDesc"),
            ("d3a_iqn_head_desc", "IqnHeadDesc"), ("d3a_iqn_loss_desc", "IqnLossDesc"),
            ("d3a_iqn_head_bwd_desc", "IqnHeadBwdDesc"), ("d3a_conv_desc", "ConvDesc"),
-           ("d3a_iqn_embed_head_desc", "IqnEmbedHeadDesc"))
+           ("d3a_iqn_embed_head_desc", "IqnEmbedHeadDesc"),
+           ("d3a_iqn_head_bwd_fused_desc", "IqnHeadBwdFusedDesc"))
 
 
 def test_struct_layouts_match_header(tmp_path):
