@@ -199,11 +199,13 @@ extern "C" int d3a_iqn_embed_head(const d3a_iqn_embed_head_desc* dp, void* strea
                 "d3a_iqn_embed_head: We, prior_out and phi_out must be 16-byte aligned");
   if (d.rows == 0) return 0;
   const int64_t ntiles = (d.rows + IF_RB - 1) / IF_RB;
-  // persistent workgroups, tiles strided; two per CU (54 KB of LDS, 167 VGPRs:
-  // four waves per SIMD) unless D3A_IQN_GRID says otherwise
+  // persistent workgroups, tiles strided, one per CU (measured on K5's
+  // 131,072-row pass: 256 / 512 / 1,024 / 4,096 workgroups -> 628 / 622 / 612 /
+  // 586 steps/s; the per-workgroup We split amortises over more tiles);
+  // D3A_IQN_GRID overrides
   static const int64_t gmax = [] {
     const char* e = getenv("D3A_IQN_GRID");
-    return e ? (int64_t)atoll(e) : (int64_t)512;
+    return e ? (int64_t)atoll(e) : (int64_t)256;
   }();
   const int64_t grid = ntiles < gmax ? ntiles : gmax;
   hipLaunchKernelGGL(d3a::iqn_embed_head_kernel, dim3((unsigned)grid), dim3(64 * (d.F / 64)), 0,

@@ -67,8 +67,8 @@ def main():
     d.out, d.sout, d.ldout = out.data_ptr(), a.rows * a.J, a.J
     d.r0, d.rows, d.C, d.h_from = 0, a.rows, C, a.h_from
     if a.hmask:
-        hm = torch.zeros(C, a.rows, H, device=dev, dtype=torch.bfloat16)
-        d.hmask, d.s_hmask = hm.data_ptr(), a.rows * H
+        hm = torch.zeros(C, a.rows, H // 32, device=dev, dtype=torch.int32)
+        d.hmask, d.s_hmask = hm.data_ptr(), a.rows * (H // 32)
     if a.aux:
         d.aux_x, d.aux_ldx, d.aux_sxb, d.aux_wdelta = xa.data_ptr(), ldx, 0, n_par
         d.aux_out, d.aux_sout, d.aux_rows = aout.data_ptr(), a.aux * a.J, a.aux
