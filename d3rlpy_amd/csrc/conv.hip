@@ -32,13 +32,15 @@
 // take consecutive slices of the split and are summed through LDS in wave
 // order; the split's partial goes to dW[split] (summed in order by the Adam
 // kernel), so the result is run-to-run deterministic.
+#include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
+#include "x6.hpp"
 
 namespace d3a {
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+using x6::f32x16;
 constexpr int kMaxKGroups = 1024;  // C*KH*KW <= 4096
 
 // x / 255 correctly rounded (== torch's x.float() / 255.0) for x in 0..255
@@ -190,6 +192,171 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(d3a_conv_desc d, const fl
     cur ^= 1;
   }
 
+  if (m0 >= M) return;
+  // epilogue: acc[j][r] -> row m0 + (r&3) + 8*(r>>2) + 4*lg, channel 32*j + li
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int n = 32 * j + li;
+    const float bn = d.bias ? d.bias[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * lg;
+      if (mm < M) {
+        float v = acc[j][r] + bn;
+        if (d.relu) v = fmaxf(v, 0.f);
+        d.y[mm * CO + n] = v;
+      }
+    }
+  }
+}
+
+// Forward on the bf16 matrix cores at fp32 accuracy (x6.hpp): the same
+// implicit GEMM, 16 k per v_mfma_f32_32x32x16_bf16.  Weights are staged per
+// 32-k chunk as three exact bf16 parts, read from nn.Conv2d's layout in the
+// walk order directly (no conv_pack launch).  fp32 input: the activation is
+// split into three parts too, six part products.  uint8 input (the first
+// layer): the byte x itself is the A operand -- an integer 0..255, exact in
+// one bf16 part -- and the weight carries the pixel scale, fl(W / 255), so a
+// tap is three products; x * fl(W / 255) differs from the reference's
+// fl(x / 255) * W by at most one fp32 rounding of the term (tests/
+// test_gpu_conv.py holds it to its 2e-5 bar against fp64).
+template <int WN, bool U8, bool ALIGNED = false>
+__global__ __launch_bounds__(256) void conv_fwd_x6_kernel(d3a_conv_desc d) {
+  using namespace x6;
+  constexpr int CO = 32 * WN, BK = 32, LDB = BK + 8;
+  __shared__ int ta[kMaxKGroups];
+  __shared__ __attribute__((aligned(16))) __bf16 Ws[2][3][CO * LDB];
+  const int KK = d.KH * d.KW;
+  const int Kc = d.C * KK;
+  const int G = Kc / 4;
+  for (int g = threadIdx.x; g < G; g += 256) ta[g] = kgroup_offset<U8>(d, g);
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  const int li = lane & 31, lg = lane >> 5;
+  const int P = d.OH * d.OW;
+  const int64_t M = (int64_t)d.B * P;
+  const int64_t m0 = ((int64_t)blockIdx.x * 4 + w) * 32;
+  const int64_t m = m0 + li;
+  const bool valid = m < M;
+  int64_t org = 0;
+  if (valid) {
+    const int64_t b = m / P;
+    const int p = (int)(m - b * P);
+    const int oy = p / d.OW, ox = p - oy * d.OW;
+    org = window_origin<U8>(d, b, oy, ox);
+  }
+  // weight chunk: CO x 32 walk-ordered values, WN x 4 per thread (co = e >> 5,
+  // kk = e & 31), read from [CO][C][KH][KW]
+  float wv[4 * WN];
+  auto wload = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 4 * WN; ++j) {
+      const int e = t + 256 * j, co = e >> 5, kk = e & 31;
+      const int k = k0 + kk;
+      float v = 0.f;
+      if (k < Kc) {
+        int src = k;  // (c, kh, kw) order for uint8 input = the native layout
+        if (!U8) {
+          const int c = k % d.C, tt = k / d.C, kw = tt % d.KW, kh = tt / d.KW;
+          src = (c * d.KH + kh) * d.KW + kw;
+        }
+        v = d.weight[(int64_t)co * Kc + src];
+        if (U8) v = __fdiv_rn(v, 255.f);
+      }
+      wv[j] = v;
+    }
+  };
+  auto wstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 4 * WN; ++j) {
+      const int e = t + 256 * j, co = e >> 5, kk = e & 31;
+      __bf16 q0, q1, q2;
+      split1(wv[j], q0, q1, q2);
+      Ws[buf][0][co * LDB + kk] = q0;
+      Ws[buf][1][co * LDB + kk] = q1;
+      Ws[buf][2][co * LDB + kk] = q2;
+    }
+  };
+  // the A operand of a chunk: per k step s, this lane's 8 k (16 s + 8 lg ..),
+  // two k groups; raw (uint32 bytes or float4) one chunk ahead
+  uint32_t ru[2][2];
+  float4 rf[2][2];
+  auto aload = [&](int k0) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int g = (k0 + 16 * s + 8 * lg) / 4 + h;
+        if (U8) {
+          uint32_t x = 0u;
+          if (valid && g < G) {
+            const uint8_t* sp = d.x_u8 + org + ta[g];
+            if (ALIGNED) x = *reinterpret_cast<const uint32_t*>(sp);
+            else x = (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) | ((uint32_t)sp[2] << 16) | ((uint32_t)sp[3] << 24);
+          }
+          ru[s][h] = x;
+        } else {
+          rf[s][h] = (valid && g < G) ? *reinterpret_cast<const float4*>(d.x_f32 + org + ta[g])
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+  };
+  f32x16 acc[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  wload(0);
+  wstore(0);
+  __syncthreads();  // also publishes the offset table
+  aload(0);
+  int cur = 0;
+  for (int k0 = 0; k0 < Kc; k0 += BK) {
+    const bool more = k0 + BK < Kc;
+    if (more) wload(k0 + BK);
+    uint32_t cu[2][2];
+    float4 cf[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        cu[s][h] = ru[s][h];
+        cf[s][h] = rf[s][h];
+      }
+    if (more) aload(k0 + BK);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 a[3];
+      if (U8) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[0][4 * h + i] = (__bf16)(float)((cu[s][h] >> (8 * i)) & 255u);
+      } else {
+        const float v[8] = {cf[s][0].x, cf[s][0].y, cf[s][0].z, cf[s][0].w,
+                            cf[s][1].x, cf[s][1].y, cf[s][1].z, cf[s][1].w};
+        split8(v, a);
+      }
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        bf16x8 bq[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          bq[q] = *reinterpret_cast<const bf16x8*>(&Ws[cur][q][(32 * j + li) * LDB + 16 * s + 8 * lg]);
+        if (U8) {
+          // the byte is exact in one part: three products, smallest first
+          acc[j] = mfma16(a[0], bq[2], acc[j]);
+          acc[j] = mfma16(a[0], bq[1], acc[j]);
+          acc[j] = mfma16(a[0], bq[0], acc[j]);
+        } else {
+          acc[j] = prod6(a, bq, acc[j]);
+        }
+      }
+    }
+    if (more) wstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
   if (m0 >= M) return;
   // epilogue: acc[j][r] -> row m0 + (r&3) + 8*(r>>2) + 4*lg, channel 32*j + li
 #pragma unroll
@@ -383,6 +550,27 @@ extern "C" int d3a_conv_fwd(const d3a_conv_desc* d, void* stream) {
                 "d3a_conv_fwd: weight must be 16-byte aligned");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)blocks), block(256);
+  // split-bf16 (fp32-accurate) implicit GEMM unless D3A_CONV_X6=0
+  static const bool use_x6 = [] {
+    const char* e = getenv("D3A_CONV_X6");
+    return !(e && atoi(e) == 0);
+  }();
+  if (use_x6) {
+    if (d->x_u8) {
+      const bool al = d->W % 4 == 0 && d->S % 4 == 0 && (reinterpret_cast<uintptr_t>(d->x_u8) & 3) == 0;
+      if (d->CO == 32 && al) hipLaunchKernelGGL((conv_fwd_x6_kernel<1, true, true>), grid, block, 0, st, *d);
+      else if (d->CO == 32) hipLaunchKernelGGL((conv_fwd_x6_kernel<1, true>), grid, block, 0, st, *d);
+      else if (al) hipLaunchKernelGGL((conv_fwd_x6_kernel<2, true, true>), grid, block, 0, st, *d);
+      else hipLaunchKernelGGL((conv_fwd_x6_kernel<2, true>), grid, block, 0, st, *d);
+    } else {
+      D3A_CHECK_ARG((reinterpret_cast<uintptr_t>(d->x_f32) & 15) == 0,
+                    "d3a_conv_fwd: fp32 input must be 16-byte aligned");
+      if (d->CO == 32) hipLaunchKernelGGL((conv_fwd_x6_kernel<1, false>), grid, block, 0, st, *d);
+      else hipLaunchKernelGGL((conv_fwd_x6_kernel<2, false>), grid, block, 0, st, *d);
+    }
+    D3A_LAUNCH_CHECK("d3a_conv_fwd");
+    return 0;
+  }
   if (d->x_u8) {
     const bool aligned = d->W % 4 == 0 && d->S % 4 == 0 &&
                          (reinterpret_cast<uintptr_t>(d->x_u8) & 3) == 0;
