@@ -284,9 +284,25 @@ __global__ __launch_bounds__(1024) void bcq_actor_head_kernel(d3a_bcq_actor_desc
     const float ga = pass ? d.dq_da[b * d.ld_da + d.da_off + j] : 0.f;
     d.dhead[i] = __fmul_rn(__fmul_rn(ga, d.scale), __fsub_rn(1.f, __fmul_rn(th, th)));
   }
-  // actor loss: Q_0 = mean over quantiles, then -mean over rows
+  // actor loss: Q_0 = mean over quantiles, then -mean over rows (16-byte
+  // loads, four in flight per thread, summed in a fixed order)
   double s = 0.0;
-  for (int64_t i = t; i < (int64_t)d.B * d.K; i += nt) s += (double)d.q0[i];
+  const int64_t nq = (int64_t)d.B * d.K;
+  if ((reinterpret_cast<uintptr_t>(d.q0) & 15) == 0) {
+    const float4* q4 = reinterpret_cast<const float4*>(d.q0);
+    const int64_t n4 = nq / 4;
+#pragma unroll 4
+    for (int64_t i = t; i < n4; i += nt) {
+      const float4 v = q4[i];
+      s += (double)v.x;
+      s += (double)v.y;
+      s += (double)v.z;
+      s += (double)v.w;
+    }
+    for (int64_t i = 4 * n4 + t; i < nq; i += nt) s += (double)d.q0[i];
+  } else {
+    for (int64_t i = t; i < nq; i += nt) s += (double)d.q0[i];
+  }
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if (lane == 0) sd[wid] = s;
   __syncthreads();

@@ -216,10 +216,11 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(d3a_conv_desc d, const fl
 // walk order directly (no conv_pack launch).  fp32 input: the activation is
 // split into three parts too, six part products.  uint8 input (the first
 // layer): the byte x itself is the A operand -- an integer 0..255, exact in
-// one bf16 part -- and the weight carries the pixel scale, fl(W / 255), so a
-// tap is three products; x * fl(W / 255) differs from the reference's
-// fl(x / 255) * W by at most one fp32 rounding of the term (tests/
-// test_gpu_conv.py holds it to its 2e-5 bar against fp64).
+// one bf16 part -- so a tap is three products, and the pixel scale is applied
+// to the sum, fl(sum x W) / 255 (correctly rounded), against the reference's
+// sum fl(x / 255) W: the same value up to fp32 rounding, and bit for bit the
+// reference's x / 255 where one tap carries the output (tests/test_gpu_conv.py:
+// the one-hot pixel-scale test and the 2e-5 bar against fp64).
 template <int WN, bool U8, bool ALIGNED = false>
 __global__ __launch_bounds__(256) void conv_fwd_x6_kernel(d3a_conv_desc d) {
   using namespace x6;
@@ -261,7 +262,6 @@ __global__ __launch_bounds__(256) void conv_fwd_x6_kernel(d3a_conv_desc d) {
           src = (c * d.KH + kh) * d.KW + kw;
         }
         v = d.weight[(int64_t)co * Kc + src];
-        if (U8) v = __fdiv_rn(v, 255.f);
       }
       wv[j] = v;
     }
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256) void conv_fwd_x6_kernel(d3a_conv_desc d) {
     for (int r = 0; r < 16; ++r) {
       const int64_t mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * lg;
       if (mm < M) {
-        float v = acc[j][r] + bn;
+        float v = (U8 ? __fdiv_rn(acc[j][r], 255.f) : acc[j][r]) + bn;
         if (d.relu) v = fmaxf(v, 0.f);
         d.y[mm * CO + n] = v;
       }
