@@ -603,8 +603,13 @@ def main():
     # the fp32-accurate split-bf16 critic kernels (CRITIC_GEMM "x6") run six bf16
     # MFMA products per fp32 product: their ceiling is the bf16 peak / 6
     x6 = _ops.CRITIC_GEMM == "x6" and args.precision == "fp32" and "x6" in kdesc
+    # a kernel whose one operand is exact in one bf16 part (K5's uint8 pixels)
+    # runs three products per fp32 product ("split-bf16 x3" in its label)
+    x3 = args.precision == "fp32" and "split-bf16 x3" in kdesc
+    nprod = 3 if x3 else 6
+    x6 = x6 or x3
     bf16 = args.precision in ("bf16", "bf16h")
-    peak_tflops = 2500.0 if bf16 else (2500.0 / 6 if x6 else 157.3)
+    peak_tflops = 2500.0 if bf16 else (2500.0 / nprod if x6 else 157.3)
     achieved = kflops / kern_s / 1e12
     traffic = None
     if args.traffic_json is None:
@@ -713,8 +718,9 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak_tflops,
                      "unit": "TFLOP/s", "frac": round(achieved / peak_tflops, 4),
                      "traffic": traffic, "kernel": kdesc,
-                     **({"bf16_mfma_frac": round(6 * achieved / 2500.0, 4),
-                         "peak_note": "bf16 dense MFMA peak 2500 TF / 6 products"} if x6 else {}),
+                     **({"bf16_mfma_frac": round(nprod * achieved / 2500.0, 4),
+                         "peak_note": f"bf16 dense MFMA peak 2500 TF / {nprod} products"}
+                        if x6 else {}),
                      "avg_launch_us": round(kern_s * 1e6, 3),
                      "launch_timing": "HIP events on the kernel's stream, 500 launches after 500 "
                                       "settling launches, right before the timed region"},

@@ -514,6 +514,8 @@ _SIGNATURES = {
     "d3a_iqn_transpose": (C.c_int, [C.POINTER(TransposeDesc), vp]),
     "d3a_conv_fwd": (C.c_int, [C.POINTER(ConvDesc), vp]),
     "d3a_conv_bwd_w": (C.c_int, [C.POINTER(ConvDesc), vp]),
+    "d3a_conv_bwd_w_splits": (C.c_int32, [C.POINTER(ConvDesc)]),
+    "d3a_conv_bwd_x": (C.c_int, [C.POINTER(ConvDesc), vp]),
     "d3a_iqn_prior": (C.c_int, [C.POINTER(IqnPriorDesc), vp]),
     "d3a_iqn_head_fwd": (C.c_int, [C.POINTER(IqnHeadDesc), vp]),
     "d3a_iqn_loss": (C.c_int, [C.POINTER(IqnLossDesc), vp]),
@@ -528,6 +530,7 @@ _SIGNATURES = {
     "d3a_bcq_actor_head": (C.c_int, [C.POINTER(BcqActorDesc), vp]),
     "d3a_mlp_bwd": (C.c_int, [C.POINTER(MlpBwdDesc), vp]),
     "d3a_q2_bwd": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
+    "d3a_q2_bwd_actor_head": (C.c_int, [C.POINTER(Q2BwdDesc), C.POINTER(SacActorHeadDesc), vp]),
     "d3a_q2_fwd_bf16": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_q2_bwd_bf16": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
     "d3a_q2_fwd_x6": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),

@@ -785,10 +785,17 @@ class _Workspace:
                 ops.call_desc("d3a_sac_actor_q", aq)
             else:
                 self._actor_critic_layers(B, A, DA)
-            ops.call_desc("d3a_sac_actor_head", hd)
-            mlp.backward(self.pbwd, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
-                         self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B,
-                         head_ready=self.head_dz)
+            # the head's work in the trunk backward's prologue where the
+            # shape takes it (d3a_q2_bwd_actor_head), else head then trunk
+            fused_head = self.head_dz and mlp.backward(
+                self.pbwd, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
+                self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B, head_ready=True,
+                head_desc=hd) is True
+            if not fused_head:
+                ops.call_desc("d3a_sac_actor_head", hd)
+                mlp.backward(self.pbwd, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
+                             self.dhead.data_ptr(), 2 * A, 2 * B * 2 * A, 0, B,
+                             head_ready=self.head_dz)
             tail = None
             if fused_tail:
                 if dp is not None:

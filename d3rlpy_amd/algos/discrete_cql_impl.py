@@ -26,6 +26,7 @@ online evaluations of obs share one encoder pass and its one backward.
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -352,6 +353,15 @@ class _EncoderPass:
                        relu=True, variant=10 if n > 512 else -1)
 
 
+# the conv input gradient as one implicit GEMM (d3a_conv_bwd_x) rather than
+# the column-matrix GEMM + col2im pair; D3A_CONV_BWD_X=0 for the pair
+_CONV_BWD_X = os.environ.get("D3A_CONV_BWD_X", "1") == "1"
+
+
+def _conv_bwd_x(ci: int, co: int) -> bool:
+    """d3a_conv_bwd_x takes this layer (input channels 32 / 64, CO % 16 == 0)."""
+    return _CONV_BWD_X and ci in (32, 64) and co % 16 == 0
+
 # the IQN head forward as one launch (d3a_iqn_embed_head); D3A_IQN_FUSED=0
 # keeps d3a_iqn_prior + the embed GEMM + d3a_iqn_head_fwd (A/B)
 _IQN_FUSED = os.environ.get("D3A_IQN_FUSED", "1") == "1"
@@ -448,14 +458,19 @@ class _Workspace:
         self.dzfc = z(B, F)
         self.dyt = z(B, impl.flat)
         self.dys = [z(B * oh * ow, co) for (ci, h, w, co, k, s, oh, ow) in impl.geom]
-        self.dcols = [None] + [z(B * oh * ow, ci * k * k)
+        self.dcols = [None] + [None if _conv_bwd_x(ci, co) else z(B * oh * ow, ci * k * k)
                                for (ci, h, w, co, k, s, oh, ow) in impl.geom[1:]]
         # gradients: split-K partials for the GEMM weight gradients, per-row
         # partials (B) for the IQN fc
         self.grads = GradSpace(dev)
         self.splits = {}
         for l, (ci, h, w, co, k, s, oh, ow) in enumerate(impl.geom):
-            S = mlp.n_splits(B * oh * ow)
+            # the split count d3a_conv_bwd_w fills the chip with (its kernel's choice)
+            gd = NAT.ConvDesc()
+            gd.B, gd.C, gd.H, gd.W, gd.KH, gd.KW, gd.S, gd.OH, gd.OW, gd.CO = \
+                B, ci, h, w, k, k, s, oh, ow, co
+            S = int(NAT.lib().d3a_conv_bwd_w_splits(C.byref(gd)))
+            assert S >= 1
             self.splits[l] = S
             self.grads.add(f"enc.c{l}.W", (1, co, ci, k, k), S)
             self.grads.add(f"enc.c{l}.b", (1, co), S)
@@ -551,10 +566,23 @@ class _Workspace:
                                    .view(B, -1))
 
     def dominant_kernel(self):
-        """The first conv GEMM of the online encoder over [obs; next_obs]
-        (2B x 400 output positions x 32 filters x 256 taps): the largest GEMM
-        of the step."""
+        """The step's longest kernel: the fused IQN head backward over the G
+        gradient passes (G B K rows x F units: dphi, dh, dWf, and the embed
+        weight gradient dWe on split-bf16 MFMA) -- per row 2 F (2 A + 1 + E) + F
+        flops; else (mean head, or D3A_K5_DOMINANT=conv1) the first conv GEMM
+        over [obs; next_obs] (2B x 400 positions x 32 filters x 256 taps)."""
         impl = self.impl
+        if (not self.mean and self.fused_bwd
+                and os.environ.get("D3A_K5_DOMINANT", "head_bwd") != "conv1"):
+            fb = self.head_bwd_fused_desc
+            rows = fb.G * fb.B * fb.K
+            F, A, E = fb.F, fb.A, fb.E
+
+            def launch_hb():
+                ops.call_desc("d3a_iqn_head_bwd_fused", fb)
+            return launch_hb, rows * (2 * F * (2 * A + 1 + E) + F), (
+                f"d3a_iqn_head_bwd_fused (dWe on split-bf16 x6 MFMA, fp32 head backward): "
+                f"{rows} rows x {F} units, E {E}, A {A}")
         ci, h, w, co, k, s, oh, ow = impl.geom[0]
         rows = 2 * self.B * oh * ow
         d = _conv_desc(impl.geom, 0, 2 * self.B, impl.store, impl.conv_names)
@@ -562,9 +590,11 @@ class _Workspace:
 
         def launch():
             ops.call_desc("d3a_conv_fwd", d)
-        return launch, 2 * rows * ci * k * k * co, (f"d3a_conv_fwd conv1 (implicit GEMM, u8 "
-                                                    f"input): [{rows}x{ci * k * k}]@"
-                                                    f"[{ci * k * k}x{co}]")
+        x3 = os.environ.get("D3A_CONV_X6", "1") != "0"
+        return launch, 2 * rows * ci * k * k * co, (
+            f"d3a_conv_fwd conv1 (implicit GEMM, u8 input"
+            f"{', split-bf16 x3: bytes exact, three bf16 products' if x3 else ''}): "
+            f"[{rows}x{ci * k * k}]@[{ci * k * k}x{co}]")
 
     def execute(self, flags, use_graph: bool) -> None:
         key = tuple(flags) + (self._external_taus,)
@@ -652,7 +682,14 @@ class _Workspace:
                 g.get(bn).data_ptr()
             cd.splits = self.splits[l]
             ops.call_desc("d3a_conv_bwd_w", cd)
-            if l > 0:
+            if l > 0 and _conv_bwd_x(ci, co):
+                # the input gradient as one implicit GEMM through the ReLU of
+                # the layer's input (no column matrix, no col2im)
+                xd = _conv_desc(impl.geom, l, B, st, impl.conv_names)
+                xd.x_f32, xd.dy, xd.y = (self.enc.ys[l - 1].data_ptr(), self.dys[l].data_ptr(),
+                                         self.dys[l - 1].data_ptr())
+                ops.call_desc("d3a_conv_bwd_x", xd)
+            elif l > 0:
                 ops.linear_bwd_x(self.dys[l].data_ptr(), co, rows * co, st.ptr(Wn),
                                  self.dcols[l].data_ptr(), Kc, rows * Kc, 1, rows, Kc, co)
                 c2 = NAT.Col2imDesc()

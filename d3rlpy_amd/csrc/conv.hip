@@ -515,6 +515,308 @@ __global__ __launch_bounds__(64 * KWV) void conv_bwd_w_kernel(d3a_conv_desc d) {
   }
 }
 
+// Weight gradient on the bf16 matrix cores at fp32 accuracy (x6.hpp):
+// dW[co][k] = sum_rows dy[row][co] col(row, k) as v_mfma_f32_32x32x16_bf16
+// over 16-row steps (M = co, N = k, K = rows).  Lane (li, lg) holds rows
+// 8 lg .. 8 lg + 7 of a step: dy[row][co0 + li] (A, three exact bf16 parts)
+// and col(row, k0 + 32 j + li) (B: an fp32 activation in three parts, six
+// products; a uint8 byte exact in one part, three products, the pixel scale
+// applied to the sum as in conv_fwd_x6_kernel).  A wave owns 32 co x 32 NK k
+// over a row sub-slice, the next step's operands loaded while the current one
+// multiplies; the 8 waves of a workgroup are summed by a fixed tree through
+// LDS and the split's partial goes to dW[split] (summed in order by Adam).
+template <int NK, bool U8>
+__global__ __launch_bounds__(512) void conv_bwd_w_x6_kernel(d3a_conv_desc d) {
+  using namespace x6;
+  constexpr int NW = 8;
+  __shared__ float red[4 * NK * 16 * 64];
+  __shared__ double rsum[NW * 32];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 31, lg = lane >> 5;
+  const int KK = d.KH * d.KW;
+  const int Kc = d.C * KK;
+  const int P = d.OH * d.OW;
+  const int64_t M = (int64_t)d.B * P;
+  const int k0 = blockIdx.x * 32 * NK;
+  const int co0 = blockIdx.y * 32;
+  const int s = blockIdx.z;
+  const int64_t chunk = (M + d.splits - 1) / d.splits;
+  const int64_t sb = s * chunk;
+  const int64_t se = sb + chunk < M ? sb + chunk : M;
+  int64_t wch = (se - sb + NW - 1) / NW;
+  wch = (wch + 15) / 16 * 16;
+  const int64_t rb = sb + w * wch;
+  const int64_t re = rb + wch < se ? rb + wch : se;
+  const bool do_bias = d.db != nullptr && blockIdx.x == 0;
+
+  int koff[NK], kout[NK];
+  bool kok[NK];
+#pragma unroll
+  for (int j = 0; j < NK; ++j) {
+    const int k = k0 + 32 * j + li;
+    kok[j] = k < Kc;
+    const int kk = kok[j] ? k : 0;
+    if (U8) {
+      const int c = kk / KK, r = kk - c * KK, kh = r / d.KW, kw = r - kh * d.KW;
+      koff[j] = (c * d.H + kh) * d.W + kw;
+      kout[j] = kk;
+    } else {
+      const int c = kk % d.C, t = kk / d.C, kw = t % d.KW, kh = t / d.KW;
+      koff[j] = (kh * d.W + kw) * d.C + c;
+      kout[j] = c * KK + kh * d.KW + kw;
+    }
+  }
+
+  f32x16 acc[NK];
+#pragma unroll
+  for (int j = 0; j < NK; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  double bs = 0.0;
+
+  // this lane's 8 rows of a step: r0 + 8 lg + i
+  float ny[8], nx[NK][8];
+  RowCursor cur;
+  if (rb < re) cur.set(rb + 8 * lg, P, d.OW);
+  auto load = [&](int64_t r0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t row = r0 + 8 * lg + i;
+      const bool ok = row < re;
+      ny[i] = ok ? d.dy[row * d.CO + co0 + li] : 0.f;
+      const int64_t org = window_origin<U8>(d, cur.b, cur.oy, cur.ox);
+#pragma unroll
+      for (int j = 0; j < NK; ++j) {
+        float v = 0.f;
+        if (ok && kok[j]) v = U8 ? (float)d.x_u8[org + koff[j]] : d.x_f32[org + koff[j]];
+        nx[j][i] = v;
+      }
+      cur.next(d.OH, d.OW);
+    }
+    // skip the other lane group's 8 rows
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cur.next(d.OH, d.OW);
+  };
+  if (rb < re) load(rb);
+  for (int64_t r0 = rb; r0 < re; r0 += 16) {
+    float cy[8], cx[NK][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      cy[i] = ny[i];
+#pragma unroll
+      for (int j = 0; j < NK; ++j) cx[j][i] = nx[j][i];
+    }
+    if (r0 + 16 < re) load(r0 + 16);
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bs += (double)cy[i];
+    }
+    bf16x8 a[3];
+    split8(cy, a);
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      if (U8) {
+        bf16x8 b;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) b[i] = (__bf16)cx[j][i];
+        // the byte is exact in one part: three products, smallest first
+        acc[j] = mfma16(a[2], b, acc[j]);
+        acc[j] = mfma16(a[1], b, acc[j]);
+        acc[j] = mfma16(a[0], b, acc[j]);
+      } else {
+        bf16x8 b[3];
+        split8(cx[j], b);
+        acc[j] = prod6(a, b, acc[j]);
+      }
+    }
+  }
+
+  // fixed-order tree over the 8 waves: (w, w + 4), then (w, w + 2), then (0, 1)
+#pragma unroll
+  for (int half = 4; half >= 1; half >>= 1) {
+    if (w >= half && w < 2 * half) {
+#pragma unroll
+      for (int j = 0; j < NK; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(((w - half) * NK + j) * 16 + r) * 64 + lane] = acc[j][r];
+    }
+    __syncthreads();
+    if (w < half) {
+#pragma unroll
+      for (int j = 0; j < NK; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] += red[((w * NK + j) * 16 + r) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  if (do_bias) {
+    bs += __shfl_xor(bs, 32, 64);
+    if (lg == 0) rsum[w * 32 + li] = bs;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  float* dW = d.dW + (int64_t)s * d.CO * Kc;
+#pragma unroll
+  for (int j = 0; j < NK; ++j) {
+    if (!kok[j]) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * lg;
+      dW[(int64_t)co * Kc + kout[j]] = U8 ? __fdiv_rn(acc[j][r], 255.f) : acc[j][r];
+    }
+  }
+  if (do_bias && lg == 0) {
+    double tot = 0.0;
+    for (int v = 0; v < NW; ++v) tot += rsum[v * 32 + li];
+    d.db[(int64_t)s * d.CO + co0 + li] = (float)tot;
+  }
+}
+
+// Input gradient on the bf16 matrix cores at fp32 accuracy: dx[b][y][x][c] =
+// [x > 0] sum over the output positions (oy, ox) whose window covers (y, x) of
+// sum_co dy[b][oy][ox][co] W[co][c][y - S oy][x - S ox] -- im2col's transpose
+// (col2im of dy W) as one implicit GEMM, no column matrix in HBM.  Rows are
+// walked per stride phase (py, px) = (y % S, x % S): every row of a phase
+// takes the same taps kh = py + S ih, kw = px + S iw, at oy = y / S - ih,
+// ox = x / S - iw, so a workgroup's weight chunk is shared by its 128 rows
+// (M = phase rows, N = c, K = (ih, iw, co), a missing position a zero
+// operand).  dy is read as float4 runs of 8 co (CO % 16 == 0); the weight is
+// staged per 32-k chunk in three bf16 parts, six products.
+template <int WN>
+__global__ __launch_bounds__(256) void conv_bwd_x_x6_kernel(d3a_conv_desc d) {
+  using namespace x6;
+  constexpr int C = 32 * WN, BK = 32, LDB = BK + 8;
+  __shared__ __attribute__((aligned(16))) __bf16 Ws[2][3][C * LDB];
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  const int li = lane & 31, lg = lane >> 5;
+  const int S = d.S, CO = d.CO;
+  const int py = blockIdx.y / S, px = blockIdx.y - py * S;
+  const int nyp = (d.H - py + S - 1) / S, nxp = (d.W - px + S - 1) / S;
+  const int NTH = (d.KH - py + S - 1) / S, NTW = (d.KW - px + S - 1) / S;
+  const int Kc = NTH * NTW * CO;
+  const int64_t Mp = (int64_t)d.B * nyp * nxp;
+  if ((int64_t)blockIdx.x * 128 >= Mp) return;  // whole workgroup, before any barrier
+  const int64_t m0 = ((int64_t)blockIdx.x * 4 + w) * 32;
+  const int64_t m = m0 + li;
+  const bool valid = m < Mp;
+  int64_t bimg = 0;
+  int yi = 0, xi = 0;
+  if (valid) {
+    bimg = m / (nyp * nxp);
+    const int r = (int)(m - bimg * nyp * nxp);
+    yi = r / nxp;
+    xi = r - yi * nxp;
+  }
+  const float* dyb = d.dy + bimg * d.OH * d.OW * CO;
+  // weight chunk: C x 32 values (c = e >> 5, kk = e & 31), WN x 4 per thread
+  float wv[4 * WN];
+  auto wload = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 4 * WN; ++j) {
+      const int e = t + 256 * j, c = e >> 5, kk = e & 31;
+      const int k = k0 + kk;
+      float v = 0.f;
+      if (k < Kc) {
+        const int tap = k / CO, co = k - tap * CO;
+        const int ih = tap / NTW, iw = tap - ih * NTW;
+        const int kh = py + S * ih, kw = px + S * iw;
+        v = d.weight[(((int64_t)co * d.C + c) * d.KH + kh) * d.KW + kw];
+      }
+      wv[j] = v;
+    }
+  };
+  auto wstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 4 * WN; ++j) {
+      const int e = t + 256 * j, c = e >> 5, kk = e & 31;
+      __bf16 q0, q1, q2;
+      split1(wv[j], q0, q1, q2);
+      Ws[buf][0][c * LDB + kk] = q0;
+      Ws[buf][1][c * LDB + kk] = q1;
+      Ws[buf][2][c * LDB + kk] = q2;
+    }
+  };
+  // the A operand of a chunk: per k step s, this lane's 8 k = 8 co of one tap
+  float4 rf[2][2];
+  auto aload = [&](int k0) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int k = k0 + 16 * s2 + 8 * lg;
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+      if (valid && k < Kc) {
+        const int tap = k / CO, co = k - tap * CO;
+        const int ih = tap / NTW, iw = tap - ih * NTW;
+        const int oy = yi - ih, ox = xi - iw;
+        if (oy >= 0 && oy < d.OH && ox >= 0 && ox < d.OW) {
+          const float4* src = reinterpret_cast<const float4*>(dyb + ((int64_t)oy * d.OW + ox) * CO + co);
+          v0 = src[0];
+          v1 = src[1];
+        }
+      }
+      rf[s2][0] = v0;
+      rf[s2][1] = v1;
+    }
+  };
+  f32x16 acc[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  wload(0);
+  wstore(0);
+  __syncthreads();
+  aload(0);
+  int cur = 0;
+  for (int k0 = 0; k0 < Kc; k0 += BK) {
+    const bool more = k0 + BK < Kc;
+    if (more) wload(k0 + BK);
+    float4 cf[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      cf[s2][0] = rf[s2][0];
+      cf[s2][1] = rf[s2][1];
+    }
+    if (more) aload(k0 + BK);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 a[3];
+      const float v[8] = {cf[s2][0].x, cf[s2][0].y, cf[s2][0].z, cf[s2][0].w,
+                          cf[s2][1].x, cf[s2][1].y, cf[s2][1].z, cf[s2][1].w};
+      split8(v, a);
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        bf16x8 bq[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          bq[q] = *reinterpret_cast<const bf16x8*>(&Ws[cur][q][(32 * j + li) * LDB + 16 * s2 + 8 * lg]);
+        acc[j] = prod6(a, bq, acc[j]);
+      }
+    }
+    if (more) wstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (m0 >= Mp) return;
+  // epilogue: acc[j][r] -> phase row m0 + (r&3) + 8*(r>>2) + 4*lg, channel 32*j + li
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * lg;
+    if (mm >= Mp) continue;
+    const int64_t bb = mm / (nyp * nxp);
+    const int rr = (int)(mm - bb * nyp * nxp);
+    const int yy = py + S * (rr / nxp), xx = px + S * (rr - (rr / nxp) * nxp);
+    const int64_t o = ((bb * d.H + yy) * d.W + xx) * C;
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int n = 32 * j + li;
+      float v = acc[j][r];
+      if (d.relu && !(d.x_f32[o + n] > 0.f)) v = 0.f;
+      d.y[o + n] = v;
+    }
+  }
+}
+
 int check_geometry(const d3a_conv_desc* d, const char* name) {
   D3A_CHECK_ARG(d != nullptr, "%s: null descriptor", name);
   D3A_CHECK_ARG((d->x_u8 != nullptr) != (d->x_f32 != nullptr),
@@ -598,6 +900,36 @@ extern "C" int d3a_conv_fwd(const d3a_conv_desc* d, void* stream) {
   return 0;
 }
 
+namespace d3a {
+namespace {
+// the split-bf16 weight-gradient kernel unless D3A_CONV_BWD_X6=0
+bool conv_bwd_x6() {
+  static const bool on = [] {
+    const char* e = getenv("D3A_CONV_BWD_X6");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+}  // namespace
+}  // namespace d3a
+
+// the weight-gradient split count that fills the chip for this geometry (the
+// caller sizes its dW / db partial space with it): about 512 workgroups of the
+// split-bf16 kernel, at least 16 rows a wave
+extern "C" int32_t d3a_conv_bwd_w_splits(const d3a_conv_desc* d) {
+  using namespace d3a;
+  if (d == nullptr) return -1;
+  const int64_t M = (int64_t)d->B * d->OH * d->OW;
+  const int64_t Kc = (int64_t)d->C * d->KH * d->KW;
+  const int64_t tiles = ((Kc + 63) / 64) * (d->CO / 32 > 0 ? d->CO / 32 : 1);
+  int64_t s = (512 + tiles - 1) / tiles;
+  const int64_t cap = M / 128 > 1 ? M / 128 : 1;  // >= 16 rows for each of 8 waves
+  if (s > cap) s = cap;
+  if (s < 1) s = 1;
+  if (s > 1024) s = 1024;
+  return (int32_t)s;
+}
+
 extern "C" int d3a_conv_bwd_w(const d3a_conv_desc* d, void* stream) {
   using namespace d3a;
   if (check_geometry(d, "d3a_conv_bwd_w")) return -1;
@@ -605,10 +937,41 @@ extern "C" int d3a_conv_bwd_w(const d3a_conv_desc* d, void* stream) {
   D3A_CHECK_ARG(d->splits >= 1 && d->splits < 65536, "d3a_conv_bwd_w: bad splits");
   const int64_t Kc = (int64_t)d->C * d->KH * d->KW;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (conv_bwd_x6()) {
+    // split-bf16 weight gradient: 32 (co) x 64 (k) per wave, 8 waves a workgroup
+    constexpr int NK = 2;
+    const dim3 grid((unsigned)((Kc + 32 * NK - 1) / (32 * NK)), (unsigned)(d->CO / 32), (unsigned)d->splits);
+    if (d->x_u8) hipLaunchKernelGGL((conv_bwd_w_x6_kernel<NK, true>), grid, dim3(512), 0, st, *d);
+    else hipLaunchKernelGGL((conv_bwd_w_x6_kernel<NK, false>), grid, dim3(512), 0, st, *d);
+    D3A_LAUNCH_CHECK("d3a_conv_bwd_w");
+    return 0;
+  }
   // 32 (co) x 32 (k) per wave, 16 waves per workgroup over consecutive row slices
   const dim3 grid((unsigned)((Kc + 31) / 32), (unsigned)(d->CO / 32), (unsigned)d->splits);
   if (d->x_u8) hipLaunchKernelGGL((conv_bwd_w_kernel<1, 16, true>), grid, dim3(1024), 0, st, *d);
   else hipLaunchKernelGGL((conv_bwd_w_kernel<1, 16, false>), grid, dim3(1024), 0, st, *d);
   D3A_LAUNCH_CHECK("d3a_conv_bwd_w");
+  return 0;
+}
+
+extern "C" int d3a_conv_bwd_x(const d3a_conv_desc* d, void* stream) {
+  using namespace d3a;
+  if (check_geometry(d, "d3a_conv_bwd_x")) return -1;
+  D3A_CHECK_ARG(d->dy && d->y, "d3a_conv_bwd_x: null dy / dx (y)");
+  D3A_CHECK_ARG(d->x_f32 || !d->relu, "d3a_conv_bwd_x: the ReLU gate reads x_f32");
+  D3A_CHECK_ARG(d->C == 32 || d->C == 64, "d3a_conv_bwd_x: C must be 32 or 64");
+  D3A_CHECK_ARG(d->CO % 16 == 0 && (reinterpret_cast<uintptr_t>(d->dy) & 15) == 0,
+                "d3a_conv_bwd_x: dy must be 16-byte aligned rows of CO %% 16 == 0 floats");
+  D3A_CHECK_ARG(d->S <= 8, "d3a_conv_bwd_x: stride must be <= 8");
+  const int64_t nyp = (d->H + d->S - 1) / d->S, nxp = (d->W + d->S - 1) / d->S;
+  const int64_t Mp = (int64_t)d->B * nyp * nxp;  // the largest phase
+  if (Mp == 0) return 0;
+  const int64_t blocks = (Mp + 127) / 128;
+  D3A_CHECK_ARG(blocks < (1ll << 31), "d3a_conv_bwd_x: too many rows");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)blocks, (unsigned)(d->S * d->S)), block(256);
+  if (d->C == 32) hipLaunchKernelGGL((conv_bwd_x_x6_kernel<1>), grid, block, 0, st, *d);
+  else hipLaunchKernelGGL((conv_bwd_x_x6_kernel<2>), grid, block, 0, st, *d);
+  D3A_LAUNCH_CHECK("d3a_conv_bwd_x");
   return 0;
 }

@@ -63,6 +63,18 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// A value of the policy head given as np partial sums (cql.hip's head_val:
+// parts summed in order)
+__device__ __forceinline__ float head_part_sum(const float* h, int64_t sp, int np, int64_t j) {
+  if (np == D3A_MLP_PARTS) {
+    const float a = h[j], b = h[sp + j], c = h[2 * sp + j], e = h[3 * sp + j];
+    return ((a + b) + c) + e;
+  }
+  float v = h[j];
+  for (int p = 1; p < np; ++p) v += h[p * sp + j];
+  return v;
+}
+
 // XL: the first layer's input width rounded up to 4 (16, 32 or 48), fixed at
 // compile time so the LDS addresses of the x operand are immediates
 // NOSTAGE (timing probe only, tools/bench_q2.py --probe): the sub-block
@@ -72,10 +84,19 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 // DZIN: dz2 is given (d.dz2, already masked: a caller's head kernel formed
 // it, e.g. d3a_sac_actor_head for the policy) instead of generated from g, w3
 // and h2; no head gradients
-template <int XL, bool NOSTAGE = false, int Q2_NSB = Q2_NSB8, bool DZIN = false>
-__global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
+// HEADIN (with DZIN, one 32-row sub-block): the SAC / CQL actor head itself
+// (d3a_sac_actor_head's dq_min arithmetic, descriptor hd) runs in this
+// launch's prologue: each workgroup forms dhead of its 32 rows and their dz2
+// from it (the same fma order: bitwise the head kernel's dz), quarter-0
+// workgroups write dhead and the head's per-row weight / bias partials, and
+// workgroup 0 the actor-loss metric -- one launch fewer in the actor phase
+template <int XL, bool NOSTAGE = false, int Q2_NSB = Q2_NSB8, bool DZIN = false, bool HEADIN = false>
+__global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d, d3a_sac_actor_head_desc hd) {
   constexpr int Q2_RB = Q2_NSB * Q2_SB;
+  static_assert(!HEADIN || (DZIN && Q2_NSB == 1), "HEADIN is the one-sub-block dz2 instantiation");
   __shared__ __attribute__((aligned(16))) Q2Lds<XL> L;
+  __shared__ float sdh[HEADIN ? Q2_SB : 1][HEADIN ? 33 : 1];  // dhead rows [row][2A]
+  __shared__ float hscr[HEADIN ? Q2_NT / 64 : 1];
   static_assert(sizeof(Q2Lds<XL>) <= 163840, "LDS");
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform
@@ -98,7 +119,7 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
   constexpr int ldh = Q2_H;  // h1 / h2 rows are [C][rows][256] (checked)
   const float* h1g = d.h1 + c * d.sh;
   // DZIN: h2g walks dz2 (same [rows][256] row layout), gg unused
-  const float* h2g = DZIN ? d.dz2 + c * d.sdz : d.h2 + c * d.sh;
+  const float* h2g = HEADIN ? nullptr : DZIN ? d.dz2 + c * d.sdz : d.h2 + c * d.sh;
   const float* gg = DZIN ? nullptr : d.g + c * d.sgb;
   const float* xg = d.x + c * d.sxb;
   const float* W2g = d.W2 + c * d.sW2;
@@ -116,6 +137,90 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
   const int ib = w & 1, kh = (w >> 1) & 1;  // dX waves: unit block, K half
   const int ob0 = 64 * (w - 4);             // dW2 waves: o block
 
+  if constexpr (HEADIN) {
+    const int A = hd.A, Cq = hd.C;
+    const int np = hd.dq_min ? hd.n_part : 1;
+    const int hp = hd.head_parts > 1 ? hd.head_parts : 1;
+    const float et = hd.scalars[0];
+    auto qv = [&](int cc, int64_t r) {
+      float v = hd.q[cc * hd.sqc + r];
+      for (int pp = 1; pp < np; ++pp) v += hd.q[pp * hd.sq_part + cc * hd.sqc + r];
+      return v;
+    };
+    if (t < Q2_SB * A) {
+      const int rl = t / A, j = t - rl * A;
+      const int64_t b = rb0 + rl;
+      float dmu = 0.f, dls = 0.f;
+      if (b < rows) {
+        // backward of min over the members (the first of least q), parts in order
+        int arg = 0;
+        float mn = qv(0, b);
+        for (int cc = 1; cc < Cq; ++cc) {
+          const float v = qv(cc, b);
+          if (v < mn) { mn = v; arg = cc; }
+        }
+        const float* jp = hd.dq_da + arg * hd.sda_c + b * hd.ld_da + hd.da_off + j;
+        float jv = jp[0];
+        for (int pp = 1; pp < np; ++pp) jv += jp[pp * hd.sda_part];
+        const float da = hd.dq_scale * jv;
+        const float dlogp = et / (float)hd.B;
+        const float* hrow = hd.head + b * 2 * A;
+        const float mu = head_part_sum(hrow, hd.s_head_part, hp, j);
+        const float lsr = head_part_sum(hrow, hd.s_head_part, hp, A + j);
+        const float l = fminf(fmaxf(lsr, hd.min_logstd), hd.max_logstd);
+        const float sd = expf(l);
+        const float u = hd.u[b * A + j];
+        const float e = hd.eps[b * A + j];
+        const float th = tanhf(u);
+        const float dm = u - mu;
+        const float var = sd * sd;
+        const float dlp_du = -dm / var + 2.f - 4.f * sigmoidf_t(-2.f * u);
+        const float du = da * (1.f - th * th) + dlogp * dlp_du;
+        dmu = du + dlogp * (dm / var);
+        const float dsd = du * e + dlogp * ((dm * dm) / (var * sd) - 1.f / sd);
+        const bool pass = (lsr >= hd.min_logstd) && (lsr <= hd.max_logstd);
+        dls = pass ? dsd * sd : 0.f;
+        if (q == 0) {
+          hd.dhead[b * 2 * A + j] = dmu;
+          hd.dhead[b * 2 * A + A + j] = dls;
+          if (hd.db_part) {
+            hd.db_part[b * 2 * A + j] = dmu;
+            hd.db_part[b * 2 * A + A + j] = dls;
+          }
+        }
+      }
+      sdh[rl][j] = dmu;
+      sdh[rl][A + j] = dls;
+    }
+    if (q == 0 && p == 0) {
+      // the actor loss mean(exp(log_temp) * logp - min_c Q) (the head kernel's
+      // last workgroup: rows strided by 256, the same block sum -- waves 4..7
+      // add zeros)
+      float lsum = 0.f;
+      if (t < 256) {
+        for (int64_t r = t; r < hd.B; r += 256) {
+          float qmin = qv(0, r);
+          for (int cc = 1; cc < Cq; ++cc) qmin = fminf(qmin, qv(cc, r));
+          lsum += et * hd.logp[r] - qmin;
+        }
+      }
+      const float tot = block_sum(lsum, hscr);
+      if (t == 0) hd.metrics[5] = tot / (float)hd.B;
+    }
+    __syncthreads();  // dhead rows in LDS
+    if (q == 0 && hd.dW_part) {
+      // the head's per-row weight partials dW[k][n] = dhead[k] h[n], n = t & 255
+      const int n = t & (Q2_H - 1);
+      for (int rl = t >> 8; rl < Q2_SB; rl += Q2_NT / Q2_H) {
+        const int64_t b = rb0 + rl;
+        if (b >= rows) continue;
+        const float hv = hd.h[b * hd.ldh + n];
+        float* pw = hd.dW_part + b * 2 * A * hd.H + n;
+        for (int k = 0; k < 2 * A; ++k) pw[(int64_t)k * hd.H] = sdh[rl][k] * hv;
+      }
+    }
+  }
+
   float w3v[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) w3v[j] = DZIN ? 0.f : w3g[lane + 64 * j];
@@ -128,8 +233,21 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
     int64_t r = rb0 + sb * Q2_SB + w + 8 * s;
     r = r < rlast ? r : rlast;
     gv[s] = DZIN ? 0.f : gg[r];
+    if constexpr (HEADIN) {
+      // dz2[r][n] = (sum_k dhead[r][k] w_head[k][n]) * [h[r][n] > 0], the head
+      // kernel's fma order (rows past the end: staged as zero later)
+      const int rl = (int)(r - rb0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) hv[s][j] = h2g[(int)r * ldh + lane + 64 * j];
+      for (int j = 0; j < 4; ++j) {
+        const int n = lane + 64 * j;
+        float v = 0.f;
+        for (int k = 0; k < 2 * hd.A; ++k) v = fmaf(sdh[rl][k], hd.w_head[(int64_t)k * hd.H + n], v);
+        hv[s][j] = hd.h[r * hd.ldh + n] > 0.f ? v : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hv[s][j] = h2g[(int)r * ldh + lane + 64 * j];
+    }
   };
   auto load_tiles = [&](int sb) {
     const int64_t base = rb0 + sb * Q2_SB;
@@ -424,6 +542,10 @@ __global__ __launch_bounds__(Q2_NT) void q2_bwd_kernel(d3a_q2_bwd_desc d) {
 
 using namespace d3a;
 
+namespace d3a {
+int q2_bwd_launch(const d3a_q2_bwd_desc& d, const d3a_sac_actor_head_desc* head, void* stream);
+}
+
 extern "C" int d3a_q2_bwd(const d3a_q2_bwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_bwd: null desc");
   const d3a_q2_bwd_desc& d = *dp;
@@ -450,37 +572,85 @@ extern "C" int d3a_q2_bwd(const d3a_q2_bwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(d.rows * (d.ldh > d.ldx ? d.ldh : d.ldx) < (int64_t(1) << 31),
                 "d3a_q2_bwd: rows x row stride exceeds 2^31");
   if (d.rows == 0) return 0;
+  return q2_bwd_launch(d, nullptr, stream);
+}
+
+// The policy trunk backward with the SAC actor head in its prologue: the
+// work of d3a_sac_actor_head (dq_min form, dz not written) followed by
+// d3a_q2_bwd with dz2, in one launch -- the same dhead, head partials, metric
+// and trunk gradients bit for bit
+extern "C" int d3a_q2_bwd_actor_head(const d3a_q2_bwd_desc* dp, const d3a_sac_actor_head_desc* hp,
+                                     void* stream) {
+  D3A_CHECK_ARG(dp && hp, "d3a_q2_bwd_actor_head: null desc");
+  const d3a_q2_bwd_desc& d = *dp;
+  const d3a_sac_actor_head_desc& h = *hp;
+  D3A_CHECK_ARG(d.m2 == nullptr && d.dz2 == nullptr,
+                "d3a_q2_bwd_actor_head: dz2 is formed here (no dz2, no mask image)");
+  D3A_CHECK_ARG(d.C == 1 && d.block_rows == 32, "d3a_q2_bwd_actor_head: one trunk, block_rows 32");
+  D3A_CHECK_ARG(d.x && d.h1 && d.W2 && d.dW1 && d.db1 && d.dW2 && d.db2,
+                "d3a_q2_bwd_actor_head: null trunk operand");
+  D3A_CHECK_ARG(d.n_in >= 1 && d.n_in <= 48 && d.ldx >= d.n_in && d.rows == h.B,
+                "d3a_q2_bwd_actor_head: bad sizes (n_in 1..48, rows == B)");
+  auto a16 = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; };
+  D3A_CHECK_ARG(a16(d.h1) && d.ldh == Q2_H && a16(d.W2) && d.sW2 % 4 == 0,
+                "d3a_q2_bwd_actor_head: h1 / W2 must be 16-byte aligned rows of 256 floats");
+  D3A_CHECK_ARG(d.rows * (d.ldh > d.ldx ? d.ldh : d.ldx) < (int64_t(1) << 31),
+                "d3a_q2_bwd_actor_head: rows x row stride exceeds 2^31");
+  D3A_CHECK_ARG(h.B >= 1 && h.A >= 1 && h.A <= 16 && h.C >= 1 && h.dq_min && h.dq_da && h.q &&
+                    h.n_part >= 1 && !h.dq_dz,
+                "d3a_q2_bwd_actor_head: the head's dq_min form (dq_da and q in n_part parts)");
+  D3A_CHECK_ARG(h.h && h.w_head && h.H == Q2_H && h.head && h.eps && h.u && h.logp && h.dhead &&
+                    h.metrics && h.scalars,
+                "d3a_q2_bwd_actor_head: null head operand, or H != 256");
+  return q2_bwd_launch(d, &h, stream);
+}
+
+// the launch of a checked descriptor (d3a_q2_bwd, d3a_q2_bwd_actor_head)
+int d3a::q2_bwd_launch(const d3a_q2_bwd_desc& d, const d3a_sac_actor_head_desc* head, void* stream) {
+  const bool dzin = d.dz2 != nullptr || head != nullptr;
   const int64_t rb = dzin ? 32 : 256;
   const int64_t units = ((d.rows + rb - 1) / rb) * d.C;
   const int64_t blocks = (units + 7) / 8 * 32;
   D3A_CHECK_ARG(blocks < (int64_t(1) << 31), "d3a_q2_bwd: too many rows");
   const int xl = (d.n_in + 3) & ~3;
   const dim3 grid((unsigned)blocks), block(Q2_NT);
+  const d3a_sac_actor_head_desc hz{};
   static const bool probe = [] {
     const char* e = getenv("D3A_Q2_PROBE");
     return e && e[0] == '1';
   }();
   if (probe && xl <= 16) {
-    hipLaunchKernelGGL((q2_bwd_kernel<16, true>), grid, block, 0, (hipStream_t)stream, d);
+    hipLaunchKernelGGL((q2_bwd_kernel<16, true>), grid, block, 0, (hipStream_t)stream, d, hz);
     D3A_LAUNCH_CHECK("d3a_q2_bwd");
+    return 0;
+  }
+  if (head != nullptr) {
+    const d3a_sac_actor_head_desc h = *head;
+    if (xl <= 16)
+      hipLaunchKernelGGL((q2_bwd_kernel<16, false, 1, true, true>), grid, block, 0, (hipStream_t)stream, d, h);
+    else if (xl <= 32)
+      hipLaunchKernelGGL((q2_bwd_kernel<32, false, 1, true, true>), grid, block, 0, (hipStream_t)stream, d, h);
+    else
+      hipLaunchKernelGGL((q2_bwd_kernel<48, false, 1, true, true>), grid, block, 0, (hipStream_t)stream, d, h);
+    D3A_LAUNCH_CHECK("d3a_q2_bwd_actor_head");
     return 0;
   }
   if (dzin) {
     if (xl <= 16)
-      hipLaunchKernelGGL((q2_bwd_kernel<16, false, 1, true>), grid, block, 0, (hipStream_t)stream, d);
+      hipLaunchKernelGGL((q2_bwd_kernel<16, false, 1, true>), grid, block, 0, (hipStream_t)stream, d, hz);
     else if (xl <= 32)
-      hipLaunchKernelGGL((q2_bwd_kernel<32, false, 1, true>), grid, block, 0, (hipStream_t)stream, d);
+      hipLaunchKernelGGL((q2_bwd_kernel<32, false, 1, true>), grid, block, 0, (hipStream_t)stream, d, hz);
     else
-      hipLaunchKernelGGL((q2_bwd_kernel<48, false, 1, true>), grid, block, 0, (hipStream_t)stream, d);
+      hipLaunchKernelGGL((q2_bwd_kernel<48, false, 1, true>), grid, block, 0, (hipStream_t)stream, d, hz);
     D3A_LAUNCH_CHECK("d3a_q2_bwd");
     return 0;
   }
   if (xl <= 16)
-    hipLaunchKernelGGL(q2_bwd_kernel<16>, grid, block, 0, (hipStream_t)stream, d);
+    hipLaunchKernelGGL(q2_bwd_kernel<16>, grid, block, 0, (hipStream_t)stream, d, hz);
   else if (xl <= 32)
-    hipLaunchKernelGGL(q2_bwd_kernel<32>, grid, block, 0, (hipStream_t)stream, d);
+    hipLaunchKernelGGL(q2_bwd_kernel<32>, grid, block, 0, (hipStream_t)stream, d, hz);
   else
-    hipLaunchKernelGGL(q2_bwd_kernel<48>, grid, block, 0, (hipStream_t)stream, d);
+    hipLaunchKernelGGL(q2_bwd_kernel<48>, grid, block, 0, (hipStream_t)stream, d, hz);
   D3A_LAUNCH_CHECK("d3a_q2_bwd");
   return 0;
 }

@@ -100,6 +100,9 @@ _XGEN = os.environ.get("D3A_XGEN", "1") == "1"
 # the x6 critic backward reads the forward's bf16 mask image of h2 instead of
 # building it from h2 (D3A_MASK_IMAGE=0: build it, A/B)
 _MASK_IMAGE = os.environ.get("D3A_MASK_IMAGE", "1") == "1"
+# the SAC / CQL actor head in the policy trunk backward's prologue
+# (d3a_q2_bwd_actor_head: one launch fewer per actor update)
+_HEAD_IN_TRUNK = os.environ.get("D3A_HEAD_IN_TRUNK", "1") == "1"
 
 
 def q2_shape(net: EnsembleMLP) -> bool:
@@ -387,7 +390,8 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
              sxb: Optional[int] = None, q_min: Optional[int] = None, sq_b: int = 0,
              q_scale: float = 0.0, g_out: Optional[int] = None,
              g_scale: Optional[int] = None, n_scaled: int = 0,
-             members: Optional[int] = None, head_ready: bool = False) -> Optional[torch.Tensor]:
+             members: Optional[int] = None, head_ready: bool = False,
+             head_desc=None) -> Optional[torch.Tensor]:
     """Backward of rows [r0, r0+n) given dL/d(output) (``dout`` points at row r0).
     Returns (per-layer path) the dz buffer holding the first layer's
     pre-activation gradient [C][rows][ld] once the trunk has run.
@@ -399,6 +403,10 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
     ``head_ready``: the caller's head kernel already wrote the head's input
     gradient into ``bs.dz[0]`` and its weight / bias gradient partials (per-
     layer path only); the backward starts at the trunk.
+    ``head_desc`` (with ``head_ready``, the one-launch trunk of a 2x256 policy):
+    the d3a_sac_actor_head descriptor (dq_min form) whose work runs in the
+    trunk launch's prologue instead (d3a_q2_bwd_actor_head); returns False
+    when the shape does not take it (the caller launches the head first).
     """
     net = bs.net
     C, L, sizes, R = net.C, net.n_layers, net.sizes, acts.R
@@ -459,8 +467,17 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         d.dW1, d.db1 = gs.get(net.wname(0)).data_ptr(), gs.get(net.bname(0)).data_ptr()
         d.dW2, d.db2 = gs.get(net.wname(1)).data_ptr(), gs.get(net.bname(1)).data_ptr()
         d.rows, d.n_in, d.C = n, sizes[0], C
+        if head_desc is not None:
+            if not (_HEAD_IN_TRUNK and C == 1 and head_desc.dq_min and not head_desc.dq_dz
+                    and head_desc.H == H and head_desc.B == n):
+                return False
+            d.dz2 = None  # formed per workgroup from dhead
+            ops.call_desc("d3a_q2_bwd_actor_head", d, head_desc)
+            return True
         ops.call_desc("d3a_q2_bwd", d)
         return None
+    if head_desc is not None:
+        return False
 
     def h_ptr(l):  # input activation of layer l at row r0
         if l == 0:

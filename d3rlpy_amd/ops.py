@@ -234,9 +234,12 @@ def philox_fill(out: torch.Tensor, n_normal: int, n_uniform: int, lo: float, hi:
                                     _stream()), "d3a_philox_fill")
 
 
-def call_desc(fn_name: str, desc: C.Structure) -> None:
+def call_desc(fn_name: str, desc: C.Structure, desc2: Optional[C.Structure] = None) -> None:
     fn = getattr(N.lib(), fn_name)
-    N.check(fn(C.byref(desc), _stream()), fn_name)
+    if desc2 is None:
+        N.check(fn(C.byref(desc), _stream()), fn_name)
+    else:
+        N.check(fn(C.byref(desc), C.byref(desc2), _stream()), fn_name)
 
 
 # ---------------------------------------------------------------------------

@@ -707,6 +707,14 @@ typedef struct d3a_sac_actor_head_desc {
   int64_t s_head_part;
 } d3a_sac_actor_head_desc;
 int d3a_sac_actor_head(const d3a_sac_actor_head_desc* d, void* stream);
+/* The policy trunk backward (d3a_q2_bwd with dz2, C == 1, block_rows 32)
+ * with d3a_sac_actor_head's dq_min work in its prologue: dz2 is formed per
+ * workgroup from dhead (not written), dhead / db_part / dW_part / metrics[5]
+ * as the head kernel writes them.  Replaces the two launches that follow
+ * torch autograd through the policy's `_mu` / `_logstd` heads and encoder
+ * (d3rlpy/models/torch/policies.py:170-176, encoders.py:165-176). */
+int d3a_q2_bwd_actor_head(const d3a_q2_bwd_desc* d, const d3a_sac_actor_head_desc* head,
+                          void* stream);
 
 /* ---- the actor phase's critic pass in one launch (CQL / SAC actor update,
  *      d3rlpy/algos/torch/sac_impl.py:120 `self._q_func(obs, action, "min")`
@@ -972,6 +980,16 @@ typedef struct d3a_conv_desc {
 } d3a_conv_desc;
 int d3a_conv_fwd(const d3a_conv_desc* d, void* stream);
 int d3a_conv_bwd_w(const d3a_conv_desc* d, void* stream);
+/* The split count d3a_conv_bwd_w fills the chip with for this geometry (reads
+ * B, C, KH, KW, OH, OW, CO only); callers size the dW / db partials with it. */
+int32_t d3a_conv_bwd_w_splits(const d3a_conv_desc* d);
+/* Input gradient of the convolution (autograd of nn.Conv2d's input,
+ * encoders.py:130-136, through the previous layer's ReLU): y (as dx, NHWC
+ * [B][H][W][C]) = [x_f32 > 0 when relu] * sum over the output positions whose
+ * window covers the pixel of dy W -- one implicit GEMM per stride phase
+ * (replaces the column-matrix GEMM + d3a_col2im pair).  Needs fp32 x
+ * geometry with C = 32 or 64, CO % 16 == 0, dy 16-byte aligned. */
+int d3a_conv_bwd_x(const d3a_conv_desc* d, void* stream);
 
 /* Per-sample [P][C] (NHWC) <-> [C][P] (NCHW) transpose, optional [mask > 0]
  * in the destination layout: the flatten before PixelEncoder._fc

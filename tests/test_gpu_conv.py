@@ -146,3 +146,39 @@ def test_conv_rejects_bad_geometry(dev):
     d.OH = 21                                    # inconsistent output size
     d.x_u8, d.weight, d.y = 1, 1, 1
     assert lib.d3a_conv_fwd(ctypes.byref(d), None) < 0
+
+
+# (B, C, H, W, CO, K, S): the K5 layers 2 and 3, uneven stride phases (H, W
+# not multiples of S), a stride whose phases take different tap counts (K 4,
+# S 3), CO 32
+BWD_X_CASES = [(5, 32, 20, 20, 64, 4, 2), (7, 64, 9, 9, 64, 3, 1), (2, 32, 11, 13, 64, 3, 2),
+               (3, 64, 10, 10, 32, 4, 3), (1, 32, 8, 8, 64, 8, 4)]
+
+
+@pytest.mark.parametrize("B,C,H,W,CO,K,S", BWD_X_CASES)
+@pytest.mark.parametrize("relu", [1, 0])
+def test_conv_bwd_x_matches_autograd(dev, B, C, H, W, CO, K, S, relu):
+    """d3a_conv_bwd_x against autograd's input gradient of conv2d (fp64),
+    times [x > 0] (the ReLU of the layer that produced x) when relu."""
+    from d3rlpy_amd import _native as N, ops
+    g = torch.Generator().manual_seed(B * 23 + C + K * 5 + S)
+    x = torch.randn(B, C, H, W, generator=g, dtype=torch.float64).float().double()
+    Wt = (torch.randn(CO, C, K, K, generator=g) * (1.0 / (C * K * K) ** 0.5))
+    OH, OW = (H - K) // S + 1, (W - K) // S + 1
+    dy = torch.randn(B, OH, OW, CO, generator=g)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, Wt.double(), None, stride=S).backward(dy.double().permute(0, 3, 1, 2))
+    ref = xr.grad * (x > 0) if relu else xr.grad
+    ref = ref.permute(0, 2, 3, 1).reshape(-1, C)
+    d = _desc(N, B, C, H, W, CO, K, S)
+    xd = x.float().permute(0, 2, 3, 1).contiguous().to(dev)
+    Wd, dyd = Wt.to(dev), dy.to(dev).contiguous()
+    dx = torch.full((B * H * W, C), float("nan"), device=dev)
+    d.x_f32, d.weight, d.dy, d.y, d.relu = xd.data_ptr(), Wd.data_ptr(), dyd.data_ptr(), \
+        dx.data_ptr(), relu
+    ops.call_desc("d3a_conv_bwd_x", d)
+    torch.cuda.synchronize()
+    assert torch.isfinite(dx).all()
+    assert _rel(dx, ref) < 2e-5
+    if relu:
+        assert bool((dx.cpu()[ref == 0] == 0).all())

@@ -392,3 +392,50 @@ def test_cql_sample_draws_equal_philox_fill():
     torch.cuda.synchronize()
     for a, b in zip(got, (ws.x_q, ws.logp_is, ws.logp_temp, ws.actor_logp, ws.eps_actor)):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("case", ["hopper", "k4_antmaze"])
+def test_actor_head_in_trunk_is_bitwise_the_two_launches(case, monkeypatch):
+    """d3a_q2_bwd_actor_head (the actor head in the policy trunk backward's
+    prologue) against d3a_sac_actor_head + d3a_q2_bwd with dz2: the same
+    policy gradients, parameters, Adam state and metrics bit for bit over
+    three updates (the fused kernel keeps the head kernel's arithmetic and
+    fma order; only the launch count differs)."""
+    from d3rlpy_amd import mlp
+    cfg = CASES[case]
+    D, A, H, N, B = cfg["D"], cfg["A"], cfg["hidden"], cfg["N"], cfg["B"]
+    orc = make_oracle(D, A, H, N, seed=5)
+    sd0 = copy.deepcopy(oracle_state(orc))
+    rs = np.random.RandomState(3)
+    gen = torch.Generator().manual_seed(4)
+    batches = [(make_batch(rs, B, D, A), CQLNoise.draw(gen, B, A, N)) for _ in range(3)]
+    runs = []
+    for fused in (False, True):
+        monkeypatch.setattr(mlp, "_HEAD_IN_TRUNK", fused)
+        impl = make_impl(D, A, H, N)
+        impl.set_state_dict(copy.deepcopy(sd0))
+        calls = []
+        from d3rlpy_amd import ops
+        real = ops.call_desc
+        monkeypatch.setattr(ops, "call_desc",
+                            lambda name, *a: (calls.append(name), real(name, *a))[1])
+        ms = [impl.update_step(HostBatch(*arrs), noise=noise_dict(nz)) for arrs, nz in batches]
+        monkeypatch.setattr(ops, "call_desc", real)
+        torch.cuda.synchronize()
+        grads = [impl.policy_grad(impl.policy.wname(l)).cpu() for l in range(impl.policy.n_layers)]
+        runs.append((ms, _impl_policy_params(impl), grads, impl.get_state_dict(), calls))
+    (m0, p0, g0, s0, c0), (m1, p1, g1, s1, c1) = runs
+    assert "d3a_q2_bwd_actor_head" in c1 and "d3a_q2_bwd_actor_head" not in c0
+    assert c1.count("d3a_sac_actor_head") == 0 and c0.count("d3a_sac_actor_head") >= 1
+    for a, b in zip(m0, m1):
+        for k in a:
+            assert a[k] == b[k] or (a[k] != a[k] and b[k] != b[k]), (k, a[k], b[k])
+    for a, b in zip(g0, g1):
+        assert torch.equal(a, b)
+    for (W0, b0), (W1, b1) in zip(p0, p1):
+        assert torch.equal(W0, W1) and torch.equal(b0, b1)
+    for k in ("_actor_optim",):
+        for a, b in zip(torch.utils._pytree.tree_leaves(s0[k]),
+                        torch.utils._pytree.tree_leaves(s1[k])):
+            if isinstance(a, torch.Tensor):
+                assert torch.equal(a, b), k

@@ -23,11 +23,14 @@ python tools/prof_timeline.py $O/prof/run_kernel_trace.csv > $O/cql_timeline.txt
 cd /tmp
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_dom_f -o run --output-format csv -- python3 $R/tools/pmc_dominant.py --algo cql > $O/pmc_dom_f.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_dom_w -o run --output-format csv -- python3 $R/tools/pmc_dominant.py --algo cql > $O/pmc_dom_w.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_dcql_f -o run --output-format csv -- python3 $R/tools/pmc_dominant.py --algo dcql --transitions 100000 > $O/pmc_dcql_f.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_dcql_w -o run --output-format csv -- python3 $R/tools/pmc_dominant.py --algo dcql --transitions 100000 > $O/pmc_dcql_w.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_step_f -o run --output-format csv -- python3 $R/tools/pmc_step.py > $O/pmc_step_f.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_step_w -o run --output-format csv -- python3 $R/tools/pmc_step.py > $O/pmc_step_w.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/pmc_sq -o run --output-format csv -- python3 $R/tools/pmc_step.py > $O/pmc_sq.log 2>&1 || exit $?
 cd $R
 python tools/pmc_summarize.py $O/pmc_dom_f $O/pmc_dom_w q2x6_fwd $O/r04_pmc_traffic_cql_x6.json > $O/pmc_dom.log 2>&1
+python tools/pmc_summarize.py $O/pmc_dcql_f $O/pmc_dcql_w iqn_head_bwd_fused $O/r04_pmc_traffic_dcql_x6.json > $O/pmc_dcql.log 2>&1
 python tools/pmc_step_kernels.py $O/pmc_step_f $O/pmc_step_w > $O/pmc_step_kernels_cql.txt 2>&1
 find $O -name "*counter_collection.csv" -size +20M -delete
 for a in bcq dcql; do
