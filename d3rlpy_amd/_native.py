@@ -509,6 +509,8 @@ _SIGNATURES = {
     "d3a_gather_batch": (C.c_int, [C.POINTER(GatherDesc), vp]),
     "d3a_mlp_fwd": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_gemm_sbf16": (C.c_int, [C.POINTER(GemmDesc), C.c_int32, vp]),
+    "d3a_splitk_epilogue_f32": (C.c_int, [vp, C.c_int32, C.c_int64, vp, vp, C.c_int64, C.c_int64,
+                                          C.c_int32, vp]),
     "d3a_im2col": (C.c_int, [C.POINTER(Im2colDesc), vp]),
     "d3a_col2im": (C.c_int, [C.POINTER(Col2imDesc), vp]),
     "d3a_iqn_transpose": (C.c_int, [C.POINTER(TransposeDesc), vp]),

@@ -327,6 +327,12 @@ class _EncoderPass:
         self.wpack = [z(co * ci * k * k) for (ci, h, w, co, k, s, oh, ow) in impl.geom]
         self.yt = z(n, impl.flat)
         self.h = z(n, impl._F)
+        # the fc as split-K split-bf16 GEMM: about one 128 x 128 tile x slice
+        # per CU (d3a_gemm_sbf16 + d3a_splitk_epilogue_f32)
+        tiles = ((n + 127) // 128) * ((impl._F + 127) // 128)
+        self.fc_splits = max(1, min(32, 256 // tiles, impl.flat // 128))
+        self.fc_part = (z(self.fc_splits, n, impl._F) if _FC_SPLITK and impl.flat % 4 == 0
+                        and impl._F % 4 == 0 else None)
 
     def forward(self, x_u8: int, store: ParamStore) -> None:
         impl = self.impl
@@ -348,10 +354,21 @@ class _EncoderPass:
         # K = 3136, few output tiles: over 2B = 1024 rows the register-direct
         # 32x64 tile with K split over waves (tools/bench_gemm_k5.py: 98 us vs
         # 139 for 64x64 LDS); at 512 rows the library's 32x32 choice (58 vs 96)
+        if self.fc_part is not None:
+            ops.linear_fwd_splitk(self.yt.data_ptr(), impl.flat, store.ptr("enc.fc.W"),
+                                  store.ptr("enc.fc.b"), self.h.data_ptr(), n, impl.flat,
+                                  impl._F, True, self.fc_part, self.fc_splits)
+            return
         ops.linear_fwd(self.yt.data_ptr(), True, impl.flat, store.ptr("enc.fc.W"),
                        store.ptr("enc.fc.b"), self.h.data_ptr(), 1, n, impl.flat, impl._F,
                        relu=True, variant=10 if n > 512 else -1)
 
+
+# the encoder fc on the bf16 matrix cores with fp32-accurate split-bf16
+# operands (d3a_gemm_sbf16, six products): the forward as split-K slices plus
+# an in-order partial-sum epilogue, the weight and input gradients as one
+# launch each; D3A_FC_SPLITK=0 for the fp32-MFMA GEMMs
+_FC_SPLITK = os.environ.get("D3A_FC_SPLITK", "1") == "1"
 
 # the conv input gradient as one implicit GEMM (d3a_conv_bwd_x) rather than
 # the column-matrix GEMM + col2im pair; D3A_CONV_BWD_X=0 for the pair
@@ -659,9 +676,9 @@ class _Workspace:
                                  self.S_emb, db=g.get("q.embed.b").data_ptr(), variant=10)
         ops.linear_bwd_w(self.dzfc.data_ptr(), F, B * F, self.enc.yt.data_ptr(), impl.flat,
                          B * impl.flat, g.get("enc.fc.W").data_ptr(), 1, B, impl.flat, F,
-                         self.S_fc, db=g.get("enc.fc.b").data_ptr())
+                         self.S_fc, db=g.get("enc.fc.b").data_ptr(), sbf16=6 if _FC_SPLITK else 0)
         ops.linear_bwd_x(self.dzfc.data_ptr(), F, B * F, st.ptr("enc.fc.W"), self.dyt.data_ptr(),
-                         impl.flat, B * impl.flat, 1, B, impl.flat, F)
+                         impl.flat, B * impl.flat, 1, B, impl.flat, F, sbf16=6 if _FC_SPLITK else 0)
         ci, h, w, co, k, s, oh, ow = impl.geom[-1]
         t = NAT.TransposeDesc()
         t.src, t.dst, t.mask = self.dyt.data_ptr(), self.dys[-1].data_ptr(), \

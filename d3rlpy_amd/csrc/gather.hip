@@ -115,6 +115,39 @@ __global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
     const int64_t fb = d.frame_bytes, nf = d.n_frames;
     uint8_t* o = d.o_frames + b * nf * fb;
     uint8_t* on = d.o_next_frames + b * nf * fb;
+    const int64_t n16 = fb >> 4;
+    const bool al = ((reinterpret_cast<uintptr_t>(d.frames) | reinterpret_cast<uintptr_t>(o) |
+                      reinterpret_cast<uintptr_t>(on) | (uintptr_t)fb) & 15) == 0;
+    if (al && nf <= 4 && n16 <= 2 * nt) {
+      // every 16-byte piece of the 2 nf frames loaded before any is stored (a
+      // copy loop's store would otherwise wait on its load, frame by frame)
+      uint4 v[8][2];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int q = i & 3;
+        const bool nx = i >= 4;
+        const bool live = q < nf && !(nx && nrow < 0);
+        const int64_t base = nx ? nrow : row;
+        const int64_t r = (base - q > ep0) ? base - q : ep0;
+        const uint4* s4 = reinterpret_cast<const uint4*>(d.frames + r * fb);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int64_t k = tid + (int64_t)j * nt;
+          v[i][j] = (live && k < n16) ? s4[k] : make_uint4(0u, 0u, 0u, 0u);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int q = i & 3;
+        if (q >= nf) continue;
+        uint4* d4 = reinterpret_cast<uint4*>((i >= 4 ? on : o) + (nf - 1 - q) * fb);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int64_t k = tid + (int64_t)j * nt;
+          if (k < n16) d4[k] = v[i][j];
+        }
+      }
+    } else {
     for (int64_t q = 0; q < nf; ++q) {
       // slot nf-1-q holds the frame q steps back, clamped at the episode start
       const int64_t r = (row - q > ep0) ? row - q : ep0;
@@ -125,6 +158,7 @@ __global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
         const int64_t rn = (nrow - q > ep0) ? nrow - q : ep0;
         copy_bytes(on + (nf - 1 - q) * fb, d.frames + rn * fb, fb, tid, nt);
       }
+    }
     }
   }
 

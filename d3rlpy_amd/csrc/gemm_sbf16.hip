@@ -222,6 +222,60 @@ __global__ __launch_bounds__(SB_NT) void gemm_sbf16_kernel(d3a_gemm_desc p, int6
 }  // namespace
 }  // namespace d3a
 
+namespace d3a {
+namespace {
+// y[m][n] = act(sum_s part[s][m][n] + bias[n]), the split-K partials of a
+// d3a_gemm_sbf16 launch added in split order (four n per thread)
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const float* __restrict__ part,
+                                                              int32_t S, int64_t sS, float* y,
+                                                              const float* bias, int64_t M,
+                                                              int64_t N, int32_t relu) {
+  const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n4 = N / 4;
+  if (i4 >= M * n4) return;
+  const int64_t m = i4 / n4, n = 4 * (i4 - m * n4);
+  const int64_t o = m * N + n;
+  float4 a = *reinterpret_cast<const float4*>(part + o);
+  for (int s = 1; s < S; ++s) {
+    const float4 v = *reinterpret_cast<const float4*>(part + s * sS + o);
+    a.x += v.x;
+    a.y += v.y;
+    a.z += v.z;
+    a.w += v.w;
+  }
+  if (bias) {
+    a.x += bias[n];
+    a.y += bias[n + 1];
+    a.z += bias[n + 2];
+    a.w += bias[n + 3];
+  }
+  if (relu) {
+    a.x = fmaxf(a.x, 0.f);
+    a.y = fmaxf(a.y, 0.f);
+    a.z = fmaxf(a.z, 0.f);
+    a.w = fmaxf(a.w, 0.f);
+  }
+  *reinterpret_cast<float4*>(y + o) = a;
+}
+}  // namespace
+}  // namespace d3a
+
+extern "C" int d3a_splitk_epilogue_f32(const float* part, int32_t S, int64_t sS, float* y,
+                                       const float* bias, int64_t M, int64_t N, int32_t relu,
+                                       void* stream) {
+  using namespace d3a;
+  D3A_CHECK_ARG(part && y && S >= 1 && M >= 0 && N >= 0, "d3a_splitk_epilogue_f32: bad args");
+  D3A_CHECK_ARG(N % 4 == 0 && sS % 4 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(y)) & 15) == 0,
+                "d3a_splitk_epilogue_f32: 16-byte aligned rows of N %% 4 == 0 floats");
+  const int64_t n = M * (N / 4);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, part, S, sS, y, bias, M, N, relu);
+  D3A_LAUNCH_CHECK("d3a_splitk_epilogue_f32");
+  return 0;
+}
+
 extern "C" int d3a_gemm_sbf16(const d3a_gemm_desc* d, int32_t terms, void* stream) {
   using namespace d3a;
   D3A_CHECK_ARG(d && d->A && d->B && d->C, "d3a_gemm_sbf16: null operand");

@@ -225,6 +225,26 @@ def gemm_sbf16(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor], y: t
     N.check(N.lib().d3a_gemm_sbf16(C.byref(d), terms, _stream()), "d3a_gemm_sbf16")
 
 
+def linear_fwd_splitk(x: int, ldx: int, W: int, b: Optional[int], y: int, R: int, n_in: int,
+                      n_out: int, relu: bool, part: torch.Tensor, splits: int) -> None:
+    """y = act(x @ W^T + b) for one long-K Linear (K5's encoder fc, 3,136 -> 512)
+    on the bf16 matrix cores with fp32-accurate split-bf16 operands (six
+    products): ``splits`` K slices into ``part`` [splits][R][n_out], then
+    d3a_splitk_epilogue_f32 adds them in order with the bias and ReLU."""
+    assert part.numel() >= splits * R * n_out and part.is_cuda
+    d = N.GemmDesc()
+    d.A, d.B, d.C = x, W, part.data_ptr()
+    d.M, d.N, d.K, d.batch = R, n_out, n_in, 1
+    d.sAb, d.sAm, d.sAk = 0, ldx, 1
+    d.sBb, d.sBk, d.sBn = 0, 1, n_in
+    d.sCb, d.sCm, d.sCn = 0, n_out, 1
+    d.splits, d.sCs = splits, R * n_out
+    d.alpha, d.relu, d.variant, d.batch2 = 1.0, 0, -1, 1
+    N.check(N.lib().d3a_gemm_sbf16(C.byref(d), 6, _stream()), "d3a_gemm_sbf16")
+    N.check(N.lib().d3a_splitk_epilogue_f32(part.data_ptr(), splits, R * n_out, y, b, R, n_out,
+                                            int(relu), _stream()), "d3a_splitk_epilogue_f32")
+
+
 def philox_fill(out: torch.Tensor, n_normal: int, n_uniform: int, lo: float, hi: float,
                 seed: int, ctr: torch.Tensor, ticket: torch.Tensor) -> None:
     _need_gpu(out, ctr, ticket)
@@ -311,11 +331,13 @@ def set_sbf16(terms: int) -> None:
 def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: int, C_: int,
                  R: int, n_in: int, n_out: int, mask: Optional[int] = None,
                  ldm: int = 0, smb: int = 0, agen: Optional[C.Structure] = None,
-                 wnext: Optional[C.Structure] = None) -> None:
+                 wnext: Optional[C.Structure] = None, sbf16: int = 0) -> None:
     """dx[c] = (dy[c] @ W[c]) * [mask[c] > 0]; with ``agen`` dy is generated
     from that single-output head (d3a_gemm_desc.agen) and not read; with
     ``wnext`` (a GemmWnext) dx is not written but the layer below's weight /
-    bias gradient partials per 128-row tile (d3a_gemm_desc.wnext)."""
+    bias gradient partials per 128-row tile (d3a_gemm_desc.wnext).  ``sbf16``
+    (3 / 6): this GEMM on d3a_gemm_sbf16 at any row count (else SBF16_TERMS
+    from SBF16_MIN_ROWS rows)."""
     if wnext is not None:
         if agen is not None and agen.dW:
             agen = type(agen).from_buffer_copy(agen)
@@ -333,7 +355,8 @@ def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: 
              sB=(n_out * n_in, n_in, 1), sC=(sdxb, ldx, 1), mask=mask, sM=(smb, ldm, 1),
              agen=agen)
         return
-    if SBF16_TERMS and R * C_ >= SBF16_MIN_ROWS and n_out % 4 == 0 and n_in % 4 == 0 \
+    terms = sbf16 or (SBF16_TERMS if R * C_ >= SBF16_MIN_ROWS else 0)
+    if terms and n_out % 4 == 0 and n_in % 4 == 0 \
             and ldy % 4 == 0 and dy % 16 == 0 and W % 16 == 0:
         d = N.GemmDesc()
         d.A, d.B, d.C, d.mask = dy, W, dx, mask
@@ -343,7 +366,7 @@ def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: 
         d.sCb, d.sCm, d.sCn = sdxb, ldx, 1
         d.sMb, d.sMm, d.sMn = smb, ldm, 1
         d.splits, d.alpha, d.variant, d.batch2 = 1, 1.0, -1, 1
-        N.check(N.lib().d3a_gemm_sbf16(C.byref(d), SBF16_TERMS, _stream()), "d3a_gemm_sbf16")
+        N.check(N.lib().d3a_gemm_sbf16(C.byref(d), terms, _stream()), "d3a_gemm_sbf16")
         return
     gemm(dy, W, dx, R, n_in, n_out, batch=C_, sA=(sdyb, ldy, 1), sB=(n_out * n_in, n_in, 1),
          sC=(sdxb, ldx, 1), mask=mask, sM=(smb, ldm, 1))
@@ -351,7 +374,8 @@ def linear_bwd_x(dy: int, ldy: int, sdyb: int, W: int, dx: int, ldx: int, sdxb: 
 
 def linear_bwd_w(dy: int, ldy: int, sdyb: int, x: int, ldx: int, sxb: int, dW: int, C_: int,
                  R: int, n_in: int, n_out: int, splits: int, db: Optional[int] = None,
-                 variant: int = -1, agen: Optional[C.Structure] = None) -> None:
+                 variant: int = -1, agen: Optional[C.Structure] = None,
+                 sbf16: int = 0) -> None:
     """dW[s][c] = sum_{r in split s} dy[c][r]^T x[c][r]  -> partials [splits][C][out][in];
     if ``db`` is given, also the bias-gradient partials db[s][c][out] = sum_r dy[c][r].
     With ``agen`` dy is generated from that single-output head, whose weight /
@@ -361,7 +385,8 @@ def linear_bwd_w(dy: int, ldy: int, sdyb: int, x: int, ldx: int, sxb: int, dW: i
              sC=(n_out * n_in, n_in, 1), splits=splits, sCs=C_ * n_out * n_in,
              rowsum=db, sR=(n_out, C_ * n_out), variant=variant, agen=agen)
         return
-    if SBF16_TERMS and SBF16_W and R * C_ >= SBF16_MIN_ROWS and n_out >= 128 and n_in >= 128 \
+    terms = sbf16 or (SBF16_TERMS if SBF16_W and R * C_ >= SBF16_MIN_ROWS else 0)
+    if terms and n_out >= 128 and n_in >= 128 \
             and n_out % 4 == 0 and n_in % 4 == 0 and ldy % 4 == 0 and ldx % 4 == 0 \
             and dy % 16 == 0 and x % 16 == 0:
         d = N.GemmDesc()
@@ -374,7 +399,7 @@ def linear_bwd_w(dy: int, ldy: int, sdyb: int, x: int, ldx: int, sxb: int, dW: i
         d.sCb, d.sCm, d.sCn = n_out * n_in, n_in, 1
         d.splits, d.sCs = splits, C_ * n_out * n_in
         d.alpha, d.variant, d.batch2 = 1.0, -1, 1
-        N.check(N.lib().d3a_gemm_sbf16(C.byref(d), SBF16_TERMS, _stream()), "d3a_gemm_sbf16")
+        N.check(N.lib().d3a_gemm_sbf16(C.byref(d), terms, _stream()), "d3a_gemm_sbf16")
         return
     gemm(dy, x, dW, n_out, n_in, R, batch=C_, sA=(sdyb, 1, ldy), sB=(sxb, ldx, 1),
          sC=(n_out * n_in, n_in, 1), splits=splits, sCs=C_ * n_out * n_in,

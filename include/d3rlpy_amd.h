@@ -120,6 +120,12 @@ int d3a_gemm_f32_pair(const d3a_gemm_desc* d1, const d3a_gemm_desc* d2, void* st
  * per product) or 6 (hi/mid/lo, ~fp32).  The throughput instantiation of the
  * ensemble-Q layer GEMMs; no split-K / rowsum / batch2. */
 int d3a_gemm_sbf16(const d3a_gemm_desc* desc, int32_t terms, void* stream);
+/* y[m][n] = act(sum_s part[s][m][n] + bias[n]) over the S split-K partials
+ * (split stride sS) of a d3a_gemm_sbf16 launch, added in split order (relu:
+ * max(., 0)); the bias / activation of nn.Linear + ReLU (encoders.py:157-160). */
+int d3a_splitk_epilogue_f32(const float* part, int32_t S, int64_t sS, float* y,
+                            const float* bias, int64_t M, int64_t N, int32_t relu,
+                            void* stream);
 
 /* out[b*sOb + r] = sum_j X[b*sXb + r*sXr + j] * w[b*swb + j] + bias[b*sbb]
  * (the 256->1 head of ContinuousMeanQFunction, mean_q_function.py:255-256) */
