@@ -17,6 +17,7 @@
 // One workgroup per batch row: lane 0 walks the n-step chain (at most
 // n_steps dependent loads), then the whole workgroup copies observation /
 // frame bytes with 16-byte accesses.
+#include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
 
@@ -49,7 +50,7 @@ __device__ __forceinline__ void zero_bytes(uint8_t* dst, int64_t n, int tid, int
   for (int64_t k = tid; k < n; k += nt) dst[k] = 0;
 }
 
-__global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
+__global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d, bool batched) {
   __shared__ RowMeta meta;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int64_t b = blockIdx.x;
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(256) void gather_kernel(d3a_gather_desc d) {
     const int64_t n16 = fb >> 4;
     const bool al = ((reinterpret_cast<uintptr_t>(d.frames) | reinterpret_cast<uintptr_t>(o) |
                       reinterpret_cast<uintptr_t>(on) | (uintptr_t)fb) & 15) == 0;
-    if (al && nf <= 4 && n16 <= 2 * nt) {
+    if (batched && al && nf <= 4 && n16 <= 2 * nt) {
       // every 16-byte piece of the 2 nf frames loaded before any is stored (a
       // copy loop's store would otherwise wait on its load, frame by frame)
       uint4 v[8][2];
@@ -277,8 +278,13 @@ extern "C" int d3a_gather_batch(const d3a_gather_desc* d, void* stream) {
     hipLaunchKernelGGL(gather_vec_kernel, dim3((unsigned)((d->B + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, *d);
   } else {
+    // all frame pieces loaded before any is stored, unless D3A_GATHER_BATCHED=0
+    static const bool batched = [] {
+      const char* e = getenv("D3A_GATHER_BATCHED");
+      return !(e && e[0] == '0');
+    }();
     hipLaunchKernelGGL(gather_kernel, dim3((unsigned)d->B), dim3(256), 0, (hipStream_t)stream,
-                       *d);
+                       *d, batched);
   }
   D3A_LAUNCH_CHECK("d3a_gather_batch");
   return 0;
