@@ -921,6 +921,11 @@ extern "C" int32_t d3a_conv_bwd_w_splits(const d3a_conv_desc* d) {
   if (d == nullptr) return -1;
   const int64_t M = (int64_t)d->B * d->OH * d->OW;
   const int64_t Kc = (int64_t)d->C * d->KH * d->KW;
+  if (d->x_u8 || !conv_bwd_x6()) {
+    // the fp32-MFMA kernel: >= 32 rows a split, at most 32 splits
+    const int64_t s = M / 32 < 32 ? M / 32 : 32;
+    return (int32_t)(s > 1 ? s : 1);
+  }
   const int64_t tiles = ((Kc + 63) / 64) * (d->CO / 32 > 0 ? d->CO / 32 : 1);
   int64_t s = (512 + tiles - 1) / tiles;
   const int64_t cap = M / 128 > 1 ? M / 128 : 1;  // >= 16 rows for each of 8 waves
@@ -937,8 +942,11 @@ extern "C" int d3a_conv_bwd_w(const d3a_conv_desc* d, void* stream) {
   D3A_CHECK_ARG(d->splits >= 1 && d->splits < 65536, "d3a_conv_bwd_w: bad splits");
   const int64_t Kc = (int64_t)d->C * d->KH * d->KW;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (conv_bwd_x6()) {
+  if (conv_bwd_x6() && !d->x_u8) {
     // split-bf16 weight gradient: 32 (co) x 64 (k) per wave, 8 waves a workgroup
+    // (fp32 input; the uint8 layer stays on the fp32-MFMA kernel: both are bound
+    // by the byte gathers there, measured 133 us at 128 splits either way, 119
+    // for the fp32 kernel at 32)
     constexpr int NK = 2;
     const dim3 grid((unsigned)((Kc + 32 * NK - 1) / (32 * NK)), (unsigned)(d->CO / 32), (unsigned)d->splits);
     if (d->x_u8) hipLaunchKernelGGL((conv_bwd_w_x6_kernel<NK, true>), grid, dim3(512), 0, st, *d);

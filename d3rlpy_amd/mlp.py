@@ -102,7 +102,10 @@ _XGEN = os.environ.get("D3A_XGEN", "1") == "1"
 _MASK_IMAGE = os.environ.get("D3A_MASK_IMAGE", "1") == "1"
 # the SAC / CQL actor head in the policy trunk backward's prologue
 # (d3a_q2_bwd_actor_head: one launch fewer per actor update)
-_HEAD_IN_TRUNK = os.environ.get("D3A_HEAD_IN_TRUNK", "1") == "1"
+# -- off by default: measured slower on K2 (the fused launch 32.9 us against
+# 8.6 + 10.6 for the pair; every quarter workgroup re-forms its rows' dz2 inside
+# the trunk's row pipeline), kept bitwise-tested for the record
+_HEAD_IN_TRUNK = os.environ.get("D3A_HEAD_IN_TRUNK", "0") == "1"
 
 
 def q2_shape(net: EnsembleMLP) -> bool:
