@@ -705,6 +705,7 @@ class _Workspace:
                 xd = _conv_desc(impl.geom, l, B, st, impl.conv_names)
                 xd.x_f32, xd.dy, xd.y = (self.enc.ys[l - 1].data_ptr(), self.dys[l].data_ptr(),
                                          self.dys[l - 1].data_ptr())
+                xd.wpack = self.enc.wpack[l].data_ptr()  # re-laid weight scratch
                 ops.call_desc("d3a_conv_bwd_x", xd)
             elif l > 0:
                 ops.linear_bwd_x(self.dys[l].data_ptr(), co, rows * co, st.ptr(Wn),

@@ -682,11 +682,32 @@ __global__ __launch_bounds__(512) void conv_bwd_w_x6_kernel(d3a_conv_desc d) {
 // (M = phase rows, N = c, K = (ih, iw, co), a missing position a zero
 // operand).  dy is read as float4 runs of 8 co (CO % 16 == 0); the weight is
 // staged per 32-k chunk in three bf16 parts, six products.
-template <int WN>
+// weight [CO][C][KH][KW] -> [KH][KW][CO][C] (d3a_conv_bwd_x's chunk order: a
+// 32-k chunk, one tap x 32 co x all c, is one contiguous run)
+__global__ __launch_bounds__(256) void conv_pack_tap_kernel(const float* __restrict__ w,
+                                                            float* __restrict__ wt, int CO, int C,
+                                                            int KH, int KW) {
+  const int64_t n = (int64_t)CO * C * KH * KW;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int kw = (int)(i % KW);
+  int64_t r = i / KW;
+  const int kh = (int)(r % KH);
+  r /= KH;
+  const int c = (int)(r % C);
+  const int co = (int)(r / C);
+  wt[(((int64_t)kh * KW + kw) * CO + co) * C + c] = w[i];
+}
+
+// F32: the products on v_mfma_f32_32x32x2_f32 instead (exact fp32 products,
+// fp32 accumulation: the column-matrix GEMM's arithmetic), the weight chunk
+// kept in fp32 in LDS -- the kernel is bound by its loads, not the matrix cores
+template <int WN, bool PACKED, bool F32 = false>
 __global__ __launch_bounds__(256) void conv_bwd_x_x6_kernel(d3a_conv_desc d) {
   using namespace x6;
-  constexpr int C = 32 * WN, BK = 32, LDB = BK + 8;
-  __shared__ __attribute__((aligned(16))) __bf16 Ws[2][3][C * LDB];
+  constexpr int C = 32 * WN, BK = 32, LDB = BK + 8, LDF = BK + 4;
+  __shared__ __attribute__((aligned(16))) __bf16 Ws[F32 ? 1 : 2][3][F32 ? 8 : C * LDB];
+  __shared__ __attribute__((aligned(16))) float Wf[F32 ? 2 : 1][F32 ? C * LDF : 4];
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
   const int li = lane & 31, lg = lane >> 5;
@@ -709,9 +730,20 @@ __global__ __launch_bounds__(256) void conv_bwd_x_x6_kernel(d3a_conv_desc d) {
     xi = r - yi * nxp;
   }
   const float* dyb = d.dy + bimg * d.OH * d.OW * CO;
-  // weight chunk: C x 32 values (c = e >> 5, kk = e & 31), WN x 4 per thread
+  // weight chunk: C x 32 values, WN x 4 per thread: packed, one contiguous run
+  // of [32 co][C] (co = e / C, c = e % C); else gathered from nn.Conv2d's
+  // layout (c = e >> 5, kk = e & 31)
   float wv[4 * WN];
   auto wload = [&](int k0) {
+    if constexpr (PACKED) {
+      const int tap = k0 / CO, co0 = k0 - tap * CO;
+      const int ih = tap / NTW, iw = tap - ih * NTW;
+      const int kh = py + S * ih, kw = px + S * iw;
+      const float* src = d.wpack + (((int64_t)kh * d.KW + kw) * CO + co0) * C;
+#pragma unroll
+      for (int j = 0; j < 4 * WN; ++j) wv[j] = k0 < Kc ? src[t + 256 * j] : 0.f;
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 4 * WN; ++j) {
       const int e = t + 256 * j, c = e >> 5, kk = e & 31;
@@ -729,12 +761,17 @@ __global__ __launch_bounds__(256) void conv_bwd_x_x6_kernel(d3a_conv_desc d) {
   auto wstore = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < 4 * WN; ++j) {
-      const int e = t + 256 * j, c = e >> 5, kk = e & 31;
-      __bf16 q0, q1, q2;
-      split1(wv[j], q0, q1, q2);
-      Ws[buf][0][c * LDB + kk] = q0;
-      Ws[buf][1][c * LDB + kk] = q1;
-      Ws[buf][2][c * LDB + kk] = q2;
+      const int e = t + 256 * j;
+      const int c = PACKED ? e % C : e >> 5, kk = PACKED ? e / C : e & 31;
+      if constexpr (F32) {
+        Wf[buf][c * LDF + kk] = wv[j];
+      } else {
+        __bf16 q0, q1, q2;
+        split1(wv[j], q0, q1, q2);
+        Ws[buf][0][c * LDB + kk] = q0;
+        Ws[buf][1][c * LDB + kk] = q1;
+        Ws[buf][2][c * LDB + kk] = q2;
+      }
     }
   };
   // the A operand of a chunk: per k step s, this lane's 8 k = 8 co of one tap
@@ -780,9 +817,23 @@ __global__ __launch_bounds__(256) void conv_bwd_x_x6_kernel(d3a_conv_desc d) {
     if (more) aload(k0 + BK);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 a[3];
       const float v[8] = {cf[s2][0].x, cf[s2][0].y, cf[s2][0].z, cf[s2][0].w,
                           cf[s2][1].x, cf[s2][1].y, cf[s2][1].z, cf[s2][1].w};
+      if constexpr (F32) {
+        // MFMA i covers k = 16 s2 + i (lane group 0) and 16 s2 + 8 + i (group 1)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          const float* wr = &Wf[cur][(32 * j + li) * LDF + 16 * s2 + 8 * lg];
+          const float4 w0 = *reinterpret_cast<const float4*>(wr);
+          const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
+          const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[i], wk[i], acc[j], 0, 0, 0);
+        }
+        continue;
+      }
+      bf16x8 a[3];
       split8(v, a);
 #pragma unroll
       for (int j = 0; j < WN; ++j) {
@@ -910,6 +961,15 @@ bool conv_bwd_x6() {
   }();
   return on;
 }
+// d3a_conv_bwd_x's products on fp32 MFMA (packed weights) unless
+// D3A_CONV_BWD_X_F32=0 (split-bf16 x6)
+bool conv_bwd_x_f32() {
+  static const bool on = [] {
+    const char* e = getenv("D3A_CONV_BWD_X_F32");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
 }  // namespace
 }  // namespace d3a
 
@@ -978,8 +1038,23 @@ extern "C" int d3a_conv_bwd_x(const d3a_conv_desc* d, void* stream) {
   D3A_CHECK_ARG(blocks < (1ll << 31), "d3a_conv_bwd_x: too many rows");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)blocks, (unsigned)(d->S * d->S)), block(256);
-  if (d->C == 32) hipLaunchKernelGGL((conv_bwd_x_x6_kernel<1>), grid, block, 0, st, *d);
-  else hipLaunchKernelGGL((conv_bwd_x_x6_kernel<2>), grid, block, 0, st, *d);
+  if (d->wpack && d->CO % 32 == 0) {
+    // the weight re-laid [KH][KW][CO][C] into the wpack scratch first: each
+    // chunk is then one coalesced run instead of 32 co x C scattered floats
+    const int64_t n = (int64_t)d->CO * d->C * d->KH * d->KW;
+    hipLaunchKernelGGL(conv_pack_tap_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       d->weight, d->wpack, d->CO, d->C, d->KH, d->KW);
+    if (conv_bwd_x_f32()) {
+      if (d->C == 32) hipLaunchKernelGGL((conv_bwd_x_x6_kernel<1, true, true>), grid, block, 0, st, *d);
+      else hipLaunchKernelGGL((conv_bwd_x_x6_kernel<2, true, true>), grid, block, 0, st, *d);
+    } else {
+      if (d->C == 32) hipLaunchKernelGGL((conv_bwd_x_x6_kernel<1, true>), grid, block, 0, st, *d);
+      else hipLaunchKernelGGL((conv_bwd_x_x6_kernel<2, true>), grid, block, 0, st, *d);
+    }
+  } else {
+    if (d->C == 32) hipLaunchKernelGGL((conv_bwd_x_x6_kernel<1, false>), grid, block, 0, st, *d);
+    else hipLaunchKernelGGL((conv_bwd_x_x6_kernel<2, false>), grid, block, 0, st, *d);
+  }
   D3A_LAUNCH_CHECK("d3a_conv_bwd_x");
   return 0;
 }

@@ -994,7 +994,9 @@ int32_t d3a_conv_bwd_w_splits(const d3a_conv_desc* d);
  * [B][H][W][C]) = [x_f32 > 0 when relu] * sum over the output positions whose
  * window covers the pixel of dy W -- one implicit GEMM per stride phase
  * (replaces the column-matrix GEMM + d3a_col2im pair).  Needs fp32 x
- * geometry with C = 32 or 64, CO % 16 == 0, dy 16-byte aligned. */
+ * geometry with C = 32 or 64, CO % 16 == 0, dy 16-byte aligned.  With wpack
+ * (CO * C * KH * KW floats of scratch) and CO % 32 == 0 the weight is first
+ * re-laid [KH][KW][CO][C] there so every chunk load is coalesced. */
 int d3a_conv_bwd_x(const d3a_conv_desc* d, void* stream);
 
 /* Per-sample [P][C] (NHWC) <-> [C][P] (NCHW) transpose, optional [mask > 0]

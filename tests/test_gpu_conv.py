@@ -157,7 +157,8 @@ BWD_X_CASES = [(5, 32, 20, 20, 64, 4, 2), (7, 64, 9, 9, 64, 3, 1), (2, 32, 11, 1
 
 @pytest.mark.parametrize("B,C,H,W,CO,K,S", BWD_X_CASES)
 @pytest.mark.parametrize("relu", [1, 0])
-def test_conv_bwd_x_matches_autograd(dev, B, C, H, W, CO, K, S, relu):
+@pytest.mark.parametrize("packed", [True, False])
+def test_conv_bwd_x_matches_autograd(dev, B, C, H, W, CO, K, S, relu, packed):
     """d3a_conv_bwd_x against autograd's input gradient of conv2d (fp64),
     times [x > 0] (the ReLU of the layer that produced x) when relu."""
     from d3rlpy_amd import _native as N, ops
@@ -176,6 +177,9 @@ def test_conv_bwd_x_matches_autograd(dev, B, C, H, W, CO, K, S, relu):
     dx = torch.full((B * H * W, C), float("nan"), device=dev)
     d.x_f32, d.weight, d.dy, d.y, d.relu = xd.data_ptr(), Wd.data_ptr(), dyd.data_ptr(), \
         dx.data_ptr(), relu
+    wpack = torch.full((CO * C * K * K,), float("nan"), device=dev)
+    if packed:  # the re-laid weight path (CO % 32 == 0; else the gather path)
+        d.wpack = wpack.data_ptr()
     ops.call_desc("d3a_conv_bwd_x", d)
     torch.cuda.synchronize()
     assert torch.isfinite(dx).all()

@@ -70,8 +70,11 @@ for (C, H, W, CO, K, S, _) in LAYERS[1:]:
     dy = torch.randn(B * OH * OW, CO, generator=g).to(dev)
     Wt = (torch.randn(CO, C, K, K, generator=g) * 0.05).to(dev)
     dx = torch.empty(B * H * W, C, device=dev)
+    wpack = torch.empty(CO * C * K * K, device=dev)
     d.x_f32, d.weight, d.dy, d.y, d.relu = x.data_ptr(), Wt.data_ptr(), dy.data_ptr(), \
         dx.data_ptr(), 1
+    if os.environ.get("PACKED", "1") == "1":
+        d.wpack = wpack.data_ptr()
     for _ in range(100):
         ops.call_desc("d3a_conv_bwd_x", d)
     torch.cuda.synchronize()
