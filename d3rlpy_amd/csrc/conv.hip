@@ -961,12 +961,13 @@ bool conv_bwd_x6() {
   }();
   return on;
 }
-// d3a_conv_bwd_x's products on fp32 MFMA (packed weights) unless
-// D3A_CONV_BWD_X_F32=0 (split-bf16 x6)
+// d3a_conv_bwd_x's products on fp32 MFMA (packed weights) when
+// D3A_CONV_BWD_X_F32=1; split-bf16 x6 by default (measured on K5: 64 / 59 us
+// against 69 / 71, both within the B = 512 arbiter's bars)
 bool conv_bwd_x_f32() {
   static const bool on = [] {
     const char* e = getenv("D3A_CONV_BWD_X_F32");
-    return !(e && atoi(e) == 0);
+    return e && atoi(e) == 1;
   }();
   return on;
 }
