@@ -221,7 +221,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(d3a_conv_desc d, const fl
 // sum fl(x / 255) W: the same value up to fp32 rounding, and bit for bit the
 // reference's x / 255 where one tap carries the output (tests/test_gpu_conv.py:
 // the one-hot pixel-scale test and the 2e-5 bar against fp64).
-template <int WN, bool U8, bool ALIGNED = false>
+// PACKED (fp32 input): the weight was re-laid in the walk order into d.wpack
+// (conv_pack_kernel), so a chunk row is 32 consecutive floats
+template <int WN, bool U8, bool ALIGNED = false, bool PACKED = false>
 __global__ __launch_bounds__(256) void conv_fwd_x6_kernel(d3a_conv_desc d) {
   using namespace x6;
   constexpr int CO = 32 * WN, BK = 32, LDB = BK + 8;
@@ -257,11 +259,11 @@ __global__ __launch_bounds__(256) void conv_fwd_x6_kernel(d3a_conv_desc d) {
       float v = 0.f;
       if (k < Kc) {
         int src = k;  // (c, kh, kw) order for uint8 input = the native layout
-        if (!U8) {
+        if (!U8 && !PACKED) {
           const int c = k % d.C, tt = k / d.C, kw = tt % d.KW, kh = tt / d.KW;
           src = (c * d.KH + kh) * d.KW + kw;
         }
-        v = d.weight[(int64_t)co * Kc + src];
+        v = (PACKED ? d.wpack : d.weight)[(int64_t)co * Kc + src];
       }
       wv[j] = v;
     }
@@ -890,6 +892,20 @@ int check_geometry(const d3a_conv_desc* d, const char* name) {
 }  // namespace
 }  // namespace d3a
 
+namespace d3a {
+namespace {
+// the split-bf16 forward of an fp32-input layer reads a walk-ordered copy of
+// the weight (one conv_pack launch) when D3A_CONV_FWD_PACK=1
+bool conv_fwd_pack() {
+  static const bool on = [] {
+    const char* e = getenv("D3A_CONV_FWD_PACK");
+    return e && atoi(e) == 1;
+  }();
+  return on;
+}
+}  // namespace
+}  // namespace d3a
+
 extern "C" int d3a_conv_fwd(const d3a_conv_desc* d, void* stream) {
   using namespace d3a;
   if (check_geometry(d, "d3a_conv_fwd")) return -1;
@@ -918,8 +934,17 @@ extern "C" int d3a_conv_fwd(const d3a_conv_desc* d, void* stream) {
     } else {
       D3A_CHECK_ARG((reinterpret_cast<uintptr_t>(d->x_f32) & 15) == 0,
                     "d3a_conv_fwd: fp32 input must be 16-byte aligned");
-      if (d->CO == 32) hipLaunchKernelGGL((conv_fwd_x6_kernel<1, false>), grid, block, 0, st, *d);
-      else hipLaunchKernelGGL((conv_fwd_x6_kernel<2, false>), grid, block, 0, st, *d);
+      if (conv_fwd_pack()) {
+        // the weight re-laid in the walk order first: coalesced chunk loads
+        const int64_t n = (int64_t)d->CO * d->C * d->KH * d->KW;
+        hipLaunchKernelGGL(conv_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                           d->weight, d->wpack, d->C, d->KH, d->KW, n);
+        if (d->CO == 32) hipLaunchKernelGGL((conv_fwd_x6_kernel<1, false, false, true>), grid, block, 0, st, *d);
+        else hipLaunchKernelGGL((conv_fwd_x6_kernel<2, false, false, true>), grid, block, 0, st, *d);
+      } else {
+        if (d->CO == 32) hipLaunchKernelGGL((conv_fwd_x6_kernel<1, false>), grid, block, 0, st, *d);
+        else hipLaunchKernelGGL((conv_fwd_x6_kernel<2, false>), grid, block, 0, st, *d);
+      }
     }
     D3A_LAUNCH_CHECK("d3a_conv_fwd");
     return 0;
@@ -961,13 +986,15 @@ bool conv_bwd_x6() {
   }();
   return on;
 }
-// d3a_conv_bwd_x's products on fp32 MFMA (packed weights) when
-// D3A_CONV_BWD_X_F32=1; split-bf16 x6 by default (measured on K5: 64 / 59 us
-// against 69 / 71, both within the B = 512 arbiter's bars)
+// d3a_conv_bwd_x's products on fp32 MFMA (packed weights) unless
+// D3A_CONV_BWD_X_F32=0 (split-bf16: 64 / 59 us against 69 / 71 on K5's layers,
+// but with the split-bf16 weight gradients of the same layers the B = 512
+// arbiter measures the first conv's bias gradient at 1.03e-5 of fp64 -- over
+// its 1e-5 bar -- where the fp32-MFMA input gradient keeps it at 4.3e-6)
 bool conv_bwd_x_f32() {
   static const bool on = [] {
     const char* e = getenv("D3A_CONV_BWD_X_F32");
-    return e && atoi(e) == 1;
+    return !(e && atoi(e) == 0);
   }();
   return on;
 }
