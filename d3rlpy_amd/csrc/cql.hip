@@ -598,9 +598,42 @@ __global__ __launch_bounds__(256) void sac_actor_head_kernel(d3a_sac_actor_head_
         const float* sc = &s_dq[0][c * 16 + j];
         da += ((sc[0] + sc[64]) + sc[128]) + sc[192];
       }
-    } else if (d.dq_min) {
+    } else if (d.dq_min && C <= 4 && np <= 4) {
       // backward of min over the members: the first member of least q
-      // (head1_min's rule) carries dq_scale, the others nothing
+      // (head1_min's rule) carries dq_scale, the others nothing.  Every
+      // member's dQ/da parts are loaded with the q parts (one round trip,
+      // not q then the chosen member's parts), then the chosen one is summed
+      float jpart[4][4], qpart[4][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const bool on = c < C && p < np;
+          jpart[c][p] = on ? d.dq_da[p * d.sda_part + c * d.sda_c + b * d.ld_da + d.da_off + j] : 0.f;
+          qpart[c][p] = on ? d.q[p * d.sq_part + c * d.sqc + b] : 0.f;
+        }
+      auto qsum = [&](int c) {
+        float v = qpart[c][0];
+        for (int p = 1; p < np; ++p) v += qpart[c][p];
+        return v;
+      };
+      int arg = 0;
+      float mn = qsum(0);
+#pragma unroll
+      for (int c = 1; c < 4; ++c) {
+        if (c >= C) break;
+        const float v = qsum(c);
+        if (v < mn) { mn = v; arg = c; }
+      }
+      float jv = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c != arg) continue;
+        jv = jpart[c][0];
+        for (int p = 1; p < np; ++p) jv += jpart[c][p];
+      }
+      da = d.dq_scale * jv;
+    } else if (d.dq_min) {
       int arg = 0;
       float mn = qv(0, b);
       for (int c = 1; c < C; ++c) {
