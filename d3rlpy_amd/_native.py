@@ -139,6 +139,7 @@ class CqlLossDesc(C.Structure):
         ("update_temp", C.c_int32), ("update_alpha", C.c_int32), ("update_critic", C.c_int32),
         ("dp_phase", C.c_int32), ("scalar_grads", vp), ("grad_scale", C.c_float),
         ("logp_targ", vp), ("soft_target", C.c_int32), ("conservative", C.c_int32),
+        ("ticket", vp),
     ]
 
 

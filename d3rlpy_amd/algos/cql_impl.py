@@ -543,6 +543,11 @@ class _Workspace:
         l.dq, l.metrics, l.scalars = (self.dq.data_ptr(), self.metrics.data_ptr(),
                                       self.scalars.data_ptr())
         l.lse = self.lse.data_ptr()
+        # the logsumexp and loss stages as one launch (a zeroed device ticket the
+        # last stage-A workgroup counts on and resets); D3A_LOSS_FUSED=0: two
+        self.loss_ticket = torch.zeros(1, dtype=torch.int32, device=self.lse.device)
+        if os.environ.get("D3A_LOSS_FUSED", "1") == "1":
+            l.ticket = self.loss_ticket.data_ptr()
         l.B, l.A, l.N, l.C, l.R = self.B, self.A, self.N, self.C, self.R
         l.gamma = impl._gamma
         tf, af = impl._temp_optim_factory, impl._alpha_optim_factory

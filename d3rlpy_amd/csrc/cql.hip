@@ -262,10 +262,8 @@ __device__ __forceinline__ float is_value(const d3a_cql_loss_desc& d, int64_t c,
 // amax shift, |max| == inf -> 0), and for the critic set the softmax
 // weights exp(v_j - lse) = exp(v_j - max) / sum_j exp(v_j - max) into dq
 // (scaled by the alpha-dependent factor in stage B).
-__global__ __launch_bounds__(256) void cql_lse_kernel(d3a_cql_loss_desc d) {
-  const int lane = threadIdx.x & 63;
+__device__ __forceinline__ void cql_lse_wave(const d3a_cql_loss_desc& d, int64_t p, int lane) {
   const int64_t B = d.B, C = d.C, N = d.N, NB = N * B, M = 3 * N;
-  const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (p >= 2 * C * B) return;
   const int64_t s = p / (C * B), c = (p / B) % C, b = p % B;
   if ((s == 0 && !d.update_alpha) || (s == 1 && !d.update_critic)) return;
@@ -292,6 +290,10 @@ __global__ __launch_bounds__(256) void cql_lse_kernel(d3a_cql_loss_desc d) {
   }
 }
 
+__global__ __launch_bounds__(256) void cql_lse_kernel(d3a_cql_loss_desc d) {
+  cql_lse_wave(d, (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+}
+
 // Stage B (one workgroup): temperature and alpha Adam steps, TD loss, and
 // final dL/dQ (scales stage A's softmax weights by the new clipped alpha).
 // Latency-bound (one CU): every input is loaded up front — the per-row values
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(256) void cql_lse_kernel(d3a_cql_loss_desc d) {
 constexpr int LOSS_MP = 8;
 
 template <bool REG>
-__global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
+__device__ __forceinline__ void cql_loss_stage(const d3a_cql_loss_desc& d) {
   __shared__ float scratch[48];  // block_sum_k<3> over 16 waves
   __shared__ float sh[4];
   __shared__ double s_bc[4];
@@ -500,6 +502,30 @@ __global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
     d.metrics[6] = td;
     d.metrics[7] = cons;
   }
+}
+
+template <bool REG>
+__global__ __launch_bounds__(1024) void cql_loss_kernel(d3a_cql_loss_desc d) {
+  cql_loss_stage<REG>(d);
+}
+
+// Stages A and B in one launch (d.ticket set): 1,024-thread workgroups run
+// stage A one wave per (s, c, b); each then counts itself done on the ticket
+// (after a device-scope fence of its lse / softmax-weight writes) and the last
+// one runs stage B -- the same 1,024-thread block as cql_loss_kernel, so the
+// same sums in the same order -- and resets the ticket for the next launch
+template <bool REG>
+__global__ __launch_bounds__(1024) void cql_lse_loss_kernel(d3a_cql_loss_desc d) {
+  __shared__ int s_last;
+  cql_lse_wave(d, (int64_t)blockIdx.x * 16 + (threadIdx.x >> 6), threadIdx.x & 63);
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(d.ticket, 1u) == gridDim.x - 1 ? 1 : 0;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();  // every other workgroup's stage-A writes are visible
+  if (threadIdx.x == 0) *d.ticket = 0u;
+  cql_loss_stage<REG>(d);
 }
 
 __global__ __launch_bounds__(256) void sac_actor_dq_kernel(const float* q, int64_t sqc, int C,
@@ -722,7 +748,18 @@ extern "C" int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream) {
                 "d3a_cql_loss: update_alpha needs the conservative term");
   D3A_CHECK_ARG(!d->conservative || d->N >= 1, "d3a_cql_loss: the conservative term needs N >= 1");
   // phase 2 reuses the logsumexp / softmax weights phase 1 wrote
-  if (d->conservative && (d->update_alpha || d->update_critic) && d->dp_phase != 2) {
+  const bool stage_a = d->conservative && (d->update_alpha || d->update_critic) && d->dp_phase != 2;
+  if (stage_a && d->ticket) {
+    const int64_t waves = 2LL * d->C * d->B;
+    const dim3 g((unsigned)((waves + 15) / 16));
+    if ((int64_t)d->C * d->B <= (int64_t)LOSS_MP * 1024)
+      hipLaunchKernelGGL(cql_lse_loss_kernel<true>, g, dim3(1024), 0, (hipStream_t)stream, *d);
+    else
+      hipLaunchKernelGGL(cql_lse_loss_kernel<false>, g, dim3(1024), 0, (hipStream_t)stream, *d);
+    D3A_LAUNCH_CHECK("d3a_cql_loss");
+    return 0;
+  }
+  if (stage_a) {
     const int64_t waves = 2LL * d->C * d->B;
     hipLaunchKernelGGL(cql_lse_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, *d);

@@ -646,6 +646,10 @@ typedef struct d3a_cql_loss_desc {
    * logsumexp stage, no alpha) */
   const float* logp_targ;
   int32_t soft_target, conservative;
+  /* ticket (optional, a zero-initialised device counter): the logsumexp stage
+   * and the loss stage in one launch -- the last workgroup of the first runs
+   * the second (same sums, same order) and resets the counter */
+  uint32_t* ticket;
 } d3a_cql_loss_desc;
 int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream);
 

@@ -439,3 +439,34 @@ def test_actor_head_in_trunk_is_bitwise_the_two_launches(case, monkeypatch):
                         torch.utils._pytree.tree_leaves(s1[k])):
             if isinstance(a, torch.Tensor):
                 assert torch.equal(a, b), k
+
+
+@pytest.mark.parametrize("case", ["hopper", "wide_ensemble"])
+def test_fused_lse_loss_is_bitwise_the_two_launches(case, monkeypatch):
+    """d3a_cql_loss with a ticket (the logsumexp stage's last workgroup runs
+    the loss stage: one launch) against the two-launch form: bitwise equal
+    metrics, parameters and optimiser state over three updates (the same
+    per-wave stage-A work and the same 1,024-thread stage B)."""
+    cfg = CASES[case]
+    D, A, H, N, B = cfg["D"], cfg["A"], cfg["hidden"], cfg["N"], cfg["B"]
+    C = cfg.get("C", 2)
+    orc = make_oracle(D, A, H, N, C=C, seed=9)
+    sd0 = copy.deepcopy(oracle_state(orc))
+    rs = np.random.RandomState(8)
+    gen = torch.Generator().manual_seed(7)
+    batches = [(make_batch(rs, B, D, A), CQLNoise.draw(gen, B, A, N)) for _ in range(3)]
+    runs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("D3A_LOSS_FUSED", fused)
+        impl = make_impl(D, A, H, N, C=C)
+        impl.set_state_dict(copy.deepcopy(sd0))
+        ms = [impl.update_step(HostBatch(*arrs), noise=noise_dict(nz)) for arrs, nz in batches]
+        torch.cuda.synchronize()
+        runs.append((ms, impl.get_state_dict()))
+    (m0, s0), (m1, s1) = runs
+    for a, b in zip(m0, m1):
+        for k in a:
+            assert a[k] == b[k] or (a[k] != a[k] and b[k] != b[k]), (k, a[k], b[k])
+    for key in ("_q_func", "_policy"):
+        for (n, a), (_, b) in zip(sorted(s0[key].items()), sorted(s1[key].items())):
+            assert torch.equal(a, b), (key, n)
