@@ -389,6 +389,7 @@ class ConvDesc(C.Structure):
         ("B", C.c_int32), ("C", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
         ("KH", C.c_int32), ("KW", C.c_int32), ("S", C.c_int32), ("OH", C.c_int32),
         ("OW", C.c_int32), ("CO", C.c_int32), ("relu", C.c_int32), ("splits", C.c_int32),
+        ("wpack_ready", C.c_int32),
     ]
 
 
@@ -519,6 +520,7 @@ _SIGNATURES = {
     "d3a_conv_bwd_w": (C.c_int, [C.POINTER(ConvDesc), vp]),
     "d3a_conv_bwd_w_splits": (C.c_int32, [C.POINTER(ConvDesc)]),
     "d3a_conv_bwd_x": (C.c_int, [C.POINTER(ConvDesc), vp]),
+    "d3a_conv_pack_weights": (C.c_int, [C.POINTER(ConvDesc), C.POINTER(C.c_int32), C.c_int32, vp]),
     "d3a_iqn_prior": (C.c_int, [C.POINTER(IqnPriorDesc), vp]),
     "d3a_iqn_head_fwd": (C.c_int, [C.POINTER(IqnHeadDesc), vp]),
     "d3a_iqn_loss": (C.c_int, [C.POINTER(IqnLossDesc), vp]),

@@ -334,7 +334,9 @@ class _EncoderPass:
         self.fc_part = (z(self.fc_splits, n, impl._F) if _FC_SPLITK and impl.flat % 4 == 0
                         and impl._F % 4 == 0 else None)
 
-    def forward(self, x_u8: int, store: ParamStore) -> None:
+    def forward(self, x_u8: int, store: ParamStore, prepacked: bool = False) -> None:
+        """``prepacked``: the fp32 layers' weight copies are already in
+        self.wpack (d3a_conv_pack_weights earlier in the step)."""
         impl = self.impl
         n = self.n
         for l in range(len(impl.geom)):
@@ -344,6 +346,7 @@ class _EncoderPass:
             else:
                 d.x_f32 = self.ys[l - 1].data_ptr()
                 d.wpack = self.wpack[l].data_ptr()
+                d.wpack_ready = int(prepacked)
             d.y = self.ys[l].data_ptr()
             ops.call_desc("d3a_conv_fwd", d)
         ci, h, w, co, k, s, oh, ow = impl.geom[-1]
@@ -373,6 +376,11 @@ _FC_SPLITK = os.environ.get("D3A_FC_SPLITK", "1") == "1"
 # the conv input gradient as one implicit GEMM (d3a_conv_bwd_x) rather than
 # the column-matrix GEMM + col2im pair; D3A_CONV_BWD_X=0 for the pair
 _CONV_BWD_X = os.environ.get("D3A_CONV_BWD_X", "1") == "1"
+
+
+# the step's conv weight copies in one d3a_conv_pack_weights launch (else each
+# conv entry packs its own); D3A_CONV_PREPACK=0 for the per-entry packs
+_CONV_PREPACK = os.environ.get("D3A_CONV_PREPACK", "1") == "1"
 
 
 def _conv_bwd_x(ci: int, co: int) -> bool:
@@ -477,6 +485,9 @@ class _Workspace:
         self.dys = [z(B * oh * ow, co) for (ci, h, w, co, k, s, oh, ow) in impl.geom]
         self.dcols = [None] + [None if _conv_bwd_x(ci, co) else z(B * oh * ow, ci * k * k)
                                for (ci, h, w, co, k, s, oh, ow) in impl.geom[1:]]
+        # the input gradients' tap-major weight copies (d3a_conv_bwd_x)
+        self.wtap = [None] + [z(co * ci * k * k) if _conv_bwd_x(ci, co) and co % 32 == 0 else None
+                              for (ci, h, w, co, k, s, oh, ow) in impl.geom[1:]]
         # gradients: split-K partials for the GEMM weight gradients, per-row
         # partials (B) for the IQN fc
         self.grads = GradSpace(dev)
@@ -639,9 +650,25 @@ class _Workspace:
         if not self._external_taus and not self.mean:
             ops.philox_fill(self.taus, 0, self.taus.numel(), 0.0, 1.0, self.seed, self.rng_ctr,
                             self.rng_ticket)
+        # every fp32 conv layer's weight copies for this step in one launch:
+        # the online and target forwards' walk order, the input gradients'
+        # tap-major order (the weights do not change before the step's Adam)
+        pre = _CONV_PREPACK and len(impl.geom) > 1
+        if pre:
+            descs, lays = [], []
+            for l in range(1, len(impl.geom)):
+                for store_, buf, lay in ((st, self.enc.wpack[l], 0), (tg, self.enc_t.wpack[l], 0),
+                                         (st, self.wtap[l], 1)):
+                    if buf is None:
+                        continue
+                    d = _conv_desc(impl.geom, l, B, store_, impl.conv_names)
+                    d.wpack = buf.data_ptr()
+                    descs.append(d)
+                    lays.append(lay)
+            ops.conv_pack_weights(descs, lays)
         # encoders
-        self.enc.forward(self.obs2.data_ptr(), st)
-        self.enc_t.forward(self.obs2.data_ptr() + self.obs2[0].numel() * B, tg)
+        self.enc.forward(self.obs2.data_ptr(), st, prepacked=pre)
+        self.enc_t.forward(self.obs2.data_ptr() + self.obs2[0].numel() * B, tg, prepacked=pre)
         h_obs = self.enc.h.data_ptr()
         h_next = h_obs + 4 * B * F
         g = self.grads
@@ -705,7 +732,9 @@ class _Workspace:
                 xd = _conv_desc(impl.geom, l, B, st, impl.conv_names)
                 xd.x_f32, xd.dy, xd.y = (self.enc.ys[l - 1].data_ptr(), self.dys[l].data_ptr(),
                                          self.dys[l - 1].data_ptr())
-                xd.wpack = self.enc.wpack[l].data_ptr()  # re-laid weight scratch
+                if self.wtap[l] is not None:
+                    xd.wpack = self.wtap[l].data_ptr()  # tap-major weight copy
+                    xd.wpack_ready = int(pre)
                 ops.call_desc("d3a_conv_bwd_x", xd)
             elif l > 0:
                 ops.linear_bwd_x(self.dys[l].data_ptr(), co, rows * co, st.ptr(Wn),

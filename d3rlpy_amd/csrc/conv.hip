@@ -704,6 +704,33 @@ __global__ __launch_bounds__(256) void conv_pack_tap_kernel(const float* __restr
 // F32: the products on v_mfma_f32_32x32x2_f32 instead (exact fp32 products,
 // fp32 accumulation: the column-matrix GEMM's arithmetic), the weight chunk
 // kept in fp32 in LDS -- the kernel is bound by its loads, not the matrix cores
+// several layers' weight copies in one launch (d3a_conv_pack_weights)
+struct PackJobs {
+  const float* w[8];
+  float* dst[8];
+  int CO[8], C[8], KH[8], KW[8], layout[8];
+  int64_t end[8];  // running element count through job i
+  int n;
+};
+
+__global__ __launch_bounds__(256) void conv_pack_multi_kernel(PackJobs J) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int j = 0;
+  while (j < J.n && g >= J.end[j]) ++j;
+  if (j >= J.n) return;
+  const int64_t i = g - (j > 0 ? J.end[j - 1] : 0);  // source index in [CO][C][KH][KW]
+  const int KW = J.KW[j], KH = J.KH[j], C = J.C[j], CO = J.CO[j];
+  const int kw = (int)(i % KW);
+  int64_t r = i / KW;
+  const int kh = (int)(r % KH);
+  r /= KH;
+  const int c = (int)(r % C);
+  const int co = (int)(r / C);
+  const int64_t o = J.layout[j] == 0 ? (((int64_t)co * KH + kh) * KW + kw) * C + c
+                                     : (((int64_t)kh * KW + kw) * CO + co) * C + c;
+  J.dst[j][o] = J.w[j][i];
+}
+
 template <int WN, bool PACKED, bool F32 = false>
 __global__ __launch_bounds__(256) void conv_bwd_x_x6_kernel(d3a_conv_desc d) {
   using namespace x6;
@@ -938,8 +965,9 @@ extern "C" int d3a_conv_fwd(const d3a_conv_desc* d, void* stream) {
       if (conv_fwd_pack()) {
         // the weight re-laid in the walk order first: coalesced chunk loads
         const int64_t n = (int64_t)d->CO * d->C * d->KH * d->KW;
-        hipLaunchKernelGGL(conv_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                           d->weight, d->wpack, d->C, d->KH, d->KW, n);
+        if (!d->wpack_ready)
+          hipLaunchKernelGGL(conv_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                             d->weight, d->wpack, d->C, d->KH, d->KW, n);
         if (d->CO == 32) hipLaunchKernelGGL((conv_fwd_x6_kernel<1, false, false, true>), grid, block, 0, st, *d);
         else hipLaunchKernelGGL((conv_fwd_x6_kernel<2, false, false, true>), grid, block, 0, st, *d);
       } else {
@@ -1068,11 +1096,13 @@ extern "C" int d3a_conv_bwd_x(const d3a_conv_desc* d, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)blocks, (unsigned)(d->S * d->S)), block(256);
   if (d->wpack && d->CO % 32 == 0) {
-    // the weight re-laid [KH][KW][CO][C] into the wpack scratch first: each
-    // chunk is then one coalesced run instead of 32 co x C scattered floats
+    // the weight re-laid [KH][KW][CO][C] into the wpack scratch first (unless
+    // the caller did: wpack_ready): each chunk is then one coalesced run
+    // instead of 32 co x C scattered floats
     const int64_t n = (int64_t)d->CO * d->C * d->KH * d->KW;
-    hipLaunchKernelGGL(conv_pack_tap_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                       d->weight, d->wpack, d->CO, d->C, d->KH, d->KW);
+    if (!d->wpack_ready)
+      hipLaunchKernelGGL(conv_pack_tap_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                         d->weight, d->wpack, d->CO, d->C, d->KH, d->KW);
     if (conv_bwd_x_f32()) {
       if (d->C == 32) hipLaunchKernelGGL((conv_bwd_x_x6_kernel<1, true, true>), grid, block, 0, st, *d);
       else hipLaunchKernelGGL((conv_bwd_x_x6_kernel<2, true, true>), grid, block, 0, st, *d);
@@ -1085,5 +1115,34 @@ extern "C" int d3a_conv_bwd_x(const d3a_conv_desc* d, void* stream) {
     else hipLaunchKernelGGL((conv_bwd_x_x6_kernel<2, false>), grid, block, 0, st, *d);
   }
   D3A_LAUNCH_CHECK("d3a_conv_bwd_x");
+  return 0;
+}
+
+extern "C" int d3a_conv_pack_weights(const d3a_conv_desc* descs, const int32_t* layouts, int32_t n,
+                                     void* stream) {
+  using namespace d3a;
+  D3A_CHECK_ARG(descs && layouts && n >= 1 && n <= 8, "d3a_conv_pack_weights: 1..8 descriptors");
+  PackJobs J{};
+  int64_t tot = 0;
+  for (int i = 0; i < n; ++i) {
+    const d3a_conv_desc& d = descs[i];
+    D3A_CHECK_ARG(d.weight && d.wpack && d.CO >= 1 && d.C >= 1 && d.KH >= 1 && d.KW >= 1,
+                  "d3a_conv_pack_weights: null weight / wpack or bad geometry");
+    D3A_CHECK_ARG(layouts[i] == 0 || layouts[i] == 1, "d3a_conv_pack_weights: layout must be 0 or 1");
+    J.w[i] = d.weight;
+    J.dst[i] = d.wpack;
+    J.CO[i] = d.CO;
+    J.C[i] = d.C;
+    J.KH[i] = d.KH;
+    J.KW[i] = d.KW;
+    J.layout[i] = layouts[i];
+    tot += (int64_t)d.CO * d.C * d.KH * d.KW;
+    J.end[i] = tot;
+  }
+  J.n = n;
+  D3A_CHECK_ARG(tot < (1ll << 31), "d3a_conv_pack_weights: too many elements");
+  hipLaunchKernelGGL(conv_pack_multi_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, J);
+  D3A_LAUNCH_CHECK("d3a_conv_pack_weights");
   return 0;
 }

@@ -245,6 +245,15 @@ def linear_fwd_splitk(x: int, ldx: int, W: int, b: Optional[int], y: int, R: int
                                             int(relu), _stream()), "d3a_splitk_epilogue_f32")
 
 
+def conv_pack_weights(descs, layouts) -> None:
+    """d3a_conv_pack_weights over up to 8 ConvDescs (weight -> wpack in layout
+    0: the forward's walk order, 1: the input gradient's tap-major order)."""
+    n = len(descs)
+    arr = (N.ConvDesc * n)(*descs)
+    lays = (C.c_int32 * n)(*layouts)
+    N.check(N.lib().d3a_conv_pack_weights(arr, lays, n, _stream()), "d3a_conv_pack_weights")
+
+
 def philox_fill(out: torch.Tensor, n_normal: int, n_uniform: int, lo: float, hi: float,
                 seed: int, ctr: torch.Tensor, ticket: torch.Tensor) -> None:
     _need_gpu(out, ctr, ticket)

@@ -987,6 +987,9 @@ typedef struct d3a_conv_desc {
   const float* dy; float* dW; float* db;
   int32_t B, C, H, W, KH, KW, S, OH, OW, CO;
   int32_t relu, splits;
+  /* wpack_ready: wpack already holds the layout the entry reads (written by
+   * d3a_conv_pack_weights earlier on the stream); 0: the entry packs it */
+  int32_t wpack_ready;
 } d3a_conv_desc;
 int d3a_conv_fwd(const d3a_conv_desc* d, void* stream);
 int d3a_conv_bwd_w(const d3a_conv_desc* d, void* stream);
@@ -1002,6 +1005,11 @@ int32_t d3a_conv_bwd_w_splits(const d3a_conv_desc* d);
  * (CO * C * KH * KW floats of scratch) and CO % 32 == 0 the weight is first
  * re-laid [KH][KW][CO][C] there so every chunk load is coalesced. */
 int d3a_conv_bwd_x(const d3a_conv_desc* d, void* stream);
+/* The weight copies of up to 8 fp32-input layers in one launch: descs[i].weight
+ * re-laid into descs[i].wpack in the order layouts[i] names -- 0: d3a_conv_fwd's
+ * walk order [CO][KH][KW][C], 1: d3a_conv_bwd_x's tap-major [KH][KW][CO][C]. */
+int d3a_conv_pack_weights(const d3a_conv_desc* descs, const int32_t* layouts, int32_t n,
+                          void* stream);
 
 /* Per-sample [P][C] (NHWC) <-> [C][P] (NCHW) transpose, optional [mask > 0]
  * in the destination layout: the flatten before PixelEncoder._fc
