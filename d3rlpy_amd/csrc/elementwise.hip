@@ -143,8 +143,13 @@ __global__ __launch_bounds__(256) void outer_mask_kernel(const float* g, int64_t
 // q = j, j + L, ... in order, then the group is summed by a fixed butterfly.
 // A lane issues up to 32 loads before it adds (clamped addresses, so short
 // segments take one memory round trip too); the addition order is q ascending.
-__host__ __device__ __forceinline__ int seg_lanes(int64_t n_partials) {
-  return n_partials >= 64 ? 16 : 1;
+// lanes per element summing a segment's partials: 16 (strided over the
+// partials, combined in a fixed order) for many partials of a small segment,
+// else 1 (each lane walks its element's partials, lanes over consecutive
+// elements: coalesced; K5's 32,768-element embedding weight with 256
+// partials read 16 partials per 64-byte line fetched on 16 lanes)
+__host__ __device__ __forceinline__ int seg_lanes(int64_t n_partials, int64_t numel) {
+  return n_partials >= 64 && numel < 8192 ? 16 : 1;
 }
 
 __device__ __forceinline__ double sum_partials(const float* g, int64_t n, int64_t stride,
@@ -183,7 +188,7 @@ __device__ __forceinline__ void locate_block(const d3a_adam_segment* segs, int n
   for (int c = 0; c < n_seg; c += 64) {
     const int s = c + lane;
     long long nb = 0;
-    if (s < n_seg) nb = (segs[s].numel * seg_lanes(segs[s].n_partials) + 255) / 256;
+    if (s < n_seg) nb = (segs[s].numel * seg_lanes(segs[s].n_partials, segs[s].numel) + 255) / 256;
     long long incl = nb;
     for (int o = 1; o < 64; o <<= 1) {
       const long long t = __shfl_up(incl, o, 64);
@@ -237,7 +242,7 @@ __global__ __launch_bounds__(256) void adam_kernel(d3a_adam_desc a) {
   if (!tab) __syncthreads();  // (block 0: every ring writer has read *ring_ctr)
   const d3a_adam_segment sg = tab ? a.blocks[blockIdx.x].seg : segs[s_seg];
   const int64_t first = tab ? a.blocks[blockIdx.x].first : s_first;
-  const int L = seg_lanes(sg.n_partials);
+  const int L = seg_lanes(sg.n_partials, sg.numel);
   const int64_t lt = ((int64_t)blockIdx.x - first) * 256 + threadIdx.x;
   const int64_t i = lt / L;
   const bool act = i < sg.numel;
@@ -298,7 +303,7 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(const d3a_adam_segment
   locate_block(segs, n_seg, &s_seg, &s_first);
   __syncthreads();
   const d3a_adam_segment sg = segs[s_seg];
-  const int L = seg_lanes(sg.n_partials);
+  const int L = seg_lanes(sg.n_partials, sg.numel);
   const int64_t lt = ((int64_t)blockIdx.x - s_first) * 256 + threadIdx.x;
   const int64_t i = lt / L;
   if (i >= sg.numel) return;  // uniform over each lane group
