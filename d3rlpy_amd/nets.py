@@ -202,7 +202,7 @@ class AdamGroup:
             segs[i].partial_stride = numel
             segs[i].grad_out = self.grad_store.ptr(n) if self.grad_store is not None else None
             # lanes per element (elementwise.hip seg_lanes)
-            lanes = 16 if parts >= 64 and numel < 8192 else 1
+            lanes = 16 if parts >= 64 else 1
             self.n_blocks += (numel * lanes + 255) // 256
             self.n_blocks_reduced += (numel + 255) // 256
         raw = bytes(segs)
@@ -229,12 +229,11 @@ class AdamGroup:
     def _block_table(self, segs, partials: bool) -> torch.Tensor:
         """d3a_adam_block per flat block (the segment search done once here,
         in the kernel's block order: segment s owns ceil(numel_s * L_s / 256)
-        blocks, L_s = 16 lanes per element for >= 64 partials of < 8,192
-        elements, else 1)."""
+        blocks, L_s = 16 lanes per element for >= 64 partials, else 1)."""
         rows = []
         first = 0
         for sg in segs:
-            lanes = 16 if (partials and sg.n_partials >= 64 and sg.numel < 8192) else 1
+            lanes = 16 if (partials and sg.n_partials >= 64) else 1
             nb = (sg.numel * lanes + 255) // 256
             for _ in range(nb):
                 blk = N.AdamBlock()
