@@ -95,3 +95,39 @@ def test_struct_layouts_match_header(tmp_path):
         assert int(out[cname]) == ctypes.sizeof(cls), cname
         for f, _ in cls._fields_:
             assert int(out[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)
+
+
+def test_round4_entry_points_validate_and_size_without_a_gpu():
+    """The round-4 entries check their arguments before any HIP call, and
+    d3a_conv_bwd_w_splits is host arithmetic: the split counts K5 sizes its
+    conv weight-gradient partials with (uint8 layer on the fp32 kernel: 32;
+    fp32 layers: ~512 workgroups of the split-bf16 kernel)."""
+    from d3rlpy_amd import _native as N
+    lib = N.lib()
+
+    def conv(B, C, H, W, CO, K, S):
+        d = N.ConvDesc()
+        d.B, d.C, d.H, d.W, d.KH, d.KW, d.S, d.CO = B, C, H, W, K, K, S, CO
+        d.OH, d.OW = (H - K) // S + 1, (W - K) // S + 1
+        return d
+
+    u8 = conv(512, 4, 84, 84, 32, 8, 4)
+    u8.x_u8 = 16
+    assert lib.d3a_conv_bwd_w_splits(ctypes.byref(u8)) == 32
+    l2, l3 = conv(512, 32, 20, 20, 64, 4, 2), conv(512, 64, 9, 9, 64, 3, 1)
+    l2.x_f32 = l3.x_f32 = 16
+    assert lib.d3a_conv_bwd_w_splits(ctypes.byref(l2)) == 32
+    assert lib.d3a_conv_bwd_w_splits(ctypes.byref(l3)) == 29
+    # input gradient: C must be 32 or 64
+    bad = conv(2, 48, 20, 20, 64, 4, 2)
+    bad.x_f32, bad.weight, bad.dy, bad.y = 16, 16, 16, 16
+    assert lib.d3a_conv_bwd_x(ctypes.byref(bad), None) < 0
+    assert b"C must be 32 or 64" in lib.d3a_last_error()
+    # the one-launch weight copies: at most 8 layers
+    descs = (N.ConvDesc * 9)()
+    lays = (ctypes.c_int32 * 9)()
+    assert lib.d3a_conv_pack_weights(descs, lays, 9, None) < 0
+    # fused actor head + trunk backward: null descriptors
+    assert lib.d3a_q2_bwd_actor_head(None, None, None) < 0
+    # split-K epilogue: rows of N % 4 == 0 floats
+    assert lib.d3a_splitk_epilogue_f32(16, 2, 12, 16, None, 4, 6, 1, None) < 0
