@@ -547,17 +547,23 @@ def main():
     gpu_steps(algo, it, 1)  # eager first update: its all-reduces are recorded
     if ar_log is not None:
         ar_log["armed"] = False
-    gpu_steps(algo, it, max(0, args.warmup - 1))
     # the dominant kernel's average launch time (HIP events on its stream),
-    # taken here, right before the timed region, over its last 500 of 1,000
-    # back-to-back launches: the MI355X takes >10 ms of load to reach its
-    # loaded clock (the same kernel measured 37.5 us after 5 warm-up steps,
-    # 34.2 after 50, 31.4 in a 300-step profile), so the measurement waits for
-    # the clock and leaves the device at it -- a short timed window (the
-    # driver's --steps 20 --warmup 5) then starts where a long one runs
-    # (profiles/r04_bench_window.jsonl)
+    # over its last 500 of 1,000 back-to-back launches, taken after the first
+    # (eager) warm-up step and before the others: the MI355X takes >10 ms of
+    # load to reach its loaded clock (the same kernel measured 37.5 us after 5
+    # warm-up steps, 34.2 after 50, 31.4 in a 300-step profile), so the
+    # measurement waits for the clock, and the remaining warm-up steps then
+    # run the whole step's working set through the caches right before the
+    # timed region (profiles/r04_bench_window.jsonl)
+    # (BENCH_MEASURE_LAST=1: the round-4 order, measurement after every warm-up
+    # step, right before the timed region)
     wsp = next(iter(algo.impl._ws.values()))
+    last = os.environ.get("BENCH_MEASURE_LAST", "0") == "1"
+    if last:
+        gpu_steps(algo, it, max(0, args.warmup - 1))
     kern_s, kflops, kdesc = measure_kernel(wsp, reps=500, settle=500)
+    if not last:
+        gpu_steps(algo, it, max(0, args.warmup - 1))
     torch.cuda.synchronize()
     _barrier(ws)
     wd.set()
@@ -723,7 +729,7 @@ def main():
                         if x6 else {}),
                      "avg_launch_us": round(kern_s * 1e6, 3),
                      "launch_timing": "HIP events on the kernel's stream, 500 launches after 500 "
-                                      "settling launches, right before the timed region"},
+                                      "settling launches, after the first warm-up step"},
         "cpu_baseline": cpu,
     }
     out["host"] = host
