@@ -562,6 +562,14 @@ def main():
     if last:
         gpu_steps(algo, it, max(0, args.warmup - 1))
     kern_s, kflops, kdesc = measure_kernel(wsp, reps=500, settle=500)
+    # the critic weight-gradient backward, measured the same way (on the last
+    # forward's kept activations)
+    bwd = None
+    if hasattr(wsp, "backward_kernel") and wsp.backward_kernel() is not None:
+        bl, bflops, bdesc = wsp.backward_kernel()
+        b_s, _, _ = measure_kernel(type("K", (), {"dominant_kernel": lambda self: (bl, bflops, bdesc)})(),
+                                   reps=500, settle=100)
+        bwd = (b_s, bflops, bdesc)
     if not last:
         gpu_steps(algo, it, max(0, args.warmup - 1))
     torch.cuda.synchronize()
@@ -584,12 +592,28 @@ def main():
     gpu_steps(algo, it, nb)
     th1 = time.perf_counter()
     torch.cuda.synchronize()
+    # where the short window's time goes: device time of each step of a
+    # 20-step window run like the timed one (HIP events on the stream between
+    # the steps' enqueues; after the timed region, so it does not perturb it)
+    import torch as _t
+    st = _t.cuda.current_stream()
+    _t.cuda.synchronize()
+    evs = [_t.cuda.Event(enable_timing=True) for _ in range(nb + 1)]
+    evs[0].record(st)
+    for k in range(nb):
+        gpu_steps(algo, it, 1)
+        evs[k + 1].record(st)
+    _t.cuda.synchronize()
+    step_trace = [round(1e3 * evs[k].elapsed_time(evs[k + 1]), 1) for k in range(nb)]
     host = {"host_us_per_step": round(1e6 * (th1 - th0) / nb, 2),
             "host_loop_us_per_step": round(1e6 * (t_enq - t0) / max(1, args.steps), 2),
             "method": f"perf_counter around next(it) + _update_async with no sync: a burst of "
                       f"{nb} steps enqueued onto an idle device (host_us_per_step), and the timed "
                       "loop's enqueue time over its steps (host_loop_us_per_step: equals "
-                      "ms_per_step when the device pushes back)"}
+                      "ms_per_step when the device pushes back)",
+            "step_trace_us": step_trace,
+            "step_trace_method": f"HIP events between the enqueues of {nb} steps after a sync "
+                                 "(device time per step, first step first)"}
     # sanity: the losses are finite
     names, vals = algo.impl.read_metrics_ring(None)
     # NaN in a column marks "not computed at this step" (TD3+BC's delayed
@@ -636,8 +660,8 @@ def main():
     cpu = None
     # the CPU baseline is a rank-0, single-GPU-run measurement (not repeated per N)
     if not args.no_cpu_baseline and ws == 1:
-        host = host_cpu()
-        threads = args.cpu_threads or host["threads"]
+        cpu_host = host_cpu()
+        threads = args.cpu_threads or cpu_host["threads"]
         sps, k, el = cpu_baseline(args.cpu_seconds, threads, args.algo)
         sps1, k1, el1 = cpu_baseline(args.cpu_seconds_1t, 1, args.algo)
         what = {"cql": "CQL update (torch CPU, op-for-op restatement of cql_impl.py/"
@@ -661,7 +685,7 @@ def main():
                          f"in {el:.1f}s on {threads} threads (this process's CPU share)",
                "one_thread": {"value": round(sps1, 3), "cores": 1,
                               "sample": f"{k1} steps in {el1:.1f}s"},
-               "host": host}
+               "host": cpu_host}
         # BASELINE.md's full protocol (>= 1000 steps after 50 warm-up, median
         # of 5, all cores and 1 thread), run by tools/cpu_baseline_protocol.py
         proto = next((p for p in (os.path.join(os.path.dirname(os.path.abspath(__file__)),
@@ -732,6 +756,25 @@ def main():
                                       "settling launches, after the first warm-up step"},
         "cpu_baseline": cpu,
     }
+    if bwd is not None:
+        b_s, bflops, bdesc = bwd
+        # the backward's large products are the 0 / 1 ReLU mask times three
+        # bf16 parts: its ceiling is the bf16 peak / 3 (fp32 MFMA: 157.3 TF)
+        bpeak = 2500.0 / 3 if (x6 and "x3" in bdesc) else 157.3
+        bach = bflops / b_s / 1e12
+        sec = {"bound": "mfma", "achieved": round(bach, 3), "peak": round(bpeak, 1),
+               "unit": "TFLOP/s", "frac": round(bach / bpeak, 4), "kernel": bdesc,
+               "avg_launch_us": round(b_s * 1e6, 3),
+               "launch_timing": "HIP events on the kernel's stream, 500 launches after 100 "
+                                "settling launches, after the first warm-up step"}
+        if x6 and "x3" in bdesc:
+            sec["bf16_mfma_frac"] = round(3 * bach / 2500.0, 4)
+        # the step's largest kernel leads: the other critic kernel beside it
+        if b_s > kern_s:
+            sec["traffic"] = None
+            out["roofline"], out["roofline_other"] = sec, out["roofline"]
+        else:
+            out["roofline_other"] = sec
     out["host"] = host
     if allreduce is not None:
         allreduce["frac_of_step"] = round(allreduce["us_per_step"] / (1e3 * out["ms_per_step"]), 4)

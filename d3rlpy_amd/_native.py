@@ -275,6 +275,7 @@ class MlpFwdDesc(C.Structure):
         ("xg_obs", vp), ("xg_a", vp), ("xg_lda", C.c_int64),
         ("xg_base", vp), ("xg_clip", C.c_float), ("xg_scale", C.c_float),
         ("hmask", vp), ("s_hmask", C.c_int64),
+        ("hmaskT", vp), ("s_hmaskT", C.c_int64),
     ]
 
 
@@ -311,6 +312,9 @@ class Q2BwdDesc(C.Structure):
         ("dz2", vp), ("sdz", C.c_int64),
         ("block_rows", C.c_int32),
         ("m2", vp), ("sm2", C.c_int64),
+        ("m2t", vp), ("sm2t", C.c_int64),
+        ("b2", vp), ("sb2", C.c_int64),
+        ("row_splits", C.c_int32),
     ]
 
 
@@ -519,6 +523,7 @@ _SIGNATURES = {
     "d3a_conv_fwd": (C.c_int, [C.POINTER(ConvDesc), vp]),
     "d3a_conv_bwd_w": (C.c_int, [C.POINTER(ConvDesc), vp]),
     "d3a_conv_bwd_w_splits": (C.c_int32, [C.POINTER(ConvDesc)]),
+    "d3a_q2_bwd_x6t_splits": (C.c_int32, [C.c_int64, C.c_int32]),
     "d3a_conv_bwd_x": (C.c_int, [C.POINTER(ConvDesc), vp]),
     "d3a_conv_pack_weights": (C.c_int, [C.POINTER(ConvDesc), C.POINTER(C.c_int32), C.c_int32, vp]),
     "d3a_iqn_prior": (C.c_int, [C.POINTER(IqnPriorDesc), vp]),

@@ -481,7 +481,10 @@ class _Workspace:
         # backward spaces + optimisers
         self.Rc = 3 * NB + B
         self.cgrads = GradSpace(dev)
-        self.cbwd = mlp.BackwardSpace(impl.critic, self.Rc, self.cgrads, dev)
+        # the critic backward reads rows [3NB, R): the slice kernel where it
+        # applies (then the critic forward keeps h[0] and the mask bits only)
+        self.cbwd = mlp.BackwardSpace(impl.critic, self.Rc, self.cgrads, dev, slice_r0=3 * NB)
+        self.qacts.no_last_h = self.cbwd.slice
         self.abwd = mlp.BackwardSpace(impl.critic, B, None, dev)
         self.pgrads = GradSpace(dev)
         # the policy head's weight / bias gradients come from
@@ -698,6 +701,32 @@ class _Workspace:
                            C, R, Hin, H, relu=True, ldy=H, sxb=R * Hin, syb=R * H)
         flops = 2 * C * R * Hin * H
         return launch, flops, f"gemm_f32 critic layer-2 fwd: C={C} x [{R}x{Hin}]@[{Hin}x{H}]"
+
+    def backward_kernel(self):
+        """(launch_fn, flops_per_launch, description) of the critic weight-
+        gradient backward over the critic set's 3NB+B rows -- the pipeline's
+        launch exactly (cql_impl.py:110-125 through ddpg_impl.py:119-133), on
+        the forward's kept activations of the last step; None when it is not
+        one launch.  FLOPs: dh1 and dW2 (2 C R 256^2 each) + dW1 (2 C R 256
+        n_in)."""
+        impl = self.impl
+        net, st = impl.critic, impl.store
+        if not self.cbwd.q2:
+            return None
+        NB, R, C, DA = self.NB, self.R, self.C, self.LDX
+        r0 = 3 * NB
+
+        def launch():
+            mlp.backward(self.cbwd, st, self.x_q.data_ptr(), True, DA, self.qacts,
+                         self.dq.data_ptr() + 4 * r0, 1, R, r0, self.Rc,
+                         g_scale=self.scalars.data_ptr() + 8, n_scaled=3 * NB)
+        s = net.sizes
+        flops = 2 * C * self.Rc * (2 * s[1] * s[2] + s[0] * s[1])
+        kind = ("slice, split-bf16 x3 mask-factored" if self.cbwd.slice else
+                "256-row blocks, split-bf16 x3 mask-factored" if ops.CRITIC_GEMM == "x6"
+                else "fp32 MFMA")
+        return launch, flops, (f"d3a_q2_bwd critic weight gradients ({kind}): C={C} x "
+                               f"{self.Rc} rows x {'-'.join(map(str, s))}")
 
     # ------------------------------------------------------------- pipeline
     def execute(self, flags, use_graph: bool) -> None:

@@ -304,6 +304,22 @@ class DiscreteCQLImpl(ImplBase):
         return next(iter(self._ws.values())).opt.grad(name)
 
 
+def conv_wgrad_splits(geom, l: int, B: int) -> int:
+    """The split count d3a_conv_bwd_w fills the chip with for conv layer l of
+    a B-sample backward (its kernel's choice, d3a_conv_bwd_w_splits): the
+    first layer reads the uint8 frames (x_u8 set, as the backward launch sets
+    it), which selects the fp32-MFMA kernel's 32 splits -- not the split-bf16
+    kernel's count for an fp32 input."""
+    ci, h, w, co, k, s, oh, ow = geom[l]
+    gd = NAT.ConvDesc()
+    gd.B, gd.C, gd.H, gd.W, gd.KH, gd.KW, gd.S, gd.OH, gd.OW, gd.CO = B, ci, h, w, k, k, s, oh, ow, co
+    if l == 0:
+        gd.x_u8 = 1  # only its presence is read by the query
+    S = int(NAT.lib().d3a_conv_bwd_w_splits(C.byref(gd)))
+    assert S >= 1
+    return S
+
+
 def _conv_desc(geom, l: int, n: int, store: ParamStore, names) -> "NAT.ConvDesc":
     ci, h, w, co, k, s, oh, ow = geom[l]
     d = NAT.ConvDesc()
@@ -493,12 +509,7 @@ class _Workspace:
         self.grads = GradSpace(dev)
         self.splits = {}
         for l, (ci, h, w, co, k, s, oh, ow) in enumerate(impl.geom):
-            # the split count d3a_conv_bwd_w fills the chip with (its kernel's choice)
-            gd = NAT.ConvDesc()
-            gd.B, gd.C, gd.H, gd.W, gd.KH, gd.KW, gd.S, gd.OH, gd.OW, gd.CO = \
-                B, ci, h, w, k, k, s, oh, ow, co
-            S = int(NAT.lib().d3a_conv_bwd_w_splits(C.byref(gd)))
-            assert S >= 1
+            S = conv_wgrad_splits(impl.geom, l, B)
             self.splits[l] = S
             self.grads.add(f"enc.c{l}.W", (1, co, ci, k, k), S)
             self.grads.add(f"enc.c{l}.b", (1, co), S)

@@ -99,6 +99,9 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   // the ReLU mask image of the last hidden layer (kept rows; NO == 1)
   uint32_t* const hmg = (!aux && NO == 1 && d.hmask) ? reinterpret_cast<uint32_t*>(d.hmask) + c * d.s_hmask
                                                      : nullptr;
+  // and transposed (word [r >> 5][unit], bit r & 31; d.r0 % 32 == 0)
+  uint32_t* const hmtg = (hmg != nullptr && d.hmaskT) ? reinterpret_cast<uint32_t*>(d.hmaskT) + c * d.s_hmaskT
+                                                      : nullptr;
   // a kept run of four activations (16 bytes fp32, 8 bytes bf16)
   auto put4 = [](HT* p, const float* v) {
     if constexpr (sizeof(HT) == 4) {
@@ -385,6 +388,30 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       bm |= (uint32_t)__shfl_xor((int)bm, 32, 64);
       if (lh == 0 && row >= h_from && row < rend) hmg[(int64_t)row * (X_H / 32) + w] = bm;
     }
+    if (hmtg != nullptr) {
+      // the tile's 32 rows as the bits of one word per unit: register 4 R + i
+      // holds unit 32 w + 8 R + i in lanes 0-31 and + 4 in lanes 32-63, so
+      // one ballot is two words; lane k of the wave stores unit 32 w + k's
+      const int row0 = m0 + 32 * tt;  // wave-uniform
+      if (row0 + 31 >= h_from && row0 < rend) {
+        int wv = 0;
+#pragma unroll
+        for (int R = 0; R < 4; ++R)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const unsigned long long bl = __ballot(v[4 * R + i] > 0.f);
+            // (selects, not v_writelane from inline asm: the compiler does not
+            // see that asm's read of the ballot's SGPRs, and the hazard between
+            // the compare writing them and the lane write went unpadded)
+            const int lo = (int)(uint32_t)bl, hi = (int)(uint32_t)(bl >> 32);
+            wv = lane == 8 * R + i ? lo : wv;
+            wv = lane == 8 * R + 4 + i ? hi : wv;
+          }
+        // (a group's 256 words lane-major for the backward's 16-lane tiles:
+        // unit o at (o & 15) 16 + (o >> 4))
+        if (lane < 32) hmtg[(int64_t)(row0 >> 5) * X_H + (lane & 15) * 16 + 2 * w + (lane >> 4)] = (uint32_t)wv;
+      }
+    }
     float hs = v[0] * ww[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) hs = fmaf(v[r], ww[r], hs);
@@ -424,6 +451,11 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
                     (d.n_out == 1 && (reinterpret_cast<uintptr_t>(d.hmask) & 3) == 0 &&
                      d.s_hmask >= (d.r0 + d.rows) * (X_H / 32)),
                 "d3a_q2_fwd_x6: hmask needs one output and rows of 8 32-bit words");
+  D3A_CHECK_ARG(d.hmaskT == nullptr ||
+                    (d.hmask != nullptr && d.r0 % 32 == 0 &&
+                     (reinterpret_cast<uintptr_t>(d.hmaskT) & 3) == 0 &&
+                     d.s_hmaskT >= (d.r0 + d.rows + 31) / 32 * X_H),
+                "d3a_q2_fwd_x6: hmaskT needs hmask, r0 % 32 == 0 and [rows / 32][256] words");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.r0 >= 0 && d.h_from >= 0 && d.aux_rows >= 0,
                 "d3a_q2_fwd_x6: bad sizes");
   auto a16 = [](const void* p, int64_t stride) {

@@ -558,17 +558,21 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
 
 using namespace d3a;
 
+namespace d3a {
+int launch_q2x6t_bwd(const d3a_q2_bwd_desc& d, hipStream_t st);  // q2_x6_bwd2.hip
+}
+
 extern "C" int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_bwd_x6: null desc");
   const d3a_q2_bwd_desc& d = *dp;
   D3A_CHECK_ARG(d.dz2 == nullptr, "d3a_q2_bwd_x6: dz2 input is not supported (use d3a_q2_bwd)");
   D3A_CHECK_ARG(d.block_rows == 0 || d.block_rows == 256, "d3a_q2_bwd_x6: block_rows must be 0 / 256");
-  D3A_CHECK_ARG(d.x && d.h1 && d.h2 && d.g && d.W2 && d.w3, "d3a_q2_bwd_x6: null input");
+  D3A_CHECK_ARG(d.x && d.h1 && (d.h2 || d.m2t) && d.g && d.W2 && d.w3, "d3a_q2_bwd_x6: null input");
   D3A_CHECK_ARG(d.dW1 && d.db1 && d.dW2 && d.db2 && d.dW3 && d.db3, "d3a_q2_bwd_x6: null output");
   D3A_CHECK_ARG(d.n_in >= 1 && d.n_in <= 48, "d3a_q2_bwd_x6: n_in must be 1..48");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.n_scaled >= 0, "d3a_q2_bwd_x6: bad sizes");
   auto a16 = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; };
-  D3A_CHECK_ARG(a16(d.h1) && a16(d.h2) && d.ldh == B6_H && d.sh % 4 == 0,
+  D3A_CHECK_ARG(a16(d.h1) && (d.m2t || a16(d.h2)) && d.ldh == B6_H && d.sh % 4 == 0,
                 "d3a_q2_bwd_x6: h1 / h2 must be 16-byte aligned rows of 256 floats");
   D3A_CHECK_ARG(a16(d.w3) && d.sw3 % 4 == 0, "d3a_q2_bwd_x6: w3 must be 16-byte aligned");
   D3A_CHECK_ARG(d.ldx >= d.n_in, "d3a_q2_bwd_x6: ldx < n_in");
@@ -577,6 +581,7 @@ extern "C" int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(d.m2 == nullptr || ((reinterpret_cast<uintptr_t>(d.m2) & 3) == 0 &&
                                     d.sm2 >= d.rows * (B6_H / 32)),
                 "d3a_q2_bwd_x6: the mask must be rows of 8 32-bit words");
+  if (d.m2t != nullptr) return launch_q2x6t_bwd(d, (hipStream_t)stream);
   if (d.rows == 0) return 0;
   const int64_t units = ((d.rows + B6_RB - 1) / B6_RB) * d.C;
   const int64_t blocks = (units + 7) / 8 * 32;

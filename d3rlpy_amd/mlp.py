@@ -49,6 +49,14 @@ class Acts:
     # first row of the mask image the last forward wrote (None: not written;
     # the backward then builds the mask from h2)
     hmask_from: Optional[int] = None
+    # the same mask transposed ([C][ceil(R / 32)][256] int32, d3a_mlp_fwd_desc.
+    # hmaskT), written with hmask where the forward's rows start on a 32-row
+    # group; read by the slice backward (d3a_q2_bwd_desc.m2t)
+    hmaskT: Optional[torch.Tensor] = None
+    hmaskT_from: Optional[int] = None
+    # the slice backward reads no h2: the x6 forward then keeps only h[0] and
+    # the mask bits (set by the owner of the backward space, BackwardSpace.slice)
+    no_last_h: bool = False
 
     @staticmethod
     def alloc(net: EnsembleMLP, R: int, device, dtype=torch.float32,
@@ -60,10 +68,24 @@ class Acts:
               for l in range(net.n_layers - 1)]
         out_dim = net.sizes[-1]
         out = torch.zeros((net.C, R) if out_dim == 1 else (net.C, R, out_dim), device=device)
-        hm = None
+        hm = hmt = None
         if with_mask and net.n_layers >= 2 and net.sizes[-2] % 32 == 0:
             hm = torch.zeros(net.C, R, net.sizes[-2] // 32, device=device, dtype=torch.int32)
-        return Acts(hs, out, R, hm)
+            if net.sizes[-2] == 256:
+                hmt = torch.zeros(net.C, (R + 31) // 32, 256, device=device, dtype=torch.int32)
+        return Acts(hs, out, R, hm, hmaskT=hmt)
+
+    def relu_decisions(self, c: int, r0: int, r1: int) -> List[torch.Tensor]:
+        """[h_l > 0] of member c, rows [r0, r1), for every hidden layer: from
+        the kept activations, the last one from the mask bits when it is not
+        kept (no_last_h)."""
+        out = [(h[c, r0:r1] > 0) for h in self.h]
+        if self.no_last_h:
+            assert self.hmask is not None and self.hmask_from is not None and self.hmask_from <= r0
+            w = self.hmask[c, r0:r1].to(torch.int64)
+            bits = (w.unsqueeze(-1) >> torch.arange(32, device=w.device)) & 1
+            out[-1] = bits.reshape(r1 - r0, -1).bool()
+        return out
 
 
 # one-launch forward (d3a_mlp_fwd) unless D3A_FUSED_MLP=0 (per-layer GEMMs,
@@ -147,6 +169,20 @@ def q2_ok(net: EnsembleMLP, rows: int) -> bool:
 _Q2P = os.environ.get("D3A_Q2P", "1") == "1"
 
 
+# the critic weight-gradient backward on the slice kernel (csrc/q2_x6_bwd2.hip:
+# transposed mask bits, no kept h2, P = d3a_q2_bwd_x6t_splits row blocks);
+# D3A_BWD_SLICE=0 keeps the 256-row-block kernel (A/B)
+_SLICE = os.environ.get("D3A_BWD_SLICE", "1") == "1"
+
+
+def slice_ok(net: EnsembleMLP, rows: int, r0: int) -> bool:
+    """The slice backward applies to a q2 backward space of ``rows`` rows read
+    from row ``r0`` of the x6 forward's activations: x6 critic GEMMs with
+    fp32 kept activations and both on 32-row groups."""
+    return (_SLICE and q2_ok(net, rows) and ops.CRITIC_GEMM == "x6"
+            and ops.CRITIC_PRECISION not in ("bf16", "bf16h") and rows % 32 == 0 and r0 % 32 == 0)
+
+
 def q2p_ok(net: EnsembleMLP, rows: int) -> bool:
     s = net.sizes
     return (_Q2P and not _FUSED_BWD and not ops.SBF16_TERMS and net.n_layers == 3
@@ -223,6 +259,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     n = r1 - r0
     if acts.hmask is not None:
         acts.hmask_from = None  # set below where this forward writes the mask image
+        acts.hmaskT_from = None
     if n <= 0:
         return False
     C = net.C if members is None else members
@@ -285,6 +322,14 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             if (entry == "d3a_q2_fwd_x6" and keep_h and members is None and sizes[-1] == 1):
                 d.hmask, d.s_hmask = acts.hmask.data_ptr(), R * (sizes[-2] // 32)
                 acts.hmask_from = d.h_from
+                if acts.hmaskT is not None and r0 % 32 == 0:
+                    d.hmaskT, d.s_hmaskT = acts.hmaskT.data_ptr(), acts.hmaskT[0].numel()
+                    acts.hmaskT_from = d.h_from
+                    if acts.no_last_h:
+                        d.h[L - 2] = None  # the slice backward reads no h2
+            elif acts.no_last_h:
+                raise RuntimeError("Acts.no_last_h: the forward must be the x6 Q forward "
+                                   "that writes the mask bits")
         means = row_mean is not None and entry == "d3a_mlp_fwd_x6"
         if means:
             assert tuple(row_mean.shape) == (C, R) and row_mean.dtype == torch.float32
@@ -342,10 +387,15 @@ class BackwardSpace:
     """dz ping-pong buffers + weight-gradient partial workspaces for one net."""
 
     def __init__(self, net: EnsembleMLP, rows: int, grads: Optional[GradSpace], device,
-                 splits: Optional[int] = None, head_partials: Optional[int] = None):
+                 splits: Optional[int] = None, head_partials: Optional[int] = None,
+                 slice_r0: Optional[int] = None):
         """``head_partials``: partial count of the head layer's weight / bias
         gradients when a caller's kernel writes them (one per row, say)
-        instead of the split-K GEMM (``backward(..., head_ready=True)``)."""
+        instead of the split-K GEMM (``backward(..., head_ready=True)``).
+        ``slice_r0``: the backward will read the forward's activations from
+        this row on; where ``slice_ok`` the weight gradients come from the
+        slice kernel (``self.slice``: its partial layout, and the caller's
+        Acts must set ``no_last_h``)."""
         self.net = net
         self.rows = rows
         hidden = net.sizes[1:-1]
@@ -366,6 +416,8 @@ class BackwardSpace:
         # the trunk from a caller-formed dz2 (head_ready), 32-row partials
         self.q2p = (grads is not None and head_partials is not None and not self.fused
                     and q2p_ok(net, rows))
+        self.slice = (self.q2 and slice_r0 is not None and slice_ok(net, rows, slice_r0))
+        self.slice_P = N.lib().d3a_q2_bwd_x6t_splits(rows, net.C) if self.slice else 0
         # first-layer weight gradients as one partial per 128-row tile, from
         # the second layer's input-gradient GEMM (backward's wnext path; it
         # needs a layer above the first one, i.e. >= 2 hidden layers)
@@ -379,11 +431,18 @@ class BackwardSpace:
                 o, i = net.sizes[l + 1], net.sizes[l]
                 parts = head_partials if (head_partials and l == net.n_layers - 1) \
                     else (self.l0_tiles if (l == 0 and self.l0_tiles) else self.splits)
-                if self.q2:
+                wparts = None
+                if self.slice:
+                    # one per row block; the head weight one per row block and
+                    # 16-unit slice of layer 1
+                    parts = self.slice_P
+                    if l == net.n_layers - 1:
+                        wparts = 16 * self.slice_P
+                elif self.q2:
                     parts = (rows + 255) // 256
                 elif self.q2p and l < net.n_layers - 1:
                     parts = (rows + 31) // 32
-                grads.add(net.wname(l), (net.C, o, i), parts)
+                grads.add(net.wname(l), (net.C, o, i), wparts or parts)
                 grads.add(net.bname(l), (net.C, o), parts)
 
 
@@ -435,6 +494,18 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         d.x, d.ldx, d.sxb = x + 4 * r0 * ldx, ldx, sxb_
         d.h1 = acts.h[0].data_ptr() + esz * r0 * H
         d.h2 = acts.h[1].data_ptr() + esz * r0 * H
+        if bs.slice:
+            # the slice kernel: row + transposed mask bits of the forward, b2,
+            # no h2 (the space's partials are laid out for it)
+            if not (acts.hmaskT_from is not None and acts.hmaskT_from <= r0 and r0 % 32 == 0
+                    and acts.hmask_from is not None and acts.hmask_from <= r0):
+                raise RuntimeError("slice backward: the forward did not write the mask bits "
+                                   f"of rows >= {r0}")
+            d.h2 = None
+            d.m2, d.sm2 = acts.hmask.data_ptr() + 4 * r0 * (H // 32), R * (H // 32)
+            d.m2t, d.sm2t = (acts.hmaskT.data_ptr() + 4 * (r0 // 32) * H, acts.hmaskT[0].numel())
+            d.b2, d.sb2 = net.b(1, store), H
+            d.row_splits = bs.slice_P
         d.sh, d.ldh = R * H, H
         d.g, d.sgb = dout, sdout_b
         if g_scale is not None:
@@ -448,7 +519,7 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         entry = "d3a_q2_bwd_bf16" if esz == 2 else "d3a_q2_bwd"
         if esz == 4 and (ops.CRITIC_GEMM == "x6" or ops.CRITIC_PRECISION == "bf16"):
             entry = "d3a_q2_bwd_x6"  # fp32-accurate split-bf16 (mask-factored)
-            if (acts.hmask is not None and acts.hmask_from is not None
+            if (not bs.slice and acts.hmask is not None and acts.hmask_from is not None
                     and acts.hmask_from <= r0 and _MASK_IMAGE):
                 # the forward's mask image of h2 (same rows as h1 / h2)
                 d.m2, d.sm2 = acts.hmask.data_ptr() + 4 * r0 * (H // 32), R * (H // 32)

@@ -274,6 +274,11 @@ typedef struct d3a_mlp_fwd_desc {
    * uint32 (bit o & 31 of word o >> 5; member stride s_hmask words) -- what
    * d3a_q2_bwd_x6 builds its mask operand from (d3a_q2_bwd_desc.m2).       */
   void* hmask; int64_t s_hmask;
+  /* Optional (with hmask, r0 % 32 == 0): the same mask transposed, [C][rows
+   * / 32][256] uint32 -- word [r >> 5][o], bit r & 31 = [h_last[r][o] > 0] --
+   * for every 32-row group holding a kept row (member stride s_hmaskT words):
+   * the operand of d3a_q2_bwd_x6's slice kernel (d3a_q2_bwd_desc.m2t).     */
+  void* hmaskT; int64_t s_hmaskT;
 } d3a_mlp_fwd_desc;
 #define D3A_MLP_PARTS 4
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);
@@ -348,7 +353,22 @@ typedef struct d3a_q2_bwd_desc {
    * sm2 words) -- the ReLU-mask operand is expanded from them, not built
    * from h2.                                                              */
   const void* m2; int64_t sm2;
+  /* Optional (d3a_q2_bwd_x6 only, with m2): the forward's transposed mask bits
+   * (d3a_mlp_fwd_desc.hmaskT; word [r / 32][o] of the rows at the base of
+   * h1, member stride sm2t words) and the layer-2 bias b2 [C][256] (stride
+   * sb2).  Selects the slice kernel (csrc/q2_x6_bwd2.hip): h2 is not read
+   * (dW3 = W2 . (m^T g' h1) + b2 (m^T g'), the forward's h2 identity), and
+   * the partials are P = row_splits (0: d3a_q2_bwd_x6t_splits(rows, C)) row
+   * blocks of ceil(rows / P) rows rounded up to 32: dW1 / db1 / dW2 / db2 /
+   * db3 [P][C][..] as above, dW3 [16 P][C][256] (one per row block and
+   * 16-unit slice of layer 1).                                              */
+  const void* m2t; int64_t sm2t;
+  const float* b2; int64_t sb2;
+  int32_t row_splits;
 } d3a_q2_bwd_desc;
+/* Row blocks P of d3a_q2_bwd_x6's slice kernel for `rows` rows of C members
+ * (about 256 workgroups of C * P * 16; the caller sizes the partials with it). */
+int32_t d3a_q2_bwd_x6t_splits(int64_t rows, int32_t C);
 int d3a_q2_bwd(const d3a_q2_bwd_desc* d, void* stream);
 
 /* bf16 throughput instantiation of the critic forward / backward (the

@@ -143,7 +143,7 @@ def hip_critic_masks(ws) -> List[dict]:
     NB, R = ws.NB, ws.R
     out = []
     for c in range(ws.C):
-        ls = [(h[c, 3 * NB:R] > 0).cpu() for h in ws.qacts.h]
+        ls = [m.cpu() for m in ws.qacts.relu_decisions(c, 3 * NB, R)]
         out.append({"blocks": [[m[k * NB:(k + 1) * NB] for m in ls] for k in range(3)],
                     "data": [m[3 * NB:] for m in ls]})
     return out

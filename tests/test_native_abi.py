@@ -131,3 +131,27 @@ def test_round4_entry_points_validate_and_size_without_a_gpu():
     assert lib.d3a_q2_bwd_actor_head(None, None, None) < 0
     # split-K epilogue: rows of N % 4 == 0 floats
     assert lib.d3a_splitk_epilogue_f32(16, 2, 12, 16, None, 4, 6, 1, None) < 0
+
+
+def test_dcql_workspace_sizes_the_uint8_conv_like_its_launch():
+    """the K5 workspace's partial count for the first (uint8) conv
+    is the one d3a_conv_bwd_w uses for it (x_u8 set: 32 splits), not the
+    split-bf16 count of an fp32 input of that shape."""
+    from d3rlpy_amd.algos.discrete_cql_impl import _geometry, conv_wgrad_splits
+    geom = _geometry((4, 84, 84))
+    assert conv_wgrad_splits(geom, 0, 512) == 32
+    assert conv_wgrad_splits(geom, 1, 512) == 32
+    assert conv_wgrad_splits(geom, 2, 512) == 29
+
+
+def test_slice_backward_row_blocks():
+    """d3a_q2_bwd_x6t_splits: about 256 workgroups (C P 16), >= 4 sub-blocks
+    of 32 rows a row block."""
+    from d3rlpy_amd import _native as N
+    lib = N.lib()
+    assert lib.d3a_q2_bwd_x6t_splits(7936, 2) == 8    # K2 critic backward
+    assert lib.d3a_q2_bwd_x6t_splits(7936, 1) == 16
+    assert lib.d3a_q2_bwd_x6t_splits(640, 10) == 1
+    assert lib.d3a_q2_bwd_x6t_splits(256, 2) == 2
+    assert lib.d3a_q2_bwd_x6t_splits(32, 2) == 1
+    assert lib.d3a_q2_bwd_x6t_splits(100, 0) < 0
