@@ -20,6 +20,8 @@ reference) from the SAME state HIP starts a stage from, and compares:
 """
 from __future__ import annotations
 
+import copy
+
 import math
 from typing import Dict
 
@@ -43,7 +45,7 @@ def load_state(orc, sd: Dict[str, dict]) -> None:
     """Load an Impl's get_state_dict() (reference layout) into an oracle;
     modules keep their dtype (load_state_dict copies with conversion)."""
     for k, v in sd.items():
-        getattr(orc, k).load_state_dict(v)
+        getattr(orc, k).load_state_dict(copy.deepcopy(v))  # (optimiser state tensors are kept, not copied)
 
 
 def hip_grads(refs, getter) -> Dict[str, torch.Tensor]:

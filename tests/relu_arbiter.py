@@ -30,6 +30,8 @@ the data values).
 """
 from __future__ import annotations
 
+import copy
+
 from typing import Dict, List, Optional
 
 import torch
@@ -167,7 +169,10 @@ def oracle_from_state(make_oracle, sd0: Dict[str, dict], dtype):
     o = make_oracle()
     for k, v in sd0.items():
         if hasattr(o, k):
-            getattr(o, k).load_state_dict(v)
+            # a private copy: torch's Optimizer.load_state_dict keeps the given
+            # state tensors (same dtype / device), and this oracle's optimiser
+            # steps would otherwise advance the caller's state dict in place
+            getattr(o, k).load_state_dict(copy.deepcopy(v))
     if dtype == torch.float64:
         for mod in (o._q_func, o._policy, o._targ_q_func, o._targ_policy, o._log_temp,
                     o._log_alpha):
@@ -225,9 +230,9 @@ def cql_critic_arbiter(label: str, make_oracle, sd0, tb, nz, g_hip: Dict[str, to
     for k, r64 in g64.items():
         e_hip, e32 = max_rel(g_hip[k], r64), max_rel(g32[k], g64a[k])
         bar = max(tol, 2.0 * e32)
-        if e_hip > 0.5 * tol:
-            print(f"  {label} {k}: hip vs fp64(HIP masks) {e_hip:.1e}, oracle32 vs "
-                  f"fp64(own masks) {e32:.1e}, bar {bar:.1e}")
+        # every tensor's margin (committed per round: profiles/r05_arbiter_margins.log)
+        print(f"  {label} {k}: hip vs fp64(HIP masks) {e_hip:.1e}, oracle32 vs "
+              f"fp64(own masks) {e32:.1e}, bar {bar:.1e}")
         assert e_hip <= bar, (label, k, e_hip, e32)
         worst = max(worst, e_hip)
         worst_ratio = max(worst_ratio, e_hip / bar)

@@ -4,6 +4,7 @@ CPU: the oracle reproduces its committed vectors bit-for-bit (guards the
 oracle against drift).  GPU (marked): the HIP gather is bit-exact against the
 gather fixture, and one HIP CQL update matches the CQL fixture.
 """
+import copy
 import os
 
 import numpy as np
@@ -34,7 +35,7 @@ def _oracle_from_fixture(g):
     D, A, H, L, N, B = (int(v) for v in g["cfg"])
     orc = CQLOracle(D, A, n_critics=2, n_action_samples=N, hidden_units=[H] * L, seed=0)
     for k, v in _state_from(g, "init/").items():
-        getattr(orc, k).load_state_dict(v)
+        getattr(orc, k).load_state_dict(copy.deepcopy(v))
     return orc, (D, A, H, L, N, B)
 
 
@@ -156,7 +157,7 @@ def _td3_oracle(g):
     orc = TD3PlusBCOracle(D, A, n_critics=2, hidden_units=[H] * L,
                           scaler=StandardScalerT(g["scaler_mean"], g["scaler_std"]), seed=0)
     for k, v in _td3_from_fixture(g, "init/").items():
-        getattr(orc, k).load_state_dict(v)
+        getattr(orc, k).load_state_dict(copy.deepcopy(v))
     # fresh Adam state, as in the fixture (built right before its first update)
     orc._critic_optim = torch.optim.Adam(orc._q_func.parameters(), lr=3e-4)
     orc._actor_optim = torch.optim.Adam(orc._policy.parameters(), lr=3e-4)

@@ -9,6 +9,7 @@ between the two fp32 implementations (HIP itself is within 1e-5 of fp64:
 tests/test_gpu_arbiters.py), parameters 1e-5 absolute or proven Adam
 amplification of a near-zero gradient entry (tests/arbiter_helpers.py).
 """
+import copy
 import numpy as np
 import pytest
 import torch
@@ -231,7 +232,7 @@ def test_bcq_checkpoint_roundtrip(tmp_path):
     sd = torch.load(str(f), weights_only=True)
     assert set(sd) == set(STATE_KEYS)
     for k in sd:
-        getattr(orc, k).load_state_dict(sd[k])
+        getattr(orc, k).load_state_dict(copy.deepcopy(sd[k]))
     impl2 = make_bcq_impl(D, A, H, N, K)
     impl2.load_model(str(f))
     assert torch.equal(impl2.store.data, impl.store.data)

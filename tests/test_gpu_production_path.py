@@ -21,6 +21,7 @@ trajectories separate only where Adam amplifies a near-zero gradient entry
 (lr * g / (|g| + eps)), which the per-step test proves entry by entry.  The
 index stream and the reproduced draws themselves are exact.
 """
+import copy
 import numpy as np
 import pytest
 import torch
@@ -134,7 +135,7 @@ def test_cql_fit_production_path_per_step_proof():
         assert ring.shape[0] >= 1
         nz = _cql_noise(ws, s, B, A, N)
         for k, v in sd0.items():
-            getattr(orc, k).load_state_dict(v)
+            getattr(orc, k).load_state_dict(copy.deepcopy(v))
         m, cgrads, pgrads = _oracle_step(orc, batches[s], nz, A)
         for j, name in enumerate(names):
             assert abs(ring[-1, j] - m[name]) <= 1e-5 * max(1.0, abs(m[name])), (s, name)
@@ -193,7 +194,7 @@ def test_cql_fit_production_path_vs_oracle():
     impl = algo.impl
     orc = make_oracle(D, A, [256, 256], N, seed=0)
     for k, v in impl.get_state_dict().items():
-        getattr(orc, k).load_state_dict(v)
+        getattr(orc, k).load_state_dict(copy.deepcopy(v))
     np.random.seed(42)
     algo.fit(ds, n_steps=STEPS, n_steps_per_epoch=STEPS, save_metrics=False, verbose=False,
              show_progress=False, index_source="numpy")
@@ -246,7 +247,7 @@ def test_td3bc_fit_production_path_vs_oracle():
     std = np.asarray(algo.scaler._std, np.float64).reshape(-1)
     orc = make_td3_oracle(D, A, [256, 256], seed=0, scaler_stats=(mean, std))
     for k, v in impl.get_state_dict().items():
-        getattr(orc, k).load_state_dict(v)
+        getattr(orc, k).load_state_dict(copy.deepcopy(v))
     np.random.seed(7)
     algo.fit(ds, n_steps=STEPS, n_steps_per_epoch=STEPS, save_metrics=False, verbose=False,
              show_progress=False, index_source="numpy")

@@ -11,6 +11,7 @@ Tolerances (fp32, 1e-5 target of BASELINE.json north_star):
   gradients   max|a-b| / max|b| <= 2e-5 per tensor (two fp32 summation orders)
   parameters  |a-b| <= 1e-5 absolute (targets included)
 """
+import copy
 import numpy as np
 import pytest
 import torch
@@ -154,7 +155,7 @@ def test_td3bc_checkpoint_roundtrip(tmp_path):
     sd = torch.load(str(f), weights_only=True)
     assert set(sd) == set(td3_oracle_state(orc))
     for k in sd:
-        getattr(orc, k).load_state_dict(sd[k])
+        getattr(orc, k).load_state_dict(copy.deepcopy(sd[k]))
     impl2 = make_td3_impl(D, A, H)
     impl2.load_model(str(f))
     assert torch.equal(impl2.store.data, impl.store.data)

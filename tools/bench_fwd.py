@@ -28,7 +28,15 @@ def main():
     ap.add_argument("--bf16", action="store_true", help="d3a_q2_fwd_bf16 (bf16 kept activations)")
     ap.add_argument("--x6", action="store_true", help="d3a_q2_fwd_x6 (split-bf16 x6, fp32-accurate)")
     ap.add_argument("--hmask", action="store_true", help="x6: also write the bf16 mask image of h2")
+    ap.add_argument("--slice", action="store_true",
+                    help="x6: the production critic forward of the slice backward -- row and "
+                         "transposed mask bits, no kept h2")
+    ap.add_argument("--stamps", action="store_true",
+                    help="with D3A_X6_PROBE=16: per-phase s_memtime cycles of wave 0, averaged "
+                         "over the workgroups")
     a = ap.parse_args()
+    if a.slice:
+        a.hmask = True
     dev, C, H = "cuda", a.C, 256
     sizes = [a.n_in, H, H, a.J]
     ldx = (a.n_in + 3) // 4 * 4
@@ -69,6 +77,10 @@ def main():
     if a.hmask:
         hm = torch.zeros(C, a.rows, H // 32, device=dev, dtype=torch.int32)
         d.hmask, d.s_hmask = hm.data_ptr(), a.rows * (H // 32)
+    if a.slice:
+        hmt = torch.zeros(C, (a.rows + 31) // 32, H, device=dev, dtype=torch.int32)
+        d.hmaskT, d.s_hmaskT = hmt.data_ptr(), hmt[0].numel()
+        d.h[1] = None
     if a.aux:
         d.aux_x, d.aux_ldx, d.aux_sxb, d.aux_wdelta = xa.data_ptr(), ldx, 0, n_par
         d.aux_out, d.aux_sout, d.aux_rows = aout.data_ptr(), a.aux * a.J, a.aux
@@ -84,7 +96,8 @@ def main():
     r2 = torch.relu(r1 @ W[1].transpose(1, 2) + bb[1])
     q = r2 @ W[2].transpose(1, 2) + bb[2]
     err = ((q - out).abs().max() / q.abs().max()).item()
-    herr = ((r2[:, a.h_from:] - h[1][:, a.h_from:].float()).abs().max()).item()
+    herr = (None if a.slice else
+            ((r2[:, a.h_from:] - h[1][:, a.h_from:].float()).abs().max()).item())
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
@@ -94,8 +107,22 @@ def main():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / a.reps
     flops = 2 * C * (a.rows + a.aux) * sum(sizes[l] * sizes[l + 1] for l in range(3))
-    print(json.dumps({"kernel": entry, "hmask": a.hmask, "rows": a.rows, "aux": a.aux, "bm": a.bm, "C": C, "J": a.J,
-                      "variant": os.environ.get("D3A_FWD_PROBE", "") + ("generic" if os.environ.get("D3A_FWD_Q2") == "0" else ""),
+    stamps = None
+    if a.stamps:
+        import ctypes
+        n = 2048 * 10
+        buf = (ctypes.c_ulonglong * n)()
+        assert N.lib().d3a_x6_stamps(buf, n) == 0
+        import numpy as np
+        st = np.frombuffer(buf, dtype=np.uint64).reshape(2048, 10).astype(np.int64)
+        nwg = min(2048, (a.rows + 127) // 128 * C)
+        st = st[:nwg]
+        ph = np.diff(st[:, :9], axis=1)
+        stamps = {"phase_cycles_mean": [round(float(v), 1) for v in ph.mean(0)],
+                  "total_cycles_mean": round(float((st[:, 8] - st[:, 0]).mean()), 1)}
+    print(json.dumps({"kernel": entry, "hmask": a.hmask, "slice": a.slice, "rows": a.rows, "aux": a.aux, "bm": a.bm, "C": C, "J": a.J,
+                      "variant": os.environ.get("D3A_FWD_PROBE", "") + os.environ.get("D3A_X6_PROBE", "") + ("generic" if os.environ.get("D3A_FWD_Q2") == "0" else ""),
+                      "stamps": stamps,
                       "avg_us": round(us, 2), "tflops": round(flops / us / 1e6, 2),
                       "frac_fp32_peak": round(flops / us / 1e6 / 157.3, 4),
                       "max_rel_err_q": err, "max_abs_err_h2": herr}))
