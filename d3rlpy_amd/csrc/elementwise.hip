@@ -153,9 +153,9 @@ __host__ __device__ __forceinline__ int seg_lanes(int64_t n_partials, int64_t nu
   return n_partials >= 64 ? 16 : 1;
 }
 
-__device__ __forceinline__ double sum_partials(const float* g, int64_t n, int64_t stride,
-                                               int64_t i, int j, int L) {
-  constexpr int U = 32;
+template <int U>
+__device__ __forceinline__ double sum_partials_u(const float* g, int64_t n, int64_t stride,
+                                                 int64_t i, int j, int L) {
   double gd = 0.0;
   for (int64_t q = j; q < n; q += (int64_t)U * L) {
     float v[U];
@@ -172,6 +172,17 @@ __device__ __forceinline__ double sum_partials(const float* g, int64_t n, int64_
   }
   for (int o = L >> 1; o > 0; o >>= 1) gd += __shfl_xor(gd, o, 64);
   return gd;
+}
+
+// the partial sum of element i in index order; the batch of loads in flight is
+// sized to the partial count (8 for the critic's slice-backward row blocks: a
+// 32-load batch would issue 24 clamped duplicates per element), the same
+// order and sum for every batch size
+__device__ __forceinline__ double sum_partials(const float* g, int64_t n, int64_t stride,
+                                               int64_t i, int j, int L) {
+  if (L == 1 && n <= 8) return sum_partials_u<8>(g, n, stride, i, j, L);
+  if (L == 1 && n <= 16) return sum_partials_u<16>(g, n, stride, i, j, L);
+  return sum_partials_u<32>(g, n, stride, i, j, L);
 }
 
 // ---- Adam (torch.optim.adam._single_tensor_adam, weight_decay = 0) ---------

@@ -62,7 +62,8 @@ struct X6FwdLds {
 // the layer-1 productions after the first, bit 2 the kept-activation stores,
 // bit 3 the W1 reloads (chunk 0's registers reused); bit 4 (diagnostic build,
 // results right) records s_memtime stamps of wave 0 at the phase boundaries
-// into x6_stamps (read with d3a_x6_stamps)
+// into x6_stamps (read with d3a_x6_stamps); bit 5 the W1 split (the loaded
+// words taken as the parts)
 //
 // NP / HT: NP = 3 the exact split (fp32-accurate, kept activations fp32);
 // NP = 1, HT = __bf16 the bf16 throughput line's forward (d3a_q2_fwd_bf16's
@@ -169,12 +170,25 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     const float* xb = aux ? d.aux_x + c * d.aux_sxb : d.x + c * d.sxb;
     const int64_t ldx = aux ? d.aux_ldx : d.ldx;
     constexpr int X4 = XL / 4;
+    // plain rows of 16-byte pieces: one unconditional float4 load per piece
+    // (row and piece clamped, the padding selected to 0 after the load) --
+    // the element path below branches per element, and each branch waits for
+    // every load in flight (the W0 / W1 / b0 prefetch included)
+    const bool vec = d.xg_mode == 0 && (ldx & 3) == 0 && (reinterpret_cast<uintptr_t>(xb) & 15) == 0;
     for (int e = t; e < X_RB * X4; e += 512) {
       const int m = e / X4, k4 = (e - m * X4) * 4;
       const int r = m0 + m;
       float v[4];
+      if (vec) {
+        const int rc = min(r, rend - 1), kc = min(k4, (int)ldx - 4);
+        const float4 f = *reinterpret_cast<const float4*>(xb + (int64_t)rc * ldx + kc);
+        const float fv[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? input_at(d, xb, ldx, r, k4 + j) : 0.f;
+        for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? fv[j] : 0.f;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? input_at(d, xb, ldx, r, k4 + j) : 0.f;
+      }
       bf16x4 p[NP];
       splitn4<NP>(v, p);
 #pragma unroll
@@ -273,7 +287,13 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       bf16x8 wa[NP];
       const float v[8] = {wc[s][0].x, wc[s][0].y, wc[s][0].z, wc[s][0].w,
                           wc[s][1].x, wc[s][1].y, wc[s][1].z, wc[s][1].w};
-      splitn8<NP>(v, wa);
+      if constexpr ((PROBE & 32) != 0) {
+        // timing probe: the loaded words as the parts, no split arithmetic
+#pragma unroll
+        for (int q = 0; q < NP; ++q) wa[q] = __builtin_bit_cast(bf16x8, q == 0 ? wc[s][0] : wc[s][1]);
+      } else {
+        splitn8<NP>(v, wa);
+      }
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
         const int idx = 4 * s + tt;
@@ -484,12 +504,13 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
     return e ? atoi(e) : 0;
   }();
   if (probe && xl == 16 && d.n_out == 1) {
-    switch (probe & 31) {
+    switch (probe & 63) {
       case 1: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 1>), grid, dim3(512), 0, st, d); break;
       case 4: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 4>), grid, dim3(512), 0, st, d); break;
       case 5: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
       case 13: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 13>), grid, dim3(512), 0, st, d); break;
       case 16: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 16>), grid, dim3(512), 0, st, d); break;
+      case 32: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 32>), grid, dim3(512), 0, st, d); break;
       default: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
     }
     D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
