@@ -308,13 +308,14 @@ def conv_wgrad_splits(geom, l: int, B: int) -> int:
     """The split count d3a_conv_bwd_w fills the chip with for conv layer l of
     a B-sample backward (its kernel's choice, d3a_conv_bwd_w_splits): the
     first layer reads the uint8 frames (x_u8 set, as the backward launch sets
-    it), which selects the fp32-MFMA kernel's 32 splits -- not the split-bf16
-    kernel's count for an fp32 input."""
+    it), which selects the first-layer kernel (conv1_bwd_w_u8s4_kernel, 256
+    splits at K5's shape) -- not the split-bf16 kernel's count for an fp32
+    input."""
     ci, h, w, co, k, s, oh, ow = geom[l]
     gd = NAT.ConvDesc()
     gd.B, gd.C, gd.H, gd.W, gd.KH, gd.KW, gd.S, gd.OH, gd.OW, gd.CO = B, ci, h, w, k, k, s, oh, ow, co
     if l == 0:
-        gd.x_u8 = 1  # only its presence is read by the query
+        gd.x_u8 = 16  # only its presence and 4-byte alignment are read by the query
     S = int(NAT.lib().d3a_conv_bwd_w_splits(C.byref(gd)))
     assert S >= 1
     return S
@@ -406,6 +407,7 @@ def _conv_bwd_x(ci: int, co: int) -> bool:
 # the IQN head forward as one launch (d3a_iqn_embed_head); D3A_IQN_FUSED=0
 # keeps d3a_iqn_prior + the embed GEMM + d3a_iqn_head_fwd (A/B)
 _IQN_FUSED = os.environ.get("D3A_IQN_FUSED", "1") == "1"
+_IQN_RECOMPUTE = os.environ.get("D3A_IQN_RECOMPUTE", "1") == "1"
 
 
 class _HeadPass:
@@ -413,11 +415,17 @@ class _HeadPass:
 
     def __init__(self, impl: DiscreteCQLImpl, rows: int, dev):
         self.impl = impl
-        z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
-        self.prior = z(rows, impl._E)
-        self.phi = z(rows, impl._F)
-        self.q = z(rows, impl._action_size)
+        self.dev = dev
+        # prior / phi ([rows][E] / [rows][F]) only once a launch keeps rows:
+        # the update's backward recomputes them from tau (d3a_iqn_head_bwd_fused)
+        self.prior = self.phi = None
+        self.q = torch.zeros(rows, impl._action_size, dtype=torch.float32, device=dev)
         self.rows = rows
+
+    def _keep_bufs(self) -> None:
+        if self.phi is None:
+            z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=self.dev)  # noqa: E731
+            self.prior, self.phi = z(self.rows, self.impl._E), z(self.rows, self.impl._F)
 
     def launch(self, taus_ptr: int, h_groups: List[int], group_rows: int, K: int,
                store: ParamStore, n_keep: Optional[int] = None) -> None:
@@ -434,12 +442,15 @@ class _HeadPass:
                 d.h[g] = hp
             d.Wf, d.bf, d.q = store.ptr("q.fc.W"), store.ptr("q.fc.b"), self.q.data_ptr()
             keep = self.rows if n_keep is None else n_keep
+            if keep:
+                self._keep_bufs()
             d.prior_out = self.prior.data_ptr() if keep else None
             d.phi_out = self.phi.data_ptr() if keep else None
             d.rows, d.group_rows, d.n_keep = self.rows, group_rows, keep
             d.K, d.E, d.F, d.A = K, impl._E, impl._F, impl._action_size
             ops.call_desc("d3a_iqn_embed_head", d)
             return
+        self._keep_bufs()
         p = NAT.IqnPriorDesc()
         p.taus, p.prior, p.rows, p.E = taus_ptr, self.prior.data_ptr(), self.rows, impl._E
         ops.call_desc("d3a_iqn_prior", p)
@@ -490,7 +501,7 @@ class _Workspace:
             self.head = _HeadPass(impl, 4 * BK, dev)   # online rows [loss|lse|data|next]
             self.head_t = _HeadPass(impl, BK, dev)     # target rows
             self.dq = z(3 * BK, A)
-            self.dphi = z(3 * BK, F)
+            self.dphi = None   # dL/dphi rows: the two-launch backward only
         self.loss_b, self.cons_b = z(B), z(B)
         self.metrics = z(len(METRIC_NAMES))
         self.ring = z(1 << 16, len(METRIC_NAMES))
@@ -527,7 +538,16 @@ class _Workspace:
             # the head backward + embed weight gradient as one launch
             # (d3a_iqn_head_bwd_fused): one partial per workgroup of NB rows b
             self.fused_bwd = (_IQN_FUSED and F == 512 and E == 64 and A <= 8 and K % 32 == 0)
-            self.NB = 2
+            # the fused backward recomputes prior / phi from tau (the forward
+            # keeps nothing); D3A_IQN_RECOMPUTE=0 keeps the kept-rows path (A/B)
+            self.recompute = self.fused_bwd and _IQN_RECOMPUTE
+            if not self.recompute:
+                self.head._keep_bufs()
+            if not self.fused_bwd:
+                self.dphi = z(3 * BK, F)
+            # 4 rows b per workgroup pair (256 workgroups at B = 512, 128
+            # partials) recomputing; 2 per workgroup keeping
+            self.NB = int(os.environ.get("D3A_IQN_NB", "4" if self.recompute else "2"))
             P = (B + self.NB - 1) // self.NB
             self.grads.add("q.fc.W", (1, A, F), P if self.fused_bwd else B)
             self.grads.add("q.fc.b", (1, A), P if self.fused_bwd else B)
@@ -568,17 +588,23 @@ class _Workspace:
         l.B, l.K, l.A, l.gamma, l.alpha = B, K, A, impl._gamma, impl._alpha
         self.loss_desc = l
         hb = NAT.IqnHeadBwdDesc()
-        hb.h, hb.phi, hb.dq = self.enc.h.data_ptr(), self.head.phi.data_ptr(), self.dq.data_ptr()
+        hb.h, hb.dq = self.enc.h.data_ptr(), self.dq.data_ptr()
+        hb.phi = self.head.phi.data_ptr() if self.head.phi is not None else None
         hb.Wf = impl.store.ptr("q.fc.W")
-        hb.dphi, hb.dh = self.dphi.data_ptr(), self.dzfc.data_ptr()
+        hb.dphi = self.dphi.data_ptr() if self.dphi is not None else None
+        hb.dh = self.dzfc.data_ptr()
         hb.dWf_part = self.grads.get("q.fc.W").data_ptr()
         hb.dbf_part = self.grads.get("q.fc.b").data_ptr()
         hb.B, hb.K, hb.F, hb.A, hb.G = B, K, F, A, 3
         self.head_bwd_desc = hb
         if self.fused_bwd:
             fb = NAT.IqnHeadBwdFusedDesc()
-            fb.h, fb.phi, fb.prior = (self.enc.h.data_ptr(), self.head.phi.data_ptr(),
-                                      self.head.prior.data_ptr())
+            fb.h = self.enc.h.data_ptr()
+            if self.recompute:
+                fb.taus = self.taus.data_ptr()   # rows g B K + b K + k: the forward's rows
+                fb.We, fb.be = impl.store.ptr("q.embed.W"), impl.store.ptr("q.embed.b")
+            else:
+                fb.phi, fb.prior = self.head.phi.data_ptr(), self.head.prior.data_ptr()
             fb.dq, fb.Wf = self.dq.data_ptr(), impl.store.ptr("q.fc.W")
             fb.dh = self.dzfc.data_ptr()
             fb.dWf_part = self.grads.get("q.fc.W").data_ptr()
@@ -608,7 +634,7 @@ class _Workspace:
         """The step's longest kernel: the fused IQN head backward over the G
         gradient passes (G B K rows x F units: dphi, dh, dWf, and the embed
         weight gradient dWe on split-bf16 MFMA) -- per row 2 F (2 A + 1 + E) + F
-        flops; else (mean head, or D3A_K5_DOMINANT=conv1) the first conv GEMM
+        flops, + 2 F E recomputing phi; else (mean head, or D3A_K5_DOMINANT=conv1) the first conv GEMM
         over [obs; next_obs] (2B x 400 positions x 32 filters x 256 taps)."""
         impl = self.impl
         if (not self.mean and self.fused_bwd
@@ -619,6 +645,12 @@ class _Workspace:
 
             def launch_hb():
                 ops.call_desc("d3a_iqn_head_bwd_fused", fb)
+            if self.recompute:
+                # + the phi recompute (2 F E per row: the forward's embed product)
+                return launch_hb, rows * (2 * F * (2 * A + 1 + 2 * E) + F), (
+                    f"d3a_iqn_head_bwd_fused (phi recomputed from tau and dWe on split-bf16 "
+                    f"x6 MFMA, fp32 head backward): {rows} rows x {F} units, E {E}, A {A}; "
+                    f"flops include the recompute")
             return launch_hb, rows * (2 * F * (2 * A + 1 + E) + F), (
                 f"d3a_iqn_head_bwd_fused (dWe on split-bf16 x6 MFMA, fp32 head backward): "
                 f"{rows} rows x {F} units, E {E}, A {A}")
@@ -698,9 +730,10 @@ class _Workspace:
                              F, B * F, 1, B, F, A, mask=h_obs, ldm=F, smb=B * F)
         else:
             # IQN heads: online rows [loss | lse | data | next], target rows
-            # (the backward reads prior / phi of the three gradient passes only)
+            # (kept prior / phi of the three gradient passes only when the
+            # backward does not recompute them)
             self.head.launch(self.taus.data_ptr(), [h_obs, h_obs, h_obs, h_next], BK, K, st,
-                             n_keep=3 * BK)
+                             n_keep=0 if self.recompute else 3 * BK)
             self.head_t.launch(self.taus.data_ptr() + 4 * 4 * BK, [self.enc_t.h.data_ptr()], BK,
                                K, tg, n_keep=0)
             ops.call_desc("d3a_iqn_loss", self.loss_desc)

@@ -674,6 +674,203 @@ __global__ __launch_bounds__(512) void conv_bwd_w_x6_kernel(d3a_conv_desc d) {
   }
 }
 
+// The uint8 stride-4, 8-wide first layer (Nature DQN conv1) weight gradient:
+// the generic kernels above gather one byte per lane and row, 52 MB of single-
+// byte loads at K5's shape (122 us).  Here the GEMM's K (rows) is walked in
+// runs of 4 consecutive output columns ox = 4 q .. 4 q + 3 of one (b, oy):
+// for a tap (c, kh, kw = 4 j + dx) their pixels x[b][c][4 oy + kh][16 q + 4 j
+// + 4 u + dx], u = 0..3, are byte dx of the 4 dwords at 16 q + 4 j.  The 4
+// lanes of a quad (dx = 0..3, one (c, kh, j)) load one dword each (u = dx)
+// and transpose the 4 x 4 bytes with two DPP exchanges + v_perm, so lane dx
+// ends with its 4 pixels.  A 16-row MFMA step is four runs; lane (li, lg)
+// holds runs 2 lg, 2 lg + 1 (its 8 k slots): B = the pixels of k = 32 t + li
+// (k-tile t; kout order c KH KW + kh KW + kw, 4 (c, kh) pairs x 8 kw per
+// tile), exact in one bf16 part; A = dy[row][co0 + li] in three parts: three
+// products, the pixel scale applied to the sum (as conv_bwd_w_x6_kernel).  A
+// wave keeps all NKT k-tiles (Kc = 32 NKT <= 256): dy is read once; the
+// k-tiles' loads are double-buffered in halves.  Waves take K-steps w, w + 8,
+// .. of their workgroup's chunk; the 8 waves meet in a fixed-order LDS tree,
+// the split's partial goes to dW[split].
+template <int NKT>
+__global__ __launch_bounds__(512) void conv1_bwd_w_u8s4_kernel(d3a_conv_desc d) {
+  using namespace x6;
+  constexpr int NW = 8, HK = NKT / 2;  // k-tiles per half
+  __shared__ float red[4 * HK * 16 * 64];
+  __shared__ double rsum[NW * 32];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 31, lg = lane >> 5;
+  const int QW = d.OW / 4;
+  const int64_t NR = (int64_t)d.B * d.OH * QW;  // runs
+  const int64_t NKS = (NR + 3) / 4;             // 16-row steps
+  const int co0 = blockIdx.y * 32;
+  const int s = blockIdx.z;
+  const int64_t chunk = (NKS + d.splits - 1) / d.splits;
+  const int64_t kb = s * chunk;
+  const int64_t ke = kb + chunk < NKS ? kb + chunk : NKS;
+  const bool do_bias = d.db != nullptr;
+  const int64_t plane = (int64_t)d.H * d.W;
+  // this lane's tap in k-tile t: pair 4 t + (li >> 3) = (c, kh), kw = li & 7
+  // = 4 j + dx; it loads dword u = dx of the tap's 16 bytes
+  const int dx = li & 3;
+  int toff[NKT];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    const int pr = 4 * t + (li >> 3), c = pr / d.KH, kh = pr - c * d.KH;
+    toff[t] = (int)(c * plane + (int64_t)kh * d.W) + 4 * ((li & 7) >> 2) + 4 * dx;
+  }
+  // quad byte transpose selectors (own dword = bytes 0-3, the partner's 4-7)
+  const uint32_t sel1 = (dx & 1) ? 0x03070105u : 0x06020400u;  // with lane ^ 1
+  const uint32_t sel2 = (dx & 2) ? 0x03020706u : 0x05040100u;  // with lane ^ 2
+
+  f32x16 acc[NKT];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  double bs = 0.0;
+
+  // a step's two runs for this lane half: image base offsets and dy rows
+  struct Runs {
+    int64_t xo[2], row[2];
+    bool ok[2];
+  };
+  auto runs_of = [&](int64_t ks) {
+    Runs R;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t rho = 4 * ks + 2 * lg + h;
+      R.ok[h] = rho < NR;
+      const int64_t rr = R.ok[h] ? rho : 0;
+      const int64_t line = rr / QW;
+      const int q = (int)(rr - line * QW);
+      const int64_t b = line / d.OH;
+      const int oy = (int)(line - b * d.OH);
+      R.xo[h] = b * d.C * plane + (int64_t)(4 * oy) * d.W + 16 * q;
+      R.row[h] = line * d.OW + 4 * q;
+    }
+    return R;
+  };
+  uint32_t xa[HK][2], xb[HK][2];  // [k-tile of the half][run]
+  float dyv[8];
+  auto load_half = [&](const Runs& R, int half, uint32_t (*xv)[2]) {
+#pragma unroll
+    for (int t = 0; t < HK; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        xv[t][h] = R.ok[h] ? *reinterpret_cast<const uint32_t*>(d.x_u8 + R.xo[h] + toff[half * HK + t])
+                           : 0u;
+  };
+  auto load_dy = [&](const Runs& R) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dyv[4 * h + u] = R.ok[h] ? d.dy[(R.row[h] + u) * d.CO + co0 + li] : 0.f;
+  };
+  auto mul_half = [&](const bf16x8* a, uint32_t (*xv)[2], int half) {
+#pragma unroll
+    for (int t = 0; t < HK; ++t) {
+      bf16x8 b;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        // 4 x 4 byte transpose across the quad: byte u of the result = dword u's byte dx
+        const uint32_t v = xv[t][h];
+        const uint32_t p1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+        const uint32_t t1 = __builtin_amdgcn_perm(p1, v, sel1);
+        const uint32_t p2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)t1, 0x4E, 0xF, 0xF, false);
+        const uint32_t px = __builtin_amdgcn_perm(p2, t1, sel2);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[4 * h + u] = (__bf16)(float)((px >> (8 * u)) & 0xffu);
+      }
+      f32x16& c = acc[half * HK + t];
+      c = mfma16(a[2], b, c);
+      c = mfma16(a[1], b, c);
+      c = mfma16(a[0], b, c);
+    }
+  };
+
+  int64_t ks = kb + w;
+  if (ks < ke) {
+    const Runs R = runs_of(ks);
+    load_dy(R);
+    load_half(R, 0, xa);
+    load_half(R, 1, xb);
+  }
+  for (; ks < ke; ks += NW) {
+    const bool more = ks + NW < ke;
+    const Runs Rn = runs_of(more ? ks + NW : ks);
+    bf16x8 a[3];
+    split8(dyv, a);
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bs += (double)dyv[i];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mul_half(a, xa, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      load_dy(Rn);
+      load_half(Rn, 0, xa);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mul_half(a, xb, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) load_half(Rn, 1, xb);
+  }
+
+  // fixed-order tree over the 8 waves per half of the k-tiles: (w, w + 4),
+  // then (w, w + 2), then (0, 1)
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int m = 4; m >= 1; m >>= 1) {
+      if (w >= m && w < 2 * m) {
+#pragma unroll
+        for (int t = 0; t < HK; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) red[(((w - m) * HK + t) * 16 + r) * 64 + lane] = acc[half * HK + t][r];
+      }
+      __syncthreads();
+      if (w < m) {
+#pragma unroll
+        for (int t = 0; t < HK; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[half * HK + t][r] += red[((w * HK + t) * 16 + r) * 64 + lane];
+      }
+      __syncthreads();
+    }
+  }
+  if (do_bias) {
+    bs += __shfl_xor(bs, 32, 64);
+    if (lg == 0) rsum[w * 32 + li] = bs;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  const int Kc = 32 * NKT;
+  float* dW = d.dW + (int64_t)s * d.CO * Kc;
+#pragma unroll
+  for (int t = 0; t < NKT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * lg;
+      dW[(int64_t)co * Kc + 32 * t + li] = __fdiv_rn(acc[t][r], 255.f);
+    }
+  if (do_bias && lg == 0) {
+    double tot = 0.0;
+    for (int v = 0; v < NW; ++v) tot += rsum[v * 32 + li];
+    d.db[(int64_t)s * d.CO + co0 + li] = (float)tot;
+  }
+}
+
+// the first-layer fast path's geometry: uint8 input, stride 4, 8-wide
+// kernel (two 4-byte column groups), whole 4-column runs, Kc = C KH 8 a
+// multiple of 64 up to 256
+inline bool conv1_u8s4_ok(const d3a_conv_desc* d) {
+  const int64_t Kc = (int64_t)d->C * d->KH * d->KW;
+  return d->x_u8 != nullptr && d->S == 4 && d->KW == 8 && d->OW % 4 == 0 && d->W % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(d->x_u8) & 3) == 0 && Kc % 64 == 0 && Kc <= 256 &&
+         d->CO % 32 == 0 && (int64_t)d->C * d->H * d->W < (int64_t)1 << 31;
+}
+
 // Input gradient on the bf16 matrix cores at fp32 accuracy: dx[b][y][x][c] =
 // [x > 0] sum over the output positions (oy, ox) whose window covers (y, x) of
 // sum_co dy[b][oy][ox][co] W[co][c][y - S oy][x - S ox] -- im2col's transpose
@@ -1015,6 +1212,16 @@ bool conv_bwd_x6() {
   }();
   return on;
 }
+
+// the first-layer weight-gradient kernel (conv1_bwd_w_u8s4_kernel);
+// D3A_CONV1_U8S4=0 keeps the generic fp32-MFMA kernel (A/B)
+bool conv1_u8s4() {
+  static const bool on = [] {
+    const char* e = getenv("D3A_CONV1_U8S4");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
 // d3a_conv_bwd_x's products on fp32 MFMA (packed weights) unless
 // D3A_CONV_BWD_X_F32=0 (split-bf16: 64 / 59 us against 69 / 71 on K5's layers,
 // but with the split-bf16 weight gradients of the same layers the B = 512
@@ -1038,6 +1245,14 @@ extern "C" int32_t d3a_conv_bwd_w_splits(const d3a_conv_desc* d) {
   if (d == nullptr) return -1;
   const int64_t M = (int64_t)d->B * d->OH * d->OW;
   const int64_t Kc = (int64_t)d->C * d->KH * d->KW;
+  if (conv1_u8s4_ok(d) && conv1_u8s4()) {
+    // the first-layer kernel: ~256 workgroups over the CO / 32 column blocks,
+    // >= 32 16-row steps (4 a wave) each
+    const int64_t steps = (M / 4 + 3) / 4;
+    int64_t s = 256 / (d->CO / 32);
+    if (s > steps / 32) s = steps / 32;
+    return (int32_t)(s > 1 ? s : 1);
+  }
   if (d->x_u8 || !conv_bwd_x6()) {
     // the fp32-MFMA kernel: >= 32 rows a split, at most 32 splits
     const int64_t s = M / 32 < 32 ? M / 32 : 32;
@@ -1059,6 +1274,17 @@ extern "C" int d3a_conv_bwd_w(const d3a_conv_desc* d, void* stream) {
   D3A_CHECK_ARG(d->splits >= 1 && d->splits < 65536, "d3a_conv_bwd_w: bad splits");
   const int64_t Kc = (int64_t)d->C * d->KH * d->KW;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (conv1_u8s4_ok(d) && conv1_u8s4()) {
+    const dim3 grid(1u, (unsigned)(d->CO / 32), (unsigned)d->splits);
+    switch (Kc / 32) {
+      case 2: hipLaunchKernelGGL(conv1_bwd_w_u8s4_kernel<2>, grid, dim3(512), 0, st, *d); break;
+      case 4: hipLaunchKernelGGL(conv1_bwd_w_u8s4_kernel<4>, grid, dim3(512), 0, st, *d); break;
+      case 6: hipLaunchKernelGGL(conv1_bwd_w_u8s4_kernel<6>, grid, dim3(512), 0, st, *d); break;
+      default: hipLaunchKernelGGL(conv1_bwd_w_u8s4_kernel<8>, grid, dim3(512), 0, st, *d); break;
+    }
+    D3A_LAUNCH_CHECK("d3a_conv_bwd_w");
+    return 0;
+  }
   if (conv_bwd_x6() && !d->x_u8) {
     // split-bf16 weight gradient: 32 (co) x 64 (k) per wave, 8 waves a workgroup
     // (fp32 input; the uint8 layer stays on the fp32-MFMA kernel: both are bound

@@ -18,6 +18,7 @@
 // uses the reference's NCHW order, so the last conv output is transposed
 // (d3a_iqn_transpose) before the fc and its gradient transposed back.
 #include "common.hpp"
+#include "iqn_cos.hpp"
 #include "../../include/d3rlpy_amd.h"
 
 namespace d3a {
@@ -107,14 +108,15 @@ __global__ __launch_bounds__(256) void transpose_kernel(d3a_transpose_desc d) {
   d.dst[i] = (d.mask && !(d.mask[i] > 0.f)) ? 0.f : v;
 }
 
-// prior[r][i] = cos(pi * (i + 1) * tau[r])   (fp32 ops in torch's order)
+// prior[r][i] = cos(pi * (i + 1) * tau[r])   (fp32 ops in torch's order; the
+// cosine is iqn_cos, iqn_cos.hpp, shared with the fused head kernels)
 __global__ __launch_bounds__(256) void iqn_prior_kernel(d3a_iqn_prior_desc d) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= d.rows * d.E) return;
   const int64_t r = i / d.E;
   const int e = (int)(i - r * d.E);
   const float ps = __fmul_rn(3.14159265358979323846f, (float)(e + 1));
-  d.prior[i] = cosf(__fmul_rn(ps, d.taus[r]));
+  d.prior[i] = iqn_cos(__fmul_rn(ps, d.taus[r]));
 }
 
 // q[r][a] = (h[b(r)] * phi[r]) . Wf[a] + bf[a]; one wave per row.

@@ -49,6 +49,9 @@ class Acts:
     # first row of the mask image the last forward wrote (None: not written;
     # the backward then builds the mask from h2)
     hmask_from: Optional[int] = None
+    # one past the last row it wrote (the forward's r1): a backward uses the
+    # image only for rows inside [hmask_from, hmask_to)
+    hmask_to: Optional[int] = None
     # the same mask transposed ([C][ceil(R / 32)][256] int32, d3a_mlp_fwd_desc.
     # hmaskT), written with hmask where the forward's rows start on a 32-row
     # group; read by the slice backward (d3a_q2_bwd_desc.m2t)
@@ -81,7 +84,8 @@ class Acts:
         kept (no_last_h)."""
         out = [(h[c, r0:r1] > 0) for h in self.h]
         if self.no_last_h:
-            assert self.hmask is not None and self.hmask_from is not None and self.hmask_from <= r0
+            assert (self.hmask is not None and self.hmask_from is not None
+                    and self.hmask_from <= r0 and r1 <= self.hmask_to)
             w = self.hmask[c, r0:r1].to(torch.int64)
             bits = (w.unsqueeze(-1) >> torch.arange(32, device=w.device)) & 1
             out[-1] = bits.reshape(r1 - r0, -1).bool()
@@ -258,7 +262,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     r1 = R if r1 is None else r1
     n = r1 - r0
     if acts.hmask is not None:
-        acts.hmask_from = None  # set below where this forward writes the mask image
+        acts.hmask_from = acts.hmask_to = None  # set below where this forward writes the mask image
         acts.hmaskT_from = None
     if n <= 0:
         return False
@@ -321,7 +325,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         if acts.hmask is not None:
             if (entry == "d3a_q2_fwd_x6" and keep_h and members is None and sizes[-1] == 1):
                 d.hmask, d.s_hmask = acts.hmask.data_ptr(), R * (sizes[-2] // 32)
-                acts.hmask_from = d.h_from
+                acts.hmask_from, acts.hmask_to = d.h_from, r1
                 if acts.hmaskT is not None and r0 % 32 == 0:
                     d.hmaskT, d.s_hmaskT = acts.hmaskT.data_ptr(), acts.hmaskT[0].numel()
                     acts.hmaskT_from = d.h_from
@@ -498,9 +502,10 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
             # the slice kernel: row + transposed mask bits of the forward, b2,
             # no h2 (the space's partials are laid out for it)
             if not (acts.hmaskT_from is not None and acts.hmaskT_from <= r0 and r0 % 32 == 0
-                    and acts.hmask_from is not None and acts.hmask_from <= r0):
+                    and acts.hmask_from is not None and acts.hmask_from <= r0
+                    and r0 + n <= acts.hmask_to):
                 raise RuntimeError("slice backward: the forward did not write the mask bits "
-                                   f"of rows >= {r0}")
+                                   f"of rows [{r0}, {r0 + n})")
             d.h2 = None
             d.m2, d.sm2 = acts.hmask.data_ptr() + 4 * r0 * (H // 32), R * (H // 32)
             d.m2t, d.sm2t = (acts.hmaskT.data_ptr() + 4 * (r0 // 32) * H, acts.hmaskT[0].numel())
@@ -520,7 +525,7 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         if esz == 4 and (ops.CRITIC_GEMM == "x6" or ops.CRITIC_PRECISION == "bf16"):
             entry = "d3a_q2_bwd_x6"  # fp32-accurate split-bf16 (mask-factored)
             if (not bs.slice and acts.hmask is not None and acts.hmask_from is not None
-                    and acts.hmask_from <= r0 and _MASK_IMAGE):
+                    and acts.hmask_from <= r0 and r0 + n <= acts.hmask_to and _MASK_IMAGE):
                 # the forward's mask image of h2 (same rows as h1 / h2)
                 d.m2, d.sm2 = acts.hmask.data_ptr() + 4 * r0 * (H // 32), R * (H // 32)
         ops.call_desc(entry, d)

@@ -11,6 +11,7 @@ import contextlib
 import ctypes as C
 import gc
 import os
+import warnings
 from typing import Optional, Sequence
 
 import torch
@@ -303,15 +304,27 @@ SBF16_W = os.environ.get("D3A_SBF16_W", "1") == "1"  # also the weight-gradient 
 # the mask-factored split-bf16 d3a_q2_bwd_x6, whose non-mask operands keep
 # three parts) or "bf16h" (round 3's line: d3a_q2_fwd_bf16 / d3a_q2_bwd_bf16,
 # every operand one bf16 part, bf16 kept activations).  Read when an Impl
-# builds its pipeline workspace and at each launch.
+# builds its pipeline workspace and at each launch.  NOTE: until round 4
+# "bf16" named what is now "bf16h"; round-3 bf16 bench lines correspond to
+# "bf16h" and are not comparable with "bf16" lines (bench.py tags each line
+# with its kernel pair).
 CRITIC_PRECISION = os.environ.get("D3A_CRITIC_PRECISION", "fp32")
+_BF16_RENAMED = ("critic precision 'bf16' selects the x1 forward + the split-bf16 x6 "
+                 "backward with fp32 kept activations since round 4; round 3's all-bf16 "
+                 "line (d3a_q2_fwd_bf16 / d3a_q2_bwd_bf16) is now 'bf16h'")
 
 
 def set_critic_precision(p: str) -> None:
     global CRITIC_PRECISION
     if p not in ("fp32", "bf16", "bf16h"):
         raise ValueError(f"critic precision must be fp32, bf16 or bf16h, got {p!r}")
+    if p == "bf16":
+        warnings.warn(_BF16_RENAMED, stacklevel=2)
     CRITIC_PRECISION = p
+
+
+if CRITIC_PRECISION == "bf16":
+    warnings.warn(_BF16_RENAMED + " (D3A_CRITIC_PRECISION)", stacklevel=1)
 
 
 # GEMM arithmetic of the [n_in <= 48, 256, 256, 1] critic passes at fp32

@@ -1146,6 +1146,10 @@ typedef struct d3a_iqn_head_bwd_fused_desc {
   const float* h; const float* phi; const float* prior; const float* dq; const float* Wf;
   float* dh; float* dWf_part; float* dbf_part; float* dWe_part; float* dbe_part;
   int32_t B, K, F, E, A, G, NB;
+  /* recompute mode (taus set; phi / prior unused, may be null): the backward
+   * rebuilds prior and phi = relu(We prior + be) of its rows from tau (row r's
+   * tau at taus[r], the forward's rows) with the forward's ops; F 256 or 512 */
+  const float* taus; const float* We; const float* be;
 } d3a_iqn_head_bwd_fused_desc;
 int d3a_iqn_head_bwd_fused(const d3a_iqn_head_bwd_fused_desc* d, void* stream);
 

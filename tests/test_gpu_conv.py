@@ -29,10 +29,13 @@ def _rel(a, b):
     return float((a - b).abs().max() / max(1e-30, float(b.abs().max())))
 
 
-# (B, C, H, W, CO, K, S, u8): the three Nature-DQN layers, ragged row counts
+# (B, C, H, W, CO, K, S, u8): the three Nature-DQN layers (conv1 also at 16
+# frames: several 16-row steps a wave in conv1_bwd_w_u8s4_kernel; and C = 2,
+# CO = 64: Kc = 128, two column blocks), ragged row counts
 # (B*OH*OW not a multiple of 128), the unaligned uint8 path (S = 2), K*K*C not
 # a multiple of 32 (C = 4, K = 3)
-CASES = [(3, 4, 84, 84, 32, 8, 4, True), (5, 32, 20, 20, 64, 4, 2, False),
+CASES = [(3, 4, 84, 84, 32, 8, 4, True), (16, 4, 84, 84, 32, 8, 4, True),
+         (2, 2, 36, 84, 64, 8, 4, True), (5, 32, 20, 20, 64, 4, 2, False),
          (7, 64, 9, 9, 64, 3, 1, False), (2, 4, 18, 18, 32, 4, 2, True),
          (3, 4, 11, 13, 64, 3, 1, False), (1, 8, 9, 9, 32, 5, 2, False)]
 

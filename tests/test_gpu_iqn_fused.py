@@ -143,3 +143,103 @@ def test_iqn_head_bwd_fused_matches_two_launches(B, K, NB):
     e_b = rel(dbe1.double().sum(0), dbe64)
     print(f"fused IQN head backward: dWe {e_w:.1e} dbe {e_b:.1e} vs fp64")
     assert e_w < 1e-5 and e_b < 1e-6, (e_w, e_b)
+
+
+@pytest.mark.parametrize("B,K,F,A,NB", [(512, 64, 512, 4, 4), (37, 32, 512, 7, 3),
+                                        (16, 96, 256, 1, 1), (9, 64, 256, 5, 4)])
+def test_iqn_head_bwd_recompute_matches_kept_rows(B, K, F, A, NB):
+    """d3a_iqn_head_bwd_fused in recompute mode (taus / We / be: prior and phi
+    rebuilt from tau in the backward, the forward keeping nothing) against the
+    same backward fed the rows d3a_iqn_embed_head kept, and against fp64.
+    Bars: dh / dWf / dbf / dbe within 1e-6 (max-normalised; the per-unit sums
+    meet across two lane halves instead of one chain), dWe within 1e-5 of fp64
+    (split-bf16 product of dphi and the prior)."""
+    dev = torch.device("cuda")
+    G, E = 3, 64
+    rows, _, taus, We, be, Wf, bf, hs = _case(B, K, G, F, A, 3 * B + K + F + A, dev)
+    h = hs[0]
+    gen = torch.Generator().manual_seed(B + K)
+    dq = (torch.randn(rows, A, generator=gen) * 1e-3).to(dev)
+    # forward keeping every row (prior / phi for the kept-rows backward)
+    q = torch.zeros(rows, A, device=dev)
+    prior = torch.zeros(rows, E, device=dev)
+    phi = torch.zeros(rows, F, device=dev)
+    d = N.IqnEmbedHeadDesc()
+    d.taus, d.We, d.be = taus.data_ptr(), We.data_ptr(), be.data_ptr()
+    for g in range(G):
+        d.h[g] = h.data_ptr()
+    d.Wf, d.bf, d.q = Wf.data_ptr(), bf.data_ptr(), q.data_ptr()
+    d.prior_out, d.phi_out = prior.data_ptr(), phi.data_ptr()
+    d.rows, d.group_rows, d.n_keep = rows, B * K, rows
+    d.K, d.E, d.F, d.A = K, E, F, A
+    ops.call_desc("d3a_iqn_embed_head", d)
+    P = (B + NB - 1) // NB
+
+    def run(recompute):
+        out = dict(dh=torch.full((B, F), float("nan"), device=dev),
+                   dWf=torch.full((P, A, F), float("nan"), device=dev),
+                   dbf=torch.full((P, A), float("nan"), device=dev),
+                   dWe=torch.full((P, F, E), float("nan"), device=dev),
+                   dbe=torch.full((P, F), float("nan"), device=dev))
+        fb = N.IqnHeadBwdFusedDesc()
+        fb.h, fb.dq, fb.Wf = h.data_ptr(), dq.data_ptr(), Wf.data_ptr()
+        if recompute:
+            fb.taus, fb.We, fb.be = taus.data_ptr(), We.data_ptr(), be.data_ptr()
+        else:
+            fb.phi, fb.prior = phi.data_ptr(), prior.data_ptr()
+        fb.dh, fb.dWf_part, fb.dbf_part = out["dh"].data_ptr(), out["dWf"].data_ptr(), out["dbf"].data_ptr()
+        fb.dWe_part, fb.dbe_part = out["dWe"].data_ptr(), out["dbe"].data_ptr()
+        fb.B, fb.K, fb.F, fb.E, fb.A, fb.G, fb.NB = B, K, F, E, A, G, NB
+        ops.call_desc("d3a_iqn_head_bwd_fused", fb)
+        torch.cuda.synchronize()
+        return out
+
+    rc = run(True)
+    for k, v in rc.items():
+        assert not torch.isnan(v).any(), k
+    rel = lambda a, b: float((a.double() - b.double()).abs().max() / b.double().abs().max())  # noqa: E731
+    # fp64 from the kept rows (the forward's phi / prior)
+    hrow = torch.cat([h.double().repeat_interleave(K, 0)] * G)
+    dprod = dq.double() @ Wf.double()
+    dphi = dprod * hrow * (phi.double() > 0)
+    dh64 = (dprod * phi.double()).view(G, B, K, F).sum((0, 2)) * (h.double() > 0)
+    dWf64 = dq.double().t() @ (hrow * phi.double())
+    errs = dict(dh=rel(rc["dh"], dh64), dWf=rel(rc["dWf"].sum(0), dWf64),
+                dbf=rel(rc["dbf"].sum(0), dq.double().sum(0)),
+                dWe=rel(rc["dWe"].sum(0), dphi.t() @ prior.double()),
+                dbe=rel(rc["dbe"].sum(0), dphi.sum(0)))
+    print("recompute backward vs fp64:", {k: f"{v:.1e}" for k, v in errs.items()})
+    assert errs["dh"] < 1e-6 and errs["dWf"] < 1e-6 and errs["dbf"] < 1e-6, errs
+    assert errs["dWe"] < 1e-5 and errs["dbe"] < 1e-6, errs
+    if F == 512:
+        kept = run(False)
+        for k in rc:
+            e = rel(rc[k].sum(0) if k != "dh" else rc[k], kept[k].sum(0) if k != "dh" else kept[k])
+            assert e < 2e-6, (k, e)
+    # run to run bit-identical
+    rc2 = run(True)
+    for k in rc:
+        assert torch.equal(rc[k], rc2[k]), k
+
+
+def test_iqn_prior_cos_faithful_on_gpu():
+    """d3a_iqn_prior's cosine (iqn_cos, shared by the fused head kernels) on
+    the device: within 1 ulp of cos in fp64 over the prior's arguments (the
+    host check of the same header: tests/test_iqn_cos.py)."""
+    dev = torch.device("cuda")
+    E, rows = 64, 1 << 15
+    taus = torch.rand(rows, generator=torch.Generator().manual_seed(5)).to(dev)
+    taus[:4] = torch.tensor([0.0, 0.5, 0.999999, 0.25])
+    prior = torch.zeros(rows, E, device=dev)
+    p = N.IqnPriorDesc()
+    p.taus, p.prior, p.rows, p.E = taus.data_ptr(), prior.data_ptr(), rows, E
+    ops.call_desc("d3a_iqn_prior", p)
+    torch.cuda.synchronize()
+    ps = (torch.tensor(np.pi, dtype=torch.float32) * torch.arange(1, E + 1, dtype=torch.float32)).to(dev)
+    x = ps.view(1, E) * taus.view(rows, 1)          # fp32 products, as the kernel
+    ref = torch.cos(x.double())
+    rf = ref.float()
+    ulp = (torch.nextafter(rf.abs(), torch.full_like(rf, float("inf"))) - rf.abs()).double()
+    err = float(((prior.double() - ref).abs() / ulp).max())
+    print(f"iqn prior cos: max {err:.3f} ulp")
+    assert err < 1.0, err

@@ -113,7 +113,7 @@ def test_round4_entry_points_validate_and_size_without_a_gpu():
 
     u8 = conv(512, 4, 84, 84, 32, 8, 4)
     u8.x_u8 = 16
-    assert lib.d3a_conv_bwd_w_splits(ctypes.byref(u8)) == 32
+    assert lib.d3a_conv_bwd_w_splits(ctypes.byref(u8)) == 256
     l2, l3 = conv(512, 32, 20, 20, 64, 4, 2), conv(512, 64, 9, 9, 64, 3, 1)
     l2.x_f32 = l3.x_f32 = 16
     assert lib.d3a_conv_bwd_w_splits(ctypes.byref(l2)) == 32
@@ -135,11 +135,11 @@ def test_round4_entry_points_validate_and_size_without_a_gpu():
 
 def test_dcql_workspace_sizes_the_uint8_conv_like_its_launch():
     """the K5 workspace's partial count for the first (uint8) conv
-    is the one d3a_conv_bwd_w uses for it (x_u8 set: 32 splits), not the
-    split-bf16 count of an fp32 input of that shape."""
+    is the one d3a_conv_bwd_w uses for it (x_u8 set: the first-layer kernel's
+    256 splits), not the split-bf16 count of an fp32 input of that shape."""
     from d3rlpy_amd.algos.discrete_cql_impl import _geometry, conv_wgrad_splits
     geom = _geometry((4, 84, 84))
-    assert conv_wgrad_splits(geom, 0, 512) == 32
+    assert conv_wgrad_splits(geom, 0, 512) == 256
     assert conv_wgrad_splits(geom, 1, 512) == 32
     assert conv_wgrad_splits(geom, 2, 512) == 29
 
