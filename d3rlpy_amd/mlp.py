@@ -148,6 +148,18 @@ def x6_narrow_shape(net: EnsembleMLP) -> bool:
             and s[0] <= 48)
 
 
+def x6_deep_shape(net: EnsembleMLP) -> bool:
+    """>= 3 hidden layers, all 256 wide (the CQL reproduction critic, [obs +
+    act, 256, 256, 256, 1]: reproductions/offline/cql.py:21-37): under
+    CRITIC_GEMM "x6" its large backward GEMMs (>= 128 wide both ways) run on
+    d3a_gemm_sbf16 with six-product split-bf16 operands (fp32-accurate)."""
+    return net.n_layers >= 4 and all(h == 256 for h in net.sizes[1:-1])
+
+
+# D3A_X6_DEEP=0 keeps the deep critics' backward on the fp32 GEMMs (A/B)
+_X6_DEEP = os.environ.get("D3A_X6_DEEP", "1") == "1"
+
+
 def x6_wide_shape(net: EnsembleMLP) -> bool:
     """[n_in <= 64, 256, 256, 1 < n_out <= 256] (not a narrow shape):
     d3a_mlp_fwd_x6's shape."""
@@ -580,13 +592,18 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         return
     ld_cur = bs.dz[0].shape[2]
     scur = bs.rows * ld_cur
+    # deep 256-wide critics under CRITIC_GEMM "x6": the 256 x 256 layers'
+    # weight and input gradients on the split-bf16 GEMM (six products); the
+    # head's dz then comes from d3a_head1_bwd (agen is an fp32-GEMM feature)
+    t6 = 6 if (ops.CRITIC_GEMM == "x6" and _X6_DEEP and x6_deep_shape(net)
+               and n * C >= 8192) else 0
     # large critic backward: the head's masked input gradient is generated
     # inside the trunk's two GEMMs (d3a_gemm_desc.agen) instead of written by
     # d3a_head1_bwd and read back; the weight-gradient GEMM also writes the
     # head's weight / bias gradient partials
     agen = None
     if out_dim == 1 and q_min is None and weight_grads and _HEAD_GEN and not ops.SBF16_TERMS \
-            and n * C >= _HEAD_GEN_MIN_ROWS:
+            and not t6 and n * C >= _HEAD_GEN_MIN_ROWS:
         agen = N.Head1BwdDesc()
         agen.g, agen.sgb = dout, sdout_b
         if g_scale is not None:
@@ -631,7 +648,7 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
     # ---- trunk layers L-2 .. 0
     # first layer's weight gradients from the second layer's dX epilogue
     ew = (bs.l0_tiles is not None and weight_grads and dx is None and n == bs.rows
-          and not ops.SBF16_TERMS)
+          and not ops.SBF16_TERMS and not t6)
     for l in range(L - 2, -1, -1):
         Hout = sizes[l + 1]
         Hin = sizes[l]
@@ -648,17 +665,17 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
             ops.gemm_pair(
                 lambda: ops.linear_bwd_w(dz.data_ptr(), ld_cur, scur, hin, ld_h, sh,
                                          gW.data_ptr(), C, n, Hin, Hout, S, db=gb.data_ptr(),
-                                         agen=ag),
+                                         agen=ag, sbf16=t6),
                 lambda: ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(l, store),
                                          nxt.data_ptr(), ld_cur, scur, C, n, Hin, Hout,
-                                         mask=hin, ldm=ld_h, smb=sh, agen=ag))
+                                         mask=hin, ldm=ld_h, smb=sh, agen=ag, sbf16=t6))
             cur = nxt
             continue
         if weight_grads:
             gW, gb = gs.get(net.wname(l)), gs.get(net.bname(l))
             S_l = bs.l0_tiles if (l == 0 and bs.l0_tiles) else S
             ops.linear_bwd_w(dz.data_ptr(), ld_cur, scur, hin, ld_h, sh, gW.data_ptr(), C, n, Hin,
-                             Hout, S_l, db=gb.data_ptr(), agen=ag)
+                             Hout, S_l, db=gb.data_ptr(), agen=ag, sbf16=t6)
         if l == 1 and ew:
             x0, ldx0, sx0 = h_ptr(0)
             wn = N.GemmWnext()
@@ -671,7 +688,7 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         if l > 0:
             nxt = bs.dz[1] if cur is bs.dz[0] else bs.dz[0]
             ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(l, store), nxt.data_ptr(), ld_cur,
-                             scur, C, n, Hin, Hout, mask=hin, ldm=ld_h, smb=sh, agen=ag)
+                             scur, C, n, Hin, Hout, mask=hin, ldm=ld_h, smb=sh, agen=ag, sbf16=t6)
             cur = nxt
         elif dx is not None:
             ops.linear_bwd_x(dz.data_ptr(), ld_cur, scur, net.W(0, store), dx.data_ptr(), Hin,
