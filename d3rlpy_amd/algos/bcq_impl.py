@@ -25,6 +25,7 @@ fused MLP forward (d3a_mlp_fwd, MFMA quantile head).
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional, Sequence
 
 import numpy as np
@@ -38,6 +39,10 @@ from ..nets import AdamGroup, EnsembleMLP, GradSpace, OptimState, ParamStore
 from .impl_base import DeviceBatch, ImplBase, as_device_batch
 
 METRIC_NAMES = ("imitator_loss", "critic_loss", "actor_loss")
+
+# concurrent graph branches in the update (BCQWorkspace._enqueue);
+# D3A_BCQ_BRANCHES=0 keeps one stream (A/B)
+_BRANCHES = os.environ.get("D3A_BCQ_BRANCHES", "1") == "1"
 
 
 def _pad4(n: int) -> int:
@@ -567,6 +572,22 @@ class _Workspace:
             self._graphs[key] = g
         g.replay()
 
+    def _side(self, i: int) -> torch.cuda.Stream:
+        if not hasattr(self, "_sides"):
+            self._sides = [torch.cuda.Stream(device=self.obs.device) for _ in range(2)]
+        return self._sides[i]
+
+    def _actor_prefix(self) -> None:
+        """The actor loss's rows up to its critic pass: (s, clamp(z)) ->
+        decoder -> residual policy -> (s, clamp(a + flex tanh)) rows."""
+        impl, st = self.impl, self.impl.store
+        ops.call_desc("d3a_bcq_rows", self.r_ad)
+        mlp.forward(impl.vae_dec, st, self.x_ad.data_ptr(), True, self.LX2, self.ad_acts,
+                    keep_h=False)
+        ops.call_desc("d3a_bcq_rows", self.r_pa)
+        mlp.forward(impl.policy, st, self.x_pa.data_ptr(), True, self.LX1, self.pa_acts)
+        ops.call_desc("d3a_bcq_rows", self.r_qa)
+
     def _enqueue(self, imitator: bool, critic: bool, actor: bool, targets: bool) -> None:
         impl = self.impl
         B, D, A, K, L = self.B, self.D, self.A, self.K, self.L
@@ -577,6 +598,22 @@ class _Workspace:
         if impl._scaler is not None:
             ops.standardize(self.obs2, self.xobs2, self.sc_mean, self.sc_std, self.sc_eps)
         ops.call_desc("d3a_bcq_rows", self.r_q)
+        # graph branches: the online critic forward on (s, a) reads only the
+        # critic's pre-update parameters, so it runs beside the imitator update
+        # and the target pass on side stream 1 (joined before the QR loss); the
+        # actor's decoder / policy prefix needs only the updated imitator, so it
+        # runs beside the critic update on side stream 2 (joined before the
+        # actor's critic pass).  Independent nodes of the captured graph then
+        # overlap instead of queueing one small launch behind another.
+        main = torch.cuda.current_stream()
+        branch = _BRANCHES and critic
+        q_pending = False
+        if branch:
+            s1 = self._side(0)
+            s1.wait_stream(main)
+            with torch.cuda.stream(s1):
+                mlp.forward(impl.critic, st, self.x_q.data_ptr(), True, self.LX1, self.q_acts)
+            q_pending = True
         if imitator:
             # update_imitator (bcq_impl.py:148-161)
             mlp.forward(impl.vae_enc, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts)
@@ -589,6 +626,13 @@ class _Workspace:
             mlp.backward(self.ve_bwd, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts,
                          self.dhead_e.data_ptr(), 2 * L, B * 2 * L, 0, B)
             self.imitator_opt.launch()
+        a_pending = False
+        if branch and actor:
+            s2 = self._side(1)
+            s2.wait_stream(main)
+            with torch.cuda.stream(s2):
+                self._actor_prefix()
+            a_pending = True
         if critic:
             # compute_target (bcq_impl.py:215-226) over B*N sampled actions
             mlp.forward(impl.vae_dec, st, self.x_td.data_ptr(), True, self.LX2, self.td_acts,
@@ -601,19 +645,20 @@ class _Workspace:
             self.target_desc.means = self.tq_means.data_ptr() if means else None
             ops.call_desc("d3a_bcq_target", self.target_desc)
             # update_critic (ddpg_impl.py:138-165) with the quantile Huber loss
-            mlp.forward(impl.critic, st, self.x_q.data_ptr(), True, self.LX1, self.q_acts)
+            if q_pending:
+                main.wait_stream(self._side(0))
+            else:
+                mlp.forward(impl.critic, st, self.x_q.data_ptr(), True, self.LX1, self.q_acts)
             ops.call_desc("d3a_bcq_qr_loss", self.qr_desc)
             mlp.backward(self.cbwd, st, self.x_q.data_ptr(), True, self.LX1, self.q_acts,
                          self.dq.data_ptr(), K, B * K, 0, B)
             self.critic_opt.launch()
         if actor:
             # compute_actor_loss (bcq_impl.py:132-146)
-            ops.call_desc("d3a_bcq_rows", self.r_ad)
-            mlp.forward(impl.vae_dec, st, self.x_ad.data_ptr(), True, self.LX2, self.ad_acts,
-                        keep_h=False)
-            ops.call_desc("d3a_bcq_rows", self.r_pa)
-            mlp.forward(impl.policy, st, self.x_pa.data_ptr(), True, self.LX1, self.pa_acts)
-            ops.call_desc("d3a_bcq_rows", self.r_qa)
+            if a_pending:
+                main.wait_stream(self._side(1))
+            else:
+                self._actor_prefix()
             mlp.forward(impl.critic, st, self.x_qa.data_ptr(), True, self.LX1, self.qa_acts,
                         members=1)
             mlp.backward(self.abwd, st, self.x_qa.data_ptr(), True, self.LX1, self.qa_acts,

@@ -285,11 +285,15 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         raise NotImplementedError("bf16 activations: [n_in <= 48, 256, 256, 1] critics, "
                                   "all members, activations kept")
     small = not bf16 and not skip_head and small_ok(net, n * C // net.C)
+    # deep 256-wide critics under CRITIC_GEMM "x6": per-layer launches with the
+    # 256 x 256 layers on the split-bf16 GEMM (six products, fp32-accurate)
+    deep6 = (not bf16 and out_parts is None and ops.CRITIC_GEMM == "x6" and _X6_DEEP
+             and x6_deep_shape(net) and n * C >= 8192 and xgen is None)
     if out_parts is not None:
         assert parts_ok(net) and not bf16 and not skip_head and aux is None
         assert tuple(out_parts.shape) == (N.MLP_PARTS, C, R, sizes[-1])
         small = True
-    if bf16 or small or fused_ok(net, n * C // net.C):
+    if not deep6 and (bf16 or small or fused_ok(net, n * C // net.C)):
         d = N.MlpFwdDesc()
         d.block_rows = 16 if small else _FUSED_BM
         d.x, d.ldx = x, ldx
@@ -362,7 +366,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     # the aux pass rides in the same launches (second batch dimension, element
     # offsets from the main pass's operands) when it has the main pass's shape
     pair = aux is not None and members is None and x_shared and sxb is None and r0 == 0 \
-        and n == R and aux[3].R == R and aux[2] == ldx
+        and n == R and aux[3].R == R and aux[2] == ldx and not deep6
     if pair:
         ast, ax, _, aacts = aux
         assert ast.size == store.size and list(ast.specs) == list(store.specs)
@@ -372,9 +376,15 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         h = acts.h[l]
         H = sizes[l + 1]
         dy = (aacts.h[l].data_ptr() - h.data_ptr()) // 4 if pair else 0
-        ops.linear_fwd(inp, False, ld_in, net.W(l, store), net.b(l, store), h.data_ptr() + 4 * r0 * H,
-                       C, n, sizes[l], H, relu=True, ldy=H, sxb=sxb_ if l == 0 else R * ld_in,
-                       syb=R * H, pair=(dx, dW, dy) if pair else None)
+        if deep6 and l >= 1:
+            ops.linear_fwd_sbf16(inp, ld_in, net.W(l, store), net.b(l, store),
+                                 h.data_ptr() + 4 * r0 * H, C, n, sizes[l], H, relu=True, ldy=H,
+                                 sxb=R * ld_in, syb=R * H)
+        else:
+            ops.linear_fwd(inp, False, ld_in, net.W(l, store), net.b(l, store),
+                           h.data_ptr() + 4 * r0 * H, C, n, sizes[l], H, relu=True, ldy=H,
+                           sxb=sxb_ if l == 0 else R * ld_in, syb=R * H,
+                           pair=(dx, dW, dy) if pair else None)
         inp, ld_in = h.data_ptr() + 4 * r0 * H, H
         dx = dy
     out_dim = sizes[-1]

@@ -226,6 +226,23 @@ def gemm_sbf16(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor], y: t
     N.check(N.lib().d3a_gemm_sbf16(C.byref(d), terms, _stream()), "d3a_gemm_sbf16")
 
 
+def linear_fwd_sbf16(x: int, ldx: int, W: int, b: Optional[int], y: int, C_: int, R: int,
+                     n_in: int, n_out: int, relu: bool, ldy: int, sxb: int, syb: int,
+                     terms: int = 6) -> None:
+    """y[c] = act(x[c] @ W[c]^T + b[c]) on d3a_gemm_sbf16 (split-bf16 operands,
+    ``terms`` 6: fp32-accurate); pointer form of ``gemm_sbf16``."""
+    d = N.GemmDesc()
+    d.A, d.B, d.C = x, W, y
+    d.bias = b
+    d.M, d.N, d.K, d.batch = R, n_out, n_in, C_
+    d.sAb, d.sAm, d.sAk = sxb, ldx, 1
+    d.sBb, d.sBk, d.sBn = n_out * n_in, 1, n_in
+    d.sCb, d.sCm, d.sCn = syb, ldy, 1
+    d.sbias_b = n_out
+    d.splits, d.alpha, d.relu, d.variant, d.batch2 = 1, 1.0, int(relu), -1, 1
+    N.check(N.lib().d3a_gemm_sbf16(C.byref(d), terms, _stream()), "d3a_gemm_sbf16")
+
+
 def linear_fwd_splitk(x: int, ldx: int, W: int, b: Optional[int], y: int, R: int, n_in: int,
                       n_out: int, relu: bool, part: torch.Tensor, splits: int) -> None:
     """y = act(x @ W^T + b) for one long-K Linear (K5's encoder fc, 3,136 -> 512)
