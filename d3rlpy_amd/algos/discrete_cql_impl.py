@@ -27,6 +27,7 @@ online evaluations of obs share one encoder pass and its one backward.
 from __future__ import annotations
 
 import ctypes as C
+import contextlib
 import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -408,6 +409,9 @@ def _conv_bwd_x(ci: int, co: int) -> bool:
 # keeps d3a_iqn_prior + the embed GEMM + d3a_iqn_head_fwd (A/B)
 _IQN_FUSED = os.environ.get("D3A_IQN_FUSED", "1") == "1"
 _IQN_RECOMPUTE = os.environ.get("D3A_IQN_RECOMPUTE", "1") == "1"
+# concurrent graph branches in the K5 update (target pass; weight gradients);
+# D3A_K5_BRANCHES=0 keeps one stream (A/B)
+_K5_BRANCHES = os.environ.get("D3A_K5_BRANCHES", "1") == "1"
 
 
 class _HeadPass:
@@ -685,6 +689,11 @@ class _Workspace:
             self._graphs[key] = g
         g.replay()
 
+    def _side(self, i: int) -> torch.cuda.Stream:
+        if not hasattr(self, "_sides"):
+            self._sides = [torch.cuda.Stream(device=self.obs2.device) for _ in range(2)]
+        return self._sides[i]
+
     def _enqueue(self, sync_target: bool) -> None:
         impl = self.impl
         B, K, A, F, E = self.B, impl._K, impl._action_size, impl._F, impl._E
@@ -709,13 +718,29 @@ class _Workspace:
                     descs.append(d)
                     lays.append(lay)
             ops.conv_pack_weights(descs, lays)
+        # graph branches: the target encoder + target head (own buffers, the
+        # target parameters) run on side stream 1 beside the online encoder +
+        # head, joined before the loss; in the backward each layer's weight
+        # gradient runs on side stream 2 beside the input-gradient chain
+        # (joined before Adam).  Nodes of the captured graph then overlap.
+        main = torch.cuda.current_stream()
+        br = _K5_BRANCHES
+        if br:
+            s1 = self._side(0)
+            s1.wait_stream(main)
         # encoders
         self.enc.forward(self.obs2.data_ptr(), st, prepacked=pre)
-        self.enc_t.forward(self.obs2.data_ptr() + self.obs2[0].numel() * B, tg, prepacked=pre)
+        with torch.cuda.stream(s1) if br else contextlib.nullcontext():
+            self.enc_t.forward(self.obs2.data_ptr() + self.obs2[0].numel() * B, tg, prepacked=pre)
+            if not self.mean:
+                self.head_t.launch(self.taus.data_ptr() + 4 * 4 * BK, [self.enc_t.h.data_ptr()],
+                                   BK, K, tg, n_keep=0)
         h_obs = self.enc.h.data_ptr()
         h_next = h_obs + 4 * B * F
         g = self.grads
         if self.mean:
+            if br:
+                main.wait_stream(s1)
             # linear heads (mean_q_function.py:22-23), the TD (+ conservative)
             # loss with dL/dQ, then the head's weight and masked input gradients
             ops.linear_fwd(h_obs, True, F, st.ptr("q.fc.W"), st.ptr("q.fc.b"),
@@ -734,8 +759,8 @@ class _Workspace:
             # backward does not recompute them)
             self.head.launch(self.taus.data_ptr(), [h_obs, h_obs, h_obs, h_next], BK, K, st,
                              n_keep=0 if self.recompute else 3 * BK)
-            self.head_t.launch(self.taus.data_ptr() + 4 * 4 * BK, [self.enc_t.h.data_ptr()], BK,
-                               K, tg, n_keep=0)
+            if br:
+                main.wait_stream(s1)
             ops.call_desc("d3a_iqn_loss", self.loss_desc)
             # backward: head, embed, encoder (obs samples)
             if self.fused_bwd:
@@ -745,9 +770,20 @@ class _Workspace:
                 ops.linear_bwd_w(self.dphi.data_ptr(), F, 3 * BK * F, self.head.prior.data_ptr(),
                                  E, 3 * BK * E, g.get("q.embed.W").data_ptr(), 1, 3 * BK, E, F,
                                  self.S_emb, db=g.get("q.embed.b").data_ptr(), variant=10)
-        ops.linear_bwd_w(self.dzfc.data_ptr(), F, B * F, self.enc.yt.data_ptr(), impl.flat,
-                         B * impl.flat, g.get("enc.fc.W").data_ptr(), 1, B, impl.flat, F,
-                         self.S_fc, db=g.get("enc.fc.b").data_ptr(), sbf16=6 if _FC_SPLITK else 0)
+        if br:
+            s2 = self._side(1)
+
+        def wgrad(fn):  # a weight gradient: on side stream 2 after main's work so far
+            if br:
+                s2.wait_stream(main)
+                with torch.cuda.stream(s2):
+                    fn()
+            else:
+                fn()
+        wgrad(lambda: ops.linear_bwd_w(
+            self.dzfc.data_ptr(), F, B * F, self.enc.yt.data_ptr(), impl.flat, B * impl.flat,
+            g.get("enc.fc.W").data_ptr(), 1, B, impl.flat, F, self.S_fc,
+            db=g.get("enc.fc.b").data_ptr(), sbf16=6 if _FC_SPLITK else 0))
         ops.linear_bwd_x(self.dzfc.data_ptr(), F, B * F, st.ptr("enc.fc.W"), self.dyt.data_ptr(),
                          impl.flat, B * impl.flat, 1, B, impl.flat, F, sbf16=6 if _FC_SPLITK else 0)
         ci, h, w, co, k, s, oh, ow = impl.geom[-1]
@@ -769,7 +805,7 @@ class _Workspace:
             cd.dy, cd.dW, cd.db = self.dys[l].data_ptr(), g.get(Wn).data_ptr(), \
                 g.get(bn).data_ptr()
             cd.splits = self.splits[l]
-            ops.call_desc("d3a_conv_bwd_w", cd)
+            wgrad(lambda cd=cd: ops.call_desc("d3a_conv_bwd_w", cd))
             if l > 0 and _conv_bwd_x(ci, co):
                 # the input gradient as one implicit GEMM through the ReLU of
                 # the layer's input (no column matrix, no col2im)
@@ -790,6 +826,8 @@ class _Workspace:
                 c2.B, c2.C, c2.H, c2.W = B, ci, h, w
                 c2.KH, c2.KW, c2.S, c2.OH, c2.OW = k, k, s, oh, ow
                 ops.call_desc("d3a_col2im", c2)
+        if br:
+            main.wait_stream(s2)
         self.opt.launch()
         ops.step_end(impl.counters, 1, self.metrics, self.ring, self.ring_ctr,
                      tg.data if sync_target else None, st.data if sync_target else None,

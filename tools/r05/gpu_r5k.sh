@@ -13,6 +13,7 @@ timeout -k 10 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method th
 tail -3 $O/par_tests.log
 B="timeout -k 10 200 python -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --transitions 100000"
 $B --algo dcql > $O/b_dcql.json 2>$O/b_dcql.err || exit 1; echo dcql; cut -c1-220 $O/b_dcql.json
+D3A_K5_BRANCHES=0 $B --algo dcql > $O/b_dcql_br0.json 2>>$O/b.err || exit 1; echo dcql_branches_off; cut -c1-220 $O/b_dcql_br0.json
 D3A_CONV1_U8S4=0 $B --algo dcql > $O/b_dcql_c1off.json 2>>$O/b.err || exit 1; echo dcql_conv1off; cut -c1-220 $O/b_dcql_c1off.json
 $B --algo cqlrepro > $O/b_repro.json 2>$O/b_repro.err || exit 1; echo repro; cut -c1-220 $O/b_repro.json
 D3A_X6_DEEP=0 $B --algo cqlrepro > $O/b_repro_off.json 2>>$O/b.err || exit 1; echo repro_x6deep_off; cut -c1-220 $O/b_repro_off.json
