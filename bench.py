@@ -645,9 +645,10 @@ def main():
     if args.traffic_json is None:
         prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
         # the PMC summary of THIS line's dominant kernel: the bf16 and x6 lines
-        # have their own kernels and files (r04_pmc_traffic_<algo>_<suffix>.json)
+        # have their own kernels and files (r0N_pmc_traffic_<algo>_<suffix>.json,
+        # the latest round's)
         suffix = f"_{args.precision}" if bf16 else "_x6" if x6 else ""
-        rounds = (4, 3, 2, 1) if not suffix else (4,)
+        rounds = (5, 4, 3, 2, 1) if not suffix else (5, 4)
         args.traffic_json = next((p for p in (os.path.join(prof, f"r0{r}_pmc_traffic_{args.algo}"
                                                            f"{suffix}.json")
                                               for r in rounds) if os.path.exists(p)), "")
