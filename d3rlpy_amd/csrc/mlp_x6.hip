@@ -254,20 +254,24 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
-    float4 hr[2][2];  // raw fp32 Wh of k steps s and s + 1
+    // raw fp32 Wh of k steps s .. s + HD - 1 in flight (an L2 round trip is
+    // longer than two steps' twelve MFMAs)
+    constexpr int HD = 4;
+    float4 hr[HD][2];
     auto load_h = [&](int s, int slot) {
       hr[slot][0] = kok ? *reinterpret_cast<const float4*>(whr + 16 * s) : make_float4(0.f, 0.f, 0.f, 0.f);
       hr[slot][1] = kok ? *reinterpret_cast<const float4*>(whr + 16 * s + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
     };
-    load_h(0, 0);
-    load_h(1, 1);
+#pragma unroll
+    for (int s = 0; s < HD; ++s) load_h(s, s);
 #pragma unroll
     for (int s = 0; s < W_H / 16; ++s) {
       bf16x8 wa[3];
-      const float v[8] = {hr[s & 1][0].x, hr[s & 1][0].y, hr[s & 1][0].z, hr[s & 1][0].w,
-                          hr[s & 1][1].x, hr[s & 1][1].y, hr[s & 1][1].z, hr[s & 1][1].w};
+      const int sl = s % HD;
+      const float v[8] = {hr[sl][0].x, hr[sl][0].y, hr[sl][0].z, hr[sl][0].w,
+                          hr[sl][1].x, hr[sl][1].y, hr[sl][1].z, hr[sl][1].w};
       split8(v, wa);
-      if (s + 2 < W_H / 16) load_h(s + 2, s & 1);
+      if (s + HD < W_H / 16) load_h(s + HD, sl);
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         bf16x8 bp[3];
