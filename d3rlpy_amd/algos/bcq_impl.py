@@ -40,9 +40,12 @@ from .impl_base import DeviceBatch, ImplBase, as_device_batch
 
 METRIC_NAMES = ("imitator_loss", "critic_loss", "actor_loss")
 
-# concurrent graph branches in the update (BCQWorkspace._enqueue);
-# D3A_BCQ_BRANCHES=0 keeps one stream (A/B)
-_BRANCHES = os.environ.get("D3A_BCQ_BRANCHES", "1") == "1"
+# concurrent graph branches in the update (_Workspace._enqueue), off by
+# default: measured slower at K3 (1,758 against 1,825 steps/s, round 5: every
+# dependency edge of a multi-stream graph costs ~4 us between the small
+# launches of the imitator chain, more than the overlap wins);
+# D3A_BCQ_BRANCHES=1 turns them on
+_BRANCHES = os.environ.get("D3A_BCQ_BRANCHES", "0") == "1"
 
 
 def _pad4(n: int) -> int:

@@ -156,8 +156,12 @@ def x6_deep_shape(net: EnsembleMLP) -> bool:
     return net.n_layers >= 4 and all(h == 256 for h in net.sizes[1:-1])
 
 
-# D3A_X6_DEEP=0 keeps the deep critics' backward on the fp32 GEMMs (A/B)
+# D3A_X6_DEEP=0 keeps the deep critics' backward on the fp32 GEMMs (A/B);
+# the forward stays on the one-launch fp32 kernel with the target aux pass
+# unless D3A_X6_DEEP_FWD=1 (per-layer split-bf16 launches: measured slower at
+# the reproduction config, 60.7 + 21.6 us against 56.5 us, round 5)
 _X6_DEEP = os.environ.get("D3A_X6_DEEP", "1") == "1"
+_X6_DEEP_FWD = os.environ.get("D3A_X6_DEEP_FWD", "0") == "1"
 
 
 def x6_wide_shape(net: EnsembleMLP) -> bool:
@@ -288,7 +292,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     # deep 256-wide critics under CRITIC_GEMM "x6": per-layer launches with the
     # 256 x 256 layers on the split-bf16 GEMM (six products, fp32-accurate)
     deep6 = (not bf16 and out_parts is None and ops.CRITIC_GEMM == "x6" and _X6_DEEP
-             and x6_deep_shape(net) and n * C >= 8192 and xgen is None)
+             and _X6_DEEP_FWD and x6_deep_shape(net) and n * C >= 8192 and xgen is None)
     if out_parts is not None:
         assert parts_ok(net) and not bf16 and not skip_head and aux is None
         assert tuple(out_parts.shape) == (N.MLP_PARTS, C, R, sizes[-1])
