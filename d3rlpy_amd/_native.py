@@ -298,6 +298,20 @@ class MlpBwdDesc(C.Structure):
     ]
 
 
+class MlpBwdSmallDesc(C.Structure):
+    _fields_ = [
+        ("x", vp), ("ldx", C.c_int64), ("sxb", C.c_int64),
+        ("h1", vp), ("h2", vp), ("sh", C.c_int64),
+        ("dout", vp), ("ld_dout", C.c_int64), ("sdout", C.c_int64),
+        ("W1", vp), ("W2", vp), ("W3", vp),
+        ("sW1", C.c_int64), ("sW2", C.c_int64), ("sW3", C.c_int64),
+        ("dW1", vp), ("db1", vp), ("dW2", vp), ("db2", vp), ("dW3", vp), ("db3", vp),
+        ("dx", vp),
+        ("scratch", vp), ("tickets", vp),
+        ("rows", C.c_int32), ("n_in", C.c_int32), ("n_out", C.c_int32), ("C", C.c_int32),
+    ]
+
+
 class Q2BwdDesc(C.Structure):
     _fields_ = [
         ("x", vp), ("ldx", C.c_int64), ("sxb", C.c_int64),
@@ -540,6 +554,7 @@ _SIGNATURES = {
     "d3a_bcq_qr_loss": (C.c_int, [C.POINTER(BcqQrDesc), vp]),
     "d3a_bcq_actor_head": (C.c_int, [C.POINTER(BcqActorDesc), vp]),
     "d3a_mlp_bwd": (C.c_int, [C.POINTER(MlpBwdDesc), vp]),
+    "d3a_mlp_bwd_small": (C.c_int, [C.POINTER(MlpBwdSmallDesc), vp]),
     "d3a_q2_bwd": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
     "d3a_q2_bwd_actor_head": (C.c_int, [C.POINTER(Q2BwdDesc), C.POINTER(SacActorHeadDesc), vp]),
     "d3a_q2_fwd_bf16": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),

@@ -414,8 +414,8 @@ class _Workspace:
         self.dx_vd = z(1, B, D + L)
         self.dhead_e = z(B, 2 * L)
         self.igrads = GradSpace(dev)
-        self.ve_bwd = mlp.BackwardSpace(impl.vae_enc, B, self.igrads, dev)
-        self.vd_bwd = mlp.BackwardSpace(impl.vae_dec, B, self.igrads, dev)
+        self.ve_bwd = mlp.BackwardSpace(impl.vae_enc, B, self.igrads, dev, small=True)
+        self.vd_bwd = mlp.BackwardSpace(impl.vae_dec, B, self.igrads, dev, small=True)
         # critic target over B*N sampled actions
         self.x_td = z(BN, self.LX2)
         self.td_acts = mlp.Acts.alloc(impl.vae_dec, BN, dev)
@@ -428,7 +428,7 @@ class _Workspace:
         self.dq = z(C, B, K)
         self.loss_cb = z(C, B)
         self.cgrads = GradSpace(dev)
-        self.cbwd = mlp.BackwardSpace(impl.critic, B, self.cgrads, dev)
+        self.cbwd = mlp.BackwardSpace(impl.critic, B, self.cgrads, dev, small=True)
         # actor
         self.x_ad = z(B, self.LX2)
         self.ad_acts = mlp.Acts.alloc(impl.vae_dec, B, dev)
@@ -439,11 +439,11 @@ class _Workspace:
         self.qa_acts = mlp.Acts.alloc(impl.critic, B, dev)
         # d(-mean_b mean_k q0)/dq0 is a constant
         self.dconst = torch.full((1, B, K), -1.0 / (B * K), dtype=torch.float32, device=dev)
-        self.abwd = mlp.BackwardSpace(impl.critic, B, None, dev)
+        self.abwd = mlp.BackwardSpace(impl.critic, B, None, dev, small=True)
         self.adx = z(1, B, D + A)
         self.dhead_pi = z(B, A)
         self.pgrads = GradSpace(dev)
-        self.pbwd = mlp.BackwardSpace(impl.policy, B, self.pgrads, dev)
+        self.pbwd = mlp.BackwardSpace(impl.policy, B, self.pgrads, dev, small=True)
         self.metrics = z(len(METRIC_NAMES))
         self.scalars = z(4)
         self.ring = z(1 << 16, len(METRIC_NAMES))

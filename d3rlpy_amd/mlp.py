@@ -148,6 +148,22 @@ def x6_narrow_shape(net: EnsembleMLP) -> bool:
             and s[0] <= 48)
 
 
+def small_bwd_ok(net: EnsembleMLP, rows: int) -> bool:
+    """[n_in <= 64, 256, 256, n_out <= 256] over at most 2,048 rows: the shape
+    of d3a_mlp_bwd_small (one launch for the whole backward)."""
+    s = net.sizes
+    return (_SMALL_BWD and net.n_layers == 3 and s[1] == 256 and s[2] == 256 and s[0] <= 64
+            and s[3] <= 256 and rows <= 2048)
+
+
+# the one-launch small-batch backward is opt-in (D3A_SMALL_BWD=1): correct
+# (tests/test_gpu_mlp_bwd_small.py, the BCQ suites) but measured slower than
+# the per-layer GEMMs it replaces at K3 (its two launches 33-43 us against
+# 25-35 us for the four or five GEMM launches; K3 1,673 against 1,824
+# steps/s, round 5, profiles/r05_bcq_timeline_smallbwd.txt)
+_SMALL_BWD = os.environ.get("D3A_SMALL_BWD", "0") == "1"
+
+
 def x6_deep_shape(net: EnsembleMLP) -> bool:
     """>= 3 hidden layers, all 256 wide (the CQL reproduction critic, [obs +
     act, 256, 256, 256, 1]: reproductions/offline/cql.py:21-37): under
@@ -418,14 +434,16 @@ class BackwardSpace:
 
     def __init__(self, net: EnsembleMLP, rows: int, grads: Optional[GradSpace], device,
                  splits: Optional[int] = None, head_partials: Optional[int] = None,
-                 slice_r0: Optional[int] = None):
+                 slice_r0: Optional[int] = None, small: bool = False):
         """``head_partials``: partial count of the head layer's weight / bias
         gradients when a caller's kernel writes them (one per row, say)
         instead of the split-K GEMM (``backward(..., head_ready=True)``).
         ``slice_r0``: the backward will read the forward's activations from
         this row on; where ``slice_ok`` the weight gradients come from the
         slice kernel (``self.slice``: its partial layout, and the caller's
-        Acts must set ``no_last_h``)."""
+        Acts must set ``no_last_h``).  ``small``: where ``small_bwd_ok`` the
+        whole backward is one d3a_mlp_bwd_small launch (``self.small``: one
+        partial per 32-row block for every layer)."""
         self.net = net
         self.rows = rows
         hidden = net.sizes[1:-1]
@@ -448,6 +466,12 @@ class BackwardSpace:
                     and q2p_ok(net, rows))
         self.slice = (self.q2 and slice_r0 is not None and slice_ok(net, rows, slice_r0))
         self.slice_P = N.lib().d3a_q2_bwd_x6t_splits(rows, net.C) if self.slice else 0
+        self.small = (small and not self.fused and not self.q2 and not self.q2p
+                      and small_bwd_ok(net, rows))
+        if self.small:
+            nrb = (rows + 31) // 32
+            self.sb_scratch = torch.zeros(8, net.C, rows, 256, device=device)
+            self.sb_tickets = torch.zeros(net.C, nrb, dtype=torch.int32, device=device)
         # first-layer weight gradients as one partial per 128-row tile, from
         # the second layer's input-gradient GEMM (backward's wnext path; it
         # needs a layer above the first one, i.e. >= 2 hidden layers)
@@ -462,7 +486,9 @@ class BackwardSpace:
                 parts = head_partials if (head_partials and l == net.n_layers - 1) \
                     else (self.l0_tiles if (l == 0 and self.l0_tiles) else self.splits)
                 wparts = None
-                if self.slice:
+                if self.small:
+                    parts = (rows + 31) // 32
+                elif self.slice:
                     # one per row block; the head weight one per row block and
                     # 16-unit slice of layer 1
                     parts = self.slice_P
@@ -583,6 +609,28 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         return None
     if head_desc is not None:
         return False
+
+    if (bs.small and q_min is None and g_out is None and g_scale is None and not head_ready
+            and (n == bs.rows or not weight_grads)):
+        # the whole backward in one launch (d3a_mlp_bwd_small)
+        d = N.MlpBwdSmallDesc()
+        H = sizes[1]
+        d.x, d.ldx, d.sxb = x + 4 * r0 * ldx, ldx, sxb_
+        d.h1 = acts.h[0].data_ptr() + 4 * r0 * H
+        d.h2 = acts.h[1].data_ptr() + 4 * r0 * H
+        d.sh = R * H
+        d.dout, d.ld_dout, d.sdout = dout, ld_dout, sdout_b
+        d.W1, d.W2, d.W3 = net.W(0, store), net.W(1, store), net.W(2, store)
+        d.sW1, d.sW2, d.sW3 = H * sizes[0], H * H, sizes[3] * H
+        if weight_grads:
+            d.dW1, d.db1 = gs.get(net.wname(0)).data_ptr(), gs.get(net.bname(0)).data_ptr()
+            d.dW2, d.db2 = gs.get(net.wname(1)).data_ptr(), gs.get(net.bname(1)).data_ptr()
+            d.dW3, d.db3 = gs.get(net.wname(2)).data_ptr(), gs.get(net.bname(2)).data_ptr()
+        d.dx = dx.data_ptr() if dx is not None else None
+        d.scratch, d.tickets = bs.sb_scratch.data_ptr(), bs.sb_tickets.data_ptr()
+        d.rows, d.n_in, d.n_out, d.C = n, sizes[0], sizes[3], C
+        ops.call_desc("d3a_mlp_bwd_small", d)
+        return None
 
     def h_ptr(l):  # input activation of layer l at row r0
         if l == 0:

@@ -313,6 +313,31 @@ typedef struct d3a_mlp_bwd_desc {
 } d3a_mlp_bwd_desc;
 int d3a_mlp_bwd(const d3a_mlp_bwd_desc* d, void* stream);
 
+/* The whole backward of a small-batch [n_in <= 64, 256, 256, n_out <= 256]
+ * ReLU MLP in one launch (csrc/mlp_bwd_small.hip; replaces the per-layer
+ * split-K / input-gradient GEMMs of the autograd of encoders.py:265-275,
+ * 328-339 and the heads -- K3's VAE, QR critics and residual policy,
+ * bcq_impl.py:132-161, ddpg_impl.py:138-165).  dout = dL/d(out) [C][rows]
+ * [ld_dout] (member stride sdout), h1 / h2 the forward's kept activations
+ * ([C][.][256], member stride sh, row 0 = the first row here), x [C][rows]
+ * [ldx] (sxb 0: shared).  Weight / bias gradients (all or none) as one
+ * partial per 32-row block, [ceil(rows / 32)][C][out][in]; dx (optional)
+ * [C][rows][n_in].  scratch: [8][C][rows][256] floats; tickets: C *
+ * ceil(rows / 32) int32, zero before the first launch (each launch leaves
+ * them zero).  Exact fp32 arithmetic. */
+typedef struct d3a_mlp_bwd_small_desc {
+  const float* x; int64_t ldx, sxb;
+  const float* h1; const float* h2; int64_t sh;
+  const float* dout; int64_t ld_dout, sdout;
+  const float* W1; const float* W2; const float* W3;
+  int64_t sW1, sW2, sW3;
+  float* dW1; float* db1; float* dW2; float* db2; float* dW3; float* db3;
+  float* dx;
+  float* scratch; int32_t* tickets;
+  int32_t rows, n_in, n_out, C;
+} d3a_mlp_bwd_small_desc;
+int d3a_mlp_bwd_small(const d3a_mlp_bwd_small_desc* d, void* stream);
+
 /* Weight gradients of a single-output Q ensemble with two hidden layers of
  * width 256 (VectorEncoderWithAction [n_in -> 256 -> 256], encoders.py:265-275,
  * 328-339, + ContinuousMeanQFunction._fc, mean_q_function.py:255-256), one

@@ -63,7 +63,8 @@ STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_gemm_wnext", "GemmWnext"),
            ("d3a_iqn_head_desc", "IqnHeadDesc"), ("d3a_iqn_loss_desc", "IqnLossDesc"),
            ("d3a_iqn_head_bwd_desc", "IqnHeadBwdDesc"), ("d3a_conv_desc", "ConvDesc"),
            ("d3a_iqn_embed_head_desc", "IqnEmbedHeadDesc"),
-           ("d3a_iqn_head_bwd_fused_desc", "IqnHeadBwdFusedDesc"))
+           ("d3a_iqn_head_bwd_fused_desc", "IqnHeadBwdFusedDesc"),
+           ("d3a_mlp_bwd_small_desc", "MlpBwdSmallDesc"))
 
 
 def test_struct_layouts_match_header(tmp_path):
