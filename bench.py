@@ -154,7 +154,9 @@ WORKLOADS = {
             "hidden [256,256], reference defaults"),
     "td3bc": ("pendulum-random", 100,
               "TD3+BC K1 (configs[0]) on 1xMI355X: obs 3, act 1, batch 100, n_critics 2, "
-              "actor every 2 steps, standard scaler, hidden [256,256], reference defaults"),
+              "actor every 2 steps, standard scaler, hidden [256,256], reference defaults; "
+              "runs on the GPU although BASELINE.json's K1 config names use_gpu=False (the "
+              "reference's CPU plumbing): this build has no CPU compute path"),
     "bcq": ("halfcheetah-medium-v0", 256,
             "BCQ K3 (configs[2]): obs 17, act 6, batch 256, QR critics n_quantiles 200, "
             "n_critics 2, n_action_samples 100, hidden [256,256], reference defaults"),
