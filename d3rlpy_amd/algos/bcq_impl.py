@@ -41,10 +41,11 @@ from .impl_base import DeviceBatch, ImplBase, as_device_batch
 METRIC_NAMES = ("imitator_loss", "critic_loss", "actor_loss")
 
 # concurrent graph branches in the update (_Workspace._enqueue), off by
-# default: measured slower at K3 (1,758 against 1,825 steps/s, round 5: every
-# dependency edge of a multi-stream graph costs ~4 us between the small
-# launches of the imitator chain, more than the overlap wins);
-# D3A_BCQ_BRANCHES=1 turns them on
+# default: measured slower at K3, round 5 -- forked at the step's start 1,758
+# against 1,825 steps/s (every cross-stream edge costs ~4 us between the small
+# launches of the imitator chain), forked behind the imitator (as now) 1,521
+# against 1,829 (the side passes' workgroups delay the one-per-CU target pass
+# and stretch its tail); D3A_BCQ_BRANCHES=1 turns them on
 _BRANCHES = os.environ.get("D3A_BCQ_BRANCHES", "0") == "1"
 
 
@@ -602,21 +603,15 @@ class _Workspace:
             ops.standardize(self.obs2, self.xobs2, self.sc_mean, self.sc_std, self.sc_eps)
         ops.call_desc("d3a_bcq_rows", self.r_q)
         # graph branches: the online critic forward on (s, a) reads only the
-        # critic's pre-update parameters, so it runs beside the imitator update
-        # and the target pass on side stream 1 (joined before the QR loss); the
-        # actor's decoder / policy prefix needs only the updated imitator, so it
-        # runs beside the critic update on side stream 2 (joined before the
-        # actor's critic pass).  Independent nodes of the captured graph then
+        # critic's pre-update parameters, so it runs beside the target pass on
+        # side stream 1 (joined before the QR loss); the actor's decoder /
+        # policy prefix needs only the updated imitator, so it runs beside the
+        # critic update on side stream 2 (joined before the actor's critic
+        # pass).  Independent nodes of the captured graph then
         # overlap instead of queueing one small launch behind another.
         main = torch.cuda.current_stream()
         branch = _BRANCHES and critic
-        q_pending = False
-        if branch:
-            s1 = self._side(0)
-            s1.wait_stream(main)
-            with torch.cuda.stream(s1):
-                mlp.forward(impl.critic, st, self.x_q.data_ptr(), True, self.LX1, self.q_acts)
-            q_pending = True
+        q_pending = a_pending = False
         if imitator:
             # update_imitator (bcq_impl.py:148-161)
             mlp.forward(impl.vae_enc, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts)
@@ -629,13 +624,20 @@ class _Workspace:
             mlp.backward(self.ve_bwd, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts,
                          self.dhead_e.data_ptr(), 2 * L, B * 2 * L, 0, B)
             self.imitator_opt.launch()
-        a_pending = False
-        if branch and actor:
-            s2 = self._side(1)
-            s2.wait_stream(main)
-            with torch.cuda.stream(s2):
-                self._actor_prefix()
-            a_pending = True
+        if branch:
+            # forked behind the imitator update, so the side work overlaps the
+            # long target pass rather than the imitator chain's small launches
+            s1 = self._side(0)
+            s1.wait_stream(main)
+            with torch.cuda.stream(s1):
+                mlp.forward(impl.critic, st, self.x_q.data_ptr(), True, self.LX1, self.q_acts)
+            q_pending = True
+            if actor:
+                s2 = self._side(1)
+                s2.wait_stream(main)
+                with torch.cuda.stream(s2):
+                    self._actor_prefix()
+                a_pending = True
         if critic:
             # compute_target (bcq_impl.py:215-226) over B*N sampled actions
             mlp.forward(impl.vae_dec, st, self.x_td.data_ptr(), True, self.LX2, self.td_acts,
