@@ -338,6 +338,7 @@ class BcqRowsDesc(C.Structure):
         ("a", vp), ("E", C.c_int32), ("lda", C.c_int64),
         ("base", vp), ("mode", C.c_int32), ("clip", C.c_float), ("scale", C.c_float),
         ("x", vp), ("ldx", C.c_int64), ("e_out", vp), ("rows", C.c_int64),
+        ("a_parts", C.c_int32), ("s_a_part", C.c_int64),
     ]
 
 
@@ -350,6 +351,7 @@ class BcqVaeDesc(C.Structure):
         ("scalars", vp), ("metrics", vp),
         ("B", C.c_int32), ("D", C.c_int32), ("A", C.c_int32), ("L", C.c_int32),
         ("beta", C.c_float), ("min_logstd", C.c_float), ("max_logstd", C.c_float),
+        ("head_parts", C.c_int32), ("s_e_part", C.c_int64), ("s_d_part", C.c_int64),
     ]
 
 
@@ -374,7 +376,7 @@ class BcqActorDesc(C.Structure):
         ("head", vp), ("a_dec", vp), ("dq_da", vp), ("ld_da", C.c_int32),
         ("da_off", C.c_int32), ("dhead", vp), ("q0", vp), ("loss_cb", vp), ("metrics", vp),
         ("B", C.c_int32), ("A", C.c_int32), ("K", C.c_int32), ("C", C.c_int32),
-        ("scale", C.c_float),
+        ("scale", C.c_float), ("head_parts", C.c_int32), ("s_head_part", C.c_int64),
     ]
 
 

@@ -40,6 +40,10 @@ from .impl_base import DeviceBatch, ImplBase, as_device_batch
 
 METRIC_NAMES = ("imitator_loss", "critic_loss", "actor_loss")
 
+# the B-row small-net passes on d3a_mlp_fwd's parts path (D3A_BCQ_PARTS=0: the
+# one-workgroup-per-16-rows small kernel, A/B)
+_PARTS = os.environ.get("D3A_BCQ_PARTS", "1") == "1"
+
 # concurrent graph branches in the update (_Workspace._enqueue), off by
 # default: measured slower at K3, round 5 -- forked at the step's start 1,758
 # against 1,825 steps/s (every cross-stream edge costs ~4 us between the small
@@ -436,6 +440,16 @@ class _Workspace:
         self.a_dec_a = z(B, A)
         self.x_pa = z(B, self.LX1)
         self.pa_acts = mlp.Acts.alloc(impl.policy, B, dev)
+        # the four B-row passes of the small nets (VAE encoder / decoder, the
+        # actor's decoder and residual policy) on d3a_mlp_fwd's parts path: the
+        # second layer split over D3A_MLP_PARTS workgroups, the head written as
+        # partial sums the consumers add in order (d3a_bcq_* head_parts)
+        P_ = NAT.MLP_PARTS
+        pz = lambda net: (torch.zeros(P_, net.C, B, net.sizes[-1], device=dev)  # noqa: E731
+                          if _PARTS and mlp.parts_ok(net) else None)
+        self.pe, self.pd = pz(impl.vae_enc), pz(impl.vae_dec)  # (the encoder's 2 L
+        # outputs exceed the parts path's 16 at K3: pe None, its head a matrix)
+        self.pad, self.ppi = pz(impl.vae_dec), pz(impl.policy)
         self.x_qa = z(B, self.LX1)
         self.qa_acts = mlp.Acts.alloc(impl.critic, B, dev)
         # d(-mean_b mean_k q0)/dq0 is a constant
@@ -458,10 +472,12 @@ class _Workspace:
         self._build_descs()
 
     def _rows(self, obs, rep, a, E, lda, mode, x, ldx, rows, base=None, e_out=None, clip=0.0,
-              scale=0.0):
+              scale=0.0, a_parts=None):
         d = NAT.BcqRowsDesc()
         d.obs, d.D, d.rep = obs.data_ptr(), self.D, rep
         d.a, d.E, d.lda = a, E, lda
+        if a_parts is not None:  # a as head parts [P][1][rows][E]
+            d.a, d.a_parts, d.s_a_part = a_parts.data_ptr(), a_parts.shape[0], a_parts[0].numel()
         d.base = base.data_ptr() if base is not None else None
         d.mode, d.clip, d.scale = mode, clip, scale
         d.x, d.ldx = x.data_ptr(), ldx
@@ -489,15 +505,20 @@ class _Workspace:
         self.r_ad = self._rows(self.obs, 1, self.z_actor.data_ptr(), L, L, 1, self.x_ad,
                                self.LX2, B, clip=0.5)
         self.r_pa = self._rows(self.obs, 1, self.ad_acts.out.data_ptr(), A, A, 2, self.x_pa,
-                               self.LX1, B, e_out=self.a_dec_a)
+                               self.LX1, B, e_out=self.a_dec_a, a_parts=self.pad)
         self.r_qa = self._rows(self.obs, 1, self.pa_acts.out.data_ptr(), A, A, 3, self.x_qa,
-                               self.LX1, B, base=self.a_dec_a, scale=flex)
+                               self.LX1, B, base=self.a_dec_a, scale=flex, a_parts=self.ppi)
 
         v = NAT.BcqVaeDesc()
         v.obs, v.act, v.eps = self.obs.data_ptr(), self.act.data_ptr(), self.eps_vae.data_ptr()
         v.head_e, v.std_out = self.ve_acts.out.data_ptr(), self.std.data_ptr()
         v.x_dec, v.ldx = self.x_vd.data_ptr(), self.LX2
         v.head_d, v.dhead_d = self.vd_acts.out.data_ptr(), self.dhead_d.data_ptr()
+        v.head_parts = NAT.MLP_PARTS
+        if self.pe is not None:
+            v.head_e, v.s_e_part = self.pe.data_ptr(), self.pe[0].numel()
+        if self.pd is not None:
+            v.head_d, v.s_d_part = self.pd.data_ptr(), self.pd[0].numel()
         v.dx_dec, v.lddx, v.dhead_e = self.dx_vd.data_ptr(), D + L, self.dhead_e.data_ptr()
         v.scalars, v.metrics = self.scalars.data_ptr(), self.metrics.data_ptr()
         v.B, v.D, v.A, v.L = B, D, A, L
@@ -520,6 +541,9 @@ class _Workspace:
 
         a = NAT.BcqActorDesc()
         a.head, a.a_dec = self.pa_acts.out.data_ptr(), self.a_dec_a.data_ptr()
+        if self.ppi is not None:
+            a.head, a.head_parts, a.s_head_part = (self.ppi.data_ptr(), self.ppi.shape[0],
+                                                   self.ppi[0].numel())
         a.dq_da, a.ld_da, a.da_off = self.adx.data_ptr(), D + A, D
         a.dhead, a.q0 = self.dhead_pi.data_ptr(), self.qa_acts.out.data_ptr()
         a.loss_cb, a.metrics = self.loss_cb.data_ptr(), self.metrics.data_ptr()
@@ -587,9 +611,10 @@ class _Workspace:
         impl, st = self.impl, self.impl.store
         ops.call_desc("d3a_bcq_rows", self.r_ad)
         mlp.forward(impl.vae_dec, st, self.x_ad.data_ptr(), True, self.LX2, self.ad_acts,
-                    keep_h=False)
+                    keep_h=False, out_parts=self.pad)
         ops.call_desc("d3a_bcq_rows", self.r_pa)
-        mlp.forward(impl.policy, st, self.x_pa.data_ptr(), True, self.LX1, self.pa_acts)
+        mlp.forward(impl.policy, st, self.x_pa.data_ptr(), True, self.LX1, self.pa_acts,
+                    out_parts=self.ppi)
         ops.call_desc("d3a_bcq_rows", self.r_qa)
 
     def _enqueue(self, imitator: bool, critic: bool, actor: bool, targets: bool) -> None:
@@ -614,9 +639,11 @@ class _Workspace:
         q_pending = a_pending = False
         if imitator:
             # update_imitator (bcq_impl.py:148-161)
-            mlp.forward(impl.vae_enc, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts)
+            mlp.forward(impl.vae_enc, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts,
+                        out_parts=self.pe)
             ops.call_desc("d3a_bcq_vae_sample", self.vae_desc)
-            mlp.forward(impl.vae_dec, st, self.x_vd.data_ptr(), True, self.LX2, self.vd_acts)
+            mlp.forward(impl.vae_dec, st, self.x_vd.data_ptr(), True, self.LX2, self.vd_acts,
+                        out_parts=self.pd)
             ops.call_desc("d3a_bcq_vae_loss", self.vae_desc)
             mlp.backward(self.vd_bwd, st, self.x_vd.data_ptr(), True, self.LX2, self.vd_acts,
                          self.dhead_d.data_ptr(), A, B * A, 0, B, dx=self.dx_vd)

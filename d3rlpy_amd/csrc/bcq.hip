@@ -16,6 +16,16 @@
 namespace d3a {
 namespace {
 
+// a head value given as D3A_MLP_PARTS partial sums (d3a_mlp_fwd's parts path;
+// part 0 holds the bias), summed in part order; np <= 1: the value itself
+__device__ __forceinline__ float part_sum(const float* h, int64_t sp, int np, int64_t i) {
+  if (np <= 1) return h[i];
+  float v = h[i];
+  for (int p = 1; p < np; ++p) v += h[p * sp + i];
+  return v;
+}
+
+
 // ---- input rows: x[r] = (obs[r / rep], f(a[r])) ----------------------------
 __global__ __launch_bounds__(256) void bcq_rows_kernel(d3a_bcq_rows_desc d) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -28,7 +38,7 @@ __global__ __launch_bounds__(256) void bcq_rows_kernel(d3a_bcq_rows_desc d) {
     return;
   }
   const int e = j - d.D;
-  const float a = d.a[r * d.lda + e];
+  const float a = part_sum(d.a, d.s_a_part, d.a_parts, r * d.lda + e);
   float v;
   switch (d.mode) {
     case 1: v = fminf(fmaxf(a, -d.clip), d.clip); break;            // latent.clamp(-c, c)
@@ -61,8 +71,10 @@ __global__ __launch_bounds__(1024) void bcq_vae_sample_kernel(d3a_bcq_vae_desc d
   for (int64_t i = t; i < n; i += nt) {
     const int64_t b = i / L;
     const int j = (int)(i - b * L);
-    const float mu = d.head_e[b * 2 * L + j];
-    const float ls = fminf(fmaxf(d.head_e[b * 2 * L + L + j], d.min_logstd), d.max_logstd);
+    const int npe = d.s_e_part ? d.head_parts : 1;
+    const float mu = part_sum(d.head_e, d.s_e_part, npe, b * 2 * L + j);
+    const float ls = fminf(fmaxf(part_sum(d.head_e, d.s_e_part, npe, b * 2 * L + L + j),
+                                 d.min_logstd), d.max_logstd);
     const float sd_ = expf(ls);
     d.std_out[i] = sd_;
     // torch.distributions.kl: var_ratio = std^2, t1 = mu^2,
@@ -96,7 +108,7 @@ __global__ __launch_bounds__(1024) void bcq_vae_loss_kernel(d3a_bcq_vae_desc d) 
   const float gm = 1.f / (float)n;
   double s = 0.0;
   for (int64_t i = t; i < n; i += nt) {
-    const float y = tanhf(d.head_d[i]);
+    const float y = tanhf(part_sum(d.head_d, d.s_d_part, d.s_d_part ? d.head_parts : 1, i));
     const float diff = __fsub_rn(y, d.act[i]);
     s += (double)__fmul_rn(diff, diff);
     // mse backward: 2 (y - a) / n; tanh backward: * (1 - y^2)
@@ -126,8 +138,9 @@ __global__ __launch_bounds__(256) void bcq_vae_enc_grad_kernel(d3a_bcq_vae_desc 
   const int j = (int)(i - b * L);
   const float kscale = __fdiv_rn(d.beta, (float)n);
   const float dz = d.dx_dec[b * d.lddx + d.D + j];
-  const float mu = d.head_e[b * 2 * L + j];
-  const float lsr = d.head_e[b * 2 * L + L + j];
+  const int npe = d.s_e_part ? d.head_parts : 1;
+  const float mu = part_sum(d.head_e, d.s_e_part, npe, b * 2 * L + j);
+  const float lsr = part_sum(d.head_e, d.s_e_part, npe, b * 2 * L + L + j);
   const float sd_ = d.std_out[i];
   d.dhead_e[b * 2 * L + j] = __fadd_rn(dz, __fmul_rn(kscale, mu));
   const bool pass = lsr >= d.min_logstd && lsr <= d.max_logstd;
@@ -278,7 +291,7 @@ __global__ __launch_bounds__(1024) void bcq_actor_head_kernel(d3a_bcq_actor_desc
   for (int64_t i = t; i < n; i += nt) {
     const int64_t b = i / d.A;
     const int j = (int)(i - b * d.A);
-    const float th = tanhf(d.head[i]);
+    const float th = tanhf(part_sum(d.head, d.s_head_part, d.head_parts, i));
     const float pre = __fadd_rn(d.a_dec[i], __fmul_rn(d.scale, th));
     const bool pass = pre >= -1.f && pre <= 1.f;
     const float ga = pass ? d.dq_da[b * d.ld_da + d.da_off + j] : 0.f;

@@ -927,6 +927,9 @@ typedef struct d3a_bcq_rows_desc {
   float* x; int64_t ldx;
   float* e_out;
   int64_t rows;
+  /* a as head parts (d3a_mlp_fwd_desc.parts): a_parts > 1 sums a[q * s_a_part
+   * + i] over q in order (part 0 holds the bias) */
+  int32_t a_parts; int64_t s_a_part;
 } d3a_bcq_rows_desc;
 int d3a_bcq_rows(const d3a_bcq_rows_desc* d, void* stream);
 
@@ -945,6 +948,10 @@ typedef struct d3a_bcq_vae_desc {
   float* scalars; float* metrics;
   int32_t B, D, A, L;
   float beta, min_logstd, max_logstd;
+  /* head_e / head_d as head parts of the encoder / decoder (head_parts > 1:
+   * summed in part order, part strides s_e_part / s_d_part; a stride of 0
+   * leaves that head a plain [B][.] matrix) */
+  int32_t head_parts; int64_t s_e_part, s_d_part;
 } d3a_bcq_vae_desc;
 int d3a_bcq_vae_sample(const d3a_bcq_vae_desc* d, void* stream);
 int d3a_bcq_vae_loss(const d3a_bcq_vae_desc* d, void* stream);
@@ -983,6 +990,7 @@ typedef struct d3a_bcq_actor_desc {
   const float* dq_da; int32_t ld_da, da_off;
   float* dhead; const float* q0; const float* loss_cb; float* metrics;
   int32_t B, A, K, C; float scale;
+  int32_t head_parts; int64_t s_head_part;  /* head as parts (summed in order) */
 } d3a_bcq_actor_desc;
 int d3a_bcq_actor_head(const d3a_bcq_actor_desc* d, void* stream);
 
