@@ -302,7 +302,10 @@ class DiscreteCQLImpl(ImplBase):
 
     # ------------------------------------------------------------ inspection
     def grad(self, name: str) -> torch.Tensor:
-        return next(iter(self._ws.values())).opt.grad(name)
+        ws = next(iter(self._ws.values()))
+        if ws.opt_late is not None and name in ws.opt_late.names:
+            return ws.opt_late.grad(name)
+        return ws.opt.grad(name)
 
 
 def conv_wgrad_splits(geom, l: int, B: int) -> int:
@@ -412,6 +415,11 @@ _IQN_RECOMPUTE = os.environ.get("D3A_IQN_RECOMPUTE", "1") == "1"
 # concurrent graph branches in the K5 update (target pass; weight gradients);
 # D3A_K5_BRANCHES=0 keeps one stream (A/B)
 _K5_BRANCHES = os.environ.get("D3A_K5_BRANCHES", "1") == "1"
+# with branches, the head / encoder-fc Adam early on the weight-gradient
+# branch (D3A_K5_EARLY_ADAM=1); off by default: measured slower, 1,071
+# against 1,126 steps/s (round 5; the Adam's HBM streams compete with the conv
+# input-gradient chain it was to hide behind)
+_K5_EARLY_ADAM = os.environ.get("D3A_K5_EARLY_ADAM", "0") == "1"
 
 
 class _HeadPass:
@@ -558,7 +566,18 @@ class _Workspace:
             self.S_emb = P if self.fused_bwd else mlp.n_splits(3 * BK)
             self.grads.add("q.embed.W", (1, F, E), self.S_emb)
             self.grads.add("q.embed.b", (1, F), self.S_emb)
-        self.opt = AdamGroup(impl.optim_state, self.grads)
+        # with graph branches the optimiser runs as two launches: the head and
+        # encoder-fc parameters on side stream 2 as soon as the fc weight
+        # gradient is formed (beside the conv input-gradient chain), the conv
+        # layers after the join
+        self.opt = self.opt_late = None
+        if _K5_BRANCHES and _K5_EARLY_ADAM:
+            conv = [n for n in impl.optim_state.names if n.startswith("enc.c")]
+            self.opt_late = AdamGroup(impl.optim_state, self.grads, names=conv)
+            self.opt = AdamGroup(impl.optim_state, self.grads,
+                                 names=[n for n in impl.optim_state.names if n not in conv])
+        else:
+            self.opt = AdamGroup(impl.optim_state, self.grads)
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._ran_eager = set()
         self._external_taus = False
@@ -786,6 +805,11 @@ class _Workspace:
             db=g.get("enc.fc.b").data_ptr(), sbf16=6 if _FC_SPLITK else 0))
         ops.linear_bwd_x(self.dzfc.data_ptr(), F, B * F, st.ptr("enc.fc.W"), self.dyt.data_ptr(),
                          impl.flat, B * impl.flat, 1, B, impl.flat, F, sbf16=6 if _FC_SPLITK else 0)
+        if self.opt_late is not None:
+            # the head / encoder-fc Adam on the weight-gradient branch, behind the
+            # fc weight gradient there and (wait on main) the fc input gradient,
+            # the last reader of those parameters in this step
+            wgrad(self.opt.launch)
         ci, h, w, co, k, s, oh, ow = impl.geom[-1]
         t = NAT.TransposeDesc()
         t.src, t.dst, t.mask = self.dyt.data_ptr(), self.dys[-1].data_ptr(), \
@@ -828,7 +852,7 @@ class _Workspace:
                 ops.call_desc("d3a_col2im", c2)
         if br:
             main.wait_stream(s2)
-        self.opt.launch()
+        (self.opt_late or self.opt).launch()
         ops.step_end(impl.counters, 1, self.metrics, self.ring, self.ring_ctr,
                      tg.data if sync_target else None, st.data if sync_target else None,
                      1.0)

@@ -174,11 +174,15 @@ class AdamGroup:
     for parity tests; the optimiser state lives in an ``OptimState``.
     """
 
-    def __init__(self, state: OptimState, grads: GradSpace, keep_grads: bool = True):
+    def __init__(self, state: OptimState, grads: GradSpace, keep_grads: bool = True,
+                 names: Optional[List[str]] = None):
+        """``names``: a subset of the state's parameters (the optimiser split in
+        launches whose gradients are ready at different times; the moments and
+        the step counter are the state's, shared)."""
         store = state.store
         self.state = state
         self.store = store
-        self.names = list(state.names)
+        self.names = list(state.names) if names is None else [n for n in state.names if n in names]
         self.lr, self.eps = state.lr, state.eps
         self.beta1, self.beta2 = state.betas
         dev = store.data.device
