@@ -733,10 +733,12 @@ def main():
                   "fp32 accumulation on the bf16 matrix cores)" if x6 else "fp32")
                  if args.precision == "fp32" else
                  "bf16 (critic-ensemble forward operands one bf16 part; backward split-bf16 "
-                 "mask-factored; fp32 accumulation, losses, optimiser)"
+                 "mask-factored; fp32 accumulation, losses, optimiser; kernels "
+                 "d3a_q2_fwd_x1 + d3a_q2_bwd_x6 -- round 3's bf16 lines are the bf16h pair)"
                  if args.precision == "bf16" else
                  "bf16 (critic-ensemble GEMM operands and kept activations; fp32 accumulation, "
-                 "losses, optimiser)"
+                 "losses, optimiser; kernels d3a_q2_fwd_bf16 + d3a_q2_bwd_bf16, round 3's "
+                 "bf16 line)"
                  if args.precision == "bf16h" else
                  "fp32 (input-gradient GEMMs: split-bf16 x6 on bf16 MFMA)",
         "data": (f"synthetic (D4RL {shape} shapes, {args.transitions} transitions, "
