@@ -12,19 +12,22 @@
 // act] over the same rows.  d3a_mlp_fwd's contract (kept activations optional,
 // no aux pass, out [C][rows][ldout]).
 //
-// A workgroup owns 64 rows of one member; eight waves (two per SIMD).
-//   layer 1: in 64-unit chunks, each a 64 x 64 block of sixteen 16 x 16 tiles
-//     (v_mfma_f32_16x16x32_bf16), two per wave -- every wave produces its share
-//     of the next chunk while layer 2 consumes the current one (a two-slot LDS
-//     ring of the three bf16 parts, [row][k]; fp32 kept rows to h[0])
-//   layer 2: wave w owns units 32 w .. + 31 over the 64 rows (two transposed
-//     32 x 32 tiles C^T[unit][row], W1 the A operand split from fp32 loads one
-//     chunk ahead, the ring the B operand)
-//   head: the layer-2 activations are written once as parts over the ring
-//     ([row][unit], 528-byte rows), then wave w < ceil(n_out / 32) computes
-//     outputs 32 w .. + 31 for the 64 rows over K = 256 (Wh rows split from
-//     fp32 loads two k steps ahead); lane = row, four runs of four outputs:
-//     16-byte stores.
+// A workgroup owns 64 rows of one member; eight waves (two per SIMD).  Every
+// layer is the same product shape: wave w computes a transposed 32 x 64 block
+// C^T[32 outputs][64 rows] (two v_mfma_f32_32x32x16_bf16 tiles; A = 32 weight
+// rows, split from fp32 loads, B = an LDS image of the layer input's parts,
+// [row][k]):
+//   layer 1: units 32 w .. + 31 over K = n_in (the staged input parts), written
+//     as parts to the 64 x 256 activation image;
+//   layer 2: units 32 w .. + 31 over K = 256 of that image -- a stream of
+//     16 k steps with no barrier, the weight rows four steps ahead;
+//   head: after one barrier the layer-2 activations replace the image, and
+//     wave w < ceil(n_out / 32) streams outputs 32 w .. + 31 the same way.
+// Barriers: input staged, image 1 written, layer 2 read out, image 2 written
+// (+ one for row_mean).  Round 5 measured the previous design (layer 1
+// produced chunk by chunk inside the layer-2 loop, a barrier per chunk) at
+// 71k cycles per workgroup, of which 12.5k were the interleaved production
+// and 3.4k its barriers (tools/bench_wide.py ablations).
 #include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
@@ -35,252 +38,217 @@ namespace {
 
 using namespace x6;
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
 constexpr int W_H = 256;    // hidden width
 constexpr int W_RB = 64;    // rows per workgroup
-constexpr int W_CK = 64;    // layer-2 k per chunk (= layer-1 units per chunk)
-constexpr int W_NCK = W_H / W_CK;
-constexpr int W_KS = W_CK / 16;
-constexpr int W_LDB = 72;   // bf16 stride of a ring row (144 B)
-constexpr int W_LDH = 264;  // bf16 stride of an h2 image row (528 B)
-
-__device__ __forceinline__ f32x4 mfma16x16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ f32x4 prod6_16(const bf16x8* a, const bf16x8* b, f32x4 c) {
-  c = mfma16x16(a[2], b[0], c);
-  c = mfma16x16(a[1], b[1], c);
-  c = mfma16x16(a[0], b[2], c);
-  c = mfma16x16(a[1], b[0], c);
-  c = mfma16x16(a[0], b[1], c);
-  c = mfma16x16(a[0], b[0], c);
-  return c;
-}
+constexpr int W_LDH = 264;  // bf16 stride of an image row (528 B)
+constexpr int W_HD = 4;     // weight k steps in flight
 
 template <int XL>
 struct WideLds {
-  union {
-    struct {
-      __bf16 ring[2][3][W_RB * W_LDB];
-      __bf16 x[3][W_RB * (XL + 8)];
-    } a;
-    __bf16 h2[3][W_RB * W_LDH];  // after layer 2
-  } u;
-  float rs[8][W_RB];  // row_mean: per-wave output sums [wave][row]
+  __bf16 x[3][W_RB * (XL + 8)];  // input parts [row][k]
+  __bf16 img[3][W_RB * W_LDH];   // layer-1, then layer-2 activation parts [row][unit]
+  float rs[8][W_RB];             // row_mean: per-wave output sums [wave][row]
 };
 
-// XL: n_in rounded up to 32 (32 or 64)
-template <int XL>
+// diagnostic phase stamps (STAMPS, D3A_WIDE_STAMPS=1; read with
+// d3a_wide_stamps): wave 0 of each workgroup records s_memtime at 0 start,
+// 1 input staged, 2 its barrier passed, 3 image 1 written, 4 layer-2 products
+// issued, 5 image 2 written, 6 head products issued, 7 outputs stored
+constexpr int W_NST = 8;
+__device__ unsigned long long wide_stamps[1024 * W_NST];
+
+// o[rt] += W[32 rows][256] x img[64 rows][256]^T for this lane's weight row
+// (wrow = row + 8 lh): hr holds the raw fp32 of k steps 0 .. W_HD - 1 on entry;
+// each step splits its slot, refills it W_HD steps ahead, then issues twelve
+// MFMAs.  With next != nullptr the freed slots are refilled with steps
+// 0 .. W_HD - 1 of the next stream (the head's rows) instead.
+__device__ __forceinline__ void stream256(const float* wrow, const float* next, float4 (&hr)[W_HD][2],
+                                          const __bf16 (&img)[3][W_RB * W_LDH], int li, int lh,
+                                          f32x16 (&o)[2]) {
+#pragma unroll
+  for (int s = 0; s < W_H / 16; ++s) {
+    bf16x8 wa[3];
+    const int sl = s % W_HD;
+    const float v[8] = {hr[sl][0].x, hr[sl][0].y, hr[sl][0].z, hr[sl][0].w,
+                        hr[sl][1].x, hr[sl][1].y, hr[sl][1].z, hr[sl][1].w};
+    split8(v, wa);
+    if (s + W_HD < W_H / 16) {
+      hr[sl][0] = *reinterpret_cast<const float4*>(wrow + 16 * (s + W_HD));
+      hr[sl][1] = *reinterpret_cast<const float4*>(wrow + 16 * (s + W_HD) + 4);
+    } else if (next != nullptr) {
+      const int s2 = s + W_HD - W_H / 16;
+      hr[sl][0] = *reinterpret_cast<const float4*>(next + 16 * s2);
+      hr[sl][1] = *reinterpret_cast<const float4*>(next + 16 * s2 + 4);
+    }
+    // keep the refill here: the scheduler would sink it to its first use
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      bf16x8 bp[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        bp[q] = *reinterpret_cast<const bf16x8*>(&img[q][(32 * rt + li) * W_LDH + 16 * s + 8 * lh]);
+      o[rt] = prod6(wa, bp, o[rt]);
+    }
+  }
+}
+
+// bias, ReLU, kept rows to hg, parts into the image: lane holds rows
+// 32 rt + li, units 32 w + 8 R + 4 lh + i
+template <bool KEEP>
+__device__ __forceinline__ void act_to_image(const f32x16 (&o)[2], const float4 (&bv)[4], float* hg, int m0,
+                                             int h_from, int rend, int w, int li, int lh,
+                                             __bf16 (&img)[3][W_RB * W_LDH]) {
+#pragma unroll
+  for (int R = 0; R < 4; ++R) {
+    const int u = 32 * w + 8 * R + 4 * lh;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int rl = 32 * rt + li;
+      const int row = m0 + rl;
+      float v[4] = {fmaxf(o[rt][4 * R + 0] + bv[R].x, 0.f), fmaxf(o[rt][4 * R + 1] + bv[R].y, 0.f),
+                    fmaxf(o[rt][4 * R + 2] + bv[R].z, 0.f), fmaxf(o[rt][4 * R + 3] + bv[R].w, 0.f)};
+      if (KEEP && hg != nullptr && row >= h_from && row < rend)
+        *reinterpret_cast<float4*>(hg + row * W_H + u) = make_float4(v[0], v[1], v[2], v[3]);
+      bf16x4 p[3];
+      split4(v, p);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&img[q][rl * W_LDH + u]) = p[q];
+    }
+  }
+}
+
+// XL: n_in rounded up to 32 (32 or 64); KEEP: some kept activations (h[0] /
+// h[1]) are written (without them no store precedes the head's)
+template <int XL, bool KEEP, bool STAMPS = false>
 __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
   constexpr int XLD = XL + 8;
-  constexpr int NS0 = XL / 32;  // layer-1 k steps (16x16x32)
+  constexpr int NS1 = XL / 16;  // layer-1 k steps
   __shared__ __attribute__((aligned(16))) WideLds<XL> L;
   static_assert(sizeof(WideLds<XL>) <= 163840, "LDS");
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int li = lane & 31, lh = lane >> 5;
-  const int l16 = lane & 15, lq = lane >> 4;
   const int c = blockIdx.z;
   const int m0 = (int)d.r0 + (int)blockIdx.x * W_RB;
   const int rend = (int)(d.r0 + d.rows);
   const int h_from = (int)d.h_from;
   const int nin = d.n_in, nout = d.n_out;
   float* const outp = d.out + c * d.sout;
-  float* const h0g = d.h[0] ? d.h[0] + c * d.sh : nullptr;
-  float* const h1g = d.h[1] ? d.h[1] + c * d.sh : nullptr;
-  const float* W0 = d.W[0] + c * d.sW[0];
+  float* const h0g = KEEP && d.h[0] ? d.h[0] + c * d.sh : nullptr;
+  float* const h1g = KEEP && d.h[1] ? d.h[1] + c * d.sh : nullptr;
+  const int u0 = 32 * w + li;  // this lane's weight row in layers 1 and 2
+  const float* W0r = d.W[0] + c * d.sW[0] + u0 * nin;
+  const float* W1r = d.W[1] + c * d.sW[1] + u0 * W_H + 8 * lh;
   const float* b0 = d.b[0] + c * d.sb[0];
-  const float* W1 = d.W[1] + c * d.sW[1] + (32 * w + li) * W_H + 8 * lh;
+  const float* b1 = d.b[1] + c * d.sb[1];
   const float* Wh = d.W[2] + c * d.sW[2];
   const float* bh = d.b[2] + c * d.sb[2];
-
-  // ---- prologue: the first W1 chunk in flight, input rows split into LDS
-  float4 wr[W_KS][2];
-  auto load_w1 = [&](int j) {
-#pragma unroll
-    for (int s = 0; s < W_KS; ++s) {
-      wr[s][0] = *reinterpret_cast<const float4*>(W1 + W_CK * j + 16 * s);
-      wr[s][1] = *reinterpret_cast<const float4*>(W1 + W_CK * j + 16 * s + 4);
+  const int nkt = (nout + 31) / 32;
+  const int kout = 32 * w + li;  // head: this lane's output row (rows past n_out read row 0:
+  const float* whr = Wh + (kout < nout ? kout : 0) * W_H + 8 * lh;  // never stored)
+  const int wgi = blockIdx.x + blockIdx.z * gridDim.x;
+  auto stamp = [&](int k) {
+    if constexpr (STAMPS) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (t == 0 && wgi < 1024) wide_stamps[wgi * W_NST + k] = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
-  load_w1(0);
+  stamp(0);
+
+  // ---- prologue: layer-2 weight steps 0 .. W_HD - 1, the layer-1 weight row
+  // (clamped k, masked at use) and both biases in flight; input rows split
+  // into LDS (input4_at: every load issued before any is used)
+  float4 hr[W_HD][2];
+#pragma unroll
+  for (int s = 0; s < W_HD; ++s) {
+    hr[s][0] = *reinterpret_cast<const float4*>(W1r + 16 * s);
+    hr[s][1] = *reinterpret_cast<const float4*>(W1r + 16 * s + 4);
+  }
+  float w0r[NS1][8];
+#pragma unroll
+  for (int s = 0; s < NS1; ++s)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w0r[s][i] = W0r[min(16 * s + 8 * lh + i, nin - 1)];
+  float4 b0v[4], b1v[4];
+#pragma unroll
+  for (int R = 0; R < 4; ++R) {
+    b0v[R] = *reinterpret_cast<const float4*>(b0 + 32 * w + 8 * R + 4 * lh);
+    b1v[R] = *reinterpret_cast<const float4*>(b1 + 32 * w + 8 * R + 4 * lh);
+  }
   {
     const float* xb = d.x + c * d.sxb;
     const int64_t ldx = d.ldx;
     constexpr int X4 = XL / 4;
     for (int e = t; e < W_RB * X4; e += 512) {
       const int m = e / X4, k4 = (e - m * X4) * 4;
-      const int r = m0 + m;
       float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? input_at(d, xb, ldx, r, k4 + j) : 0.f;
+      input4_at(d, xb, ldx, m0 + m, k4, rend, nin, v);
       bf16x4 p[3];
       split4(v, p);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&L.u.a.x[q][m * XLD + k4]) = p[q];
+      for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&L.x[q][m * XLD + k4]) = p[q];
     }
   }
-  __syncthreads();  // x parts staged
+  stamp(1);
+  __syncthreads();  // input parts staged
+  stamp(2);
 
-  // ---- layer 1, chunk j: sixteen 16 x 16 tiles (unit tile ut = w >> 1 of 16
-  // units, row tiles rt0 + {0, 1}, rt0 = 2 (w & 1)); lane: row 16 rt + l16,
-  // units 16 ut + 4 lq + i.  W0 rows and bias of the next chunk loaded one
-  // production ahead.
-  const int ut = w >> 1, rt0 = 2 * (w & 1);
-  float w0n[NS0][8];
-  float4 b0n;
-  auto load_w0 = [&](int j) {
-    const int u = W_CK * j + 16 * ut + l16;
-#pragma unroll
-    for (int s = 0; s < NS0; ++s)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int k = 32 * s + 8 * lq + i;
-        w0n[s][i] = k < nin ? W0[u * nin + k] : 0.f;
-      }
-    b0n = *reinterpret_cast<const float4*>(b0 + W_CK * j + 16 * ut + 4 * lq);
-  };
-  load_w0(0);
-  auto produce = [&](int j) {
-    f32x4 a[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) a[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < NS0; ++s) {
-      bf16x8 wp[3];
-      split8(w0n[s], wp);
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        bf16x8 xp[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          xp[q] = *reinterpret_cast<const bf16x8*>(
-              &L.u.a.x[q][(16 * (rt0 + r) + l16) * XLD + 32 * s + 8 * lq]);
-        a[r] = prod6_16(wp, xp, a[r]);
-      }
-    }
-    const float4 bv = b0n;
-    if (j + 1 < W_NCK) load_w0(j + 1);
-    const int k = 16 * ut + 4 * lq;  // local k of the chunk
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int rl = 16 * (rt0 + r) + l16;
-      const int row = m0 + rl;
-      float v[4] = {fmaxf(a[r][0] + bv.x, 0.f), fmaxf(a[r][1] + bv.y, 0.f),
-                    fmaxf(a[r][2] + bv.z, 0.f), fmaxf(a[r][3] + bv.w, 0.f)};
-      if (h0g != nullptr && row >= h_from && row < rend)
-        *reinterpret_cast<float4*>(h0g + row * W_H + W_CK * j + k) = make_float4(v[0], v[1], v[2], v[3]);
-      bf16x4 p[3];
-      split4(v, p);
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        *reinterpret_cast<bf16x4*>(&L.u.a.ring[j & 1][q][rl * W_LDB + k]) = p[q];
-    }
-  };
-  produce(0);
-  __syncthreads();  // chunk 0 in slot 0
-
-  // ---- layer 2: acc[rt] = C^T[units 32 w ..][rows 32 rt ..]
-  f32x16 acc[2];
+  // ---- layer 1: units 32 w .. over K = XL (x parts past n_in are zero, the
+  // weights there masked to zero)
+  f32x16 o[2];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[rt][r] = 0.f;
-#pragma unroll 1
-  for (int j = 0; j < W_NCK; ++j) {
-    float4 wc[W_KS][2];
+    for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
 #pragma unroll
-    for (int s = 0; s < W_KS; ++s) {
-      wc[s][0] = wr[s][0];
-      wc[s][1] = wr[s][1];
-    }
-    if (j + 1 < W_NCK) load_w1(j + 1);
-    const int slot = j & 1;
+  for (int s = 0; s < NS1; ++s) {
+    float v[8];
 #pragma unroll
-    for (int s = 0; s < W_KS; ++s) {
-      bf16x8 wa[3];
-      const float v[8] = {wc[s][0].x, wc[s][0].y, wc[s][0].z, wc[s][0].w,
-                          wc[s][1].x, wc[s][1].y, wc[s][1].z, wc[s][1].w};
-      split8(v, wa);
+    for (int i = 0; i < 8; ++i) v[i] = 16 * s + 8 * lh + i < nin ? w0r[s][i] : 0.f;
+    bf16x8 wa[3];
+    split8(v, wa);
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        bf16x8 bp[3];
+    for (int rt = 0; rt < 2; ++rt) {
+      bf16x8 bp[3];
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          bp[q] = *reinterpret_cast<const bf16x8*>(
-              &L.u.a.ring[slot][q][(32 * rt + li) * W_LDB + 16 * s + 8 * lh]);
-        acc[rt] = prod6(wa, bp, acc[rt]);
-      }
-      if (s == 1 && j + 1 < W_NCK) produce(j + 1);
-    }
-    __syncthreads();  // slot j & 1 free; chunk j + 1 in slot (j + 1) & 1
-  }
-
-  // ---- layer-2 epilogue: bias, ReLU, kept rows to h[1], parts to the h2
-  // image (over the ring: every wave passed the loop's last barrier)
-  {
-    const float* b1 = d.b[1] + c * d.sb[1];
-#pragma unroll
-    for (int R = 0; R < 4; ++R) {
-      const int u = 32 * w + 8 * R + 4 * lh;
-      const float4 bv = *reinterpret_cast<const float4*>(b1 + u);
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        const int rl = 32 * rt + li;
-        const int row = m0 + rl;
-        float v[4] = {fmaxf(acc[rt][4 * R + 0] + bv.x, 0.f), fmaxf(acc[rt][4 * R + 1] + bv.y, 0.f),
-                      fmaxf(acc[rt][4 * R + 2] + bv.z, 0.f), fmaxf(acc[rt][4 * R + 3] + bv.w, 0.f)};
-        if (h1g != nullptr && row >= h_from && row < rend)
-          *reinterpret_cast<float4*>(h1g + row * W_H + u) = make_float4(v[0], v[1], v[2], v[3]);
-        bf16x4 p[3];
-        split4(v, p);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&L.u.h2[q][rl * W_LDH + u]) = p[q];
-      }
+      for (int q = 0; q < 3; ++q)
+        bp[q] = *reinterpret_cast<const bf16x8*>(&L.x[q][(32 * rt + li) * XLD + 16 * s + 8 * lh]);
+      o[rt] = prod6(wa, bp, o[rt]);
     }
   }
-  __syncthreads();  // h2 image complete
+  act_to_image<KEEP>(o, b0v, h0g, m0, h_from, rend, w, li, lh, L.img);
+  __syncthreads();  // image 1 complete
+  stamp(3);
 
-  // ---- head: wave w computes outputs 32 w .. + 31 (A = Wh rows, B = h2 image)
-  const int nkt = (nout + 31) / 32;
+  // ---- layer 2: units 32 w .. over the image; the head's first weight
+  // steps follow in the freed slots
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
+  stream256(W1r, w < nkt ? whr : nullptr, hr, L.img, li, lh, o);
+  stamp(4);
+  __syncthreads();  // every wave done reading image 1
+  act_to_image<KEEP>(o, b1v, h1g, m0, h_from, rend, w, li, lh, L.img);
+  // head bias of this lane's outputs 32 w + 8 R + 4 lh + i (clamped index)
+  float bhv[4][4];
+#pragma unroll
+  for (int R = 0; R < 4; ++R)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bhv[R][i] = bh[min(32 * w + 8 * R + 4 * lh + i, nout - 1)];
+  __syncthreads();  // image 2 complete
+  stamp(5);
+
+  // ---- head: wave w < nkt computes outputs 32 w .. + 31
   if (w < nkt) {
-    const int kout = 32 * w + li;  // A-operand row (output) of this lane
-    const bool kok = kout < nout;
-    const float* whr = Wh + (kok ? kout : 0) * W_H + 8 * lh;
-    f32x16 o[2];
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
-    // raw fp32 Wh of k steps s .. s + HD - 1 in flight (an L2 round trip is
-    // longer than two steps' twelve MFMAs)
-    constexpr int HD = 4;
-    float4 hr[HD][2];
-    auto load_h = [&](int s, int slot) {
-      hr[slot][0] = kok ? *reinterpret_cast<const float4*>(whr + 16 * s) : make_float4(0.f, 0.f, 0.f, 0.f);
-      hr[slot][1] = kok ? *reinterpret_cast<const float4*>(whr + 16 * s + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    };
-#pragma unroll
-    for (int s = 0; s < HD; ++s) load_h(s, s);
-#pragma unroll
-    for (int s = 0; s < W_H / 16; ++s) {
-      bf16x8 wa[3];
-      const int sl = s % HD;
-      const float v[8] = {hr[sl][0].x, hr[sl][0].y, hr[sl][0].z, hr[sl][0].w,
-                          hr[sl][1].x, hr[sl][1].y, hr[sl][1].z, hr[sl][1].w};
-      split8(v, wa);
-      if (s + HD < W_H / 16) load_h(s + HD, sl);
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        bf16x8 bp[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          bp[q] = *reinterpret_cast<const bf16x8*>(&L.u.h2[q][(32 * rt + li) * W_LDH + 16 * s + 8 * lh]);
-        o[rt] = prod6(wa, bp, o[rt]);
-      }
-    }
+    stream256(whr, nullptr, hr, L.img, li, lh, o);
+    stamp(6);
     // lane: row 32 rt + li, outputs 32 w + 8 R + 4 lh + i
     const int64_t ldo = d.ldout;
     float rsum[2] = {0.f, 0.f};  // row_mean: this lane's outputs, in output order
@@ -290,7 +258,7 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
       const int k0 = 32 * w + 8 * R + 4 * lh;
       float bv[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bv[i] = k0 + i < nout ? bh[k0 + i] : 0.f;
+      for (int i = 0; i < 4; ++i) bv[i] = k0 + i < nout ? bhv[R][i] : 0.f;
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         const int row = m0 + 32 * rt + li;
@@ -331,6 +299,7 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
       if (row < rend) d.row_mean[c * d.s_mean + row] = s / (float)nout;
     }
   }
+  stamp(7);
 }
 
 }  // namespace
@@ -371,10 +340,33 @@ extern "C" int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
   if (d.rows == 0) return 0;
   const dim3 grid((unsigned)((d.rows + W_RB - 1) / W_RB), 1, (unsigned)d.C);
   const hipStream_t st = (hipStream_t)stream;
-  if (d.n_in <= 32)
-    hipLaunchKernelGGL(mlp_x6_wide_kernel<32>, grid, dim3(512), 0, st, d);
+  static const bool stamps = [] {
+    const char* e = getenv("D3A_WIDE_STAMPS");
+    return e && atoi(e) != 0;
+  }();
+  const bool keep = d.h[0] != nullptr || d.h[1] != nullptr;
+  if (stamps && d.n_in <= 32 && !keep)
+    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false, true>), grid, dim3(512), 0, st, d);
+  else if (d.n_in <= 32 && keep)
+    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, true>), grid, dim3(512), 0, st, d);
+  else if (d.n_in <= 32)
+    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false>), grid, dim3(512), 0, st, d);
+  else if (keep)
+    hipLaunchKernelGGL((mlp_x6_wide_kernel<64, true>), grid, dim3(512), 0, st, d);
   else
-    hipLaunchKernelGGL(mlp_x6_wide_kernel<64>, grid, dim3(512), 0, st, d);
+    hipLaunchKernelGGL((mlp_x6_wide_kernel<64, false>), grid, dim3(512), 0, st, d);
   D3A_LAUNCH_CHECK("d3a_mlp_fwd_x6");
+  return 0;
+}
+
+// diagnostic (synchronous, not for graphs): the stamps of the last
+// D3A_WIDE_STAMPS=1 launch, [workgroup][8]
+extern "C" int d3a_wide_stamps(unsigned long long* dst, int n) {
+  D3A_CHECK_ARG(dst && n >= 0 && n <= 1024 * W_NST, "d3a_wide_stamps: bad arguments");
+  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(d3a::wide_stamps), (size_t)n * 8, 0,
+                          hipMemcpyDeviceToHost) != hipSuccess) {
+    set_error("d3a_wide_stamps: copy failed");
+    return -1;
+  }
   return 0;
 }

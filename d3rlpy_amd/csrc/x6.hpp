@@ -135,5 +135,54 @@ __device__ __forceinline__ float input_at(const d3a_mlp_fwd_desc& d, const float
   }
 }
 
+// input_at for features k4 .. k4 + 3 of row r, zero past nin / rend, without
+// branches around the loads: every load comes from clamped (in-range)
+// indices and is issued before any is used, so the row costs one memory round
+// trip and the compiler's wait counts stay exact (a load under a divergent
+// branch makes it wait for every load in flight, prefetches included)
+__device__ __forceinline__ void input4_at(const d3a_mlp_fwd_desc& d, const float* xb, int64_t ldx, int r,
+                                          int k4, int rend, int nin, float v[4]) {
+  const bool rok = r < rend;
+  const int rr = rok ? r : rend - 1;
+  int kc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) kc[j] = min(k4 + j, nin - 1);
+  if (d.xg_mode == 0) {
+    float raw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) raw[j] = xb[(int64_t)rr * ldx + kc[j]];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (rok && k4 + j < nin) ? raw[j] : 0.f;
+    return;
+  }
+  const int D = d.xg_D;
+  const float* orow = d.xg_obs + (int64_t)(rr / d.xg_rep) * D;
+  const float* arow = d.xg_a + (int64_t)rr * d.xg_lda;
+  float ob[4], a[4], bs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = max(kc[j] - D, 0);
+    ob[j] = orow[min(kc[j], D - 1)];
+    a[j] = arow[e];
+  }
+  if (d.xg_mode >= 3) {
+    const float* brow = d.xg_base + (int64_t)rr * d.xg_E;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bs[j] = brow[max(kc[j] - D, 0)];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float y;
+    switch (d.xg_mode) {
+      case 1: y = fminf(fmaxf(a[j], -d.xg_clip), d.xg_clip); break;
+      case 2: y = tanhf(a[j]); break;
+      case 3: y = fminf(fmaxf(__fadd_rn(bs[j], __fmul_rn(d.xg_scale, tanhf(a[j]))), -1.f), 1.f); break;
+      default:
+        y = fminf(fmaxf(__fadd_rn(tanhf(bs[j]), __fmul_rn(d.xg_scale, tanhf(a[j]))), -1.f), 1.f);
+    }
+    v[j] = (rok && k4 + j < nin) ? (k4 + j < D ? ob[j] : y) : 0.f;
+  }
+}
+
 }  // namespace x6
 }  // namespace d3a

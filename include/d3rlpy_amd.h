@@ -426,6 +426,10 @@ int d3a_q2_fwd_x1(const d3a_mlp_fwd_desc* d, void* stream);
  * and parts; e.g. BCQ's target QR critics over B*N sampled actions
  * (bcq_impl.py:215-226, qr_q_function.py:97-161). */
 int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* d, void* stream);
+/* Diagnostic (synchronous, not for graphs): the phase stamps ([workgroup][6]
+ * s_memtime values) of the last d3a_mlp_fwd_x6 launch made with
+ * D3A_WIDE_STAMPS=1 in the environment. */
+int d3a_wide_stamps(unsigned long long* dst, int n);
 /* Diagnostic (synchronous, not for graphs): the phase-boundary s_memtime
  * stamps of the last d3a_q2_fwd_x6 launch built with D3A_X6_PROBE bit 4. */
 int d3a_x6_stamps(unsigned long long* dst, int n);
