@@ -28,6 +28,7 @@
 // produced chunk by chunk inside the layer-2 loop, a barrier per chunk) at
 // 71k cycles per workgroup, of which 12.5k were the interleaved production
 // and 3.4k its barriers (tools/bench_wide.py ablations).
+#include <algorithm>
 #include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
@@ -41,55 +42,110 @@ using namespace x6;
 constexpr int W_H = 256;    // hidden width
 constexpr int W_RB = 64;    // rows per workgroup
 constexpr int W_LDH = 264;  // bf16 stride of an image row (528 B)
-constexpr int W_HD = 4;     // weight k steps in flight
+// weight k steps in flight (8 registers a step).  It divides the 16 steps of
+// a stream: the refills at a stream's end leave the next stream's steps
+// 0 .. W_HD - 1 in slots 0 .. W_HD - 1.
+constexpr int W_HD = 4;
+static_assert(16 % W_HD == 0, "W_HD must divide 16");
 
 template <int XL>
 struct WideLds {
   __bf16 x[3][W_RB * (XL + 8)];  // input parts [row][k]
-  __bf16 img[3][W_RB * W_LDH];   // layer-1, then layer-2 activation parts [row][unit]
+  // layer-1, then layer-2 activation parts [row][part][unit]: the parts of a
+  // row adjacent, so every read of a lane's two row tiles lies within 64 KB
+  // of one base (one address register + immediate offsets)
+  __bf16 img[W_RB * 3 * W_LDH];
   float rs[8][W_RB];             // row_mean: per-wave output sums [wave][row]
 };
 
 // diagnostic phase stamps (STAMPS, D3A_WIDE_STAMPS=1; read with
-// d3a_wide_stamps): wave 0 of each workgroup records s_memtime at 0 start,
-// 1 input staged, 2 its barrier passed, 3 image 1 written, 4 layer-2 products
-// issued, 5 image 2 written, 6 head products issued, 7 outputs stored
-constexpr int W_NST = 8;
+// d3a_wide_stamps): wave 0 of each workgroup records s_memtime in its
+// second tile (the steady state) at 0 the tile's start, 1 before the input
+// barrier, 2 after it, 3 image 1 written, 4 layer-2 products issued, 5 image
+// 2 written, 6 head products issued, 7 outputs stored; 8 = the kernel's end
+// minus its start (the workgroup's whole lifetime)
+constexpr int W_NST = 9;
 __device__ unsigned long long wide_stamps[1024 * W_NST];
 
+// a weight matrix as a buffer resource: raw buffer loads are ordered by the
+// compiler fences below (plain loads of read-only weights are free to sink to
+// their first use, undoing the prefetch), and an offset past the matrix
+// reads zero
+struct WMat {
+  __amdgpu_buffer_rsrc_t rs;
+};
+__device__ __forceinline__ WMat wmat(const void* base, int bytes) {
+  return WMat{__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000)};
+}
+// (lane offset in voffset, the step's constant in soffset: a constant in
+// voffset gets its own register per step)
+__device__ __forceinline__ float4 wload(const WMat& m, int lane_off, int step_off) {
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  const f32x4v v =
+      __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(m.rs, lane_off, step_off, 0));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // o[rt] += W[32 rows][256] x img[64 rows][256]^T for this lane's weight row
-// (wrow = row + 8 lh): hr holds the raw fp32 of k steps 0 .. W_HD - 1 on entry;
-// each step splits its slot, refills it W_HD steps ahead, then issues twelve
-// MFMAs.  With next != nullptr the freed slots are refilled with steps
-// 0 .. W_HD - 1 of the next stream (the head's rows) instead.
-__device__ __forceinline__ void stream256(const float* wrow, const float* next, float4 (&hr)[W_HD][2],
-                                          const __bf16 (&img)[3][W_RB * W_LDH], int li, int lh,
-                                          f32x16 (&o)[2]) {
-#pragma unroll
-  for (int s = 0; s < W_H / 16; ++s) {
-    bf16x8 wa[3];
-    const int sl = s % W_HD;
+// (byte offset wo of its k = 8 lh in matrix wm): hr holds the raw fp32 of k
+// steps 0 .. w_hd - 1 on entry and, on exit, steps 0 .. w_hd - 1 of the row at
+// (nm, no) (the stream that follows).  Software-pipelined by hand: step s
+// issues step s + 1's image reads and weight split (and the refill of the
+// slot that split frees) ahead of its own twelve MFMAs; a compiler memory
+// fence closes each step, and the schedule interleaves the split's vector
+// instructions into the MFMA gaps (an MFMA issues 32 cycles, holding the
+// vector issue for 8 of them).
+__device__ __forceinline__ void stream256(const WMat& wm, int wo, const WMat& nm, int no,
+                                          float4 (&hr)[W_HD][2], const __bf16 (&img)[W_RB * 3 * W_LDH],
+                                          int li, int lh, f32x16 (&o)[2]) {
+  constexpr int NS = W_H / 16;
+  auto split_slot = [&](int sl, bf16x8 (&wa)[3]) {
     const float v[8] = {hr[sl][0].x, hr[sl][0].y, hr[sl][0].z, hr[sl][0].w,
                         hr[sl][1].x, hr[sl][1].y, hr[sl][1].z, hr[sl][1].w};
     split8(v, wa);
-    if (s + W_HD < W_H / 16) {
-      hr[sl][0] = *reinterpret_cast<const float4*>(wrow + 16 * (s + W_HD));
-      hr[sl][1] = *reinterpret_cast<const float4*>(wrow + 16 * (s + W_HD) + 4);
-    } else if (next != nullptr) {
-      const int s2 = s + W_HD - W_H / 16;
-      hr[sl][0] = *reinterpret_cast<const float4*>(next + 16 * s2);
-      hr[sl][1] = *reinterpret_cast<const float4*>(next + 16 * s2 + 4);
-    }
-    // keep the refill here: the scheduler would sink it to its first use
-    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto refill = [&](int s) {  // the slot of step s, with step s + W_HD
+    const int sl = s % W_HD, s2 = s + W_HD;
+    const WMat& m = s2 < NS ? wm : nm;
+    const int lo = s2 < NS ? wo : no, st = 64 * (s2 < NS ? s2 : s2 - NS);
+    hr[sl][0] = wload(m, lo, st);
+    hr[sl][1] = wload(m, lo, st + 16);
+  };
+  auto read_img = [&](int s, bf16x8 (&bp)[2][3]) {
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      bf16x8 bp[3];
+    for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        bp[q] = *reinterpret_cast<const bf16x8*>(&img[q][(32 * rt + li) * W_LDH + 16 * s + 8 * lh]);
-      o[rt] = prod6(wa, bp, o[rt]);
+        bp[rt][q] = *reinterpret_cast<const bf16x8*>(&img[((32 * rt + li) * 3 + q) * W_LDH + 16 * s + 8 * lh]);
+  };
+  bf16x8 wa[2][3], bp[2][2][3];
+  split_slot(0, wa[0]);
+  refill(0);
+  read_img(0, bp[0]);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int cur = s & 1, nx = cur ^ 1;
+    if (s + 1 < NS) {
+      read_img(s + 1, bp[nx]);
+      split_slot((s + 1) % W_HD, wa[nx]);
+      refill(s + 1);
     }
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) o[rt] = prod6(wa[cur], bp[cur][rt], o[rt]);
+    if (s + 1 < NS) {
+      __builtin_amdgcn_sched_group_barrier(0x0100, 6, 0);  // next step's image reads
+      __builtin_amdgcn_sched_group_barrier(0x0020, 2, 0);  // the refill
+#pragma unroll
+      for (int m = 0; m < 12; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);  // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x0002, 4, 0);  // up to four vector instructions
+      }
+    }
+    // a compiler memory fence: the next step's reads stay in this step
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -98,7 +154,7 @@ __device__ __forceinline__ void stream256(const float* wrow, const float* next, 
 template <bool KEEP>
 __device__ __forceinline__ void act_to_image(const f32x16 (&o)[2], const float4 (&bv)[4], float* hg, int m0,
                                              int h_from, int rend, int w, int li, int lh,
-                                             __bf16 (&img)[3][W_RB * W_LDH]) {
+                                             __bf16 (&img)[W_RB * 3 * W_LDH]) {
 #pragma unroll
   for (int R = 0; R < 4; ++R) {
     const int u = 32 * w + 8 * R + 4 * lh;
@@ -113,25 +169,41 @@ __device__ __forceinline__ void act_to_image(const f32x16 (&o)[2], const float4 
       bf16x4 p[3];
       split4(v, p);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&img[q][rl * W_LDH + u]) = p[q];
+      for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&img[(rl * 3 + q) * W_LDH + u]) = p[q];
     }
   }
 }
 
 // XL: n_in rounded up to 32 (32 or 64); KEEP: some kept activations (h[0] /
-// h[1]) are written (without them no store precedes the head's)
+// h[1]) are written (without them no store precedes the head's).
+//
+// Persistent: grid (G, 1, C), G <= the CU count / C, one workgroup per CU
+// (the LDS image allows no second).  Member c's rows are cut into 32-row
+// halves, workgroup k owning the contiguous range [k H / G, (k + 1) H / G)
+// of its H halves, processed as 64-row tiles (a last odd half as a
+// 32-row tile with the second row tile masked): every workgroup carries
+// 2-3.5 tiles' work instead of whole 64-row blocks dealt in rounds (3.125
+// rounds of 256 at K3's 800 blocks = 4 rounds).  While tile i runs its layer 2
+// and head, the next tile's input rows and first weight steps are in flight
+// (XRaw4 registers, the freed slots of the weight stream), so only the first
+// tile pays the prologue's memory round trip.
 template <int XL, bool KEEP, bool STAMPS = false>
 __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
   constexpr int XLD = XL + 8;
   constexpr int NS1 = XL / 16;  // layer-1 k steps
+  constexpr int X4 = XL / 4;
+  constexpr int NXQ = (W_RB * X4 + 511) / 512;  // input quads per thread
   __shared__ __attribute__((aligned(16))) WideLds<XL> L;
   static_assert(sizeof(WideLds<XL>) <= 163840, "LDS");
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int li = lane & 31, lh = lane >> 5;
   const int c = blockIdx.z;
-  const int m0 = (int)d.r0 + (int)blockIdx.x * W_RB;
-  const int rend = (int)(d.r0 + d.rows);
+  const int r0 = (int)d.r0, rlim = (int)(d.r0 + d.rows);
+  const int nh = (int)((d.rows + 31) / 32);  // 32-row halves of this member
+  const int G = (int)gridDim.x, k = (int)blockIdx.x;
+  const int hb = (int)((int64_t)k * nh / G), he = (int)((int64_t)(k + 1) * nh / G);
+  if (hb >= he) return;  // uniform: no rows for this workgroup
   const int h_from = (int)d.h_from;
   const int nin = d.n_in, nout = d.n_out;
   float* const outp = d.out + c * d.sout;
@@ -139,167 +211,216 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
   float* const h1g = KEEP && d.h[1] ? d.h[1] + c * d.sh : nullptr;
   const int u0 = 32 * w + li;  // this lane's weight row in layers 1 and 2
   const float* W0r = d.W[0] + c * d.sW[0] + u0 * nin;
-  const float* W1r = d.W[1] + c * d.sW[1] + u0 * W_H + 8 * lh;
+  const WMat W1m = wmat(d.W[1] + c * d.sW[1], W_H * W_H * 4);
+  const int w1o = (u0 * W_H + 8 * lh) * 4;  // byte offset of this lane's W1 row piece
   const float* b0 = d.b[0] + c * d.sb[0];
   const float* b1 = d.b[1] + c * d.sb[1];
   const float* Wh = d.W[2] + c * d.sW[2];
   const float* bh = d.b[2] + c * d.sb[2];
+  const float* xb = d.x + c * d.sxb;
+  const int64_t ldx = d.ldx;
   const int nkt = (nout + 31) / 32;
   const int kout = 32 * w + li;  // head: this lane's output row (rows past n_out read row 0:
-  const float* whr = Wh + (kout < nout ? kout : 0) * W_H + 8 * lh;  // never stored)
+  const WMat Whm = wmat(Wh, nout * W_H * 4);
+  const int who = ((kout < nout ? kout : 0) * W_H + 8 * lh) * 4;  // never stored)
   const int wgi = blockIdx.x + blockIdx.z * gridDim.x;
-  auto stamp = [&](int k) {
+  const unsigned long long t_start = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto stamp = [&](int s, bool on) {
     if constexpr (STAMPS) {
       __builtin_amdgcn_sched_barrier(0);
-      if (t == 0 && wgi < 1024) wide_stamps[wgi * W_NST + k] = __builtin_amdgcn_s_memtime();
+      if (on && t == 0 && wgi < 1024) wide_stamps[wgi * W_NST + s] = __builtin_amdgcn_s_memtime();
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  stamp(0);
 
-  // ---- prologue: layer-2 weight steps 0 .. W_HD - 1, the layer-1 weight row
-  // (clamped k, masked at use) and both biases in flight; input rows split
-  // into LDS (input4_at: every load issued before any is used)
+  // the tile starting at half h: rows [r0 + 32 h, tile_end)
+  auto tile_end = [&](int h) { return min(r0 + 32 * min(h + 2, he), rlim); };
+  XRaw4 xr[NXQ];
+  // (the lane-dependent index arithmetic of the tile loop works from a
+  // laundered thread index: hoisted out of the loop, its clamped indices and
+  // lane predicates would occupy registers across the whole loop)
+  auto opaque = [](int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+  auto issue_x = [&](int h) {
+    const int m0 = r0 + 32 * h, te = tile_end(h);
+    const int tl = opaque(t);
+#pragma unroll
+    for (int q = 0; q < NXQ; ++q) {
+      const int e = tl + 512 * q;
+      const int m = min(e / X4, W_RB - 1), k4 = (e % X4) * 4;
+      input4_issue(d, xb, ldx, m0 + m, k4, te, nin, xr[q]);
+    }
+  };
+  auto stage_x = [&](int h) {
+    const int m0 = r0 + 32 * h, te = tile_end(h);
+    const int tl = opaque(t);
+#pragma unroll
+    for (int q = 0; q < NXQ; ++q) {
+      const int e = tl + 512 * q;
+      if (e < W_RB * X4) {
+        const int m = e / X4, k4 = (e % X4) * 4;
+        float v[4];
+        input4_finish(d, m0 + m, k4, te, nin, xr[q], v);
+        bf16x4 p[3];
+        split4(v, p);
+#pragma unroll
+        for (int q3 = 0; q3 < 3; ++q3) *reinterpret_cast<bf16x4*>(&L.x[q3][m * XLD + k4]) = p[q3];
+      }
+    }
+  };
+
+  // ---- prologue: layer-2 weight steps 0 .. w_hd - 1 and the first tile's rows
   float4 hr[W_HD][2];
 #pragma unroll
   for (int s = 0; s < W_HD; ++s) {
-    hr[s][0] = *reinterpret_cast<const float4*>(W1r + 16 * s);
-    hr[s][1] = *reinterpret_cast<const float4*>(W1r + 16 * s + 4);
+    hr[s][0] = wload(W1m, w1o, 64 * s);
+    hr[s][1] = wload(W1m, w1o, 64 * s + 16);
   }
-  float w0r[NS1][8];
-#pragma unroll
-  for (int s = 0; s < NS1; ++s)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w0r[s][i] = W0r[min(16 * s + 8 * lh + i, nin - 1)];
-  float4 b0v[4], b1v[4];
-#pragma unroll
-  for (int R = 0; R < 4; ++R) {
-    b0v[R] = *reinterpret_cast<const float4*>(b0 + 32 * w + 8 * R + 4 * lh);
-    b1v[R] = *reinterpret_cast<const float4*>(b1 + 32 * w + 8 * R + 4 * lh);
-  }
-  {
-    const float* xb = d.x + c * d.sxb;
-    const int64_t ldx = d.ldx;
-    constexpr int X4 = XL / 4;
-    for (int e = t; e < W_RB * X4; e += 512) {
-      const int m = e / X4, k4 = (e - m * X4) * 4;
-      float v[4];
-      input4_at(d, xb, ldx, m0 + m, k4, rend, nin, v);
-      bf16x4 p[3];
-      split4(v, p);
-#pragma unroll
-      for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&L.x[q][m * XLD + k4]) = p[q];
-    }
-  }
-  stamp(1);
-  __syncthreads();  // input parts staged
-  stamp(2);
+  issue_x(hb);
+  stage_x(hb);
 
-  // ---- layer 1: units 32 w .. over K = XL (x parts past n_in are zero, the
-  // weights there masked to zero)
-  f32x16 o[2];
+  for (int h = hb; h < he; h += 2) {  // uniform
+    const int m0 = r0 + 32 * h, rend = tile_end(h);
+    const bool has_next = h + 2 < he;
+    const bool first = h == hb + 2;  // the stamped tile
+    stamp(0, first);
+    // the layer-1 weight row (clamped k, masked at use) and bias, reloaded per
+    // tile (L2 hits) so that no register holds them across the streams; a
+    // wave reaching this point early waits at the barrier anyway
+    const int lhl = opaque(lh);
+    float w0r[NS1][8];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+    for (int s = 0; s < NS1; ++s)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
+      for (int i = 0; i < 8; ++i) w0r[s][i] = W0r[min(16 * s + 8 * lhl + i, nin - 1)];
+    float4 b0v[4];
 #pragma unroll
-  for (int s = 0; s < NS1; ++s) {
-    float v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = 16 * s + 8 * lh + i < nin ? w0r[s][i] : 0.f;
-    bf16x8 wa[3];
-    split8(v, wa);
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      bf16x8 bp[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        bp[q] = *reinterpret_cast<const bf16x8*>(&L.x[q][(32 * rt + li) * XLD + 16 * s + 8 * lh]);
-      o[rt] = prod6(wa, bp, o[rt]);
-    }
-  }
-  act_to_image<KEEP>(o, b0v, h0g, m0, h_from, rend, w, li, lh, L.img);
-  __syncthreads();  // image 1 complete
-  stamp(3);
+    for (int R = 0; R < 4; ++R) b0v[R] = *reinterpret_cast<const float4*>(b0 + 32 * w + 8 * R + 4 * lh);
+    stamp(1, first);
+    __syncthreads();  // input parts staged; the previous head done with the image
+    stamp(2, first);
 
-  // ---- layer 2: units 32 w .. over the image; the head's first weight
-  // steps follow in the freed slots
-#pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
-  stream256(W1r, w < nkt ? whr : nullptr, hr, L.img, li, lh, o);
-  stamp(4);
-  __syncthreads();  // every wave done reading image 1
-  act_to_image<KEEP>(o, b1v, h1g, m0, h_from, rend, w, li, lh, L.img);
-  // head bias of this lane's outputs 32 w + 8 R + 4 lh + i (clamped index)
-  float bhv[4][4];
-#pragma unroll
-  for (int R = 0; R < 4; ++R)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bhv[R][i] = bh[min(32 * w + 8 * R + 4 * lh + i, nout - 1)];
-  __syncthreads();  // image 2 complete
-  stamp(5);
-
-  // ---- head: wave w < nkt computes outputs 32 w .. + 31
-  if (w < nkt) {
+    // ---- layer 1: units 32 w .. over K = XL (x parts past n_in are zero, the
+    // weights there masked to zero)
+    f32x16 o[2];
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
-    stream256(whr, nullptr, hr, L.img, li, lh, o);
-    stamp(6);
-    // lane: row 32 rt + li, outputs 32 w + 8 R + 4 lh + i
-    const int64_t ldo = d.ldout;
-    float rsum[2] = {0.f, 0.f};  // row_mean: this lane's outputs, in output order
-    const bool vec = ((reinterpret_cast<uintptr_t>(outp) & 15) == 0) && (ldo & 3) == 0;
 #pragma unroll
-    for (int R = 0; R < 4; ++R) {
-      const int k0 = 32 * w + 8 * R + 4 * lh;
-      float bv[4];
+    for (int s = 0; s < NS1; ++s) {
+      float v[8];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bv[i] = k0 + i < nout ? bhv[R][i] : 0.f;
+      for (int i = 0; i < 8; ++i) v[i] = 16 * s + 8 * lhl + i < nin ? w0r[s][i] : 0.f;
+      bf16x8 wa[3];
+      split8(v, wa);
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
-        const int row = m0 + 32 * rt + li;
-        if (row >= rend) continue;
-        float* op = outp + (int64_t)row * ldo + k0;
-        const float v0 = o[rt][4 * R] + bv[0], v1 = o[rt][4 * R + 1] + bv[1];
-        const float v2 = o[rt][4 * R + 2] + bv[2], v3 = o[rt][4 * R + 3] + bv[3];
-        if (k0 + 0 < nout) rsum[rt] += v0;
-        if (k0 + 1 < nout) rsum[rt] += v1;
-        if (k0 + 2 < nout) rsum[rt] += v2;
-        if (k0 + 3 < nout) rsum[rt] += v3;
-        if (k0 + 3 < nout && vec) {
-          *reinterpret_cast<float4*>(op) = make_float4(v0, v1, v2, v3);
-        } else {
-          if (k0 + 0 < nout) op[0] = v0;
-          if (k0 + 1 < nout) op[1] = v1;
-          if (k0 + 2 < nout) op[2] = v2;
-          if (k0 + 3 < nout) op[3] = v3;
+        bf16x8 bp[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          bp[q] = *reinterpret_cast<const bf16x8*>(&L.x[q][(32 * rt + li) * XLD + 16 * s + 8 * lh]);
+        o[rt] = prod6(wa, bp, o[rt]);
+      }
+    }
+    float4 b1v[4];
+#pragma unroll
+    for (int R = 0; R < 4; ++R) b1v[R] = *reinterpret_cast<const float4*>(b1 + 32 * w + 8 * R + 4 * lh);
+    act_to_image<KEEP>(o, b0v, h0g, m0, h_from, rend, w, li, lh, L.img);
+    __syncthreads();  // image 1 complete; every wave done reading the input parts
+    stamp(3, first);
+    if (has_next) issue_x(h + 2);  // uniform
+
+    // ---- layer 2: units 32 w .. over the image; the freed weight slots take
+    // the head's first steps (waves with no head: the next tile's layer 2)
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
+    {
+      const WMat nm{w < nkt ? Whm.rs : W1m.rs};  // uniform
+      stream256(W1m, w1o, nm, w < nkt ? who : w1o, hr, L.img, li, lh, o);
+    }
+    stamp(4, first);
+    __syncthreads();  // every wave done reading image 1
+    act_to_image<KEEP>(o, b1v, h1g, m0, h_from, rend, w, li, lh, L.img);
+    // head bias of this lane's outputs 32 w + 8 R + 4 lh + i (clamped index)
+    float bhv[4][4];
+#pragma unroll
+    for (int R = 0; R < 4; ++R)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bhv[R][i] = bh[min(32 * w + 8 * R + 4 * lhl + i, nout - 1)];
+    if (has_next) stage_x(h + 2);  // the input region is free since image 1
+    __syncthreads();  // image 2 complete
+    stamp(5, first);
+
+    // ---- head: wave w < nkt computes outputs 32 w .. + 31; its freed weight
+    // slots take the next tile's first layer-2 steps
+    if (w < nkt) {
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
+      stream256(Whm, who, W1m, w1o, hr, L.img, li, lh, o);
+      stamp(6, first);
+      // lane: row 32 rt + li, outputs 32 w + 8 R + 4 lh + i
+      const int64_t ldo = d.ldout;
+      float rsum[2] = {0.f, 0.f};  // row_mean: this lane's outputs, in output order
+      const bool vec = ((reinterpret_cast<uintptr_t>(outp) & 15) == 0) && (ldo & 3) == 0;
+      const int lho = opaque(lh), lio = opaque(li);
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const int k0 = 32 * w + 8 * R + 4 * lho;
+        float bv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bv[i] = k0 + i < nout ? bhv[R][i] : 0.f;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          const int row = m0 + 32 * rt + lio;
+          if (row >= rend) continue;
+          float* op = outp + (int64_t)row * ldo + k0;
+          const float v0 = o[rt][4 * R] + bv[0], v1 = o[rt][4 * R + 1] + bv[1];
+          const float v2 = o[rt][4 * R + 2] + bv[2], v3 = o[rt][4 * R + 3] + bv[3];
+          if (k0 + 0 < nout) rsum[rt] += v0;
+          if (k0 + 1 < nout) rsum[rt] += v1;
+          if (k0 + 2 < nout) rsum[rt] += v2;
+          if (k0 + 3 < nout) rsum[rt] += v3;
+          if (k0 + 3 < nout && vec) {
+            *reinterpret_cast<float4*>(op) = make_float4(v0, v1, v2, v3);
+          } else {
+            if (k0 + 0 < nout) op[0] = v0;
+            if (k0 + 1 < nout) op[1] = v1;
+            if (k0 + 2 < nout) op[2] = v2;
+            if (k0 + 3 < nout) op[3] = v3;
+          }
+        }
+      }
+      if (d.row_mean != nullptr) {
+        // the two lane halves hold interleaved runs of four outputs: the wave's
+        // 32 outputs of a row as (lane half 0's 16) + (lane half 1's 16)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          const float other = __shfl_xor(rsum[rt], 32, 64);
+          if (lh == 0) L.rs[w][32 * rt + li] = rsum[rt] + other;
         }
       }
     }
     if (d.row_mean != nullptr) {
-      // the two lane halves hold interleaved runs of four outputs: the wave's
-      // 32 outputs of a row as (lane half 0's 16) + (lane half 1's 16)
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        const float other = __shfl_xor(rsum[rt], 32, 64);
-        if (lh == 0) L.rs[w][32 * rt + li] = rsum[rt] + other;
+      __syncthreads();  // uniform: row_mean is a kernel argument
+      if (t < W_RB) {
+        float s = L.rs[0][t];
+        for (int v = 1; v < nkt; ++v) s += L.rs[v][t];
+        const int row = m0 + t;
+        if (row < rend) d.row_mean[c * d.s_mean + row] = s / (float)nout;
       }
     }
+    stamp(7, first);
   }
-  if (d.row_mean != nullptr) {
-    __syncthreads();  // uniform: row_mean is a kernel argument
-    if (t < W_RB) {
-      float s = L.rs[0][t];
-      for (int v = 1; v < nkt; ++v) s += L.rs[v][t];
-      const int row = m0 + t;
-      if (row < rend) d.row_mean[c * d.s_mean + row] = s / (float)nout;
-    }
+  if constexpr (STAMPS) {
+    if (t == 0 && wgi < 1024) wide_stamps[wgi * W_NST + 8] = __builtin_amdgcn_s_memtime() - t_start;
   }
-  stamp(7);
 }
 
 }  // namespace
@@ -338,7 +459,17 @@ extern "C" int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
                                           d.s_mean * (int64_t)d.C < (int64_t(1) << 31)),
                 "d3a_mlp_fwd_x6: row_mean member stride must cover the rows");
   if (d.rows == 0) return 0;
-  const dim3 grid((unsigned)((d.rows + W_RB - 1) / W_RB), 1, (unsigned)d.C);
+  // persistent: one workgroup per CU, the CUs shared between the members
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      n = 256;
+    return n;
+  }();
+  const int64_t halves = (d.rows + 31) / 32;
+  const int64_t g = std::min<int64_t>(std::max(1, n_cu / d.C), (halves + 1) / 2);
+  const dim3 grid((unsigned)g, 1, (unsigned)d.C);
   const hipStream_t st = (hipStream_t)stream;
   static const bool stamps = [] {
     const char* e = getenv("D3A_WIDE_STAMPS");
@@ -360,7 +491,7 @@ extern "C" int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
 }
 
 // diagnostic (synchronous, not for graphs): the stamps of the last
-// D3A_WIDE_STAMPS=1 launch, [workgroup][8]
+// D3A_WIDE_STAMPS=1 launch, [workgroup][9]
 extern "C" int d3a_wide_stamps(unsigned long long* dst, int n) {
   D3A_CHECK_ARG(dst && n >= 0 && n <= 1024 * W_NST, "d3a_wide_stamps: bad arguments");
   if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(d3a::wide_stamps), (size_t)n * 8, 0,

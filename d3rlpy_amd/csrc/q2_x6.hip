@@ -186,8 +186,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? fv[j] : 0.f;
       } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? input_at(d, xb, ldx, r, k4 + j) : 0.f;
+        input4_at(d, xb, ldx, r, k4, rend, nin, v);
       }
       bf16x4 p[NP];
       splitn4<NP>(v, p);

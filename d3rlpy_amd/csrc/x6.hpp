@@ -111,77 +111,77 @@ inline bool xgen_ok(const d3a_mlp_fwd_desc& d) {
          (d.xg_mode < 3 || d.xg_base != nullptr);
 }
 
-// element k of input row r of a forward pass: x itself, or the row the
-// descriptor's builder defines (d3a_mlp_fwd_desc.xg_mode; d3a_bcq_rows's
-// arithmetic, bcq.hip)
-__device__ __forceinline__ float input_at(const d3a_mlp_fwd_desc& d, const float* xb, int64_t ldx,
-                                          int r, int k) {
-  if (d.xg_mode == 0) return xb[(int64_t)r * ldx + k];
-  if (k < d.xg_D) return d.xg_obs[(int64_t)(r / d.xg_rep) * d.xg_D + k];
-  const int e = k - d.xg_D;
-  const float a = d.xg_a[(int64_t)r * d.xg_lda + e];
-  switch (d.xg_mode) {
-    case 1: return fminf(fmaxf(a, -d.xg_clip), d.xg_clip);
-    case 2: return tanhf(a);
-    case 3: {
-      const float res = __fmul_rn(d.xg_scale, tanhf(a));
-      return fminf(fmaxf(__fadd_rn(d.xg_base[(int64_t)r * d.xg_E + e], res), -1.f), 1.f);
-    }
-    default: {
-      const float res = __fmul_rn(d.xg_scale, tanhf(a));
-      const float base = tanhf(d.xg_base[(int64_t)r * d.xg_E + e]);
-      return fminf(fmaxf(__fadd_rn(base, res), -1.f), 1.f);
-    }
-  }
-}
-
-// input_at for features k4 .. k4 + 3 of row r, zero past nin / rend, without
+// features k4 .. k4 + 3 of input row r of a forward pass, zero past nin /
+// rend: x itself, or the row the descriptor's builder defines
+// (d3a_mlp_fwd_desc.xg_mode; d3a_bcq_rows's arithmetic, bcq.hip).  No
 // branches around the loads: every load comes from clamped (in-range)
 // indices and is issued before any is used, so the row costs one memory round
 // trip and the compiler's wait counts stay exact (a load under a divergent
-// branch makes it wait for every load in flight, prefetches included)
-__device__ __forceinline__ void input4_at(const d3a_mlp_fwd_desc& d, const float* xb, int64_t ldx, int r,
-                                          int k4, int rend, int nin, float v[4]) {
-  const bool rok = r < rend;
-  const int rr = rok ? r : rend - 1;
+// branch makes it wait for every load in flight, prefetches included).
+// input4_issue only loads (the raw operands, to be finished later: a
+// persistent kernel prefetches its next tile's rows that way).
+struct XRaw4 {
+  float ob[4], a[4], bs[4];
+};
+
+__device__ __forceinline__ void input4_issue(const d3a_mlp_fwd_desc& d, const float* xb, int64_t ldx, int r,
+                                             int k4, int rend, int nin, XRaw4& x) {
+  const int rr = r < rend ? r : rend - 1;
   int kc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) kc[j] = min(k4 + j, nin - 1);
   if (d.xg_mode == 0) {
-    float raw[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) raw[j] = xb[(int64_t)rr * ldx + kc[j]];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (rok && k4 + j < nin) ? raw[j] : 0.f;
+    for (int j = 0; j < 4; ++j) {
+      x.ob[j] = xb[(int64_t)rr * ldx + kc[j]];
+      x.a[j] = x.bs[j] = 0.f;
+    }
     return;
   }
   const int D = d.xg_D;
   const float* orow = d.xg_obs + (int64_t)(rr / d.xg_rep) * D;
   const float* arow = d.xg_a + (int64_t)rr * d.xg_lda;
-  float ob[4], a[4], bs[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int e = max(kc[j] - D, 0);
-    ob[j] = orow[min(kc[j], D - 1)];
-    a[j] = arow[e];
+    x.ob[j] = orow[min(kc[j], D - 1)];
+    x.a[j] = arow[max(kc[j] - D, 0)];
+    x.bs[j] = 0.f;
   }
   if (d.xg_mode >= 3) {
     const float* brow = d.xg_base + (int64_t)rr * d.xg_E;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bs[j] = brow[max(kc[j] - D, 0)];
+    for (int j = 0; j < 4; ++j) x.bs[j] = brow[max(kc[j] - D, 0)];
   }
+}
+
+__device__ __forceinline__ void input4_finish(const d3a_mlp_fwd_desc& d, int r, int k4, int rend, int nin,
+                                              const XRaw4& x, float v[4]) {
+  const bool rok = r < rend;
+  if (d.xg_mode == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (rok && k4 + j < nin) ? x.ob[j] : 0.f;
+    return;
+  }
+  const int D = d.xg_D;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float y;
     switch (d.xg_mode) {
-      case 1: y = fminf(fmaxf(a[j], -d.xg_clip), d.xg_clip); break;
-      case 2: y = tanhf(a[j]); break;
-      case 3: y = fminf(fmaxf(__fadd_rn(bs[j], __fmul_rn(d.xg_scale, tanhf(a[j]))), -1.f), 1.f); break;
+      case 1: y = fminf(fmaxf(x.a[j], -d.xg_clip), d.xg_clip); break;
+      case 2: y = tanhf(x.a[j]); break;
+      case 3: y = fminf(fmaxf(__fadd_rn(x.bs[j], __fmul_rn(d.xg_scale, tanhf(x.a[j]))), -1.f), 1.f); break;
       default:
-        y = fminf(fmaxf(__fadd_rn(tanhf(bs[j]), __fmul_rn(d.xg_scale, tanhf(a[j]))), -1.f), 1.f);
+        y = fminf(fmaxf(__fadd_rn(tanhf(x.bs[j]), __fmul_rn(d.xg_scale, tanhf(x.a[j]))), -1.f), 1.f);
     }
-    v[j] = (rok && k4 + j < nin) ? (k4 + j < D ? ob[j] : y) : 0.f;
+    v[j] = (rok && k4 + j < nin) ? (k4 + j < D ? x.ob[j] : y) : 0.f;
   }
+}
+
+__device__ __forceinline__ void input4_at(const d3a_mlp_fwd_desc& d, const float* xb, int64_t ldx, int r,
+                                          int k4, int rend, int nin, float v[4]) {
+  XRaw4 x;
+  input4_issue(d, xb, ldx, r, k4, rend, nin, x);
+  input4_finish(d, r, k4, rend, nin, x, v);
 }
 
 }  // namespace x6

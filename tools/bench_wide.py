@@ -24,8 +24,8 @@ def main():
     bench.gpu_steps(algo, it, 5)
     torch.cuda.synchronize()
     launch, flops, desc = next(iter(algo.impl._ws.values())).dominant_kernel()
-    out = {"kernel": desc, "phase_names": ["loads+staging", "x barrier", "layer 1 + image 1", "layer 2",
-                                                  "image 2", "head", "stores + mean"]}
+    out = {"kernel": desc, "phase_names": ["second tile: weight reloads", "x barrier", "layer 1 + image 1",
+                                                  "layer 2", "image 2", "head", "stores + mean"]}
     # D3A_WIDE_ABL: 0 as built; 1 no W1 refetch, 2 no layer-1 production in the
     # loop, 4 no loop barriers, 8 no Wh refetch, 16 no input loads, 32 / 64 no
     # W1 / Wh split (timing only)
@@ -40,14 +40,18 @@ def main():
         ev[1].record()
         torch.cuda.synchronize()
         us = ev[0].elapsed_time(ev[1]) * 1000 / 20
-        n = 800 * 8
+        n = 1024 * 9
         buf = (ctypes.c_ulonglong * n)()
         assert N.lib().d3a_wide_stamps(buf, n) == 0
-        st = np.array(buf, dtype=np.float64).reshape(800, 8)
+        st = np.array(buf, dtype=np.float64).reshape(1024, 9)
+        st = st[st[:, 8] != 0]  # workgroups of this launch (the grid may be < 1024)
+        life = st[:, 8].copy()
+        st = st[st[:, 0] != 0][:, :8]  # ... with a second tile
         ph = np.diff(st, axis=1)
         out[f"abl{abl}"] = {"avg_us": round(us, 2),
                             "phase_cycles_mean": [round(float(v)) for v in ph.mean(0)],
-                            "wg_cycles_mean": round(float((st[:, 7] - st[:, 0]).mean()))}
+                            "tile_cycles_mean": round(float((st[:, 7] - st[:, 0]).mean())),
+                            "wg_cycles_mean": round(float(life.mean())), "wg_cycles_max": round(float(life.max()))}
     print(json.dumps(out, indent=1))
 
 

@@ -4,6 +4,7 @@ the median per dispatch over each kernel's dispatches, the wait / active
 fractions of the wave cycles, and MFMA-busy cycles per SIMD (1,024 SIMDs).
 
     python tools/pmc_sq_summary.py PMC_DIR > profiles/r04_pmc_sq_step_cql.txt
+    python tools/pmc_sq_summary.py PMC_DIR wide   # every counter's median, kernels matching "wide"
 """
 import csv
 import glob
@@ -26,6 +27,15 @@ def main():
             grid[k] = r.get("Grid_Size", "")
             if k not in order:
                 order.append(k)
+    if len(sys.argv) > 2:
+        for k in order:
+            if sys.argv[2] not in k:
+                continue
+            ds = [v for (kk, _), v in per.items() if kk == k]
+            print(k.split("(")[0][-60:], f"({len(ds)} dispatches)")
+            for c in sorted({c for d in ds for c in d}):
+                print(f"  {c:<28} {statistics.median([d.get(c, 0.0) for d in ds]):.4e}")
+        return
     print("kernel grid wave_cycles wait_any_frac wait_inst_any_frac active_inst_frac "
           "mfma_busy_per_simd(k cycles)")
     for k in order:

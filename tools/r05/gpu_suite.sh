@@ -1,0 +1,13 @@
+#!/bin/bash
+# the whole GPU suite, then the stamps of K3's target pass and a bcq bench line
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+O=$R/gpurun_out/r5suite
+cd $R && mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+ABLS=0 D3A_WIDE_STAMPS=1 timeout -k 10 200 python -u tools/bench_wide.py > $O/wide.json 2>$O/wide.err || { tail -20 $O/wide.err; exit 1; }
+timeout -k 10 200 python -u bench.py --algo bcq --steps 300 --warmup 50 --no-cpu-baseline > $O/bench_bcq.json 2>$O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python -c "
+import json; d=json.load(open('$O/wide.json')); v=d['abl0']; print(v)
+d=json.loads(open('$O/bench_bcq.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'])"
