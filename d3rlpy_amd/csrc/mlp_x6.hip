@@ -29,6 +29,7 @@
 // 71k cycles per workgroup, of which 12.5k were the interleaved production
 // and 3.4k its barriers (tools/bench_wide.py ablations).
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
@@ -95,9 +96,11 @@ __device__ __forceinline__ float4 wload(const WMat& m, int lane_off, int step_of
 // fence closes each step, and the schedule interleaves the split's vector
 // instructions into the MFMA gaps (an MFMA issues 32 cycles, holding the
 // vector issue for 8 of them).
+// NRT: row tiles of 32 (1 for a workgroup's last odd 32-row half)
+template <int NRT>
 __device__ __forceinline__ void stream256(const WMat& wm, int wo, const WMat& nm, int no,
                                           float4 (&hr)[W_HD][2], const __bf16 (&img)[W_RB * 3 * W_LDH],
-                                          int li, int lh, f32x16 (&o)[2]) {
+                                          int li, int lh, f32x16 (&o)[NRT]) {
   constexpr int NS = W_H / 16;
   auto split_slot = [&](int sl, bf16x8 (&wa)[3]) {
     const float v[8] = {hr[sl][0].x, hr[sl][0].y, hr[sl][0].z, hr[sl][0].w,
@@ -111,14 +114,14 @@ __device__ __forceinline__ void stream256(const WMat& wm, int wo, const WMat& nm
     hr[sl][0] = wload(m, lo, st);
     hr[sl][1] = wload(m, lo, st + 16);
   };
-  auto read_img = [&](int s, bf16x8 (&bp)[2][3]) {
+  auto read_img = [&](int s, bf16x8 (&bp)[NRT][3]) {
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < NRT; ++rt)
 #pragma unroll
       for (int q = 0; q < 3; ++q)
         bp[rt][q] = *reinterpret_cast<const bf16x8*>(&img[((32 * rt + li) * 3 + q) * W_LDH + 16 * s + 8 * lh]);
   };
-  bf16x8 wa[2][3], bp[2][2][3];
+  bf16x8 wa[2][3], bp[2][NRT][3];
   split_slot(0, wa[0]);
   refill(0);
   read_img(0, bp[0]);
@@ -133,14 +136,14 @@ __device__ __forceinline__ void stream256(const WMat& wm, int wo, const WMat& nm
       refill(s + 1);
     }
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) o[rt] = prod6(wa[cur], bp[cur][rt], o[rt]);
+    for (int rt = 0; rt < NRT; ++rt) o[rt] = prod6(wa[cur], bp[cur][rt], o[rt]);
     if (s + 1 < NS) {
-      __builtin_amdgcn_sched_group_barrier(0x0100, 6, 0);  // next step's image reads
-      __builtin_amdgcn_sched_group_barrier(0x0020, 2, 0);  // the refill
+      __builtin_amdgcn_sched_group_barrier(0x0100, 3 * NRT, 0);  // next step's image reads
+      __builtin_amdgcn_sched_group_barrier(0x0020, 2, 0);         // the refill
 #pragma unroll
-      for (int m = 0; m < 12; ++m) {
-        __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);  // one MFMA
-        __builtin_amdgcn_sched_group_barrier(0x0002, 4, 0);  // up to four vector instructions
+      for (int m = 0; m < 6 * NRT; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);            // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x0002, 8 / NRT, 0);  // the split's vector instructions
       }
     }
     // a compiler memory fence: the next step's reads stay in this step
@@ -151,15 +154,15 @@ __device__ __forceinline__ void stream256(const WMat& wm, int wo, const WMat& nm
 
 // bias, ReLU, kept rows to hg, parts into the image: lane holds rows
 // 32 rt + li, units 32 w + 8 R + 4 lh + i
-template <bool KEEP>
-__device__ __forceinline__ void act_to_image(const f32x16 (&o)[2], const float4 (&bv)[4], float* hg, int m0,
+template <bool KEEP, int NRT>
+__device__ __forceinline__ void act_to_image(const f32x16 (&o)[NRT], const float4 (&bv)[4], float* hg, int m0,
                                              int h_from, int rend, int w, int li, int lh,
                                              __bf16 (&img)[W_RB * 3 * W_LDH]) {
 #pragma unroll
   for (int R = 0; R < 4; ++R) {
     const int u = 32 * w + 8 * R + 4 * lh;
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
+    for (int rt = 0; rt < NRT; ++rt) {
       const int rl = 32 * rt + li;
       const int row = m0 + rl;
       float v[4] = {fmaxf(o[rt][4 * R + 0] + bv[R].x, 0.f), fmaxf(o[rt][4 * R + 1] + bv[R].y, 0.f),
@@ -281,143 +284,150 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
   issue_x(hb);
   stage_x(hb);
 
-  for (int h = hb; h < he; h += 2) {  // uniform
-    const int m0 = r0 + 32 * h, rend = tile_end(h);
-    const bool has_next = h + 2 < he;
-    const bool first = h == hb + 2;  // the stamped tile
-    stamp(0, first);
-    // the layer-1 weight row (clamped k, masked at use) and bias, reloaded per
-    // tile (L2 hits) so that no register holds them across the streams; a
-    // wave reaching this point early waits at the barrier anyway
-    const int lhl = opaque(lh);
-    float w0r[NS1][8];
-#pragma unroll
-    for (int s = 0; s < NS1; ++s)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) w0r[s][i] = W0r[min(16 * s + 8 * lhl + i, nin - 1)];
-    float4 b0v[4];
-#pragma unroll
-    for (int R = 0; R < 4; ++R) b0v[R] = *reinterpret_cast<const float4*>(b0 + 32 * w + 8 * R + 4 * lh);
-    stamp(1, first);
-    __syncthreads();  // input parts staged; the previous head done with the image
-    stamp(2, first);
+  // one tile: 64 rows from half h (NRT = 2), or the last odd half alone
+  // (NRT = 1: one row tile, half the products)
+  auto tile = [&](auto nrt, int h) {
+    constexpr int NRT = decltype(nrt)::value;
+      const int m0 = r0 + 32 * h, rend = tile_end(h);
+      const bool has_next = h + 2 < he;
+      const bool first = h == hb + 2;  // the stamped tile
+      stamp(0, first);
+      // the layer-1 weight row (clamped k, masked at use) and bias, reloaded per
+      // tile (L2 hits) so that no register holds them across the streams; a
+      // wave reaching this point early waits at the barrier anyway
+      const int lhl = opaque(lh);
+      float w0r[NS1][8];
+  #pragma unroll
+      for (int s = 0; s < NS1; ++s)
+  #pragma unroll
+        for (int i = 0; i < 8; ++i) w0r[s][i] = W0r[min(16 * s + 8 * lhl + i, nin - 1)];
+      float4 b0v[4];
+  #pragma unroll
+      for (int R = 0; R < 4; ++R) b0v[R] = *reinterpret_cast<const float4*>(b0 + 32 * w + 8 * R + 4 * lh);
+      stamp(1, first);
+      __syncthreads();  // input parts staged; the previous head done with the image
+      stamp(2, first);
 
-    // ---- layer 1: units 32 w .. over K = XL (x parts past n_in are zero, the
-    // weights there masked to zero)
-    f32x16 o[2];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
-#pragma unroll
-    for (int s = 0; s < NS1; ++s) {
-      float v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = 16 * s + 8 * lhl + i < nin ? w0r[s][i] : 0.f;
-      bf16x8 wa[3];
-      split8(v, wa);
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        bf16x8 bp[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          bp[q] = *reinterpret_cast<const bf16x8*>(&L.x[q][(32 * rt + li) * XLD + 16 * s + 8 * lh]);
-        o[rt] = prod6(wa, bp, o[rt]);
-      }
-    }
-    float4 b1v[4];
-#pragma unroll
-    for (int R = 0; R < 4; ++R) b1v[R] = *reinterpret_cast<const float4*>(b1 + 32 * w + 8 * R + 4 * lh);
-    act_to_image<KEEP>(o, b0v, h0g, m0, h_from, rend, w, li, lh, L.img);
-    __syncthreads();  // image 1 complete; every wave done reading the input parts
-    stamp(3, first);
-    if (has_next) issue_x(h + 2);  // uniform
-
-    // ---- layer 2: units 32 w .. over the image; the freed weight slots take
-    // the head's first steps (waves with no head: the next tile's layer 2)
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
-    {
-      const WMat nm{w < nkt ? Whm.rs : W1m.rs};  // uniform
-      stream256(W1m, w1o, nm, w < nkt ? who : w1o, hr, L.img, li, lh, o);
-    }
-    stamp(4, first);
-    __syncthreads();  // every wave done reading image 1
-    act_to_image<KEEP>(o, b1v, h1g, m0, h_from, rend, w, li, lh, L.img);
-    // head bias of this lane's outputs 32 w + 8 R + 4 lh + i (clamped index)
-    float bhv[4][4];
-#pragma unroll
-    for (int R = 0; R < 4; ++R)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) bhv[R][i] = bh[min(32 * w + 8 * R + 4 * lhl + i, nout - 1)];
-    if (has_next) stage_x(h + 2);  // the input region is free since image 1
-    __syncthreads();  // image 2 complete
-    stamp(5, first);
-
-    // ---- head: wave w < nkt computes outputs 32 w .. + 31; its freed weight
-    // slots take the next tile's first layer-2 steps
-    if (w < nkt) {
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
+      // ---- layer 1: units 32 w .. over K = XL (x parts past n_in are zero, the
+      // weights there masked to zero)
+      f32x16 o[NRT];
+  #pragma unroll
+      for (int rt = 0; rt < NRT; ++rt)
+  #pragma unroll
         for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
-      stream256(Whm, who, W1m, w1o, hr, L.img, li, lh, o);
-      stamp(6, first);
-      // lane: row 32 rt + li, outputs 32 w + 8 R + 4 lh + i
-      const int64_t ldo = d.ldout;
-      float rsum[2] = {0.f, 0.f};  // row_mean: this lane's outputs, in output order
-      const bool vec = ((reinterpret_cast<uintptr_t>(outp) & 15) == 0) && (ldo & 3) == 0;
-      const int lho = opaque(lh), lio = opaque(li);
-#pragma unroll
-      for (int R = 0; R < 4; ++R) {
-        const int k0 = 32 * w + 8 * R + 4 * lho;
-        float bv[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) bv[i] = k0 + i < nout ? bhv[R][i] : 0.f;
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-          const int row = m0 + 32 * rt + lio;
-          if (row >= rend) continue;
-          float* op = outp + (int64_t)row * ldo + k0;
-          const float v0 = o[rt][4 * R] + bv[0], v1 = o[rt][4 * R + 1] + bv[1];
-          const float v2 = o[rt][4 * R + 2] + bv[2], v3 = o[rt][4 * R + 3] + bv[3];
-          if (k0 + 0 < nout) rsum[rt] += v0;
-          if (k0 + 1 < nout) rsum[rt] += v1;
-          if (k0 + 2 < nout) rsum[rt] += v2;
-          if (k0 + 3 < nout) rsum[rt] += v3;
-          if (k0 + 3 < nout && vec) {
-            *reinterpret_cast<float4*>(op) = make_float4(v0, v1, v2, v3);
-          } else {
-            if (k0 + 0 < nout) op[0] = v0;
-            if (k0 + 1 < nout) op[1] = v1;
-            if (k0 + 2 < nout) op[2] = v2;
-            if (k0 + 3 < nout) op[3] = v3;
+  #pragma unroll
+      for (int s = 0; s < NS1; ++s) {
+        float v[8];
+  #pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = 16 * s + 8 * lhl + i < nin ? w0r[s][i] : 0.f;
+        bf16x8 wa[3];
+        split8(v, wa);
+  #pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) {
+          bf16x8 bp[3];
+  #pragma unroll
+          for (int q = 0; q < 3; ++q)
+            bp[q] = *reinterpret_cast<const bf16x8*>(&L.x[q][(32 * rt + li) * XLD + 16 * s + 8 * lh]);
+          o[rt] = prod6(wa, bp, o[rt]);
+        }
+      }
+      float4 b1v[4];
+  #pragma unroll
+      for (int R = 0; R < 4; ++R) b1v[R] = *reinterpret_cast<const float4*>(b1 + 32 * w + 8 * R + 4 * lh);
+      act_to_image<KEEP, NRT>(o, b0v, h0g, m0, h_from, rend, w, li, lh, L.img);
+      __syncthreads();  // image 1 complete; every wave done reading the input parts
+      stamp(3, first);
+      if (has_next) issue_x(h + 2);  // uniform
+
+      // ---- layer 2: units 32 w .. over the image; the freed weight slots take
+      // the head's first steps (waves with no head: the next tile's layer 2)
+  #pragma unroll
+      for (int rt = 0; rt < NRT; ++rt)
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
+      {
+        const WMat nm{w < nkt ? Whm.rs : W1m.rs};  // uniform
+        stream256<NRT>(W1m, w1o, nm, w < nkt ? who : w1o, hr, L.img, li, lh, o);
+      }
+      stamp(4, first);
+      __syncthreads();  // every wave done reading image 1
+      act_to_image<KEEP, NRT>(o, b1v, h1g, m0, h_from, rend, w, li, lh, L.img);
+      // head bias of this lane's outputs 32 w + 8 R + 4 lh + i (clamped index)
+      float bhv[4][4];
+  #pragma unroll
+      for (int R = 0; R < 4; ++R)
+  #pragma unroll
+        for (int i = 0; i < 4; ++i) bhv[R][i] = bh[min(32 * w + 8 * R + 4 * lhl + i, nout - 1)];
+      if (has_next) stage_x(h + 2);  // the input region is free since image 1
+      __syncthreads();  // image 2 complete
+      stamp(5, first);
+
+      // ---- head: wave w < nkt computes outputs 32 w .. + 31; its freed weight
+      // slots take the next tile's first layer-2 steps
+      if (w < nkt) {
+  #pragma unroll
+        for (int rt = 0; rt < NRT; ++rt)
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
+        stream256<NRT>(Whm, who, W1m, w1o, hr, L.img, li, lh, o);
+        stamp(6, first);
+        // lane: row 32 rt + li, outputs 32 w + 8 R + 4 lh + i
+        const int64_t ldo = d.ldout;
+        float rsum[2] = {0.f, 0.f};  // row_mean: this lane's outputs, in output order
+        const bool vec = ((reinterpret_cast<uintptr_t>(outp) & 15) == 0) && (ldo & 3) == 0;
+        const int lho = opaque(lh), lio = opaque(li);
+  #pragma unroll
+        for (int R = 0; R < 4; ++R) {
+          const int k0 = 32 * w + 8 * R + 4 * lho;
+          float bv[4];
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) bv[i] = k0 + i < nout ? bhv[R][i] : 0.f;
+  #pragma unroll
+          for (int rt = 0; rt < NRT; ++rt) {
+            const int row = m0 + 32 * rt + lio;
+            if (row >= rend) continue;
+            float* op = outp + (int64_t)row * ldo + k0;
+            const float v0 = o[rt][4 * R] + bv[0], v1 = o[rt][4 * R + 1] + bv[1];
+            const float v2 = o[rt][4 * R + 2] + bv[2], v3 = o[rt][4 * R + 3] + bv[3];
+            if (k0 + 0 < nout) rsum[rt] += v0;
+            if (k0 + 1 < nout) rsum[rt] += v1;
+            if (k0 + 2 < nout) rsum[rt] += v2;
+            if (k0 + 3 < nout) rsum[rt] += v3;
+            if (k0 + 3 < nout && vec) {
+              *reinterpret_cast<float4*>(op) = make_float4(v0, v1, v2, v3);
+            } else {
+              if (k0 + 0 < nout) op[0] = v0;
+              if (k0 + 1 < nout) op[1] = v1;
+              if (k0 + 2 < nout) op[2] = v2;
+              if (k0 + 3 < nout) op[3] = v3;
+            }
+          }
+        }
+        if (d.row_mean != nullptr) {
+          // the two lane halves hold interleaved runs of four outputs: the wave's
+          // 32 outputs of a row as (lane half 0's 16) + (lane half 1's 16)
+  #pragma unroll
+          for (int rt = 0; rt < NRT; ++rt) {
+            const float other = __shfl_xor(rsum[rt], 32, 64);
+            if (lh == 0) L.rs[w][32 * rt + li] = rsum[rt] + other;
           }
         }
       }
       if (d.row_mean != nullptr) {
-        // the two lane halves hold interleaved runs of four outputs: the wave's
-        // 32 outputs of a row as (lane half 0's 16) + (lane half 1's 16)
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-          const float other = __shfl_xor(rsum[rt], 32, 64);
-          if (lh == 0) L.rs[w][32 * rt + li] = rsum[rt] + other;
+        __syncthreads();  // uniform: row_mean is a kernel argument
+        if (t < W_RB) {
+          float s = L.rs[0][t];
+          for (int v = 1; v < nkt; ++v) s += L.rs[v][t];
+          const int row = m0 + t;
+          if (row < rend) d.row_mean[c * d.s_mean + row] = s / (float)nout;
         }
       }
-    }
-    if (d.row_mean != nullptr) {
-      __syncthreads();  // uniform: row_mean is a kernel argument
-      if (t < W_RB) {
-        float s = L.rs[0][t];
-        for (int v = 1; v < nkt; ++v) s += L.rs[v][t];
-        const int row = m0 + t;
-        if (row < rend) d.row_mean[c * d.s_mean + row] = s / (float)nout;
-      }
-    }
-    stamp(7, first);
-  }
+      stamp(7, first);
+  
+  };
+  int h = hb;
+  for (; h + 1 < he; h += 2) tile(std::integral_constant<int, 2>{}, h);  // uniform
+  if (h < he) tile(std::integral_constant<int, 1>{}, h);
   if constexpr (STAMPS) {
     if (t == 0 && wgi < 1024) wide_stamps[wgi * W_NST + 8] = __builtin_amdgcn_s_memtime() - t_start;
   }

@@ -3,8 +3,8 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/r5wide
 cd $R && mkdir -p $O
-true || timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_x6.py tests/test_gpu_bcq_parity.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
-true
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_x6.py tests/test_gpu_bcq_parity.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
 ABLS=0 D3A_WIDE_STAMPS=1 timeout -k 10 200 python -u tools/bench_wide.py > $O/wide.json 2>$O/wide.err || { tail -20 $O/wide.err; exit 1; }
 python -c "
 import json; d=json.load(open('$O/wide.json'))
