@@ -156,12 +156,12 @@ def small_bwd_ok(net: EnsembleMLP, rows: int) -> bool:
             and s[3] <= 256 and rows <= 2048)
 
 
-# the one-launch small-batch backward is opt-in (D3A_SMALL_BWD=1): correct
-# (tests/test_gpu_mlp_bwd_small.py, the BCQ suites) but measured slower than
-# the per-layer GEMMs it replaces at K3 (its two launches 33-43 us against
-# 25-35 us for the four or five GEMM launches; K3 1,673 against 1,824
-# steps/s, round 5, profiles/r05_bcq_timeline_smallbwd.txt)
-_SMALL_BWD = os.environ.get("D3A_SMALL_BWD", "0") == "1"
+# the two-launch small-batch backward (d3a_mlp_bwd_small) replaces the four or
+# five per-layer GEMM launches of each K3 network's backward.  Its first
+# version (VALU fma chains, 33-43 us) lost to them (K3 1,673 against 1,824
+# steps/s, profiles/r05_bcq_timeline_smallbwd.txt); on the fp32 matrix cores it
+# wins (K3 2,047 -> 2,134).  D3A_SMALL_BWD=0 keeps the per-layer GEMMs (A/B).
+_SMALL_BWD = os.environ.get("D3A_SMALL_BWD", "1") == "1"
 
 
 def x6_deep_shape(net: EnsembleMLP) -> bool:

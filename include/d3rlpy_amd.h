@@ -337,6 +337,10 @@ typedef struct d3a_mlp_bwd_small_desc {
   int32_t rows, n_in, n_out, C;
 } d3a_mlp_bwd_small_desc;
 int d3a_mlp_bwd_small(const d3a_mlp_bwd_small_desc* d, void* stream);
+/* Diagnostic (synchronous, not for graphs): the phase stamps ([launch 0/1:
+ * stage A/B][workgroup][4] s_memtime values) of the last d3a_mlp_bwd_small
+ * launch made with D3A_SB_STAMPS=1 in the environment. */
+int d3a_small_bwd_stamps(unsigned long long* dst, int n);
 
 /* Weight gradients of a single-output Q ensemble with two hidden layers of
  * width 256 (VectorEncoderWithAction [n_in -> 256 -> 256], encoders.py:265-275,
@@ -426,7 +430,7 @@ int d3a_q2_fwd_x1(const d3a_mlp_fwd_desc* d, void* stream);
  * and parts; e.g. BCQ's target QR critics over B*N sampled actions
  * (bcq_impl.py:215-226, qr_q_function.py:97-161). */
 int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* d, void* stream);
-/* Diagnostic (synchronous, not for graphs): the phase stamps ([workgroup][6]
+/* Diagnostic (synchronous, not for graphs): the phase stamps ([workgroup][9]
  * s_memtime values) of the last d3a_mlp_fwd_x6 launch made with
  * D3A_WIDE_STAMPS=1 in the environment. */
 int d3a_wide_stamps(unsigned long long* dst, int n);
