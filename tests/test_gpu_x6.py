@@ -362,6 +362,52 @@ def test_mlp_fwd_x6_wide_head_vs_fp64(entry, rows, n_in, n_out, keep):
     assert rel < 1e-5, rel
 
 
+@pytest.mark.parametrize("rows,r0,h_from,C", [(300, 40, 100, 2), (1000, 33, 33, 1), (70, 7, 50, 2)])
+def test_mlp_fwd_x6_row_window_bitwise(rows, r0, h_from, C):
+    """d3a_mlp_fwd_x6 over a row window [r0, rows) (its persistent workgroups cut
+    the window into 32-row halves from r0) gives bitwise the rows of the
+    whole-range launch, writes kept activations only from h_from on, and
+    touches no row outside the window."""
+    dev = torch.device("cuda")
+    n_in, n_out, H = 23, 200, 256
+    gen = torch.Generator().manual_seed(rows + r0)
+    sizes = [n_in, H, H, n_out]
+    Ws = [(torch.randn(C, sizes[l + 1], sizes[l], generator=gen) / np.sqrt(sizes[l])).to(dev) for l in range(3)]
+    bs = [(torch.randn(C, sizes[l + 1], generator=gen) * 0.1).to(dev) for l in range(3)]
+    ldx = 24
+    x = torch.randn(rows, ldx, generator=gen).to(dev)
+
+    def run(rr0, hf, keep):
+        out = torch.full((C, rows, n_out), float("nan"), device=dev)
+        means = torch.full((C, rows), float("nan"), device=dev)
+        h = [torch.full((C, rows, H), float("nan"), device=dev) for _ in range(2)]
+        d = N.MlpFwdDesc()
+        d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
+        d.n_in, d.n_hidden, d.H, d.n_out = n_in, 2, H, n_out
+        for l in range(3):
+            d.W[l], d.b[l] = Ws[l].data_ptr(), bs[l].data_ptr()
+            d.sW[l], d.sb[l] = sizes[l + 1] * sizes[l], sizes[l + 1]
+        for l in range(2):
+            d.h[l] = h[l].data_ptr() if keep else None
+        d.sh = rows * H
+        d.out, d.sout, d.ldout = out.data_ptr(), rows * n_out, n_out
+        d.r0, d.rows, d.C, d.h_from = rr0, rows - rr0, C, hf
+        if not keep:
+            d.row_mean, d.s_mean = means.data_ptr(), rows
+        ops.call_desc("d3a_mlp_fwd_x6", d)
+        torch.cuda.synchronize()
+        return out, means, h
+
+    full, fmeans, _ = run(0, 0, False)
+    win, wmeans, _ = run(r0, r0, False)
+    assert torch.isnan(win[:, :r0]).all() and torch.isnan(wmeans[:, :r0]).all()
+    assert torch.equal(win[:, r0:], full[:, r0:]) and torch.equal(wmeans[:, r0:], fmeans[:, r0:])
+    kept, _, h = run(r0, h_from, True)
+    assert torch.equal(kept[:, r0:], full[:, r0:])
+    for t in h:
+        assert torch.isnan(t[:, :h_from]).all() and not torch.isnan(t[:, h_from:]).any()
+
+
 @pytest.mark.parametrize("entry,mode,n_out", [("d3a_q2_fwd_x6", 1, 6), ("d3a_q2_fwd_x6", 2, 6),
                                               ("d3a_mlp_fwd_x6", 4, 200), ("d3a_q2_fwd_x6", 3, 1)])
 def test_x6_input_row_builder_matches_bcq_rows(entry, mode, n_out):
