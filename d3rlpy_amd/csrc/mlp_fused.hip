@@ -360,7 +360,8 @@ extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
   }
   if (d.block_rows == 16) {
     D3A_CHECK_ARG(mlp_small_launch(d, (hipStream_t)stream),
-                  "d3a_mlp_fwd: block_rows 16 needs H == 256, n_in <= 256, n_out <= 64 and "
+                  "d3a_mlp_fwd: block_rows 16 needs H == 256, n_in <= 256, n_out <= 64 (<= 256 with "
+                  "two hidden layers and a 16-byte aligned head) and "
                   "16-byte aligned W[1..], biases and activation rows");
     D3A_LAUNCH_CHECK("d3a_mlp_fwd");
     return 0;

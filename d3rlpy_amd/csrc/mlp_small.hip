@@ -20,7 +20,10 @@
 // of 16 k, lane group q = lane >> 4 supplying k = 16 g + 4 q + i to MFMA i
 // (the same permutation on both operands: an exact fp32 chain, deterministic).
 // The head (n_out <= 64 columns) reads the last layer from LDS: four threads
-// per (row, column) dot, then a fixed butterfly.
+// per (row, column) dot, then a fixed butterfly.  A wide head (WH: 64 < n_out
+// <= 256, e.g. BCQ's 200-quantile QR critics over their 256 batch rows) runs
+// as one more MFMA layer instead -- wave w owning outputs 32 w .. + 31, no
+// ReLU -- so those passes are one launch rather than three per-layer GEMMs.
 #include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
@@ -49,7 +52,7 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // of the prefetched weights are allocated statically)
 // PROBE (timing probes only, D3A_SMALL_PROBE): bit 0 skips the 256-wide
 // layers' MFMAs, bit 1 the head
-template <int NL, int PROBE = 0>
+template <int NL, int PROBE = 0, bool WH = false>
 __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
   __shared__ __attribute__((aligned(16))) SmallLds S;
   const int t = threadIdx.x, lane = t & 63;
@@ -88,7 +91,7 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
   for (int i = 0; i < WS; ++i) {
     const int e = t + 512 * i;
-    whs[i] = e < J * S_H ? Wh[e] : 0.f;
+    whs[i] = (!WH && e < J * S_H) ? Wh[e] : 0.f;
   }
   const float* W0 = d.W[0] + wdel + c * d.sW[0];
   const bool w0_regs = K0p <= 32;  // first layer's operand in registers
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
     bias[l][1] = *reinterpret_cast<const float4*>(b + 32 * w + 16 + 4 * lq);
   }
   const float* bh = d.b[L] + wdel + c * d.sb[L];
-  const float bh0 = bh[((t >> 2) % J)];  // the head bias of this thread's first pair
+  const float bh0 = WH ? 0.f : bh[((t >> 2) % J)];  // the head bias of this thread's first pair
   float4 wa[16], wb[16];
   auto load_w = [&](int l) {
     const float* W = d.W[l] + wdel + c * d.sW[l];
@@ -128,8 +131,10 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
       S.x[m * S_LDK + k] = xs[i];
     }
   }
+  if constexpr (!WH) {
 #pragma unroll
-  for (int i = 0; i < WS; ++i) S.wh[t + 512 * i] = whs[i];
+    for (int i = 0; i < WS; ++i) S.wh[t + 512 * i] = whs[i];
+  }
   __syncthreads();
 
   // ---- hidden layers
@@ -204,6 +209,39 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
   // ---- head: out[row][j] = h[row] . Wh[j] + bh[j]; four threads per pair
   const float* hl = S.h[(L - 1) & 1];
   if (PROBE & 2) return;
+  if constexpr (WH) {
+    // the head as one more MFMA layer: wave w's outputs 32 w + 16 tile + lr
+    // (rows of Wh past n_out read row n_out - 1; their outputs are not stored)
+    if (32 * w >= J) return;  // uniform: no outputs for this wave
+    const int ja = min(u0, J - 1), jb = min(u0 + 16, J - 1);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      wa[g] = *reinterpret_cast<const float4*>(Wh + ja * S_H + 16 * g + 4 * lq);
+      wb[g] = *reinterpret_cast<const float4*>(Wh + jb * S_H + 16 * g + 4 * lq);
+    }
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const float4 a = *reinterpret_cast<const float4*>(&hl[lr * S_LDK + 16 * g + 4 * lq]);
+      acc0 = mfma4(wa[g].x, a.x, acc0); acc1 = mfma4(wb[g].x, a.x, acc1);
+      acc0 = mfma4(wa[g].y, a.y, acc0); acc1 = mfma4(wb[g].y, a.y, acc1);
+      acc0 = mfma4(wa[g].z, a.z, acc0); acc1 = mfma4(wb[g].z, a.z, acc1);
+      acc0 = mfma4(wa[g].w, a.w, acc0); acc1 = mfma4(wb[g].w, a.w, acc1);
+    }
+    // lane: row lr, outputs 32 w + 16 tile + 4 lq + i
+    const int row = m0 + lr;
+    if (row < rend) {
+#pragma unroll
+      for (int tl = 0; tl < 2; ++tl) {
+        const f32x4& a = tl ? acc1 : acc0;
+        const int j0 = 32 * w + 16 * tl + 4 * lq;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (j0 + i < J) outp[(int64_t)row * d.ldout + j0 + i] = a[i] + bh[j0 + i];
+      }
+    }
+    return;
+  }
   for (int p = t >> 2; p < S_RB * J; p += 128) {
     const int m = p / J, j = p - m * J, q = t & 3;
     float s = 0.f;
@@ -384,7 +422,11 @@ bool mlp_parts_launch(const d3a_mlp_fwd_desc& d, hipStream_t st) {
 
 // d3a_mlp_fwd's block_rows == 16 path; false when the shape does not fit
 bool mlp_small_launch(const d3a_mlp_fwd_desc& d, hipStream_t st) {
-  if (d.H != S_H || d.n_out > S_JMAX || d.n_in > S_H || d.n_hidden < 1 || d.n_hidden > 4)
+  if (d.H != S_H || d.n_out > S_H || d.n_in > S_H || d.n_hidden < 1 || d.n_hidden > 4)
+    return false;
+  const bool wide = d.n_out > S_JMAX;
+  if (wide && (d.n_hidden != 2 || (reinterpret_cast<uintptr_t>(d.W[d.n_hidden]) & 15) != 0 ||
+               d.sW[d.n_hidden] % 4 != 0))
     return false;
   auto a16 = [](const void* p, int64_t stride) {
     return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && stride % 4 == 0;
@@ -402,6 +444,10 @@ bool mlp_small_launch(const d3a_mlp_fwd_desc& d, hipStream_t st) {
     const char* e = getenv("D3A_SMALL_PROBE");
     return e ? atoi(e) : 0;
   }();
+  if (wide) {
+    hipLaunchKernelGGL((mlp_small_kernel<2, 0, true>), grid, dim3(512), 0, st, d);
+    return true;
+  }
   if (probe && d.n_hidden == 2) {
     if (probe == 1) hipLaunchKernelGGL((mlp_small_kernel<2, 1>), grid, dim3(512), 0, st, d);
     else if (probe == 2) hipLaunchKernelGGL((mlp_small_kernel<2, 2>), grid, dim3(512), 0, st, d);

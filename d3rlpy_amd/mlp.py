@@ -162,6 +162,10 @@ def small_bwd_ok(net: EnsembleMLP, rows: int) -> bool:
 # steps/s, profiles/r05_bcq_timeline_smallbwd.txt); on the fp32 matrix cores it
 # wins (K3 2,047 -> 2,134).  D3A_SMALL_BWD=0 keeps the per-layer GEMMs (A/B).
 _SMALL_BWD = os.environ.get("D3A_SMALL_BWD", "1") == "1"
+# the small-pass forward also takes heads of 65-256 outputs (as an MFMA layer;
+# BCQ's QR critics over their batch rows); D3A_SMALL_WIDE=0 keeps those on the
+# per-layer GEMMs (A/B)
+_SMALL_WIDE = os.environ.get("D3A_SMALL_WIDE", "1") == "1"
 
 
 def x6_deep_shape(net: EnsembleMLP) -> bool:
@@ -238,8 +242,10 @@ _PARTS = os.environ.get("D3A_MLP_PARTS", "1") == "1"
 
 def small_ok(net: EnsembleMLP, rows: int) -> bool:
     hidden = net.sizes[1:-1]
+    # (a head wider than 64 runs as an MFMA layer: two hidden layers only)
     return (_SMALL and 1 <= len(hidden) <= N.MLP_MAX_HIDDEN and set(hidden) == {256}
-            and net.sizes[0] <= 256 and net.sizes[-1] <= 64 and rows * net.C <= SMALL_MAX_ROWS)
+            and net.sizes[0] <= 256 and rows * net.C <= SMALL_MAX_ROWS
+            and (net.sizes[-1] <= 64 or (_SMALL_WIDE and net.sizes[-1] <= 256 and len(hidden) == 2)))
 
 
 def parts_ok(net: EnsembleMLP) -> bool:

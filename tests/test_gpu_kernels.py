@@ -408,6 +408,8 @@ def test_fused_mlp_forward(dev, C, R, r0, n, K0, H, L, J, x_shared, bm, monkeypa
     (1, 100, 0, 100, 3, 2, 1, True),       # K1 TD3+BC policy, odd rows
     (3, 77, 5, 60, 37, 1, 5, False),       # per-member inputs, one hidden layer, r0 > 0
     (2, 300, 0, 300, 256, 3, 64, True),    # widest first layer and head, 3 hidden layers
+    (2, 256, 0, 256, 23, 2, 200, True),    # K3 QR critics over the batch rows: the MFMA head
+    (1, 90, 7, 70, 29, 2, 256, False),     # widest MFMA head, r0 > 0, odd rows
 ])
 def test_small_mlp_forward(dev, C, R, r0, n, K0, L, J, x_shared, monkeypatch):
     """d3a_mlp_fwd block_rows 16 (csrc/mlp_small.hip: 16-row workgroups on
