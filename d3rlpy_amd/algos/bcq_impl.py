@@ -51,6 +51,11 @@ _PARTS = os.environ.get("D3A_BCQ_PARTS", "1") == "1"
 # against 1,829 (the side passes' workgroups delay the one-per-CU target pass
 # and stretch its tail); D3A_BCQ_BRANCHES=1 turns them on
 _BRANCHES = os.environ.get("D3A_BCQ_BRANCHES", "0") == "1"
+# a full update (imitator, critic, actor and targets) carries the targets' soft
+# update and the step bookkeeping in its three Adam launches instead of a
+# d3a_step_end launch (as CQL's update does); D3A_BCQ_ADAM_TAIL=0 keeps
+# step_end (A/B)
+_ADAM_TAIL = os.environ.get("D3A_BCQ_ADAM_TAIL", "1") == "1"
 
 
 def _pad4(n: int) -> int:
@@ -637,6 +642,16 @@ class _Workspace:
         main = torch.cuda.current_stream()
         branch = _BRANCHES and critic
         q_pending = a_pending = False
+        # the fused tail: each Adam advances a counter it does not read --
+        # imitator -> critic's, critic -> actor's, actor -> imitator's -- so
+        # the critic and actor Adams read their step already advanced
+        # (step_add 0); the critic / actor Adams soft-update their targets
+        # (soft_span = critic + policy, contiguous), the actor's pushes the
+        # metric ring
+        s_c0, s_c1 = impl.store.span(impl.critic.names())
+        s_p0, s_p1 = impl.store.span(impl.policy.names())
+        fused_tail = (_ADAM_TAIL and imitator and critic and actor and targets
+                      and s_c1 == s_p0 and (s_c0, s_p1) == tuple(impl.soft_span))
         if imitator:
             # update_imitator (bcq_impl.py:148-161)
             mlp.forward(impl.vae_enc, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts,
@@ -650,7 +665,8 @@ class _Workspace:
             ops.call_desc("d3a_bcq_vae_enc_grad", self.vae_desc)
             mlp.backward(self.ve_bwd, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts,
                          self.dhead_e.data_ptr(), 2 * L, B * 2 * L, 0, B)
-            self.imitator_opt.launch()
+            self.imitator_opt.launch(
+                tail=dict(counters=impl.counters, inc_mask=1) if fused_tail else None)
         if branch:
             # forked behind the imitator update, so the side work overlaps the
             # long target pass rather than the imitator chain's small launches
@@ -684,7 +700,9 @@ class _Workspace:
             ops.call_desc("d3a_bcq_qr_loss", self.qr_desc)
             mlp.backward(self.cbwd, st, self.x_q.data_ptr(), True, self.LX1, self.q_acts,
                          self.dq.data_ptr(), K, B * K, 0, B)
-            self.critic_opt.launch()
+            self.critic_opt.launch(
+                tail=dict(targ=tg, tau=impl._tau, counters=impl.counters, inc_mask=2, step_add=0)
+                if fused_tail else None)
         if actor:
             # compute_actor_loss (bcq_impl.py:132-146)
             if a_pending:
@@ -699,7 +717,12 @@ class _Workspace:
             ops.call_desc("d3a_bcq_actor_head", self.actor_desc)
             mlp.backward(self.pbwd, st, self.x_pa.data_ptr(), True, self.LX1, self.pa_acts,
                          self.dhead_pi.data_ptr(), A, B * A, 0, B)
-            self.actor_opt.launch()
+            self.actor_opt.launch(
+                tail=dict(targ=tg, tau=impl._tau, counters=impl.counters, inc_mask=4, step_add=0,
+                          metrics=self.metrics, ring=self.ring, ring_ctr=self.ring_ctr)
+                if fused_tail else None)
+        if fused_tail:
+            return
         s0, s1 = impl.soft_span
         mask = (1 if critic else 0) | (2 if actor else 0) | (4 if imitator else 0)
         ops.step_end(impl.counters, mask, self.metrics, self.ring, self.ring_ctr,
