@@ -452,8 +452,8 @@ class _Workspace:
         P_ = NAT.MLP_PARTS
         pz = lambda net: (torch.zeros(P_, net.C, B, net.sizes[-1], device=dev)  # noqa: E731
                           if _PARTS and mlp.parts_ok(net) else None)
-        self.pe, self.pd = pz(impl.vae_enc), pz(impl.vae_dec)  # (the encoder's 2 L
-        # outputs exceed the parts path's 16 at K3: pe None, its head a matrix)
+        self.pe, self.pd = pz(impl.vae_enc), pz(impl.vae_dec)  # (pe None where the
+        # encoder's 2 L outputs exceed the parts path's 32: its head a matrix)
         self.pad, self.ppi = pz(impl.vae_dec), pz(impl.policy)
         self.x_qa = z(B, self.LX1)
         self.qa_acts = mlp.Acts.alloc(impl.critic, B, dev)

@@ -20,6 +20,15 @@ namespace {
 // part 0 holds the bias), summed in part order; np <= 1: the value itself
 __device__ __forceinline__ float part_sum(const float* h, int64_t sp, int np, int64_t i) {
   if (np <= 1) return h[i];
+  if (np == D3A_MLP_PARTS) {  // every load issued before the first add (same order)
+    float v[D3A_MLP_PARTS];
+#pragma unroll
+    for (int p = 0; p < D3A_MLP_PARTS; ++p) v[p] = h[p * sp + i];
+    float a = v[0];
+#pragma unroll
+    for (int p = 1; p < D3A_MLP_PARTS; ++p) a += v[p];
+    return a;
+  }
   float v = h[i];
   for (int p = 1; p < np; ++p) v += h[p * sp + i];
   return v;

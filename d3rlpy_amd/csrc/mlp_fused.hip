@@ -349,10 +349,10 @@ extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
   }
   if (d.parts > 1) {
     D3A_CHECK_ARG(d.parts == D3A_MLP_PARTS && d.block_rows == 16 && d.n_hidden == 2 &&
-                      d.H == 256 && d.n_in <= 64 && d.n_out <= 16 && d.aux_rows == 0 &&
+                      d.H == 256 && d.n_in <= 64 && d.n_out <= 32 && d.aux_rows == 0 &&
                       d.s_part >= (int64_t)d.C * d.sout,
                   "d3a_mlp_fwd: parts needs parts == D3A_MLP_PARTS, block_rows 16, two hidden "
-                  "layers of 256, n_in <= 64, n_out <= 16, no aux pass, s_part >= C * sout");
+                  "layers of 256, n_in <= 64, n_out <= 32, no aux pass, s_part >= C * sout");
     D3A_CHECK_ARG(mlp_parts_launch(d, (hipStream_t)stream),
                   "d3a_mlp_fwd: parts needs 16-byte aligned W[1], biases and activation rows");
     D3A_LAUNCH_CHECK("d3a_mlp_fwd");

@@ -271,17 +271,22 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
 // units of h2 Wh[j] (+ bias in part 0).  Four waves: wave w owns first-layer
 // units 64 w .. 64 w + 63 (four tiles) and second-layer units U0 + 16 w ..
 // U0 + 16 w + 15 (one tile, full k chain).  The head is summed over lane
-// groups by a fixed butterfly and over waves in wave order.
+// groups by a fixed butterfly and over waves in wave order.  JM: the head
+// width bound, 16 (the head rows of the part's units in registers) or 32 (e.g.
+// BCQ's VAE encoder, mu | logstd of 12 latents: staged in LDS instead).
 constexpr int P_LDX = 68;  // input row stride in LDS (n_in <= 64)
 
+template <int JM>
 struct PartsLds {
   float x[S_RB * P_LDX];
   float h1[S_RB * S_LDK];
-  float op[4][S_RB][16];  // per-wave head partials
+  float op[4][S_RB][JM];  // per-wave head partials
+  float wh[JM > 16 ? JM : 1][64];  // JM 32: Wh[j][U0 .. U0 + 63]
 };
 
+template <int JM>
 __global__ __launch_bounds__(256) void mlp_parts_kernel(d3a_mlp_fwd_desc d) {
-  __shared__ __attribute__((aligned(16))) PartsLds S;
+  __shared__ __attribute__((aligned(16))) PartsLds<JM> S;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int lr = lane & 15, lq = lane >> 4;
@@ -320,9 +325,20 @@ __global__ __launch_bounds__(256) void mlp_parts_kernel(d3a_mlp_fwd_desc d) {
       *reinterpret_cast<const float4*>(d.b[1] + c * d.sb[1] + U0 + 16 * w + 4 * lq);
   const float* Wh = d.W[2] + c * d.sW[2] + U0 + 16 * w + 4 * lq;
   float4 whv[16];
+  if constexpr (JM <= 16) {
 #pragma unroll
-  for (int j = 0; j < 16; ++j)
-    whv[j] = j < J ? *reinterpret_cast<const float4*>(Wh + j * S_H) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < 16; ++j)
+      whv[j] = j < J ? *reinterpret_cast<const float4*>(Wh + j * S_H) : make_float4(0.f, 0.f, 0.f, 0.f);
+  } else {
+    // the part's head columns, [j][64 units]: 512 float4 pieces over 256 threads
+    const float* Whp = d.W[2] + c * d.sW[2] + U0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = t + 256 * q, j = e >> 4, u4 = 4 * (e & 15);
+      const float4 v = *reinterpret_cast<const float4*>(Whp + min(j, J - 1) * S_H + u4);
+      *reinterpret_cast<float4*>(&S.wh[j][u4]) = j < J ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
   __syncthreads();
 
   // ---- first layer, all 256 units
@@ -376,13 +392,15 @@ __global__ __launch_bounds__(256) void mlp_parts_kernel(d3a_mlp_fwd_desc d) {
     if (d.h[1] && row >= d.h_from && row < rend)
       *reinterpret_cast<float4*>(d.h[1] + c * d.sh + (int64_t)row * S_H + U0 + 16 * w + 4 * lq) = v;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < JM; ++j) {
       if (j < J) {
+        const float4 wv = JM <= 16 ? whv[j < 16 ? j : 0]
+                                   : *reinterpret_cast<const float4*>(&S.wh[j][16 * w + 4 * lq]);
         float s = 0.f;
-        s = fmaf(v.x, whv[j].x, s);
-        s = fmaf(v.y, whv[j].y, s);
-        s = fmaf(v.z, whv[j].z, s);
-        s = fmaf(v.w, whv[j].w, s);
+        s = fmaf(v.x, wv.x, s);
+        s = fmaf(v.y, wv.y, s);
+        s = fmaf(v.z, wv.z, s);
+        s = fmaf(v.w, wv.w, s);
         s += __shfl_xor(s, 16, 64);
         s += __shfl_xor(s, 32, 64);
         if (lq == 0) S.op[w][lr][j] = s;
@@ -390,8 +408,8 @@ __global__ __launch_bounds__(256) void mlp_parts_kernel(d3a_mlp_fwd_desc d) {
     }
   }
   __syncthreads();
-  if (t < S_RB * J) {
-    const int m = t / J, j = t - m * J;
+  for (int e = t; e < S_RB * J; e += 256) {
+    const int m = e / J, j = e - m * J;
     const int r = m0 + m;
     if (r < rend) {
       float v = ((S.op[0][m][j] + S.op[1][m][j]) + S.op[2][m][j]) + S.op[3][m][j];
@@ -416,7 +434,10 @@ bool mlp_parts_launch(const d3a_mlp_fwd_desc& d, hipStream_t st) {
     if (d.h[l] && !a16(d.h[l], d.sh)) return false;
   if (d.rows == 0) return true;
   const dim3 grid((unsigned)((d.rows + S_RB - 1) / S_RB), (unsigned)d.C, (unsigned)D3A_MLP_PARTS);
-  hipLaunchKernelGGL(mlp_parts_kernel, grid, dim3(256), 0, st, d);
+  if (d.n_out <= 16)
+    hipLaunchKernelGGL(mlp_parts_kernel<16>, grid, dim3(256), 0, st, d);
+  else
+    hipLaunchKernelGGL(mlp_parts_kernel<32>, grid, dim3(256), 0, st, d);
   return true;
 }
 

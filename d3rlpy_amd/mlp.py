@@ -250,9 +250,9 @@ def small_ok(net: EnsembleMLP, rows: int) -> bool:
 
 def parts_ok(net: EnsembleMLP) -> bool:
     """Shape of d3a_mlp_fwd's parts path (two hidden layers of 256, the
-    second split into D3A_MLP_PARTS unit parts; n_in <= 64, n_out <= 16)."""
+    second split into D3A_MLP_PARTS unit parts; n_in <= 64, n_out <= 32)."""
     return (_PARTS and list(net.sizes[1:-1]) == [256, 256] and net.sizes[0] <= 64
-            and net.sizes[-1] <= 16)
+            and net.sizes[-1] <= 32)
 
 
 def fused_ok(net: EnsembleMLP, rows: Optional[int] = None, backward: bool = False) -> bool:

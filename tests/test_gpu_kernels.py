@@ -683,6 +683,8 @@ def test_gemm_pair_bit_identical(dev, C_, R, n_in, n_out, S):
     (1, 512, 0, 512, 11, 6, True),       # CQL policy on [obs; next_obs] (mu | logstd)
     (1, 512, 0, 512, 29, 16, True),      # K4 policy (antmaze 29 -> 2 x 8)
     (2, 300, 7, 200, 64, 5, False),      # widest input, per-member inputs, r0 > 0, ragged
+    (1, 256, 0, 256, 23, 24, True),      # K3 VAE encoder (mu | logstd of 12 latents): head in LDS
+    (2, 100, 3, 90, 17, 32, False),      # widest parts head, per-member inputs, ragged
 ])
 def test_mlp_forward_parts(dev, C, R, r0, n, K0, J, x_shared):
     """d3a_mlp_fwd parts (the second hidden layer's units split into
