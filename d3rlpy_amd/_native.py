@@ -276,6 +276,7 @@ class MlpFwdDesc(C.Structure):
         ("xg_base", vp), ("xg_clip", C.c_float), ("xg_scale", C.c_float),
         ("hmask", vp), ("s_hmask", C.c_int64),
         ("hmaskT", vp), ("s_hmaskT", C.c_int64),
+        ("xg_a_parts", C.c_int32), ("xg_s_apart", C.c_int64),
     ]
 
 

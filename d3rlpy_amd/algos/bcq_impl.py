@@ -614,13 +614,13 @@ class _Workspace:
         """The actor loss's rows up to its critic pass: (s, clamp(z)) ->
         decoder -> residual policy -> (s, clamp(a + flex tanh)) rows."""
         impl, st = self.impl, self.impl.store
-        ops.call_desc("d3a_bcq_rows", self.r_ad)
+        # (the decoder's rows are built while it stages them: mlp.forward xgen;
+        # the policy's are kept for its backward, with the decoded action)
         mlp.forward(impl.vae_dec, st, self.x_ad.data_ptr(), True, self.LX2, self.ad_acts,
-                    keep_h=False, out_parts=self.pad)
+                    keep_h=False, out_parts=self.pad, xgen=self.r_ad)
         ops.call_desc("d3a_bcq_rows", self.r_pa)
         mlp.forward(impl.policy, st, self.x_pa.data_ptr(), True, self.LX1, self.pa_acts,
                     out_parts=self.ppi)
-        ops.call_desc("d3a_bcq_rows", self.r_qa)
 
     def _enqueue(self, imitator: bool, critic: bool, actor: bool, targets: bool) -> None:
         impl = self.impl
@@ -709,8 +709,9 @@ class _Workspace:
                 main.wait_stream(self._side(1))
             else:
                 self._actor_prefix()
+            # (its rows built while staged: only dx is taken from this pass)
             mlp.forward(impl.critic, st, self.x_qa.data_ptr(), True, self.LX1, self.qa_acts,
-                        members=1)
+                        members=1, xgen=self.r_qa)
             mlp.backward(self.abwd, st, self.x_qa.data_ptr(), True, self.LX1, self.qa_acts,
                          self.dconst.data_ptr(), K, B * K, 0, B, weight_grads=False, dx=self.adx,
                          members=1)

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
+#include "x6.hpp"
 
 namespace d3a {
 // q2_fwd.hip: the register-resident instantiation for [n_in, 256, 256, 1]
@@ -302,10 +303,14 @@ using namespace d3a;
 extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
   D3A_CHECK_ARG(d_in, "d3a_mlp_fwd: null desc");
   D3A_CHECK_ARG(d_in->row_mean == nullptr, "d3a_mlp_fwd: row_mean is d3a_mlp_fwd_x6 only");
-  D3A_CHECK_ARG(d_in->xg_mode == 0, "d3a_mlp_fwd: no input-row builder (xg_mode)");
+  // the input-row builder (xg_*) only on the small-pass paths (block_rows 16:
+  // mlp_small.hip), without an aux pass
+  D3A_CHECK_ARG(d_in->xg_mode == 0 || (d_in->block_rows == 16 && d_in->aux_rows == 0 && x6::xgen_ok(*d_in)),
+                "d3a_mlp_fwd: the input-row builder (xg_mode) needs block_rows 16, no aux pass and a "
+                "valid builder");
   D3A_CHECK_ARG(d_in->hmask == nullptr, "d3a_mlp_fwd: hmask is d3a_q2_fwd_x6 only");
   d3a_mlp_fwd_desc d = *d_in;
-  D3A_CHECK_ARG(d.x && d.out, "d3a_mlp_fwd: null input / output");
+  D3A_CHECK_ARG((d.x || d.xg_mode) && d.out, "d3a_mlp_fwd: null input / output");
   D3A_CHECK_ARG(d.n_hidden >= 1 && d.n_hidden <= D3A_MLP_MAX_HIDDEN,
                 "d3a_mlp_fwd: 1..D3A_MLP_MAX_HIDDEN hidden layers");
   D3A_CHECK_ARG(d.H % 32 == 0 && d.H >= 32 && d.H <= 256, "d3a_mlp_fwd: H must be 32..256, %32");

@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
+#include "x6.hpp"
 
 namespace d3a {
 namespace {
@@ -78,12 +79,22 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
   const int64_t ldx = aux ? d.aux_ldx : d.ldx;
   constexpr int XS = (S_RB * S_H + 511) / 512;  // staged input elements per thread (<= 8)
   float xs[XS];
+  const bool xg = d.xg_mode != 0;  // uniform: rows from the input-row builder
+  if (xg) {
+    // (d3a_mlp_fwd_desc.xg_*, no aux pass): quads of k, straight into LDS
+    for (int e4 = t; e4 < S_RB * (K0p / 4); e4 += 512) {
+      const int m = e4 / (K0p / 4), k4 = 4 * (e4 - m * (K0p / 4));
+      float v[4];
+      x6::input4_at(d, nullptr, 0, m0 + m, k4, rend, K0, v);
+      *reinterpret_cast<float4*>(&S.x[m * S_LDK + k4]) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < XS; ++i) {
     const int e = t + 512 * i;
     const int m = e / K0p, k = e - m * K0p;
     const int r = m0 + m;
-    xs[i] = (e < S_RB * K0p && r < rend && k < K0) ? xb[(int64_t)r * ldx + k] : 0.f;
+    xs[i] = (!xg && e < S_RB * K0p && r < rend && k < K0) ? xb[(int64_t)r * ldx + k] : 0.f;
   }
   const float* Wh = d.W[L] + wdel + c * d.sW[L];
   constexpr int WS = (S_JMAX * S_H) / 512;  // head weights per thread (<= 32)
@@ -126,7 +137,7 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
   for (int i = 0; i < XS; ++i) {
     const int e = t + 512 * i;
-    if (e < S_RB * K0p) {
+    if (!xg && e < S_RB * K0p) {
       const int m = e / K0p, k = e - m * K0p;
       S.x[m * S_LDK + k] = xs[i];
     }
@@ -296,10 +307,19 @@ __global__ __launch_bounds__(256) void mlp_parts_kernel(d3a_mlp_fwd_desc d) {
   const int rend = (int)(d.r0 + d.rows);
   const int K0 = d.n_in, K0p = (K0 + 15) / 16 * 16, J = d.n_out;
   const float* xb = d.x + c * d.sxb;
-  for (int e = t; e < S_RB * P_LDX; e += 256) {
-    const int m = e / P_LDX, k = e - m * P_LDX;
-    const int r = m0 + m;
-    S.x[e] = (k < K0 && r < rend) ? xb[(int64_t)r * d.ldx + k] : 0.f;
+  if (d.xg_mode != 0) {  // uniform: rows from the input-row builder (quads of k)
+    for (int e4 = t; e4 < S_RB * (P_LDX / 4); e4 += 256) {
+      const int m = e4 / (P_LDX / 4), k4 = 4 * (e4 - m * (P_LDX / 4));
+      float v[4];
+      x6::input4_at(d, nullptr, 0, m0 + m, k4, rend, K0, v);
+      *reinterpret_cast<float4*>(&S.x[m * P_LDX + k4]) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  } else {
+    for (int e = t; e < S_RB * P_LDX; e += 256) {
+      const int m = e / P_LDX, k = e - m * P_LDX;
+      const int r = m0 + m;
+      S.x[e] = (k < K0 && r < rend) ? xb[(int64_t)r * d.ldx + k] : 0.f;
+    }
   }
   const float* W0 = d.W[0] + c * d.sW[0];
   float w0r[4][16];  // tile tt, group g, element i: W0[unit][min(16 g + 4 lq + i, n_in - 1)]

@@ -108,7 +108,8 @@ inline bool xgen_ok(const d3a_mlp_fwd_desc& d) {
   if (d.xg_mode == 0) return true;
   return d.xg_mode >= 1 && d.xg_mode <= 4 && d.xg_obs && d.xg_a && d.xg_D >= 1 && d.xg_rep >= 1 &&
          d.xg_E >= 1 && d.xg_D + d.xg_E == d.n_in && d.aux_rows == 0 && d.xg_lda >= d.xg_E &&
-         (d.xg_mode < 3 || d.xg_base != nullptr);
+         (d.xg_mode < 3 || d.xg_base != nullptr) && d.xg_a_parts >= 0 && d.xg_a_parts <= 8 &&
+         (d.xg_a_parts <= 1 || d.xg_s_apart > 0);
 }
 
 // features k4 .. k4 + 3 of input row r of a forward pass, zero past nin /
@@ -146,6 +147,15 @@ __device__ __forceinline__ void input4_issue(const d3a_mlp_fwd_desc& d, const fl
     x.ob[j] = orow[min(kc[j], D - 1)];
     x.a[j] = arow[max(kc[j] - D, 0)];
     x.bs[j] = 0.f;
+  }
+  if (d.xg_a_parts > 1) {  // uniform: a as head parts, summed in order
+    for (int q = 1; q < d.xg_a_parts; ++q) {
+      float t[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t[j] = arow[q * d.xg_s_apart + max(kc[j] - D, 0)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x.a[j] += t[j];
+    }
   }
   if (d.xg_mode >= 3) {
     const float* brow = d.xg_base + (int64_t)rr * d.xg_E;

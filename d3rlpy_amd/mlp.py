@@ -356,11 +356,17 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
               and out_parts is None and not d.aux_rows and n * C >= 8192):
             entry = "d3a_mlp_fwd_x6"  # wide head (e.g. BCQ's target QR critics)
         if xgen is not None:
-            if (_XGEN and entry in ("d3a_q2_fwd_x6", "d3a_mlp_fwd_x6") and not d.aux_rows
-                    and r0 == 0):
+            # the builder rides in the x6 forwards and the small-pass ones
+            # (block_rows 16); a builder with a side output (e_out) keeps its
+            # own launch
+            xg_ok = (entry in ("d3a_q2_fwd_x6", "d3a_mlp_fwd_x6")
+                     or (entry == "d3a_mlp_fwd" and d.block_rows == 16))
+            if (_XGEN and xg_ok and not d.aux_rows and r0 == 0 and not xgen.e_out):
                 d.xg_mode, d.xg_D, d.xg_rep, d.xg_E = xgen.mode, xgen.D, xgen.rep, xgen.E
                 d.xg_obs, d.xg_a, d.xg_lda = xgen.obs, xgen.a, xgen.lda
                 d.xg_base, d.xg_clip, d.xg_scale = xgen.base, xgen.clip, xgen.scale
+                if xgen.a_parts > 1:
+                    d.xg_a_parts, d.xg_s_apart = xgen.a_parts, xgen.s_a_part
             else:
                 ops.call_desc("d3a_bcq_rows", xgen)
             xgen = None

@@ -279,6 +279,11 @@ typedef struct d3a_mlp_fwd_desc {
    * for every 32-row group holding a kept row (member stride s_hmaskT words):
    * the operand of d3a_q2_bwd_x6's slice kernel (d3a_q2_bwd_desc.m2t).     */
   void* hmaskT; int64_t s_hmaskT;
+  /* Optional, with xg_mode: xg_a given as xg_a_parts > 1 partial sums (a
+   * parts-path head, d3a_mlp_fwd_desc.parts), part q at xg_a + q *
+   * xg_s_apart, summed in order (d3a_bcq_rows_desc.a_parts's arithmetic).
+   * 0 / 1: one array.                                                      */
+  int32_t xg_a_parts; int64_t xg_s_apart;
 } d3a_mlp_fwd_desc;
 #define D3A_MLP_PARTS 4
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);

@@ -474,3 +474,64 @@ def test_x6_input_row_builder_matches_bcq_rows(entry, mode, n_out):
         outs.append(out)
     assert not torch.isnan(outs[0]).any()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("path,mode,n_out,a_parts", [
+    ("small", 1, 6, 1), ("small", 3, 200, 4), ("small", 4, 24, 1),
+    ("parts", 2, 6, 4), ("parts", 1, 24, 1), ("parts", 3, 16, 4)])
+def test_small_forward_input_row_builder_matches_bcq_rows(path, mode, n_out, a_parts):
+    """The small-pass forwards (d3a_mlp_fwd block_rows 16: mlp_small, with the
+    MFMA head past 64 outputs, and the parts path) build their input rows
+    (xg_*, the action columns optionally a parts-path head summed in order:
+    xg_a_parts) bitwise as d3a_bcq_rows writes them -- BCQ's actor prefix,
+    bcq_impl.py:132-146."""
+    dev = torch.device("cuda")
+    C, D, E, rep, Bn = (1 if path == "parts" else 2), 17, 6 if mode != 1 else 12, 4, 64
+    rows = Bn * rep
+    n_in = D + E
+    gen = torch.Generator().manual_seed(mode * 11 + n_out + a_parts)
+    sizes = [n_in, 256, 256, n_out]
+    Ws = [(torch.randn(C, sizes[l + 1], sizes[l], generator=gen) / np.sqrt(sizes[l])).to(dev)
+          for l in range(3)]
+    bs = [(torch.randn(C, sizes[l + 1], generator=gen) * 0.1).to(dev) for l in range(3)]
+    obs = torch.randn(Bn, D, generator=gen).to(dev)
+    ap = (torch.randn(a_parts, rows, E, generator=gen) * 0.7).to(dev)
+    base = torch.randn(rows, E, generator=gen).clamp(-1, 1).to(dev)
+    ldx = (n_in + 3) // 4 * 4
+    x = torch.zeros(rows, ldx, device=dev)
+    r = N.BcqRowsDesc()
+    r.obs, r.D, r.rep, r.a, r.E, r.lda = obs.data_ptr(), D, rep, ap.data_ptr(), E, E
+    r.base = base.data_ptr() if mode >= 3 else None
+    r.mode, r.clip, r.scale = mode, 0.5, 0.05
+    r.x, r.ldx, r.e_out, r.rows = x.data_ptr(), ldx, None, rows
+    if a_parts > 1:
+        r.a_parts, r.s_a_part = a_parts, rows * E
+    P = N.MLP_PARTS if path == "parts" else 1
+    outs = []
+    for fused in (False, True):
+        out = torch.full((P, C, rows, n_out), float("nan"), device=dev)
+        d = N.MlpFwdDesc()
+        d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
+        d.n_in, d.n_hidden, d.H, d.n_out = n_in, 2, 256, n_out
+        for l in range(3):
+            d.W[l], d.b[l] = Ws[l].data_ptr(), bs[l].data_ptr()
+            d.sW[l], d.sb[l] = sizes[l + 1] * sizes[l], sizes[l + 1]
+        d.sh = rows * 256
+        d.out, d.sout, d.ldout = out.data_ptr(), rows * n_out, n_out
+        d.r0, d.rows, d.C, d.h_from, d.block_rows = 0, rows, C, 0, 16
+        if path == "parts":
+            d.parts, d.s_part = P, C * rows * n_out
+        if fused:
+            x.fill_(float("nan"))  # the kernel must not read x
+            d.xg_mode, d.xg_D, d.xg_rep, d.xg_E = mode, D, rep, E
+            d.xg_obs, d.xg_a, d.xg_lda = obs.data_ptr(), ap.data_ptr(), E
+            d.xg_base, d.xg_clip, d.xg_scale = r.base, 0.5, 0.05
+            if a_parts > 1:
+                d.xg_a_parts, d.xg_s_apart = a_parts, rows * E
+        else:
+            ops.call_desc("d3a_bcq_rows", r)
+        ops.call_desc("d3a_mlp_fwd", d)
+        torch.cuda.synchronize()
+        outs.append(out)
+    assert not torch.isnan(outs[0]).any()
+    assert torch.equal(outs[0], outs[1])
