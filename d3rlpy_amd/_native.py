@@ -353,6 +353,7 @@ class BcqVaeDesc(C.Structure):
         ("B", C.c_int32), ("D", C.c_int32), ("A", C.c_int32), ("L", C.c_int32),
         ("beta", C.c_float), ("min_logstd", C.c_float), ("max_logstd", C.c_float),
         ("head_parts", C.c_int32), ("s_e_part", C.c_int64), ("s_d_part", C.c_int64),
+        ("kl", vp),
     ]
 
 

@@ -520,6 +520,10 @@ class _Workspace:
         v.x_dec, v.ldx = self.x_vd.data_ptr(), self.LX2
         v.head_d, v.dhead_d = self.vd_acts.out.data_ptr(), self.dhead_d.data_ptr()
         v.head_parts = NAT.MLP_PARTS
+        # per-element KL terms: the sample kernel runs over many workgroups,
+        # the loss kernel forms the logged KL mean
+        self.kl_terms = torch.zeros(B * L, device=self.obs.device)
+        v.kl = self.kl_terms.data_ptr()
         if self.pe is not None:
             v.head_e, v.s_e_part = self.pe.data_ptr(), self.pe[0].numel()
         if self.pd is not None:

@@ -10,6 +10,7 @@
 //   compute_max_with_n_actions                        models/torch/q_functions/__init__.py:8-72
 //   quantile Huber loss                               models/torch/q_functions/utility.py:27-61
 //   BCQImpl.compute_actor_loss                        algos/torch/bcq_impl.py:132-146
+#include <algorithm>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
 
@@ -109,6 +110,33 @@ __global__ __launch_bounds__(1024) void bcq_vae_sample_kernel(d3a_bcq_vae_desc d
   }
 }
 
+// the same per element, one thread per (row, latent) and per obs element over
+// many workgroups, the KL terms to d.kl (summed by bcq_vae_loss_kernel)
+__global__ __launch_bounds__(256) void bcq_vae_sample_wide_kernel(d3a_bcq_vae_desc d) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int L = d.L;
+  const int64_t n = (int64_t)d.B * L;
+  if (i < n) {
+    const int64_t b = i / L;
+    const int j = (int)(i - b * L);
+    const int npe = d.s_e_part ? d.head_parts : 1;
+    const float mu = part_sum(d.head_e, d.s_e_part, npe, b * 2 * L + j);
+    const float ls = fminf(fmaxf(part_sum(d.head_e, d.s_e_part, npe, b * 2 * L + L + j),
+                                 d.min_logstd), d.max_logstd);
+    const float sd_ = expf(ls);
+    d.std_out[i] = sd_;
+    const float vr = __fmul_rn(sd_, sd_);
+    const float t1 = __fmul_rn(mu, mu);
+    d.kl[i] = __fmul_rn(0.5f, __fsub_rn(__fsub_rn(__fadd_rn(vr, t1), 1.f), logf(vr)));
+    d.x_dec[b * d.ldx + d.D + j] = __fadd_rn(mu, __fmul_rn(d.eps[i], sd_));
+  }
+  if (i < (int64_t)d.B * d.D) {
+    const int64_t b = i / d.D;
+    const int j = (int)(i - b * d.D);
+    d.x_dec[b * d.ldx + j] = d.obs[b * d.D + j];
+  }
+}
+
 // ---- VAE decode loss: mse(tanh(head), a) + beta * KL (one workgroup) --------
 __global__ __launch_bounds__(1024) void bcq_vae_loss_kernel(d3a_bcq_vae_desc d) {
   __shared__ double sd[16];
@@ -124,14 +152,30 @@ __global__ __launch_bounds__(1024) void bcq_vae_loss_kernel(d3a_bcq_vae_desc d) 
     const float gy = __fmul_rn(__fmul_rn(2.f, diff), gm);
     d.dhead_d[i] = __fmul_rn(gy, __fsub_rn(1.f, __fmul_rn(y, y)));
   }
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if (lane == 0) sd[wid] = s;
+  // the KL mean from d.kl's terms (the wide sample kernel), same reduction order
+  double k = 0.0;
+  const int64_t nk = (int64_t)d.B * d.L;
+  if (d.kl != nullptr)
+    for (int64_t i = t; i < nk; i += nt) k += (double)d.kl[i];
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    k += __shfl_xor(k, o, 64);
+  }
+  __shared__ double sk[16];
+  if (lane == 0) {
+    sd[wid] = s;
+    sk[wid] = k;
+  }
   __syncthreads();
   if (t == 0) {
-    double tot = 0.0;
-    for (int w = 0; w < (nt >> 6); ++w) tot += sd[w];
+    double tot = 0.0, ktot = 0.0;
+    for (int w = 0; w < (nt >> 6); ++w) {
+      tot += sd[w];
+      ktot += sk[w];
+    }
     const float mse = (float)(tot / (double)n);
-    d.metrics[0] = __fadd_rn(mse, __fmul_rn(d.beta, d.scalars[0]));
+    const float klm = d.kl != nullptr ? (float)(ktot / (double)nk) : d.scalars[0];
+    d.metrics[0] = __fadd_rn(mse, __fmul_rn(d.beta, klm));
   }
 }
 
@@ -368,7 +412,13 @@ extern "C" int d3a_bcq_rows(const d3a_bcq_rows_desc* d, void* stream) {
 extern "C" int d3a_bcq_vae_sample(const d3a_bcq_vae_desc* d, void* stream) {
   D3A_CHECK_ARG(d && d->head_e && d->eps && d->obs && d->x_dec && d->std_out && d->scalars,
                 "d3a_bcq_vae_sample: null pointer");
-  hipLaunchKernelGGL(bcq_vae_sample_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, *d);
+  if (d->kl != nullptr) {
+    const int64_t n = std::max((int64_t)d->B * d->L, (int64_t)d->B * d->D);
+    hipLaunchKernelGGL(bcq_vae_sample_wide_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, *d);
+  } else {
+    hipLaunchKernelGGL(bcq_vae_sample_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, *d);
+  }
   D3A_LAUNCH_CHECK("d3a_bcq_vae_sample");
   return 0;
 }

@@ -965,6 +965,11 @@ typedef struct d3a_bcq_vae_desc {
    * summed in part order, part strides s_e_part / s_d_part; a stride of 0
    * leaves that head a plain [B][.] matrix) */
   int32_t head_parts; int64_t s_e_part, s_d_part;
+  /* optional: [B][L] per-element KL terms.  When set, d3a_bcq_vae_sample runs
+   * one thread per (row, latent) over many workgroups and writes them, and
+   * d3a_bcq_vae_loss forms the KL mean of the logged loss from them (in a
+   * fixed order); null: one workgroup forms it into scalars[0]. */
+  float* kl;
 } d3a_bcq_vae_desc;
 int d3a_bcq_vae_sample(const d3a_bcq_vae_desc* d, void* stream);
 int d3a_bcq_vae_loss(const d3a_bcq_vae_desc* d, void* stream);
