@@ -650,12 +650,14 @@ class _Workspace:
         # imitator -> critic's, critic -> actor's, actor -> imitator's -- so
         # the critic and actor Adams read their step already advanced
         # (step_add 0); the critic / actor Adams soft-update their targets
-        # (soft_span = critic + policy, contiguous), the actor's pushes the
+        # (soft_span = critic + policy), the actor's pushes the
         # metric ring
         s_c0, s_c1 = impl.store.span(impl.critic.names())
         s_p0, s_p1 = impl.store.span(impl.policy.names())
+        # (the span between the critic and policy segments holds only the
+        # store's alignment padding, zeros in both copies)
         fused_tail = (_ADAM_TAIL and imitator and critic and actor and targets
-                      and s_c1 == s_p0 and (s_c0, s_p1) == tuple(impl.soft_span))
+                      and s_c1 <= s_p0 and (s_c0, s_p1) == tuple(impl.soft_span))
         if imitator:
             # update_imitator (bcq_impl.py:148-161)
             mlp.forward(impl.vae_enc, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts,

@@ -173,6 +173,9 @@ def test_bcq_full_step_equals_stages():
         assert torch.equal(a.store.data, b.store.data)
         s0, s1 = a.soft_span
         assert torch.equal(a.targ.data[s0:s1], b.targ.data[s0:s1])
+        # the full step's bookkeeping rides in its Adam launches (no step_end):
+        # the same optimiser step counters as the staged runs' step_end
+        assert torch.equal(a.counters[:3], b.counters[:3]), (a.counters, b.counters)
 
 
 def test_bcq_standard_scaler_matches_prescaled_batch():
