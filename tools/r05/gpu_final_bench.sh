@@ -19,3 +19,8 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_cql -o run --output-format csv -- python3 $R/bench.py --steps 500 --warmup 20 --no-cpu-baseline > $O/prof_cql.log 2>&1 || exit 1
 cd $R && cp $O/prof_cql/run_kernel_stats.csv $O/r05_cql_kernel_stats_final.csv && python tools/prof_timeline.py $O/prof_cql/run_kernel_trace.csv > $O/r05_cql_timeline_final.txt; rm -f $O/prof_cql/run_kernel_trace.csv
 tail -14 $O/r05_cql_timeline_final.txt
+# K3's step timeline on the final tree
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_bcq -o run --output-format csv -- python3 $R/bench.py --algo bcq --steps 200 --warmup 20 --no-cpu-baseline > $O/prof_bcq.log 2>&1 || exit 1
+cd $R && python tools/prof_timeline.py $O/prof_bcq/run_kernel_trace.csv > $O/r05_bcq_timeline_final.txt; rm -f $O/prof_bcq/run_kernel_trace.csv
+tail -1 $O/r05_bcq_timeline_final.txt
