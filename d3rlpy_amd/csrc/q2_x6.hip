@@ -63,7 +63,8 @@ struct X6FwdLds {
 // bit 3 the W1 reloads (chunk 0's registers reused); bit 4 (diagnostic build,
 // results right) records s_memtime stamps of wave 0 at the phase boundaries
 // into x6_stamps (read with d3a_x6_stamps); bit 5 the W1 split (the loaded
-// words taken as the parts)
+// words taken as the parts); bit 6 (results right) the round-4 chunk schedule
+// (the production epilogue after the chunk's MFMAs, kept rows on branches)
 //
 // NP / HT: NP = 3 the exact split (fp32-accurate, kept activations fp32);
 // NP = 1, HT = __bf16 the bf16 throughput line's forward (d3a_q2_fwd_bf16's
@@ -154,7 +155,8 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       for (int i = 0; i < 8; ++i) {
         const int k = 16 * s + 8 * lh + i;
         const float v = W0[u * nin + (k < nin ? k : nin - 1)];  // branch-free
-        w0n[s][i] = k < nin ? v : 0.f;
+        // (the interleaved schedule zeroes the padding at the split)
+        w0n[s][i] = ((PROBE & 64) == 0 && XL == 16) || k < nin ? v : 0.f;
       }
   };
   auto load_b0 = [&](int j) {
@@ -209,7 +211,20 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
     for (int s = 0; s < NS0; ++s) {
       bf16x8 wp[NP], xp[NP];
-      splitn8<NP>(w0n[s], wp);
+      if constexpr ((PROBE & 64) == 0 && XL == 16) {
+        // (as split_w below: keeps the split of the prefetched W0 words from
+        // being hoisted next to their loads)
+        typedef float f32x4v __attribute__((ext_vector_type(4)));
+        f32x4v r0 = {w0n[s][0], w0n[s][1], w0n[s][2], w0n[s][3]};
+        f32x4v r1 = {w0n[s][4], w0n[s][5], w0n[s][6], w0n[s][7]};
+        asm volatile("" : "+v"(r0), "+v"(r1));
+        float v[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = 16 * s + 8 * lh + i < nin ? v[i] : 0.f;
+        splitn8<NP>(v, wp);
+      } else {
+        splitn8<NP>(w0n[s], wp);
+      }
 #pragma unroll
       for (int q = 0; q < NP; ++q)
         xp[q] = *reinterpret_cast<const bf16x8*>(&L.x[q][(32 * ptt + li) * XLD + 16 * s + 8 * lh]);
@@ -254,6 +269,116 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[tt][r] = 0.f;
+  if constexpr ((PROBE & 64) == 0 && XL == 16) {
+    // the chunk interval as sixteen (k step, row tile) regions of NP * NP
+    // products each: region idx issues the next region's LDS reads, the
+    // regions 4 s split W1 step s + 1, and regions 5, 7, 9, 11 carry the
+    // next chunk's production epilogue one 8-unit run at a time -- its
+    // vector work interleaved into the MFMA gaps (sched_group_barrier)
+    // instead of trailing the chunk's last MFMAs, its kept-row stores
+    // branch-free (masked lanes store out of the buffer's range and are
+    // dropped: a branch would end the scheduling region).  (XL == 16: with
+    // the wider layer-1 tiles the schedule spills)
+    const __amdgpu_buffer_rsrc_t h0r =
+        __builtin_amdgcn_make_buffer_rsrc(h0g, (short)0, 0x7fffffff, 0x00020000);
+    const int prow = m0 + 32 * ptt + li;  // the production lane's row
+    const bool pkeep = h0g != nullptr && prow >= h_from && prow < rend && !(PROBE & 4);
+    auto epi_run = [&](int jn, const f32x16& a, const float4& bv, int R) {
+      const int k = ut + 8 * R + 4 * lh;  // local k of the chunk
+      float v[4] = {fmaxf(a[4 * R + 0] + bv.x, 0.f), fmaxf(a[4 * R + 1] + bv.y, 0.f),
+                    fmaxf(a[4 * R + 2] + bv.z, 0.f), fmaxf(a[4 * R + 3] + bv.w, 0.f)};
+      const uint32_t off = pkeep ? (uint32_t)((prow * X_H + X_CK * jn + k) * (int)sizeof(HT)) : 0x80000000u;
+      if constexpr (sizeof(HT) == 4) {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 bits = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                            __float_as_uint(v[3])};
+        __builtin_amdgcn_raw_buffer_store_b128(bits, h0r, off, 0, 0);
+      } else {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        bf16x4 b;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b[i] = (__bf16)v[i];
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), h0r, off, 0, 0);
+      }
+      bf16x4 p[NP];
+      splitn4<NP>(v, p);
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+        *reinterpret_cast<bf16x4*>(&L.h[jn & 1][q][(32 * ptt + li) * X_LDB + k]) = p[q];
+    };
+    // W1 as a four-slot ring of k steps: slot s holds step s of the current
+    // chunk until its split, then is refilled with step s of the next
+#pragma unroll
+    for (int j = 0; j < X_NCK; ++j) {
+      const bool more = j + 1 < X_NCK && !(PROBE & 1);
+      f32x16 pa;
+      if (more) {
+        produce_mma(pa);
+        if (j + 2 < X_NCK) load_w0w(j + 2);
+      }
+      const bool refill = j + 1 < X_NCK && !((PROBE & 8) && j > 0);
+      auto refill_w1 = [&](int s) {
+        wr[s][0] = *reinterpret_cast<const float4*>(W1 + X_CK * (j + 1) + 16 * s);
+        wr[s][1] = *reinterpret_cast<const float4*>(W1 + X_CK * (j + 1) + 16 * s + 4);
+      };
+      const __bf16* hb = &L.h[j & 1][0][li * X_LDB + 8 * lh];
+      constexpr int PS = X_RB * X_LDB;  // part stride
+      auto rd = [&](int idx, bf16x8* bp) {  // idx = 4 s + tt
+        const int s = idx >> 2, tt = idx & 3;
+#pragma unroll
+        for (int q = 0; q < NP; ++q)
+          bp[q] = *reinterpret_cast<const bf16x8*>(hb + q * PS + 32 * tt * X_LDB + 16 * s);
+      };
+      auto split_w = [&](int s, bf16x8* wa) {
+        // (the raw words pass through an empty asm here: the split is pure
+        // arithmetic, and the compiler otherwise hoists it above the chunk
+        // barrier to right behind the refill's load, waiting for it there)
+        typedef float f32x4v __attribute__((ext_vector_type(4)));
+        f32x4v r0 = {wr[s][0].x, wr[s][0].y, wr[s][0].z, wr[s][0].w};
+        f32x4v r1 = {wr[s][1].x, wr[s][1].y, wr[s][1].z, wr[s][1].w};
+        asm volatile("" : "+v"(r0), "+v"(r1));
+        const float v[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        if constexpr ((PROBE & 32) != 0) {
+#pragma unroll
+          for (int q = 0; q < NP; ++q) wa[q] = __builtin_bit_cast(bf16x8, q == 0 ? wr[s][0] : wr[s][1]);
+        } else {
+          splitn8<NP>(v, wa);
+        }
+      };
+      bf16x8 wa[2][NP], bcur[NP], bnx[NP];
+      split_w(0, wa[0]);
+      if (refill) refill_w1(0);
+      rd(0, bcur);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int idx = 0; idx < 4 * X_KS; ++idx) {
+        const int s = idx >> 2, tt = idx & 3;
+        if (idx + 1 < 4 * X_KS) rd(idx + 1, bnx);
+        if (tt == 0 && s + 1 < X_KS) {
+          split_w(s + 1, wa[(s + 1) & 1]);
+          if (refill) refill_w1(s + 1);
+        }
+        if (more && idx >= 5 && idx <= 11 && (idx & 1)) {
+          const int R = (idx - 5) >> 1;
+          epi_run(j + 1, pa, b0n[R], R);
+        }
+        acc[tt] = prodn<NP>(wa[s & 1], bcur, acc[tt]);
+        if (idx + 1 < 4 * X_KS) __builtin_amdgcn_sched_group_barrier(0x0100, NP, 0);  // next reads
+        if (tt == 0 && s + 1 < X_KS && refill) __builtin_amdgcn_sched_group_barrier(0x0020, 2, 0);
+#pragma unroll
+        for (int m = 0; m < (NP == 3 ? 6 : 1); ++m) {
+          __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);  // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x0002, 8, 0);  // vector instructions
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < NP; ++q) bcur[q] = bnx[q];
+      }
+      if (more && j + 2 < X_NCK) load_b0(j + 2);
+      __syncthreads();  // slot j & 1 free; chunk j + 1 in slot (j + 1) & 1
+      stamp(3 + j);
+    }
+  } else {
   // (fully unrolled: a rolled loop makes the compiler drain every outstanding
   // memory operation -- the kept-row stores included -- at its back edge)
 #pragma unroll
@@ -308,6 +433,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     __syncthreads();  // slot j & 1 free; chunk j + 1 in slot (j + 1) & 1
     stamp(3 + j);
   }
+  }  // PROBE & 64: the round-4 schedule
 
   // ---- epilogue: bias, ReLU, kept rows to h[1], the head dot of the lane's
   // 16 units in order, then the two lane halves and the eight waves in order
@@ -493,6 +619,8 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
                     (d.r0 + d.rows) * d.ldx < (int64_t(1) << 31) &&
                     d.aux_rows * (int64_t)(d.aux_ldx > X_H ? d.aux_ldx : X_H) < (int64_t(1) << 31),
                 "d3a_q2_fwd_x6: rows x row stride exceeds 2^31");
+  D3A_CHECK_ARG((d.r0 + d.rows) * (int64_t)X_H * 4 < (int64_t(1) << 31),
+                "d3a_q2_fwd_x6: kept rows exceed 2 GB (32-bit buffer offsets)");
   if (d.rows == 0 && d.aux_rows == 0) return 0;
   const int64_t nb = (d.rows + X_RB - 1) / X_RB + (d.aux_rows + X_RB - 1) / X_RB;
   const dim3 grid((unsigned)nb, 1, (unsigned)d.C);
@@ -503,13 +631,15 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
     return e ? atoi(e) : 0;
   }();
   if (probe && xl == 16 && d.n_out == 1) {
-    switch (probe & 63) {
+    switch (probe & 127) {
       case 1: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 1>), grid, dim3(512), 0, st, d); break;
       case 4: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 4>), grid, dim3(512), 0, st, d); break;
       case 5: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
       case 13: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 13>), grid, dim3(512), 0, st, d); break;
       case 16: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 16>), grid, dim3(512), 0, st, d); break;
       case 32: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 32>), grid, dim3(512), 0, st, d); break;
+      case 64: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 64>), grid, dim3(512), 0, st, d); break;
+      case 80: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 80>), grid, dim3(512), 0, st, d); break;
       default: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
     }
     D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
@@ -580,6 +710,8 @@ extern "C" int d3a_q2_fwd_x1(const d3a_mlp_fwd_desc* dp, void* stream) {
                     (e.r0 + e.rows) * e.ldx < (int64_t(1) << 31) &&
                     e.aux_rows * (int64_t)(e.aux_ldx > X_H ? e.aux_ldx : X_H) < (int64_t(1) << 31),
                 "d3a_q2_fwd_x1: rows x row stride exceeds 2^31");
+  D3A_CHECK_ARG((e.r0 + e.rows) * (int64_t)X_H * 4 < (int64_t(1) << 31),
+                "d3a_q2_fwd_x1: kept rows exceed 2 GB (32-bit buffer offsets)");
   if (e.rows == 0 && e.aux_rows == 0) return 0;
   const int64_t nb = (e.rows + X_RB - 1) / X_RB + (e.aux_rows + X_RB - 1) / X_RB;
   const dim3 grid((unsigned)nb, 1, (unsigned)e.C);
