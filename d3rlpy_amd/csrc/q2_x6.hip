@@ -64,7 +64,9 @@ struct X6FwdLds {
 // results right) records s_memtime stamps of wave 0 at the phase boundaries
 // into x6_stamps (read with d3a_x6_stamps); bit 5 the W1 split (the loaded
 // words taken as the parts); bit 6 (results right) the round-4 chunk schedule
-// (the production epilogue after the chunk's MFMAs, kept rows on branches)
+// (the production epilogue after the chunk's MFMAs, kept rows on branches);
+// bit 7 (results right) the interleaved chunks without the tile-major last
+// chunk (the Q head's epilogue after the MFMAs)
 //
 // NP / HT: NP = 3 the exact split (fp32-accurate, kept activations fp32);
 // NP = 1, HT = __bf16 the bf16 throughput line's forward (d3a_q2_fwd_bf16's
@@ -79,6 +81,10 @@ template <int XL, int PROBE = 0, int NP = 3, typename HT = float, int NO = 1>
 __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   constexpr int XLD = XL + 8;
   constexpr int NS0 = XL / 16;  // layer-1 k steps
+  // the round-5 schedules (see the chunk loop): interleaved chunks (XL == 16)
+  // and, for the Q head, the tile-major last chunk carrying the epilogue
+  constexpr bool CHUNKIL = (PROBE & 64) == 0 && XL == 16;
+  constexpr bool LASTIL = CHUNKIL && NO == 1 && (PROBE & 128) == 0;
   __shared__ __attribute__((aligned(16))) X6FwdLds<XL, NP, NO> L;
   static_assert(sizeof(X6FwdLds<XL, NP, NO>) <= 163840, "LDS");
   static_assert(NO == 1 || 8 * NO * X_RB * 4 <= (int)sizeof(L.h), "head partials fit the ring");
@@ -156,7 +162,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
         const int k = 16 * s + 8 * lh + i;
         const float v = W0[u * nin + (k < nin ? k : nin - 1)];  // branch-free
         // (the interleaved schedule zeroes the padding at the split)
-        w0n[s][i] = ((PROBE & 64) == 0 && XL == 16) || k < nin ? v : 0.f;
+        w0n[s][i] = CHUNKIL || k < nin ? v : 0.f;
       }
   };
   auto load_b0 = [&](int j) {
@@ -211,7 +217,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
     for (int s = 0; s < NS0; ++s) {
       bf16x8 wp[NP], xp[NP];
-      if constexpr ((PROBE & 64) == 0 && XL == 16) {
+      if constexpr (CHUNKIL) {
         // (as split_w below: keeps the split of the prefetched W0 words from
         // being hoisted next to their loads)
         typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -269,7 +275,8 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[tt][r] = 0.f;
-  if constexpr ((PROBE & 64) == 0 && XL == 16) {
+  float b2l = 0.f;  // (LASTIL) the head bias, loaded with the last chunk's operands
+  if constexpr (CHUNKIL) {
     // the chunk interval as sixteen (k step, row tile) regions of NP * NP
     // products each: region idx issues the next region's LDS reads, the
     // regions 4 s split W1 step s + 1, and regions 5, 7, 9, 11 carry the
@@ -305,6 +312,134 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
       for (int q = 0; q < NP; ++q)
         *reinterpret_cast<bf16x4*>(&L.h[jn & 1][q][(32 * ptt + li) * X_LDB + k]) = p[q];
+    };
+    // the last chunk (LASTIL, the Q head): tile-major -- row tile tt's four k
+    // steps back to back -- so tile tt's epilogue (bias, ReLU, kept h2 rows,
+    // the mask bits both ways, the head dot) runs one quarter per region in
+    // the MFMA gaps of tile tt + 1, every store branch-free; only tile 3's
+    // epilogue trails the MFMAs
+    float bb[16], ww[16];
+    float vt[16];
+    const __amdgpu_buffer_rsrc_t h1r =
+        __builtin_amdgcn_make_buffer_rsrc(h1g, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t hmr =
+        __builtin_amdgcn_make_buffer_rsrc(hmg, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t hmtr =
+        __builtin_amdgcn_make_buffer_rsrc(hmtg, (short)0, 0x7fffffff, 0x00020000);
+    // (lane indices laundered through an empty asm: the compiler otherwise
+    // keeps chunk 0's address arithmetic live across the kernel and spills it)
+    auto opaque = [](int v) {
+      asm volatile("" : "+v"(v));
+      return v;
+    };
+    auto tile_epi = [&](int tt, int piece) {
+      const int lane = opaque(t) & 63, li = lane & 31, lh = lane >> 5;
+      const int row = m0 + 32 * tt + li;
+      const bool in = row >= h_from && row < rend;
+      if (piece == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) vt[r] = fmaxf(acc[tt][r] + bb[r], 0.f);
+        const bool kp = h1g != nullptr && in && !(PROBE & 4);
+#pragma unroll
+        for (int R = 0; R < 4; ++R) {
+          const uint32_t off =
+              kp ? (uint32_t)((row * X_H + 32 * w + 8 * R + 4 * lh) * (int)sizeof(HT)) : 0x80000000u;
+          if constexpr (sizeof(HT) == 4) {
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 bits = {__float_as_uint(vt[4 * R]), __float_as_uint(vt[4 * R + 1]),
+                                __float_as_uint(vt[4 * R + 2]), __float_as_uint(vt[4 * R + 3])};
+            __builtin_amdgcn_raw_buffer_store_b128(bits, h1r, off, 0, 0);
+          } else {
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            bf16x4 b;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b[i] = (__bf16)vt[4 * R + i];
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), h1r, off, 0, 0);
+          }
+        }
+      } else if (piece == 1) {
+        // the lane's 16 units as bits of the wave's 32-unit word, the two
+        // lane halves or-ed (both halves then store the same word)
+        uint32_t bm = 0u;
+#pragma unroll
+        for (int R = 0; R < 4; ++R)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) bm |= (vt[4 * R + i] > 0.f ? 1u : 0u) << (8 * R + 4 * lh + i);
+        bm |= (uint32_t)__shfl_xor((int)bm, 32, 64);
+        const uint32_t off = (hmg != nullptr && in) ? (uint32_t)((row * (X_H / 32) + w) * 4) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32(bm, hmr, off, 0, 0);
+      } else if (piece == 2) {
+        // the tile's 32 rows as one word per unit (see the round-4 epilogue)
+        const int row0 = m0 + 32 * tt;
+        const bool ok = hmtg != nullptr && row0 + 31 >= h_from && row0 < rend && lane < 32;
+        int wv = 0;
+#pragma unroll
+        for (int R = 0; R < 4; ++R)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const unsigned long long bl = __ballot(vt[4 * R + i] > 0.f);
+            const int lo = (int)(uint32_t)bl, hi = (int)(uint32_t)(bl >> 32);
+            wv = lane == 8 * R + i ? lo : wv;
+            wv = lane == 8 * R + 4 + i ? hi : wv;
+          }
+        const uint32_t off =
+            ok ? (uint32_t)((((row0 >> 5) * X_H) + (lane & 15) * 16 + 2 * w + (lane >> 4)) * 4) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)wv, hmtr, off, 0, 0);
+      } else {
+        // the head dot of the lane's 16 units in order, the halves summed
+        // (both halves hold the same sum and write it to the same slot)
+        float hs = vt[0] * ww[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) hs = fmaf(vt[r], ww[r], hs);
+        const float o = __shfl_xor(hs, 32, 64);
+        L.hp[w][32 * tt + li] = hs + o;
+      }
+    };
+    auto last_chunk = [&](const __bf16* hb, auto& split_w) {
+      {
+        const float* b1 = d.b[1] + wdel + c * d.sb[1];
+        const float* wh = d.W[2] + wdel + c * d.sW[2];
+#pragma unroll
+        for (int R = 0; R < 4; ++R) {
+          const int u = 32 * w + 8 * R + 4 * lh;
+          const float4 bv = *reinterpret_cast<const float4*>(b1 + u);
+          const float4 hv = *reinterpret_cast<const float4*>(wh + u);
+          bb[4 * R] = bv.x; bb[4 * R + 1] = bv.y; bb[4 * R + 2] = bv.z; bb[4 * R + 3] = bv.w;
+          ww[4 * R] = hv.x; ww[4 * R + 1] = hv.y; ww[4 * R + 2] = hv.z; ww[4 * R + 3] = hv.w;
+        }
+        b2l = (d.b[2] + wdel + c * d.sb[2])[0];
+      }
+      asm volatile("" ::: "memory");  // (the loads stay here, a tile ahead of their use)
+      constexpr int PS = X_RB * X_LDB;
+      auto rd2 = [&](int s, int tt, bf16x8* bp) {
+#pragma unroll
+        for (int q = 0; q < NP; ++q)
+          bp[q] = *reinterpret_cast<const bf16x8*>(hb + q * PS + 32 * tt * X_LDB + 16 * s);
+      };
+      bf16x8 wl[X_KS][NP], bcur[NP], bnx[NP];
+#pragma unroll
+      for (int s = 0; s < X_KS; ++s) split_w(s, wl[s]);
+      rd2(0, 0, bcur);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int idx = 0; idx < 4 * X_KS; ++idx) {
+        const int tt = idx >> 2, s = idx & 3;
+        if (idx + 1 < 4 * X_KS) rd2((idx + 1) & 3, (idx + 1) >> 2, bnx);
+        if (tt >= 1) tile_epi(tt - 1, s);
+        acc[tt] = prodn<NP>(wl[s], bcur, acc[tt]);
+        if (idx + 1 < 4 * X_KS) __builtin_amdgcn_sched_group_barrier(0x0100, NP, 0);  // next reads
+#pragma unroll
+        for (int m = 0; m < (NP == 3 ? 6 : 1); ++m) {
+          __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);  // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x0002, 8, 0);  // vector instructions
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < NP; ++q) bcur[q] = bnx[q];
+      }
+#pragma unroll
+      for (int piece = 0; piece < 4; ++piece) tile_epi(3, piece);
+      stamp(3 + X_NCK - 1);
     };
     // W1 as a four-slot ring of k steps: slot s holds step s of the current
     // chunk until its split, then is refilled with step s of the next
@@ -345,6 +480,12 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
           splitn8<NP>(v, wa);
         }
       };
+      if constexpr (LASTIL) {
+        if (j == X_NCK - 1) {
+          last_chunk(hb, split_w);
+          continue;
+        }
+      }
       bf16x8 wa[2][NP], bcur[NP], bnx[NP];
       split_w(0, wa[0]);
       if (refill) refill_w1(0);
@@ -498,6 +639,8 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     }
     return;
   }
+  const float b2v = LASTIL ? b2l : (d.b[2] + wdel + c * d.sb[2])[0];
+  if constexpr (!LASTIL) {
   float bb[16], ww[16];
   {
     const float* b1 = d.b[1] + wdel + c * d.sb[1];
@@ -511,7 +654,6 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       ww[4 * R] = hv.x; ww[4 * R + 1] = hv.y; ww[4 * R + 2] = hv.z; ww[4 * R + 3] = hv.w;
     }
   }
-  const float b2v = (d.b[2] + wdel + c * d.sb[2])[0];
 #pragma unroll
   for (int tt = 0; tt < 4; ++tt) {
     float v[16];
@@ -563,6 +705,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     const float o = __shfl_xor(hs, 32, 64);
     if (lh == 0) L.hp[w][32 * tt + li] = hs + o;
   }
+  }  // !LASTIL
   stamp(7);
   __syncthreads();
   if (t < X_RB) {
@@ -631,7 +774,7 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
     return e ? atoi(e) : 0;
   }();
   if (probe && xl == 16 && d.n_out == 1) {
-    switch (probe & 127) {
+    switch (probe & 255) {
       case 1: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 1>), grid, dim3(512), 0, st, d); break;
       case 4: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 4>), grid, dim3(512), 0, st, d); break;
       case 5: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
@@ -640,6 +783,8 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
       case 32: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 32>), grid, dim3(512), 0, st, d); break;
       case 64: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 64>), grid, dim3(512), 0, st, d); break;
       case 80: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 80>), grid, dim3(512), 0, st, d); break;
+      case 128: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 128>), grid, dim3(512), 0, st, d); break;
+      case 144: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 144>), grid, dim3(512), 0, st, d); break;
       default: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
     }
     D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
