@@ -320,6 +320,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     // epilogue trails the MFMAs
     float bb[16], ww[16];
     float vt[16];
+    uint32_t bmt = 0u;  // the tile's row word of mask bits, piece 1 -> piece 2
     const __amdgpu_buffer_rsrc_t h1r =
         __builtin_amdgcn_make_buffer_rsrc(h1g, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t hmr =
@@ -360,31 +361,42 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       } else if (piece == 1) {
         // the lane's 16 units as bits of the wave's 32-unit word, the two
         // lane halves or-ed (both halves then store the same word)
-        uint32_t bm = 0u;
+        uint32_t bm = 0u;  // (constant bit selects, then one shift by the half)
 #pragma unroll
         for (int R = 0; R < 4; ++R)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) bm |= (vt[4 * R + i] > 0.f ? 1u : 0u) << (8 * R + 4 * lh + i);
+          for (int i = 0; i < 4; ++i) bm |= vt[4 * R + i] > 0.f ? 1u << (8 * R + i) : 0u;
+        bm <<= 4 * lh;
         bm |= (uint32_t)__shfl_xor((int)bm, 32, 64);
         const uint32_t off = (hmg != nullptr && in) ? (uint32_t)((row * (X_H / 32) + w) * 4) : 0x80000000u;
         __builtin_amdgcn_raw_buffer_store_b32(bm, hmr, off, 0, 0);
+        bmt = bm;
       } else if (piece == 2) {
-        // the tile's 32 rows as one word per unit (see the round-4 epilogue)
+        // the tile's 32 rows as one word per unit: the 32 x 32 bit matrix of
+        // the lanes' row words (lane & 31 = row, bit = unit) transposed across
+        // the lanes in five block-swap stages, after which lane k holds unit
+        // 32 w + k's word (bit r = row r) -- the round-4 epilogue's 16 ballots
+        // and lane selects cost three times the vector instructions
         const int row0 = m0 + 32 * tt;
         const bool ok = hmtg != nullptr && row0 + 31 >= h_from && row0 < rend && lane < 32;
-        int wv = 0;
+        uint32_t a = bmt;
 #pragma unroll
-        for (int R = 0; R < 4; ++R)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const unsigned long long bl = __ballot(vt[4 * R + i] > 0.f);
-            const int lo = (int)(uint32_t)bl, hi = (int)(uint32_t)(bl >> 32);
-            wv = lane == 8 * R + i ? lo : wv;
-            wv = lane == 8 * R + 4 + i ? hi : wv;
-          }
+        for (int st = 0; st < 5; ++st) {
+          const int j = 16 >> st;
+          const uint32_t m = j == 16 ? 0x0000ffffu : j == 8 ? 0x00ff00ffu : j == 4 ? 0x0f0f0f0fu
+                           : j == 2 ? 0x33333333u : 0x55555555u;
+          const uint32_t x = (uint32_t)__shfl_xor((int)a, j, 64);
+          // rows r (r & j == 0) take the partner's low-column block into their
+          // high columns; rows r | j its high-column block into their low
+          // (an all-ones / all-zeros lane mask selects: a ?: here compiles to
+          // a branch)
+          const uint32_t hs = 0u - ((uint32_t)(lane >> (4 - st)) & 1u);
+          const uint32_t hv = (a & ~m) | ((x >> j) & m), lv = (a & m) | ((x << j) & ~m);
+          a = (hv & hs) | (lv & ~hs);
+        }
         const uint32_t off =
             ok ? (uint32_t)((((row0 >> 5) * X_H) + (lane & 15) * 16 + 2 * w + (lane >> 4)) * 4) : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)wv, hmtr, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(a, hmtr, off, 0, 0);
       } else {
         // the head dot of the lane's 16 units in order, the halves summed
         // (both halves hold the same sum and write it to the same slot)
