@@ -171,6 +171,36 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   };
   // ---- prologue: every load of the first chunk and production in flight at
   // once, then the input rows split into LDS
+  if constexpr (CHUNKIL) {
+    // one 16-byte piece of the 128 x 16 input rows a thread: its load issued
+    // ahead of the weights' so that waiting for it does not wait for them
+    // (the load counter is in order)
+    static_assert(X_RB * (XL / 4) == 512, "one piece a thread");
+    const float* xb = aux ? d.aux_x + c * d.aux_sxb : d.x + c * d.sxb;
+    const int64_t ldx = aux ? d.aux_ldx : d.ldx;
+    const bool vec = d.xg_mode == 0 && (ldx & 3) == 0 && (reinterpret_cast<uintptr_t>(xb) & 15) == 0;
+    const int m = t >> 2, k4 = (t & 3) * 4, r = m0 + m;
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vec) {
+      const int rc = min(r, rend - 1), kc = min(k4, (int)ldx - 4);
+      f = *reinterpret_cast<const float4*>(xb + (int64_t)rc * ldx + kc);
+    }
+    load_w0w(0);
+    load_b0(0);
+    load_w1(0);
+    float v[4];
+    if (vec) {
+      const float fv[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? fv[j] : 0.f;
+    } else {
+      input4_at(d, xb, ldx, r, k4, rend, nin, v);
+    }
+    bf16x4 p[NP];
+    splitn4<NP>(v, p);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x4*>(&L.x[q][m * XLD + k4]) = p[q];
+  } else {
   load_w0w(0);
   load_b0(0);
   load_w1(0);
@@ -202,6 +232,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x4*>(&L.x[q][m * XLD + k4]) = p[q];
     }
   }
+  }  // CHUNKIL
   __syncthreads();  // x parts staged
   stamp(1);
 
