@@ -66,7 +66,8 @@ struct X6FwdLds {
 // words taken as the parts); bit 6 (results right) the round-4 chunk schedule
 // (the production epilogue after the chunk's MFMAs, kept rows on branches);
 // bit 7 (results right) the interleaved chunks without the tile-major last
-// chunk (the Q head's epilogue after the MFMAs)
+// chunk (the Q head's epilogue after the MFMAs); bit 8 (results right) no
+// static priority for waves 4-7
 //
 // NP / HT: NP = 3 the exact split (fp32-accurate, kept activations fp32);
 // NP = 1, HT = __bf16 the bf16 throughput line's forward (d3a_q2_fwd_bf16's
@@ -307,6 +308,12 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[tt][r] = 0.f;
   float b2l = 0.f;  // (LASTIL) the head bias, loaded with the last chunk's operands
+  if constexpr (CHUNKIL && (PROBE & 256) == 0) {
+    // the second-dispatched half (waves 4-7, each SIMD's younger wave) at a
+    // static higher issue priority: it otherwise loses every VALU
+    // arbitration to its older partner (MI355X_MICROARCH.md, item 4)
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   if constexpr (CHUNKIL) {
     // the chunk interval as sixteen (k step, row tile) regions of NP * NP
     // products each: region idx issues the next region's LDS reads, the
@@ -817,7 +824,7 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
     return e ? atoi(e) : 0;
   }();
   if (probe && xl == 16 && d.n_out == 1) {
-    switch (probe & 255) {
+    switch (probe & 511) {
       case 1: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 1>), grid, dim3(512), 0, st, d); break;
       case 4: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 4>), grid, dim3(512), 0, st, d); break;
       case 5: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
@@ -828,6 +835,7 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
       case 80: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 80>), grid, dim3(512), 0, st, d); break;
       case 128: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 128>), grid, dim3(512), 0, st, d); break;
       case 144: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 144>), grid, dim3(512), 0, st, d); break;
+      case 256: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 256>), grid, dim3(512), 0, st, d); break;
       default: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
     }
     D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
