@@ -82,9 +82,9 @@ template <int XL, int PROBE = 0, int NP = 3, typename HT = float, int NO = 1>
 __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   constexpr int XLD = XL + 8;
   constexpr int NS0 = XL / 16;  // layer-1 k steps
-  // the round-5 schedules (see the chunk loop): interleaved chunks (XL == 16)
+  // the round-5 schedules (see the chunk loop): interleaved chunks (XL <= 32)
   // and, for the Q head, the tile-major last chunk carrying the epilogue
-  constexpr bool CHUNKIL = (PROBE & 64) == 0 && XL == 16;
+  constexpr bool CHUNKIL = (PROBE & 64) == 0 && XL <= 32;
   constexpr bool LASTIL = CHUNKIL && NO == 1 && (PROBE & 128) == 0;
   __shared__ __attribute__((aligned(16))) X6FwdLds<XL, NP, NO> L;
   static_assert(sizeof(X6FwdLds<XL, NP, NO>) <= 163840, "LDS");
@@ -176,31 +176,40 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     // one 16-byte piece of the 128 x 16 input rows a thread: its load issued
     // ahead of the weights' so that waiting for it does not wait for them
     // (the load counter is in order)
-    static_assert(X_RB * (XL / 4) == 512, "one piece a thread");
+    constexpr int X4 = XL / 4, NPC = X_RB * X4 / 512;  // pieces a thread
+    static_assert(X_RB * X4 == 512 * NPC, "whole pieces a thread");
     const float* xb = aux ? d.aux_x + c * d.aux_sxb : d.x + c * d.sxb;
     const int64_t ldx = aux ? d.aux_ldx : d.ldx;
     const bool vec = d.xg_mode == 0 && (ldx & 3) == 0 && (reinterpret_cast<uintptr_t>(xb) & 15) == 0;
-    const int m = t >> 2, k4 = (t & 3) * 4, r = m0 + m;
-    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (vec) {
-      const int rc = min(r, rend - 1), kc = min(k4, (int)ldx - 4);
-      f = *reinterpret_cast<const float4*>(xb + (int64_t)rc * ldx + kc);
+    float4 f[NPC];
+#pragma unroll
+    for (int pc = 0; pc < NPC; ++pc) {
+      const int e = t + 512 * pc, m = e / X4, k4 = (e - m * X4) * 4, r = m0 + m;
+      f[pc] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (vec) {
+        const int rc = min(r, rend - 1), kc = min(k4, (int)ldx - 4);
+        f[pc] = *reinterpret_cast<const float4*>(xb + (int64_t)rc * ldx + kc);
+      }
     }
     load_w0w(0);
     load_b0(0);
     load_w1(0);
-    float v[4];
-    if (vec) {
-      const float fv[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? fv[j] : 0.f;
-    } else {
-      input4_at(d, xb, ldx, r, k4, rend, nin, v);
+    for (int pc = 0; pc < NPC; ++pc) {
+      const int e = t + 512 * pc, m = e / X4, k4 = (e - m * X4) * 4, r = m0 + m;
+      float v[4];
+      if (vec) {
+        const float fv[4] = {f[pc].x, f[pc].y, f[pc].z, f[pc].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? fv[j] : 0.f;
+      } else {
+        input4_at(d, xb, ldx, r, k4, rend, nin, v);
+      }
+      bf16x4 p[NP];
+      splitn4<NP>(v, p);
+#pragma unroll
+      for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x4*>(&L.x[q][m * XLD + k4]) = p[q];
     }
-    bf16x4 p[NP];
-    splitn4<NP>(v, p);
-#pragma unroll
-    for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x4*>(&L.x[q][m * XLD + k4]) = p[q];
   } else {
   load_w0w(0);
   load_b0(0);
@@ -322,8 +331,8 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     // vector work interleaved into the MFMA gaps (sched_group_barrier)
     // instead of trailing the chunk's last MFMAs, its kept-row stores
     // branch-free (masked lanes store out of the buffer's range and are
-    // dropped: a branch would end the scheduling region).  (XL == 16: with
-    // the wider layer-1 tiles the schedule spills)
+    // dropped: a branch would end the scheduling region).  (XL <= 32: with
+    // XL = 48's layer-1 tiles the schedule spills)
     const __amdgpu_buffer_rsrc_t h0r =
         __builtin_amdgcn_make_buffer_rsrc(h0g, (short)0, 0x7fffffff, 0x00020000);
     const int prow = m0 + 32 * ptt + li;  // the production lane's row
@@ -841,9 +850,17 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
     D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
     return 0;
   }
+  // (timing A/B: D3A_X6_LEGACY=1 runs the narrow head at XL 32 on the round-4
+  // chunk schedule)
+  static const bool legacy32 = [] {
+    const char* e = getenv("D3A_X6_LEGACY");
+    return e && atoi(e) != 0;
+  }();
   if (d.n_out > 1) {
     if (xl == 16)
       hipLaunchKernelGGL((q2x6_fwd_kernel<16, 0, 3, float, X_NOMAX>), grid, dim3(512), 0, st, d);
+    else if (xl == 32 && legacy32)
+      hipLaunchKernelGGL((q2x6_fwd_kernel<32, 64, 3, float, X_NOMAX>), grid, dim3(512), 0, st, d);
     else if (xl == 32)
       hipLaunchKernelGGL((q2x6_fwd_kernel<32, 0, 3, float, X_NOMAX>), grid, dim3(512), 0, st, d);
     else
