@@ -25,44 +25,25 @@ __device__ __forceinline__ void split1(float x, __bf16& p0, __bf16& p1, __bf16& 
   p2 = (__bf16)(r1 - (float)p1);
 }
 
-// the same split of two values at once, written on two-wide vectors so each
-// step is one packed instruction (v_cvt_pk_bf16_f32 rounds both, v_pk_add_f32
-// subtracts both): nine vector instructions a pair instead of the ~15 the
-// per-value form compiles to -- bitwise the same parts
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void split2(f32x2 x, bf16x2& p0, bf16x2& p1, bf16x2& p2) {
-  p0 = __builtin_convertvector(x, bf16x2);
-  const f32x2 r1 = x - __builtin_convertvector(p0, f32x2);
-  p1 = __builtin_convertvector(r1, bf16x2);
-  p2 = __builtin_convertvector(r1 - __builtin_convertvector(p1, f32x2), bf16x2);
-}
-
 __device__ __forceinline__ void split8(const float* x, bf16x8* p) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    bf16x2 a, b, c;
-    split2(f32x2{x[2 * i], x[2 * i + 1]}, a, b, c);
-    p[0][2 * i] = a[0];
-    p[0][2 * i + 1] = a[1];
-    p[1][2 * i] = b[0];
-    p[1][2 * i + 1] = b[1];
-    p[2][2 * i] = c[0];
-    p[2][2 * i + 1] = c[1];
+  for (int i = 0; i < 8; ++i) {
+    __bf16 a, b, c;
+    split1(x[i], a, b, c);
+    p[0][i] = a;
+    p[1][i] = b;
+    p[2][i] = c;
   }
 }
 
 __device__ __forceinline__ void split4(const float* x, bf16x4* p) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    bf16x2 a, b, c;
-    split2(f32x2{x[2 * i], x[2 * i + 1]}, a, b, c);
-    p[0][2 * i] = a[0];
-    p[0][2 * i + 1] = a[1];
-    p[1][2 * i] = b[0];
-    p[1][2 * i + 1] = b[1];
-    p[2][2 * i] = c[0];
-    p[2][2 * i + 1] = c[1];
+  for (int i = 0; i < 4; ++i) {
+    __bf16 a, b, c;
+    split1(x[i], a, b, c);
+    p[0][i] = a;
+    p[1][i] = b;
+    p[2][i] = c;
   }
 }
 
