@@ -277,6 +277,7 @@ class MlpFwdDesc(C.Structure):
         ("hmask", vp), ("s_hmask", C.c_int64),
         ("hmaskT", vp), ("s_hmaskT", C.c_int64),
         ("xg_a_parts", C.c_int32), ("xg_s_apart", C.c_int64),
+        ("xg_xout", vp), ("xg_ldxo", C.c_int64), ("xg_eout", vp),
     ]
 
 

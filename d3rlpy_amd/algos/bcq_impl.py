@@ -622,9 +622,10 @@ class _Workspace:
         # the policy's are kept for its backward, with the decoded action)
         mlp.forward(impl.vae_dec, st, self.x_ad.data_ptr(), True, self.LX2, self.ad_acts,
                     keep_h=False, out_parts=self.pad, xgen=self.r_ad)
-        ops.call_desc("d3a_bcq_rows", self.r_pa)
+        # (the policy's rows and the decoded actions written by its forward:
+        # the policy backward and the critic pass's residual read them)
         mlp.forward(impl.policy, st, self.x_pa.data_ptr(), True, self.LX1, self.pa_acts,
-                    out_parts=self.ppi)
+                    out_parts=self.ppi, xgen=self.r_pa, xgen_keep=True)
 
     def _enqueue(self, imitator: bool, critic: bool, actor: bool, targets: bool) -> None:
         impl = self.impl
@@ -635,7 +636,10 @@ class _Workspace:
                             self.rng_ctr, self.rng_ticket)
         if impl._scaler is not None:
             ops.standardize(self.obs2, self.xobs2, self.sc_mean, self.sc_std, self.sc_eps)
-        ops.call_desc("d3a_bcq_rows", self.r_q)
+        if not imitator:
+            ops.call_desc("d3a_bcq_rows", self.r_q)
+        # (else the VAE encoder's forward forms the (s, a) rows and writes
+        # them for the critic passes and the encoder backward)
         # graph branches: the online critic forward on (s, a) reads only the
         # critic's pre-update parameters, so it runs beside the target pass on
         # side stream 1 (joined before the QR loss); the actor's decoder /
@@ -661,7 +665,7 @@ class _Workspace:
         if imitator:
             # update_imitator (bcq_impl.py:148-161)
             mlp.forward(impl.vae_enc, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts,
-                        out_parts=self.pe)
+                        out_parts=self.pe, xgen=self.r_q, xgen_keep=True)
             ops.call_desc("d3a_bcq_vae_sample", self.vae_desc)
             mlp.forward(impl.vae_dec, st, self.x_vd.data_ptr(), True, self.LX2, self.vd_acts,
                         out_parts=self.pd)

@@ -308,6 +308,8 @@ extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
   D3A_CHECK_ARG(d_in->xg_mode == 0 || (d_in->block_rows == 16 && d_in->aux_rows == 0 && x6::xgen_ok(*d_in)),
                 "d3a_mlp_fwd: the input-row builder (xg_mode) needs block_rows 16, no aux pass and a "
                 "valid builder");
+  D3A_CHECK_ARG(d_in->xg_mode != 0 || (d_in->xg_xout == nullptr && d_in->xg_eout == nullptr),
+                "d3a_mlp_fwd: xg_xout / xg_eout need the input-row builder (xg_mode)");
   D3A_CHECK_ARG(d_in->hmask == nullptr, "d3a_mlp_fwd: hmask is d3a_q2_fwd_x6 only");
   d3a_mlp_fwd_desc d = *d_in;
   D3A_CHECK_ARG((d.x || d.xg_mode) && d.out, "d3a_mlp_fwd: null input / output");

@@ -308,11 +308,23 @@ __global__ __launch_bounds__(256) void mlp_parts_kernel(d3a_mlp_fwd_desc d) {
   const int K0 = d.n_in, K0p = (K0 + 15) / 16 * 16, J = d.n_out;
   const float* xb = d.x + c * d.sxb;
   if (d.xg_mode != 0) {  // uniform: rows from the input-row builder (quads of k)
+    // (the part-0 workgroups also write the rows out: xg_xout / xg_eout)
+    const bool xo = d.xg_xout != nullptr && p == 0, eo = d.xg_eout != nullptr && p == 0;
     for (int e4 = t; e4 < S_RB * (P_LDX / 4); e4 += 256) {
       const int m = e4 / (P_LDX / 4), k4 = 4 * (e4 - m * (P_LDX / 4));
+      const int r = m0 + m;
       float v[4];
-      x6::input4_at(d, nullptr, 0, m0 + m, k4, rend, K0, v);
+      x6::input4_at(d, nullptr, 0, r, k4, rend, K0, v);
       *reinterpret_cast<float4*>(&S.x[m * P_LDX + k4]) = make_float4(v[0], v[1], v[2], v[3]);
+      if (xo && r < rend && k4 < d.xg_ldxo)
+        *reinterpret_cast<float4*>(d.xg_xout + (int64_t)r * d.xg_ldxo + k4) = make_float4(v[0], v[1], v[2], v[3]);
+      if (eo && r < rend) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int e = k4 + j - d.xg_D;
+          if (e >= 0 && e < d.xg_E) d.xg_eout[(int64_t)r * d.xg_E + e] = v[j];
+        }
+      }
     }
   } else {
     for (int e = t; e < S_RB * P_LDX; e += 256) {

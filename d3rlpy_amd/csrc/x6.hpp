@@ -103,13 +103,18 @@ __device__ __forceinline__ f32x16 prodn(const bf16x8* a, const bf16x8* b, f32x16
 namespace d3a {
 namespace x6 {
 
-// host: the input-row builder's fields are consistent (or it is off)
+// host: the input-row builder's fields are consistent (or it is off); the
+// row write-out (xg_xout / xg_eout) only on the parts path
 inline bool xgen_ok(const d3a_mlp_fwd_desc& d) {
   if (d.xg_mode == 0) return true;
-  return d.xg_mode >= 1 && d.xg_mode <= 4 && d.xg_obs && d.xg_a && d.xg_D >= 1 && d.xg_rep >= 1 &&
+  const bool outs_ok =
+      (d.xg_xout == nullptr && d.xg_eout == nullptr) ||
+      (d.parts > 1 && (d.xg_xout == nullptr || (d.xg_ldxo >= d.n_in && d.xg_ldxo % 4 == 0 &&
+                                                (reinterpret_cast<uintptr_t>(d.xg_xout) & 15) == 0)));
+  return d.xg_mode >= 1 && d.xg_mode <= 5 && d.xg_obs && d.xg_a && d.xg_D >= 1 && d.xg_rep >= 1 &&
          d.xg_E >= 1 && d.xg_D + d.xg_E == d.n_in && d.aux_rows == 0 && d.xg_lda >= d.xg_E &&
-         (d.xg_mode < 3 || d.xg_base != nullptr) && d.xg_a_parts >= 0 && d.xg_a_parts <= 8 &&
-         (d.xg_a_parts <= 1 || d.xg_s_apart > 0);
+         ((d.xg_mode != 3 && d.xg_mode != 4) || d.xg_base != nullptr) && d.xg_a_parts >= 0 &&
+         d.xg_a_parts <= 8 && (d.xg_a_parts <= 1 || d.xg_s_apart > 0) && outs_ok;
 }
 
 // features k4 .. k4 + 3 of input row r of a forward pass, zero past nin /
@@ -157,7 +162,7 @@ __device__ __forceinline__ void input4_issue(const d3a_mlp_fwd_desc& d, const fl
       for (int j = 0; j < 4; ++j) x.a[j] += t[j];
     }
   }
-  if (d.xg_mode >= 3) {
+  if (d.xg_mode == 3 || d.xg_mode == 4) {
     const float* brow = d.xg_base + (int64_t)rr * d.xg_E;
 #pragma unroll
     for (int j = 0; j < 4; ++j) x.bs[j] = brow[max(kc[j] - D, 0)];
@@ -180,8 +185,10 @@ __device__ __forceinline__ void input4_finish(const d3a_mlp_fwd_desc& d, int r, 
       case 1: y = fminf(fmaxf(x.a[j], -d.xg_clip), d.xg_clip); break;
       case 2: y = tanhf(x.a[j]); break;
       case 3: y = fminf(fmaxf(__fadd_rn(x.bs[j], __fmul_rn(d.xg_scale, tanhf(x.a[j]))), -1.f), 1.f); break;
-      default:
+      case 4:
         y = fminf(fmaxf(__fadd_rn(tanhf(x.bs[j]), __fmul_rn(d.xg_scale, tanhf(x.a[j]))), -1.f), 1.f);
+        break;
+      default: y = x.a[j];  // 5: the copy
     }
     v[j] = (rok && k4 + j < nin) ? (k4 + j < D ? x.ob[j] : y) : 0.f;
   }

@@ -268,7 +268,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             members: Optional[int] = None, keep_h: bool = True,
             h_from: Optional[int] = None, aux: Optional[tuple] = None,
             skip_head: bool = False, out_parts: Optional[torch.Tensor] = None,
-            row_mean: Optional[torch.Tensor] = None, xgen=None) -> bool:
+            row_mean: Optional[torch.Tensor] = None, xgen=None, xgen_keep: bool = False) -> bool:
     """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
     (through its first ``members`` members only, when given).  ``keep_h``:
     store the hidden activations in ``acts.h`` (needed by a backward pass),
@@ -287,6 +287,10 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     ``xgen`` (a d3a_bcq_rows descriptor whose x is this pass's input ``x``):
     the input rows are that builder's; the x6 kernels form them while staging
     (d3a_mlp_fwd_desc.xg_*), any other path launches d3a_bcq_rows first.
+    ``xgen_keep``: the rows (and the builder's e_out) must also be written, as
+    d3a_bcq_rows writes them, for a later reader; the parts path forms and
+    writes them in-kernel (xg_xout / xg_eout), any other path launches
+    d3a_bcq_rows first.
 
     ``row_mean`` ([C][R] fp32): also the mean of each row's outputs, where the
     launch is d3a_mlp_fwd_x6 (its epilogue forms it); returns whether it was
@@ -361,12 +365,19 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             # own launch
             xg_ok = (entry in ("d3a_q2_fwd_x6", "d3a_mlp_fwd_x6")
                      or (entry == "d3a_mlp_fwd" and d.block_rows == 16))
-            if (_XGEN and xg_ok and not d.aux_rows and r0 == 0 and not xgen.e_out):
-                d.xg_mode, d.xg_D, d.xg_rep, d.xg_E = xgen.mode, xgen.D, xgen.rep, xgen.E
+            # (writing the rows out: the parts path only)
+            parts_path = entry == "d3a_mlp_fwd" and out_parts is not None
+            outs = xgen_keep or bool(xgen.e_out)
+            if (_XGEN and xg_ok and not d.aux_rows and r0 == 0 and (not outs or (xgen_keep and parts_path))):
+                # (d3a_bcq_rows mode 0, the copy, is the builder's mode 5)
+                d.xg_mode = xgen.mode if xgen.mode != 0 else 5
+                d.xg_D, d.xg_rep, d.xg_E = xgen.D, xgen.rep, xgen.E
                 d.xg_obs, d.xg_a, d.xg_lda = xgen.obs, xgen.a, xgen.lda
                 d.xg_base, d.xg_clip, d.xg_scale = xgen.base, xgen.clip, xgen.scale
                 if xgen.a_parts > 1:
                     d.xg_a_parts, d.xg_s_apart = xgen.a_parts, xgen.s_a_part
+                if xgen_keep:
+                    d.xg_xout, d.xg_ldxo, d.xg_eout = xgen.x, xgen.ldx, xgen.e_out
             else:
                 ops.call_desc("d3a_bcq_rows", xgen)
             xgen = None

@@ -284,6 +284,13 @@ typedef struct d3a_mlp_fwd_desc {
    * xg_s_apart, summed in order (d3a_bcq_rows_desc.a_parts's arithmetic).
    * 0 / 1: one array.                                                      */
   int32_t xg_a_parts; int64_t xg_s_apart;
+  /* Optional, with xg_mode on the parts path (parts > 1): the part-0
+   * workgroups also write the rows they form to xg_xout (row stride xg_ldxo,
+   * a multiple of 4, 16-byte aligned; columns past n_in zero) and f(a) to
+   * xg_eout ([rows][xg_E]) -- d3a_bcq_rows's x and e_out, so a pass whose rows
+   * a later stage reads (a backward's dW1) needs no d3a_bcq_rows launch.
+   * xg_mode 5: f(a) = a (d3a_bcq_rows mode 0). */
+  float* xg_xout; int64_t xg_ldxo; float* xg_eout;
 } d3a_mlp_fwd_desc;
 #define D3A_MLP_PARTS 4
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);

@@ -535,3 +535,65 @@ def test_small_forward_input_row_builder_matches_bcq_rows(path, mode, n_out, a_p
         outs.append(out)
     assert not torch.isnan(outs[0]).any()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,a_parts", [(0, 1), (2, 4)])
+def test_parts_forward_writes_its_built_rows(mode, a_parts):
+    """The parts-path forward with the input-row builder and the write-out
+    (xg_xout / xg_eout, mlp.forward xgen_keep): its head parts, the rows it
+    writes and f(a) all bitwise as d3a_bcq_rows + the plain forward -- BCQ's
+    (s, a) rows of the VAE encoder (mode 0, the copy: xg_mode 5) and the
+    actor's policy rows with the decoded actions (mode 2 over a parts head),
+    bcq_impl.py:132-146, 163-187."""
+    dev = torch.device("cuda")
+    C, D, E, n_out, rows = 1, 17, 6, 24 if mode == 0 else 6, 256
+    n_in = D + E
+    gen = torch.Generator().manual_seed(31 + mode)
+    sizes = [n_in, 256, 256, n_out]
+    Ws = [(torch.randn(C, sizes[l + 1], sizes[l], generator=gen) / np.sqrt(sizes[l])).to(dev)
+          for l in range(3)]
+    bs = [(torch.randn(C, sizes[l + 1], generator=gen) * 0.1).to(dev) for l in range(3)]
+    obs = torch.randn(rows, D, generator=gen).to(dev)
+    ap = (torch.randn(a_parts, rows, E, generator=gen) * 0.7).to(dev)
+    ldx = (n_in + 3) // 4 * 4
+    P = N.MLP_PARTS
+    res = []
+    for fused in (False, True):
+        x = torch.zeros(rows, ldx, device=dev) if not fused else torch.full((rows, ldx), float("nan"), device=dev)
+        e_out = torch.full((rows, E), float("nan"), device=dev)
+        r = N.BcqRowsDesc()
+        r.obs, r.D, r.rep, r.a, r.E, r.lda = obs.data_ptr(), D, 1, ap.data_ptr(), E, E
+        r.mode, r.clip, r.scale = mode, 0.5, 0.05
+        r.x, r.ldx, r.e_out, r.rows = x.data_ptr(), ldx, e_out.data_ptr(), rows
+        if a_parts > 1:
+            r.a_parts, r.s_a_part = a_parts, rows * E
+        out = torch.full((P, C, rows, n_out), float("nan"), device=dev)
+        d = N.MlpFwdDesc()
+        d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
+        d.n_in, d.n_hidden, d.H, d.n_out = n_in, 2, 256, n_out
+        for l in range(3):
+            d.W[l], d.b[l] = Ws[l].data_ptr(), bs[l].data_ptr()
+            d.sW[l], d.sb[l] = sizes[l + 1] * sizes[l], sizes[l + 1]
+        d.sh = rows * 256
+        d.out, d.sout, d.ldout = out.data_ptr(), rows * n_out, n_out
+        d.r0, d.rows, d.C, d.h_from, d.block_rows = 0, rows, C, 0, 16
+        d.parts, d.s_part = P, C * rows * n_out
+        if fused:
+            d.xg_mode, d.xg_D, d.xg_rep, d.xg_E = (mode if mode else 5), D, 1, E
+            d.xg_obs, d.xg_a, d.xg_lda = obs.data_ptr(), ap.data_ptr(), E
+            d.xg_clip, d.xg_scale = 0.5, 0.05
+            if a_parts > 1:
+                d.xg_a_parts, d.xg_s_apart = a_parts, rows * E
+            d.xg_xout, d.xg_ldxo, d.xg_eout = x.data_ptr(), ldx, e_out.data_ptr()
+        else:
+            ops.call_desc("d3a_bcq_rows", r)
+            x[:, n_in:] = 0.0
+        ops.call_desc("d3a_mlp_fwd", d)
+        torch.cuda.synchronize()
+        res.append((out, x, e_out))
+    (o0, x0, e0), (o1, x1, e1) = res
+    assert not torch.isnan(o0).any() and not torch.isnan(x1).any() and not torch.isnan(e1).any()
+    assert torch.equal(o0, o1)
+    assert torch.equal(x0, x1)
+    assert torch.equal(e0, e1)
