@@ -371,6 +371,8 @@ class BcqQrDesc(C.Structure):
         ("q", vp), ("target", vp), ("rew", vp), ("term", vp), ("n_steps", vp),
         ("dq", vp), ("loss_cb", vp),
         ("B", C.c_int32), ("K", C.c_int32), ("C", C.c_int32), ("gamma", C.c_float),
+        ("tg_q", vp), ("tg_means", vp), ("tg_N", C.c_int32), ("tg_C", C.c_int32),
+        ("tg_lam", C.c_float),
     ]
 
 

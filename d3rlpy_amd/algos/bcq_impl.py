@@ -56,6 +56,10 @@ _BRANCHES = os.environ.get("D3A_BCQ_BRANCHES", "0") == "1"
 # d3a_step_end launch (as CQL's update does); D3A_BCQ_ADAM_TAIL=0 keeps
 # step_end (A/B)
 _ADAM_TAIL = os.environ.get("D3A_BCQ_ADAM_TAIL", "1") == "1"
+# the target rows formed inside the QR-loss launch (from the target pass's
+# quantile means) instead of a d3a_bcq_target launch; D3A_BCQ_FUSED_TARGET=0
+# keeps the launch (A/B)
+_FUSED_TARGET = os.environ.get("D3A_BCQ_FUSED_TARGET", "1") == "1"
 
 
 def _pad4(n: int) -> int:
@@ -701,7 +705,15 @@ class _Workspace:
                                 self.tq_acts, keep_h=False, row_mean=self.tq_means,
                                 xgen=self.r_tq)
             self.target_desc.means = self.tq_means.data_ptr() if means else None
-            ops.call_desc("d3a_bcq_target", self.target_desc)
+            q = self.qr_desc
+            if means and _FUSED_TARGET:
+                # the loss launch forms the target rows (d3a_bcq_target's
+                # arithmetic) from the means and quantiles
+                t = self.target_desc
+                q.tg_q, q.tg_means, q.tg_N, q.tg_C, q.tg_lam = t.q, t.means, t.N, t.C, t.lam
+            else:
+                q.tg_means = None
+                ops.call_desc("d3a_bcq_target", self.target_desc)
             # update_critic (ddpg_impl.py:138-165) with the quantile Huber loss
             if q_pending:
                 main.wait_stream(self._side(0))

@@ -206,6 +206,36 @@ __global__ __launch_bounds__(256) void bcq_vae_enc_grad_kernel(d3a_bcq_vae_desc 
 // q: [C][B*N][K] target-critic quantiles (row b*N + n); one workgroup of
 // sixteen waves per b (the waves keep eight quantile rows each in flight)
 constexpr int TG_T = 1024;
+// wave 0: the argmax over n of the mix of the per-critic means sm[C][N] (the
+// first n of the largest value, as a sequential strict-greater scan picks
+// it; NaN never wins): each lane scans n = lane, lane + 64, .. in order, then
+// the wave reduces (largest value, then smallest n)
+__device__ __forceinline__ void tg_argmax(const float* sm, int C, int N, float lam, int lane, int* s_arg,
+                                          int* s_cmax, int* s_cmin) {
+  float best = -INFINITY;
+  int arg = -1, bmax = 0, bmin = 0;
+  for (int n = lane; n < N; n += 64) {
+    float mx = sm[n], mn = sm[n];
+    int cmx = 0, cmn = 0;
+    for (int c = 1; c < C; ++c) {
+      const float v = sm[c * N + n];
+      if (v > mx) { mx = v; cmx = c; }
+      if (v < mn) { mn = v; cmn = c; }
+    }
+    // mix_values = (1 - lam) * max_values + lam * min_values
+    const float mix = __fadd_rn(__fmul_rn(1.f - lam, mx), __fmul_rn(lam, mn));
+    if (mix > best) { best = mix; arg = n; bmax = cmx; bmin = cmn; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oa = __shfl_xor(arg, o, 64);
+    const int ox = __shfl_xor(bmax, o, 64), on = __shfl_xor(bmin, o, 64);
+    const bool take = oa >= 0 && (arg < 0 || ob > best || (ob == best && oa < arg));
+    if (take) { best = ob; arg = oa; bmax = ox; bmin = on; }
+  }
+  if (lane == 0) { *s_arg = arg < 0 ? 0 : arg; *s_cmax = bmax; *s_cmin = bmin; }
+}
+
 __global__ __launch_bounds__(TG_T) void bcq_target_kernel(d3a_bcq_target_desc d) {
   extern __shared__ float sm[];  // [C][N] quantile means
   __shared__ int s_arg, s_cmax, s_cmin;
@@ -259,34 +289,7 @@ __global__ __launch_bounds__(TG_T) void bcq_target_kernel(d3a_bcq_target_desc d)
     }
   }
   __syncthreads();
-  if (wid == 0) {
-    // argmax over n of the mix (the first n of the largest value, as a
-    // sequential strict-greater scan picks it; NaN never wins): each lane
-    // scans n = lane, lane + 64, .. in order, then the wave reduces
-    // (largest value, then smallest n)
-    float best = -INFINITY;
-    int arg = -1, bmax = 0, bmin = 0;
-    for (int n = lane; n < N; n += 64) {
-      float mx = sm[n], mn = sm[n];
-      int cmx = 0, cmn = 0;
-      for (int c = 1; c < C; ++c) {
-        const float v = sm[c * N + n];
-        if (v > mx) { mx = v; cmx = c; }
-        if (v < mn) { mn = v; cmn = c; }
-      }
-      // mix_values = (1 - lam) * max_values + lam * min_values
-      const float mix = __fadd_rn(__fmul_rn(1.f - d.lam, mx), __fmul_rn(d.lam, mn));
-      if (mix > best) { best = mix; arg = n; bmax = cmx; bmin = cmn; }
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ob = __shfl_xor(best, o, 64);
-      const int oa = __shfl_xor(arg, o, 64);
-      const int ox = __shfl_xor(bmax, o, 64), on = __shfl_xor(bmin, o, 64);
-      const bool take = oa >= 0 && (arg < 0 || ob > best || (ob == best && oa < arg));
-      if (take) { best = ob; arg = oa; bmax = ox; bmin = on; }
-    }
-    if (lane == 0) { s_arg = arg < 0 ? 0 : arg; s_cmax = bmax; s_cmin = bmin; }
-  }
+  if (wid == 0) tg_argmax(sm, C, N, d.lam, lane, &s_arg, &s_cmax, &s_cmin);
   __syncthreads();
   const float* qmax = d.q + ((int64_t)s_cmax * BN + b * N + s_arg) * K;
   const float* qmin = d.q + ((int64_t)s_cmin * BN + b * N + s_arg) * K;
@@ -298,22 +301,47 @@ __global__ __launch_bounds__(TG_T) void bcq_target_kernel(d3a_bcq_target_desc d)
 // y_i = r + gamma^n * target_i * (1 - term); per quantile j of q:
 //   l_j = sum_i |tau_j - [y_i - q_j < 0]| * huber(y_i - q_j)
 // loss_cb = sum_j l_j / K; dL/dq_j = -(1/(B K)) sum_i w_ij * huber'(y_i - q_j)
+// (tg_means set: the target row formed here, d3a_bcq_target's arithmetic on
+// the target pass's means and quantiles, by every critic's workgroup of row b)
 __global__ __launch_bounds__(256) void bcq_qr_loss_kernel(d3a_bcq_qr_desc d) {
-  extern __shared__ float ys[];  // [K]
+  extern __shared__ float ys[];  // [K], then (tg_means) the means [tg_C][tg_N]
   __shared__ float scratch[16];
+  __shared__ int s_arg, s_cmax, s_cmin;
   const int t = threadIdx.x;
   const int K = d.K;
   const int64_t c = blockIdx.y, b = blockIdx.x;
+  // this thread's first quantile of q, loaded before the target rows (one
+  // round trip fewer in front of the Huber loop)
+  const float* q = d.q + (c * d.B + b) * K;
+  const float qpre = q[t < K ? t : K - 1];
   const float gam = powf(d.gamma, d.n_steps[b]);
   const float nt = __fsub_rn(1.f, d.term[b]);
-  for (int i = t; i < K; i += 256)
-    ys[i] = __fadd_rn(d.rew[b], __fmul_rn(__fmul_rn(gam, d.target[b * K + i]), nt));
+  if (d.tg_means != nullptr) {  // uniform
+    float* sm = ys + K;
+    const int TC = d.tg_C, TN = d.tg_N;
+    const int64_t BN = (int64_t)d.B * TN;
+    for (int p = t; p < TC * TN; p += 256) {
+      const int cc = p / TN, n = p - cc * TN;
+      sm[p] = d.tg_means[(int64_t)cc * BN + b * TN + n];
+    }
+    __syncthreads();
+    if (t < 64) tg_argmax(sm, TC, TN, d.tg_lam, t, &s_arg, &s_cmax, &s_cmin);
+    __syncthreads();
+    const float* qmax = d.tg_q + ((int64_t)s_cmax * BN + b * TN + s_arg) * K;
+    const float* qmin = d.tg_q + ((int64_t)s_cmin * BN + b * TN + s_arg) * K;
+    for (int i = t; i < K; i += 256) {
+      const float tg = __fadd_rn(__fmul_rn(1.f - d.tg_lam, qmax[i]), __fmul_rn(d.tg_lam, qmin[i]));
+      ys[i] = __fadd_rn(d.rew[b], __fmul_rn(__fmul_rn(gam, tg), nt));
+    }
+  } else {
+    for (int i = t; i < K; i += 256)
+      ys[i] = __fadd_rn(d.rew[b], __fmul_rn(__fmul_rn(gam, d.target[b * K + i]), nt));
+  }
   __syncthreads();
-  const float* q = d.q + (c * d.B + b) * K;
   const float gscale = -1.f / ((float)d.B * (float)K);
   float lsum = 0.f;
   for (int j = t; j < K; j += 256) {
-    const float qj = q[j];
+    const float qj = j == t ? qpre : q[j];
     // taus = ((j + 1) / K + j / K) / 2
     const float tau = __fdiv_rn(__fadd_rn(__fdiv_rn((float)(j + 1), (float)K),
                                           __fdiv_rn((float)j, (float)K)), 2.f);
@@ -451,11 +479,16 @@ extern "C" int d3a_bcq_target(const d3a_bcq_target_desc* d, void* stream) {
 }
 
 extern "C" int d3a_bcq_qr_loss(const d3a_bcq_qr_desc* d, void* stream) {
-  D3A_CHECK_ARG(d && d->q && d->target && d->rew && d->term && d->n_steps && d->dq && d->loss_cb,
+  D3A_CHECK_ARG(d && d->q && (d->target || d->tg_means) && d->rew && d->term && d->n_steps && d->dq &&
+                    d->loss_cb,
                 "d3a_bcq_qr_loss: null pointer");
   D3A_CHECK_ARG(d->K >= 1 && d->K <= 8192 && d->B >= 1 && d->C >= 1, "d3a_bcq_qr_loss: bad sizes");
-  hipLaunchKernelGGL(bcq_qr_loss_kernel, dim3((unsigned)d->B, (unsigned)d->C), dim3(256),
-                     (size_t)d->K * sizeof(float), (hipStream_t)stream, *d);
+  D3A_CHECK_ARG(d->tg_means == nullptr ||
+                    (d->tg_q && d->tg_N >= 1 && d->tg_C >= 1 && d->tg_C * d->tg_N <= 8192),
+                "d3a_bcq_qr_loss: the in-launch target needs tg_q and 1 <= tg_C tg_N <= 8192");
+  const size_t smem = ((size_t)d->K + (d->tg_means ? (size_t)d->tg_C * d->tg_N : 0)) * sizeof(float);
+  hipLaunchKernelGGL(bcq_qr_loss_kernel, dim3((unsigned)d->B, (unsigned)d->C), dim3(256), smem,
+                     (hipStream_t)stream, *d);
   D3A_LAUNCH_CHECK("d3a_bcq_qr_loss");
   return 0;
 }

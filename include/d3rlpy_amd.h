@@ -1003,6 +1003,11 @@ typedef struct d3a_bcq_qr_desc {
   const float* rew; const float* term; const float* n_steps;
   float* dq; float* loss_cb;
   int32_t B, K, C; float gamma;
+  /* optional: the target formed in the loss launch (d3a_bcq_target's
+   * arithmetic, bitwise) from the target pass's quantiles tg_q
+   * [tg_C][B*tg_N][K] and their means tg_means [tg_C][B*tg_N]; target is then
+   * not read (one launch fewer) */
+  const float* tg_q; const float* tg_means; int32_t tg_N, tg_C; float tg_lam;
 } d3a_bcq_qr_desc;
 int d3a_bcq_qr_loss(const d3a_bcq_qr_desc* d, void* stream);
 

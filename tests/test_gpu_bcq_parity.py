@@ -246,3 +246,46 @@ def test_bcq_predict_best_action_shape():
     impl = make_bcq_impl(D, A, H, N, K)
     a = impl.predict_best_action(np.random.RandomState(0).randn(7, D).astype(np.float32))
     assert a.shape == (7, A) and np.all(np.abs(a) <= 1.0)
+
+
+@pytest.mark.parametrize("N,K", [(10, 200), (3, 7)])
+def test_qr_loss_in_launch_target_is_bitwise_the_target_launch(N, K):
+    """d3a_bcq_qr_loss with tg_* (the target rows formed in the loss launch
+    from the target pass's quantiles and means) writes dq and loss_cb bitwise
+    as d3a_bcq_target + d3a_bcq_qr_loss (bcq_impl.py:215-226 +
+    qr_q_function.py:130-150), ties in the means included."""
+    from d3rlpy_amd import _native as N_
+    from d3rlpy_amd import ops
+    dev = torch.device("cuda")
+    B, C, lam, gamma = 64, 2, 0.75, 0.99
+    g = torch.Generator().manual_seed(N * 100 + K)
+    tq = torch.randn(C, B * N, K, generator=g).to(dev)
+    tq[:, ::5] = tq[:, 1::5][:, : tq[:, ::5].shape[1]]  # repeated rows: tied means
+    means = tq.mean(dim=2).contiguous()
+    q = torch.randn(C, B, K, generator=g).to(dev)
+    rew = torch.randn(B, generator=g).to(dev)
+    term = (torch.rand(B, generator=g) < 0.2).float().to(dev)
+    nst = torch.ones(B, device=dev)
+    target = torch.zeros(B, K, device=dev)
+    res = []
+    for fused in (False, True):
+        dq = torch.full((C, B, K), float("nan"), device=dev)
+        loss = torch.full((C, B), float("nan"), device=dev)
+        d = N_.BcqQrDesc()
+        d.q, d.rew, d.term, d.n_steps = q.data_ptr(), rew.data_ptr(), term.data_ptr(), nst.data_ptr()
+        d.dq, d.loss_cb, d.B, d.K, d.C, d.gamma = dq.data_ptr(), loss.data_ptr(), B, K, C, gamma
+        if fused:
+            d.target = None
+            d.tg_q, d.tg_means, d.tg_N, d.tg_C, d.tg_lam = tq.data_ptr(), means.data_ptr(), N, C, lam
+        else:
+            t = N_.BcqTargetDesc()
+            t.q, t.target, t.B, t.N, t.K, t.C, t.lam = tq.data_ptr(), target.data_ptr(), B, N, K, C, lam
+            t.means = means.data_ptr()
+            ops.call_desc("d3a_bcq_target", t)
+            d.target = target.data_ptr()
+        ops.call_desc("d3a_bcq_qr_loss", d)
+        torch.cuda.synchronize()
+        res.append((dq, loss))
+    assert not torch.isnan(res[0][0]).any() and not torch.isnan(res[1][1]).any()
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])

@@ -1,9 +1,9 @@
 #!/bin/bash
-# the parts-path row write-out (BCQ's two remaining d3a_bcq_rows launches):
+# BCQ launch folds (the parts-path row write-out, the in-launch target):
 # tests, a K3 line and its step timeline
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
-O=$R/gpurun_out/r5n
+O=$R/gpurun_out/r5q
 cd $R && mkdir -p $O
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_x6.py tests/test_gpu_bcq_parity.py tests/test_gpu_kernels.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
