@@ -86,6 +86,9 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   // and, for the Q head, the tile-major last chunk carrying the epilogue
   constexpr bool CHUNKIL = (PROBE & 64) == 0 && XL <= 32;
   constexpr bool LASTIL = CHUNKIL && NO == 1 && (PROBE & 128) == 0;
+  // vector instructions interleaved per MFMA (timing probes: bit 9 four, bit 10
+  // sixteen)
+  constexpr int VG = (PROBE & 512) ? 4 : (PROBE & 1024) ? 16 : 8;
   __shared__ __attribute__((aligned(16))) X6FwdLds<XL, NP, NO> L;
   static_assert(sizeof(X6FwdLds<XL, NP, NO>) <= 163840, "LDS");
   static_assert(NO == 1 || 8 * NO * X_RB * 4 <= (int)sizeof(L.h), "head partials fit the ring");
@@ -490,7 +493,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
         for (int m = 0; m < (NP == 3 ? 6 : 1); ++m) {
           __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);  // one MFMA
-          __builtin_amdgcn_sched_group_barrier(0x0002, 8, 0);  // vector instructions
+          __builtin_amdgcn_sched_group_barrier(0x0002, VG, 0);  // vector instructions
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -568,7 +571,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
         for (int m = 0; m < (NP == 3 ? 6 : 1); ++m) {
           __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);  // one MFMA
-          __builtin_amdgcn_sched_group_barrier(0x0002, 8, 0);  // vector instructions
+          __builtin_amdgcn_sched_group_barrier(0x0002, VG, 0);  // vector instructions
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -833,7 +836,7 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
     return e ? atoi(e) : 0;
   }();
   if (probe && xl == 16 && d.n_out == 1) {
-    switch (probe & 511) {
+    switch (probe & 2047) {
       case 1: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 1>), grid, dim3(512), 0, st, d); break;
       case 4: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 4>), grid, dim3(512), 0, st, d); break;
       case 5: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
@@ -845,6 +848,8 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
       case 128: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 128>), grid, dim3(512), 0, st, d); break;
       case 144: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 144>), grid, dim3(512), 0, st, d); break;
       case 256: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 256>), grid, dim3(512), 0, st, d); break;
+      case 512: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 512>), grid, dim3(512), 0, st, d); break;
+      case 1024: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 1024>), grid, dim3(512), 0, st, d); break;
       default: hipLaunchKernelGGL((q2x6_fwd_kernel<16, 5>), grid, dim3(512), 0, st, d); break;
     }
     D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");

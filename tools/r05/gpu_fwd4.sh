@@ -3,9 +3,9 @@
 # CQL tests, a K2 bench line
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
-O=$R/gpurun_out/r5m
+O=$R/gpurun_out/r5r
 cd $R && mkdir -p $O
-for v in 0 64 0 64; do
+for v in 0 512 1024 0 512 1024; do
   D3A_X6_PROBE=$v timeout -k 10 120 python -u tools/bench_fwd.py --x6 --slice --reps 1000 >> $O/fwd.jsonl 2>>$O/fwd.err || exit $?
 done
 D3A_X6_PROBE=16 timeout -k 10 120 python -u tools/bench_fwd.py --x6 --slice --stamps --reps 1 >> $O/fwd.jsonl 2>>$O/fwd.err || exit $?
