@@ -33,6 +33,10 @@ import time
 import numpy as np
 
 
+# the build round: PMC traffic files are read from profiles/r{ROUND}_*
+ROUND = 6
+
+
 def _free_port() -> int:
     import socket
     s = socket.socket()
@@ -643,21 +647,22 @@ def main():
     bf16 = args.precision in ("bf16", "bf16h")
     peak_tflops = 2500.0 if bf16 else (2500.0 / nprod if x6 else 157.3)
     achieved = kflops / kern_s / 1e12
-    traffic = None
+    traffic, traffic_src = None, None
     if args.traffic_json is None:
         prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
-        # the PMC summary of THIS line's dominant kernel: the bf16 and x6 lines
-        # have their own kernels and files (r0N_pmc_traffic_<algo>_<suffix>.json,
-        # the latest round's)
+        # the PMC summary of THIS line's dominant kernel, this round's only:
+        # r{ROUND}_pmc_traffic_<algo><suffix>.json whose bench_desc is this
+        # line's kernel description (no older round's file stands in)
         suffix = f"_{args.precision}" if bf16 else "_x6" if x6 else ""
-        rounds = (5, 4, 3, 2, 1) if not suffix else (5, 4)
-        args.traffic_json = next((p for p in (os.path.join(prof, f"r0{r}_pmc_traffic_{args.algo}"
-                                                           f"{suffix}.json")
-                                              for r in rounds) if os.path.exists(p)), "")
+        args.traffic_json = os.path.join(prof, f"r{ROUND:02d}_pmc_traffic_{args.algo}{suffix}.json")
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                tj = json.load(f)
+            if tj.get("bench_desc") == kdesc:
+                traffic = tj.get("hbm_bytes_per_launch")
+                traffic_src = os.path.relpath(args.traffic_json, os.path.dirname(
+                    os.path.abspath(__file__)))
         except Exception:
             traffic = None
     cpu = None
@@ -753,6 +758,8 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak_tflops,
                      "unit": "TFLOP/s", "frac": round(achieved / peak_tflops, 4),
                      "traffic": traffic, "kernel": kdesc,
+                     "traffic_source": traffic_src or "none: no PMC file of this round "
+                                                     "names this kernel",
                      **({"bf16_mfma_frac": round(nprod * achieved / 2500.0, 4),
                          "peak_note": f"bf16 dense MFMA peak 2500 TF / {nprod} products"}
                         if x6 else {}),

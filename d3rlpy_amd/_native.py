@@ -108,6 +108,18 @@ class AdamBlock(C.Structure):
     _fields_ = [("seg", AdamSegment), ("first", C.c_int64)]
 
 
+class X6SplitJob(C.Structure):
+    _fields_ = [("src", vp), ("dst", vp), ("rows", C.c_int32), ("k", C.c_int32),
+                ("kpad", C.c_int32), ("pad_", C.c_int32)]
+
+
+X6_SPLIT_MAX_JOBS = 4
+
+
+class X6SplitDesc(C.Structure):
+    _fields_ = [("job", X6SplitJob * X6_SPLIT_MAX_JOBS), ("n_jobs", C.c_int32)]
+
+
 class CqlSampleDesc(C.Structure):
     _fields_ = [
         ("head", vp), ("obs", vp), ("next_obs", vp), ("act", vp),
@@ -121,6 +133,7 @@ class CqlSampleDesc(C.Structure):
         ("noise_base", vp), ("rng_ctr", vp), ("eps_actor_out", vp), ("seed", C.c_uint64),
         ("n_normal", C.c_int64), ("gen_noise", C.c_int32),
         ("head_parts", C.c_int32), ("s_head_part", C.c_int64),
+        ("presplit", X6SplitDesc),
     ]
 
 
@@ -278,6 +291,7 @@ class MlpFwdDesc(C.Structure):
         ("hmaskT", vp), ("s_hmaskT", C.c_int64),
         ("xg_a_parts", C.c_int32), ("xg_s_apart", C.c_int64),
         ("xg_xout", vp), ("xg_ldxo", C.c_int64), ("xg_eout", vp),
+        ("wp", vp * 2), ("aux_wp", vp * 2),
     ]
 
 
@@ -530,6 +544,7 @@ _SIGNATURES = {
     "d3a_head1_bwd": (C.c_int, [C.POINTER(Head1BwdDesc), vp]),
     "d3a_head1_min": (C.c_int, [C.POINTER(Head1MinDesc), vp]),
     "d3a_cql_sample": (C.c_int, [C.POINTER(CqlSampleDesc), vp]),
+    "d3a_x6_split": (C.c_int, [C.POINTER(X6SplitDesc), vp]),
     "d3a_cql_loss": (C.c_int, [C.POINTER(CqlLossDesc), vp]),
     "d3a_sac_actor_dq": (C.c_int, [vp, C.c_int64, C.c_int32, C.c_int32, vp, C.c_int64, vp]),
     "d3a_sac_actor_head": (C.c_int, [C.POINTER(SacActorHeadDesc), vp]),

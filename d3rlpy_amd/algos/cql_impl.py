@@ -467,6 +467,12 @@ class _Workspace:
                                     with_mask=not bf16 and mlp.q2_shape(impl.critic))
         self.tacts = mlp.Acts.alloc(impl.critic, B, dev)
         self.aacts = mlp.Acts.alloc(impl.critic, B, dev)
+        # the critic forward's W0 / W1 as split-bf16 operand images of the
+        # online critics and their targets, formed from the step's weights by
+        # the sampler's launch (d3a_cql_sample_desc.presplit) -- no launch of
+        # their own, and no per-workgroup split in the forward
+        self.wimg = (mlp.WeightImages(impl.critic, (impl.store, impl.targ), dev)
+                     if mlp.presplit_ok(impl.critic) and not bf16 else None)
         self.dq = z(C, self.R)
         self.lse = z(2, C, B)
         self.adq = z(C, B)
@@ -500,6 +506,7 @@ class _Workspace:
         if prev:
             raise NotImplementedError("one batch size per CQLImpl is supported")
         self._graphs: Dict[Tuple, torch.cuda.CUDAGraph] = {}
+        self._op_state = None  # tensors the update-step op declares mutated
         self._ran_eager = set()
         self._build_descs()
 
@@ -529,6 +536,8 @@ class _Workspace:
         s.eps_actor_out, s.seed, s.n_normal = self.eps_actor.data_ptr(), self.seed, self.n_normal
         if self.soft:
             s.eps_targ, s.logp_targ = self.eps_targ.data_ptr(), self.logp_targ.data_ptr()
+        if self.wimg is not None:
+            s.presplit = self.wimg.jobs()
         self.sample_desc = s
 
         l = NAT.CqlLossDesc()
@@ -681,7 +690,8 @@ class _Workspace:
             def launch():
                 mlp.forward(net, st, self.x_q.data_ptr(), True, DA, self.qacts, r0, R,
                             h_from=3 * self.NB,
-                            aux=(impl.targ, self.x_targ.data_ptr(), DA, self.tacts))
+                            aux=(impl.targ, self.x_targ.data_ptr(), DA, self.tacts),
+                            wparts=self.wimg.wparts(0, 1) if self.wimg is not None else None)
             flops = 2 * C * (R - r0 + B) * sum(s[l] * s[l + 1] for l in range(len(s) - 1))
             gemm = "fp32"
             if mlp.q2_shape(net):
@@ -690,7 +700,8 @@ class _Workspace:
                 elif ops.CRITIC_PRECISION == "bf16":
                     gemm = "bf16 x1"
                 elif ops.CRITIC_GEMM == "x6":
-                    gemm = "split-bf16 x6"
+                    gemm = ("split-bf16 x6, pre-split W images" if self.wimg is not None
+                            else "split-bf16 x6")
             return launch, flops, (f"d3a_mlp_fwd critic ensemble ({gemm} MFMA): C={C} x "
                                    f"({R - r0} + {B} target) rows x {'-'.join(map(str, s))}")
         H, Hin = s[2], s[1]
@@ -746,7 +757,10 @@ class _Workspace:
             with ops.graph_capture(g):
                 self._enqueue(*flags)
             self._graphs[key] = g
-        g.replay()
+        # the replay through the torch custom op (TORCH_LIBRARY d3rlpy_amd)
+        if self._op_state is None:
+            self._op_state = ops.update_state(self.impl, self)
+        ops.replay_update(g, self._op_state, cql=True)
 
     def _enqueue(self, temp: bool, alpha: bool, critic: bool, actor: bool, targets: bool) -> None:
         impl = self.impl
@@ -772,7 +786,8 @@ class _Workspace:
             # launch (aux pass) when the critic is updated
             targ = (impl.targ, self.x_targ.data_ptr(), DA, self.tacts) if critic else None
             mlp.forward(impl.critic, impl.store, self.x_q.data_ptr(), True, DA, self.qacts, r0, R,
-                        h_from=3 * NB, aux=targ)
+                        h_from=3 * NB, aux=targ,
+                        wparts=self.wimg.wparts(0, 1) if self.wimg is not None else None)
         dp = impl._dp
         if temp or alpha or critic:
             l = self.loss_desc

@@ -579,6 +579,7 @@ class _Workspace:
         else:
             self.opt = AdamGroup(impl.optim_state, self.grads)
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._op_state = None  # tensors the update-step op declares mutated
         self._ran_eager = set()
         self._external_taus = False
         self._build_descs()
@@ -706,7 +707,10 @@ class _Workspace:
             with ops.graph_capture(g):
                 self._enqueue(*flags)
             self._graphs[key] = g
-        g.replay()
+        # the replay through the torch custom op (TORCH_LIBRARY d3rlpy_amd)
+        if self._op_state is None:
+            self._op_state = ops.update_state(self.impl, self)
+        ops.replay_update(g, self._op_state)
 
     def _side(self, i: int) -> torch.cuda.Stream:
         if not hasattr(self, "_sides"):

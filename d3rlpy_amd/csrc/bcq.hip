@@ -486,9 +486,43 @@ extern "C" int d3a_bcq_qr_loss(const d3a_bcq_qr_desc* d, void* stream) {
   D3A_CHECK_ARG(d->tg_means == nullptr ||
                     (d->tg_q && d->tg_N >= 1 && d->tg_C >= 1 && d->tg_C * d->tg_N <= 8192),
                 "d3a_bcq_qr_loss: the in-launch target needs tg_q and 1 <= tg_C tg_N <= 8192");
-  const size_t smem = ((size_t)d->K + (d->tg_means ? (size_t)d->tg_C * d->tg_N : 0)) * sizeof(float);
+  size_t smem = ((size_t)d->K + (d->tg_means ? (size_t)d->tg_C * d->tg_N : 0)) * sizeof(float);
+  // the dynamic LDS (K targets + the in-launch target's C N means) beside
+  // the kernel's static arrays must fit the device's per-workgroup LDS (160
+  // KB here; 64 KB on other parts): otherwise the target rows come from their
+  // own launch (d3a_bcq_target into d->target) and the loss reads them
+  static const size_t lds_max = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
+      v = 65536;
+    return (size_t)v;
+  }();
+  static const size_t lds_static = [] {
+    hipFuncAttributes fa{};
+    return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&bcq_qr_loss_kernel)) == hipSuccess
+               ? (size_t)fa.sharedSizeBytes
+               : (size_t)0;
+  }();
+  d3a_bcq_qr_desc e = *d;
+  if (d->tg_means && smem + lds_static > lds_max) {
+    D3A_CHECK_ARG(d->target != nullptr,
+                  "d3a_bcq_qr_loss: the in-launch target's LDS exceeds the device's; give target "
+                  "(the rows are then formed by d3a_bcq_target first)");
+    d3a_bcq_target_desc t{};
+    t.q = d->tg_q;
+    t.means = d->tg_means;
+    t.target = const_cast<float*>(d->target);  // (written here, read by the loss below)
+    t.B = d->B, t.N = d->tg_N, t.K = d->K, t.C = d->tg_C;
+    t.lam = d->tg_lam;
+    const int rc = d3a_bcq_target(&t, stream);
+    if (rc != 0) return rc;
+    e.tg_means = nullptr;
+    smem = (size_t)d->K * sizeof(float);
+  }
+  D3A_CHECK_ARG(smem + lds_static <= lds_max, "d3a_bcq_qr_loss: K targets exceed the device's LDS");
   hipLaunchKernelGGL(bcq_qr_loss_kernel, dim3((unsigned)d->B, (unsigned)d->C), dim3(256), smem,
-                     (hipStream_t)stream, *d);
+                     (hipStream_t)stream, e);
   D3A_LAUNCH_CHECK("d3a_bcq_qr_loss");
   return 0;
 }

@@ -11,6 +11,7 @@
 // needs no host synchronisation.
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
+#include "x6.hpp"
 
 namespace d3a {
 namespace {
@@ -127,6 +128,13 @@ __global__ __launch_bounds__(SMP_T) void cql_sample_kernel(d3a_cql_sample_desc d
     for (int64_t jj = k; jj < D; jj += 4) xl[jj] = o[jj];
   };
   float t[4] = {0.f, 0.f, 0.f, 0.f};
+  // the step's critic weight images (d3a_x6_split jobs) for the critic
+  // forward that follows: one or two pieces a thread, ahead of the rows
+  if (d.presplit.n_jobs > 0) {
+    const int64_t tot = x6::x6_split_total(d.presplit);
+    for (int64_t p = (int64_t)blockIdx.x * SMP_T + threadIdx.x; p < tot; p += (int64_t)gridDim.x * SMP_T)
+      x6::x6_split_piece(d.presplit, p);
+  }
 
   if (i >= total) {
     // past the last row: nothing (the copy-out skips it)
@@ -729,6 +737,9 @@ extern "C" int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream) {
                     (reinterpret_cast<uintptr_t>(d->x_targ) & 15) == 0 &&
                     (reinterpret_cast<uintptr_t>(d->x_actor) & 15) == 0,
                 "d3a_cql_sample: x_q / x_targ / x_actor must be 16-byte aligned");
+  D3A_CHECK_ARG(x6::x6_split_ok(d->presplit),
+                "d3a_cql_sample: presplit jobs need src, 16-byte aligned dst, 1 <= k <= kpad, "
+                "kpad % 16 == 0");
   const int64_t total = 6LL * d->N * d->B + 4LL * d->B;
   hipLaunchKernelGGL(cql_sample_kernel, dim3((unsigned)((total + SMP_R - 1) / SMP_R)), dim3(SMP_T), 0,
                      (hipStream_t)stream, *d);

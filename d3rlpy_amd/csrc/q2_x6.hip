@@ -78,7 +78,12 @@ struct X6FwdLds {
 // B*N target rows, bcq_impl.py:215-226): head rows staged in LDS, one dot per
 // output, the per-wave partials over the freed chunk ring
 __device__ unsigned long long x6_stamps[2048 * 10];
-template <int XL, int PROBE = 0, int NP = 3, typename HT = float, int NO = 1>
+//
+// PRE: W0 / W1 streamed as pre-split operand images (d3a_mlp_fwd_desc.wp,
+// d3a_x6_split's layout, formed once per step by an earlier launch) instead
+// of fp32 words split in every workgroup -- the split's vector instructions
+// (W1: 128 values a lane, W0: 32) leave the MFMA gaps; bitwise the same parts
+template <int XL, int PROBE = 0, int NP = 3, typename HT = float, int NO = 1, bool PRE = false>
 __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   constexpr int XLD = XL + 8;
   constexpr int NS0 = XL / 16;  // layer-1 k steps
@@ -89,6 +94,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   // vector instructions interleaved per MFMA (timing probes: bit 9 four, bit 10
   // sixteen)
   constexpr int VG = (PROBE & 512) ? 4 : (PROBE & 1024) ? 16 : 8;
+  static_assert(!PRE || (CHUNKIL && NP == 3), "pre-split images: the interleaved schedule");
   __shared__ __attribute__((aligned(16))) X6FwdLds<XL, NP, NO> L;
   static_assert(sizeof(X6FwdLds<XL, NP, NO>) <= 163840, "LDS");
   static_assert(NO == 1 || 8 * NO * X_RB * 4 <= (int)sizeof(L.h), "head partials fit the ring");
@@ -144,14 +150,36 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   // one chunk ahead.  W0 / b0: the wave's layer-1 tile of a chunk, one
   // production ahead.
   float4 wr[X_KS][2];  // raw fp32 W1 of the chunk in flight: [k step][half]
+  // (PRE) the W1 image as a four-slot ring of k steps: slot s holds step s's
+  // parts of the current chunk until its last MFMA, then the next chunk's
+  bf16x8 wq[X_KS][NP];
+  // this lane's W1 image row (unit 32 w + li) at k block lh, and the member's
+  // W0 image (rows of XL / 8 blocks of 48 bytes)
+  const char* wp1l = nullptr;
+  const char* wp0b = nullptr;
+  if constexpr (PRE) {
+    wp1l = static_cast<const char*>(aux ? d.aux_wp[1] : d.wp[1]) +
+           ((int64_t)c * X_H + 32 * w + li) * (X_H * 6) + lh * 48;
+    wp0b = static_cast<const char*>(aux ? d.aux_wp[0] : d.wp[0]) + (int64_t)c * X_H * (XL * 6);
+  }
+  auto load_w1p = [&](int j, int s) {
+    const bf16x8* p = reinterpret_cast<const bf16x8*>(wp1l + (8 * j + 2 * s) * 48);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) wq[s][q] = p[q];
+  };
   auto load_w1 = [&](int j) {
 #pragma unroll
     for (int s = 0; s < X_KS; ++s) {
-      wr[s][0] = *reinterpret_cast<const float4*>(W1 + X_CK * j + 16 * s);
-      wr[s][1] = *reinterpret_cast<const float4*>(W1 + X_CK * j + 16 * s + 4);
+      if constexpr (PRE) {
+        load_w1p(j, s);
+      } else {
+        wr[s][0] = *reinterpret_cast<const float4*>(W1 + X_CK * j + 16 * s);
+        wr[s][1] = *reinterpret_cast<const float4*>(W1 + X_CK * j + 16 * s + 4);
+      }
     }
   };
   float w0n[NS0][8];
+  bf16x8 w0p[NS0][NP];  // (PRE) the W0 image's parts
   float4 b0n[4];
   const int ut = 32 * (w >> 2);  // this wave's unit tile inside a chunk
   const int ptt = w & 3;         // and its row tile
@@ -159,6 +187,16 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   // so that a whole chunk interval covers their latency)
   auto load_w0w = [&](int j) {
     const int u = X_CK * j + ut + li;
+    if constexpr (PRE) {
+      const char* rowp = wp0b + (int64_t)u * (XL * 6);
+#pragma unroll
+      for (int s = 0; s < NS0; ++s) {
+        const bf16x8* p = reinterpret_cast<const bf16x8*>(rowp + (2 * s + lh) * 48);
+#pragma unroll
+        for (int q = 0; q < NP; ++q) w0p[s][q] = p[q];
+      }
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < NS0; ++s)
 #pragma unroll
@@ -261,7 +299,10 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
     for (int s = 0; s < NS0; ++s) {
       bf16x8 wp[NP], xp[NP];
-      if constexpr (CHUNKIL) {
+      if constexpr (PRE) {
+#pragma unroll
+        for (int q = 0; q < NP; ++q) wp[q] = w0p[s][q];
+      } else if constexpr (CHUNKIL) {
         // (as split_w below: keeps the split of the prefetched W0 words from
         // being hoisted next to their loads)
         typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -479,8 +520,10 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
           bp[q] = *reinterpret_cast<const bf16x8*>(hb + q * PS + 32 * tt * X_LDB + 16 * s);
       };
       bf16x8 wl[X_KS][NP], bcur[NP], bnx[NP];
+      if constexpr (!PRE) {
 #pragma unroll
-      for (int s = 0; s < X_KS; ++s) split_w(s, wl[s]);
+        for (int s = 0; s < X_KS; ++s) split_w(s, wl[s]);
+      }
       rd2(0, 0, bcur);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -488,7 +531,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
         const int tt = idx >> 2, s = idx & 3;
         if (idx + 1 < 4 * X_KS) rd2((idx + 1) & 3, (idx + 1) >> 2, bnx);
         if (tt >= 1) tile_epi(tt - 1, s);
-        acc[tt] = prodn<NP>(wl[s], bcur, acc[tt]);
+        acc[tt] = prodn<NP>(PRE ? wq[s] : wl[s], bcur, acc[tt]);
         if (idx + 1 < 4 * X_KS) __builtin_amdgcn_sched_group_barrier(0x0100, NP, 0);  // next reads
 #pragma unroll
         for (int m = 0; m < (NP == 3 ? 6 : 1); ++m) {
@@ -549,15 +592,20 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
         }
       }
       bf16x8 wa[2][NP], bcur[NP], bnx[NP];
-      split_w(0, wa[0]);
-      if (refill) refill_w1(0);
+      if constexpr (!PRE) {
+        split_w(0, wa[0]);
+        if (refill) refill_w1(0);
+      }
       rd(0, bcur);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int idx = 0; idx < 4 * X_KS; ++idx) {
         const int s = idx >> 2, tt = idx & 3;
         if (idx + 1 < 4 * X_KS) rd(idx + 1, bnx);
-        if (tt == 0 && s + 1 < X_KS) {
+        if constexpr (PRE) {
+          // slot s - 1 took its last MFMAs in the region before
+          if (tt == 0 && s >= 1 && refill) load_w1p(j + 1, s - 1);
+        } else if (tt == 0 && s + 1 < X_KS) {
           split_w(s + 1, wa[(s + 1) & 1]);
           if (refill) refill_w1(s + 1);
         }
@@ -565,9 +613,13 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
           const int R = (idx - 5) >> 1;
           epi_run(j + 1, pa, b0n[R], R);
         }
-        acc[tt] = prodn<NP>(wa[s & 1], bcur, acc[tt]);
+        acc[tt] = prodn<NP>(PRE ? wq[s] : wa[s & 1], bcur, acc[tt]);
         if (idx + 1 < 4 * X_KS) __builtin_amdgcn_sched_group_barrier(0x0100, NP, 0);  // next reads
-        if (tt == 0 && s + 1 < X_KS && refill) __builtin_amdgcn_sched_group_barrier(0x0020, 2, 0);
+        if constexpr (PRE) {
+          if (tt == 0 && s >= 1 && refill) __builtin_amdgcn_sched_group_barrier(0x0020, NP, 0);
+        } else if (tt == 0 && s + 1 < X_KS && refill) {
+          __builtin_amdgcn_sched_group_barrier(0x0020, 2, 0);
+        }
 #pragma unroll
         for (int m = 0; m < (NP == 3 ? 6 : 1); ++m) {
           __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);  // one MFMA
@@ -576,6 +628,9 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < NP; ++q) bcur[q] = bnx[q];
+      }
+      if constexpr (PRE) {
+        if (refill) load_w1p(j + 1, X_KS - 1);
       }
       if (more && j + 2 < X_NCK) load_b0(j + 2);
       __syncthreads();  // slot j & 1 free; chunk j + 1 in slot (j + 1) & 1
@@ -826,11 +881,27 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
                 "d3a_q2_fwd_x6: rows x row stride exceeds 2^31");
   D3A_CHECK_ARG((d.r0 + d.rows) * (int64_t)X_H * 4 < (int64_t(1) << 31),
                 "d3a_q2_fwd_x6: kept rows exceed 2 GB (32-bit buffer offsets)");
+  const bool pre = d.wp[0] != nullptr || d.wp[1] != nullptr;
+  if (pre) {
+    auto al = [](const void* p) { return p != nullptr && (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    D3A_CHECK_ARG(d.n_out == 1 && d.n_in <= 32 && d.xg_mode == 0 && al(d.wp[0]) && al(d.wp[1]) &&
+                      (d.aux_rows == 0 || (al(d.aux_wp[0]) && al(d.aux_wp[1]))),
+                  "d3a_q2_fwd_x6: wp needs one output, n_in <= 32, no row builder and 16-byte aligned images "
+                  "for both layers (and the aux pass's)");
+  }
   if (d.rows == 0 && d.aux_rows == 0) return 0;
   const int64_t nb = (d.rows + X_RB - 1) / X_RB + (d.aux_rows + X_RB - 1) / X_RB;
   const dim3 grid((unsigned)nb, 1, (unsigned)d.C);
   const hipStream_t st = (hipStream_t)stream;
   const int xl = (d.n_in + 15) / 16 * 16;
+  if (pre) {
+    if (xl == 16)
+      hipLaunchKernelGGL((q2x6_fwd_kernel<16, 0, 3, float, 1, true>), grid, dim3(512), 0, st, d);
+    else
+      hipLaunchKernelGGL((q2x6_fwd_kernel<32, 0, 3, float, 1, true>), grid, dim3(512), 0, st, d);
+    D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");
+    return 0;
+  }
   static const int probe = [] {
     const char* e = getenv("D3A_X6_PROBE");
     return e ? atoi(e) : 0;
@@ -942,6 +1013,23 @@ extern "C" int d3a_q2_fwd_x1(const d3a_mlp_fwd_desc* dp, void* stream) {
   else
     hipLaunchKernelGGL((q2x6_fwd_kernel<48, 0, 1, float>), grid, dim3(512), 0, st, e);
   D3A_LAUNCH_CHECK("d3a_q2_fwd_x1");
+  return 0;
+}
+
+// ---- d3a_x6_split (include/d3rlpy_amd.h): one piece a thread
+__global__ __launch_bounds__(256) void x6_split_kernel(d3a_x6_split_desc d, int64_t total) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p < total) x6::x6_split_piece(d, p);
+}
+
+extern "C" int d3a_x6_split(const d3a_x6_split_desc* dp, void* stream) {
+  D3A_CHECK_ARG(dp && x6::x6_split_ok(*dp),
+                "d3a_x6_split: jobs need src, 16-byte aligned dst, 1 <= k <= kpad, kpad % 16 == 0");
+  const int64_t total = x6::x6_split_total(*dp);
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(x6_split_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, *dp, total);
+  D3A_LAUNCH_CHECK("d3a_x6_split");
   return 0;
 }
 

@@ -37,6 +37,15 @@
 //   squashed_gaussian_sample(mu, logstd, eps, lo, hi) / _backward
 //                                  SquashedNormalPolicy.sample_with_log_prob
 //                                  (distributions.py:112-135, policies.py:196-216)
+//   cql_update_step(graph, state)  one whole CQLImpl update (CQL._update,
+//                                  algos/cql.py:234-258 over cql_impl.py:119-243,
+//                                  sac_impl.py, ddpg_impl.py): the step's HIP
+//                                  kernels as the update pipeline's captured HIP
+//                                  graph, launched on the current stream; `state`
+//                                  lists the tensors the step mutates (parameters,
+//                                  targets, optimiser state, metric ring) so the
+//                                  dispatcher sees the effect.  update_step: the
+//                                  same for the TD3+BC, BCQ and DiscreteCQL Impls.
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
 #include <torch/library.h>
@@ -558,6 +567,19 @@ std::vector<at::Tensor> squashed_gaussian_sample_backward_meta(
   return {at::empty_like(mu), at::empty_like(mu)};
 }
 
+// the captured update pipeline (a hipGraphExec_t owned by the caller's
+// torch.cuda.CUDAGraph, CUDAGraph.raw_cuda_graph_exec()) launched on the
+// current stream.  The graph draws its noise from the library's own Philox
+// stream (no torch generator state to advance), so the launch is the whole
+// replay.
+void update_step_hip(int64_t graph_exec, at::TensorList state) {
+  TORCH_CHECK(graph_exec != 0, "update_step: null graph");
+  for (const at::Tensor& t : state) TORCH_CHECK(t.is_cuda(), "update_step: state tensors must be on the GPU");
+  const hipError_t e =
+      hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(graph_exec), at::hip::getCurrentHIPStream().stream());
+  TORCH_CHECK(e == hipSuccess, "update_step: hipGraphLaunch failed: ", hipGetErrorString(e));
+}
+
 }  // namespace
 
 TORCH_LIBRARY(d3rlpy_amd, m) {
@@ -583,6 +605,8 @@ TORCH_LIBRARY(d3rlpy_amd, m) {
         "float max_logstd) -> Tensor[]");
   m.def("squashed_gaussian_sample_backward(Tensor grad_action, Tensor grad_log_prob, Tensor mu, "
         "Tensor logstd, Tensor eps, float min_logstd, float max_logstd) -> Tensor[]");
+  m.def("cql_update_step(int graph_exec, Tensor(a!)[] state) -> ()");
+  m.def("update_step(int graph_exec, Tensor(a!)[] state) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(d3rlpy_amd, CUDA, m) {
@@ -604,6 +628,8 @@ TORCH_LIBRARY_IMPL(d3rlpy_amd, CUDA, m) {
   m.impl("iqn_cos_embed_backward", &iqn_cos_embed_backward_hip);
   m.impl("squashed_gaussian_sample", &squashed_gaussian_sample_hip);
   m.impl("squashed_gaussian_sample_backward", &squashed_gaussian_sample_backward_hip);
+  m.impl("cql_update_step", &update_step_hip);
+  m.impl("update_step", &update_step_hip);
 }
 
 TORCH_LIBRARY_IMPL(d3rlpy_amd, Meta, m) {

@@ -194,6 +194,65 @@ __device__ __forceinline__ void input4_finish(const d3a_mlp_fwd_desc& d, int r, 
   }
 }
 
+// ---- d3a_x6_split: the weights' operand images (include/d3rlpy_amd.h).
+// A piece is one 8-wide k block of one row: two 16-byte loads where the row
+// allows, the split8 above (the forward's own split, so a forward streaming
+// the image is bitwise the forward that splits), three 16-byte stores.
+__host__ __device__ inline int64_t x6_split_pieces(const d3a_x6_split_job& j) {
+  return (int64_t)j.rows * (j.kpad >> 3);
+}
+
+__host__ __device__ inline int64_t x6_split_total(const d3a_x6_split_desc& d) {
+  int64_t n = 0;
+  for (int i = 0; i < d.n_jobs; ++i) n += x6_split_pieces(d.job[i]);
+  return n;
+}
+
+// piece p of the desc's pieces (job by job)
+__device__ __forceinline__ void x6_split_piece(const d3a_x6_split_desc& d, int64_t p) {
+  int ji = 0;
+  for (; ji < d.n_jobs - 1; ++ji) {
+    const int64_t n = x6_split_pieces(d.job[ji]);
+    if (p < n) break;
+    p -= n;
+  }
+  const d3a_x6_split_job& j = d.job[ji];
+  const int nkb = j.kpad >> 3;
+  const int64_t r = p / nkb;
+  const int kb = (int)(p - r * nkb);
+  const float* src = j.src + r * j.k + 8 * kb;
+  float v[8];
+  if (8 * kb >= j.k) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;  // the padding blocks
+  } else if ((j.k & 7) == 0 && (reinterpret_cast<uintptr_t>(j.src) & 15) == 0) {
+    const float4 a = reinterpret_cast<const float4*>(src)[0];
+    const float4 b = reinterpret_cast<const float4*>(src)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 8 * kb + i < j.k ? src[i] : 0.f;
+  }
+  bf16x8 pp[3];
+  split8(v, pp);
+  bf16x8* dst = reinterpret_cast<bf16x8*>(static_cast<char*>(j.dst) + (r * nkb + kb) * 48);
+  dst[0] = pp[0];
+  dst[1] = pp[1];
+  dst[2] = pp[2];
+}
+
+inline bool x6_split_ok(const d3a_x6_split_desc& d) {
+  if (d.n_jobs < 0 || d.n_jobs > D3A_X6_SPLIT_MAX_JOBS) return false;
+  for (int i = 0; i < d.n_jobs; ++i) {
+    const d3a_x6_split_job& j = d.job[i];
+    if (!j.src || !j.dst || j.rows < 0 || j.k < 1 || j.kpad < j.k || j.kpad % 16 != 0 ||
+        (reinterpret_cast<uintptr_t>(j.dst) & 15) != 0)
+      return false;
+  }
+  return true;
+}
+
 __device__ __forceinline__ void input4_at(const d3a_mlp_fwd_desc& d, const float* xb, int64_t ldx, int r,
                                           int k4, int rend, int nin, float v[4]) {
   XRaw4 x;

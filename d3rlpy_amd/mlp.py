@@ -168,6 +168,58 @@ _SMALL_BWD = os.environ.get("D3A_SMALL_BWD", "1") == "1"
 _SMALL_WIDE = os.environ.get("D3A_SMALL_WIDE", "1") == "1"
 
 
+# the x6 Q forward streams W0 / W1 as split-bf16 operand images formed once
+# per step by an earlier launch (d3a_mlp_fwd_desc.wp; in the CQL step the
+# sampler's launch forms them) instead of splitting the fp32 weights in every
+# workgroup; D3A_X6_PRESPLIT=0 keeps the in-kernel split (A/B)
+_PRESPLIT = os.environ.get("D3A_X6_PRESPLIT", "1") == "1"
+
+
+def presplit_ok(net: EnsembleMLP) -> bool:
+    """The shape and arithmetic of the pre-split x6 Q forward: [n_in <= 32,
+    256, 256, 1] critics on the fp32-accurate split-bf16 kernels."""
+    return (_PRESPLIT and q2_shape(net) and net.sizes[0] <= 32 and ops.CRITIC_GEMM == "x6"
+            and ops.CRITIC_PRECISION not in ("bf16", "bf16h"))
+
+
+class WeightImages:
+    """Split-bf16 operand images (d3a_x6_split's layout) of a q2 critic's W0
+    and W1, one pair per parameter store (e.g. the online critics and their
+    targets): ``jobs()`` is the d3a_x6_split descriptor that forms them from
+    the stores' current weights, ``wparts(i, j)`` the (W0, W1) images of stores
+    i (main pass) and j (aux pass) for ``forward(..., wparts=...)``.  The
+    images are valid only after the jobs ran on the weights the forward
+    reads."""
+
+    def __init__(self, net: EnsembleMLP, stores, device):
+        assert presplit_ok(net)
+        self.net = net
+        self.xl = (net.sizes[0] + 15) // 16 * 16
+        C, H = net.C, net.sizes[1]
+        self.imgs = [(st, torch.zeros(C * H * self.xl * 3, dtype=torch.bfloat16, device=device),
+                      torch.zeros(C * H * net.sizes[2] * 3, dtype=torch.bfloat16, device=device))
+                     for st in stores]
+
+    def jobs(self) -> "N.X6SplitDesc":
+        net, C = self.net, self.net.C
+        d = N.X6SplitDesc()
+        i = 0
+        for st, w0, w1 in self.imgs:
+            for l, img, k, kpad in ((0, w0, net.sizes[0], self.xl), (1, w1, net.sizes[1], net.sizes[1])):
+                j = d.job[i]
+                j.src, j.dst = net.W(l, st), img.data_ptr()
+                j.rows, j.k, j.kpad = C * net.sizes[l + 1], k, kpad
+                i += 1
+        d.n_jobs = i
+        return d
+
+    def wparts(self, main: int, aux: Optional[int] = None) -> tuple:
+        m = self.imgs[main]
+        a = self.imgs[aux] if aux is not None else None
+        return (m[1].data_ptr(), m[2].data_ptr(),
+                a[1].data_ptr() if a else None, a[2].data_ptr() if a else None)
+
+
 def x6_deep_shape(net: EnsembleMLP) -> bool:
     """>= 3 hidden layers, all 256 wide (the CQL reproduction critic, [obs +
     act, 256, 256, 256, 1]: reproductions/offline/cql.py:21-37): under
@@ -268,7 +320,8 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             members: Optional[int] = None, keep_h: bool = True,
             h_from: Optional[int] = None, aux: Optional[tuple] = None,
             skip_head: bool = False, out_parts: Optional[torch.Tensor] = None,
-            row_mean: Optional[torch.Tensor] = None, xgen=None, xgen_keep: bool = False) -> bool:
+            row_mean: Optional[torch.Tensor] = None, xgen=None, xgen_keep: bool = False,
+            wparts: Optional[tuple] = None) -> bool:
     """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
     (through its first ``members`` members only, when given).  ``keep_h``:
     store the hidden activations in ``acts.h`` (needed by a backward pass),
@@ -291,6 +344,10 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     d3a_bcq_rows writes them, for a later reader; the parts path forms and
     writes them in-kernel (xg_xout / xg_eout), any other path launches
     d3a_bcq_rows first.
+
+    ``wparts`` (WeightImages.wparts): where the launch is the pre-split x6 Q
+    forward, its W0 / W1 (and the aux pass's) are read from those images
+    (formed from the current weights by an earlier launch of the step).
 
     ``row_mean`` ([C][R] fp32): also the mean of each row's outputs, where the
     launch is d3a_mlp_fwd_x6 (its epilogue forms it); returns whether it was
@@ -393,6 +450,12 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             elif acts.no_last_h:
                 raise RuntimeError("Acts.no_last_h: the forward must be the x6 Q forward "
                                    "that writes the mask bits")
+        if (wparts is not None and entry == "d3a_q2_fwd_x6" and presplit_ok(net)
+                and members is None and d.xg_mode == 0):
+            d.wp[0], d.wp[1] = wparts[0], wparts[1]
+            if d.aux_rows:
+                assert wparts[2] is not None and wparts[3] is not None
+                d.aux_wp[0], d.aux_wp[1] = wparts[2], wparts[3]
         means = row_mean is not None and entry == "d3a_mlp_fwd_x6"
         if means:
             assert tuple(row_mean.shape) == (C, R) and row_mean.dtype == torch.float32

@@ -445,6 +445,51 @@ def linear_bwd_w(dy: int, ldy: int, sdyb: int, x: int, ldx: int, sxb: int, dW: i
          rowsum=db, sR=(n_out, C_ * n_out), variant=variant)
 
 
+# D3A_OP_REPLAY=0: replay the update graphs with CUDAGraph.replay instead of
+# the update-step custom op (A/B of the two host paths)
+_OP_REPLAY = os.environ.get("D3A_OP_REPLAY", "1") == "1"
+
+
+def update_state(*objs) -> list:
+    """The device tensors an update step mutates, for the update-step op's
+    ``Tensor(a!)[] state``: every GPU tensor attribute of the given objects
+    (an Impl and its workspace), the flat buffers of their ParamStores and
+    OptimStates, one tensor per storage."""
+    from .nets import OptimState, ParamStore
+    out, seen = [], set()
+
+    def add(t):
+        if torch.is_tensor(t) and t.is_cuda:
+            k = t.untyped_storage().data_ptr()
+            if k not in seen:
+                seen.add(k)
+                out.append(t)
+    for o in objs:
+        for v in vars(o).values():
+            if isinstance(v, ParamStore):
+                add(v.data)
+            elif isinstance(v, OptimState):
+                add(v.exp_avg.data)
+                add(v.exp_avg_sq.data)
+                add(v.step)
+            else:
+                add(v)
+    return out
+
+
+def replay_update(g, state: list, cql: bool = False) -> None:
+    """Launch a captured update pipeline through the PyTorch custom op
+    (``torch.ops.d3rlpy_amd.cql_update_step`` / ``update_step``,
+    csrc/torch_ops.cpp): the graph's exec handle on the current stream, the
+    mutated tensors declared.  No fallback: the op library must be built."""
+    if not _OP_REPLAY:
+        g.replay()  # (A/B: torch.cuda.CUDAGraph.replay)
+        return
+    from . import torch_ops
+    ns = torch_ops.load()
+    (ns.cql_update_step if cql else ns.update_step)(g.raw_cuda_graph_exec(), state)
+
+
 @contextlib.contextmanager
 def graph_capture(g):
     """``torch.cuda.graph(g)`` with Python's cyclic garbage collector paused for

@@ -291,6 +291,15 @@ typedef struct d3a_mlp_fwd_desc {
    * a later stage reads (a backward's dW1) needs no d3a_bcq_rows launch.
    * xg_mode 5: f(a) = a (d3a_bcq_rows mode 0). */
   float* xg_xout; int64_t xg_ldxo; float* xg_eout;
+  /* Optional (d3a_q2_fwd_x6 with one output and n_in <= 32; all four set or
+   * all null): W[0] and W[1] of the main pass (wp) and of the aux pass
+   * (aux_wp) as split-bf16 operand images -- d3a_x6_split's layout with kpad
+   * = n_in rounded up to 16 (W[0]) and 256 (W[1]), every member's rows --
+   * formed by an earlier launch from the same weights.  The kernel streams the
+   * parts instead of splitting the fp32 weights in every workgroup; its
+   * results are bitwise those of the in-kernel split.                       */
+  const void* wp[2];
+  const void* aux_wp[2];
 } d3a_mlp_fwd_desc;
 #define D3A_MLP_PARTS 4
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);
@@ -326,7 +335,11 @@ typedef struct d3a_mlp_bwd_desc {
 int d3a_mlp_bwd(const d3a_mlp_bwd_desc* d, void* stream);
 
 /* The whole backward of a small-batch [n_in <= 64, 256, 256, n_out <= 256]
- * ReLU MLP in one launch (csrc/mlp_bwd_small.hip; replaces the per-layer
+ * ReLU MLP in two launches on one stream (csrc/mlp_bwd_small.hip: stage A,
+ * one workgroup per 32 rows x 32 units of the second hidden layer -- dW3 /
+ * dW2 / db2 of its unit slice and its share of dz2 W2 into scratch; stage B,
+ * one workgroup per 32-row block -- the eight shares summed in order, dz1,
+ * dW1 / db1 / dx; replaces the per-layer
  * split-K / input-gradient GEMMs of the autograd of encoders.py:265-275,
  * 328-339 and the heads -- K3's VAE, QR critics and residual policy,
  * bcq_impl.py:132-161, ddpg_impl.py:138-165).  dout = dL/d(out) [C][rows]
@@ -334,9 +347,9 @@ int d3a_mlp_bwd(const d3a_mlp_bwd_desc* d, void* stream);
  * ([C][.][256], member stride sh, row 0 = the first row here), x [C][rows]
  * [ldx] (sxb 0: shared).  Weight / bias gradients (all or none) as one
  * partial per 32-row block, [ceil(rows / 32)][C][out][in]; dx (optional)
- * [C][rows][n_in].  scratch: [8][C][rows][256] floats; tickets: C *
- * ceil(rows / 32) int32, zero before the first launch (each launch leaves
- * them zero).  Exact fp32 arithmetic. */
+ * [C][rows][n_in].  scratch: [8][C][rows][256] floats (stage A -> stage B);
+ * tickets: reserved, not read (may be NULL; the one-launch ticketed form was
+ * measured slower and removed).  Exact fp32 arithmetic. */
 typedef struct d3a_mlp_bwd_small_desc {
   const float* x; int64_t ldx, sxb;
   const float* h1; const float* h2; int64_t sh;
@@ -616,6 +629,29 @@ int d3a_philox_fill(float* out, int64_t n_normal, int64_t n_uniform, float lo,
                     float hi, uint64_t seed, int64_t* ctr,
                     unsigned int* ticket, void* stream);
 
+/* ---- split-bf16 operand images of critic weights ------------------------ */
+
+/* Exact three-way split of fp32 weights into bf16 parts, laid out as the
+ * split-bf16 critic forward's MFMA A operand (d3a_mlp_fwd_desc.wp): for row
+ * r < rows and 8-wide k block kb < kpad / 8, dst + (r * (kpad / 8) + kb) * 48
+ * bytes holds parts 0, 1, 2 of src[r][8 kb .. 8 kb + 7] (8 bf16 each; x = p0
+ * + p1 + p2 exactly: p0 = bf16(x), p1 = bf16(x - p0), p2 = bf16(x - p0 -
+ * p1)), columns k .. kpad zero.  src is row-major [rows][k] (nn.Linear's
+ * weight, members stacked); kpad a multiple of 16, >= k; dst 16-byte aligned.
+ * No reference counterpart: the reference multiplies the fp32 weights
+ * (encoders.py:265-275, 328-339); this is the same product's operand. */
+typedef struct d3a_x6_split_job {
+  const float* src;
+  void* dst;
+  int32_t rows, k, kpad, pad_;
+} d3a_x6_split_job;
+#define D3A_X6_SPLIT_MAX_JOBS 4
+typedef struct d3a_x6_split_desc {
+  d3a_x6_split_job job[D3A_X6_SPLIT_MAX_JOBS];
+  int32_t n_jobs;
+} d3a_x6_split_desc;
+int d3a_x6_split(const d3a_x6_split_desc* d, void* stream);
+
 /* ---- CQL / SAC fused stages (d3rlpy/algos/torch/cql_impl.py,
  *      sac_impl.py) ------------------------------------------------------- */
 
@@ -668,6 +704,10 @@ typedef struct d3a_cql_sample_desc {
    * head + p*s_head_part (d3a_mlp_fwd parts), summed in order here */
   int32_t head_parts;
   int64_t s_head_part;
+  /* presplit.n_jobs > 0: this launch also runs those d3a_x6_split jobs (the
+   * critic weights the step's critic forward streams as parts, formed by the
+   * launch before it -- no launch of their own). */
+  d3a_x6_split_desc presplit;
 } d3a_cql_sample_desc;
 int d3a_cql_sample(const d3a_cql_sample_desc* d, void* stream);
 

@@ -45,6 +45,11 @@ def test_argument_errors_are_reported_without_a_gpu():
         N.check(rc, "d3a_gemm_f32")
 
 
+import os
+
+# the uint8 first-layer weight-gradient kernel switched off (A/B runs)
+_U8S4_OFF = os.environ.get("D3A_CONV1_U8S4", "1") == "0"
+
 STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_gemm_wnext", "GemmWnext"),
            ("d3a_adam_segment", "AdamSegment"), ("d3a_adam_desc", "AdamDesc"),
            ("d3a_head1_bwd_desc", "Head1BwdDesc"), ("d3a_head1_min_desc", "Head1MinDesc"),
@@ -64,7 +69,8 @@ STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_gemm_wnext", "GemmWnext"),
            ("d3a_iqn_head_bwd_desc", "IqnHeadBwdDesc"), ("d3a_conv_desc", "ConvDesc"),
            ("d3a_iqn_embed_head_desc", "IqnEmbedHeadDesc"),
            ("d3a_iqn_head_bwd_fused_desc", "IqnHeadBwdFusedDesc"),
-           ("d3a_mlp_bwd_small_desc", "MlpBwdSmallDesc"))
+           ("d3a_mlp_bwd_small_desc", "MlpBwdSmallDesc"),
+           ("d3a_x6_split_job", "X6SplitJob"), ("d3a_x6_split_desc", "X6SplitDesc"))
 
 
 def test_struct_layouts_match_header(tmp_path):
@@ -114,7 +120,9 @@ def test_round4_entry_points_validate_and_size_without_a_gpu():
 
     u8 = conv(512, 4, 84, 84, 32, 8, 4)
     u8.x_u8 = 16
-    assert lib.d3a_conv_bwd_w_splits(ctypes.byref(u8)) == 256
+    # (256 splits on the uint8 first-layer kernel; D3A_CONV1_U8S4=0, the A/B
+    # switch back to the generic fp32 kernel, keeps its 32)
+    assert lib.d3a_conv_bwd_w_splits(ctypes.byref(u8)) == (32 if _U8S4_OFF else 256)
     l2, l3 = conv(512, 32, 20, 20, 64, 4, 2), conv(512, 64, 9, 9, 64, 3, 1)
     l2.x_f32 = l3.x_f32 = 16
     assert lib.d3a_conv_bwd_w_splits(ctypes.byref(l2)) == 32
@@ -140,7 +148,7 @@ def test_dcql_workspace_sizes_the_uint8_conv_like_its_launch():
     256 splits), not the split-bf16 count of an fp32 input of that shape."""
     from d3rlpy_amd.algos.discrete_cql_impl import _geometry, conv_wgrad_splits
     geom = _geometry((4, 84, 84))
-    assert conv_wgrad_splits(geom, 0, 512) == 256
+    assert conv_wgrad_splits(geom, 0, 512) == (32 if _U8S4_OFF else 256)
     assert conv_wgrad_splits(geom, 1, 512) == 32
     assert conv_wgrad_splits(geom, 2, 512) == 29
 
@@ -156,3 +164,23 @@ def test_slice_backward_row_blocks():
     assert lib.d3a_q2_bwd_x6t_splits(256, 2) == 2
     assert lib.d3a_q2_bwd_x6t_splits(32, 2) == 1
     assert lib.d3a_q2_bwd_x6t_splits(100, 0) < 0
+
+
+def test_presplit_forward_and_split_validate_without_a_gpu():
+    """d3a_q2_fwd_x6 with weight images (wp) needs n_in <= 32 and aligned
+    images for both layers; d3a_x6_split needs kpad % 16 == 0 and kpad >= k."""
+    from d3rlpy_amd import _native as N
+    lib = N.lib()
+    d = N.MlpFwdDesc()
+    d.n_in, d.n_hidden, d.H, d.n_out, d.C, d.rows, d.ldout = 40, 2, 256, 1, 1, 10, 1
+    d.x = d.out = 16
+    for l in range(3):
+        d.W[l] = d.b[l] = 16
+    d.wp[0], d.wp[1] = 16, 16
+    assert lib.d3a_q2_fwd_x6(ctypes.byref(d), None) < 0
+    assert b"wp needs" in lib.d3a_last_error()
+    s = N.X6SplitDesc()
+    s.n_jobs = 1
+    s.job[0].src, s.job[0].dst, s.job[0].rows, s.job[0].k, s.job[0].kpad = 16, 16, 4, 14, 8
+    assert lib.d3a_x6_split(ctypes.byref(s), None) < 0
+    assert b"kpad % 16" in lib.d3a_last_error()

@@ -40,6 +40,16 @@ def test_ops_registered_with_schemas():
         assert torch._C._dispatch_has_kernel_for_dispatch_key(f"d3rlpy_amd::{name}", "Meta")
 
 
+def test_update_step_ops_registered():
+    """The shipped Impls replay their captured update pipelines through
+    torch.ops.d3rlpy_amd.cql_update_step / update_step (ops.replay_update)."""
+    ops = torch_ops.load()
+    for name in ("cql_update_step", "update_step"):
+        assert str(getattr(ops, name).default._schema) == (
+            f"d3rlpy_amd::{name}(int graph_exec, Tensor(a!)[] state) -> ()")
+        assert torch._C._dispatch_has_kernel_for_dispatch_key(f"d3rlpy_amd::{name}", "CUDA")
+
+
 def test_meta_shapes_of_loss_and_backward_ops():
     ops = torch_ops.load()
     m = lambda *s: torch.empty(*s, device="meta")  # noqa: E731
@@ -202,3 +212,44 @@ def test_torchscript_roundtrip_and_save_policy(tmp_path):
     xo = ds.observations[:33]
     got = prog(torch.as_tensor(xo, device="cuda")).cpu().numpy()
     np.testing.assert_allclose(got, algo.predict(xo), rtol=2e-6, atol=2e-6)
+
+
+@pytest.mark.gpu
+def test_cql_impl_replays_through_the_update_step_op(monkeypatch):
+    """CQLImpl.update_step's graph replays go through the custom op, and three
+    replayed steps are bitwise the CUDAGraph.replay path's (D3A_OP_REPLAY=0)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from cql_helpers import HostBatch, make_batch, make_impl
+    from d3rlpy_amd import ops as dops
+    D, A, N_, B = 11, 3, 10, 256
+    calls = []
+    real = dops.replay_update
+
+    def spy(g, state, cql=False):
+        calls.append((dops._OP_REPLAY, cql, len(state)))
+        real(g, state, cql)
+    monkeypatch.setattr(dops, "replay_update", spy)
+    impls = []
+    for via_op in (True, False):
+        torch.manual_seed(0)
+        impl = make_impl(D, A, [256, 256], N_)
+        if impls:
+            impl.set_state_dict(impls[0].get_state_dict())
+        impls.append((impl, via_op))
+    for impl, via_op in impls:
+        monkeypatch.setattr(dops, "_OP_REPLAY", via_op)
+        rs = np.random.RandomState(2)
+        ws = impl._workspace(B)
+        ws.seed = 1234  # both impls draw the same device noise
+        ws._build_descs()
+        for _ in range(4):  # eager, capture + replay, replay, replay
+            impl.update_step(HostBatch(*make_batch(rs, B, D, A)))
+        torch.cuda.synchronize()
+    assert any(c[0] and c[1] and c[2] > 8 for c in calls)
+    s0, s1 = impls[0][0].get_state_dict(), impls[1][0].get_state_dict()
+    for k in s0:
+        for n in s0[k]:
+            if torch.is_tensor(s0[k][n]):
+                assert torch.equal(s0[k][n], s1[k][n]), (k, n)

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--slice", action="store_true",
                     help="x6: the production critic forward of the slice backward -- row and "
                          "transposed mask bits, no kept h2")
+    ap.add_argument("--pre", action="store_true",
+                    help="x6: W0 / W1 streamed as pre-split images (d3a_x6_split, desc.wp)")
+    ap.add_argument("--warm", type=int, default=5, help="untimed launches before the timed ones")
     ap.add_argument("--stamps", action="store_true",
                     help="with D3A_X6_PROBE=16: per-phase s_memtime cycles of wave 0, averaged "
                          "over the workgroups")
@@ -84,7 +87,23 @@ def main():
     if a.aux:
         d.aux_x, d.aux_ldx, d.aux_sxb, d.aux_wdelta = xa.data_ptr(), ldx, 0, n_par
         d.aux_out, d.aux_sout, d.aux_rows = aout.data_ptr(), a.aux * a.J, a.aux
-    for _ in range(5):
+    if a.pre:
+        xl = (a.n_in + 15) // 16 * 16
+        imgs = []
+        for si in range(2 if a.aux else 1):
+            w0 = torch.zeros(C * H * xl * 3, dtype=torch.bfloat16, device=dev)
+            w1 = torch.zeros(C * H * H * 3, dtype=torch.bfloat16, device=dev)
+            sd = N.X6SplitDesc()
+            for i, (l, im, k, kp) in enumerate(((0, w0, a.n_in, xl), (1, w1, H, H))):
+                sd.job[i].src = store.data_ptr() + 4 * (si * n_par + offs[l][0])
+                sd.job[i].dst, sd.job[i].rows, sd.job[i].k, sd.job[i].kpad = im.data_ptr(), C * H, k, kp
+            sd.n_jobs = 2
+            ops.call_desc("d3a_x6_split", sd)
+            imgs.append((w0, w1))
+        d.wp[0], d.wp[1] = imgs[0][0].data_ptr(), imgs[0][1].data_ptr()
+        if a.aux:
+            d.aux_wp[0], d.aux_wp[1] = imgs[1][0].data_ptr(), imgs[1][1].data_ptr()
+    for _ in range(a.warm):
         ops.call_desc(entry, d)
     torch.cuda.synchronize()
     # check against torch fp32 on a row sample
@@ -120,7 +139,7 @@ def main():
         ph = np.diff(st[:, :9], axis=1)
         stamps = {"phase_cycles_mean": [round(float(v), 1) for v in ph.mean(0)],
                   "total_cycles_mean": round(float((st[:, 8] - st[:, 0]).mean()), 1)}
-    print(json.dumps({"kernel": entry, "hmask": a.hmask, "slice": a.slice, "rows": a.rows, "aux": a.aux, "bm": a.bm, "C": C, "J": a.J,
+    print(json.dumps({"kernel": entry, "pre": a.pre, "hmask": a.hmask, "slice": a.slice, "rows": a.rows, "aux": a.aux, "bm": a.bm, "C": C, "J": a.J,
                       "variant": os.environ.get("D3A_FWD_PROBE", "") + os.environ.get("D3A_X6_PROBE", "") + ("generic" if os.environ.get("D3A_FWD_Q2") == "0" else ""),
                       "stamps": stamps,
                       "avg_us": round(us, 2), "tflops": round(flops / us / 1e6, 2),

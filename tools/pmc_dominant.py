@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--transitions", type=int, default=200_000)
     ap.add_argument("--precision", choices=["fp32", "bf16", "bf16h"], default="fp32")
     ap.add_argument("--critic-gemm", choices=["fp32", "x6"], default=None)
+    ap.add_argument("--desc-out", default=None,
+                    help="write {desc, flops} of the launched kernel here (bench.py matches a "
+                         "traffic file to its line by this desc)")
     a = ap.parse_args()
     from d3rlpy_amd import ops
     if a.precision != "fp32":
@@ -38,6 +41,10 @@ def main():
         launch()
     torch.cuda.synchronize()
     print(desc, flops)
+    if a.desc_out:
+        import json
+        with open(a.desc_out, "w") as f:
+            json.dump({"desc": desc, "flops": flops, "algo": a.algo}, f)
 
 
 if __name__ == "__main__":
