@@ -101,6 +101,8 @@ class AdamDesc(C.Structure):
         ("metrics", vp), ("n_metrics", C.c_int32),
         ("ring", vp), ("ring_cap", C.c_int64), ("ring_ctr", vp), ("metric_scale", C.c_float),
         ("blocks", vp),
+        ("commit_src", vp), ("commit_dst", vp * 8), ("n_commit", C.c_int32),
+        ("commit_step", vp * 2),
     ]
 
 
@@ -153,6 +155,7 @@ class CqlLossDesc(C.Structure):
         ("dp_phase", C.c_int32), ("scalar_grads", vp), ("grad_scale", C.c_float),
         ("logp_targ", vp), ("soft_target", C.c_int32), ("conservative", C.c_int32),
         ("ticket", vp),
+        ("split", C.c_int32), ("td2", vp), ("bc", vp), ("stage", vp),
     ]
 
 
@@ -583,6 +586,7 @@ _SIGNATURES = {
     "d3a_q2_bwd_bf16": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
     "d3a_q2_fwd_x6": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_q2_bwd_x6": (C.c_int, [C.POINTER(Q2BwdDesc), vp]),
+    "d3a_q2_bwd_x6_cql": (C.c_int, [C.POINTER(Q2BwdDesc), C.POINTER(CqlLossDesc), vp]),
     "d3a_q2_fwd_x1": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_iqn_embed_head": (C.c_int, [C.POINTER(IqnEmbedHeadDesc), vp]),
     "d3a_iqn_head_bwd_fused": (C.c_int, [C.POINTER(IqnHeadBwdFusedDesc), vp]),

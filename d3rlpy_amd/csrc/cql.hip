@@ -129,12 +129,14 @@ __global__ __launch_bounds__(SMP_T) void cql_sample_kernel(d3a_cql_sample_desc d
   };
   float t[4] = {0.f, 0.f, 0.f, 0.f};
   // the step's critic weight images (d3a_x6_split jobs) for the critic
-  // forward that follows: one or two pieces a thread, ahead of the rows
-  if (d.presplit.n_jobs > 0) {
-    const int64_t tot = x6::x6_split_total(d.presplit);
-    for (int64_t p = (int64_t)blockIdx.x * SMP_T + threadIdx.x; p < tot; p += (int64_t)gridDim.x * SMP_T)
-      x6::x6_split_piece(d.presplit, p);
-  }
+  // forward that follows: a thread's first piece is loaded here, ahead of its
+  // row's loads, and split and stored after the row (one memory round trip
+  // for both); pieces past the grid's threads (a grid smaller than the
+  // images) follow in a loop
+  const int64_t ps_tot = d.presplit.n_jobs > 0 ? x6::x6_split_total(d.presplit) : 0;
+  const int64_t ps_p = (int64_t)blockIdx.x * SMP_T + threadIdx.x;
+  x6::X6Piece ps_piece;
+  if (ps_tot > 0) x6::x6_split_load(d.presplit, ps_p < ps_tot ? ps_p : ps_tot - 1, ps_piece);
 
   if (i >= total) {
     // past the last row: nothing (the copy-out skips it)
@@ -237,6 +239,9 @@ __global__ __launch_bounds__(SMP_T) void cql_sample_kernel(d3a_cql_sample_desc d
     const float* sr = xs + r2 * LS + c4;
     *reinterpret_cast<float4*>(dst + c4) = make_float4(sr[0], sr[1], sr[2], sr[3]);
   }
+  if (ps_p < ps_tot) x6::x6_split_store(ps_piece);
+  for (int64_t p = ps_p + (int64_t)gridDim.x * SMP_T; p < ps_tot; p += (int64_t)gridDim.x * SMP_T)
+    x6::x6_split_piece(d.presplit, p);
 }
 
 // Adam on a single scalar parameter (torch single-tensor path) held in

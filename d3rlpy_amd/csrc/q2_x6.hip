@@ -83,7 +83,11 @@ __device__ unsigned long long x6_stamps[2048 * 10];
 // d3a_x6_split's layout, formed once per step by an earlier launch) instead
 // of fp32 words split in every workgroup -- the split's vector instructions
 // (W1: 128 values a lane, W0: 32) leave the MFMA gaps; bitwise the same parts
-template <int XL, int PROBE = 0, int NP = 3, typename HT = float, int NO = 1, bool PRE = false>
+//
+// NOH2 (with PRE; host: d.h[1] null, as for the slice backward, which reads
+// the mask bits instead of h2): the last chunk issues no h2 stores at all
+template <int XL, int PROBE = 0, int NP = 3, typename HT = float, int NO = 1, bool PRE = false,
+          bool NOH2 = false>
 __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
   constexpr int XLD = XL + 8;
   constexpr int NS0 = XL / 16;  // layer-1 k steps
@@ -221,7 +225,11 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
     static_assert(X_RB * X4 == 512 * NPC, "whole pieces a thread");
     const float* xb = aux ? d.aux_x + c * d.aux_sxb : d.x + c * d.sxb;
     const int64_t ldx = aux ? d.aux_ldx : d.ldx;
-    const bool vec = d.xg_mode == 0 && (ldx & 3) == 0 && (reinterpret_cast<uintptr_t>(xb) & 15) == 0;
+    // (PRE: plain 16-byte rows, checked on the host -- no row-builder code,
+    // whose branchy loads made the compiler wait for every load in flight,
+    // the W1 stream's included, before staging x)
+    const bool vec =
+        PRE || (d.xg_mode == 0 && (ldx & 3) == 0 && (reinterpret_cast<uintptr_t>(xb) & 15) == 0);
     float4 f[NPC];
 #pragma unroll
     for (int pc = 0; pc < NPC; ++pc) {
@@ -240,10 +248,16 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
       const int e = t + 512 * pc, m = e / X4, k4 = (e - m * X4) * 4, r = m0 + m;
       float v[4];
       if (vec) {
-        const float fv[4] = {f[pc].x, f[pc].y, f[pc].z, f[pc].w};
+        // (the whole piece through an empty asm: the compiler otherwise
+        // narrows the load to the elements the selects below may keep and
+        // loads the rest under a branch that waits for every load in flight)
+        typedef float f32x4v __attribute__((ext_vector_type(4)));
+        f32x4v ff = {f[pc].x, f[pc].y, f[pc].z, f[pc].w};
+        asm volatile("" : "+v"(ff));
+        const float fv[4] = {ff.x, ff.y, ff.z, ff.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = (r < rend && k4 + j < nin) ? fv[j] : 0.f;
-      } else {
+      } else if constexpr (!PRE) {
         input4_at(d, xb, ldx, r, k4, rend, nin, v);
       }
       bf16x4 p[NP];
@@ -433,7 +447,7 @@ __global__ __launch_bounds__(512) void q2x6_fwd_kernel(d3a_mlp_fwd_desc d) {
         for (int r = 0; r < 16; ++r) vt[r] = fmaxf(acc[tt][r] + bb[r], 0.f);
         const bool kp = h1g != nullptr && in && !(PROBE & 4);
 #pragma unroll
-        for (int R = 0; R < 4; ++R) {
+        for (int R = 0; R < (NOH2 ? 0 : 4); ++R) {
           const uint32_t off =
               kp ? (uint32_t)((row * X_H + 32 * w + 8 * R + 4 * lh) * (int)sizeof(HT)) : 0x80000000u;
           if constexpr (sizeof(HT) == 4) {
@@ -885,9 +899,11 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
   if (pre) {
     auto al = [](const void* p) { return p != nullptr && (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     D3A_CHECK_ARG(d.n_out == 1 && d.n_in <= 32 && d.xg_mode == 0 && al(d.wp[0]) && al(d.wp[1]) &&
-                      (d.aux_rows == 0 || (al(d.aux_wp[0]) && al(d.aux_wp[1]))),
-                  "d3a_q2_fwd_x6: wp needs one output, n_in <= 32, no row builder and 16-byte aligned images "
-                  "for both layers (and the aux pass's)");
+                      (d.aux_rows == 0 || (al(d.aux_wp[0]) && al(d.aux_wp[1]))) && al(d.x) &&
+                      d.ldx % 4 == 0 && d.sxb % 4 == 0 &&
+                      (d.aux_rows == 0 || (al(d.aux_x) && d.aux_ldx % 4 == 0 && d.aux_sxb % 4 == 0)),
+                  "d3a_q2_fwd_x6: wp needs one output, n_in <= 32, no row builder, 16-byte aligned "
+                  "images for both layers (and the aux pass's) and 16-byte input rows");
   }
   if (d.rows == 0 && d.aux_rows == 0) return 0;
   const int64_t nb = (d.rows + X_RB - 1) / X_RB + (d.aux_rows + X_RB - 1) / X_RB;
@@ -895,8 +911,19 @@ extern "C" int d3a_q2_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
   const hipStream_t st = (hipStream_t)stream;
   const int xl = (d.n_in + 15) / 16 * 16;
   if (pre) {
-    if (xl == 16)
+    static const int pprobe = [] {
+      const char* e = getenv("D3A_X6_PROBE");
+      return e ? atoi(e) : 0;
+    }();
+    const bool noh2 = d.h[1] == nullptr;
+    if (xl == 16 && pprobe == 16 && noh2)  // (diagnostic: phase stamps, d3a_x6_stamps)
+      hipLaunchKernelGGL((q2x6_fwd_kernel<16, 16, 3, float, 1, true, true>), grid, dim3(512), 0, st, d);
+    else if (xl == 16 && noh2)
+      hipLaunchKernelGGL((q2x6_fwd_kernel<16, 0, 3, float, 1, true, true>), grid, dim3(512), 0, st, d);
+    else if (xl == 16)
       hipLaunchKernelGGL((q2x6_fwd_kernel<16, 0, 3, float, 1, true>), grid, dim3(512), 0, st, d);
+    else if (noh2)
+      hipLaunchKernelGGL((q2x6_fwd_kernel<32, 0, 3, float, 1, true, true>), grid, dim3(512), 0, st, d);
     else
       hipLaunchKernelGGL((q2x6_fwd_kernel<32, 0, 3, float, 1, true>), grid, dim3(512), 0, st, d);
     D3A_LAUNCH_CHECK("d3a_q2_fwd_x6");

@@ -208,8 +208,16 @@ __host__ __device__ inline int64_t x6_split_total(const d3a_x6_split_desc& d) {
   return n;
 }
 
-// piece p of the desc's pieces (job by job)
-__device__ __forceinline__ void x6_split_piece(const d3a_x6_split_desc& d, int64_t p) {
+// piece p of the desc's pieces (job by job), in two halves: the loads
+// (branch-free: clamped indices, the padding selected to zero after the load,
+// so a caller can issue them ahead of its own work without the compiler
+// waiting for them early) and the split + stores
+struct X6Piece {
+  float v[8];
+  char* dst;  // the piece's 48 bytes
+};
+
+__device__ __forceinline__ void x6_split_load(const d3a_x6_split_desc& d, int64_t p, X6Piece& o) {
   int ji = 0;
   for (; ji < d.n_jobs - 1; ++ji) {
     const int64_t n = x6_split_pieces(d.job[ji]);
@@ -220,26 +228,37 @@ __device__ __forceinline__ void x6_split_piece(const d3a_x6_split_desc& d, int64
   const int nkb = j.kpad >> 3;
   const int64_t r = p / nkb;
   const int kb = (int)(p - r * nkb);
-  const float* src = j.src + r * j.k + 8 * kb;
-  float v[8];
-  if (8 * kb >= j.k) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = 0.f;  // the padding blocks
-  } else if ((j.k & 7) == 0 && (reinterpret_cast<uintptr_t>(j.src) & 15) == 0) {
-    const float4 a = reinterpret_cast<const float4*>(src)[0];
-    const float4 b = reinterpret_cast<const float4*>(src)[1];
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  const float* row = j.src + r * j.k;
+  const bool vec = (j.k & 7) == 0 && (reinterpret_cast<uintptr_t>(j.src) & 15) == 0;
+  if (vec) {
+    // (a padding block reads the row's first block, zeroed below)
+    const int kc = 8 * kb < j.k ? 8 * kb : 0;
+    const float4 a = reinterpret_cast<const float4*>(row + kc)[0];
+    const float4 b = reinterpret_cast<const float4*>(row + kc)[1];
+    o.v[0] = a.x; o.v[1] = a.y; o.v[2] = a.z; o.v[3] = a.w;
+    o.v[4] = b.x; o.v[5] = b.y; o.v[6] = b.z; o.v[7] = b.w;
   } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = 8 * kb + i < j.k ? src[i] : 0.f;
+    for (int i = 0; i < 8; ++i) o.v[i] = row[min(8 * kb + i, j.k - 1)];
   }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o.v[i] = 8 * kb + i < j.k ? o.v[i] : 0.f;
+  o.dst = static_cast<char*>(j.dst) + (r * nkb + kb) * 48;
+}
+
+__device__ __forceinline__ void x6_split_store(const X6Piece& o) {
   bf16x8 pp[3];
-  split8(v, pp);
-  bf16x8* dst = reinterpret_cast<bf16x8*>(static_cast<char*>(j.dst) + (r * nkb + kb) * 48);
+  split8(o.v, pp);
+  bf16x8* dst = reinterpret_cast<bf16x8*>(o.dst);
   dst[0] = pp[0];
   dst[1] = pp[1];
   dst[2] = pp[2];
+}
+
+__device__ __forceinline__ void x6_split_piece(const d3a_x6_split_desc& d, int64_t p) {
+  X6Piece o;
+  x6_split_load(d, p, o);
+  x6_split_store(o);
 }
 
 inline bool x6_split_ok(const d3a_x6_split_desc& d) {

@@ -424,6 +424,19 @@ typedef struct d3a_q2_bwd_desc {
  * (about 256 workgroups of C * P * 16; the caller sizes the partials with it). */
 int32_t d3a_q2_bwd_x6t_splits(int64_t rows, int32_t C);
 int d3a_q2_bwd(const d3a_q2_bwd_desc* d, void* stream);
+/* d3a_q2_bwd_x6's slice kernel with the CQL loss stage in every workgroup's
+ * prologue (no launch of its own): from the logsumexp stage's outputs (loss
+ * with split set; d.g = dq at the critic set's first row, n_scaled = 3NB) each
+ * workgroup forms the alpha Adam step of update_alpha (cql_impl.py:119-141)
+ * itself -- the same sums in the same order in every workgroup -- and so the
+ * conservative scale ca cw / (C B): the 3NB importance-sampled rows' softmax
+ * weights are multiplied by it, the data rows' alpha-free gradients have it
+ * subtracted (ddpg_impl.py:138-165 with cql_impl.py:110-117).  Workgroup 0
+ * also takes update_temp's step (sac_impl.py:123-146), writes metrics[0:8]
+ * (but 5) and scalars[0:3] as d3a_cql_loss does, and the new scalar optimiser
+ * state to loss.stage (committed by a later launch: every workgroup reads the
+ * old state).  gscale is not read. */
+int d3a_q2_bwd_x6_cql(const d3a_q2_bwd_desc* d, const d3a_cql_loss_desc* loss, void* stream);
 
 /* bf16 throughput instantiation of the critic forward / backward (the
  * `--precision bf16` bench line, never the parity path): the same contracts
@@ -529,6 +542,12 @@ typedef struct d3a_adam_desc {
    * = the segment owning flat block b in the layout above and its first
    * block; segs is then not read */
   const d3a_adam_block* blocks;
+  /* optional, block 0 (n_commit <= 8): *commit_dst[i] = commit_src[i], and
+   * *commit_step[k] += 1 where commit_step[k] != NULL -- a scalar optimiser
+   * state an earlier launch of the update computed but could not write in
+   * place (d3a_cql_loss_desc.stage) */
+  const float* commit_src; float* commit_dst[8]; int32_t n_commit;
+  int64_t* commit_step[2];
 } d3a_adam_desc;
 int d3a_adam_step(const d3a_adam_desc* d, void* stream);
 
@@ -755,6 +774,19 @@ typedef struct d3a_cql_loss_desc {
    * and the loss stage in one launch -- the last workgroup of the first runs
    * the second (same sums, same order) and resets the counter */
   uint32_t* ticket;
+  /* split != 0 (the loss stage inside the critic backward, d3a_q2_bwd_x6_cql;
+   * single device, conservative, no soft target, update_critic): this entry
+   * launches only the logsumexp stage, which also writes every data row's
+   * alpha-free gradient dq[c][6NB + b] = 2 (q - y) / B (the backward
+   * subtracts the conservative term), td2[c][b] = (q - y)^2 and bc[0:4] = 1 -
+   * beta1^t, 1 - beta2^t of the coming temperature step, then of alpha's.
+   * stage [6]: the new log_temp, temp_m, temp_v, log_alpha, alpha_m, alpha_v
+   * the backward computes; the critic Adam's tail commits them
+   * (d3a_adam_desc.commit_*). */
+  int32_t split;
+  float* td2;
+  double* bc;
+  float* stage;
 } d3a_cql_loss_desc;
 int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream);
 

@@ -236,7 +236,7 @@ def test_cql_impl_replays_through_the_update_step_op(monkeypatch):
         torch.manual_seed(0)
         impl = make_impl(D, A, [256, 256], N_)
         if impls:
-            impl.set_state_dict(impls[0].get_state_dict())
+            impl.set_state_dict(impls[0][0].get_state_dict())
         impls.append((impl, via_op))
     for impl, via_op in impls:
         monkeypatch.setattr(dops, "_OP_REPLAY", via_op)
