@@ -58,6 +58,11 @@ _DQ_IN_HEAD_MAX_PAIRS = min(32, int(os.environ.get("D3A_DQ_IN_HEAD_MAX_PAIRS", "
 # full update_step: the soft target updates, counters and metric ring ride in
 # the two Adam launches (d3a_adam_step) instead of a d3a_step_end launch
 _ADAM_TAIL = os.environ.get("D3A_ADAM_TAIL", "1") == "1"
+# the CQL loss stage (temperature / alpha Adam, TD, the conservative scale) in
+# the slice critic backward's prologue instead of its own one-workgroup launch
+# (d3a_q2_bwd_x6_cql; the new scalar state committed by the critic Adam);
+# D3A_LOSS_IN_BWD=0 keeps the d3a_cql_loss launch (A/B)
+_LOSS_IN_BWD = os.environ.get("D3A_LOSS_IN_BWD", "1") == "1"
 
 class CQLImpl(ImplBase):
     # conservative term + alpha (cql_impl.py); SACImpl (algos/sac.py) clears it
@@ -475,6 +480,11 @@ class _Workspace:
                      if mlp.presplit_ok(impl.critic) and not bf16 else None)
         self.dq = z(C, self.R)
         self.lse = z(2, C, B)
+        # (loss stage in the critic backward) squared TD errors, the Adam bias
+        # corrections and the staged scalar optimiser state
+        self.td2 = z(C, B)
+        self.bc = torch.zeros(4, dtype=torch.float64, device=dev)
+        self.stage_s = z(8)
         self.adq = z(C, B)
         self.adx = z(C, B, DA)
         self.dhead = z(B, 2 * A)
@@ -577,6 +587,7 @@ class _Workspace:
         l.grad_scale = 1.0 if impl._dp is None else impl._dp.scale
         l.soft_target, l.conservative = int(self.soft), int(impl._CONSERVATIVE)
         l.logp_targ = self.logp_targ.data_ptr()
+        l.td2, l.bc, l.stage = self.td2.data_ptr(), self.bc.data_ptr(), self.stage_s.data_ptr()
         self.loss_desc = l
 
         h = NAT.SacActorHeadDesc()
@@ -789,6 +800,10 @@ class _Workspace:
                         h_from=3 * NB, aux=targ,
                         wparts=self.wimg.wparts(0, 1) if self.wimg is not None else None)
         dp = impl._dp
+        # the loss stage inside the slice critic backward (d3a_q2_bwd_x6_cql)
+        loss_in_bwd = (_LOSS_IN_BWD and critic and dp is None and impl._CONSERVATIVE
+                       and not self.soft and self.cbwd.slice and not self.loss_desc.ticket)
+        self.loss_desc.split = int(loss_in_bwd)
         if temp or alpha or critic:
             l = self.loss_desc
             l.update_temp, l.update_alpha, l.update_critic = int(temp), int(alpha), int(critic)
@@ -816,10 +831,18 @@ class _Workspace:
             # (alpha-dependent factor from the loss kernel) as it is read
             mlp.backward(self.cbwd, impl.store, self.x_q.data_ptr(), True, DA, self.qacts,
                          self.dq.data_ptr() + 4 * r0, 1, R, r0, self.Rc,
-                         g_scale=self.scalars.data_ptr() + 8, n_scaled=3 * NB)
+                         g_scale=self.scalars.data_ptr() + 8, n_scaled=3 * NB,
+                         cql_loss=self.loss_desc if loss_in_bwd else None)
             tail = None
             if fused_tail:
                 tail = dict(targ=impl.targ, tau=impl._tau, counters=impl.counters, inc_mask=2)
+            if loss_in_bwd:
+                # the backward staged the new temperature / alpha state
+                tail = dict(tail or {}, commit_src=self.stage_s,
+                            commit_dst=(impl.log_temp, impl.temp_m, impl.temp_v, impl.log_alpha,
+                                        impl.alpha_m, impl.alpha_v),
+                            commit_step=(impl.temp_step if temp else None,
+                                         impl.alpha_step if alpha else None))
             self._apply(self.critic_opt, dp, tail)
         if actor:
             if not (temp or alpha or critic):

@@ -81,6 +81,21 @@ __device__ __forceinline__ void block_sum_k(float (&v)[K], float* scratch) {
   }
 }
 
+// Adam on a single scalar parameter (torch single-tensor path) held in
+// registers; returns the new p, updates m / v (the caller stores them).
+// bc = {1 - b1^t, 1 - b2^t} for the step t being taken.
+__device__ __forceinline__ float adam_scalar_r(float p, float& m, float& v, float g, double lr,
+                                               double b1, double b2, double eps, const double* bc) {
+  float mm = fmaf((float)(1.0 - b1), __fsub_rn(g, m), m);
+  float vv = __fmul_rn(v, (float)b2);
+  vv = __fadd_rn(vv, __fmul_rn(__fmul_rn((float)(1.0 - b2), g), g));
+  const float step_size = (float)(lr / bc[0]);
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vv), (float)sqrt(bc[1])), (float)eps);
+  m = mm;
+  v = vv;
+  return __fadd_rn(p, __fmul_rn(-step_size, __fdiv_rn(mm, denom)));
+}
+
 // torch.nn.functional.softplus(x, beta=1, threshold=20)
 __device__ __forceinline__ float softplus_t(float x) {
   return x > 20.f ? x : log1pf(expf(x));

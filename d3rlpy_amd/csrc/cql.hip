@@ -244,21 +244,6 @@ __global__ __launch_bounds__(SMP_T) void cql_sample_kernel(d3a_cql_sample_desc d
     x6::x6_split_piece(d.presplit, p);
 }
 
-// Adam on a single scalar parameter (torch single-tensor path) held in
-// registers; returns the new p, updates m / v (the caller stores them).
-// bc = {1 - b1^t, 1 - b2^t} for the step t being taken.
-__device__ __forceinline__ float adam_scalar_r(float p, float& m, float& v, float g, double lr,
-                                               double b1, double b2, double eps, const double* bc) {
-  float mm = fmaf((float)(1.0 - b1), __fsub_rn(g, m), m);
-  float vv = __fmul_rn(v, (float)b2);
-  vv = __fadd_rn(vv, __fmul_rn(__fmul_rn((float)(1.0 - b2), g), g));
-  const float step_size = (float)(lr / bc[0]);
-  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vv), (float)sqrt(bc[1])), (float)eps);
-  m = mm;
-  v = vv;
-  return __fadd_rn(p, __fmul_rn(-step_size, __fdiv_rn(mm, denom)));
-}
-
 // logsumexp over the 3N importance-sampled values of (c, b) in set s.
 __device__ __forceinline__ float is_value(const d3a_cql_loss_desc& d, int64_t c, int64_t s,
                                           int64_t b, int64_t j, float rand_logp) {
@@ -279,6 +264,28 @@ __device__ __forceinline__ void cql_lse_wave(const d3a_cql_loss_desc& d, int64_t
   const int64_t B = d.B, C = d.C, N = d.N, NB = N * B, M = 3 * N;
   if (p >= 2 * C * B) return;
   const int64_t s = p / (C * B), c = (p / B) % C, b = p % B;
+  if (d.split && p == 0 && lane < 4) {
+    // (split: the loss stage runs in the critic backward) the bias
+    // corrections 1 - beta^t of the coming temperature / alpha Adam steps,
+    // fp64 pow as cql_loss_stage computes them
+    const bool on = lane < 2 ? d.update_temp != 0 : d.update_alpha != 0;
+    if (on) {
+      const int64_t t = (lane < 2 ? *d.temp_step : *d.alpha_step) + 1;
+      d.bc[lane] = 1.0 - pow((lane & 1) ? d.beta2 : d.beta1, (double)t);
+    }
+  }
+  if (d.split && s == 1 && lane == 0) {
+    // the data row's gradient without the conservative term (subtracted by
+    // the backward, which knows the new alpha) and its squared TD error --
+    // cql_loss_stage's arithmetic for row 6NB + b
+    float tq = d.q_targ[b];
+    for (int64_t k = 1; k < C; ++k) tq = fminf(tq, d.q_targ[k * B + b]);
+    const float gam = powf(d.gamma, d.n_steps[b]);
+    const float y = d.rew[b] + gam * tq * (1.f - d.term[b]);
+    const float diff = d.q[c * d.R + 6 * NB + b] - y;
+    d.dq[c * d.R + 6 * NB + b] = 2.f * diff / (float)B;
+    d.td2[c * B + b] = diff * diff;
+  }
   if ((s == 0 && !d.update_alpha) || (s == 1 && !d.update_critic)) return;
   const float rand_logp = (float)log(pow(0.5, (double)d.A));
   float mx = -INFINITY;
@@ -763,6 +770,19 @@ extern "C" int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream) {
   D3A_CHECK_ARG(d->conservative || !d->update_alpha,
                 "d3a_cql_loss: update_alpha needs the conservative term");
   D3A_CHECK_ARG(!d->conservative || d->N >= 1, "d3a_cql_loss: the conservative term needs N >= 1");
+  D3A_CHECK_ARG(!d->split || (d->conservative && d->update_critic && !d->soft_target &&
+                               d->dp_phase == 0 && d->td2 && d->bc && d->stage && !d->ticket),
+                "d3a_cql_loss: split needs the conservative critic update on one device, no soft "
+                "target, td2, bc and stage");
+  if (d->split) {
+    // the logsumexp stage only (with the data rows' gradients, td2, bc); the
+    // loss stage runs in d3a_q2_bwd_x6_cql
+    const int64_t waves = 2LL * d->C * d->B;
+    hipLaunchKernelGGL(cql_lse_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, *d);
+    D3A_LAUNCH_CHECK("d3a_cql_loss");
+    return 0;
+  }
   // phase 2 reuses the logsumexp / softmax weights phase 1 wrote
   const bool stage_a = d->conservative && (d->update_alpha || d->update_critic) && d->dp_phase != 2;
   if (stage_a && d->ticket) {

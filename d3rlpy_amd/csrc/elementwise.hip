@@ -276,6 +276,10 @@ __global__ __launch_bounds__(256) void adam_kernel(d3a_adam_desc a) {
   if (tail) {
     if (a.ring && threadIdx.x == 0) *a.ring_ctr = rc0 + 1;
     if (threadIdx.x < 32 && (a.inc_mask >> threadIdx.x & 1u)) a.counters[threadIdx.x] += 1;
+    // the scalar state an earlier launch staged (d3a_cql_loss_desc.stage)
+    if ((int)threadIdx.x < a.n_commit) *a.commit_dst[threadIdx.x] = a.commit_src[threadIdx.x];
+    if (threadIdx.x >= 64 && threadIdx.x < 66 && a.commit_step[threadIdx.x - 64])
+      *a.commit_step[threadIdx.x - 64] += 1;
   }
   if (act) {  // uniform over each lane group
     if (!lead) return;
@@ -488,6 +492,8 @@ extern "C" int d3a_adam_step(const d3a_adam_desc* a, void* stream) {
                 "d3a_adam_step: bad n_blocks");
   D3A_CHECK_ARG(a->step_add == 0 || a->step_add == 1, "d3a_adam_step: step_add must be 0 or 1");
   D3A_CHECK_ARG(!a->inc_mask || a->counters, "d3a_adam_step: counters required");
+  D3A_CHECK_ARG(a->n_commit >= 0 && a->n_commit <= 8 && (a->n_commit == 0 || a->commit_src),
+                "d3a_adam_step: n_commit in [0, 8] with commit_src");
   D3A_CHECK_ARG(!a->ring || (a->metrics && a->ring_ctr && a->n_metrics >= 1 &&
                              a->n_metrics <= 256 && a->ring_cap > 0),
                 "d3a_adam_step: bad metric ring");

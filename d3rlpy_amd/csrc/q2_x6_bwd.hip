@@ -559,7 +559,8 @@ __global__ __launch_bounds__(B6_NT) void q2x6_bwd_kernel(d3a_q2_bwd_desc d) {
 using namespace d3a;
 
 namespace d3a {
-int launch_q2x6t_bwd(const d3a_q2_bwd_desc& d, hipStream_t st);  // q2_x6_bwd2.hip
+int launch_q2x6t_bwd(const d3a_q2_bwd_desc& d, hipStream_t st,
+                     const d3a_cql_loss_desc* lc = nullptr);  // q2_x6_bwd2.hip
 }
 
 extern "C" int d3a_q2_bwd_x6(const d3a_q2_bwd_desc* dp, void* stream) {

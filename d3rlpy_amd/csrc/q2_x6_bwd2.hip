@@ -67,6 +67,7 @@ struct TLds {
   double g3[4];                     // col waves' sum g' (slice 0)
   f32x4 w1[4][T_NDBMAX][64];        // row waves' dW1 [wave][x block][lane]
   double b1[4][64];                 // row waves' db1 [wave][lane]
+  float cs[5][8];                   // (CQL) the loss stage's wave sums [sum][wave]
 };
 
 __device__ __forceinline__ f32x4 m16(bf16x8 a, bf16x8 b, f32x4 c) {
@@ -122,9 +123,15 @@ struct RowOps {
 };
 
 // NDB: 16-wide blocks of x (n_in <= 16 NDB); nkw: sub-blocks per wave, a
-// multiple of 4 >= ceil(sub-blocks per row block / 4)
-template <int NDB>
-__global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int P, int rbp, int nkw) {
+// multiple of 4 >= ceil(sub-blocks per row block / 4).
+// CQL (d3a_q2_bwd_x6_cql): the CQL loss stage (cql.hip cql_loss_stage's
+// arithmetic, after the logsumexp stage of a split d3a_cql_loss) in the
+// prologue of every workgroup -- the conservative scale of the rows' gradients
+// from the alpha step each workgroup takes itself; workgroup 0 writes the
+// metrics, scalars and the new scalar optimiser state (lc.stage)
+template <int NDB, bool CQL = false>
+__global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int P, int rbp, int nkw,
+                                                         d3a_cql_loss_desc lc) {
   __shared__ __attribute__((aligned(16))) TLds L;
   static_assert(sizeof(TLds) <= 163840, "LDS");
   const int t = threadIdx.x, lane = t & 63;
@@ -154,11 +161,51 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
   const float* w3g = d.w3 + c * d.sw3;
   const uint32_t* m2g = reinterpret_cast<const uint32_t*>(d.m2) + c * d.sm2;
   const uint32_t* mtg = reinterpret_cast<const uint32_t*>(d.m2t) + c * d.sm2t;
-  const float gs = d.gscale ? *d.gscale : 1.f;
+  // g' scale of the first n_scaled rows; (CQL) and the term subtracted from
+  // the rest, both formed after the prologue's barrier
+  float gs = CQL ? 0.f : (d.gscale ? *d.gscale : 1.f);
+  float gsub = 0.f;
   const int64_t pc = (int64_t)p * d.C + c;
   const bool col = w >= 4;
   const int rw = w & 3;  // wave within its role: sub-blocks rw, rw + 4, ...
 
+  // (CQL) this thread's share of the loss stage's sums, loaded up front (slot
+  // p = t; clamped and masked, so no load waits behind a branch): alpha's
+  // sum of lse and data Q; workgroup 0 also the critic set's lse, the squared
+  // TD errors and the temperature's log-probs
+  const bool wg0 = blockIdx.x == 0;
+  float cv[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  [[maybe_unused]] float st_lt = 0.f, st_tm = 0.f, st_tv = 0.f, st_la = 0.f, st_am = 0.f, st_av = 0.f;
+  if constexpr (CQL) {
+    const int64_t B = lc.B, CB = (int64_t)lc.C * lc.B, NB = (int64_t)lc.N * lc.B;
+    // (every state value, updated or not: the stage carries all six)
+    st_lt = *lc.log_temp;
+    st_la = *lc.log_alpha;
+    st_tm = *lc.temp_m;
+    st_tv = *lc.temp_v;
+    st_am = *lc.alpha_m;
+    st_av = *lc.alpha_v;
+    auto add = [&](int64_t pp, bool first) {
+      const int64_t p2 = pp < CB ? pp : CB - 1;
+      const bool ok = pp < CB;
+      const int64_t cc = p2 / B, bb = p2 - cc * B;
+      const float qd = lc.q[cc * lc.R + 6 * NB + bb];
+      const float la = lc.update_alpha ? lc.lse[p2] : 0.f;
+      float lcv = 0.f, t2 = 0.f;
+      if (wg0) {
+        lcv = lc.lse[CB + p2];
+        t2 = lc.td2[p2];
+      }
+      cv[0] = first ? keep_if(ok, la) : cv[0] + keep_if(ok, la);
+      cv[1] = first ? keep_if(ok, qd) : cv[1] + keep_if(ok, qd);
+      cv[2] = first ? keep_if(ok, lcv) : cv[2] + keep_if(ok, lcv);
+      cv[3] = first ? keep_if(ok, t2) : cv[3] + keep_if(ok, t2);
+    };
+    add(t, true);
+    for (int64_t pp = t + T_NT; pp < CB; pp += T_NT) add(pp, false);
+    if (wg0 && lc.update_temp)
+      for (int64_t bb = t; bb < B; bb += T_NT) cv[4] += lc.logp_temp[bb] - (float)lc.A;
+  }
   // ---- prologue: the byte table and the slice's (w3 W2) parts
   if (t < 256) {
     uint4 v;
@@ -188,6 +235,77 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
       L.bw[2][(t & 15) * T_BLD + o] = e;
     }
   }
+  if constexpr (CQL) {
+    // the wave's sums (cql_loss_stage's block_sum order: wave sums, then the
+    // waves in order after the barrier)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) cv[k] = wave_sum(cv[k]);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) L.cs[k][w] = cv[k];
+    }
+  }
+  // (CQL) after the prologue's barrier: the sums, alpha's Adam step and the
+  // conservative scale, formed by every thread (workgroup 0's thread 0 also
+  // the temperature's step and the stage's outputs)
+  auto cql_scalars = [&]() {
+    if constexpr (CQL) {
+      float sum[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        float s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s2 += L.cs[k][i];
+        sum[k] = s2;
+      }
+      const float B = (float)lc.B, CB = (float)((int64_t)lc.C * lc.B);
+      float lalpha = st_la, am = st_am, av = st_av;
+      float alpha_loss = 0.f;
+      if (lc.update_alpha) {
+        const float loss = sum[0] / CB - sum[1] / CB;
+        const float scaled = lc.conservative_weight * loss;
+        const float e = expf(lalpha);
+        const float ca0 = fminf(fmaxf(e, 0.f), 1e6f);
+        alpha_loss = -(ca0 * (scaled - lc.alpha_threshold));
+        const bool pass = (e >= 0.f) && (e <= 1e6f);
+        const float g = pass ? -(scaled - lc.alpha_threshold) * e : 0.f;
+        const double bcl[2] = {lc.bc[2], lc.bc[3]};
+        lalpha = adam_scalar_r(lalpha, am, av, g, lc.alpha_lr, lc.beta1, lc.beta2, lc.adam_eps, bcl);
+      }
+      const float ca = fminf(fmaxf(expf(lalpha), 0.f), 1e6f);
+      const float gcons = ca * lc.conservative_weight / CB;
+      // (every lane holds the same value: a scalar register through the loop)
+      gs = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, gcons)));
+      gsub = gs;
+      if (wg0 && t == 0) {
+        float ltemp = st_lt, tm = st_tm, tv = st_tv;
+        if (lc.update_temp) {
+          const float e = expf(ltemp);
+          lc.metrics[0] = -(e * sum[4]) / B;
+          const float g = (-1.f / B) * sum[4] * e;
+          const double bct[2] = {lc.bc[0], lc.bc[1]};
+          ltemp = adam_scalar_r(ltemp, tm, tv, g, lc.temp_lr, lc.beta1, lc.beta2, lc.adam_eps, bct);
+          lc.metrics[1] = expf(ltemp);
+        }
+        if (lc.update_alpha) {
+          lc.metrics[2] = alpha_loss;
+          lc.metrics[3] = expf(lalpha);
+        }
+        lc.stage[0] = ltemp; lc.stage[1] = tm; lc.stage[2] = tv;
+        lc.stage[3] = lalpha; lc.stage[4] = am; lc.stage[5] = av;
+        const float temp = expf(ltemp);
+        lc.scalars[0] = temp;
+        lc.scalars[1] = ca;
+        lc.scalars[2] = gcons;
+        const float td = sum[3] / B;
+        const float loss = sum[2] / CB - sum[1] / CB;
+        const float cons = ca * (lc.conservative_weight * loss - lc.alpha_threshold);
+        lc.metrics[4] = td + cons;
+        lc.metrics[6] = td;
+        lc.metrics[7] = cons;
+      }
+    }
+  };
   // first row the operands of the wave's k-th sub-block are loaded from: the
   // sub-block's own (rows % 32 == 0), or the last sub-block of the rows for a
   // sub-block past the end (its rows are all invalid: g' = 0); wave-uniform,
@@ -197,13 +315,19 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
   auto sb_row = [&](int k) { return min(rb0 + T_SB * (rw + 4 * k), rows - T_SB); };
   const int nsc = (int)min(d.n_scaled, d.rows);
   auto gprime = [&](float graw, int r) {  // g' of row r from its raw load, 0 past the block
-    const float v = r < nsc ? graw * gs : graw;
+    const float v = r < nsc ? graw * gs : (CQL ? graw - gsub : graw);
     return r < rb1 ? v : 0.f;
   };
   auto lut8 = [&](uint32_t byte) {
     return *reinterpret_cast<const bf16x8*>(&L.lut[byte]);
   };
 
+  if constexpr (CQL) {
+    // the wave sums published, then every thread forms the scalars (one
+    // barrier more than the plain kernel, ahead of the sub-block loads)
+    __syncthreads();
+    cql_scalars();
+  }
   if (col) {
     // ================= col waves: R[o][i] += m^T (g' h1), S, sum g'
     f32x4 R[T_NQ];
@@ -481,7 +605,7 @@ extern "C" int32_t d3a_q2_bwd_x6t_splits(int64_t rows, int32_t C) {
 }
 
 namespace d3a {
-int launch_q2x6t_bwd(const d3a_q2_bwd_desc& d, hipStream_t st) {
+int launch_q2x6t_bwd(const d3a_q2_bwd_desc& d, hipStream_t st, const d3a_cql_loss_desc* lc) {
   D3A_CHECK_ARG(d.m2 && d.m2t && d.b2, "d3a_q2_bwd_x6 (transposed mask): m2, m2t and b2 are required");
   D3A_CHECK_ARG((reinterpret_cast<uintptr_t>(d.m2) & 15) == 0 && d.sm2 % 4 == 0 &&
                     (reinterpret_cast<uintptr_t>(d.m2t) & 3) == 0,
@@ -501,13 +625,40 @@ int launch_q2x6t_bwd(const d3a_q2_bwd_desc& d, hipStream_t st) {
   const int64_t nkw = ((rbp / T_SB + 3) / 4 + 3) / 4 * 4;
   const dim3 grid((unsigned)blocks), block(T_NT);
   const int ndb = (d.n_in + 15) / 16;
-  if (ndb <= 1)
-    hipLaunchKernelGGL(q2x6t_bwd_kernel<1>, grid, block, 0, st, d, (int)P, (int)rbp, (int)nkw);
-  else if (ndb == 2)
-    hipLaunchKernelGGL(q2x6t_bwd_kernel<2>, grid, block, 0, st, d, (int)P, (int)rbp, (int)nkw);
-  else
-    hipLaunchKernelGGL(q2x6t_bwd_kernel<3>, grid, block, 0, st, d, (int)P, (int)rbp, (int)nkw);
+  const d3a_cql_loss_desc l = lc ? *lc : d3a_cql_loss_desc{};
+  const int Pi = (int)P, rbpi = (int)rbp, nkwi = (int)nkw;
+  if (lc) {
+    if (ndb <= 1)
+      hipLaunchKernelGGL((q2x6t_bwd_kernel<1, true>), grid, block, 0, st, d, Pi, rbpi, nkwi, l);
+    else if (ndb == 2)
+      hipLaunchKernelGGL((q2x6t_bwd_kernel<2, true>), grid, block, 0, st, d, Pi, rbpi, nkwi, l);
+    else
+      hipLaunchKernelGGL((q2x6t_bwd_kernel<3, true>), grid, block, 0, st, d, Pi, rbpi, nkwi, l);
+  } else if (ndb <= 1) {
+    hipLaunchKernelGGL(q2x6t_bwd_kernel<1>, grid, block, 0, st, d, Pi, rbpi, nkwi, l);
+  } else if (ndb == 2) {
+    hipLaunchKernelGGL(q2x6t_bwd_kernel<2>, grid, block, 0, st, d, Pi, rbpi, nkwi, l);
+  } else {
+    hipLaunchKernelGGL(q2x6t_bwd_kernel<3>, grid, block, 0, st, d, Pi, rbpi, nkwi, l);
+  }
   D3A_LAUNCH_CHECK("d3a_q2_bwd_x6");
   return 0;
 }
 }  // namespace d3a
+
+extern "C" int d3a_q2_bwd_x6_cql(const d3a_q2_bwd_desc* dp, const d3a_cql_loss_desc* lc, void* stream) {
+  D3A_CHECK_ARG(dp && lc, "d3a_q2_bwd_x6_cql: null desc");
+  const d3a_q2_bwd_desc& d = *dp;
+  D3A_CHECK_ARG(lc->split && lc->update_critic && lc->conservative && !lc->soft_target &&
+                    lc->dp_phase == 0 && lc->td2 && lc->bc && lc->stage && lc->lse && lc->metrics &&
+                    lc->scalars,
+                "d3a_q2_bwd_x6_cql: needs a split CQL loss desc (conservative critic update, one "
+                "device, no soft target) with td2, bc, stage, lse, metrics and scalars");
+  D3A_CHECK_ARG(d.g == lc->dq + 3LL * lc->N * lc->B && d.n_scaled == 3LL * lc->N * lc->B &&
+                    d.C == lc->C && d.rows == 3LL * lc->N * lc->B + lc->B && d.sgb == lc->R,
+                "d3a_q2_bwd_x6_cql: the backward's rows must be the loss's critic set (g = dq + 3NB, "
+                "n_scaled 3NB, rows 3NB + B)");
+  D3A_CHECK_ARG(d.dz2 == nullptr && d.m2t != nullptr,
+                "d3a_q2_bwd_x6_cql: the slice kernel (m2t set, no dz2)");
+  return launch_q2x6t_bwd(d, (hipStream_t)stream, lc);
+}

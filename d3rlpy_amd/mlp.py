@@ -595,10 +595,13 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
              q_scale: float = 0.0, g_out: Optional[int] = None,
              g_scale: Optional[int] = None, n_scaled: int = 0,
              members: Optional[int] = None, head_ready: bool = False,
-             head_desc=None) -> Optional[torch.Tensor]:
+             head_desc=None, cql_loss=None) -> Optional[torch.Tensor]:
     """Backward of rows [r0, r0+n) given dL/d(output) (``dout`` points at row r0).
     Returns (per-layer path) the dz buffer holding the first layer's
     pre-activation gradient [C][rows][ld] once the trunk has run.
+
+    ``cql_loss`` (a split d3a_cql_loss_desc): the slice kernel with the CQL
+    loss stage in its prologue (d3a_q2_bwd_x6_cql; g_scale is then not read).
 
     dout layout: [C] x rows, member stride sdout_b, row stride ld_dout (1 for a
     single-output head).  ``dx`` (if given) receives dL/dx as [C][n][in].
@@ -666,6 +669,10 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
                     and acts.hmask_from <= r0 and r0 + n <= acts.hmask_to and _MASK_IMAGE):
                 # the forward's mask image of h2 (same rows as h1 / h2)
                 d.m2, d.sm2 = acts.hmask.data_ptr() + 4 * r0 * (H // 32), R * (H // 32)
+        if cql_loss is not None:
+            assert entry == "d3a_q2_bwd_x6" and bs.slice
+            ops.call_desc("d3a_q2_bwd_x6_cql", d, cql_loss)
+            return None
         ops.call_desc(entry, d)
         return None
 

@@ -149,7 +149,9 @@ def adam_step(segs: torch.Tensor, n_seg: int, n_blocks: int, step: torch.Tensor,
               counters: Optional[torch.Tensor] = None, inc_mask: int = 0,
               metrics: Optional[torch.Tensor] = None, ring: Optional[torch.Tensor] = None,
               ring_ctr: Optional[torch.Tensor] = None, metric_scale: float = 1.0,
-              blocks: Optional[torch.Tensor] = None) -> None:
+              blocks: Optional[torch.Tensor] = None, commit_src: Optional[torch.Tensor] = None,
+              commit_dst: Sequence[torch.Tensor] = (),
+              commit_step: Sequence[Optional[torch.Tensor]] = ()) -> None:
     """d3a_adam_step: Adam with the soft target update (``targ_delta`` != 0:
     the target copy ``targ_delta`` elements from each parameter) and the
     step's counter / metric-ring bookkeeping in one launch."""
@@ -164,6 +166,14 @@ def adam_step(segs: torch.Tensor, n_seg: int, n_blocks: int, step: torch.Tensor,
         d.ring, d.ring_cap, d.ring_ctr = ptr(ring), ring.shape[0], ptr(ring_ctr)
     d.metric_scale = metric_scale
     d.blocks = ptr(blocks)  # per-block segment table (AdamGroup), or None
+    if commit_src is not None:
+        # a scalar optimiser state staged by an earlier launch of the update
+        assert len(commit_dst) <= 8 and commit_src.numel() >= len(commit_dst)
+        d.commit_src, d.n_commit = ptr(commit_src), len(commit_dst)
+        for i, t in enumerate(commit_dst):
+            d.commit_dst[i] = ptr(t)
+        for i, t in enumerate(commit_step):
+            d.commit_step[i] = ptr(t)
     N.check(N.lib().d3a_adam_step(C.byref(d), _stream()), "d3a_adam_step")
 
 

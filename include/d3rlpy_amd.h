@@ -424,19 +424,7 @@ typedef struct d3a_q2_bwd_desc {
  * (about 256 workgroups of C * P * 16; the caller sizes the partials with it). */
 int32_t d3a_q2_bwd_x6t_splits(int64_t rows, int32_t C);
 int d3a_q2_bwd(const d3a_q2_bwd_desc* d, void* stream);
-/* d3a_q2_bwd_x6's slice kernel with the CQL loss stage in every workgroup's
- * prologue (no launch of its own): from the logsumexp stage's outputs (loss
- * with split set; d.g = dq at the critic set's first row, n_scaled = 3NB) each
- * workgroup forms the alpha Adam step of update_alpha (cql_impl.py:119-141)
- * itself -- the same sums in the same order in every workgroup -- and so the
- * conservative scale ca cw / (C B): the 3NB importance-sampled rows' softmax
- * weights are multiplied by it, the data rows' alpha-free gradients have it
- * subtracted (ddpg_impl.py:138-165 with cql_impl.py:110-117).  Workgroup 0
- * also takes update_temp's step (sac_impl.py:123-146), writes metrics[0:8]
- * (but 5) and scalars[0:3] as d3a_cql_loss does, and the new scalar optimiser
- * state to loss.stage (committed by a later launch: every workgroup reads the
- * old state).  gscale is not read. */
-int d3a_q2_bwd_x6_cql(const d3a_q2_bwd_desc* d, const d3a_cql_loss_desc* loss, void* stream);
+
 
 /* bf16 throughput instantiation of the critic forward / backward (the
  * `--precision bf16` bench line, never the parity path): the same contracts
@@ -789,6 +777,19 @@ typedef struct d3a_cql_loss_desc {
   float* stage;
 } d3a_cql_loss_desc;
 int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream);
+/* d3a_q2_bwd_x6's slice kernel with the CQL loss stage in every workgroup's
+ * prologue (no launch of its own): from the logsumexp stage's outputs (loss
+ * with split set; d.g = dq at the critic set's first row, n_scaled = 3NB) each
+ * workgroup forms the alpha Adam step of update_alpha (cql_impl.py:119-141)
+ * itself -- the same sums in the same order in every workgroup -- and so the
+ * conservative scale ca cw / (C B): the 3NB importance-sampled rows' softmax
+ * weights are multiplied by it, the data rows' alpha-free gradients have it
+ * subtracted (ddpg_impl.py:138-165 with cql_impl.py:110-117).  Workgroup 0
+ * also takes update_temp's step (sac_impl.py:123-146), writes metrics[0:8]
+ * (but 5) and scalars[0:3] as d3a_cql_loss does, and the new scalar optimiser
+ * state to loss.stage (committed by a later launch: every workgroup reads the
+ * old state).  gscale is not read. */
+int d3a_q2_bwd_x6_cql(const d3a_q2_bwd_desc* d, const d3a_cql_loss_desc* loss, void* stream);
 
 /* Actor stage helpers (SACImpl.compute_actor_loss, sac_impl.py:114-121):
  * from the critics' Q at (s, tanh u) and the policy head, the per-row
