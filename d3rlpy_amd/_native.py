@@ -295,6 +295,7 @@ class MlpFwdDesc(C.Structure):
         ("xg_a_parts", C.c_int32), ("xg_s_apart", C.c_int64),
         ("xg_xout", vp), ("xg_ldxo", C.c_int64), ("xg_eout", vp),
         ("wp", vp * 2), ("aux_wp", vp * 2),
+        ("presplit", X6SplitDesc),
     ]
 
 
@@ -592,6 +593,7 @@ _SIGNATURES = {
     "d3a_iqn_head_bwd_fused": (C.c_int, [C.POINTER(IqnHeadBwdFusedDesc), vp]),
     "d3a_mlp_fwd_x6": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
     "d3a_x6_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
+    "d3a_bwd_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_wide_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_small_bwd_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_td3_prep": (C.c_int, [C.POINTER(Td3PrepDesc), vp]),

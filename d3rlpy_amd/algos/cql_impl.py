@@ -517,6 +517,7 @@ class _Workspace:
             raise NotImplementedError("one batch size per CQLImpl is supported")
         self._graphs: Dict[Tuple, torch.cuda.CUDAGraph] = {}
         self._op_state = None  # tensors the update-step op declares mutated
+        self._loss_in_bwd = False  # the last enqueue ran the loss stage in the backward
         self._ran_eager = set()
         self._build_descs()
 
@@ -546,8 +547,15 @@ class _Workspace:
         s.eps_actor_out, s.seed, s.n_normal = self.eps_actor.data_ptr(), self.seed, self.n_normal
         if self.soft:
             s.eps_targ, s.logp_targ = self.eps_targ.data_ptr(), self.logp_targ.data_ptr()
+        # the weight images' split jobs ride in the policy forward's launch
+        # (extra workgroups on the CUs its few hundred rows leave idle) where
+        # it is the parts path, else in the sampler's
+        self.presplit_jobs = None
         if self.wimg is not None:
-            s.presplit = self.wimg.jobs()
+            if self.phead is not None:
+                self.presplit_jobs = self.wimg.jobs()
+            else:
+                s.presplit = self.wimg.jobs()
         self.sample_desc = s
 
         l = NAT.CqlLossDesc()
@@ -738,13 +746,20 @@ class _Workspace:
         NB, R, C, DA = self.NB, self.R, self.C, self.LDX
         r0 = 3 * NB
 
+        # (the pipeline's launch: with the loss stage in its prologue when the
+        # last update ran it there -- recomputing that step's scalars from the
+        # same inputs and the same uncommitted state, so repeated launches
+        # write the same values)
+        lib = self.loss_desc if self._loss_in_bwd else None
+
         def launch():
             mlp.backward(self.cbwd, st, self.x_q.data_ptr(), True, DA, self.qacts,
                          self.dq.data_ptr() + 4 * r0, 1, R, r0, self.Rc,
-                         g_scale=self.scalars.data_ptr() + 8, n_scaled=3 * NB)
+                         g_scale=self.scalars.data_ptr() + 8, n_scaled=3 * NB, cql_loss=lib)
         s = net.sizes
         flops = 2 * C * self.Rc * (2 * s[1] * s[2] + s[0] * s[1])
-        kind = ("slice, split-bf16 x3 mask-factored" if self.cbwd.slice else
+        kind = ("slice, split-bf16 x3 mask-factored" + (", CQL loss stage in the prologue" if lib
+                                                         else "") if self.cbwd.slice else
                 "256-row blocks, split-bf16 x3 mask-factored" if ops.CRITIC_GEMM == "x6"
                 else "fp32 MFMA")
         return launch, flops, (f"d3a_q2_bwd critic weight gradients ({kind}): C={C} x "
@@ -786,7 +801,7 @@ class _Workspace:
         if sampled:
             # 1. policy on [obs; next_obs]
             mlp.forward(impl.policy, impl.store, self.xobs2.data_ptr(), True, D, self.pacts,
-                        out_parts=self.phead)
+                        out_parts=self.phead, presplit=self.presplit_jobs)
             # 2. samples and Q inputs
             ops.call_desc("d3a_cql_sample", self.sample_desc)
         if alpha or critic:
@@ -804,6 +819,7 @@ class _Workspace:
         loss_in_bwd = (_LOSS_IN_BWD and critic and dp is None and impl._CONSERVATIVE
                        and not self.soft and self.cbwd.slice and not self.loss_desc.ticket)
         self.loss_desc.split = int(loss_in_bwd)
+        self._loss_in_bwd = loss_in_bwd
         if temp or alpha or critic:
             l = self.loss_desc
             l.update_temp, l.update_alpha, l.update_critic = int(temp), int(alpha), int(critic)

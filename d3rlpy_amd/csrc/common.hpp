@@ -96,6 +96,20 @@ __device__ __forceinline__ float adam_scalar_r(float p, float& m, float& v, floa
   return __fadd_rn(p, __fmul_rn(-step_size, __fdiv_rn(mm, denom)));
 }
 
+// adam_scalar_r with the step's two float constants given: step_size =
+// (float)(lr / bc1) and bc2_sqrt = (float)sqrt(bc2) (bitwise the same step)
+__device__ __forceinline__ float adam_scalar_f(float p, float& m, float& v, float g, double b1,
+                                               double b2, double eps, float step_size,
+                                               float bc2_sqrt) {
+  float mm = fmaf((float)(1.0 - b1), __fsub_rn(g, m), m);
+  float vv = __fmul_rn(v, (float)b2);
+  vv = __fadd_rn(vv, __fmul_rn(__fmul_rn((float)(1.0 - b2), g), g));
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vv), bc2_sqrt), (float)eps);
+  m = mm;
+  v = vv;
+  return __fadd_rn(p, __fmul_rn(-step_size, __fdiv_rn(mm, denom)));
+}
+
 // torch.nn.functional.softplus(x, beta=1, threshold=20)
 __device__ __forceinline__ float softplus_t(float x) {
   return x > 20.f ? x : log1pf(expf(x));

@@ -268,23 +268,26 @@ __device__ __forceinline__ void cql_lse_wave(const d3a_cql_loss_desc& d, int64_t
     // (split: the loss stage runs in the critic backward) the bias
     // corrections 1 - beta^t of the coming temperature / alpha Adam steps,
     // fp64 pow as cql_loss_stage computes them
+    // (as the floats adam_scalar_r forms from them: lr / bc1, sqrt(bc2))
     const bool on = lane < 2 ? d.update_temp != 0 : d.update_alpha != 0;
     if (on) {
       const int64_t t = (lane < 2 ? *d.temp_step : *d.alpha_step) + 1;
-      d.bc[lane] = 1.0 - pow((lane & 1) ? d.beta2 : d.beta1, (double)t);
+      const double bc = 1.0 - pow((lane & 1) ? d.beta2 : d.beta1, (double)t);
+      const double lr = lane < 2 ? d.temp_lr : d.alpha_lr;
+      d.bc[lane] = (lane & 1) ? (double)(float)sqrt(bc) : (double)(float)(lr / bc);
     }
   }
-  if (d.split && s == 1 && lane == 0) {
-    // the data row's gradient without the conservative term (subtracted by
-    // the backward, which knows the new alpha) and its squared TD error --
-    // cql_loss_stage's arithmetic for row 6NB + b
-    float tq = d.q_targ[b];
-    for (int64_t k = 1; k < C; ++k) tq = fminf(tq, d.q_targ[k * B + b]);
-    const float gam = powf(d.gamma, d.n_steps[b]);
-    const float y = d.rew[b] + gam * tq * (1.f - d.term[b]);
-    const float diff = d.q[c * d.R + 6 * NB + b] - y;
-    d.dq[c * d.R + 6 * NB + b] = 2.f * diff / (float)B;
-    d.td2[c * B + b] = diff * diff;
+  // (split, critic set) the data row's inputs, loaded with the logsumexp's
+  // own loads and used after them (one memory round trip for both): lane k <
+  // C the target Q of critic k, every lane the row's reward, terminal, n and Q
+  const bool drow = d.split && s == 1;
+  float dr_tq = 0.f, dr_rw = 0.f, dr_tm = 0.f, dr_ns = 0.f, dr_q = 0.f;
+  if (drow) {
+    dr_tq = d.q_targ[(lane < C ? lane : 0) * B + b];
+    dr_rw = d.rew[b];
+    dr_tm = d.term[b];
+    dr_ns = d.n_steps[b];
+    dr_q = d.q[c * d.R + 6 * NB + b];
   }
   if ((s == 0 && !d.update_alpha) || (s == 1 && !d.update_critic)) return;
   const float rand_logp = (float)log(pow(0.5, (double)d.A));
@@ -306,6 +309,24 @@ __device__ __forceinline__ void cql_lse_wave(const d3a_cql_loss_desc& d, int64_t
       const int64_t blk = j / N, n = j % N;
       d.dq[c * d.R + 3 * NB + blk * NB + b * N + n] =
           __fdiv_rn(expf(is_value(d, c, 1, b, j, rand_logp) - mx), se);
+    }
+  }
+  if (drow) {
+    // the data row's gradient without the conservative term (subtracted by
+    // the backward, which knows the new alpha) and its squared TD error --
+    // cql_loss_stage's arithmetic for row 6NB + b (the min over the critics
+    // in k order)
+    float tq = __shfl(dr_tq, 0, 64);
+    for (int64_t k = 1; k < C; ++k) {
+      const float v = k < 64 ? __shfl(dr_tq, (int)k, 64) : d.q_targ[k * B + b];
+      tq = fminf(tq, v);
+    }
+    if (lane == 0) {
+      const float gam = powf(d.gamma, dr_ns);
+      const float y = dr_rw + gam * tq * (1.f - dr_tm);
+      const float diff = dr_q - y;
+      d.dq[c * d.R + 6 * NB + b] = 2.f * diff / (float)B;
+      d.td2[c * B + b] = diff * diff;
     }
   }
 }

@@ -354,6 +354,9 @@ extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
     D3A_LAUNCH_CHECK("d3a_mlp_fwd");
     return 0;
   }
+  D3A_CHECK_ARG(d.presplit.n_jobs == 0 || (d.parts > 1 && x6::x6_split_ok(d.presplit)),
+                "d3a_mlp_fwd: presplit jobs only on the parts path, each with src, 16-byte aligned "
+                "dst, 1 <= k <= kpad and kpad % 16 == 0");
   if (d.parts > 1) {
     D3A_CHECK_ARG(d.parts == D3A_MLP_PARTS && d.block_rows == 16 && d.n_hidden == 2 &&
                       d.H == 256 && d.n_in <= 64 && d.n_out <= 32 && d.aux_rows == 0 &&

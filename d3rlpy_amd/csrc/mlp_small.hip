@@ -298,6 +298,18 @@ struct PartsLds {
 template <int JM>
 __global__ __launch_bounds__(256) void mlp_parts_kernel(d3a_mlp_fwd_desc d) {
   __shared__ __attribute__((aligned(16))) PartsLds<JM> S;
+  {
+    // workgroups past the pass's (d.presplit jobs): d3a_x6_split pieces on
+    // the CUs the pass leaves idle, one piece a thread
+    const int nbx = (int)((d.rows + S_RB - 1) / S_RB);
+    if ((int)blockIdx.x >= nbx) {
+      const int64_t tot = x6::x6_split_total(d.presplit);
+      const int64_t nwg = (int64_t)(gridDim.x - nbx) * gridDim.y * gridDim.z;
+      const int64_t wgi = ((int64_t)(blockIdx.x - nbx) * gridDim.y + blockIdx.y) * gridDim.z + blockIdx.z;
+      for (int64_t pp = wgi * 256 + threadIdx.x; pp < tot; pp += nwg * 256) x6::x6_split_piece(d.presplit, pp);
+      return;
+    }
+  }
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int lr = lane & 15, lq = lane >> 4;
@@ -464,8 +476,12 @@ bool mlp_parts_launch(const d3a_mlp_fwd_desc& d, hipStream_t st) {
     return false;
   for (int l = 0; l < 2; ++l)
     if (d.h[l] && !a16(d.h[l], d.sh)) return false;
-  if (d.rows == 0) return true;
-  const dim3 grid((unsigned)((d.rows + S_RB - 1) / S_RB), (unsigned)d.C, (unsigned)D3A_MLP_PARTS);
+  if (d.rows == 0 && d.presplit.n_jobs == 0) return true;
+  // (presplit: enough extra workgroups for one piece a thread)
+  const int64_t pieces = d.presplit.n_jobs > 0 ? x6::x6_split_total(d.presplit) : 0;
+  const int64_t per_x = 256LL * d.C * D3A_MLP_PARTS;
+  const int64_t ex = (pieces + per_x - 1) / per_x;
+  const dim3 grid((unsigned)((d.rows + S_RB - 1) / S_RB + ex), (unsigned)d.C, (unsigned)D3A_MLP_PARTS);
   if (d.n_out <= 16)
     hipLaunchKernelGGL(mlp_parts_kernel<16>, grid, dim3(256), 0, st, d);
   else

@@ -39,6 +39,7 @@
 // Reference: the autograd backward of update_critic's loss (ddpg_impl.py:119-133
 // via cql_impl.py:110-125) through VectorEncoderWithAction (encoders.py:265-275,
 // 328-339) and ContinuousMeanQFunction._fc (mean_q_function.py:255-256).
+#include <cstdlib>
 #include "common.hpp"
 #include "../../include/d3rlpy_amd.h"
 #include "x6.hpp"
@@ -129,7 +130,10 @@ struct RowOps {
 // prologue of every workgroup -- the conservative scale of the rows' gradients
 // from the alpha step each workgroup takes itself; workgroup 0 writes the
 // metrics, scalars and the new scalar optimiser state (lc.stage)
-template <int NDB, bool CQL = false>
+// ST (diagnostic build, D3A_BWD_STAMPS=1; results right): s_memtime stamps of
+// waves 0 and 4 of every workgroup at the phase boundaries (d3a_bwd_stamps)
+__device__ unsigned long long bwd_stamps[256 * 2 * 8];
+template <int NDB, bool CQL = false, bool ST = false>
 __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int P, int rbp, int nkw,
                                                          d3a_cql_loss_desc lc) {
   __shared__ __attribute__((aligned(16))) TLds L;
@@ -137,6 +141,13 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int l16 = lane & 15, g = lane >> 4;
+  auto stamp = [&](int k) {
+    if constexpr (ST) {
+      if ((t == 0 || t == 256) && blockIdx.x < 256)
+        bwd_stamps[(blockIdx.x * 2 + (t >> 8)) * 8 + k] = __builtin_amdgcn_s_memtime();
+    }
+  };
+  stamp(0);
   // decode: block id b = 8 k + x (x the XCD under round-robin dispatch); the
   // 16 slices q = k & 15 of unit u = (k >> 4) 8 + x share the XCD
   const int bid = blockIdx.x;
@@ -169,43 +180,27 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
   const bool col = w >= 4;
   const int rw = w & 3;  // wave within its role: sub-blocks rw, rw + 4, ...
 
-  // (CQL) this thread's share of the loss stage's sums, loaded up front (slot
-  // p = t; clamped and masked, so no load waits behind a branch): alpha's
-  // sum of lse and data Q; workgroup 0 also the critic set's lse, the squared
-  // TD errors and the temperature's log-probs
+  // (CQL) this thread's share of the loss stage's sums: slot p = t's values
+  // loaded raw up front (clamped, masked where summed after the staging, so
+  // no load waits before the staging's own loads are out): alpha's lse and
+  // data Q; workgroup 0 also the critic set's lse and the squared TD errors
   const bool wg0 = blockIdx.x == 0;
   float cv[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   [[maybe_unused]] float st_lt = 0.f, st_tm = 0.f, st_tv = 0.f, st_la = 0.f, st_am = 0.f, st_av = 0.f;
-  if constexpr (CQL) {
-    const int64_t B = lc.B, CB = (int64_t)lc.C * lc.B, NB = (int64_t)lc.N * lc.B;
-    // (every state value, updated or not: the stage carries all six)
-    st_lt = *lc.log_temp;
-    st_la = *lc.log_alpha;
-    st_tm = *lc.temp_m;
-    st_tv = *lc.temp_v;
-    st_am = *lc.alpha_m;
-    st_av = *lc.alpha_v;
-    auto add = [&](int64_t pp, bool first) {
-      const int64_t p2 = pp < CB ? pp : CB - 1;
-      const bool ok = pp < CB;
-      const int64_t cc = p2 / B, bb = p2 - cc * B;
-      const float qd = lc.q[cc * lc.R + 6 * NB + bb];
-      const float la = lc.update_alpha ? lc.lse[p2] : 0.f;
-      float lcv = 0.f, t2 = 0.f;
-      if (wg0) {
-        lcv = lc.lse[CB + p2];
-        t2 = lc.td2[p2];
-      }
-      cv[0] = first ? keep_if(ok, la) : cv[0] + keep_if(ok, la);
-      cv[1] = first ? keep_if(ok, qd) : cv[1] + keep_if(ok, qd);
-      cv[2] = first ? keep_if(ok, lcv) : cv[2] + keep_if(ok, lcv);
-      cv[3] = first ? keep_if(ok, t2) : cv[3] + keep_if(ok, t2);
-    };
-    add(t, true);
-    for (int64_t pp = t + T_NT; pp < CB; pp += T_NT) add(pp, false);
-    if (wg0 && lc.update_temp)
-      for (int64_t bb = t; bb < B; bb += T_NT) cv[4] += lc.logp_temp[bb] - (float)lc.A;
-  }
+  [[maybe_unused]] float r_qd = 0.f, r_la = 0.f, r_lc = 0.f, r_t2 = 0.f, r_lt = 0.f;
+  const int cb_n = CQL ? lc.C * lc.B : 0;  // C B (< 2^31: checked on the host)
+  auto cql_row = [&](int pp, float& qd, float& la, float& lcv, float& t2) {
+    const int p2 = pp < cb_n ? pp : cb_n - 1;
+    const int cc = p2 / lc.B, bb = p2 - cc * lc.B;
+    // (every load unconditional -- in range -- and masked where summed: a load
+    // under a branch makes the compiler wait for every load in flight)
+    qd = lc.q[(int64_t)cc * lc.R + 6LL * lc.N * lc.B + bb];
+    la = lc.lse[p2];
+    lcv = lc.lse[cb_n + p2];
+    t2 = lc.td2[p2];
+  };
+
+
   // ---- prologue: the byte table and the slice's (w3 W2) parts
   if (t < 256) {
     uint4 v;
@@ -225,6 +220,24 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
       wv[k] = W2g[o * T_H + i0 + (t & 15)];
       w3v[k] = w3g[o];
     }
+    // (CQL) the loss stage's loads after the staging's (the counter is in
+    // order: the staging below waits for its own loads only)
+    if constexpr (CQL) {
+      cql_row(t, r_qd, r_la, r_lc, r_t2);
+      r_lt = lc.logp_temp[t < lc.B ? t : lc.B - 1];  // (used by workgroup 0)
+      // the scalar optimiser state (every value, updated or not: the stage
+      // carries all six) as vector loads through an opaque zero index, in
+      // the vector counter's order: as scalar loads the kernel-argument
+      // loads' waits would wait for them
+      int z0;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(z0));
+      st_lt = lc.log_temp[z0];
+      st_la = lc.log_alpha[z0];
+      st_tm = lc.temp_m[z0];
+      st_tv = lc.temp_v[z0];
+      st_am = lc.alpha_m[z0];
+      st_av = lc.alpha_v[z0];
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int o = (t >> 4) + 32 * k;
@@ -235,7 +248,28 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
       L.bw[2][(t & 15) * T_BLD + o] = e;
     }
   }
+  stamp(1);
+  // (CQL) the wave's sums published in LDS for the prologue's barrier
+  auto cql_publish = [&]() {
   if constexpr (CQL) {
+    // slot t's values, then (C B > 512) the rest in p order; workgroup 0's
+    // temperature log-probs
+    const bool ok = t < cb_n, oa = ok && lc.update_alpha, o0 = ok && wg0;
+    cv[0] = keep_if(oa, r_la);
+    cv[1] = keep_if(ok, r_qd);
+    cv[2] = keep_if(o0, r_lc);
+    cv[3] = keep_if(o0, r_t2);
+    for (int pp = t + T_NT; pp < cb_n; pp += T_NT) {
+      float a0, a1, a2, a3;
+      cql_row(pp, a1, a0, a2, a3);
+      cv[0] += keep_if(lc.update_alpha, a0);
+      cv[1] += a1;
+      cv[2] += keep_if(wg0, a2);
+      cv[3] += keep_if(wg0, a3);
+    }
+    cv[4] = keep_if(wg0 && lc.update_temp && t < lc.B, r_lt - (float)lc.A);
+    if (wg0 && lc.update_temp)
+      for (int bb = t + T_NT; bb < lc.B; bb += T_NT) cv[4] += lc.logp_temp[bb] - (float)lc.A;
     // the wave's sums (cql_loss_stage's block_sum order: wave sums, then the
     // waves in order after the barrier)
 #pragma unroll
@@ -245,6 +279,7 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
       for (int k = 0; k < 5; ++k) L.cs[k][w] = cv[k];
     }
   }
+  };
   // (CQL) after the prologue's barrier: the sums, alpha's Adam step and the
   // conservative scale, formed by every thread (workgroup 0's thread 0 also
   // the temperature's step and the stage's outputs)
@@ -269,8 +304,8 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
         alpha_loss = -(ca0 * (scaled - lc.alpha_threshold));
         const bool pass = (e >= 0.f) && (e <= 1e6f);
         const float g = pass ? -(scaled - lc.alpha_threshold) * e : 0.f;
-        const double bcl[2] = {lc.bc[2], lc.bc[3]};
-        lalpha = adam_scalar_r(lalpha, am, av, g, lc.alpha_lr, lc.beta1, lc.beta2, lc.adam_eps, bcl);
+        lalpha = adam_scalar_f(lalpha, am, av, g, lc.beta1, lc.beta2, lc.adam_eps, (float)lc.bc[2],
+                               (float)lc.bc[3]);
       }
       const float ca = fminf(fmaxf(expf(lalpha), 0.f), 1e6f);
       const float gcons = ca * lc.conservative_weight / CB;
@@ -283,8 +318,8 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
           const float e = expf(ltemp);
           lc.metrics[0] = -(e * sum[4]) / B;
           const float g = (-1.f / B) * sum[4] * e;
-          const double bct[2] = {lc.bc[0], lc.bc[1]};
-          ltemp = adam_scalar_r(ltemp, tm, tv, g, lc.temp_lr, lc.beta1, lc.beta2, lc.adam_eps, bct);
+          ltemp = adam_scalar_f(ltemp, tm, tv, g, lc.beta1, lc.beta2, lc.adam_eps, (float)lc.bc[0],
+                                (float)lc.bc[1]);
           lc.metrics[1] = expf(ltemp);
         }
         if (lc.update_alpha) {
@@ -322,12 +357,7 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
     return *reinterpret_cast<const bf16x8*>(&L.lut[byte]);
   };
 
-  if constexpr (CQL) {
-    // the wave sums published, then every thread forms the scalars (one
-    // barrier more than the plain kernel, ahead of the sub-block loads)
-    __syncthreads();
-    cql_scalars();
-  }
+  cql_publish();  // (before the role split: one copy of the code)
   if (col) {
     // ================= col waves: R[o][i] += m^T (g' h1), S, sum g'
     f32x4 R[T_NQ];
@@ -390,6 +420,9 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
     ColOps A, B;
     load(A, 0);
     __syncthreads();  // table and parts staged (col waves only need the table)
+    stamp(2);
+    cql_scalars();    // (CQL: the wave sums published by the same barrier)
+    stamp(3);
     // nkw sub-blocks (a multiple of 4) in chunks of four, each chunk straight-
     // line code with no branch for the compiler to sink the prefetch loads
     // into (a sub-block past the wave's last is computed too: g' = 0 there,
@@ -411,6 +444,7 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    stamp(4);
 #pragma unroll
     for (int tt = 0; tt < T_NQ; ++tt) L.red[rw][tt][lane] = R[tt];
     L.s[rw][lane] = s_acc;
@@ -498,6 +532,9 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
     RowOps<NDB> A, B;
     load(A, 0);
     __syncthreads();  // table and parts staged
+    stamp(2);
+    cql_scalars();
+    stamp(3);
     // nkw sub-blocks (a multiple of 4) in chunks of four, each chunk straight-
     // line code with no branch for the compiler to sink the prefetch loads
     // into (a sub-block past the wave's last is computed too: g' = 0 there,
@@ -519,11 +556,13 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    stamp(4);
 #pragma unroll
     for (int db = 0; db < NDB; ++db) L.w1[rw][db][lane] = W1acc[db];
     L.b1[rw][lane] = b1_acc;
   }
   __syncthreads();
+  stamp(5);
 
   // ---- epilogue: the four waves of each role summed in fp64, in wave order
   float* dW2 = d.dW2 + pc * (T_H * T_H);
@@ -583,6 +622,7 @@ __global__ __launch_bounds__(T_NT) void q2x6t_bwd_kernel(d3a_q2_bwd_desc d, int 
       d.db3[pc] = (float)(((L.g3[0] + L.g3[1]) + L.g3[2]) + L.g3[3]);
     }
   }
+  stamp(6);
 }
 
 int64_t default_splits(int64_t rows, int C) {
@@ -627,7 +667,16 @@ int launch_q2x6t_bwd(const d3a_q2_bwd_desc& d, hipStream_t st, const d3a_cql_los
   const int ndb = (d.n_in + 15) / 16;
   const d3a_cql_loss_desc l = lc ? *lc : d3a_cql_loss_desc{};
   const int Pi = (int)P, rbpi = (int)rbp, nkwi = (int)nkw;
-  if (lc) {
+  static const bool stamps = [] {
+    const char* e = getenv("D3A_BWD_STAMPS");
+    return e && atoi(e) != 0;
+  }();
+  if (stamps && ndb <= 1) {  // (diagnostic: phase stamps, d3a_bwd_stamps)
+    if (lc)
+      hipLaunchKernelGGL((q2x6t_bwd_kernel<1, true, true>), grid, block, 0, st, d, Pi, rbpi, nkwi, l);
+    else
+      hipLaunchKernelGGL((q2x6t_bwd_kernel<1, false, true>), grid, block, 0, st, d, Pi, rbpi, nkwi, l);
+  } else if (lc) {
     if (ndb <= 1)
       hipLaunchKernelGGL((q2x6t_bwd_kernel<1, true>), grid, block, 0, st, d, Pi, rbpi, nkwi, l);
     else if (ndb == 2)
@@ -660,5 +709,17 @@ extern "C" int d3a_q2_bwd_x6_cql(const d3a_q2_bwd_desc* dp, const d3a_cql_loss_d
                 "n_scaled 3NB, rows 3NB + B)");
   D3A_CHECK_ARG(d.dz2 == nullptr && d.m2t != nullptr,
                 "d3a_q2_bwd_x6_cql: the slice kernel (m2t set, no dz2)");
+  D3A_CHECK_ARG((int64_t)lc->C * lc->B < (int64_t(1) << 30), "d3a_q2_bwd_x6_cql: C B too large");
   return launch_q2x6t_bwd(d, (hipStream_t)stream, lc);
+}
+
+// diagnostic: copy the stamp buffer of the last D3A_BWD_STAMPS=1 launch
+extern "C" int d3a_bwd_stamps(unsigned long long* dst, int n) {
+  D3A_CHECK_ARG(dst && n >= 0 && n <= 256 * 2 * 8, "d3a_bwd_stamps: bad arguments");
+  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(bwd_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) !=
+      hipSuccess) {
+    set_error("d3a_bwd_stamps: copy failed");
+    return -2;
+  }
+  return 0;
 }

@@ -321,7 +321,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             h_from: Optional[int] = None, aux: Optional[tuple] = None,
             skip_head: bool = False, out_parts: Optional[torch.Tensor] = None,
             row_mean: Optional[torch.Tensor] = None, xgen=None, xgen_keep: bool = False,
-            wparts: Optional[tuple] = None) -> bool:
+            wparts: Optional[tuple] = None, presplit=None) -> bool:
     """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
     (through its first ``members`` members only, when given).  ``keep_h``:
     store the hidden activations in ``acts.h`` (needed by a backward pass),
@@ -348,6 +348,9 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     ``wparts`` (WeightImages.wparts): where the launch is the pre-split x6 Q
     forward, its W0 / W1 (and the aux pass's) are read from those images
     (formed from the current weights by an earlier launch of the step).
+
+    ``presplit`` (an X6SplitDesc, with ``out_parts``): the parts-path launch
+    also runs those d3a_x6_split jobs on extra workgroups.
 
     ``row_mean`` ([C][R] fp32): also the mean of each row's outputs, where the
     launch is d3a_mlp_fwd_x6 (its epilogue forms it); returns whether it was
@@ -397,6 +400,8 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         d.sout, d.ldout = R * sizes[-1], sizes[-1]
         if out_parts is not None:
             d.out, d.parts, d.s_part = out_parts.data_ptr(), N.MLP_PARTS, C * R * sizes[-1]
+            if presplit is not None:
+                d.presplit = presplit
         d.r0, d.rows, d.C = r0, n, C
         d.h_from = r0 if h_from is None else max(r0, h_from)
         if aux is not None and members is None:

@@ -206,6 +206,29 @@ typedef struct d3a_head1_min_desc {
 } d3a_head1_min_desc;
 int d3a_head1_min(const d3a_head1_min_desc* desc, void* stream);
 
+/* ---- split-bf16 operand images of critic weights ------------------------ */
+
+/* Exact three-way split of fp32 weights into bf16 parts, laid out as the
+ * split-bf16 critic forward's MFMA A operand (d3a_mlp_fwd_desc.wp): for row
+ * r < rows and 8-wide k block kb < kpad / 8, dst + (r * (kpad / 8) + kb) * 48
+ * bytes holds parts 0, 1, 2 of src[r][8 kb .. 8 kb + 7] (8 bf16 each; x = p0
+ * + p1 + p2 exactly: p0 = bf16(x), p1 = bf16(x - p0), p2 = bf16(x - p0 -
+ * p1)), columns k .. kpad zero.  src is row-major [rows][k] (nn.Linear's
+ * weight, members stacked); kpad a multiple of 16, >= k; dst 16-byte aligned.
+ * No reference counterpart: the reference multiplies the fp32 weights
+ * (encoders.py:265-275, 328-339); this is the same product's operand. */
+typedef struct d3a_x6_split_job {
+  const float* src;
+  void* dst;
+  int32_t rows, k, kpad, pad_;
+} d3a_x6_split_job;
+#define D3A_X6_SPLIT_MAX_JOBS 4
+typedef struct d3a_x6_split_desc {
+  d3a_x6_split_job job[D3A_X6_SPLIT_MAX_JOBS];
+  int32_t n_jobs;
+} d3a_x6_split_desc;
+int d3a_x6_split(const d3a_x6_split_desc* d, void* stream);
+
 /* Whole-MLP forward, one launch (replaces the per-layer nn.Linear + ReLU
  * chain of VectorEncoder / VectorEncoderWithAction, encoders.py:265-275,
  * 328-339, and the linear head: mean_q_function.py:255-256 `_fc`,
@@ -300,6 +323,11 @@ typedef struct d3a_mlp_fwd_desc {
    * results are bitwise those of the in-kernel split.                       */
   const void* wp[2];
   const void* aux_wp[2];
+  /* Optional (the parts path only): presplit.n_jobs > 0 appends workgroups
+   * that run those d3a_x6_split jobs -- on the CUs the few-hundred-row pass
+   * leaves idle (the CQL step's critic weight images, formed by the policy
+   * forward that precedes the critic forward). */
+  d3a_x6_split_desc presplit;
 } d3a_mlp_fwd_desc;
 #define D3A_MLP_PARTS 4
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);
@@ -636,28 +664,7 @@ int d3a_philox_fill(float* out, int64_t n_normal, int64_t n_uniform, float lo,
                     float hi, uint64_t seed, int64_t* ctr,
                     unsigned int* ticket, void* stream);
 
-/* ---- split-bf16 operand images of critic weights ------------------------ */
 
-/* Exact three-way split of fp32 weights into bf16 parts, laid out as the
- * split-bf16 critic forward's MFMA A operand (d3a_mlp_fwd_desc.wp): for row
- * r < rows and 8-wide k block kb < kpad / 8, dst + (r * (kpad / 8) + kb) * 48
- * bytes holds parts 0, 1, 2 of src[r][8 kb .. 8 kb + 7] (8 bf16 each; x = p0
- * + p1 + p2 exactly: p0 = bf16(x), p1 = bf16(x - p0), p2 = bf16(x - p0 -
- * p1)), columns k .. kpad zero.  src is row-major [rows][k] (nn.Linear's
- * weight, members stacked); kpad a multiple of 16, >= k; dst 16-byte aligned.
- * No reference counterpart: the reference multiplies the fp32 weights
- * (encoders.py:265-275, 328-339); this is the same product's operand. */
-typedef struct d3a_x6_split_job {
-  const float* src;
-  void* dst;
-  int32_t rows, k, kpad, pad_;
-} d3a_x6_split_job;
-#define D3A_X6_SPLIT_MAX_JOBS 4
-typedef struct d3a_x6_split_desc {
-  d3a_x6_split_job job[D3A_X6_SPLIT_MAX_JOBS];
-  int32_t n_jobs;
-} d3a_x6_split_desc;
-int d3a_x6_split(const d3a_x6_split_desc* d, void* stream);
 
 /* ---- CQL / SAC fused stages (d3rlpy/algos/torch/cql_impl.py,
  *      sac_impl.py) ------------------------------------------------------- */
@@ -766,8 +773,9 @@ typedef struct d3a_cql_loss_desc {
    * single device, conservative, no soft target, update_critic): this entry
    * launches only the logsumexp stage, which also writes every data row's
    * alpha-free gradient dq[c][6NB + b] = 2 (q - y) / B (the backward
-   * subtracts the conservative term), td2[c][b] = (q - y)^2 and bc[0:4] = 1 -
-   * beta1^t, 1 - beta2^t of the coming temperature step, then of alpha's.
+   * subtracts the conservative term), td2[c][b] = (q - y)^2 and bc[0:4] =
+   * the coming temperature step's (float) lr / (1 - beta1^t) and (float)
+   * sqrt(1 - beta2^t), then alpha's (fp64 pows, the loss stage's constants).
    * stage [6]: the new log_temp, temp_m, temp_v, log_alpha, alpha_m, alpha_v
    * the backward computes; the critic Adam's tail commits them
    * (d3a_adam_desc.commit_*). */
@@ -790,6 +798,10 @@ int d3a_cql_loss(const d3a_cql_loss_desc* d, void* stream);
  * state to loss.stage (committed by a later launch: every workgroup reads the
  * old state).  gscale is not read. */
 int d3a_q2_bwd_x6_cql(const d3a_q2_bwd_desc* d, const d3a_cql_loss_desc* loss, void* stream);
+/* Diagnostic (synchronous, not for graphs): the phase stamps ([workgroup
+ * < 256][wave 0 / 4][8] s_memtime values) of the last slice-backward launch
+ * made with D3A_BWD_STAMPS=1 in the environment. */
+int d3a_bwd_stamps(unsigned long long* dst, int n);
 
 /* Actor stage helpers (SACImpl.compute_actor_loss, sac_impl.py:114-121):
  * from the critics' Q at (s, tanh u) and the policy head, the per-row

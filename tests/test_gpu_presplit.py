@@ -156,7 +156,7 @@ def test_presplit_forward_is_bitwise_the_splitting_forward(rows, h_from, aux, n_
 
 
 def test_cql_step_forms_the_images_of_the_step_weights():
-    """The sampler launch's presplit jobs: after update_step, the workspace's
+    """The policy forward's presplit workgroups: after update_step, the workspace's
     images are d3a_x6_split of the critic / target weights as they were when
     the step started (the weights its critic forward read)."""
     import sys

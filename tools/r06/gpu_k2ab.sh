@@ -14,5 +14,5 @@ fi
 for v in 1 0 1 0; do
   env $VAR=$v timeout -k 10 300 python -u bench.py --algo $ALGO --steps 2000 --warmup 50 --no-cpu-baseline > $O/bench_$v.json 2>$O/bench.err || { tail -20 $O/bench.err; exit 1; }
   python -c "
-import json; d=json.loads(open('$O/bench_$v.json').read().strip().splitlines()[-1]); print('$VAR=$v', d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'], d['roofline']['frac'])"
+import json; d=json.loads(open('$O/bench_$v.json').read().strip().splitlines()[-1]); print('$VAR=$v', d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'], d['roofline']['frac'], d.get('roofline_other',{}).get('avg_launch_us'))"
 done
