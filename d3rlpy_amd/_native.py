@@ -102,7 +102,7 @@ class AdamDesc(C.Structure):
         ("ring", vp), ("ring_cap", C.c_int64), ("ring_ctr", vp), ("metric_scale", C.c_float),
         ("blocks", vp),
         ("commit_src", vp), ("commit_dst", vp * 8), ("n_commit", C.c_int32),
-        ("commit_step", vp * 2),
+        ("commit_step", vp * 2), ("one_elem", C.c_int32),
     ]
 
 

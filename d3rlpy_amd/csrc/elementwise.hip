@@ -153,36 +153,87 @@ __host__ __device__ __forceinline__ int seg_lanes(int64_t n_partials, int64_t nu
   return n_partials >= 64 ? 16 : 1;
 }
 
+// elements per thread: 4 for large one-lane segments whose size is a
+// multiple of 4 (16-byte state / partial loads where the pointers allow --
+// K5's 1.6 M fc weights were a thread each: its Adam 41.6 -> 34.4 us), else 1
+// (K2's 65 K-weight critic segments at 4 a thread filled a third of the
+// chip: 6.6 -> 7.2 us); threads per segment = numel * L / V (nets.py
+// AdamGroup counts the blocks by the same rule)
+__host__ __device__ __forceinline__ int seg_vec(int64_t n_partials, int64_t numel) {
+  return (seg_lanes(n_partials, numel) == 1 && numel % 4 == 0 && numel >= (1 << 18)) ? 4 : 1;
+}
+__host__ __device__ __forceinline__ int64_t seg_threads(int64_t n_partials, int64_t numel) {
+  return numel * seg_lanes(n_partials, numel) / seg_vec(n_partials, numel);
+}
+
+// Offsets are 32-bit bytes from the segment's (uniform) base: one VGPR per
+// load address instead of two (a segment's partials are < 4 GiB: nets.py
+// AdamGroup checks), which took adam_kernel from 142 VGPRs (3 waves a SIMD,
+// every launch a dozen latency rounds) to the 8-wave range.
 template <int U>
 __device__ __forceinline__ double sum_partials_u(const float* g, int64_t n, int64_t stride,
                                                  int64_t i, int j, int L) {
   double gd = 0.0;
-  for (int64_t q = j; q < n; q += (int64_t)U * L) {
+  const char* gb = reinterpret_cast<const char*>(g);
+  const uint32_t n32 = (uint32_t)n, s4 = (uint32_t)stride * 4u, i4 = (uint32_t)i * 4u;
+  for (uint32_t q = (uint32_t)j; q < n32; q += (uint32_t)(U * L)) {
     float v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       // a clamped (always valid) address: the loads stay unconditional, so
       // none of them is fenced behind a branch and all are in flight at once
-      const int64_t qq = q + (int64_t)u * L;
-      v[u] = g[(qq < n ? qq : n - 1) * stride + i];
+      const uint32_t qq = q + (uint32_t)(u * L);
+      v[u] = *reinterpret_cast<const float*>(gb + ((qq < n32 ? qq : n32 - 1u) * s4 + i4));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (q + (int64_t)u * L < n) gd += (double)v[u];
+      if (q + (uint32_t)(u * L) < n32) gd += (double)v[u];
   }
   for (int o = L >> 1; o > 0; o >>= 1) gd += __shfl_xor(gd, o, 64);
   return gd;
+}
+
+// four consecutive elements' partial sums (one lane, q ascending, fp64: the
+// one-lane order of sum_partials_u), 16-byte loads; at most 8 in flight
+__device__ __forceinline__ void sum_partials4(const float* g, int64_t n, int64_t stride,
+                                              int64_t i, double (&gd)[4]) {
+  const char* gb = reinterpret_cast<const char*>(g);
+  const uint32_t n32 = (uint32_t)n, s4 = (uint32_t)stride * 4u, i4 = (uint32_t)i * 4u;
+  constexpr int U = 8;
+  for (uint32_t q = 0; q < n32; q += U) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t qq = q + (uint32_t)u;
+      v[u] = *reinterpret_cast<const float4*>(gb + ((qq < n32 ? qq : n32 - 1u) * s4 + i4));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (q + (uint32_t)u < n32) {
+        gd[0] += (double)v[u].x;
+        gd[1] += (double)v[u].y;
+        gd[2] += (double)v[u].z;
+        gd[3] += (double)v[u].w;
+      }
+  }
 }
 
 // the partial sum of element i in index order; the batch of loads in flight is
 // sized to the partial count (8 for the critic's slice-backward row blocks: a
 // 32-load batch would issue 24 clamped duplicates per element), the same
 // order and sum for every batch size
+// (the batch: the lane's partial count rounded up to a power of two, at most
+// 16 -- K5's 128 embedding-weight partials over 16 lanes are eight a lane: a
+// 32-load batch issued 24 clamped duplicates each; the fc's 4 split-K
+// partials 4 of 8)
 __device__ __forceinline__ double sum_partials(const float* g, int64_t n, int64_t stride,
                                                int64_t i, int j, int L) {
-  if (L == 1 && n <= 8) return sum_partials_u<8>(g, n, stride, i, j, L);
-  if (L == 1 && n <= 16) return sum_partials_u<16>(g, n, stride, i, j, L);
-  return sum_partials_u<32>(g, n, stride, i, j, L);
+  const int64_t per = (n + L - 1) / L;  // uniform over the segment
+  if (per <= 1) return sum_partials_u<1>(g, n, stride, i, j, L);
+  if (per <= 2) return sum_partials_u<2>(g, n, stride, i, j, L);
+  if (per <= 4) return sum_partials_u<4>(g, n, stride, i, j, L);
+  if (per <= 8) return sum_partials_u<8>(g, n, stride, i, j, L);
+  return sum_partials_u<16>(g, n, stride, i, j, L);
 }
 
 // ---- Adam (torch.optim.adam._single_tensor_adam, weight_decay = 0) ---------
@@ -200,7 +251,7 @@ __device__ __forceinline__ void locate_block(const d3a_adam_segment* segs, int n
   for (int c = 0; c < n_seg; c += 64) {
     const int s = c + lane;
     long long nb = 0;
-    if (s < n_seg) nb = (segs[s].numel * seg_lanes(segs[s].n_partials, segs[s].numel) + 255) / 256;
+    if (s < n_seg) nb = (seg_threads(segs[s].n_partials, segs[s].numel) + 255) / 256;
     long long incl = nb;
     for (int o = 1; o < 64; o <<= 1) {
       const long long t = __shfl_up(incl, o, 64);
@@ -218,7 +269,8 @@ __device__ __forceinline__ void locate_block(const d3a_adam_segment* segs, int n
   }
 }
 
-__global__ __launch_bounds__(256) void adam_kernel(d3a_adam_desc a) {
+template <bool VEC>
+__global__ __launch_bounds__(256, VEC ? 6 : 8) void adam_kernel(d3a_adam_desc a) {
   __shared__ float s_step_size, s_bc2_sqrt;
   __shared__ int s_seg;
   __shared__ int64_t s_first;
@@ -255,22 +307,47 @@ __global__ __launch_bounds__(256) void adam_kernel(d3a_adam_desc a) {
   const d3a_adam_segment sg = tab ? a.blocks[blockIdx.x].seg : segs[s_seg];
   const int64_t first = tab ? a.blocks[blockIdx.x].first : s_first;
   const int L = seg_lanes(sg.n_partials, sg.numel);
+  // (VEC false: the host's one_elem -- no segment has seg_vec 4)
+  const int V = VEC ? seg_vec(sg.n_partials, sg.numel) : 1;
   const int64_t lt = ((int64_t)blockIdx.x - first) * 256 + threadIdx.x;
-  const int64_t i = lt / L;
+  const int64_t i = V == 4 ? lt * 4 : lt / L;  // the thread's first element
   const bool act = i < sg.numel;
-  float m = 0.f, v = 0.f, p = 0.f, tv = 0.f;
   float* tg = a.soft ? sg.param + a.targ_delta : nullptr;
-  const bool lead = (lt % L) == 0;
-  double gd = 0.0;
+  // 16-byte accesses when every stream is 16-byte aligned (a flat store's
+  // segment offsets need not be), else four scalar ones
+  const bool v4 = V == 4 && sg.partial_stride % 4 == 0 &&
+                  ((reinterpret_cast<uintptr_t>(sg.param) | reinterpret_cast<uintptr_t>(sg.exp_avg) |
+                    reinterpret_cast<uintptr_t>(sg.exp_avg_sq) | reinterpret_cast<uintptr_t>(sg.grad) |
+                    reinterpret_cast<uintptr_t>(sg.grad_out) | reinterpret_cast<uintptr_t>(tg)) & 15) == 0;
+  const bool lead = V == 4 || (lt % L) == 0;
+  float m[4] = {}, v[4] = {}, p[4] = {}, tv[4] = {};
+  double gd[4] = {};
   if (act) {
     // the state loads go out with the partial loads (one round trip for both)
-    if (lead) {
-      m = sg.exp_avg[i];
-      v = sg.exp_avg_sq[i];
-      p = sg.param[i];
-      if (tg) tv = tg[i];
+    if (v4) {
+      const float4 m4 = *reinterpret_cast<const float4*>(sg.exp_avg + i);
+      const float4 v4_ = *reinterpret_cast<const float4*>(sg.exp_avg_sq + i);
+      const float4 p4 = *reinterpret_cast<const float4*>(sg.param + i);
+      m[0] = m4.x, m[1] = m4.y, m[2] = m4.z, m[3] = m4.w;
+      v[0] = v4_.x, v[1] = v4_.y, v[2] = v4_.z, v[3] = v4_.w;
+      p[0] = p4.x, p[1] = p4.y, p[2] = p4.z, p[3] = p4.w;
+      if (tg) {
+        const float4 t4 = *reinterpret_cast<const float4*>(tg + i);
+        tv[0] = t4.x, tv[1] = t4.y, tv[2] = t4.z, tv[3] = t4.w;
+      }
+      sum_partials4(sg.grad, sg.n_partials, sg.partial_stride, i, gd);
+    } else {
+      for (int e = 0; e < V; ++e) {
+        if (lead) {
+          m[e] = sg.exp_avg[i + e];
+          v[e] = sg.exp_avg_sq[i + e];
+          p[e] = sg.param[i + e];
+          if (tg) tv[e] = tg[i + e];
+        }
+        gd[e] = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i + e,
+                             V == 4 ? 0 : (int)(lt % L), V == 4 ? 1 : L);
+      }
     }
-    gd = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i, (int)(lt % L), L);
   }
   if (tab) __syncthreads();  // s_step_size; block 0: every ring writer has read *ring_ctr
   if (tail) {
@@ -283,28 +360,45 @@ __global__ __launch_bounds__(256) void adam_kernel(d3a_adam_desc a) {
   }
   if (act) {  // uniform over each lane group
     if (!lead) return;
-    // grad_scale: 1, or 1/world after a data-parallel SUM all-reduce (exact
-    // for power-of-two worlds)
-    const float g = grad_scale == 1.f ? (float)gd : __fmul_rn((float)gd, grad_scale);
-    if (sg.grad_out) sg.grad_out[i] = g;
-    // exp_avg.lerp_(grad, 1 - beta1): weight < 0.5 -> self + w * (end - self)
-    // (ATen's vectorised CPU lerp: fmadd(weight, end - self, self))
-    const float w = (float)(1.0 - beta1);
-    m = fmaf(w, __fsub_rn(g, m), m);
-    // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
-    v = __fmul_rn(v, (float)beta2);
-    const float omb2 = (float)(1.0 - beta2);
-    v = __fadd_rn(v, __fmul_rn(__fmul_rn(omb2, g), g));
     const float step_size = s_step_size;
     const float bc2_sqrt = s_bc2_sqrt;
-    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), (float)a.eps);
-    const float pnew = __fadd_rn(p, __fmul_rn(-step_size, __fdiv_rn(m, denom)));
-    sg.exp_avg[i] = m;
-    sg.exp_avg_sq[i] = v;
-    sg.param[i] = pnew;
-    // soft_sync of the target copy from the updated parameter, the three
-    // separately rounded ops of d3a_soft_update_f32 (torch_utility.py:27-33)
-    if (tg) tg[i] = __fadd_rn(__fmul_rn(tv, (float)(1.0 - a.tau)), __fmul_rn((float)a.tau, pnew));
+    float gs[4] = {}, tn[4] = {};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (e >= V) break;
+      // grad_scale: 1, or 1/world after a data-parallel SUM all-reduce (exact
+      // for power-of-two worlds)
+      const float g = grad_scale == 1.f ? (float)gd[e] : __fmul_rn((float)gd[e], grad_scale);
+      gs[e] = g;
+      // exp_avg.lerp_(grad, 1 - beta1): weight < 0.5 -> self + w * (end - self)
+      // (ATen's vectorised CPU lerp: fmadd(weight, end - self, self))
+      const float w = (float)(1.0 - beta1);
+      m[e] = fmaf(w, __fsub_rn(g, m[e]), m[e]);
+      // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
+      v[e] = __fmul_rn(v[e], (float)beta2);
+      const float omb2 = (float)(1.0 - beta2);
+      v[e] = __fadd_rn(v[e], __fmul_rn(__fmul_rn(omb2, g), g));
+      const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v[e]), bc2_sqrt), (float)a.eps);
+      p[e] = __fadd_rn(p[e], __fmul_rn(-step_size, __fdiv_rn(m[e], denom)));
+      // soft_sync of the target copy from the updated parameter, the three
+      // separately rounded ops of d3a_soft_update_f32 (torch_utility.py:27-33)
+      if (tg) tn[e] = __fadd_rn(__fmul_rn(tv[e], (float)(1.0 - a.tau)), __fmul_rn((float)a.tau, p[e]));
+    }
+    if (v4) {
+      if (sg.grad_out) *reinterpret_cast<float4*>(sg.grad_out + i) = make_float4(gs[0], gs[1], gs[2], gs[3]);
+      *reinterpret_cast<float4*>(sg.exp_avg + i) = make_float4(m[0], m[1], m[2], m[3]);
+      *reinterpret_cast<float4*>(sg.exp_avg_sq + i) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(sg.param + i) = make_float4(p[0], p[1], p[2], p[3]);
+      if (tg) *reinterpret_cast<float4*>(tg + i) = make_float4(tn[0], tn[1], tn[2], tn[3]);
+    } else {
+      for (int e = 0; e < V; ++e) {
+        if (sg.grad_out) sg.grad_out[i + e] = gs[e];
+        sg.exp_avg[i + e] = m[e];
+        sg.exp_avg_sq[i + e] = v[e];
+        sg.param[i + e] = p[e];
+        if (tg) tg[i + e] = tn[e];
+      }
+    }
   }
   // the step counter this launch reads is committed by another kernel
   // (d3a_step_end, or a later d3a_adam_step's inc_mask)
@@ -320,9 +414,25 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(const d3a_adam_segment
   __syncthreads();
   const d3a_adam_segment sg = segs[s_seg];
   const int L = seg_lanes(sg.n_partials, sg.numel);
+  const int V = seg_vec(sg.n_partials, sg.numel);
   const int64_t lt = ((int64_t)blockIdx.x - s_first) * 256 + threadIdx.x;
-  const int64_t i = lt / L;
+  const int64_t i = V == 4 ? lt * 4 : lt / L;
   if (i >= sg.numel) return;  // uniform over each lane group
+  if (V == 4) {
+    const bool v4 = sg.partial_stride % 4 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(sg.grad) |
+                      reinterpret_cast<uintptr_t>(sg.grad_out)) & 15) == 0;
+    double gd[4] = {};
+    if (v4) {
+      sum_partials4(sg.grad, sg.n_partials, sg.partial_stride, i, gd);
+      *reinterpret_cast<float4*>(sg.grad_out + i) =
+          make_float4((float)gd[0], (float)gd[1], (float)gd[2], (float)gd[3]);
+    } else {
+      for (int e = 0; e < 4; ++e)
+        sg.grad_out[i + e] = (float)sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i + e, 0, 1);
+    }
+    return;
+  }
   const double gd = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i, (int)(lt % L), L);
   if (lt % L) return;
   sg.grad_out[i] = (float)gd;
@@ -498,8 +608,12 @@ extern "C" int d3a_adam_step(const d3a_adam_desc* a, void* stream) {
                              a->n_metrics <= 256 && a->ring_cap > 0),
                 "d3a_adam_step: bad metric ring");
   D3A_CHECK_ARG(!a->soft || a->targ_delta != 0, "d3a_adam_step: soft update needs targ_delta");
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)a->n_blocks), dim3(256), 0, (hipStream_t)stream,
-                     *a);
+  if (a->one_elem)
+    hipLaunchKernelGGL(adam_kernel<false>, dim3((unsigned)a->n_blocks), dim3(256), 0,
+                       (hipStream_t)stream, *a);
+  else
+    hipLaunchKernelGGL(adam_kernel<true>, dim3((unsigned)a->n_blocks), dim3(256), 0,
+                       (hipStream_t)stream, *a);
   D3A_LAUNCH_CHECK("d3a_adam_step");
   return 0;
 }

@@ -167,6 +167,15 @@ class OptimState:
         self.step = torch.zeros(1, dtype=torch.int64, device=dev) if step is None else step
 
 
+def _seg_threads(n_partials: int, numel: int) -> int:
+    """Threads of one Adam / reduce segment (elementwise.hip seg_threads):
+    16 lanes per element for >= 64 partials, else one lane per 4 elements when
+    the size is a multiple of 4 and at least 2^18, else one per element."""
+    if n_partials >= 64:
+        return numel * 16
+    return numel // 4 if (numel % 4 == 0 and numel >= 1 << 18) else numel
+
+
 class AdamGroup:
     """A torch.optim.Adam equivalent over a set of segments of a ParamStore.
 
@@ -193,10 +202,13 @@ class AdamGroup:
         segs = (N.AdamSegment * len(self.names))()
         self.n_blocks = 0  # flat launch over the segments (d3a_adam_f32)
         self.n_blocks_reduced = 0
+        self.one_elem = True  # no segment takes four elements a thread
         for i, n in enumerate(self.names):
             gt, parts = grads.parts[n]
             numel = store.numel(n)
             assert gt.numel() == parts * numel, (n, gt.shape, numel)
+            if parts * numel * 4 >= 2 ** 32:  # elementwise.hip sum_partials_u: 32-bit offsets
+                raise ValueError(f"AdamGroup: {n}'s partials exceed 4 GiB ({parts} x {numel})")
             segs[i].param = store.ptr(n)
             segs[i].exp_avg = self.exp_avg.ptr(n)
             segs[i].exp_avg_sq = self.exp_avg_sq.ptr(n)
@@ -205,10 +217,9 @@ class AdamGroup:
             segs[i].n_partials = parts
             segs[i].partial_stride = numel
             segs[i].grad_out = self.grad_store.ptr(n) if self.grad_store is not None else None
-            # lanes per element (elementwise.hip seg_lanes)
-            lanes = 16 if parts >= 64 else 1
-            self.n_blocks += (numel * lanes + 255) // 256
-            self.n_blocks_reduced += (numel + 255) // 256
+            self.n_blocks += (_seg_threads(parts, numel) + 255) // 256
+            self.one_elem &= _seg_threads(parts, numel) == numel * (16 if parts >= 64 else 1)
+            self.n_blocks_reduced += (_seg_threads(1, numel) + 255) // 256
         raw = bytes(segs)
         self.seg_table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
         self._segs = segs
@@ -232,13 +243,12 @@ class AdamGroup:
 
     def _block_table(self, segs, partials: bool) -> torch.Tensor:
         """d3a_adam_block per flat block (the segment search done once here,
-        in the kernel's block order: segment s owns ceil(numel_s * L_s / 256)
-        blocks, L_s = 16 lanes per element for >= 64 partials, else 1)."""
+        in the kernel's block order: segment s owns ceil(threads_s / 256)
+        blocks, _seg_threads)."""
         rows = []
         first = 0
         for sg in segs:
-            lanes = 16 if (partials and sg.n_partials >= 64) else 1
-            nb = (sg.numel * lanes + 255) // 256
+            nb = (_seg_threads(sg.n_partials if partials else 1, sg.numel) + 255) // 256
             for _ in range(nb):
                 blk = N.AdamBlock()
                 blk.seg, blk.first = sg, first
@@ -269,8 +279,9 @@ class AdamGroup:
             kw["targ_delta"] = (targ.data.data_ptr() - self.store.data.data_ptr()) // 4
             assert kw["targ_delta"] != 0
         blocks = self.block_table_reduced if reduced else self.block_table
+        # (the reduced table: one partial, the same four-a-thread segments)
         ops.adam_step(table, len(self.names), nb, self.step, self.lr, self.beta1, self.beta2,
-                      self.eps, grad_scale, blocks=blocks, **kw)
+                      self.eps, grad_scale, blocks=blocks, one_elem=self.one_elem, **kw)
 
     def reduce(self) -> None:
         """grad_store <- sum of the split-K partials (no parameter update)."""

@@ -151,10 +151,12 @@ def adam_step(segs: torch.Tensor, n_seg: int, n_blocks: int, step: torch.Tensor,
               ring_ctr: Optional[torch.Tensor] = None, metric_scale: float = 1.0,
               blocks: Optional[torch.Tensor] = None, commit_src: Optional[torch.Tensor] = None,
               commit_dst: Sequence[torch.Tensor] = (),
-              commit_step: Sequence[Optional[torch.Tensor]] = ()) -> None:
+              commit_step: Sequence[Optional[torch.Tensor]] = (),
+              one_elem: bool = False) -> None:
     """d3a_adam_step: Adam with the soft target update (``targ_delta`` != 0:
     the target copy ``targ_delta`` elements from each parameter) and the
-    step's counter / metric-ring bookkeeping in one launch."""
+    step's counter / metric-ring bookkeeping in one launch.  ``one_elem``: no
+    segment takes four elements a thread (AdamGroup.one_elem)."""
     d = N.AdamDesc()
     d.segs, d.n_seg, d.n_blocks = ptr(segs), n_seg, n_blocks
     d.step, d.step_add = ptr(step), step_add
@@ -166,6 +168,7 @@ def adam_step(segs: torch.Tensor, n_seg: int, n_blocks: int, step: torch.Tensor,
         d.ring, d.ring_cap, d.ring_ctr = ptr(ring), ring.shape[0], ptr(ring_ctr)
     d.metric_scale = metric_scale
     d.blocks = ptr(blocks)  # per-block segment table (AdamGroup), or None
+    d.one_elem = int(one_elem)
     if commit_src is not None:
         # a scalar optimiser state staged by an earlier launch of the update
         assert len(commit_dst) <= 8 and commit_src.numel() >= len(commit_dst)

@@ -564,6 +564,10 @@ typedef struct d3a_adam_desc {
    * place (d3a_cql_loss_desc.stage) */
   const float* commit_src; float* commit_dst[8]; int32_t n_commit;
   int64_t* commit_step[2];
+  /* 1: no segment takes four elements a thread (>= 2^18 elements, a multiple
+   * of 4, < 64 partials) -- the launch runs the one-element kernel (fewer
+   * registers); 0: either */
+  int32_t one_elem;
 } d3a_adam_desc;
 int d3a_adam_step(const d3a_adam_desc* d, void* stream);
 

@@ -85,6 +85,11 @@ def test_cql_softmax_weights_vs_fp64():
             print(f"c{c} IS block {k}: {e:.2e}")
             worst = max(worst, e)
         hip_d, ref_d = dq[c, 6 * NB: 6 * NB + B], rec[c]["data"]
+        if ws._loss_in_bwd:
+            # the loss stage inside the slice backward leaves the data rows'
+            # TD part in ws.dq; the backward subtracts the conservative
+            # constant (scalars[2]) as it reads them (q2_x6_bwd2.hip)
+            hip_d = (dq[c, 6 * NB: 6 * NB + B].float() - ws.scalars[2].cpu()).double()
         e = float((hip_d - ref_d).abs().max() / ref_d.abs().max())
         print(f"c{c} data rows: {e:.2e}")
         worst = max(worst, e)

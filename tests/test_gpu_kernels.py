@@ -336,6 +336,61 @@ def test_adam_block_table_bit_identical(dev):
         assert torch.equal(a, b)
 
 
+def test_adam_vector_segments(dev):
+    """Segments of >= 2^18 elements (a multiple of 4) with < 64 partials run
+    four elements a thread (elementwise.hip seg_vec): 2 Adam steps vs
+    torch.optim.Adam on the fp64 partial sums, the partial reduction, and a
+    soft target copy 4 bytes off 16-byte alignment (the four-scalar fallback)
+    bitwise equal to an aligned one."""
+    from d3rlpy_amd import ops
+    from d3rlpy_amd.nets import AdamGroup, GradSpace, OptimState, ParamStore
+    shapes = {"w": ((520, 512), 5), "b": ((7,), 3), "e": (((1 << 18) + 4,), 1),
+              "u": ((300, 877), 1)}
+    runs = []
+    for shift in (0, 1):
+        g = torch.Generator().manual_seed(4)
+        store = ParamStore()
+        for n, (shp, _) in shapes.items():
+            store.add(n, shp)
+        store.allocate(dev)
+        gs = GradSpace(dev)
+        views, tp = {}, {}
+        for n, (shp, P) in shapes.items():
+            x0 = torch.randn(*shp, generator=g)
+            store.view(n).copy_(x0)
+            views[n] = gs.add(n, shp, P)
+            tp[n] = torch.nn.Parameter(x0.clone())
+        opt = AdamGroup(OptimState(store, list(shapes), lr=1e-3), gs)
+        topt = torch.optim.Adam(list(tp.values()), lr=1e-3)
+        tbuf = torch.zeros(store.size + 4, device=dev)
+        targ = tbuf[shift: shift + store.size]
+        targ.copy_(store.data * 0.5)
+        for it in range(2):
+            for n, (shp, P) in shapes.items():
+                parts = torch.randn(P, *shp, generator=g)
+                views[n].copy_(parts.view(views[n].shape))
+                tp[n].grad = parts.double().sum(0).float()
+            ops.adam_step(opt.seg_table, len(shapes), opt.n_blocks, opt.step, opt.lr, opt.beta1,
+                          opt.beta2, opt.eps, 1.0,
+                          targ_delta=(targ.data_ptr() - store.data.data_ptr()) // 4,
+                          tau=0.005, blocks=opt.block_table)
+            ops.step_end(opt.step, 1)
+            topt.step()
+        torch.cuda.synchronize()
+        for n in shapes:
+            torch.testing.assert_close(store.view(n).cpu(), tp[n].detach(), rtol=1e-6, atol=1e-7,
+                                       msg=n)
+        opt.grad_store.data.zero_()
+        opt.reduce()
+        torch.cuda.synchronize()
+        for n in shapes:
+            torch.testing.assert_close(opt.grad(n).cpu(), tp[n].grad, rtol=2e-7, atol=1e-9, msg=n)
+        runs.append((store.data.clone(), targ.clone(), opt.exp_avg.data.clone(),
+                     opt.exp_avg_sq.data.clone()))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+
+
 def test_philox_statistics(dev):
     from d3rlpy_amd import ops
     out = torch.zeros(1 << 20, device=dev)
