@@ -721,6 +721,10 @@ class _Workspace:
                 elif ops.CRITIC_GEMM == "x6":
                     gemm = ("split-bf16 x6, pre-split W images" if self.wimg is not None
                             else "split-bf16 x6")
+            elif (mlp.x6_deep3_shape(net) and mlp._X6_DEEP3 and ops.CRITIC_GEMM == "x6"
+                  and (R - r0 + B) * C >= 8192):
+                # the three-hidden-layer critic on d3a_mlp_fwd_x6 (register Q head)
+                gemm = "split-bf16 x6, three hidden layers"
             return launch, flops, (f"d3a_mlp_fwd critic ensemble ({gemm} MFMA): C={C} x "
                                    f"({R - r0} + {B} target) rows x {'-'.join(map(str, s))}")
         H, Hin = s[2], s[1]

@@ -178,7 +178,19 @@ __device__ __forceinline__ void act_to_image(const f32x16 (&o)[NRT], const float
 }
 
 // XL: n_in rounded up to 32 (32 or 64); KEEP: some kept activations (h[0] /
-// h[1]) are written (without them no store precedes the head's).
+// h[1] / h[2]) are written (without them no store precedes the head's).
+//
+// NHID: 256-wide hidden layers (2, or 3 for the CQL reproduction critic
+// [obs + act, 256, 256, 256, 1], reproductions/offline/cql.py:21-37): the
+// third is one more barrier-free stream over the image of the second.
+// HD (one output): the Q head as a register dot -- each wave's last-layer
+// activations times its 32 head weights, the lane halves and the eight waves'
+// partials summed in order -- instead of a head stream on one wave while
+// seven idle.
+//
+// Aux pass (d3a_mlp_fwd_desc.aux_rows > 0): workgroups C Gm .. C Gm + C Ga - 1
+// run the same network at parameter offset aux_wdelta (the target critics)
+// over aux_x, into aux_out, keeping nothing; Gm / Ga workgroups a member.
 //
 // Persistent: grid (G, 1, C), G <= the CU count / C, one workgroup per CU
 // (the LDS image allows no second).  Member c's rows are cut into 32-row
@@ -190,8 +202,8 @@ __device__ __forceinline__ void act_to_image(const f32x16 (&o)[NRT], const float
 // and head, the next tile's input rows and first weight steps are in flight
 // (XRaw4 registers, the freed slots of the weight stream), so only the first
 // tile pays the prologue's memory round trip.
-template <int XL, bool KEEP, bool STAMPS = false>
-__global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
+template <int XL, bool KEEP, bool STAMPS = false, int NHID = 2, bool HD = false>
+__global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, int Gm, int Ga) {
   constexpr int XLD = XL + 8;
   constexpr int NS1 = XL / 16;  // layer-1 k steps
   constexpr int X4 = XL / 4;
@@ -201,32 +213,41 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int li = lane & 31, lh = lane >> 5;
-  const int c = blockIdx.z;
-  const int r0 = (int)d.r0, rlim = (int)(d.r0 + d.rows);
-  const int nh = (int)((d.rows + 31) / 32);  // 32-row halves of this member
-  const int G = (int)gridDim.x, k = (int)blockIdx.x;
+  // (flat grid: the main pass's C Gm workgroups, then the aux pass's C Ga)
+  const int bid = (int)blockIdx.x;
+  const bool aux = bid >= d.C * Gm;
+  const int G = aux ? Ga : Gm;
+  const int c = aux ? (bid - d.C * Gm) / Ga : bid / Gm;
+  const int k = aux ? (bid - d.C * Gm) % Ga : bid % Gm;
+  const int r0 = aux ? 0 : (int)d.r0, rlim = aux ? (int)d.aux_rows : (int)(d.r0 + d.rows);
+  const int nh = (rlim - r0 + 31) / 32;  // 32-row halves of this member
   const int hb = (int)((int64_t)k * nh / G), he = (int)((int64_t)(k + 1) * nh / G);
   if (hb >= he) return;  // uniform: no rows for this workgroup
-  const int h_from = (int)d.h_from;
+  const int h_from = aux ? rlim : (int)d.h_from;
   const int nin = d.n_in, nout = d.n_out;
-  float* const outp = d.out + c * d.sout;
-  float* const h0g = KEEP && d.h[0] ? d.h[0] + c * d.sh : nullptr;
-  float* const h1g = KEEP && d.h[1] ? d.h[1] + c * d.sh : nullptr;
-  const int u0 = 32 * w + li;  // this lane's weight row in layers 1 and 2
-  const float* W0r = d.W[0] + c * d.sW[0] + u0 * nin;
-  const WMat W1m = wmat(d.W[1] + c * d.sW[1], W_H * W_H * 4);
+  const int64_t wdel = aux ? d.aux_wdelta : 0;
+  float* const outp = aux ? d.aux_out + c * d.aux_sout : d.out + c * d.sout;
+  float* const h0g = KEEP && !aux && d.h[0] ? d.h[0] + c * d.sh : nullptr;
+  float* const h1g = KEEP && !aux && d.h[1] ? d.h[1] + c * d.sh : nullptr;
+  float* const h2g = KEEP && NHID == 3 && !aux && d.h[2] ? d.h[2] + c * d.sh : nullptr;
+  float* const rmean = aux ? nullptr : d.row_mean;
+  const int u0 = 32 * w + li;  // this lane's weight row in the hidden layers
+  const float* W0r = d.W[0] + wdel + c * d.sW[0] + u0 * nin;
+  const WMat W1m = wmat(d.W[1] + wdel + c * d.sW[1], W_H * W_H * 4);
+  const WMat W2m = wmat(d.W[NHID == 3 ? 2 : 1] + wdel + c * d.sW[NHID == 3 ? 2 : 1], W_H * W_H * 4);
   const int w1o = (u0 * W_H + 8 * lh) * 4;  // byte offset of this lane's W1 row piece
-  const float* b0 = d.b[0] + c * d.sb[0];
-  const float* b1 = d.b[1] + c * d.sb[1];
-  const float* Wh = d.W[2] + c * d.sW[2];
-  const float* bh = d.b[2] + c * d.sb[2];
-  const float* xb = d.x + c * d.sxb;
-  const int64_t ldx = d.ldx;
+  const float* b0 = d.b[0] + wdel + c * d.sb[0];
+  const float* b1 = d.b[1] + wdel + c * d.sb[1];
+  const float* b2 = d.b[NHID == 3 ? 2 : 1] + wdel + c * d.sb[NHID == 3 ? 2 : 1];
+  const float* Wh = d.W[NHID] + wdel + c * d.sW[NHID];
+  const float* bh = d.b[NHID] + wdel + c * d.sb[NHID];
+  const float* xb = aux ? d.aux_x + c * d.aux_sxb : d.x + c * d.sxb;
+  const int64_t ldx = aux ? d.aux_ldx : d.ldx;
   const int nkt = (nout + 31) / 32;
   const int kout = 32 * w + li;  // head: this lane's output row (rows past n_out read row 0:
   const WMat Whm = wmat(Wh, nout * W_H * 4);
   const int who = ((kout < nout ? kout : 0) * W_H + 8 * lh) * 4;  // never stored)
-  const int wgi = blockIdx.x + blockIdx.z * gridDim.x;
+  const int wgi = bid;
   const unsigned long long t_start = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
   auto stamp = [&](int s, bool on) {
     if constexpr (STAMPS) {
@@ -290,7 +311,8 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
     constexpr int NRT = decltype(nrt)::value;
       const int m0 = r0 + 32 * h, rend = tile_end(h);
       const bool has_next = h + 2 < he;
-      const bool first = h == hb + 2;  // the stamped tile
+      // the stamped tile: the second (the steady state), or a workgroup's only one
+      const bool first = h == hb + 2 || he - hb <= 2;
       stamp(0, first);
       // the layer-1 weight row (clamped k, masked at use) and bias, reloaded per
       // tile (L2 hits) so that no register holds them across the streams; a
@@ -340,18 +362,93 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
       if (has_next) issue_x(h + 2);  // uniform
 
       // ---- layer 2: units 32 w .. over the image; the freed weight slots take
-      // the head's first steps (waves with no head: the next tile's layer 2)
+      // the next stream's first steps: layer 3's (NHID 3), else the head's
+      // (waves with no head: the next tile's layer 2)
   #pragma unroll
       for (int rt = 0; rt < NRT; ++rt)
   #pragma unroll
         for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
-      {
-        const WMat nm{w < nkt ? Whm.rs : W1m.rs};  // uniform
-        stream256<NRT>(W1m, w1o, nm, w < nkt ? who : w1o, hr, L.img, li, lh, o);
+      // (waves streaming a head after the last hidden layer; HD: none)
+      const bool hs = !HD && w < nkt;
+      if constexpr (NHID == 3) {
+        stream256<NRT>(W1m, w1o, W2m, w1o, hr, L.img, li, lh, o);
+      } else {
+        const WMat nm{hs ? Whm.rs : W1m.rs};  // uniform
+        stream256<NRT>(W1m, w1o, nm, hs ? who : w1o, hr, L.img, li, lh, o);
       }
       stamp(4, first);
       __syncthreads();  // every wave done reading image 1
-      act_to_image<KEEP, NRT>(o, b1v, h1g, m0, h_from, rend, w, li, lh, L.img);
+      if constexpr (NHID == 3) {
+        float4 b2v[4];
+  #pragma unroll
+        for (int R = 0; R < 4; ++R) b2v[R] = *reinterpret_cast<const float4*>(b2 + 32 * w + 8 * R + 4 * lh);
+        act_to_image<KEEP, NRT>(o, b1v, h1g, m0, h_from, rend, w, li, lh, L.img);
+        __syncthreads();  // image 2 complete
+        stamp(5, first);
+        // ---- layer 3 over image 2; the freed slots take the head's first
+        // steps (no head stream: the next tile's layer 2)
+  #pragma unroll
+        for (int rt = 0; rt < NRT; ++rt)
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
+        {
+          const WMat nm{hs ? Whm.rs : W1m.rs};  // uniform
+          stream256<NRT>(W2m, w1o, nm, hs ? who : w1o, hr, L.img, li, lh, o);
+        }
+        stamp(6, first);
+        __syncthreads();  // every wave done reading image 2
+  #pragma unroll
+        for (int R = 0; R < 4; ++R) b1v[R] = b2v[R];
+      }
+      // the last hidden layer's activations: kept rows, and (no register head)
+      // the image the head streams
+      float* const hlg = NHID == 3 ? h2g : h1g;
+      if constexpr (HD) {
+        // Q head as a register dot: this lane's 16 units of each of its rows
+        float hw[4][4];
+  #pragma unroll
+        for (int R = 0; R < 4; ++R) {
+          const float4 q = *reinterpret_cast<const float4*>(Wh + 32 * w + 8 * R + 4 * lh);
+          hw[R][0] = q.x, hw[R][1] = q.y, hw[R][2] = q.z, hw[R][3] = q.w;
+        }
+  #pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) {
+          const int rl = 32 * rt + li;
+          const int row = m0 + rl;
+          float acc = 0.f;
+  #pragma unroll
+          for (int R = 0; R < 4; ++R) {
+            const int u = 32 * w + 8 * R + 4 * lh;
+            const float bb[4] = {b1v[R].x, b1v[R].y, b1v[R].z, b1v[R].w};
+            float v[4];
+  #pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              v[i] = fmaxf(o[rt][4 * R + i] + bb[i], 0.f);
+              acc = fmaf(v[i], hw[R][i], acc);
+            }
+            if (KEEP && hlg != nullptr && row >= h_from && row < rend)
+              *reinterpret_cast<float4*>(hlg + row * W_H + u) = make_float4(v[0], v[1], v[2], v[3]);
+          }
+          const float other = __shfl_xor(acc, 32, 64);
+          if (lh == 0) L.rs[w][rl] = acc + other;
+        }
+        if (has_next) stage_x(h + 2);  // the input region is free since image 1
+        __syncthreads();  // the eight waves' head partials
+        if (t < 32 * NRT) {
+          float q = L.rs[0][t];
+  #pragma unroll
+          for (int v = 1; v < 8; ++v) q += L.rs[v][t];
+          const int row = m0 + t;
+          if (row < rend) {
+            q += bh[0];
+            outp[(int64_t)row * d.ldout] = q;
+            if (rmean != nullptr) rmean[c * d.s_mean + row] = q;
+          }
+        }
+        stamp(7, first);
+        return;
+      } else {
+      act_to_image<KEEP, NRT>(o, b1v, hlg, m0, h_from, rend, w, li, lh, L.img);
       // head bias of this lane's outputs 32 w + 8 R + 4 lh + i (clamped index)
       float bhv[4][4];
   #pragma unroll
@@ -403,7 +500,7 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
             }
           }
         }
-        if (d.row_mean != nullptr) {
+        if (rmean != nullptr) {
           // the two lane halves hold interleaved runs of four outputs: the wave's
           // 32 outputs of a row as (lane half 0's 16) + (lane half 1's 16)
   #pragma unroll
@@ -413,17 +510,17 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d) {
           }
         }
       }
-      if (d.row_mean != nullptr) {
+      if (rmean != nullptr) {
         __syncthreads();  // uniform: row_mean is a kernel argument
         if (t < W_RB) {
           float s = L.rs[0][t];
           for (int v = 1; v < nkt; ++v) s += L.rs[v][t];
           const int row = m0 + t;
-          if (row < rend) d.row_mean[c * d.s_mean + row] = s / (float)nout;
+          if (row < rend) rmean[c * d.s_mean + row] = s / (float)nout;
         }
       }
       stamp(7, first);
-  
+      }  // (no register head)
   };
   int h = hb;
   for (; h + 1 < he; h += 2) tile(std::integral_constant<int, 2>{}, h);  // uniform
@@ -441,26 +538,34 @@ using namespace d3a;
 extern "C" int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_mlp_fwd_x6: null desc");
   const d3a_mlp_fwd_desc& d = *dp;
-  D3A_CHECK_ARG(d.n_hidden == 2 && d.H == W_H && d.n_out >= 1 && d.n_out <= 256 && d.n_in >= 1 &&
-                    d.n_in <= 64,
-                "d3a_mlp_fwd_x6: needs [n_in <= 64, 256, 256, n_out <= 256]");
-  D3A_CHECK_ARG((d.x || d.xg_mode) && d.out && d.W[0] && d.W[1] && d.W[2] && d.b[0] && d.b[1] &&
-                    d.b[2],
-                "d3a_mlp_fwd_x6: null operand");
+  const int nhid = d.n_hidden;
+  D3A_CHECK_ARG((nhid == 2 || nhid == 3) && d.H == W_H && d.n_out >= 1 && d.n_out <= 256 &&
+                    d.n_in >= 1 && d.n_in <= 64,
+                "d3a_mlp_fwd_x6: needs [n_in <= 64, 256, 256 (, 256), n_out <= 256]");
+  bool ops_ok = (d.x || d.xg_mode) && d.out;
+  for (int l = 0; l <= nhid; ++l) ops_ok = ops_ok && d.W[l] && d.b[l];
+  D3A_CHECK_ARG(ops_ok, "d3a_mlp_fwd_x6: null operand");
   D3A_CHECK_ARG(xgen_ok(d), "d3a_mlp_fwd_x6: bad input-row builder (xg_*)");
   D3A_CHECK_ARG(d.hmask == nullptr, "d3a_mlp_fwd_x6: hmask is d3a_q2_fwd_x6 only");
-  D3A_CHECK_ARG(d.aux_rows == 0 && d.parts <= 1, "d3a_mlp_fwd_x6: no aux pass / parts");
+  D3A_CHECK_ARG(d.parts <= 1, "d3a_mlp_fwd_x6: no parts");
+  D3A_CHECK_ARG(d.aux_rows == 0 || (d.aux_rows > 0 && d.aux_x && d.aux_out && d.xg_mode == 0 &&
+                                    d.row_mean == nullptr && d.aux_rows * d.aux_ldx < (int64_t(1) << 31) &&
+                                    d.aux_rows * (int64_t)d.ldout < (int64_t(1) << 31)),
+                "d3a_mlp_fwd_x6: aux pass needs aux_x / aux_out, no builder, no row_mean");
   D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.r0 >= 0 && d.h_from >= 0, "d3a_mlp_fwd_x6: bad sizes");
   auto a16 = [](const void* p, int64_t stride) {
     return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && stride % 4 == 0;
   };
-  D3A_CHECK_ARG(a16(d.W[1], d.sW[1]) && a16(d.W[2], d.sW[2]) && a16(d.b[0], d.sb[0]) &&
-                    a16(d.b[1], d.sb[1]),
-                "d3a_mlp_fwd_x6: W1, Wh, b0 and b1 must be 16-byte aligned");
-  D3A_CHECK_ARG((d.h[0] == nullptr || (reinterpret_cast<uintptr_t>(d.h[0]) & 15) == 0) &&
-                    (d.h[1] == nullptr || (reinterpret_cast<uintptr_t>(d.h[1]) & 15) == 0) &&
-                    d.sh % 4 == 0,
-                "d3a_mlp_fwd_x6: kept activations must be 16-byte aligned rows of 256");
+  // (the aux pass's parameters sit aux_wdelta floats on: a multiple of 4
+  // keeps them 16-byte aligned)
+  bool al = d.aux_rows == 0 || d.aux_wdelta % 4 == 0;
+  for (int l = 1; l <= nhid; ++l) al = al && a16(d.W[l], d.sW[l]);
+  for (int l = 0; l < nhid; ++l) al = al && a16(d.b[l], d.sb[l]);
+  if (d.n_out == 1) al = al && a16(d.W[nhid], d.sW[nhid]);
+  D3A_CHECK_ARG(al, "d3a_mlp_fwd_x6: hidden W / b and the head's W must be 16-byte aligned");
+  bool hk = d.sh % 4 == 0;
+  for (int l = 0; l < nhid; ++l) hk = hk && (d.h[l] == nullptr || (reinterpret_cast<uintptr_t>(d.h[l]) & 15) == 0);
+  D3A_CHECK_ARG(hk, "d3a_mlp_fwd_x6: kept activations must be 16-byte aligned rows of 256");
   D3A_CHECK_ARG((d.r0 + d.rows) * (int64_t)(d.ldout > W_H ? d.ldout : W_H) < (int64_t(1) << 31) &&
                     (d.r0 + d.rows) * d.ldx < (int64_t(1) << 31),
                 "d3a_mlp_fwd_x6: rows x row stride exceeds 2^31");
@@ -468,8 +573,9 @@ extern "C" int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(d.row_mean == nullptr || (d.s_mean >= d.r0 + d.rows &&
                                           d.s_mean * (int64_t)d.C < (int64_t(1) << 31)),
                 "d3a_mlp_fwd_x6: row_mean member stride must cover the rows");
-  if (d.rows == 0) return 0;
-  // persistent: one workgroup per CU, the CUs shared between the members
+  if (d.rows == 0 && d.aux_rows == 0) return 0;
+  // persistent: one workgroup per CU, the CUs shared between the members and
+  // (aux pass) between the passes in proportion to their rows
   static const int n_cu = [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -477,25 +583,50 @@ extern "C" int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
       n = 256;
     return n;
   }();
-  const int64_t halves = (d.rows + 31) / 32;
-  const int64_t g = std::min<int64_t>(std::max(1, n_cu / d.C), (halves + 1) / 2);
-  const dim3 grid((unsigned)g, 1, (unsigned)d.C);
+  const int64_t halves = (d.rows + 31) / 32, ahalves = (d.aux_rows + 31) / 32;
+  int64_t ga = 0;
+  if (ahalves > 0)
+    ga = std::min<int64_t>((ahalves + 1) / 2,
+                           std::max<int64_t>(1, n_cu * ahalves / ((halves + ahalves) * d.C)));
+  const int64_t gm = halves > 0 ? std::min<int64_t>(std::max<int64_t>(1, (n_cu - d.C * ga) / d.C),
+                                                    (halves + 1) / 2)
+                                : 1;
+  const dim3 grid((unsigned)(d.C * (gm + ga)));
+  const int Gm = (int)gm, Ga = (int)std::max<int64_t>(ga, 1);
   const hipStream_t st = (hipStream_t)stream;
   static const bool stamps = [] {
     const char* e = getenv("D3A_WIDE_STAMPS");
     return e && atoi(e) != 0;
   }();
-  const bool keep = d.h[0] != nullptr || d.h[1] != nullptr;
-  if (stamps && d.n_in <= 32 && !keep)
-    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false, true>), grid, dim3(512), 0, st, d);
-  else if (d.n_in <= 32 && keep)
-    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, true>), grid, dim3(512), 0, st, d);
-  else if (d.n_in <= 32)
-    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false>), grid, dim3(512), 0, st, d);
-  else if (keep)
-    hipLaunchKernelGGL((mlp_x6_wide_kernel<64, true>), grid, dim3(512), 0, st, d);
-  else
-    hipLaunchKernelGGL((mlp_x6_wide_kernel<64, false>), grid, dim3(512), 0, st, d);
+  bool keep = false;
+  for (int l = 0; l < nhid; ++l) keep = keep || d.h[l] != nullptr;
+  const bool x32 = d.n_in <= 32;
+  if (nhid == 3) {
+    // the CQL reproduction critic: Q head (register dot) or a wide head
+    if (d.n_out == 1) {
+      if (stamps && x32 && keep)
+        hipLaunchKernelGGL((mlp_x6_wide_kernel<32, true, true, 3, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+      else if (x32 && keep) hipLaunchKernelGGL((mlp_x6_wide_kernel<32, true, false, 3, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+      else if (x32) hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false, false, 3, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+      else if (keep) hipLaunchKernelGGL((mlp_x6_wide_kernel<64, true, false, 3, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+      else hipLaunchKernelGGL((mlp_x6_wide_kernel<64, false, false, 3, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+    } else {
+      if (x32 && keep) hipLaunchKernelGGL((mlp_x6_wide_kernel<32, true, false, 3>), grid, dim3(512), 0, st, d, Gm, Ga);
+      else if (x32) hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false, false, 3>), grid, dim3(512), 0, st, d, Gm, Ga);
+      else if (keep) hipLaunchKernelGGL((mlp_x6_wide_kernel<64, true, false, 3>), grid, dim3(512), 0, st, d, Gm, Ga);
+      else hipLaunchKernelGGL((mlp_x6_wide_kernel<64, false, false, 3>), grid, dim3(512), 0, st, d, Gm, Ga);
+    }
+  } else if (stamps && x32 && !keep) {
+    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+  } else if (x32 && keep) {
+    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+  } else if (x32) {
+    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false>), grid, dim3(512), 0, st, d, Gm, Ga);
+  } else if (keep) {
+    hipLaunchKernelGGL((mlp_x6_wide_kernel<64, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+  } else {
+    hipLaunchKernelGGL((mlp_x6_wide_kernel<64, false>), grid, dim3(512), 0, st, d, Gm, Ga);
+  }
   D3A_LAUNCH_CHECK("d3a_mlp_fwd_x6");
   return 0;
 }

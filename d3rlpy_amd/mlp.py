@@ -234,6 +234,16 @@ def x6_deep_shape(net: EnsembleMLP) -> bool:
 # the reproduction config, 60.7 + 21.6 us against 56.5 us, round 5)
 _X6_DEEP = os.environ.get("D3A_X6_DEEP", "1") == "1"
 _X6_DEEP_FWD = os.environ.get("D3A_X6_DEEP_FWD", "0") == "1"
+# the three-hidden-layer critic's forward (+ its target aux pass) in one
+# d3a_mlp_fwd_x6 launch (round 6; D3A_X6_DEEP3=0: the fp32 fused kernel)
+_X6_DEEP3 = os.environ.get("D3A_X6_DEEP3", "1") == "1"
+
+
+def x6_deep3_shape(net: EnsembleMLP) -> bool:
+    """[n_in <= 64, 256, 256, 256, n_out <= 256]: d3a_mlp_fwd_x6's three-layer
+    instantiation (the CQL reproduction critic)."""
+    s = net.sizes
+    return net.n_layers == 4 and s[1] == s[2] == s[3] == 256 and s[0] <= 64 and 1 <= s[4] <= 256
 
 
 def x6_wide_shape(net: EnsembleMLP) -> bool:
@@ -421,6 +431,9 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         elif (not bf16 and not small and ops.CRITIC_GEMM == "x6" and x6_wide_shape(net)
               and out_parts is None and not d.aux_rows and n * C >= 8192):
             entry = "d3a_mlp_fwd_x6"  # wide head (e.g. BCQ's target QR critics)
+        elif big and _X6_DEEP3 and ops.CRITIC_GEMM == "x6" and x6_deep3_shape(net) \
+                and members is None and (xgen is None or not d.aux_rows):
+            entry = "d3a_mlp_fwd_x6"  # three hidden layers (+ the aux pass, same launch)
         if xgen is not None:
             # the builder rides in the x6 forwards and the small-pass ones
             # (block_rows 16); a builder with a side output (e_out) keeps its

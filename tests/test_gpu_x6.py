@@ -597,3 +597,101 @@ def test_parts_forward_writes_its_built_rows(mode, a_parts):
     assert torch.equal(o0, o1)
     assert torch.equal(x0, x1)
     assert torch.equal(e0, e1)
+
+
+@pytest.mark.parametrize("rows,n_in,n_out,h_from,aux,C", [
+    (7936, 14, 1, 7680, 256, 2),   # the CQL reproduction critic pass (+ target rows)
+    (1000, 23, 1, 0, 77, 2), (333, 64, 1, 100, 0, 1), (515, 17, 40, 0, 33, 2)])
+def test_mlp_fwd_x6_three_hidden_vs_fp64(rows, n_in, n_out, h_from, aux, C):
+    """d3a_mlp_fwd_x6 with three hidden layers ([n_in, 256, 256, 256, n_out]:
+    reproductions/offline/cql.py:21-37's critic), the Q head as a register
+    dot (n_out 1) or a head stream, and the target aux pass in the same launch:
+    per layer against fp64 relative to the layer's rounding scale on the
+    kernel's own inputs, end to end, kept rows only from h_from, aux outputs
+    against fp64 through the target parameters, run to run bit-identical."""
+    dev = torch.device("cuda")
+    gen = torch.Generator().manual_seed(rows + n_out + aux)
+    sizes = [n_in, 256, 256, 256, n_out]
+    L = 4
+
+    def net():
+        Ws = [(torch.randn(C, sizes[l + 1], sizes[l], generator=gen) / np.sqrt(sizes[l])).to(dev)
+              for l in range(L)]
+        bs = [(torch.randn(C, sizes[l + 1], generator=gen) * 0.1).to(dev) for l in range(L)]
+        return Ws, bs
+    (Ws, bs), (Wt, bt) = net(), net()
+    offs, o = [], 0
+    for W in Ws:
+        o = (o + 3) // 4 * 4
+        offs.append(o)
+        o += W.numel()
+    boffs = []
+    for b in bs:
+        o = (o + 3) // 4 * 4
+        boffs.append(o)
+        o += b.numel()
+    n1 = (o + 63) // 64 * 64
+    buf = torch.zeros(2 * n1, device=dev)
+    for base, (Wl, bl) in ((0, (Ws, bs)), (n1, (Wt, bt))):
+        for W, of in zip(Wl, offs):
+            buf[base + of: base + of + W.numel()] = W.reshape(-1)
+        for b, of in zip(bl, boffs):
+            buf[base + of: base + of + b.numel()] = b.reshape(-1)
+    ldx = (n_in + 3) // 4 * 4
+    x = torch.randn(rows, ldx, generator=gen).to(dev)
+    xa = torch.randn(max(aux, 1), ldx, generator=gen).to(dev)
+    h = [torch.full((C, rows, 256), float("nan"), device=dev) for _ in range(3)]
+    out = torch.full((C, rows, n_out), float("nan"), device=dev)
+    aout = torch.full((C, max(aux, 1), n_out), float("nan"), device=dev)
+    d = N.MlpFwdDesc()
+    d.x, d.ldx, d.sxb = x.data_ptr(), ldx, 0
+    d.n_in, d.n_hidden, d.H, d.n_out = n_in, 3, 256, n_out
+    for l in range(L):
+        d.W[l], d.b[l] = buf.data_ptr() + 4 * offs[l], buf.data_ptr() + 4 * boffs[l]
+        d.sW[l], d.sb[l] = sizes[l + 1] * sizes[l], sizes[l + 1]
+    for l in range(3):
+        d.h[l] = h[l].data_ptr()
+    d.sh = rows * 256
+    d.out, d.sout, d.ldout = out.data_ptr(), rows * n_out, n_out
+    d.r0, d.rows, d.C, d.h_from = 0, rows, C, h_from
+    if aux:
+        d.aux_x, d.aux_ldx, d.aux_sxb, d.aux_wdelta = xa.data_ptr(), ldx, 0, n1
+        d.aux_out, d.aux_sout, d.aux_rows = aout.data_ptr(), aux * n_out, aux
+    ops.call_desc("d3a_mlp_fwd_x6", d)
+    torch.cuda.synchronize()
+    assert not torch.isnan(out).any()
+    for l in range(3):
+        assert torch.isnan(h[l][:, :h_from]).all()
+    # per layer on the kernel's own inputs
+    a = x[:, :n_in].double()[h_from:]
+    errs = []
+    for l in range(L):
+        W, b = Ws[l].double(), bs[l].double().unsqueeze(1)
+        z = a @ W.transpose(-1, -2) + b
+        sz = a.abs() @ W.abs().transpose(-1, -2) + b.abs()
+        got = (h[l][:, h_from:] if l < 3 else out[:, h_from:]).double()
+        if l < 3:
+            z = z.clamp_min(0)
+        errs.append(float(((got - z).abs() / sz).max()))
+        a = got
+    print(f"x6 three-layer forward vs fp64 (rounding scale): {['%.1e' % e for e in errs]}")
+    assert max(errs) < SCALE_BAR, errs
+
+    def fwd64(xx, Wl, bl):
+        a = xx.double()
+        for l in range(L):
+            a = a @ Wl[l].double().transpose(-1, -2) + bl[l].double().unsqueeze(1)
+            if l < 3:
+                a = a.clamp_min(0)
+        return a
+    q = fwd64(x[:, :n_in], Ws, bs)
+    rel = float((out.double() - q).abs().max() / q.abs().max())
+    assert rel < 1e-5, rel
+    if aux:
+        qa = fwd64(xa[:aux, :n_in], Wt, bt)
+        rela = float((aout[:, :aux].double() - qa).abs().max() / qa.abs().max())
+        assert rela < 1e-5, rela
+    o1, a1 = out.clone(), aout.clone()
+    ops.call_desc("d3a_mlp_fwd_x6", d)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, out) and (not aux or torch.equal(a1, aout))
