@@ -595,6 +595,7 @@ _SIGNATURES = {
     "d3a_x6_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_bwd_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_wide_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
+    "d3a_wide_wave_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_small_bwd_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_td3_prep": (C.c_int, [C.POINTER(Td3PrepDesc), vp]),
     "d3a_td3_target": (C.c_int, [C.POINTER(Td3TargetDesc), vp]),

@@ -478,6 +478,10 @@ class _Workspace:
         # their own, and no per-workgroup split in the forward
         self.wimg = (mlp.WeightImages(impl.critic, (impl.store, impl.targ), dev)
                      if mlp.presplit_ok(impl.critic) and not bf16 else None)
+        # (the three-hidden-layer critic: its 256 x 256 stream matrices W1 / W2)
+        if (self.wimg is None and not bf16 and mlp._X6_DEEP3 and mlp.x6_deep3_shape(impl.critic)
+                and mlp.wide_presplit_ok(impl.critic)):
+            self.wimg = mlp.WeightImages(impl.critic, (impl.store, impl.targ), dev, streams=True)
         self.dq = z(C, self.R)
         self.lse = z(2, C, B)
         # (loss stage in the critic backward) squared TD errors, the Adam bias
@@ -724,7 +728,8 @@ class _Workspace:
             elif (mlp.x6_deep3_shape(net) and mlp._X6_DEEP3 and ops.CRITIC_GEMM == "x6"
                   and (R - r0 + B) * C >= 8192):
                 # the three-hidden-layer critic on d3a_mlp_fwd_x6 (register Q head)
-                gemm = "split-bf16 x6, three hidden layers"
+                gemm = ("split-bf16 x6, three hidden layers, pre-split W images"
+                        if self.wimg is not None else "split-bf16 x6, three hidden layers")
             return launch, flops, (f"d3a_mlp_fwd critic ensemble ({gemm} MFMA): C={C} x "
                                    f"({R - r0} + {B} target) rows x {'-'.join(map(str, s))}")
         H, Hin = s[2], s[1]

@@ -67,6 +67,8 @@ struct WideLds {
 // minus its start (the workgroup's whole lifetime)
 constexpr int W_NST = 9;
 __device__ unsigned long long wide_stamps[1024 * W_NST];
+// (three hidden layers) every wave's stamps: [workgroup < 512][wave][8]
+__device__ unsigned long long wide_wstamps[512 * 8 * 8];
 
 // a weight matrix as a buffer resource: raw buffer loads are ordered by the
 // compiler fences below (plain loads of read-only weights are free to sink to
@@ -152,6 +154,60 @@ __device__ __forceinline__ void stream256(const WMat& wm, int wo, const WMat& nm
   }
 }
 
+// PW: the weights as pre-split operand images (d3a_x6_split's layout: a row
+// of 256 k is 32 blocks of [3 parts][8 bf16], 1536 bytes; the lane's k = 8 lh
+// block at byte wo, step s at + 96 s): the ring holds each step's three parts
+// and the MFMAs read them in place -- no split instructions between the
+// MFMAs (with two waves a SIMD, a wave's vector instructions delay the other
+// wave's products nearly one for one: tools/bench_wide3.py's wave stamps)
+template <bool PW> struct WRing;
+template <> struct WRing<false> { float4 r[W_HD][2]; };
+template <> struct WRing<true> { bf16x8 r[W_HD][3]; };
+
+__device__ __forceinline__ bf16x8 pload(const WMat& m, int lane_off, int step_off) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  return __builtin_bit_cast(bf16x8, __builtin_bit_cast(s16x8, __builtin_amdgcn_raw_buffer_load_b128(m.rs, lane_off, step_off, 0)));
+}
+
+template <int NRT>
+__device__ __forceinline__ void stream256p(const WMat& wm, int wo, const WMat& nm, int no,
+                                           WRing<true>& hq, const __bf16 (&img)[W_RB * 3 * W_LDH],
+                                           int li, int lh, f32x16 (&o)[NRT]) {
+  constexpr int NS = W_H / 16;
+  auto refill = [&](int s) {  // the slot of step s, with step s + W_HD
+    const int sl = s % W_HD, s2 = s + W_HD;
+    const WMat& m = s2 < NS ? wm : nm;
+    const int lo = s2 < NS ? wo : no, st = 96 * (s2 < NS ? s2 : s2 - NS);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) hq.r[sl][q] = pload(m, lo, st + 16 * q);
+  };
+  auto read_img = [&](int s, bf16x8 (&bp)[NRT][3]) {
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        bp[rt][q] = *reinterpret_cast<const bf16x8*>(&img[((32 * rt + li) * 3 + q) * W_LDH + 16 * s + 8 * lh]);
+  };
+  bf16x8 bp[2][NRT][3];
+  read_img(0, bp[0]);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int cur = s & 1, nx = cur ^ 1;
+    if (s + 1 < NS) read_img(s + 1, bp[nx]);
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt) o[rt] = prod6(hq.r[s % W_HD], bp[cur][rt], o[rt]);
+    refill(s);  // (after the products that read the slot)
+    if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x0100, 3 * NRT, 0);  // next step's image reads
+#pragma unroll
+    for (int m = 0; m < 6 * NRT; ++m) __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x0020, 3, 0);  // the refill
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // bias, ReLU, kept rows to hg, parts into the image: lane holds rows
 // 32 rt + li, units 32 w + 8 R + 4 lh + i
 template <bool KEEP, int NRT>
@@ -202,7 +258,7 @@ __device__ __forceinline__ void act_to_image(const f32x16 (&o)[NRT], const float
 // and head, the next tile's input rows and first weight steps are in flight
 // (XRaw4 registers, the freed slots of the weight stream), so only the first
 // tile pays the prologue's memory round trip.
-template <int XL, bool KEEP, bool STAMPS = false, int NHID = 2, bool HD = false>
+template <int XL, bool KEEP, bool STAMPS = false, int NHID = 2, bool HD = false, bool PW = false>
 __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, int Gm, int Ga) {
   constexpr int XLD = XL + 8;
   constexpr int NS1 = XL / 16;  // layer-1 k steps
@@ -233,9 +289,16 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, in
   float* const rmean = aux ? nullptr : d.row_mean;
   const int u0 = 32 * w + li;  // this lane's weight row in the hidden layers
   const float* W0r = d.W[0] + wdel + c * d.sW[0] + u0 * nin;
-  const WMat W1m = wmat(d.W[1] + wdel + c * d.sW[1], W_H * W_H * 4);
-  const WMat W2m = wmat(d.W[NHID == 3 ? 2 : 1] + wdel + c * d.sW[NHID == 3 ? 2 : 1], W_H * W_H * 4);
-  const int w1o = (u0 * W_H + 8 * lh) * 4;  // byte offset of this lane's W1 row piece
+  // (PW: the stream matrices' images, wp[0] = W[1]'s and wp[1] = W[2]'s --
+  // layer 3's, or the wide head's)
+  const char* const wpi0 = PW ? static_cast<const char*>(aux ? d.aux_wp[0] : d.wp[0]) : nullptr;
+  const char* const wpi1 = PW ? static_cast<const char*>(aux ? d.aux_wp[1] : d.wp[1]) : nullptr;
+  const WMat W1m = PW ? wmat(wpi0 + (int64_t)c * W_H * 1536, W_H * 1536)
+                      : wmat(d.W[1] + wdel + c * d.sW[1], W_H * W_H * 4);
+  const WMat W2m = PW ? wmat(wpi1 + (int64_t)c * W_H * 1536, W_H * 1536)
+                      : wmat(d.W[NHID == 3 ? 2 : 1] + wdel + c * d.sW[NHID == 3 ? 2 : 1], W_H * W_H * 4);
+  // byte offset of this lane's W1 row piece (k = 8 lh)
+  const int w1o = PW ? u0 * 1536 + lh * 48 : (u0 * W_H + 8 * lh) * 4;
   const float* b0 = d.b[0] + wdel + c * d.sb[0];
   const float* b1 = d.b[1] + wdel + c * d.sb[1];
   const float* b2 = d.b[NHID == 3 ? 2 : 1] + wdel + c * d.sb[NHID == 3 ? 2 : 1];
@@ -245,14 +308,27 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, in
   const int64_t ldx = aux ? d.aux_ldx : d.ldx;
   const int nkt = (nout + 31) / 32;
   const int kout = 32 * w + li;  // head: this lane's output row (rows past n_out read row 0:
-  const WMat Whm = wmat(Wh, nout * W_H * 4);
-  const int who = ((kout < nout ? kout : 0) * W_H + 8 * lh) * 4;  // never stored)
+  const WMat Whm = PW && NHID == 2 ? wmat(wpi1 + (int64_t)c * nout * 1536, nout * 1536)
+                                   : wmat(Wh, nout * W_H * 4);
+  const int who = PW && NHID == 2 ? (kout < nout ? kout : 0) * 1536 + lh * 48
+                                  : ((kout < nout ? kout : 0) * W_H + 8 * lh) * 4;  // never stored)
   const int wgi = bid;
   const unsigned long long t_start = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
   auto stamp = [&](int s, bool on) {
     if constexpr (STAMPS) {
       __builtin_amdgcn_sched_barrier(0);
       if (on && t == 0 && wgi < 1024) wide_stamps[wgi * W_NST + s] = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // (three hidden layers) every wave: 0 tile start, 1 image 1 written, 2 layer
+  // 2 issued, 3 past the barrier after it, 4 image 2 formed, 5 image 2
+  // written, 6 layer 3 issued, 7 head written
+  auto wstamp = [&](int s, bool on) {
+    if constexpr (STAMPS && NHID == 3) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (on && lane == 0 && wgi < 512) wide_wstamps[(wgi * 8 + w) * 8 + s] = __builtin_amdgcn_s_memtime();
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -296,12 +372,25 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, in
   };
 
   // ---- prologue: layer-2 weight steps 0 .. w_hd - 1 and the first tile's rows
-  float4 hr[W_HD][2];
+  WRing<PW> ring;
 #pragma unroll
   for (int s = 0; s < W_HD; ++s) {
-    hr[s][0] = wload(W1m, w1o, 64 * s);
-    hr[s][1] = wload(W1m, w1o, 64 * s + 16);
+    if constexpr (PW) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) ring.r[s][q] = pload(W1m, w1o, 96 * s + 16 * q);
+    } else {
+      ring.r[s][0] = wload(W1m, w1o, 64 * s);
+      ring.r[s][1] = wload(W1m, w1o, 64 * s + 16);
+    }
   }
+  // one stream over the image: weights wm (this lane at byte wo), the next
+  // stream's first steps from nm at no into the freed slots
+  auto stream = [&](auto nrt, const WMat& wm, int wo, const WMat& nm, int no,
+                    f32x16 (&oo)[decltype(nrt)::value]) {
+    constexpr int NRT_ = decltype(nrt)::value;
+    if constexpr (PW) stream256p<NRT_>(wm, wo, nm, no, ring, L.img, li, lh, oo);
+    else stream256<NRT_>(wm, wo, nm, no, ring.r, L.img, li, lh, oo);
+  };
   issue_x(hb);
   stage_x(hb);
 
@@ -314,6 +403,7 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, in
       // the stamped tile: the second (the steady state), or a workgroup's only one
       const bool first = h == hb + 2 || he - hb <= 2;
       stamp(0, first);
+      wstamp(0, first);
       // the layer-1 weight row (clamped k, masked at use) and bias, reloaded per
       // tile (L2 hits) so that no register holds them across the streams; a
       // wave reaching this point early waits at the barrier anyway
@@ -359,6 +449,7 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, in
       act_to_image<KEEP, NRT>(o, b0v, h0g, m0, h_from, rend, w, li, lh, L.img);
       __syncthreads();  // image 1 complete; every wave done reading the input parts
       stamp(3, first);
+      wstamp(1, first);
       if (has_next) issue_x(h + 2);  // uniform
 
       // ---- layer 2: units 32 w .. over the image; the freed weight slots take
@@ -371,20 +462,27 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, in
       // (waves streaming a head after the last hidden layer; HD: none)
       const bool hs = !HD && w < nkt;
       if constexpr (NHID == 3) {
-        stream256<NRT>(W1m, w1o, W2m, w1o, hr, L.img, li, lh, o);
+        stream(std::integral_constant<int, NRT>{}, W1m, w1o, W2m, w1o, o);
       } else {
         const WMat nm{hs ? Whm.rs : W1m.rs};  // uniform
-        stream256<NRT>(W1m, w1o, nm, hs ? who : w1o, hr, L.img, li, lh, o);
+        stream(std::integral_constant<int, NRT>{}, W1m, w1o, nm, hs ? who : w1o, o);
       }
       stamp(4, first);
-      __syncthreads();  // every wave done reading image 1
+      wstamp(2, first);
       if constexpr (NHID == 3) {
         float4 b2v[4];
   #pragma unroll
         for (int R = 0; R < 4; ++R) b2v[R] = *reinterpret_cast<const float4*>(b2 + 32 * w + 8 * R + 4 * lh);
+        // (measured: forming the parts before this barrier, so that an early
+        // wave splits while its SIMD's other wave multiplies, slowed that
+        // wave's stream by as much -- 37.3 against 37.4 us)
+        __syncthreads();  // every wave done reading image 1
+        wstamp(3, first);
         act_to_image<KEEP, NRT>(o, b1v, h1g, m0, h_from, rend, w, li, lh, L.img);
+        wstamp(4, first);
         __syncthreads();  // image 2 complete
         stamp(5, first);
+        wstamp(5, first);
         // ---- layer 3 over image 2; the freed slots take the head's first
         // steps (no head stream: the next tile's layer 2)
   #pragma unroll
@@ -393,12 +491,17 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, in
           for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
         {
           const WMat nm{hs ? Whm.rs : W1m.rs};  // uniform
-          stream256<NRT>(W2m, w1o, nm, hs ? who : w1o, hr, L.img, li, lh, o);
+          stream(std::integral_constant<int, NRT>{}, W2m, w1o, nm, hs ? who : w1o, o);
         }
         stamp(6, first);
-        __syncthreads();  // every wave done reading image 2
+        wstamp(6, first);
+        // (the register head writes no image: no barrier; a wave that is
+        // done forms its head partials while the others still multiply)
+        if constexpr (!HD) __syncthreads();  // every wave done reading image 2
   #pragma unroll
         for (int R = 0; R < 4; ++R) b1v[R] = b2v[R];
+      } else {
+        __syncthreads();  // every wave done reading image 1
       }
       // the last hidden layer's activations: kept rows, and (no register head)
       // the image the head streams
@@ -446,6 +549,7 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, in
           }
         }
         stamp(7, first);
+        wstamp(7, first);
         return;
       } else {
       act_to_image<KEEP, NRT>(o, b1v, hlg, m0, h_from, rend, w, li, lh, L.img);
@@ -466,7 +570,7 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, in
         for (int rt = 0; rt < NRT; ++rt)
   #pragma unroll
           for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
-        stream256<NRT>(Whm, who, W1m, w1o, hr, L.img, li, lh, o);
+        stream(std::integral_constant<int, NRT>{}, Whm, who, W1m, w1o, o);
         stamp(6, first);
         // lane: row 32 rt + li, outputs 32 w + 8 R + 4 lh + i
         const int64_t ldo = d.ldout;
@@ -601,33 +705,65 @@ extern "C" int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* dp, void* stream) {
   bool keep = false;
   for (int l = 0; l < nhid; ++l) keep = keep || d.h[l] != nullptr;
   const bool x32 = d.n_in <= 32;
+  // pre-split stream images (n_in <= 32; the three-layer Q-head form or the
+  // two-layer wide head: wp[0] = W[1]'s image, wp[1] = W[2]'s)
+  const bool pw = d.wp[0] != nullptr;
+  if (pw) {
+    D3A_CHECK_ARG(x32 && d.wp[1] && ((nhid == 3 && d.n_out == 1) || (nhid == 2 && d.n_out > 1)),
+                  "d3a_mlp_fwd_x6: stream images need n_in <= 32 and [.., 256, 256, 256, 1] or "
+                  "[.., 256, 256, n_out > 1], wp[0] and wp[1]");
+    D3A_CHECK_ARG(d.aux_rows == 0 || (d.aux_wp[0] && d.aux_wp[1]), "d3a_mlp_fwd_x6: aux pass needs aux_wp");
+    bool al = true;
+    for (int i = 0; i < 2; ++i)
+      al = al && (reinterpret_cast<uintptr_t>(d.wp[i]) & 15) == 0 &&
+           (reinterpret_cast<uintptr_t>(d.aux_wp[i]) & 15) == 0;
+    D3A_CHECK_ARG(al, "d3a_mlp_fwd_x6: stream images must be 16-byte aligned");
+  }
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(512), 0, st, d, Gm, Ga); };
   if (nhid == 3) {
     // the CQL reproduction critic: Q head (register dot) or a wide head
     if (d.n_out == 1) {
-      if (stamps && x32 && keep)
-        hipLaunchKernelGGL((mlp_x6_wide_kernel<32, true, true, 3, true>), grid, dim3(512), 0, st, d, Gm, Ga);
-      else if (x32 && keep) hipLaunchKernelGGL((mlp_x6_wide_kernel<32, true, false, 3, true>), grid, dim3(512), 0, st, d, Gm, Ga);
-      else if (x32) hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false, false, 3, true>), grid, dim3(512), 0, st, d, Gm, Ga);
-      else if (keep) hipLaunchKernelGGL((mlp_x6_wide_kernel<64, true, false, 3, true>), grid, dim3(512), 0, st, d, Gm, Ga);
-      else hipLaunchKernelGGL((mlp_x6_wide_kernel<64, false, false, 3, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+      if (pw && stamps && keep) go(mlp_x6_wide_kernel<32, true, true, 3, true, true>);
+      else if (pw && keep) go(mlp_x6_wide_kernel<32, true, false, 3, true, true>);
+      else if (pw) go(mlp_x6_wide_kernel<32, false, false, 3, true, true>);
+      else if (stamps && x32 && keep) go(mlp_x6_wide_kernel<32, true, true, 3, true>);
+      else if (x32 && keep) go(mlp_x6_wide_kernel<32, true, false, 3, true>);
+      else if (x32) go(mlp_x6_wide_kernel<32, false, false, 3, true>);
+      else if (keep) go(mlp_x6_wide_kernel<64, true, false, 3, true>);
+      else go(mlp_x6_wide_kernel<64, false, false, 3, true>);
     } else {
-      if (x32 && keep) hipLaunchKernelGGL((mlp_x6_wide_kernel<32, true, false, 3>), grid, dim3(512), 0, st, d, Gm, Ga);
-      else if (x32) hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false, false, 3>), grid, dim3(512), 0, st, d, Gm, Ga);
-      else if (keep) hipLaunchKernelGGL((mlp_x6_wide_kernel<64, true, false, 3>), grid, dim3(512), 0, st, d, Gm, Ga);
-      else hipLaunchKernelGGL((mlp_x6_wide_kernel<64, false, false, 3>), grid, dim3(512), 0, st, d, Gm, Ga);
+      if (x32 && keep) go(mlp_x6_wide_kernel<32, true, false, 3>);
+      else if (x32) go(mlp_x6_wide_kernel<32, false, false, 3>);
+      else if (keep) go(mlp_x6_wide_kernel<64, true, false, 3>);
+      else go(mlp_x6_wide_kernel<64, false, false, 3>);
     }
+  } else if (pw) {
+    if (keep) go(mlp_x6_wide_kernel<32, true, false, 2, false, true>);
+    else go(mlp_x6_wide_kernel<32, false, false, 2, false, true>);
   } else if (stamps && x32 && !keep) {
-    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+    go(mlp_x6_wide_kernel<32, false, true>);
   } else if (x32 && keep) {
-    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+    go(mlp_x6_wide_kernel<32, true>);
   } else if (x32) {
-    hipLaunchKernelGGL((mlp_x6_wide_kernel<32, false>), grid, dim3(512), 0, st, d, Gm, Ga);
+    go(mlp_x6_wide_kernel<32, false>);
   } else if (keep) {
-    hipLaunchKernelGGL((mlp_x6_wide_kernel<64, true>), grid, dim3(512), 0, st, d, Gm, Ga);
+    go(mlp_x6_wide_kernel<64, true>);
   } else {
-    hipLaunchKernelGGL((mlp_x6_wide_kernel<64, false>), grid, dim3(512), 0, st, d, Gm, Ga);
+    go(mlp_x6_wide_kernel<64, false>);
   }
   D3A_LAUNCH_CHECK("d3a_mlp_fwd_x6");
+  return 0;
+}
+
+// diagnostic (synchronous): every wave's stamps of the last three-layer
+// D3A_WIDE_STAMPS=1 launch, [workgroup < 512][wave][8]
+extern "C" int d3a_wide_wave_stamps(unsigned long long* dst, int n) {
+  D3A_CHECK_ARG(dst && n >= 0 && n <= 512 * 64, "d3a_wide_wave_stamps: bad arguments");
+  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(d3a::wide_wstamps), (size_t)n * 8, 0,
+                          hipMemcpyDeviceToHost) != hipSuccess) {
+    set_error("d3a_wide_wave_stamps: copy failed");
+    return -1;
+  }
   return 0;
 }
 

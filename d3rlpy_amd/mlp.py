@@ -182,33 +182,53 @@ def presplit_ok(net: EnsembleMLP) -> bool:
             and ops.CRITIC_PRECISION not in ("bf16", "bf16h"))
 
 
-class WeightImages:
-    """Split-bf16 operand images (d3a_x6_split's layout) of a q2 critic's W0
-    and W1, one pair per parameter store (e.g. the online critics and their
-    targets): ``jobs()`` is the d3a_x6_split descriptor that forms them from
-    the stores' current weights, ``wparts(i, j)`` the (W0, W1) images of stores
-    i (main pass) and j (aux pass) for ``forward(..., wparts=...)``.  The
-    images are valid only after the jobs ran on the weights the forward
-    reads."""
+# d3a_mlp_fwd_x6 streaming pre-split images (D3A_X6_WIDE_PRESPLIT=1): off --
+# measured slower at the reproduction config (forward 40.5 against 34.9 us in
+# the step: the three 16-byte part loads a k step, three steps ahead, leave the
+# products waiting on L2 where the fp32 words' split filled the gaps)
+_WIDE_PRESPLIT = os.environ.get("D3A_X6_WIDE_PRESPLIT", "0") == "1"
 
-    def __init__(self, net: EnsembleMLP, stores, device):
-        assert presplit_ok(net)
+
+def wide_presplit_ok(net: EnsembleMLP) -> bool:
+    """d3a_mlp_fwd_x6's pre-split stream images apply: n_in <= 32 and
+    [.., 256, 256, 256, 1] or [.., 256, 256, 1 < n_out <= 256] (x6 GEMMs)."""
+    s = net.sizes
+    return (_PRESPLIT and _WIDE_PRESPLIT and ops.CRITIC_GEMM == "x6" and ops.CRITIC_PRECISION not in ("bf16", "bf16h")
+            and s[0] <= 32 and ((x6_deep3_shape(net) and s[-1] == 1) or x6_wide_shape(net)))
+
+
+class WeightImages:
+    """Split-bf16 operand images (d3a_x6_split's layout) of two of a critic's
+    weight matrices, one pair per parameter store (e.g. the online critics
+    and their targets): a q2 critic's W0 and W1 (the pre-split x6 Q forward),
+    or the 256-wide stream matrices of d3a_mlp_fwd_x6 -- W1 and W2 of a
+    three-hidden-layer critic, W1 and the wide head of a two-layer one
+    (``streams``).  ``jobs()`` is the d3a_x6_split descriptor that forms them
+    from the stores' current weights, ``wparts(i, j)`` the images of stores i
+    (main pass) and j (aux pass) for ``forward(..., wparts=...)``.  The images
+    are valid only after the jobs ran on the weights the forward reads."""
+
+    def __init__(self, net: EnsembleMLP, stores, device, streams: bool = False):
+        assert wide_presplit_ok(net) if streams else presplit_ok(net)
         self.net = net
-        self.xl = (net.sizes[0] + 15) // 16 * 16
-        C, H = net.C, net.sizes[1]
-        self.imgs = [(st, torch.zeros(C * H * self.xl * 3, dtype=torch.bfloat16, device=device),
-                      torch.zeros(C * H * net.sizes[2] * 3, dtype=torch.bfloat16, device=device))
+        self.layers = (1, 2) if streams else (0, 1)
+        self.kpad = [(net.sizes[l] + 15) // 16 * 16 for l in self.layers]
+        self.xl = (net.sizes[0] + 15) // 16 * 16  # (W0's padded k)
+        C = net.C
+        self.imgs = [(st,) + tuple(torch.zeros(C * net.sizes[l + 1] * kp * 3, dtype=torch.bfloat16,
+                                               device=device)
+                                   for l, kp in zip(self.layers, self.kpad))
                      for st in stores]
 
     def jobs(self) -> "N.X6SplitDesc":
         net, C = self.net, self.net.C
         d = N.X6SplitDesc()
         i = 0
-        for st, w0, w1 in self.imgs:
-            for l, img, k, kpad in ((0, w0, net.sizes[0], self.xl), (1, w1, net.sizes[1], net.sizes[1])):
+        for st, ia, ib in self.imgs:
+            for l, img, kpad in zip(self.layers, (ia, ib), self.kpad):
                 j = d.job[i]
                 j.src, j.dst = net.W(l, st), img.data_ptr()
-                j.rows, j.k, j.kpad = C * net.sizes[l + 1], k, kpad
+                j.rows, j.k, j.kpad = C * net.sizes[l + 1], net.sizes[l], kpad
                 i += 1
         d.n_jobs = i
         return d
@@ -471,6 +491,12 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
         if (wparts is not None and entry == "d3a_q2_fwd_x6" and presplit_ok(net)
                 and members is None and d.xg_mode == 0):
             d.wp[0], d.wp[1] = wparts[0], wparts[1]
+            if d.aux_rows:
+                assert wparts[2] is not None and wparts[3] is not None
+                d.aux_wp[0], d.aux_wp[1] = wparts[2], wparts[3]
+        elif wparts is not None and entry == "d3a_mlp_fwd_x6" and wide_presplit_ok(net) \
+                and members is None:
+            d.wp[0], d.wp[1] = wparts[0], wparts[1]  # the stream matrices' images
             if d.aux_rows:
                 assert wparts[2] is not None and wparts[3] is not None
                 d.aux_wp[0], d.aux_wp[1] = wparts[2], wparts[3]

@@ -183,20 +183,24 @@ def test_cql_step_forms_the_images_of_the_step_weights():
         assert torch.equal(w1.view(torch.int16).view(-1), split_ref(W[si, 1], 256).view(-1))
 
 
-def test_cql_update_presplit_is_bitwise_the_splitting_update(monkeypatch):
+@pytest.mark.parametrize("hidden", [[256, 256], [256, 256, 256]])
+def test_cql_update_presplit_is_bitwise_the_splitting_update(monkeypatch, hidden):
     """Two CQL impls from one state, one with the pre-split forward and one
     without (D3A_X6_PRESPLIT=0's path): three updates leave every parameter
-    bitwise equal."""
+    bitwise equal.  [256, 256, 256]: the CQL reproduction critic, whose
+    three-layer d3a_mlp_fwd_x6 streams W1 / W2 from images the sampler forms."""
     import sys
     import os
     sys.path.insert(0, os.path.dirname(__file__))
     from cql_helpers import HostBatch, make_batch, make_impl
     D, A, N_, B = 11, 3, 10, 256
     impls = []
+    # (the three-layer critic's stream images are opt-in: D3A_X6_WIDE_PRESPLIT)
+    monkeypatch.setattr(mlp, "_WIDE_PRESPLIT", True)
     for pre in (True, False):
         monkeypatch.setattr(mlp, "_PRESPLIT", pre)
         torch.manual_seed(0)
-        impl = make_impl(D, A, [256, 256], N_)
+        impl = make_impl(D, A, hidden, N_)
         if impls:
             impl.set_state_dict(impls[0].get_state_dict())
         impls.append(impl)

@@ -51,6 +51,13 @@ def main():
            # (single-tile workgroups: lifetime - tile = the kernel prologue)
            "prologue_cycles_mean": round(float((st[(st[:, 0] != 0) & (st[:, 7] != 0)][:, 8]
                                                - (ok[:, 7] - ok[:, 0])).mean()))}
+    # every wave: cycles from the workgroup's tile start (wave 0's stamp 0)
+    wb = (ctypes.c_ulonglong * (512 * 64))()
+    assert N.lib().d3a_wide_wave_stamps(wb, 512 * 64) == 0
+    ws = np.array(wb, dtype=np.float64).reshape(512, 8, 8)
+    ws = ws[(ws != 0).all(axis=(1, 2))]
+    rel = ws - ws[:, :1, :1]
+    out["wave_cum_cycles_mean"] = [[round(float(v)) for v in rel[:, w].mean(0)] for w in range(8)]
     print(json.dumps(out, indent=1))
 
 
