@@ -772,18 +772,29 @@ def main():
         b_s, bflops, bdesc = bwd
         # the backward's large products are the 0 / 1 ReLU mask times three
         # bf16 parts: its ceiling is the bf16 peak / 3 (fp32 MFMA: 157.3 TF)
-        bpeak = 2500.0 / 3 if (x6 and "x3" in bdesc) else 157.3
+        # (the bf16 line's backward is the same split-bf16 x3 kernel: priced alike)
+        bx3 = "x3" in bdesc and args.precision in ("fp32", "bf16")
+        bpeak = 2500.0 / 3 if bx3 else 157.3
         bach = bflops / b_s / 1e12
         sec = {"bound": "mfma", "achieved": round(bach, 3), "peak": round(bpeak, 1),
                "unit": "TFLOP/s", "frac": round(bach / bpeak, 4), "kernel": bdesc,
                "avg_launch_us": round(b_s * 1e6, 3),
                "launch_timing": "HIP events on the kernel's stream, 500 launches after 100 "
                                 "settling launches, after the first warm-up step"}
-        if x6 and "x3" in bdesc:
+        if bx3:
             sec["bf16_mfma_frac"] = round(3 * bach / 2500.0, 4)
         # the step's largest kernel leads: the other critic kernel beside it
         if b_s > kern_s:
-            sec["traffic"] = None
+            # (its PMC summary: r{ROUND}_pmc_traffic_<algo><suffix>_bwd.json,
+            # tools/pmc_dominant.py --backward, matched by description)
+            sec["traffic"], sec["traffic_source"] = None, None
+            bj = args.traffic_json[:-5] + "_bwd.json" if args.traffic_json.endswith(".json") else None
+            if bj and os.path.exists(bj):
+                with open(bj) as f:
+                    tj = json.load(f)
+                if tj.get("bench_desc") == bdesc and tj.get("hbm_bytes_per_launch"):
+                    sec["traffic"] = float(tj["hbm_bytes_per_launch"])
+                    sec["traffic_source"] = os.path.relpath(bj, os.path.dirname(os.path.abspath(__file__)))
             out["roofline"], out["roofline_other"] = sec, out["roofline"]
         else:
             out["roofline_other"] = sec

@@ -1044,8 +1044,17 @@ extern "C" int d3a_q2_fwd_x1(const d3a_mlp_fwd_desc* dp, void* stream) {
   D3A_CHECK_ARG(dp, "d3a_q2_fwd_x1: null desc");
   D3A_CHECK_ARG(dp->row_mean == nullptr, "d3a_q2_fwd_x1: row_mean is d3a_mlp_fwd_x6 only");
   D3A_CHECK_ARG(dp->xg_mode == 0, "d3a_q2_fwd_x1: no input-row builder");
-  D3A_CHECK_ARG(dp->hmask == nullptr, "d3a_q2_fwd_x1: hmask is d3a_q2_fwd_x6 only");
   const d3a_mlp_fwd_desc& e = *dp;  // d3a_q2_fwd_x6's contract
+  // (the ReLU mask bits of the slice backward: the same epilogue as x6's)
+  D3A_CHECK_ARG(e.hmask == nullptr ||
+                    ((reinterpret_cast<uintptr_t>(e.hmask) & 3) == 0 &&
+                     e.s_hmask >= (e.r0 + e.rows) * (X_H / 32)),
+                "d3a_q2_fwd_x1: hmask needs rows of 8 32-bit words");
+  D3A_CHECK_ARG(e.hmaskT == nullptr ||
+                    (e.hmask != nullptr && e.r0 % 32 == 0 &&
+                     (reinterpret_cast<uintptr_t>(e.hmaskT) & 3) == 0 &&
+                     e.s_hmaskT >= (e.r0 + e.rows + 31) / 32 * X_H),
+                "d3a_q2_fwd_x1: hmaskT needs hmask, r0 % 32 == 0 and [rows / 32][256] words");
   D3A_CHECK_ARG(e.n_hidden == 2 && e.H == X_H && e.n_out == 1 && e.n_in >= 1 && e.n_in <= 48,
                 "d3a_q2_fwd_x1: needs [n_in <= 48, 256, 256, 1]");
   D3A_CHECK_ARG(e.x && e.out && e.W[0] && e.W[1] && e.W[2] && e.b[0] && e.b[1] && e.b[2],

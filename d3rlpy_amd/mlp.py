@@ -301,8 +301,9 @@ def slice_ok(net: EnsembleMLP, rows: int, r0: int) -> bool:
     """The slice backward applies to a q2 backward space of ``rows`` rows read
     from row ``r0`` of the x6 forward's activations: x6 critic GEMMs with
     fp32 kept activations and both on 32-row groups."""
+    # (the bf16 line's x1 forward writes the same mask bits: round 6)
     return (_SLICE and q2_ok(net, rows) and ops.CRITIC_GEMM == "x6"
-            and ops.CRITIC_PRECISION not in ("bf16", "bf16h") and rows % 32 == 0 and r0 % 32 == 0)
+            and ops.CRITIC_PRECISION != "bf16h" and rows % 32 == 0 and r0 % 32 == 0)
 
 
 def q2p_ok(net: EnsembleMLP, rows: int) -> bool:
@@ -477,7 +478,8 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
                 ops.call_desc("d3a_bcq_rows", xgen)
             xgen = None
         if acts.hmask is not None:
-            if (entry == "d3a_q2_fwd_x6" and keep_h and members is None and sizes[-1] == 1):
+            if (entry in ("d3a_q2_fwd_x6", "d3a_q2_fwd_x1") and keep_h and members is None
+                    and sizes[-1] == 1):
                 d.hmask, d.s_hmask = acts.hmask.data_ptr(), R * (sizes[-2] // 32)
                 acts.hmask_from, acts.hmask_to = d.h_from, r1
                 if acts.hmaskT is not None and r0 % 32 == 0:

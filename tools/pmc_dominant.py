@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--transitions", type=int, default=200_000)
     ap.add_argument("--precision", choices=["fp32", "bf16", "bf16h"], default="fp32")
     ap.add_argument("--critic-gemm", choices=["fp32", "x6"], default=None)
+    ap.add_argument("--backward", action="store_true",
+                    help="launch the critic backward (backward_kernel) instead: the bench "
+                         "line's lead kernel when it outlasts the forward")
     ap.add_argument("--desc-out", default=None,
                     help="write {desc, flops} of the launched kernel here (bench.py matches a "
                          "traffic file to its line by this desc)")
@@ -36,7 +39,8 @@ def main():
     algo, it = bench.build_workload(0, a.transitions, a.algo)
     bench.gpu_steps(algo, it, 5)
     torch.cuda.synchronize()
-    launch, flops, desc = next(iter(algo.impl._ws.values())).dominant_kernel()
+    wsp = next(iter(algo.impl._ws.values()))
+    launch, flops, desc = wsp.backward_kernel() if a.backward else wsp.dominant_kernel()
     for _ in range(a.reps):
         launch()
     torch.cuda.synchronize()
