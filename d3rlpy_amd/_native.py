@@ -498,7 +498,7 @@ class IqnHeadBwdFusedDesc(C.Structure):
         ("dh", vp), ("dWf_part", vp), ("dbf_part", vp), ("dWe_part", vp), ("dbe_part", vp),
         ("B", C.c_int32), ("K", C.c_int32), ("F", C.c_int32), ("E", C.c_int32),
         ("A", C.c_int32), ("G", C.c_int32), ("NB", C.c_int32),
-        ("taus", vp), ("We", vp), ("be", vp),
+        ("taus", vp), ("We", vp), ("be", vp), ("phi_dbg", vp),
     ]
 
 

@@ -566,6 +566,7 @@ __global__ __launch_bounds__(512) void iqn_head_bwd_rc_kernel(d3a_iqn_head_bwd_f
       if ((r & 3) == 0) __builtin_amdgcn_sched_barrier(0);
       const int m = 8 * (r >> 2) + 4 * lh + (r & 3);
       const float ph = fmaxf(acc[r] + be_u, 0.f);
+      if (d.phi_dbg != nullptr) d.phi_dbg[(rbase_of(ti) + m) * F + u] = ph;
       const float4 q0 = *reinterpret_cast<const float4*>(&L.dq[buf][m][0]);
       float4 q1 = make_float4(0.f, 0.f, 0.f, 0.f);
       if constexpr (AM > 4) q1 = *reinterpret_cast<const float4*>(&L.dq[buf][m][4]);

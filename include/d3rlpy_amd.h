@@ -488,6 +488,11 @@ int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* d, void* stream);
  * s_memtime values) of the last d3a_mlp_fwd_x6 launch made with
  * D3A_WIDE_STAMPS=1 in the environment. */
 int d3a_wide_stamps(unsigned long long* dst, int n);
+/* diagnostic: every wave's phase stamps of the last three-hidden-layer
+ * D3A_WIDE_STAMPS=1 d3a_mlp_fwd_x6 launch, [workgroup < 512][wave][8]
+ * (s_memtime at tile start, the input barrier, image 1, layer 2 issued,
+ * image 2, layer 3 issued, head written) */
+int d3a_wide_wave_stamps(unsigned long long* dst, int n);
 /* Diagnostic (synchronous, not for graphs): the phase-boundary s_memtime
  * stamps of the last d3a_q2_fwd_x6 launch built with D3A_X6_PROBE bit 4. */
 int d3a_x6_stamps(unsigned long long* dst, int n);
@@ -1302,6 +1307,10 @@ typedef struct d3a_iqn_head_bwd_fused_desc {
    * rebuilds prior and phi = relu(We prior + be) of its rows from tau (row r's
    * tau at taus[r], the forward's rows) with the forward's ops; F 256 or 512 */
   const float* taus; const float* We; const float* be;
+  /* optional (recompute mode, tests / diagnostics): the recomputed phi rows,
+   * [rows][F] in the forward's row order -- what the backward's ReLU mask and
+   * dh use, to compare with d3a_iqn_embed_head's phi_out */
+  float* phi_dbg;
 } d3a_iqn_head_bwd_fused_desc;
 int d3a_iqn_head_bwd_fused(const d3a_iqn_head_bwd_fused_desc* d, void* stream);
 

@@ -175,7 +175,9 @@ def test_iqn_head_bwd_recompute_matches_kept_rows(B, K, F, A, NB):
     ops.call_desc("d3a_iqn_embed_head", d)
     P = (B + NB - 1) // NB
 
-    def run(recompute):
+    phi_rc = torch.full((rows, F), float("nan"), device=dev)
+
+    def run(recompute, dbg=False):
         out = dict(dh=torch.full((B, F), float("nan"), device=dev),
                    dWf=torch.full((P, A, F), float("nan"), device=dev),
                    dbf=torch.full((P, A), float("nan"), device=dev),
@@ -185,6 +187,8 @@ def test_iqn_head_bwd_recompute_matches_kept_rows(B, K, F, A, NB):
         fb.h, fb.dq, fb.Wf = h.data_ptr(), dq.data_ptr(), Wf.data_ptr()
         if recompute:
             fb.taus, fb.We, fb.be = taus.data_ptr(), We.data_ptr(), be.data_ptr()
+            if dbg:
+                fb.phi_dbg = phi_rc.data_ptr()
         else:
             fb.phi, fb.prior = phi.data_ptr(), prior.data_ptr()
         fb.dh, fb.dWf_part, fb.dbf_part = out["dh"].data_ptr(), out["dWf"].data_ptr(), out["dbf"].data_ptr()
@@ -220,6 +224,13 @@ def test_iqn_head_bwd_recompute_matches_kept_rows(B, K, F, A, NB):
     rc2 = run(True)
     for k in rc:
         assert torch.equal(rc[k], rc2[k]), k
+    # the recomputed phi -- whose sign is the backward's ReLU mask -- is bitwise
+    # the forward's (the reference's autograd uses the saved phi): the same
+    # prior, the same six part products in the same order
+    rc3 = run(True, dbg=True)
+    assert torch.equal(phi_rc, phi), float((phi_rc - phi).abs().max())
+    for k in rc:
+        assert torch.equal(rc[k], rc3[k]), k
 
 
 def test_iqn_prior_cos_faithful_on_gpu():
