@@ -170,9 +170,11 @@ __host__ __device__ __forceinline__ int64_t seg_threads(int64_t n_partials, int6
 // load address instead of two (a segment's partials are < 4 GiB: nets.py
 // AdamGroup checks), which took adam_kernel from 142 VGPRs (3 waves a SIMD,
 // every launch a dozen latency rounds) to the 8-wave range.
+// Lt: lanes of the closing butterfly (L, or 1 where the caller combines the
+// L slots itself: the slot-major 16-lane blocks)
 template <int U>
 __device__ __forceinline__ double sum_partials_u(const float* g, int64_t n, int64_t stride,
-                                                 int64_t i, int j, int L) {
+                                                 int64_t i, int j, int L, int Lt) {
   double gd = 0.0;
   const char* gb = reinterpret_cast<const char*>(g);
   const uint32_t n32 = (uint32_t)n, s4 = (uint32_t)stride * 4u, i4 = (uint32_t)i * 4u;
@@ -189,8 +191,23 @@ __device__ __forceinline__ double sum_partials_u(const float* g, int64_t n, int6
     for (int u = 0; u < U; ++u)
       if (q + (uint32_t)(u * L) < n32) gd += (double)v[u];
   }
-  for (int o = L >> 1; o > 0; o >>= 1) gd += __shfl_xor(gd, o, 64);
+  for (int o = Lt >> 1; o > 0; o >>= 1) gd += __shfl_xor(gd, o, 64);
   return gd;
+}
+
+// The 16-lane groups (>= 64 partials) run slot-major: in a 256-thread block
+// slot j = thread / 16 of element base + thread % 16, so one load instruction
+// of a wave reads 64 contiguous bytes of each of four partial rows (the
+// element-major groups read 16 bytes of each of sixteen); the block combines
+// the sixteen slot sums through LDS with the butterfly's pairing -- the same
+// additions, so the same value (fp64 addition commutes).
+__device__ __forceinline__ double slot_tree16(const double (&r)[16][16], int e) {
+  double a8[8], b4[4];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a8[k] = r[k][e] + r[k + 8][e];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) b4[k] = a8[k] + a8[k + 4];
+  return (b4[0] + b4[2]) + (b4[1] + b4[3]);
 }
 
 // four consecutive elements' partial sums (one lane, q ascending, fp64: the
@@ -227,13 +244,13 @@ __device__ __forceinline__ void sum_partials4(const float* g, int64_t n, int64_t
 // 32-load batch issued 24 clamped duplicates each; the fc's 4 split-K
 // partials 4 of 8)
 __device__ __forceinline__ double sum_partials(const float* g, int64_t n, int64_t stride,
-                                               int64_t i, int j, int L) {
+                                               int64_t i, int j, int L, int Lt) {
   const int64_t per = (n + L - 1) / L;  // uniform over the segment
-  if (per <= 1) return sum_partials_u<1>(g, n, stride, i, j, L);
-  if (per <= 2) return sum_partials_u<2>(g, n, stride, i, j, L);
-  if (per <= 4) return sum_partials_u<4>(g, n, stride, i, j, L);
-  if (per <= 8) return sum_partials_u<8>(g, n, stride, i, j, L);
-  return sum_partials_u<16>(g, n, stride, i, j, L);
+  if (per <= 1) return sum_partials_u<1>(g, n, stride, i, j, L, Lt);
+  if (per <= 2) return sum_partials_u<2>(g, n, stride, i, j, L, Lt);
+  if (per <= 4) return sum_partials_u<4>(g, n, stride, i, j, L, Lt);
+  if (per <= 8) return sum_partials_u<8>(g, n, stride, i, j, L, Lt);
+  return sum_partials_u<16>(g, n, stride, i, j, L, Lt);
 }
 
 // ---- Adam (torch.optim.adam._single_tensor_adam, weight_decay = 0) ---------
@@ -310,7 +327,10 @@ __global__ __launch_bounds__(256, VEC ? 6 : 8) void adam_kernel(d3a_adam_desc a)
   // (VEC false: the host's one_elem -- no segment has seg_vec 4)
   const int V = VEC ? seg_vec(sg.n_partials, sg.numel) : 1;
   const int64_t lt = ((int64_t)blockIdx.x - first) * 256 + threadIdx.x;
-  const int64_t i = V == 4 ? lt * 4 : lt / L;  // the thread's first element
+  const bool smj = L == 16;  // slot-major 16-lane block (uniform)
+  // the thread's first element, and its partial slot
+  const int64_t i = V == 4 ? lt * 4 : smj ? ((int64_t)blockIdx.x - first) * 16 + (threadIdx.x & 15) : lt / L;
+  const int slot = smj ? (int)(threadIdx.x >> 4) : (int)(lt % L);
   const bool act = i < sg.numel;
   float* tg = a.soft ? sg.param + a.targ_delta : nullptr;
   // 16-byte accesses when every stream is 16-byte aligned (a flat store's
@@ -319,7 +339,7 @@ __global__ __launch_bounds__(256, VEC ? 6 : 8) void adam_kernel(d3a_adam_desc a)
                   ((reinterpret_cast<uintptr_t>(sg.param) | reinterpret_cast<uintptr_t>(sg.exp_avg) |
                     reinterpret_cast<uintptr_t>(sg.exp_avg_sq) | reinterpret_cast<uintptr_t>(sg.grad) |
                     reinterpret_cast<uintptr_t>(sg.grad_out) | reinterpret_cast<uintptr_t>(tg)) & 15) == 0;
-  const bool lead = V == 4 || (lt % L) == 0;
+  const bool lead = V == 4 || slot == 0;
   float m[4] = {}, v[4] = {}, p[4] = {}, tv[4] = {};
   double gd[4] = {};
   if (act) {
@@ -345,9 +365,15 @@ __global__ __launch_bounds__(256, VEC ? 6 : 8) void adam_kernel(d3a_adam_desc a)
           if (tg) tv[e] = tg[i + e];
         }
         gd[e] = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i + e,
-                             V == 4 ? 0 : (int)(lt % L), V == 4 ? 1 : L);
+                             V == 4 ? 0 : slot, V == 4 ? 1 : L, V == 4 || smj ? 1 : L);
       }
     }
+  }
+  if (smj) {  // uniform: the sixteen slots' sums meet in LDS
+    __shared__ double s_red[16][16];
+    s_red[slot][threadIdx.x & 15] = gd[0];
+    __syncthreads();
+    if (lead) gd[0] = slot_tree16(s_red, threadIdx.x & 15);
   }
   if (tab) __syncthreads();  // s_step_size; block 0: every ring writer has read *ring_ctr
   if (tail) {
@@ -416,6 +442,15 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(const d3a_adam_segment
   const int L = seg_lanes(sg.n_partials, sg.numel);
   const int V = seg_vec(sg.n_partials, sg.numel);
   const int64_t lt = ((int64_t)blockIdx.x - s_first) * 256 + threadIdx.x;
+  if (L == 16) {  // slot-major (uniform), as adam_kernel
+    __shared__ double s_red[16][16];
+    const int e = threadIdx.x & 15, slot = threadIdx.x >> 4;
+    const int64_t i = ((int64_t)blockIdx.x - s_first) * 16 + e;
+    s_red[slot][e] = i < sg.numel ? sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i, slot, 16, 1) : 0.0;
+    __syncthreads();
+    if (slot == 0 && i < sg.numel) sg.grad_out[i] = (float)slot_tree16(s_red, e);
+    return;
+  }
   const int64_t i = V == 4 ? lt * 4 : lt / L;
   if (i >= sg.numel) return;  // uniform over each lane group
   if (V == 4) {
@@ -429,11 +464,11 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(const d3a_adam_segment
           make_float4((float)gd[0], (float)gd[1], (float)gd[2], (float)gd[3]);
     } else {
       for (int e = 0; e < 4; ++e)
-        sg.grad_out[i + e] = (float)sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i + e, 0, 1);
+        sg.grad_out[i + e] = (float)sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i + e, 0, 1, 1);
     }
     return;
   }
-  const double gd = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i, (int)(lt % L), L);
+  const double gd = sum_partials(sg.grad, sg.n_partials, sg.partial_stride, i, (int)(lt % L), L, L);
   if (lt % L) return;
   sg.grad_out[i] = (float)gd;
 }
