@@ -11,6 +11,9 @@ timeout -k 10 400 python -u -m pytest tests -q -m gpu -p no:cacheprovider --time
 tail -1 $O/gpu_tests.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
+# the arbiter's per-tensor margins (HIP vs fp64 on HIP's ReLU decisions, the bar)
+timeout -k 10 400 python -u -m pytest -s -v -p no:cacheprovider --timeout 120 --timeout-method thread tests/test_gpu_cql_parity.py tests/test_gpu_arbiters.py tests/test_gpu_dp.py tests/test_gpu_production_path.py tests/test_gpu_sac_parity.py > $O/arbiter_margins.log 2>&1 || { tail -30 $O/arbiter_margins.log; exit 1; }
+tail -1 $O/arbiter_margins.log
 timeout -k 10 300 python bench.py > $O/bench_cql.json 2> $O/bench_cql.err || { tail -20 $O/bench_cql.err; exit 1; }
 for spec in "cql --precision bf16:cql_bf16" "cqldp:cqldp" "cqlrepro:cqlrepro" "td3bc:td3bc" "bcq:bcq" "dcql:dcql"; do
   IFS=: read args name <<< "$spec"
