@@ -60,6 +60,9 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int lr = lane & 15, lq = lane >> 4;
   const int c = blockIdx.z;
+  // (WH) the head's outputs in halves of 128 over blockIdx.y: both halves run
+  // the hidden layers, half 0 keeps the activations
+  const int hq = WH ? (int)blockIdx.y : 0;
   const int nb_main = (int)((d.rows + S_RB - 1) / S_RB);
   const bool aux = (int)blockIdx.x >= nb_main;
   const int m0 = aux ? ((int)blockIdx.x - nb_main) * S_RB : (int)d.r0 + (int)blockIdx.x * S_RB;
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
       }
     }
     // epilogue: lane holds row lr, units 32 w + 16 tile + 4 lq + i
-    float* hg = (!aux && d.h[l]) ? d.h[l] + c * d.sh : nullptr;
+    float* hg = (!aux && d.h[l] && hq == 0) ? d.h[l] + c * d.sh : nullptr;
     const int row = m0 + lr;
     const bool keep = hg != nullptr && row >= h_from && row < rend;
 #pragma unroll
@@ -221,10 +224,14 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
   const float* hl = S.h[(L - 1) & 1];
   if (PROBE & 2) return;
   if constexpr (WH) {
-    // the head as one more MFMA layer: wave w's outputs 32 w + 16 tile + lr
-    // (rows of Wh past n_out read row n_out - 1; their outputs are not stored)
-    if (32 * w >= J) return;  // uniform: no outputs for this wave
-    const int ja = min(u0, J - 1), jb = min(u0 + 16, J - 1);
+    // the head as one more MFMA layer: wave w (< 4 with halves) of half hq
+    // owns outputs 128 hq + 32 w + 16 tile + lr (rows of Wh past n_out read row n_out - 1;
+    // their outputs are not stored).  Two halves: each SIMD streams one
+    // output tile's 128-MFMA chain instead of two (measured: the head was 8
+    // of the pass's 22.4 us)
+    const int jw = 128 * hq + 32 * w;
+    if ((gridDim.y > 1 && w >= 4) || jw >= J) return;  // uniform: no outputs for this wave
+    const int ja = min(jw + lr, J - 1), jb = min(jw + 16 + lr, J - 1);
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       wa[g] = *reinterpret_cast<const float4*>(Wh + ja * S_H + 16 * g + 4 * lq);
@@ -245,7 +252,7 @@ __global__ __launch_bounds__(512) void mlp_small_kernel(d3a_mlp_fwd_desc d) {
 #pragma unroll
       for (int tl = 0; tl < 2; ++tl) {
         const f32x4& a = tl ? acc1 : acc0;
-        const int j0 = 32 * w + 16 * tl + 4 * lq;
+        const int j0 = jw + 16 * tl + 4 * lq;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (j0 + i < J) outp[(int64_t)row * d.ldout + j0 + i] = a[i] + bh[j0 + i];
@@ -514,7 +521,16 @@ bool mlp_small_launch(const d3a_mlp_fwd_desc& d, hipStream_t st) {
     return e ? atoi(e) : 0;
   }();
   if (wide) {
-    hipLaunchKernelGGL((mlp_small_kernel<2, 0, true>), grid, dim3(512), 0, st, d);
+    // (the head's output halves on grid y; D3A_SMALL_WIDE_HALVES=0: one)
+    static const bool halves = [] {
+      const char* e = getenv("D3A_SMALL_WIDE_HALVES");
+      return !(e && e[0] == '0');
+    }();
+    const dim3 grid((unsigned)nb, (unsigned)(halves ? (d.n_out + 127) / 128 : 1), (unsigned)d.C);
+    if (probe == 1) hipLaunchKernelGGL((mlp_small_kernel<2, 1, true>), grid, dim3(512), 0, st, d);
+    else if (probe == 2) hipLaunchKernelGGL((mlp_small_kernel<2, 2, true>), grid, dim3(512), 0, st, d);
+    else if (probe == 3) hipLaunchKernelGGL((mlp_small_kernel<2, 3, true>), grid, dim3(512), 0, st, d);
+    else hipLaunchKernelGGL((mlp_small_kernel<2, 0, true>), grid, dim3(512), 0, st, d);
     return true;
   }
   if (probe && d.n_hidden == 2) {
