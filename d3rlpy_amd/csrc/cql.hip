@@ -291,6 +291,22 @@ __device__ __forceinline__ void cql_lse_wave(const d3a_cql_loss_desc& d, int64_t
   }
   if ((s == 0 && !d.update_alpha) || (s == 1 && !d.update_critic)) return;
   const float rand_logp = (float)log(pow(0.5, (double)d.A));
+  if (M <= 64) {
+    // (3N <= 64: one value a lane, loaded once -- the loops below reload it
+    // for the max, the sum and the weights, three dependent round trips; the
+    // same operations, so the same values)
+    const float vj = lane < M ? is_value(d, c, s, b, lane, rand_logp) : -INFINITY;
+    float mx = wave_max(vj);
+    if (isinf(mx)) mx = 0.f;
+    const float ej = lane < M ? expf(vj - mx) : 0.f;
+    const float se = wave_sum(ej);
+    const float l = logf(se) + mx;
+    if (lane == 0) d.lse[(s * C + c) * B + b] = l;
+    if (s == 1 && lane < M) {
+      const int64_t blk = lane / N, n = lane % N;
+      d.dq[c * d.R + 3 * NB + blk * NB + b * N + n] = __fdiv_rn(ej, se);
+    }
+  } else {
   float mx = -INFINITY;
   for (int64_t j = lane; j < M; j += 64) mx = fmaxf(mx, is_value(d, c, s, b, j, rand_logp));
   mx = wave_max(mx);
@@ -311,6 +327,7 @@ __device__ __forceinline__ void cql_lse_wave(const d3a_cql_loss_desc& d, int64_t
           __fdiv_rn(expf(is_value(d, c, 1, b, j, rand_logp) - mx), se);
     }
   }
+  }  // M > 64
   if (drow) {
     // the data row's gradient without the conservative term (subtracted by
     // the backward, which knows the new alpha) and its squared TD error --
