@@ -184,3 +184,50 @@ def test_presplit_forward_and_split_validate_without_a_gpu():
     s.job[0].src, s.job[0].dst, s.job[0].rows, s.job[0].k, s.job[0].kpad = 16, 16, 4, 14, 8
     assert lib.d3a_x6_split(ctypes.byref(s), None) < 0
     assert b"kpad % 16" in lib.d3a_last_error()
+
+
+def test_wide_forward_validates_without_a_gpu():
+    """d3a_mlp_fwd_x6 (round 6): up to three hidden layers; stream images only
+    for n_in <= 32 and the three-layer Q-head / two-layer wide-head forms; an
+    aux pass needs its inputs and excludes row_mean."""
+    from d3rlpy_amd import _native as N
+    lib = N.lib()
+
+    def desc(n_hidden, n_in=14, n_out=1):
+        d = N.MlpFwdDesc()
+        d.n_in, d.n_hidden, d.H, d.n_out, d.C, d.rows, d.ldout = n_in, n_hidden, 256, n_out, 2, 64, n_out
+        d.x = d.out = 16
+        for l in range(n_hidden + 1):
+            d.W[l] = d.b[l] = 16
+            d.sW[l], d.sb[l] = 256 * 256, 256
+        d.sh = 64 * 256
+        return d
+    d = desc(4)
+    assert lib.d3a_mlp_fwd_x6(ctypes.byref(d), None) < 0
+    assert b"256, 256 (, 256)" in lib.d3a_last_error()
+    d = desc(3, n_in=40)
+    d.wp[0], d.wp[1] = 16, 16
+    assert lib.d3a_mlp_fwd_x6(ctypes.byref(d), None) < 0
+    assert b"stream images" in lib.d3a_last_error()
+    d = desc(2, n_out=1)  # two hidden layers with a one-output head: no image form
+    d.wp[0], d.wp[1] = 16, 16
+    assert lib.d3a_mlp_fwd_x6(ctypes.byref(d), None) < 0
+    assert b"stream images" in lib.d3a_last_error()
+    d = desc(3)
+    d.aux_rows, d.aux_x, d.aux_out = 8, 16, 16
+    mean = (ctypes.c_float * 1)()
+    d.row_mean, d.s_mean = ctypes.addressof(mean), 64
+    assert lib.d3a_mlp_fwd_x6(ctypes.byref(d), None) < 0
+    assert b"aux pass" in lib.d3a_last_error()
+
+
+def test_adam_thread_counts_mirror_the_kernel_rule():
+    """nets._seg_threads is elementwise.hip's seg_threads: 16 lanes an element
+    for >= 64 partials, four elements a thread for >= 2^18 elements (a multiple
+    of 4), else one; AdamGroup.one_elem says no segment takes four."""
+    from d3rlpy_amd.nets import _seg_threads
+    assert _seg_threads(128, 33280) == 33280 * 16
+    assert _seg_threads(4, 1605632) == 1605632 // 4
+    assert _seg_threads(4, (1 << 18) - 4) == (1 << 18) - 4
+    assert _seg_threads(1, (1 << 18) + 2) == (1 << 18) + 2
+    assert _seg_threads(63, 1 << 20) == (1 << 20) // 4
