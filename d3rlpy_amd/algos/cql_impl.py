@@ -63,6 +63,9 @@ _ADAM_TAIL = os.environ.get("D3A_ADAM_TAIL", "1") == "1"
 # (d3a_q2_bwd_x6_cql; the new scalar state committed by the critic Adam);
 # D3A_LOSS_IN_BWD=0 keeps the d3a_cql_loss launch (A/B)
 _LOSS_IN_BWD = os.environ.get("D3A_LOSS_IN_BWD", "1") == "1"
+# (A/B) the weight images' split jobs in the sampler's launch even where the
+# policy forward is the parts path (D3A_SPLIT_IN_SAMPLER=1)
+_SPLIT_IN_SAMPLER = os.environ.get("D3A_SPLIT_IN_SAMPLER", "0") == "1"
 
 class CQLImpl(ImplBase):
     # conservative term + alpha (cql_impl.py); SACImpl (algos/sac.py) clears it
@@ -556,7 +559,7 @@ class _Workspace:
         # it is the parts path, else in the sampler's
         self.presplit_jobs = None
         if self.wimg is not None:
-            if self.phead is not None:
+            if self.phead is not None and not _SPLIT_IN_SAMPLER:
                 self.presplit_jobs = self.wimg.jobs()
             else:
                 s.presplit = self.wimg.jobs()
