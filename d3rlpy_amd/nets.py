@@ -202,7 +202,10 @@ class AdamGroup:
         segs = (N.AdamSegment * len(self.names))()
         self.n_blocks = 0  # flat launch over the segments (d3a_adam_f32)
         self.n_blocks_reduced = 0
-        self.one_elem = True  # no segment takes four elements a thread
+        # no segment takes four elements a thread (in the partials' table /
+        # the reduced table, whose one-partial segments may)
+        self.one_elem = True
+        self.one_elem_reduced = True
         for i, n in enumerate(self.names):
             gt, parts = grads.parts[n]
             numel = store.numel(n)
@@ -219,6 +222,7 @@ class AdamGroup:
             segs[i].grad_out = self.grad_store.ptr(n) if self.grad_store is not None else None
             self.n_blocks += (_seg_threads(parts, numel) + 255) // 256
             self.one_elem &= _seg_threads(parts, numel) == numel * (16 if parts >= 64 else 1)
+            self.one_elem_reduced &= _seg_threads(1, numel) == numel
             self.n_blocks_reduced += (_seg_threads(1, numel) + 255) // 256
         raw = bytes(segs)
         self.seg_table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
@@ -281,7 +285,8 @@ class AdamGroup:
         blocks = self.block_table_reduced if reduced else self.block_table
         # (the reduced table: one partial, the same four-a-thread segments)
         ops.adam_step(table, len(self.names), nb, self.step, self.lr, self.beta1, self.beta2,
-                      self.eps, grad_scale, blocks=blocks, one_elem=self.one_elem, **kw)
+                      self.eps, grad_scale, blocks=blocks,
+                      one_elem=self.one_elem_reduced if reduced else self.one_elem, **kw)
 
     def reduce(self) -> None:
         """grad_store <- sum of the split-K partials (no parameter update)."""

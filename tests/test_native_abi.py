@@ -231,3 +231,20 @@ def test_adam_thread_counts_mirror_the_kernel_rule():
     assert _seg_threads(4, (1 << 18) - 4) == (1 << 18) - 4
     assert _seg_threads(1, (1 << 18) + 2) == (1 << 18) + 2
     assert _seg_threads(63, 1 << 20) == (1 << 20) // 4
+
+
+def test_adam_one_elem_per_table():
+    """AdamGroup.one_elem (the partials' table) and one_elem_reduced (the
+    one-partial table of the data-parallel path) are decided separately: a
+    segment of >= 2^18 elements with >= 64 partials runs 16 lanes an element in
+    the first and four elements a thread in the second."""
+    import torch
+    from d3rlpy_amd.nets import AdamGroup, GradSpace, OptimState, ParamStore
+    dev = torch.device("cpu")
+    store = ParamStore()
+    store.add("w", (1 << 18,))
+    store.allocate(dev)
+    gs = GradSpace(dev)
+    gs.add("w", (1 << 18,), 64)
+    opt = AdamGroup(OptimState(store, ["w"], lr=1e-3), gs, keep_grads=True)
+    assert opt.one_elem and not opt.one_elem_reduced
