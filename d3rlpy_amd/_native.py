@@ -118,6 +118,12 @@ class X6SplitJob(C.Structure):
 X6_SPLIT_MAX_JOBS = 4
 
 
+class PhiloxJob(C.Structure):
+    _fields_ = [("out", vp), ("n_normal", C.c_int64), ("n_uniform", C.c_int64),
+                ("lo", C.c_float), ("hi", C.c_float), ("seed", C.c_uint64),
+                ("ctr", vp), ("ticket", vp)]
+
+
 class X6SplitDesc(C.Structure):
     _fields_ = [("job", X6SplitJob * X6_SPLIT_MAX_JOBS), ("n_jobs", C.c_int32)]
 
@@ -295,7 +301,7 @@ class MlpFwdDesc(C.Structure):
         ("xg_a_parts", C.c_int32), ("xg_s_apart", C.c_int64),
         ("xg_xout", vp), ("xg_ldxo", C.c_int64), ("xg_eout", vp),
         ("wp", vp * 2), ("aux_wp", vp * 2),
-        ("presplit", X6SplitDesc),
+        ("presplit", X6SplitDesc), ("philox", PhiloxJob),
     ]
 
 

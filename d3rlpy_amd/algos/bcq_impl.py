@@ -56,6 +56,9 @@ _BRANCHES = os.environ.get("D3A_BCQ_BRANCHES", "0") == "1"
 # d3a_step_end launch (as CQL's update does); D3A_BCQ_ADAM_TAIL=0 keeps
 # step_end (A/B)
 _ADAM_TAIL = os.environ.get("D3A_BCQ_ADAM_TAIL", "1") == "1"
+# the step's Philox noise on extra workgroups of the VAE encoder's launch
+# (round 6; D3A_BCQ_PHILOX_IN_ENC=0: its own d3a_philox_fill launch)
+_PHILOX_IN_ENC = os.environ.get("D3A_BCQ_PHILOX_IN_ENC", "1") == "1"
 # the target rows formed inside the QR-loss launch (from the target pass's
 # quantile means) instead of a d3a_bcq_target launch; D3A_BCQ_FUSED_TARGET=0
 # keeps the launch (A/B)
@@ -639,9 +642,19 @@ class _Workspace:
         impl = self.impl
         B, D, A, K, L = self.B, self.D, self.A, self.K, self.L
         st, tg = impl.store, impl.targ
+        # the step's noise: on extra workgroups of the VAE encoder's parts-path
+        # launch when the imitator update runs (it precedes every reader), else
+        # its own launch
+        ph = None
         if not self._external_noise:
-            ops.philox_fill(self.noise, self.noise.numel(), 0, -1.0, 1.0, self.seed,
-                            self.rng_ctr, self.rng_ticket)
+            if imitator and _PHILOX_IN_ENC and self.pe is not None:
+                ph = NAT.PhiloxJob()
+                ph.out, ph.n_normal, ph.n_uniform = self.noise.data_ptr(), self.noise.numel(), 0
+                ph.lo, ph.hi, ph.seed = -1.0, 1.0, self.seed
+                ph.ctr, ph.ticket = self.rng_ctr.data_ptr(), self.rng_ticket.data_ptr()
+            else:
+                ops.philox_fill(self.noise, self.noise.numel(), 0, -1.0, 1.0, self.seed,
+                                self.rng_ctr, self.rng_ticket)
         if impl._scaler is not None:
             ops.standardize(self.obs2, self.xobs2, self.sc_mean, self.sc_std, self.sc_eps)
         if not imitator:
@@ -673,7 +686,7 @@ class _Workspace:
         if imitator:
             # update_imitator (bcq_impl.py:148-161)
             mlp.forward(impl.vae_enc, st, self.x_q.data_ptr(), True, self.LX1, self.ve_acts,
-                        out_parts=self.pe, xgen=self.r_q, xgen_keep=True)
+                        out_parts=self.pe, xgen=self.r_q, xgen_keep=True, philox=ph)
             ops.call_desc("d3a_bcq_vae_sample", self.vae_desc)
             mlp.forward(impl.vae_dec, st, self.x_vd.data_ptr(), True, self.LX2, self.vd_acts,
                         out_parts=self.pd)

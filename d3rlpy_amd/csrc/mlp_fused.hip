@@ -357,6 +357,10 @@ extern "C" int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d_in, void* stream) {
   D3A_CHECK_ARG(d.presplit.n_jobs == 0 || (d.parts > 1 && x6::x6_split_ok(d.presplit)),
                 "d3a_mlp_fwd: presplit jobs only on the parts path, each with src, 16-byte aligned "
                 "dst, 1 <= k <= kpad and kpad % 16 == 0");
+  D3A_CHECK_ARG((d.philox.n_normal == 0 && d.philox.n_uniform == 0) ||
+                    (d.parts > 1 && d.philox.out && d.philox.ctr && d.philox.ticket &&
+                     d.philox.n_normal >= 0 && d.philox.n_uniform >= 0),
+                "d3a_mlp_fwd: a philox job only on the parts path, with out, ctr and ticket");
   if (d.parts > 1) {
     D3A_CHECK_ARG(d.parts == D3A_MLP_PARTS && d.block_rows == 16 && d.n_hidden == 2 &&
                       d.H == 256 && d.n_in <= 64 && d.n_out <= 32 && d.aux_rows == 0 &&

@@ -310,10 +310,38 @@ __global__ __launch_bounds__(256) void mlp_parts_kernel(d3a_mlp_fwd_desc d) {
     // the CUs the pass leaves idle, one piece a thread
     const int nbx = (int)((d.rows + S_RB - 1) / S_RB);
     if ((int)blockIdx.x >= nbx) {
+      // (x columns nbx .. nbx + es - 1: the split jobs; the rest: the Philox job)
+      const int64_t per_x = 256LL * gridDim.y * gridDim.z;
       const int64_t tot = x6::x6_split_total(d.presplit);
-      const int64_t nwg = (int64_t)(gridDim.x - nbx) * gridDim.y * gridDim.z;
-      const int64_t wgi = ((int64_t)(blockIdx.x - nbx) * gridDim.y + blockIdx.y) * gridDim.z + blockIdx.z;
-      for (int64_t pp = wgi * 256 + threadIdx.x; pp < tot; pp += nwg * 256) x6::x6_split_piece(d.presplit, pp);
+      const int es = (int)((tot + per_x - 1) / per_x);
+      if ((int)blockIdx.x < nbx + es) {
+        const int64_t nwg = (int64_t)es * gridDim.y * gridDim.z;
+        const int64_t wgi = ((int64_t)(blockIdx.x - nbx) * gridDim.y + blockIdx.y) * gridDim.z + blockIdx.z;
+        for (int64_t pp = wgi * 256 + threadIdx.x; pp < tot; pp += nwg * 256) x6::x6_split_piece(d.presplit, pp);
+        return;
+      }
+      // d3a_philox_fill's body: one Philox call -> 4 outputs a thread, then
+      // the last of these workgroups advances the counter
+      const d3a_philox_job& ph = d.philox;
+      const int64_t total = ph.n_normal + ph.n_uniform;
+      const int64_t nwp = (int64_t)(gridDim.x - nbx - es) * gridDim.y * gridDim.z;
+      const int64_t wgi = ((int64_t)(blockIdx.x - nbx - es) * gridDim.y + blockIdx.y) * gridDim.z + blockIdx.z;
+      const int64_t step = *ph.ctr;
+      const int64_t e0 = (wgi * 256 + threadIdx.x) * 4;
+      if (e0 < total) {
+        for (int q = 0; q < 4; ++q) {
+          const int64_t e = e0 + q;
+          if (e < total) ph.out[e] = philox_elem(ph.seed, (uint64_t)step, e, ph.n_normal, ph.lo, ph.hi);
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const unsigned prev = atomicAdd(ph.ticket, 1u);
+        if (prev == (unsigned)(nwp - 1)) {
+          *ph.ctr = step + 1;
+          *ph.ticket = 0u;
+        }
+      }
       return;
     }
   }
@@ -483,12 +511,15 @@ bool mlp_parts_launch(const d3a_mlp_fwd_desc& d, hipStream_t st) {
     return false;
   for (int l = 0; l < 2; ++l)
     if (d.h[l] && !a16(d.h[l], d.sh)) return false;
-  if (d.rows == 0 && d.presplit.n_jobs == 0) return true;
-  // (presplit: enough extra workgroups for one piece a thread)
+  const int64_t ph_total = d.philox.n_normal + d.philox.n_uniform;
+  if (d.rows == 0 && d.presplit.n_jobs == 0 && ph_total <= 0) return true;
+  // (presplit: enough extra workgroups for one piece a thread; philox: for
+  // four outputs a thread)
   const int64_t pieces = d.presplit.n_jobs > 0 ? x6::x6_split_total(d.presplit) : 0;
   const int64_t per_x = 256LL * d.C * D3A_MLP_PARTS;
   const int64_t ex = (pieces + per_x - 1) / per_x;
-  const dim3 grid((unsigned)((d.rows + S_RB - 1) / S_RB + ex), (unsigned)d.C, (unsigned)D3A_MLP_PARTS);
+  const int64_t exp = ph_total > 0 ? ((ph_total + 3) / 4 + per_x - 1) / per_x : 0;
+  const dim3 grid((unsigned)((d.rows + S_RB - 1) / S_RB + ex + exp), (unsigned)d.C, (unsigned)D3A_MLP_PARTS);
   if (d.n_out <= 16)
     hipLaunchKernelGGL(mlp_parts_kernel<16>, grid, dim3(256), 0, st, d);
   else

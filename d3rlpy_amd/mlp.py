@@ -352,7 +352,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             h_from: Optional[int] = None, aux: Optional[tuple] = None,
             skip_head: bool = False, out_parts: Optional[torch.Tensor] = None,
             row_mean: Optional[torch.Tensor] = None, xgen=None, xgen_keep: bool = False,
-            wparts: Optional[tuple] = None, presplit=None) -> bool:
+            wparts: Optional[tuple] = None, presplit=None, philox=None) -> bool:
     """Forward rows [r0, r1) of x (row stride ldx) through the ensemble
     (through its first ``members`` members only, when given).  ``keep_h``:
     store the hidden activations in ``acts.h`` (needed by a backward pass),
@@ -381,7 +381,8 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     (formed from the current weights by an earlier launch of the step).
 
     ``presplit`` (an X6SplitDesc, with ``out_parts``): the parts-path launch
-    also runs those d3a_x6_split jobs on extra workgroups.
+    also runs those d3a_x6_split jobs on extra workgroups; ``philox`` (a
+    PhiloxJob, with ``out_parts``) likewise a d3a_philox_fill.
 
     ``row_mean`` ([C][R] fp32): also the mean of each row's outputs, where the
     launch is d3a_mlp_fwd_x6 (its epilogue forms it); returns whether it was
@@ -410,6 +411,7 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
     # 256 x 256 layers on the split-bf16 GEMM (six products, fp32-accurate)
     deep6 = (not bf16 and out_parts is None and ops.CRITIC_GEMM == "x6" and _X6_DEEP
              and _X6_DEEP_FWD and x6_deep_shape(net) and n * C >= 8192 and xgen is None)
+    assert philox is None or out_parts is not None, "a philox job rides on the parts path only"
     if out_parts is not None:
         assert parts_ok(net) and not bf16 and not skip_head and aux is None
         assert tuple(out_parts.shape) == (N.MLP_PARTS, C, R, sizes[-1])
@@ -433,6 +435,8 @@ def forward(net: EnsembleMLP, store: ParamStore, x: int, x_shared: bool, ldx: in
             d.out, d.parts, d.s_part = out_parts.data_ptr(), N.MLP_PARTS, C * R * sizes[-1]
             if presplit is not None:
                 d.presplit = presplit
+            if philox is not None:
+                d.philox = philox
         d.r0, d.rows, d.C = r0, n, C
         d.h_from = r0 if h_from is None else max(r0, h_from)
         if aux is not None and members is None:

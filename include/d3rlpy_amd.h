@@ -247,6 +247,14 @@ int d3a_x6_split(const d3a_x6_split_desc* d, void* stream);
  * biases and h rows).  Automatic on [n_in <= 48, 256, 256, 1] over >= 8,192
  * member-rows: the register-resident critic kernel (csrc/q2_fwd.hip). */
 #define D3A_MLP_MAX_HIDDEN 4
+/* A Philox fill -- d3a_philox_fill's stream, arithmetic and counter ticket --
+ * run by extra workgroups of another launch (d3a_mlp_fwd_desc.philox, the
+ * parts path); enabled when n_normal + n_uniform > 0. */
+typedef struct d3a_philox_job {
+  float* out; int64_t n_normal, n_uniform; float lo, hi; uint64_t seed;
+  int64_t* ctr; unsigned int* ticket;
+} d3a_philox_job;
+
 typedef struct d3a_mlp_fwd_desc {
   const float* x; int64_t ldx, sxb;
   int32_t n_in, n_hidden, H, n_out;
@@ -328,6 +336,10 @@ typedef struct d3a_mlp_fwd_desc {
    * leaves idle (the CQL step's critic weight images, formed by the policy
    * forward that precedes the critic forward). */
   d3a_x6_split_desc presplit;
+  /* Optional (the parts path only, round 6): a Philox fill on further
+   * appended workgroups (BCQ's step noise in the VAE encoder's launch, which
+   * precedes every reader of the noise). */
+  d3a_philox_job philox;
 } d3a_mlp_fwd_desc;
 #define D3A_MLP_PARTS 4
 int d3a_mlp_fwd(const d3a_mlp_fwd_desc* d, void* stream);

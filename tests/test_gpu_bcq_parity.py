@@ -289,3 +289,28 @@ def test_qr_loss_in_launch_target_is_bitwise_the_target_launch(N, K):
     assert not torch.isnan(res[0][0]).any() and not torch.isnan(res[1][1]).any()
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])
+
+
+def test_bcq_philox_in_encoder_launch_is_bitwise_the_fill_launch(monkeypatch):
+    """The step's Philox noise formed by extra workgroups of the VAE encoder's
+    parts-path launch (d3a_mlp_fwd_desc.philox, round 6) against its own
+    d3a_philox_fill launch: three graph-replayed K3 updates from one state and
+    seed leave every parameter, target and the noise counter bitwise equal."""
+    from d3rlpy_amd.algos import bcq_impl
+    D, A, H, N, K, B = 17, 6, [256, 256], 100, 200, 256
+    a = make_bcq_impl(D, A, H, N, K)
+    b = make_bcq_impl(D, A, H, N, K)
+    b.set_state_dict(a.get_state_dict())
+    for impl, fused in ((a, True), (b, False)):
+        monkeypatch.setattr(bcq_impl, "_PHILOX_IN_ENC", fused)
+        impl._workspace(B).seed = 11
+        rs = np.random.RandomState(6)
+        for _ in range(3):
+            impl.update_step(HostBatch(*_batch(rs, B, D, A)), use_graph=True)
+        torch.cuda.synchronize()
+    assert torch.equal(a.store.data, b.store.data)
+    s0, s1 = a.soft_span
+    assert torch.equal(a.targ.data[s0:s1], b.targ.data[s0:s1])
+    wa, wb = a._workspace(B), b._workspace(B)
+    assert torch.equal(wa.noise, wb.noise) and torch.equal(wa.rng_ctr, wb.rng_ctr)
+    assert int(wa.rng_ctr.item()) == 3
