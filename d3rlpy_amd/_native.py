@@ -573,6 +573,8 @@ _SIGNATURES = {
     "d3a_q2_bwd_x6t_splits": (C.c_int32, [C.c_int64, C.c_int32]),
     "d3a_conv_bwd_x": (C.c_int, [C.POINTER(ConvDesc), vp]),
     "d3a_conv_pack_weights": (C.c_int, [C.POINTER(ConvDesc), C.POINTER(C.c_int32), C.c_int32, vp]),
+    "d3a_conv_pack_weights_philox": (C.c_int, [C.POINTER(ConvDesc), C.POINTER(C.c_int32), C.c_int32,
+                                               C.POINTER(PhiloxJob), vp]),
     "d3a_iqn_prior": (C.c_int, [C.POINTER(IqnPriorDesc), vp]),
     "d3a_iqn_head_fwd": (C.c_int, [C.POINTER(IqnHeadDesc), vp]),
     "d3a_iqn_loss": (C.c_int, [C.POINTER(IqnLossDesc), vp]),

@@ -402,6 +402,8 @@ _CONV_BWD_X = os.environ.get("D3A_CONV_BWD_X", "1") == "1"
 # the step's conv weight copies in one d3a_conv_pack_weights launch (else each
 # conv entry packs its own); D3A_CONV_PREPACK=0 for the per-entry packs
 _CONV_PREPACK = os.environ.get("D3A_CONV_PREPACK", "1") == "1"
+# the step's taus on the weight-copy launch's appended workgroups (round 6)
+_PHILOX_IN_PACK = os.environ.get("D3A_K5_PHILOX_IN_PACK", "1") == "1"
 
 
 def _conv_bwd_x(ci: int, co: int) -> bool:
@@ -722,13 +724,22 @@ class _Workspace:
         B, K, A, F, E = self.B, impl._K, impl._action_size, impl._F, impl._E
         BK = B * K
         st, tg = impl.store, impl.targ
-        if not self._external_taus and not self.mean:
-            ops.philox_fill(self.taus, 0, self.taus.numel(), 0.0, 1.0, self.seed, self.rng_ctr,
-                            self.rng_ticket)
         # every fp32 conv layer's weight copies for this step in one launch:
         # the online and target forwards' walk order, the input gradients'
-        # tap-major order (the weights do not change before the step's Adam)
+        # tap-major order (the weights do not change before the step's Adam);
+        # the step's taus drawn on that launch's appended workgroups (round 6;
+        # D3A_K5_PHILOX_IN_PACK=0: their own d3a_philox_fill launch)
         pre = _CONV_PREPACK and len(impl.geom) > 1
+        ph = None
+        if not self._external_taus and not self.mean:
+            if pre and _PHILOX_IN_PACK:
+                ph = NAT.PhiloxJob()
+                ph.out, ph.n_normal, ph.n_uniform = self.taus.data_ptr(), 0, self.taus.numel()
+                ph.lo, ph.hi, ph.seed = 0.0, 1.0, self.seed
+                ph.ctr, ph.ticket = self.rng_ctr.data_ptr(), self.rng_ticket.data_ptr()
+            else:
+                ops.philox_fill(self.taus, 0, self.taus.numel(), 0.0, 1.0, self.seed, self.rng_ctr,
+                                self.rng_ticket)
         if pre:
             descs, lays = [], []
             for l in range(1, len(impl.geom)):
@@ -740,7 +751,11 @@ class _Workspace:
                     d.wpack = buf.data_ptr()
                     descs.append(d)
                     lays.append(lay)
-            ops.conv_pack_weights(descs, lays)
+            if descs:
+                ops.conv_pack_weights(descs, lays, philox=ph)
+            elif ph is not None:
+                ops.philox_fill(self.taus, 0, self.taus.numel(), 0.0, 1.0, self.seed, self.rng_ctr,
+                                self.rng_ticket)
         # graph branches: the target encoder + target head (own buffers, the
         # target parameters) run on side stream 1 beside the online encoder +
         # head, joined before the loss; in the backward each layer's weight

@@ -908,9 +908,36 @@ struct PackJobs {
   int CO[8], C[8], KH[8], KW[8], layout[8];
   int64_t end[8];  // running element count through job i
   int n;
+  // (d3a_conv_pack_weights_philox) a Philox fill on the blocks past the
+  // copies' (pk_blocks of them): d3a_philox_fill's body and counter ticket
+  d3a_philox_job ph;
+  int pk_blocks;
 };
 
 __global__ __launch_bounds__(256) void conv_pack_multi_kernel(PackJobs J) {
+  if ((int)blockIdx.x >= J.pk_blocks) {
+    const int64_t total = J.ph.n_normal + J.ph.n_uniform;
+    const int64_t nwp = (int64_t)gridDim.x - J.pk_blocks;
+    const int64_t wgi = (int64_t)blockIdx.x - J.pk_blocks;
+    const int64_t step = *J.ph.ctr;
+    const int64_t e0 = (wgi * 256 + threadIdx.x) * 4;
+    if (e0 < total) {
+      for (int q = 0; q < 4; ++q) {
+        const int64_t e = e0 + q;
+        if (e < total)
+          J.ph.out[e] = philox_elem(J.ph.seed, (uint64_t)step, e, J.ph.n_normal, J.ph.lo, J.ph.hi);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned prev = atomicAdd(J.ph.ticket, 1u);
+      if (prev == (unsigned)(nwp - 1)) {
+        *J.ph.ctr = step + 1;
+        *J.ph.ticket = 0u;
+      }
+    }
+    return;
+  }
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
   int j = 0;
   while (j < J.n && g >= J.end[j]) ++j;
@@ -1344,10 +1371,13 @@ extern "C" int d3a_conv_bwd_x(const d3a_conv_desc* d, void* stream) {
   return 0;
 }
 
-extern "C" int d3a_conv_pack_weights(const d3a_conv_desc* descs, const int32_t* layouts, int32_t n,
-                                     void* stream) {
+extern "C" int d3a_conv_pack_weights_philox(const d3a_conv_desc* descs, const int32_t* layouts,
+                                            int32_t n, const d3a_philox_job* ph, void* stream) {
   using namespace d3a;
   D3A_CHECK_ARG(descs && layouts && n >= 1 && n <= 8, "d3a_conv_pack_weights: 1..8 descriptors");
+  D3A_CHECK_ARG(ph == nullptr || (ph->out && ph->ctr && ph->ticket && ph->n_normal >= 0 &&
+                                  ph->n_uniform >= 0),
+                "d3a_conv_pack_weights_philox: the philox job needs out, ctr and ticket");
   PackJobs J{};
   int64_t tot = 0;
   for (int i = 0; i < n; ++i) {
@@ -1367,8 +1397,19 @@ extern "C" int d3a_conv_pack_weights(const d3a_conv_desc* descs, const int32_t* 
   }
   J.n = n;
   D3A_CHECK_ARG(tot < (1ll << 31), "d3a_conv_pack_weights: too many elements");
-  hipLaunchKernelGGL(conv_pack_multi_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+  J.pk_blocks = (int)((tot + 255) / 256);
+  int64_t ph_blocks = 0;
+  if (ph != nullptr && ph->n_normal + ph->n_uniform > 0) {
+    J.ph = *ph;
+    ph_blocks = ((ph->n_normal + ph->n_uniform + 3) / 4 + 255) / 256;
+  }
+  hipLaunchKernelGGL(conv_pack_multi_kernel, dim3((unsigned)(J.pk_blocks + ph_blocks)), dim3(256), 0,
                      (hipStream_t)stream, J);
   D3A_LAUNCH_CHECK("d3a_conv_pack_weights");
   return 0;
+}
+
+extern "C" int d3a_conv_pack_weights(const d3a_conv_desc* descs, const int32_t* layouts, int32_t n,
+                                     void* stream) {
+  return d3a_conv_pack_weights_philox(descs, layouts, n, nullptr, stream);
 }

@@ -276,12 +276,18 @@ def linear_fwd_splitk(x: int, ldx: int, W: int, b: Optional[int], y: int, R: int
                                             int(relu), _stream()), "d3a_splitk_epilogue_f32")
 
 
-def conv_pack_weights(descs, layouts) -> None:
+def conv_pack_weights(descs, layouts, philox=None) -> None:
     """d3a_conv_pack_weights over up to 8 ConvDescs (weight -> wpack in layout
-    0: the forward's walk order, 1: the input gradient's tap-major order)."""
+    0: the forward's walk order, 1: the input gradient's tap-major order);
+    ``philox`` (a PhiloxJob): d3a_conv_pack_weights_philox, the fill on the
+    same launch's appended workgroups."""
     n = len(descs)
     arr = (N.ConvDesc * n)(*descs)
     lays = (C.c_int32 * n)(*layouts)
+    if philox is not None:
+        N.check(N.lib().d3a_conv_pack_weights_philox(arr, lays, n, C.byref(philox), _stream()),
+                "d3a_conv_pack_weights_philox")
+        return
     N.check(N.lib().d3a_conv_pack_weights(arr, lays, n, _stream()), "d3a_conv_pack_weights")
 
 

@@ -1199,6 +1199,11 @@ int d3a_conv_bwd_x(const d3a_conv_desc* d, void* stream);
  * walk order [CO][KH][KW][C], 1: d3a_conv_bwd_x's tap-major [KH][KW][CO][C]. */
 int d3a_conv_pack_weights(const d3a_conv_desc* descs, const int32_t* layouts, int32_t n,
                           void* stream);
+/* The same, with a Philox fill (d3a_philox_fill's stream, arithmetic and
+ * counter ticket; ph may be NULL) on appended workgroups: K5's tau draw for
+ * the step's IQN evaluations in the weight copies' launch (round 6). */
+int d3a_conv_pack_weights_philox(const d3a_conv_desc* descs, const int32_t* layouts, int32_t n,
+                                 const d3a_philox_job* ph, void* stream);
 
 /* Per-sample [P][C] (NHWC) <-> [C][P] (NCHW) transpose, optional [mask > 0]
  * in the destination layout: the flatten before PixelEncoder._fc

@@ -129,3 +129,26 @@ def test_discrete_cql_predict_and_checkpoint(tmp_path):
     impl2 = make_impl(A)
     impl2.load_model(str(f))
     assert torch.equal(impl2.store.data, impl.store.data)
+
+
+def test_discrete_cql_taus_in_pack_launch_are_bitwise_the_fill_launch(monkeypatch):
+    """K5's taus drawn on the weight-copy launch's appended workgroups
+    (d3a_conv_pack_weights_philox, round 6) against their own d3a_philox_fill
+    launch: three graph-replayed updates from one state and seed leave the
+    parameters, the taus and the draw counter bitwise equal."""
+    from d3rlpy_amd.algos import discrete_cql_impl as dci
+    A, B = 4, 64
+    a = make_impl(A)
+    b = make_impl(A)
+    b.set_state_dict(a.get_state_dict())
+    for impl, fused in ((a, True), (b, False)):
+        monkeypatch.setattr(dci, "_PHILOX_IN_PACK", fused)
+        impl._workspace(B).seed = 9
+        rs = np.random.RandomState(3)
+        for it in range(3):
+            impl.update_step(_HB(*_batch(rs, B, A)), update_target=False, use_graph=True)
+        torch.cuda.synchronize()
+    wa, wb = a._workspace(B), b._workspace(B)
+    assert torch.equal(wa.taus, wb.taus) and torch.equal(wa.rng_ctr, wb.rng_ctr)
+    assert int(wa.rng_ctr.item()) == 3
+    assert torch.equal(a.store.data, b.store.data)
