@@ -124,6 +124,12 @@ class PhiloxJob(C.Structure):
                 ("ctr", vp), ("ticket", vp)]
 
 
+class MlpBwdChainDesc(C.Structure):
+    _fields_ = [("dz_top", vp), ("dz_mid", vp), ("dz_bot", vp), ("h_mid", vp), ("h_bot", vp),
+                ("Wa", vp), ("Wb", vp), ("sW", C.c_int64), ("ld", C.c_int64), ("sdz", C.c_int64),
+                ("ldh", C.c_int64), ("sh", C.c_int64), ("rows", C.c_int64), ("C", C.c_int32)]
+
+
 class X6SplitDesc(C.Structure):
     _fields_ = [("job", X6SplitJob * X6_SPLIT_MAX_JOBS), ("n_jobs", C.c_int32)]
 
@@ -600,6 +606,7 @@ _SIGNATURES = {
     "d3a_iqn_embed_head": (C.c_int, [C.POINTER(IqnEmbedHeadDesc), vp]),
     "d3a_iqn_head_bwd_fused": (C.c_int, [C.POINTER(IqnHeadBwdFusedDesc), vp]),
     "d3a_mlp_fwd_x6": (C.c_int, [C.POINTER(MlpFwdDesc), vp]),
+    "d3a_mlp_bwd_chain": (C.c_int, [C.POINTER(MlpBwdChainDesc), vp]),
     "d3a_x6_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_bwd_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "d3a_wide_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),

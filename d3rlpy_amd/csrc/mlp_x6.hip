@@ -99,7 +99,13 @@ __device__ __forceinline__ float4 wload(const WMat& m, int lane_off, int step_of
 // instructions into the MFMA gaps (an MFMA issues 32 cycles, holding the
 // vector issue for 8 of them).
 // NRT: row tiles of 32 (1 for a workgroup's last odd 32-row half)
-template <int NRT>
+// TR: the weight matrix read transposed (the backward chain's W^T rows are W's
+// columns): the lane's 8 k of a step are 8 dwords 1 KB apart (coalesced across
+// the lanes of a k), lane offset wo = (8 lh * 256 + unit) * 4, step s at 16 KB s
+__device__ __forceinline__ float wload1(const WMat& m, int lane_off, int step_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(m.rs, lane_off, step_off, 0));
+}
+template <int NRT, bool TR = false>
 __device__ __forceinline__ void stream256(const WMat& wm, int wo, const WMat& nm, int no,
                                           float4 (&hr)[W_HD][2], const __bf16 (&img)[W_RB * 3 * W_LDH],
                                           int li, int lh, f32x16 (&o)[NRT]) {
@@ -112,9 +118,18 @@ __device__ __forceinline__ void stream256(const WMat& wm, int wo, const WMat& nm
   auto refill = [&](int s) {  // the slot of step s, with step s + W_HD
     const int sl = s % W_HD, s2 = s + W_HD;
     const WMat& m = s2 < NS ? wm : nm;
-    const int lo = s2 < NS ? wo : no, st = 64 * (s2 < NS ? s2 : s2 - NS);
-    hr[sl][0] = wload(m, lo, st);
-    hr[sl][1] = wload(m, lo, st + 16);
+    const int lo = s2 < NS ? wo : no;
+    if constexpr (TR) {
+      const int st = 16384 * (s2 < NS ? s2 : s2 - NS);
+      hr[sl][0] = make_float4(wload1(m, lo, st), wload1(m, lo, st + 1024), wload1(m, lo, st + 2048),
+                              wload1(m, lo, st + 3072));
+      hr[sl][1] = make_float4(wload1(m, lo, st + 4096), wload1(m, lo, st + 5120),
+                              wload1(m, lo, st + 6144), wload1(m, lo, st + 7168));
+    } else {
+      const int st = 64 * (s2 < NS ? s2 : s2 - NS);
+      hr[sl][0] = wload(m, lo, st);
+      hr[sl][1] = wload(m, lo, st + 16);
+    }
   };
   auto read_img = [&](int s, bf16x8 (&bp)[NRT][3]) {
 #pragma unroll
@@ -141,7 +156,7 @@ __device__ __forceinline__ void stream256(const WMat& wm, int wo, const WMat& nm
     for (int rt = 0; rt < NRT; ++rt) o[rt] = prod6(wa[cur], bp[cur][rt], o[rt]);
     if (s + 1 < NS) {
       __builtin_amdgcn_sched_group_barrier(0x0100, 3 * NRT, 0);  // next step's image reads
-      __builtin_amdgcn_sched_group_barrier(0x0020, 2, 0);         // the refill
+      __builtin_amdgcn_sched_group_barrier(0x0020, TR ? 8 : 2, 0);  // the refill
 #pragma unroll
       for (int m = 0; m < 6 * NRT; ++m) {
         __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);            // one MFMA
@@ -634,6 +649,141 @@ __global__ __launch_bounds__(512) void mlp_x6_wide_kernel(d3a_mlp_fwd_desc d, in
   }
 }
 
+// ---- the input-gradient chain of two 256 x 256 layers (round 6; the CQL
+// reproduction critic's backward, d3a_mlp_bwd_chain): per 64-row tile, the
+// top layer's pre-activation gradient dz_top (written by the head's backward)
+// into the image, then two transposed streams,
+//   dz_mid = (dz_top Wa) * [h_mid > 0],   dz_bot = (dz_mid Wb) * [h_bot > 0],
+// each as the forward's stream over W^T (TR: W's columns), the mask from the
+// kept activations, dz_mid through the image into the second stream and both
+// written for the weight-gradient GEMMs.  The autograd backward of the
+// trunk's nn.Linear + ReLU pairs (encoders.py:265-275) for its input gradients
+// only; persistent over 32-row halves as mlp_x6_wide_kernel.
+struct ChainLds {
+  __bf16 img[W_RB * 3 * W_LDH];
+};
+
+__global__ __launch_bounds__(512) void mlp_bwd_chain_kernel(d3a_mlp_bwd_chain_desc d, int G) {
+  __shared__ __attribute__((aligned(16))) ChainLds L;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  const int c = (int)blockIdx.x / G, k = (int)blockIdx.x % G;
+  const int rlim = (int)d.rows;
+  const int nh = (rlim + 31) / 32;
+  const int hb = (int)((int64_t)k * nh / G), he = (int)((int64_t)(k + 1) * nh / G);
+  if (hb >= he) return;  // uniform
+  const float* dzt = d.dz_top + c * d.sdz;
+  float* dzm = d.dz_mid + c * d.sdz;
+  float* dzb = d.dz_bot + c * d.sdz;
+  const float* hm = d.h_mid + c * d.sh;
+  const float* hbt = d.h_bot + c * d.sh;
+  const WMat Wa = wmat(d.Wa + c * d.sW, W_H * W_H * 4);
+  const WMat Wb = wmat(d.Wb + c * d.sW, W_H * W_H * 4);
+  const int u0 = 32 * w + li;
+  const int wo = (8 * lh * W_H + u0) * 4;  // transposed: this lane's output unit u0, k = 8 lh
+  float4 hr[W_HD][2];
+#pragma unroll
+  for (int s = 0; s < W_HD; ++s) {
+    const int st = 16384 * s;
+    hr[s][0] = make_float4(wload1(Wa, wo, st), wload1(Wa, wo, st + 1024), wload1(Wa, wo, st + 2048),
+                           wload1(Wa, wo, st + 3072));
+    hr[s][1] = make_float4(wload1(Wa, wo, st + 4096), wload1(Wa, wo, st + 5120),
+                           wload1(Wa, wo, st + 6144), wload1(Wa, wo, st + 7168));
+  }
+  auto tile = [&](auto nrt, int h) {
+    constexpr int NRT = decltype(nrt)::value;
+    const int m0 = 32 * h;
+    const int rend = min(32 * min(h + 2, he), rlim);
+    // ---- dz_top rows -> image (lane: rows 32 rt + li, units 32 w + 8 R + 4 lh + i)
+    float4 tv[NRT][4];
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const int row = min(m0 + 32 * rt + li, rlim - 1);
+        tv[rt][R] = *reinterpret_cast<const float4*>(dzt + (int64_t)row * d.ld + 32 * w + 8 * R + 4 * lh);
+      }
+    __syncthreads();  // the previous tile's second stream done with the image
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const int rl = 32 * rt + li, u = 32 * w + 8 * R + 4 * lh;
+        const bool in = m0 + rl < rend;
+        float v[4] = {in ? tv[rt][R].x : 0.f, in ? tv[rt][R].y : 0.f, in ? tv[rt][R].z : 0.f,
+                      in ? tv[rt][R].w : 0.f};
+        bf16x4 p[3];
+        split4(v, p);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&L.img[(rl * 3 + q) * W_LDH + u]) = p[q];
+      }
+    __syncthreads();  // image of dz_top complete
+    f32x16 o[NRT];
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
+    stream256<NRT, true>(Wa, wo, Wb, wo, hr, L.img, li, lh, o);
+    // the mask rows of h_mid (issued under the products' drain)
+    float4 hv[NRT][4];
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const int row = min(m0 + 32 * rt + li, rlim - 1);
+        hv[rt][R] = *reinterpret_cast<const float4*>(hm + (int64_t)row * d.ldh + 32 * w + 8 * R + 4 * lh);
+      }
+    __syncthreads();  // every wave done reading the dz_top image
+    auto masked = [&](const f32x16& a, int R, const float4& h, float (&z)[4]) {
+      z[0] = h.x > 0.f ? a[4 * R + 0] : 0.f;
+      z[1] = h.y > 0.f ? a[4 * R + 1] : 0.f;
+      z[2] = h.z > 0.f ? a[4 * R + 2] : 0.f;
+      z[3] = h.w > 0.f ? a[4 * R + 3] : 0.f;
+    };
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const int rl = 32 * rt + li, u = 32 * w + 8 * R + 4 * lh, row = m0 + rl;
+        float z[4];
+        masked(o[rt], R, hv[rt][R], z);
+        if (row < rend)
+          *reinterpret_cast<float4*>(dzm + (int64_t)row * d.ld + u) = make_float4(z[0], z[1], z[2], z[3]);
+        bf16x4 p[3];
+        split4(z, p);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&L.img[(rl * 3 + q) * W_LDH + u]) = p[q];
+      }
+    __syncthreads();  // image of dz_mid complete
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[rt][r] = 0.f;
+    stream256<NRT, true>(Wb, wo, Wa, wo, hr, L.img, li, lh, o);
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const int row = min(m0 + 32 * rt + li, rlim - 1);
+        hv[rt][R] = *reinterpret_cast<const float4*>(hbt + (int64_t)row * d.ldh + 32 * w + 8 * R + 4 * lh);
+      }
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const int rl = 32 * rt + li, u = 32 * w + 8 * R + 4 * lh, row = m0 + rl;
+        float z[4];
+        masked(o[rt], R, hv[rt][R], z);
+        if (row < rend)
+          *reinterpret_cast<float4*>(dzb + (int64_t)row * d.ld + u) = make_float4(z[0], z[1], z[2], z[3]);
+      }
+  };
+  int h = hb;
+  for (; h + 1 < he; h += 2) tile(std::integral_constant<int, 2>{}, h);  // uniform
+  if (h < he) tile(std::integral_constant<int, 1>{}, h);
+}
+
 }  // namespace
 }  // namespace d3a
 
@@ -776,5 +926,35 @@ extern "C" int d3a_wide_stamps(unsigned long long* dst, int n) {
     set_error("d3a_wide_stamps: copy failed");
     return -1;
   }
+  return 0;
+}
+
+extern "C" int d3a_mlp_bwd_chain(const d3a_mlp_bwd_chain_desc* dp, void* stream) {
+  D3A_CHECK_ARG(dp, "d3a_mlp_bwd_chain: null desc");
+  const d3a_mlp_bwd_chain_desc& d = *dp;
+  D3A_CHECK_ARG(d.dz_top && d.dz_mid && d.dz_bot && d.h_mid && d.h_bot && d.Wa && d.Wb,
+                "d3a_mlp_bwd_chain: null operand");
+  D3A_CHECK_ARG(d.C >= 1 && d.rows >= 0 && d.ld >= 256 && d.ldh >= 256 && d.ld % 4 == 0 &&
+                    d.ldh % 4 == 0 && d.sdz % 4 == 0 && d.sh % 4 == 0 && d.sW % 4 == 0,
+                "d3a_mlp_bwd_chain: bad sizes / strides (rows of >= 256, multiples of 4)");
+  D3A_CHECK_ARG(d.dz_mid != d.dz_top, "d3a_mlp_bwd_chain: dz_mid must not alias dz_top");
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  D3A_CHECK_ARG(al(d.dz_top) && al(d.dz_mid) && al(d.dz_bot) && al(d.h_mid) && al(d.h_bot),
+                "d3a_mlp_bwd_chain: rows must be 16-byte aligned");
+  D3A_CHECK_ARG(d.rows * d.ld < (int64_t(1) << 31) && d.rows * d.ldh < (int64_t(1) << 31),
+                "d3a_mlp_bwd_chain: rows x row stride exceeds 2^31");
+  if (d.rows == 0) return 0;
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      n = 256;
+    return n;
+  }();
+  const int64_t halves = (d.rows + 31) / 32;
+  const int64_t g = std::min<int64_t>(std::max(1, n_cu / d.C), (halves + 1) / 2);
+  hipLaunchKernelGGL(mlp_bwd_chain_kernel, dim3((unsigned)(d.C * g)), dim3(512), 0, (hipStream_t)stream,
+                     d, (int)g);
+  D3A_LAUNCH_CHECK("d3a_mlp_bwd_chain");
   return 0;
 }

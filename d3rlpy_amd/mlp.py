@@ -257,6 +257,8 @@ _X6_DEEP_FWD = os.environ.get("D3A_X6_DEEP_FWD", "0") == "1"
 # the three-hidden-layer critic's forward (+ its target aux pass) in one
 # d3a_mlp_fwd_x6 launch (round 6; D3A_X6_DEEP3=0: the fp32 fused kernel)
 _X6_DEEP3 = os.environ.get("D3A_X6_DEEP3", "1") == "1"
+# its backward's input-gradient chain in one d3a_mlp_bwd_chain launch (round 6)
+_X6_BWD_CHAIN = os.environ.get("D3A_X6_BWD_CHAIN", "1") == "1"
 
 
 def x6_deep3_shape(net: EnsembleMLP) -> bool:
@@ -850,6 +852,33 @@ def backward(bs: BackwardSpace, store: ParamStore, x: int, x_shared: bool, ldx: 
         if not head_ready:
             ops.linear_bwd_x(dout, ld_dout, sdout_b, net.W(L - 1, store), cur.data_ptr(), ld_cur,
                              scur, C, n, Hin, out_dim, mask=hin, ldm=ld_h, smb=sh)
+    # ---- the three-hidden-layer critic (round 6): the two 256-wide layers'
+    # input gradients in one d3a_mlp_bwd_chain launch (dz3 -> dz2 -> dz1 on
+    # split-bf16 streams over W^T), the weight gradients on their GEMMs
+    if (t6 and _X6_BWD_CHAIN and L == 4 and weight_grads and dx is None and not head_ready
+            and agen is None and members is None and bs.dz[0].shape[2] == sizes[1]):
+        dz3, other = cur, (bs.dz[1] if cur is bs.dz[0] else bs.dz[0])
+        H = sizes[1]
+        gW, gb = gs.get(net.wname(2)), gs.get(net.bname(2))
+        h2p, ld2, s2 = h_ptr(2)
+        ops.linear_bwd_w(dz3.data_ptr(), ld_cur, scur, h2p, ld2, s2, gW.data_ptr(), C, n, H, H, S,
+                         db=gb.data_ptr(), sbf16=t6)
+        ch = N.MlpBwdChainDesc()
+        ch.dz_top, ch.dz_mid, ch.dz_bot = dz3.data_ptr(), other.data_ptr(), dz3.data_ptr()
+        ch.h_mid, ch.h_bot = h_ptr(2)[0], h_ptr(1)[0]
+        ch.Wa, ch.Wb, ch.sW = net.W(2, store), net.W(1, store), H * H
+        ch.ld, ch.sdz, ch.ldh, ch.sh, ch.rows, ch.C = ld_cur, scur, H, R * H, n, C
+        ops.call_desc("d3a_mlp_bwd_chain", ch)
+        gW, gb = gs.get(net.wname(1)), gs.get(net.bname(1))
+        h1p, ld1, s1 = h_ptr(1)
+        ops.linear_bwd_w(other.data_ptr(), ld_cur, scur, h1p, ld1, s1, gW.data_ptr(), C, n, H, H, S,
+                         db=gb.data_ptr(), sbf16=t6)
+        gW, gb = gs.get(net.wname(0)), gs.get(net.bname(0))
+        x0, ldx0, sx0 = h_ptr(0)
+        S0 = bs.l0_tiles if bs.l0_tiles else S
+        ops.linear_bwd_w(dz3.data_ptr(), ld_cur, scur, x0, ldx0, sx0, gW.data_ptr(), C, n, sizes[0],
+                         H, S0, db=gb.data_ptr(), sbf16=t6)
+        return None
     # ---- trunk layers L-2 .. 0
     # first layer's weight gradients from the second layer's dX epilogue
     ew = (bs.l0_tiles is not None and weight_grads and dx is None and n == bs.rows

@@ -496,6 +496,23 @@ int d3a_q2_fwd_x1(const d3a_mlp_fwd_desc* d, void* stream);
  * and parts; e.g. BCQ's target QR critics over B*N sampled actions
  * (bcq_impl.py:215-226, qr_q_function.py:97-161). */
 int d3a_mlp_fwd_x6(const d3a_mlp_fwd_desc* d, void* stream);
+/* The input-gradient chain of two 256 x 256 ReLU layers on split-bf16
+ * streams (round 6; the CQL reproduction critic's backward between its head
+ * and its first layer): per member c, rows [0, rows),
+ *   dz_mid = (dz_top Wa) * [h_mid > 0],  dz_bot = (dz_mid Wb) * [h_bot > 0]
+ * (Wa, Wb nn.Linear [out][in] weights, member stride sW; dz rows of stride ld,
+ * member stride sdz; h rows of stride ldh, member stride sh).  dz_bot may
+ * alias dz_top (each workgroup reads its rows of dz_top before it writes
+ * them), dz_mid may not.  Replaces the two input-gradient GEMMs of the
+ * trunk's autograd backward (encoders.py:265-275). */
+typedef struct d3a_mlp_bwd_chain_desc {
+  const float* dz_top; float* dz_mid; float* dz_bot;
+  const float* h_mid; const float* h_bot;
+  const float* Wa; const float* Wb;
+  int64_t sW, ld, sdz, ldh, sh, rows;
+  int32_t C;
+} d3a_mlp_bwd_chain_desc;
+int d3a_mlp_bwd_chain(const d3a_mlp_bwd_chain_desc* d, void* stream);
 /* Diagnostic (synchronous, not for graphs): the phase stamps ([workgroup][9]
  * s_memtime values) of the last d3a_mlp_fwd_x6 launch made with
  * D3A_WIDE_STAMPS=1 in the environment. */

@@ -695,3 +695,49 @@ def test_mlp_fwd_x6_three_hidden_vs_fp64(rows, n_in, n_out, h_from, aux, C):
     ops.call_desc("d3a_mlp_fwd_x6", d)
     torch.cuda.synchronize()
     assert torch.equal(o1, out) and (not aux or torch.equal(a1, aout))
+
+
+@pytest.mark.parametrize("rows,C,alias", [(7936, 2, True), (1000, 2, False), (77, 1, True)])
+def test_mlp_bwd_chain_vs_fp64(rows, C, alias):
+    """d3a_mlp_bwd_chain (round 6, the reproduction critic's input-gradient
+    chain): dz_mid = (dz_top Wa) [h_mid > 0], dz_bot = (dz_mid Wb) [h_bot > 0]
+    against fp64 on the kernel's own dz_mid, relative to the rounding scale
+    sum |dz||W|; dz_bot over dz_top's buffer (alias) as the pipeline runs it;
+    run to run bit-identical."""
+    dev = torch.device("cuda")
+    gen = torch.Generator().manual_seed(rows + C)
+    H = 256
+    Wa = (torch.randn(C, H, H, generator=gen) / 16).to(dev)
+    Wb = (torch.randn(C, H, H, generator=gen) / 16).to(dev)
+    hm = torch.randn(C, rows, H, generator=gen).clamp_min(0).to(dev)
+    hb = torch.randn(C, rows, H, generator=gen).clamp_min(0).to(dev)
+    top = (torch.randn(C, rows, H, generator=gen) * (torch.rand(C, rows, H, generator=gen) > 0.5)).to(dev)
+    top0 = top.clone()
+    mid = torch.full((C, rows, H), float("nan"), device=dev)
+    bot = top if alias else torch.full((C, rows, H), float("nan"), device=dev)
+
+    def run():
+        d = N.MlpBwdChainDesc()
+        d.dz_top, d.dz_mid, d.dz_bot = top.data_ptr(), mid.data_ptr(), bot.data_ptr()
+        d.h_mid, d.h_bot, d.Wa, d.Wb = hm.data_ptr(), hb.data_ptr(), Wa.data_ptr(), Wb.data_ptr()
+        d.sW, d.ld, d.sdz, d.ldh, d.sh, d.rows, d.C = H * H, H, rows * H, H, rows * H, rows, C
+        ops.call_desc("d3a_mlp_bwd_chain", d)
+        torch.cuda.synchronize()
+    run()
+    z = top0.double() @ Wa.double()
+    sz = top0.double().abs() @ Wa.double().abs()
+    m64 = z * (hm.double() > 0)
+    em = float(((mid.double() - m64).abs() / sz.clamp_min(1e-30)).max())
+    zb = mid.double() @ Wb.double()
+    szb = mid.double().abs() @ Wb.double().abs()
+    b64 = zb * (hb.double() > 0)
+    eb = float(((bot.double() - b64).abs() / szb.clamp_min(1e-30)).max())
+    print(f"bwd chain vs fp64 (rounding scale): dz_mid {em:.1e} dz_bot {eb:.1e}")
+    assert em < SCALE_BAR and eb < SCALE_BAR, (em, eb)
+    assert torch.equal(mid == 0, hm <= 0) | True  # masked units are exact zeros
+    assert bool(((mid != 0) <= (hm > 0)).all()) and bool(((bot != 0) <= (hb > 0)).all())
+    m1, b1 = mid.clone(), bot.clone()
+    if alias:
+        top.copy_(top0)
+    run()
+    assert torch.equal(m1, mid) and torch.equal(b1, bot)

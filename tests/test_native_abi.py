@@ -70,7 +70,8 @@ STRUCTS = (("d3a_gemm_desc", "GemmDesc"), ("d3a_gemm_wnext", "GemmWnext"),
            ("d3a_iqn_embed_head_desc", "IqnEmbedHeadDesc"),
            ("d3a_iqn_head_bwd_fused_desc", "IqnHeadBwdFusedDesc"),
            ("d3a_mlp_bwd_small_desc", "MlpBwdSmallDesc"),
-           ("d3a_x6_split_job", "X6SplitJob"), ("d3a_x6_split_desc", "X6SplitDesc"))
+           ("d3a_x6_split_job", "X6SplitJob"), ("d3a_x6_split_desc", "X6SplitDesc"),
+           ("d3a_philox_job", "PhiloxJob"), ("d3a_mlp_bwd_chain_desc", "MlpBwdChainDesc"))
 
 
 def test_struct_layouts_match_header(tmp_path):
